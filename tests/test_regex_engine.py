@@ -1,0 +1,122 @@
+"""Native Go-regexp engine (exact host pass) vs the oracle -- CPU only.
+
+Covers every builtin rule regex (pkg/fanal/secret/builtin-rules.go), the golden
+configs' custom regexes, and the builtin allow-rule regexes, on texts mixing
+noise, planted samples of each regex's language, non-ASCII runes, invalid UTF-8
+and the fold-special runes U+212A / U+017F / U+0130.  Also checks that a
+search restricted to start windows that contain every true match start equals
+the unrestricted search (the GPU-candidate contract).
+"""
+import json
+import random
+from pathlib import Path
+
+import pytest
+import yaml
+
+from oracle.goregexp import GoRegexp
+from oracle.gostd import bytes_to_lower
+from tests.regex_sampler import sample_regex
+from trivy_amd import _lib
+
+ROOT = Path(__file__).resolve().parent.parent
+BUILTIN = json.loads((ROOT / "trivy_amd/secret/builtin_rules.json").read_text())
+
+
+def _golden_custom_regexes():
+    out = []
+    for f in sorted((ROOT / "tests/golden/scanner").glob("*.yaml")):
+        d = yaml.safe_load(f.read_text()) or {}
+        for r in d.get("rules") or []:
+            if r.get("regex"):
+                out.append(str(r["regex"]))
+            for a in r.get("allow-rules") or []:
+                for k in ("regex", "path"):
+                    if a.get(k):
+                        out.append(str(a[k]))
+        for a in d.get("allow-rules") or []:
+            for k in ("regex", "path"):
+                if a.get(k):
+                    out.append(str(a[k]))
+    return sorted(set(out))
+
+
+# Nullable loop bodies such as (a|)+ are excluded: CPython's backtracker and
+# Go's Pike VM (which the native engine follows) record different captures for
+# the final empty iteration; no rule uses that construct.
+PATTERNS = ([r["regex"] for r in BUILTIN["rules"]]
+            + [a[k] for a in BUILTIN["allow_rules"] for k in ("regex", "path") if a[k]]
+            + _golden_custom_regexes()
+            + [r"a*", r"x{2,5}?y", r"(?m)^ab$", r"\bfoo\b", r"(?i)straße", r"(?s).{0,3}z",
+               r"[^\x00-\x7f]+", r"\x{FFFD}", r"(?U)a+b", r"(?i)k+s", r"^", r"$", r"(?i)[^k]"])
+
+NOISE = ["the quick brown fox ", "key=", "secret: ", "\n", "  ", "'", '"', "AKIA", "ghp_",
+         "sk_live_", "K", "ſ", "İ", "é", "日本", "\udcff", "-----BEGIN ", "=>",
+         "xoxb-", "eyJ", ".", "hooks.slack.com", "\t", ",", "_", "0123456789abcdef"]
+
+
+def _text(rng, pats, n_parts=40):
+    parts = []
+    for _ in range(n_parts):
+        if rng.random() < 0.35:
+            parts.append(sample_regex(rng.choice(pats), rng))
+        else:
+            parts.append(rng.choice(NOISE).encode("utf-8", "surrogateescape"))
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("idx", range(len(PATTERNS)))
+def test_native_regex_matches_oracle(idx):
+    pat = PATTERNS[idx]
+    ref = GoRegexp(pat)
+    rng = random.Random(1000 + idx)
+    for trial in range(25):
+        text = _text(rng, [pat], n_parts=rng.randint(1, 30))
+        want = ref.find_all_submatch_index(text)
+        got = _lib.regex_find_all(pat, text, submatch=True)
+        assert got == want, (pat, text)
+        assert _lib.regex_match(pat, text) == ref.match_string(text)
+
+
+@pytest.mark.parametrize("idx", range(len(PATTERNS)))
+def test_windowed_search_equals_full(idx):
+    pat = PATTERNS[idx]
+    rng = random.Random(7 + idx)
+    for trial in range(15):
+        text = _text(rng, [pat], n_parts=rng.randint(1, 30))
+        full = _lib.regex_find_all(pat, text, submatch=True)
+        if any(m[0] == m[1] for m in full):
+            continue  # nullable patterns are never anchored (whole-file path)
+        # any superset of the true starts must give the same answer
+        ws = []
+        for m in full:
+            lo = max(0, m[0] - rng.randint(0, 4))
+            ws.append((lo, m[0] + rng.randint(0, 4)))
+        for _ in range(rng.randint(0, 4)):
+            a = rng.randint(0, max(0, len(text)))
+            ws.append((a, a + rng.randint(0, 8)))
+        ws.sort()
+        merged = []
+        for lo, hi in ws:
+            if merged and lo <= merged[-1][1] + 1:
+                merged[-1] = (merged[-1][0], max(hi, merged[-1][1]))
+            else:
+                merged.append((lo, hi))
+        got = _lib.regex_find_all(pat, text, submatch=True, windows=merged)
+        assert got == full, (pat, text, merged)
+
+
+def test_bytes_to_lower_matches_oracle():
+    rng = random.Random(5)
+    for _ in range(200):
+        b = _text(rng, [r"(?i)[a-z]{3}"], n_parts=rng.randint(0, 12))
+        assert _lib.go_bytes_to_lower(b) == bytes_to_lower(b)
+
+
+def test_compile_errors_agree():
+    bad = ["a**", "(", "[a", "x{2}{3}", "\\1", "(?P<>a)", "a{1001}", "*a", "(?i", "[z-a]", "\\pL"]
+    for p in bad:
+        with pytest.raises(ValueError):
+            GoRegexp(p)
+        with pytest.raises(ValueError):
+            _lib.regex_find_all(p, b"abc")

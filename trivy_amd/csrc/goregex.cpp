@@ -1,0 +1,1102 @@
+// Go regexp semantics (see goregex.h).  Cited Go behaviour: regexp/syntax
+// parse.go (flags, escapes, classes, repeat limits), simplify.go (counted
+// repeats), compile.go (Alt priorities, loop/quest/star), regexp/exec.go
+// (Pike VM: add/step/match), regexp/regexp.go allMatches (FindAll loop).
+#include "goregex.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace tsg {
+
+#include "unicode_tables.inc"
+
+namespace {
+constexpr uint32_t kMaxRune = 0x10FFFF;
+constexpr int kMaxRepeat = 1000;
+
+void Clean(RuneRanges* r) {
+  std::sort(r->begin(), r->end());
+  RuneRanges out;
+  for (auto& p : *r) {
+    if (!out.empty() && p.first <= out.back().second + 1) {
+      if (p.second > out.back().second) out.back().second = p.second;
+    } else {
+      out.push_back(p);
+    }
+  }
+  r->swap(out);
+}
+
+RuneRanges Negate(const RuneRanges& in) {
+  RuneRanges r = in;
+  Clean(&r);
+  RuneRanges out;
+  uint32_t next = 0;
+  for (auto& p : r) {
+    if (p.first > next) out.push_back({next, p.first - 1});
+    next = p.second + 1;
+  }
+  if (next <= kMaxRune) out.push_back({next, kMaxRune});
+  return out;
+}
+
+bool InRanges(const RuneRanges& r, uint32_t c) {
+  // binary search over sorted disjoint ranges
+  size_t lo = 0, hi = r.size();
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (c < r[m].first) hi = m;
+    else if (c > r[m].second) lo = m + 1;
+    else return true;
+  }
+  return false;
+}
+
+bool IsWordChar(int32_t r) {
+  return (r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_';
+}
+
+uint8_t EmptyOpContext(int32_t r1, int32_t r2) {  // regexp/syntax.EmptyOpContext
+  uint8_t op = kEmptyNoWordBoundary;
+  int boundary = 0;
+  if (IsWordChar(r1)) boundary = 1;
+  else if (r1 == '\n') op |= kEmptyBeginLine;
+  else if (r1 < 0) op |= kEmptyBeginText | kEmptyBeginLine;
+  if (IsWordChar(r2)) boundary ^= 1;
+  else if (r2 == '\n') op |= kEmptyEndLine;
+  else if (r2 < 0) op |= kEmptyEndText | kEmptyEndLine;
+  if (boundary) op ^= (kEmptyWordBoundary | kEmptyNoWordBoundary);
+  return op;
+}
+}  // namespace
+
+uint32_t SimpleFold(uint32_t r) {
+  size_t n = sizeof(kFoldNext) / sizeof(kFoldNext[0]);
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (kFoldNext[m][0] < r) lo = m + 1;
+    else hi = m;
+  }
+  if (lo < n && kFoldNext[lo][0] == r) return kFoldNext[lo][1];
+  return r;
+}
+
+uint32_t GoToLower(uint32_t r) {
+  if (r < 0x80) return (r >= 'A' && r <= 'Z') ? r + 32 : r;
+  size_t n = sizeof(kLower) / sizeof(kLower[0]);
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (kLower[m][0] < r) lo = m + 1;
+    else hi = m;
+  }
+  if (lo < n && kLower[lo][0] == r) return kLower[lo][1];
+  return r;
+}
+
+Rune DecodeRune(const uint8_t* s, int64_t n, int64_t pos) {
+  if (pos >= n) return {-1, 0};
+  uint8_t b0 = s[pos];
+  if (b0 < 0x80) return {b0, 1};
+  auto cont = [&](int64_t i, uint8_t lo = 0x80, uint8_t hi = 0xBF) {
+    return i < n && s[i] >= lo && s[i] <= hi;
+  };
+  if (b0 >= 0xC2 && b0 <= 0xDF) {
+    if (cont(pos + 1)) return {int32_t(((b0 & 0x1F) << 6) | (s[pos + 1] & 0x3F)), 2};
+    return {0xFFFD, 1};
+  }
+  if (b0 >= 0xE0 && b0 <= 0xEF) {
+    uint8_t lo = 0x80, hi = 0xBF;
+    if (b0 == 0xE0) lo = 0xA0;
+    if (b0 == 0xED) hi = 0x9F;
+    if (cont(pos + 1, lo, hi) && cont(pos + 2))
+      return {int32_t(((b0 & 0x0F) << 12) | ((s[pos + 1] & 0x3F) << 6) | (s[pos + 2] & 0x3F)), 3};
+    return {0xFFFD, 1};
+  }
+  if (b0 >= 0xF0 && b0 <= 0xF4) {
+    uint8_t lo = 0x80, hi = 0xBF;
+    if (b0 == 0xF0) lo = 0x90;
+    if (b0 == 0xF4) hi = 0x8F;
+    if (cont(pos + 1, lo, hi) && cont(pos + 2) && cont(pos + 3))
+      return {int32_t(((b0 & 0x07) << 18) | ((s[pos + 1] & 0x3F) << 12) | ((s[pos + 2] & 0x3F) << 6) |
+                      (s[pos + 3] & 0x3F)),
+              4};
+    return {0xFFFD, 1};
+  }
+  return {0xFFFD, 1};
+}
+
+static void AppendUtf8(std::string* out, uint32_t r) {
+  if (r < 0x80) {
+    out->push_back(char(r));
+  } else if (r < 0x800) {
+    out->push_back(char(0xC0 | (r >> 6)));
+    out->push_back(char(0x80 | (r & 0x3F)));
+  } else if (r < 0x10000) {
+    out->push_back(char(0xE0 | (r >> 12)));
+    out->push_back(char(0x80 | ((r >> 6) & 0x3F)));
+    out->push_back(char(0x80 | (r & 0x3F)));
+  } else {
+    out->push_back(char(0xF0 | (r >> 18)));
+    out->push_back(char(0x80 | ((r >> 12) & 0x3F)));
+    out->push_back(char(0x80 | ((r >> 6) & 0x3F)));
+    out->push_back(char(0x80 | (r & 0x3F)));
+  }
+}
+
+std::string GoBytesToLower(const uint8_t* s, size_t n) {
+  bool ascii = true;
+  for (size_t i = 0; i < n; i++)
+    if (s[i] >= 0x80) { ascii = false; break; }
+  std::string out;
+  out.reserve(n);
+  if (ascii) {
+    for (size_t i = 0; i < n; i++) {
+      uint8_t c = s[i];
+      out.push_back(char((c >= 'A' && c <= 'Z') ? c + 32 : c));
+    }
+    return out;
+  }
+  int64_t pos = 0;
+  while (pos < int64_t(n)) {
+    Rune r = DecodeRune(s, n, pos);
+    AppendUtf8(&out, GoToLower(uint32_t(r.r)));
+    pos += r.width;
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Parser (regexp/syntax parse.go semantics, Perl flags)
+// ---------------------------------------------------------------------------
+class Parser {
+ public:
+  Parser(Regex* re, const std::string& s) : re_(re), s_(s) {}
+
+  bool Parse(std::string* err) {
+    re_->cap_names_.push_back("");
+    int n = Alt();
+    if (!err_.empty()) { *err = err_; return false; }
+    if (i_ < s_.size()) {
+      *err = s_[i_] == ')' ? "unexpected )" : "trailing input";
+      return false;
+    }
+    re_->root_ = n;
+    re_->num_cap_ = ncap_;
+    return true;
+  }
+
+ private:
+  Regex* re_;
+  const std::string& s_;
+  size_t i_ = 0;
+  bool fi_ = false, fm_ = false, fs_ = false, fU_ = false;
+  int ncap_ = 0;
+  std::string err_;
+
+  int Fail(const std::string& m) {
+    if (err_.empty()) err_ = "error parsing regexp: " + m + ": `" + s_ + "`";
+    return NewNode(NodeOp::NoMatch);
+  }
+  int NewNode(NodeOp op) {
+    re_->nodes_.push_back(Node());
+    re_->nodes_.back().op = op;
+    return int(re_->nodes_.size()) - 1;
+  }
+  Node& N(int i) { return re_->nodes_[i]; }
+  bool AtEnd() const { return i_ >= s_.size(); }
+  int Peek(size_t k = 0) const { return i_ + k < s_.size() ? (uint8_t)s_[i_ + k] : -1; }
+
+  // Next rune of the pattern (patterns are UTF-8 text).
+  uint32_t NextRune() {
+    Rune r = DecodeRune((const uint8_t*)s_.data(), s_.size(), i_);
+    i_ += r.width;
+    return uint32_t(r.r);
+  }
+
+  int ClassNode(RuneRanges r) {
+    Clean(&r);
+    int n = NewNode(NodeOp::Class);
+    N(n).ranges = std::move(r);
+    return n;
+  }
+
+  void AddFolded(RuneRanges* out, uint32_t lo, uint32_t hi) {
+    // appendFoldedRange: add lo..hi plus every member of each rune's orbit.
+    out->push_back({lo, hi});
+    if (hi - lo > 0x20000) return;  // whole-plane ranges already contain their folds
+    for (uint32_t c = lo; c <= hi; c++) {
+      for (uint32_t f = SimpleFold(c); f != c; f = SimpleFold(f)) {
+        if (f < lo || f > hi) out->push_back({f, f});
+      }
+    }
+  }
+
+  int Literal(uint32_t r) {
+    RuneRanges rr;
+    if (fi_) AddFolded(&rr, r, r);
+    else rr.push_back({r, r});
+    return ClassNode(rr);
+  }
+
+  int Alt() {
+    std::vector<int> br;
+    br.push_back(Concat());
+    while (Peek() == '|') {
+      i_++;
+      br.push_back(Concat());
+    }
+    if (br.size() == 1) return br[0];
+    int n = NewNode(NodeOp::Alt);
+    N(n).subs = br;
+    return n;
+  }
+
+  bool RepeatSpec(size_t j, int* lo, int* hi, size_t* len) {
+    // {n} {n,} {n,m}
+    if (j >= s_.size() || s_[j] != '{') return false;
+    size_t k = j + 1;
+    auto num = [&](int* v) {
+      size_t st = k;
+      long x = 0;
+      while (k < s_.size() && s_[k] >= '0' && s_[k] <= '9') {
+        x = x * 10 + (s_[k] - '0');
+        if (x > 100000) x = 100000;
+        k++;
+      }
+      *v = int(x);
+      return k > st;
+    };
+    if (!num(lo)) return false;
+    if (k < s_.size() && s_[k] == '}') {
+      *hi = *lo;
+      *len = k + 1 - j;
+      return true;
+    }
+    if (k >= s_.size() || s_[k] != ',') return false;
+    k++;
+    if (k < s_.size() && s_[k] == '}') {
+      *hi = -1;
+      *len = k + 1 - j;
+      return true;
+    }
+    if (!num(hi)) return false;
+    if (k >= s_.size() || s_[k] != '}') return false;
+    *len = k + 1 - j;
+    return true;
+  }
+
+  int Concat() {
+    std::vector<int> items;
+    while (!AtEnd() && err_.empty()) {
+      int c = Peek();
+      if (c == '|' || c == ')') break;
+      if (c == '*' || c == '+' || c == '?') return Fail("missing argument to repetition operator");
+      int lo, hi;
+      size_t ln;
+      if (c == '{' && RepeatSpec(i_, &lo, &hi, &ln)) return Fail("missing argument to repetition operator");
+      std::vector<int> atoms;
+      bool is_flag = false;
+      Atom(&atoms, &is_flag);
+      if (is_flag) continue;
+      if (atoms.empty()) continue;
+      // repetition applies to the last atom only (\Q..\E yields several)
+      int last = Repeats(atoms.back());
+      atoms.back() = last;
+      for (int a : atoms) items.push_back(a);
+    }
+    if (items.empty()) return NewNode(NodeOp::Empty);
+    if (items.size() == 1) return items[0];
+    int n = NewNode(NodeOp::Cat);
+    N(n).subs = items;
+    return n;
+  }
+
+  int Repeats(int atom) {
+    bool had = false;
+    while (!AtEnd()) {
+      int c = Peek();
+      int lo, hi;
+      size_t ln = 1;
+      if (c == '*') { lo = 0; hi = -1; }
+      else if (c == '+') { lo = 1; hi = -1; }
+      else if (c == '?') { lo = 0; hi = 1; }
+      else if (c == '{') {
+        if (!RepeatSpec(i_, &lo, &hi, &ln)) return atom;
+        if (lo > kMaxRepeat || hi > kMaxRepeat || (hi >= 0 && lo > hi)) return Fail("invalid repeat count");
+      } else {
+        return atom;
+      }
+      if (had) return Fail("invalid nested repetition operator");
+      i_ += ln;
+      bool greedy = true;
+      if (Peek() == '?') { i_++; greedy = false; }
+      if (fU_) greedy = !greedy;
+      int n = NewNode(NodeOp::Repeat);
+      N(n).min = lo;
+      N(n).max = hi;
+      N(n).greedy = greedy;
+      N(n).subs = {atom};
+      atom = n;
+      had = true;
+    }
+    return atom;
+  }
+
+  uint32_t EscapeRune() {  // parseEscape; i_ points after the backslash
+    if (AtEnd()) { Fail("trailing backslash at end of expression"); return 0; }
+    int c = Peek();
+    i_++;
+    if (c >= '1' && c <= '7') {
+      int nx = Peek();
+      if (nx < '0' || nx > '7') { Fail("invalid escape sequence"); return 0; }
+      c = '0';
+      i_--;
+    }
+    if (c == '0') {
+      uint32_t v = 0;
+      for (int k = 0; k < 2; k++) {
+        int nx = Peek();
+        if (nx >= '0' && nx <= '7') { v = v * 8 + uint32_t(nx - '0'); i_++; }
+        else break;
+      }
+      return v;
+    }
+    if (c == 'x') {
+      auto hexv = [](int ch) -> int {
+        if (ch >= '0' && ch <= '9') return ch - '0';
+        if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+        if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+        return -1;
+      };
+      if (Peek() == '{') {
+        i_++;
+        uint64_t v = 0;
+        int nd = 0;
+        while (!AtEnd() && Peek() != '}') {
+          int h = hexv(Peek());
+          if (h < 0) { Fail("invalid escape sequence"); return 0; }
+          v = v * 16 + h;
+          if (v > kMaxRune) { Fail("invalid escape sequence"); return 0; }
+          nd++;
+          i_++;
+        }
+        if (AtEnd() || nd == 0) { Fail("invalid escape sequence"); return 0; }
+        i_++;
+        return uint32_t(v);
+      }
+      int h1 = hexv(Peek()), h2 = hexv(Peek(1));
+      if (h1 < 0 || h2 < 0) { Fail("invalid escape sequence"); return 0; }
+      i_ += 2;
+      return uint32_t(h1 * 16 + h2);
+    }
+    switch (c) {
+      case 'a': return 7;
+      case 'f': return 12;
+      case 'n': return 10;
+      case 'r': return 13;
+      case 't': return 9;
+      case 'v': return 11;
+    }
+    if (c < 0x80 && !((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')))
+      return uint32_t(c);
+    Fail("invalid escape sequence");
+    return 0;
+  }
+
+  static RuneRanges Perl(int c) {
+    switch (c) {
+      case 'd': return {{'0', '9'}};
+      case 's': return {{9, 10}, {12, 13}, {32, 32}};
+      case 'w': return {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+    }
+    return {};
+  }
+
+  static bool Posix(const std::string& name, RuneRanges* r) {
+    static const struct { const char* n; RuneRanges r; } kT[] = {
+        {"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}},
+        {"alpha", {{'A', 'Z'}, {'a', 'z'}}},
+        {"ascii", {{0, 0x7F}}},
+        {"blank", {{9, 9}, {32, 32}}},
+        {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}},
+        {"digit", {{'0', '9'}}},
+        {"graph", {{0x21, 0x7E}}},
+        {"lower", {{'a', 'z'}}},
+        {"print", {{0x20, 0x7E}}},
+        {"punct", {{0x21, 0x2F}, {0x3A, 0x40}, {0x5B, 0x60}, {0x7B, 0x7E}}},
+        {"space", {{9, 13}, {32, 32}}},
+        {"upper", {{'A', 'Z'}}},
+        {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}},
+        {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}},
+    };
+    for (auto& e : kT)
+      if (name == e.n) { *r = e.r; return true; }
+    return false;
+  }
+
+  void Atom(std::vector<int>* out, bool* is_flag) {
+    int c = Peek();
+    if (c == '(') { out->push_back(Group(is_flag)); return; }
+    if (c == '[') { out->push_back(Class()); return; }
+    if (c == '.') {
+      i_++;
+      if (fs_) out->push_back(ClassNode({{0, kMaxRune}}));
+      else out->push_back(ClassNode({{0, 9}, {11, kMaxRune}}));
+      return;
+    }
+    if (c == '^' || c == '$') {
+      i_++;
+      int n = NewNode(NodeOp::Assert);
+      if (c == '^') N(n).assert_op = fm_ ? kEmptyBeginLine : kEmptyBeginText;
+      else N(n).assert_op = fm_ ? kEmptyEndLine : kEmptyEndText;
+      out->push_back(n);
+      return;
+    }
+    if (c == '\\') {
+      i_++;
+      if (AtEnd()) { out->push_back(Fail("trailing backslash at end of expression")); return; }
+      int e = Peek();
+      if (e == 'A' || e == 'z' || e == 'b' || e == 'B') {
+        i_++;
+        int n = NewNode(NodeOp::Assert);
+        N(n).assert_op = e == 'A' ? kEmptyBeginText : e == 'z' ? kEmptyEndText
+                         : e == 'b' ? kEmptyWordBoundary : kEmptyNoWordBoundary;
+        out->push_back(n);
+        return;
+      }
+      if (e == 'd' || e == 's' || e == 'w' || e == 'D' || e == 'S' || e == 'W') {
+        i_++;
+        RuneRanges r = Perl(e | 0x20);
+        out->push_back(ClassNode((e & 0x20) ? r : Negate(r)));
+        return;
+      }
+      if (e == 'p' || e == 'P') { out->push_back(Fail("unicode classes unsupported")); return; }
+      if (e == 'Q') {
+        i_++;
+        size_t end = s_.find("\\E", i_);
+        size_t stop = end == std::string::npos ? s_.size() : end;
+        while (i_ < stop) out->push_back(Literal(NextRune()));
+        i_ = end == std::string::npos ? s_.size() : end + 2;
+        return;
+      }
+      uint32_t r = EscapeRune();
+      out->push_back(Literal(r));
+      return;
+    }
+    out->push_back(Literal(NextRune()));
+  }
+
+  int Group(bool* is_flag) {
+    // named captures (?P<name>re) / (?<name>re)
+    size_t nstart = 0;
+    if (s_.compare(i_, 4, "(?P<") == 0) nstart = i_ + 4;
+    else if (s_.compare(i_, 3, "(?<") == 0 && s_.compare(i_, 4, "(?<=") != 0 && s_.compare(i_, 4, "(?<!") != 0)
+      nstart = i_ + 3;
+    if (nstart) {
+      size_t end = s_.find('>', nstart);
+      if (end == std::string::npos) return Fail("invalid named capture");
+      std::string name = s_.substr(nstart, end - nstart);
+      if (name.empty()) return Fail("invalid named capture");
+      for (char ch : name)
+        if (!(isalnum((unsigned char)ch) || ch == '_')) return Fail("invalid named capture");
+      i_ = end + 1;
+      return Capture(name);
+    }
+    if (s_.compare(i_, 2, "(?") == 0) {
+      size_t j = i_ + 2;
+      bool neg = false, seen = false;
+      bool fl[4] = {fi_, fm_, fs_, fU_};
+      for (;; j++) {
+        if (j >= s_.size()) return Fail("missing closing )");
+        char ch = s_[j];
+        int k = ch == 'i' ? 0 : ch == 'm' ? 1 : ch == 's' ? 2 : ch == 'U' ? 3 : -1;
+        if (k >= 0) { fl[k] = !neg; seen = true; continue; }
+        if (ch == '-') {
+          if (neg) return Fail("invalid or unsupported Perl syntax");
+          neg = true;
+          seen = false;
+          continue;
+        }
+        if (ch == ':' || ch == ')') {
+          if (neg && !seen) return Fail("invalid or unsupported Perl syntax");
+          if (ch == ')' && !seen) return Fail("invalid or unsupported Perl syntax");
+          break;
+        }
+        return Fail("invalid or unsupported Perl syntax");
+      }
+      if (s_[j] == ')') {
+        fi_ = fl[0]; fm_ = fl[1]; fs_ = fl[2]; fU_ = fl[3];
+        i_ = j + 1;
+        *is_flag = true;
+        return -1;
+      }
+      bool sv[4] = {fi_, fm_, fs_, fU_};
+      fi_ = fl[0]; fm_ = fl[1]; fs_ = fl[2]; fU_ = fl[3];
+      i_ = j + 1;
+      int sub = Alt();
+      if (Peek() != ')') return Fail("missing closing )");
+      i_++;
+      fi_ = sv[0]; fm_ = sv[1]; fs_ = sv[2]; fU_ = sv[3];
+      return sub;
+    }
+    i_++;
+    return Capture("");
+  }
+
+  int Capture(const std::string& name) {
+    int idx = ++ncap_;
+    re_->cap_names_.push_back(name);
+    bool sv[4] = {fi_, fm_, fs_, fU_};
+    int sub = Alt();
+    if (Peek() != ')') return Fail("missing closing )");
+    i_++;
+    fi_ = sv[0]; fm_ = sv[1]; fs_ = sv[2]; fU_ = sv[3];
+    int n = NewNode(NodeOp::Capture);
+    N(n).cap = idx;
+    N(n).subs = {sub};
+    return n;
+  }
+
+  uint32_t ClassChar() {
+    if (Peek() == '\\') {
+      i_++;
+      return EscapeRune();
+    }
+    return NextRune();
+  }
+
+  int Class() {
+    i_++;
+    bool negated = false;
+    if (Peek() == '^') { negated = true; i_++; }
+    RuneRanges rr;
+    bool first = true;
+    for (;;) {
+      if (!err_.empty()) return NewNode(NodeOp::NoMatch);
+      int c = Peek();
+      if (c < 0) return Fail("missing closing ]");
+      if (c == ']' && !first) { i_++; break; }
+      first = false;
+      if (c == '[' && Peek(1) == ':') {
+        size_t end = s_.find(":]", i_ + 2);
+        if (end != std::string::npos) {
+          std::string name = s_.substr(i_ + 2, end - i_ - 2);
+          bool neg = !name.empty() && name[0] == '^';
+          if (neg) name = name.substr(1);
+          RuneRanges pr;
+          if (Posix(name, &pr)) {
+            if (neg) pr = Negate(pr);
+            if (fi_) { for (auto& p : pr) AddFolded(&rr, p.first, p.second); }
+            else rr.insert(rr.end(), pr.begin(), pr.end());
+            i_ = end + 2;
+            continue;
+          }
+        }
+      }
+      if (c == '\\') {
+        int e = Peek(1);
+        if (e == 'd' || e == 's' || e == 'w' || e == 'D' || e == 'S' || e == 'W') {
+          RuneRanges r = Perl(e | 0x20);
+          if (!(e & 0x20)) r = Negate(r);
+          rr.insert(rr.end(), r.begin(), r.end());
+          i_ += 2;
+          continue;
+        }
+        if (e == 'p' || e == 'P') return Fail("unicode classes unsupported");
+      }
+      uint32_t lo = ClassChar(), hi = lo;
+      if (Peek() == '-' && Peek(1) >= 0 && Peek(1) != ']') {
+        i_++;
+        hi = ClassChar();
+        if (hi < lo) return Fail("invalid character class range");
+      }
+      if (fi_) AddFolded(&rr, lo, hi);
+      else rr.push_back({lo, hi});
+    }
+    Clean(&rr);
+    if (negated) rr = Negate(rr);
+    int n = NewNode(NodeOp::Class);
+    N(n).ranges = std::move(rr);
+    return n;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Compiler (simplify.go repeats + compile.go)
+// ---------------------------------------------------------------------------
+class Compiler {
+ public:
+  explicit Compiler(Regex* re) : re_(re) {}
+
+  struct Frag {
+    uint32_t i;
+    std::vector<uint32_t> out;  // patch list: (inst << 1) | (0 = out, 1 = arg)
+    bool nullable;
+  };
+
+  void Run() {
+    auto& p = re_->prog_;
+    p.clear();
+    p.push_back(Inst());  // inst 0 = fail (Go: c.init())
+    Frag f = Comp(re_->root_);
+    uint32_t m = Emit(kIMatch);
+    Patch(f.out, m);
+    re_->start_ = f.i;
+  }
+
+ private:
+  Regex* re_;
+
+  uint32_t Emit(InstOp op) {
+    re_->prog_.push_back(Inst());
+    re_->prog_.back().op = op;
+    return uint32_t(re_->prog_.size() - 1);
+  }
+  void Patch(const std::vector<uint32_t>& l, uint32_t to) {
+    for (uint32_t x : l) {
+      Inst& in = re_->prog_[x >> 1];
+      if (x & 1) in.arg = to;
+      else in.out = to;
+    }
+  }
+  static std::vector<uint32_t> Cat(std::vector<uint32_t> a, const std::vector<uint32_t>& b) {
+    a.insert(a.end(), b.begin(), b.end());
+    return a;
+  }
+
+  Frag Nop() {
+    uint32_t i = Emit(kINop);
+    return {i, {i << 1}, true};
+  }
+  Frag FailFrag() { return {0, {}, false}; }
+
+  Frag CatFrag(Frag a, Frag b) {
+    if (a.i == 0 || b.i == 0) return FailFrag();
+    Patch(a.out, b.i);
+    return {a.i, b.out, a.nullable && b.nullable};
+  }
+  Frag AltFrag(Frag a, Frag b) {
+    if (a.i == 0) return b;
+    if (b.i == 0) return a;
+    uint32_t i = Emit(kIAlt);
+    re_->prog_[i].out = a.i;
+    re_->prog_[i].arg = b.i;
+    return {i, Cat(a.out, b.out), a.nullable || b.nullable};
+  }
+  Frag Quest(Frag a, bool nongreedy) {
+    uint32_t i = Emit(kIAlt);
+    std::vector<uint32_t> out;
+    if (nongreedy) {
+      re_->prog_[i].arg = a.i;
+      out = {i << 1};
+    } else {
+      re_->prog_[i].out = a.i;
+      out = {(i << 1) | 1};
+    }
+    return {i, Cat(out, a.out), true};
+  }
+  Frag Loop(Frag a, bool nongreedy) {
+    uint32_t i = Emit(kIAlt);
+    std::vector<uint32_t> out;
+    if (nongreedy) {
+      re_->prog_[i].arg = a.i;
+      out = {i << 1};
+    } else {
+      re_->prog_[i].out = a.i;
+      out = {(i << 1) | 1};
+    }
+    Patch(a.out, i);
+    return {i, out, a.nullable};
+  }
+  Frag Star(Frag a, bool nongreedy) {
+    if (a.nullable) return Quest(Plus(a, nongreedy), nongreedy);
+    return Loop(a, nongreedy);
+  }
+  Frag Plus(Frag a, bool nongreedy) {
+    Frag l = Loop(a, nongreedy);
+    return {a.i, l.out, a.nullable};
+  }
+
+  // Simplified-repeat structure (simplify.go): returns an op tag for idempotence
+  Frag Repeat(int sub, int min, int max, bool greedy) {
+    bool ng = !greedy;
+    const Node& s = re_->nodes_[sub];
+    if (min == 0 && max == 0) return Nop();  // x{0} -> empty
+    // empty-match sub: repeating it is still empty (simplify1)
+    if (s.op == NodeOp::Empty) return Nop();
+    if (max == -1) {
+      if (min == 0) {
+        if (s.op == NodeOp::Repeat && s.min == 0 && s.max == -1 && s.greedy == greedy) return Comp(sub);
+        return Star(Comp(sub), ng);
+      }
+      if (min == 1) {
+        if (s.op == NodeOp::Repeat && s.min == 1 && s.max == -1 && s.greedy == greedy) return Comp(sub);
+        return Plus(Comp(sub), ng);
+      }
+      Frag f = Comp(sub);
+      for (int k = 0; k < min - 2; k++) f = CatFrag(f, Comp(sub));
+      return CatFrag(f, Plus(Comp(sub), ng));
+    }
+    if (min == 1 && max == 1) return Comp(sub);
+    if (min == 0 && max == 1 && s.op == NodeOp::Repeat && s.min == 0 && s.max == 1 && s.greedy == greedy)
+      return Comp(sub);
+    // x{n,m} = n copies of x, then nested (x(x(x)?)?)?
+    bool have = false;
+    Frag prefix{0, {}, true};
+    for (int k = 0; k < min; k++) {
+      Frag c = Comp(sub);
+      prefix = have ? CatFrag(prefix, c) : c;
+      have = true;
+    }
+    if (max > min) {
+      // build suffix from the innermost outwards, as Go does: suffix = x?; then (x suffix)? ...
+      // compile order matters only for instruction numbering, not semantics.
+      Frag suffix = Quest(Comp(sub), ng);
+      for (int k = min + 1; k < max; k++) {
+        Frag c = Comp(sub);
+        suffix = Quest(CatFrag(c, suffix), ng);
+      }
+      prefix = have ? CatFrag(prefix, suffix) : suffix;
+      have = true;
+    }
+    if (!have) return FailFrag();
+    return prefix;
+  }
+
+  Frag Comp(int ni) {
+    const Node n = re_->nodes_[ni];  // copy: nodes_ is not modified, but keep it simple
+    switch (n.op) {
+      case NodeOp::Empty: return Nop();
+      case NodeOp::NoMatch: return FailFrag();
+      case NodeOp::Class: {
+        if (n.ranges.empty()) return FailFrag();
+        if (n.ranges.size() == 1 && n.ranges[0].first == 0 && n.ranges[0].second == kMaxRune) {
+          uint32_t i = Emit(kIAny);
+          return {i, {i << 1}, false};
+        }
+        if (n.ranges.size() == 2 && n.ranges[0].first == 0 && n.ranges[0].second == 9 &&
+            n.ranges[1].first == 11 && n.ranges[1].second == kMaxRune) {
+          uint32_t i = Emit(kIAnyNotNL);
+          return {i, {i << 1}, false};
+        }
+        if (n.ranges.size() == 1 && n.ranges[0].first == n.ranges[0].second) {
+          uint32_t i = Emit(kIRune1);
+          re_->prog_[i].rune = n.ranges[0].first;
+          return {i, {i << 1}, false};
+        }
+        uint32_t i = Emit(kIRune);
+        re_->prog_[i].cls = int(re_->classes_.size());
+        re_->classes_.push_back(n.ranges);
+        return {i, {i << 1}, false};
+      }
+      case NodeOp::Assert: {
+        uint32_t i = Emit(kIEmpty);
+        re_->prog_[i].empty = n.assert_op;
+        return {i, {i << 1}, true};
+      }
+      case NodeOp::Cat: {
+        Frag f{0, {}, true};
+        bool have = false;
+        for (int s : n.subs) {
+          Frag g = Comp(s);
+          if (!have) { f = g; have = true; }
+          else f = CatFrag(f, g);
+        }
+        return have ? f : Nop();
+      }
+      case NodeOp::Alt: {
+        Frag f = Comp(n.subs[0]);
+        for (size_t k = 1; k < n.subs.size(); k++) f = AltFrag(f, Comp(n.subs[k]));
+        return f;
+      }
+      case NodeOp::Capture: {
+        uint32_t a = Emit(kICapture);
+        re_->prog_[a].arg = uint32_t(2 * n.cap);
+        Frag sub = Comp(n.subs[0]);
+        uint32_t b = Emit(kICapture);
+        re_->prog_[b].arg = uint32_t(2 * n.cap + 1);
+        Frag fa{a, {a << 1}, true};
+        Frag fb{b, {b << 1}, true};
+        return CatFrag(CatFrag(fa, sub), fb);
+      }
+      case NodeOp::Repeat: return Repeat(n.subs[0], n.min, n.max, n.greedy);
+    }
+    return FailFrag();
+  }
+};
+
+std::unique_ptr<Regex> Regex::Compile(const std::string& pattern, std::string* err) {
+  std::unique_ptr<Regex> re(new Regex());
+  re->pattern_ = pattern;
+  Parser p(re.get(), pattern);
+  if (!p.Parse(err)) return nullptr;
+  Compiler c(re.get());
+  c.Run();
+  // onepass-style anchoring info: does every path start with \A ?
+  {
+    uint32_t pc = re->start_;
+    for (int guard = 0; guard < 1000; guard++) {
+      const Inst& in = re->prog_[pc];
+      if (in.op == kINop || in.op == kICapture) { pc = in.out; continue; }
+      if (in.op == kIEmpty && (in.empty & kEmptyBeginText)) re->anchored_begin_ = true;
+      break;
+    }
+  }
+  return re;
+}
+
+// ---------------------------------------------------------------------------
+// Pike VM (regexp/exec.go)
+// ---------------------------------------------------------------------------
+class Machine {
+ public:
+  Machine(const Regex* re, int ncap) : re_(re), ncap_(ncap) {
+    size_t n = re->prog_.size();
+    for (int k = 0; k < 2; k++) {
+      q_[k].sparse.assign(n, 0);
+      q_[k].dense.reserve(n);
+    }
+    matchcap_.assign(ncap, -1);
+    // Pre-size thread storage: a queue holds at most one thread per pc, so
+    // 2*|prog| threads suffice; capture pointers into caps_ must stay valid.
+    size_t maxt = 2 * n + 4;
+    tinst_.reserve(maxt);
+    caps_.reserve(maxt * size_t(ncap > 0 ? ncap : 1));
+  }
+
+  // One leftmost-first search from `pos` (m.match).  Returns true on match,
+  // filling matchcap_.  `wins`: allowed start windows (nullptr = everywhere).
+  bool Search(const uint8_t* s, int64_t n, int64_t pos, const std::vector<Window>* wins) {
+    matched_ = false;
+    std::fill(matchcap_.begin(), matchcap_.end(), -1);
+    Queue* runq = &q_[0];
+    Queue* nextq = &q_[1];
+    Clear(runq);
+    Clear(nextq);
+    size_t wi = 0;
+    if (wins) {
+      while (wi < wins->size() && (*wins)[wi].hi < pos) wi++;
+    }
+    Rune r = DecodeRune(s, n, pos);
+    Rune r1 = r.r >= 0 ? DecodeRune(s, n, pos + r.width) : Rune{-1, 0};
+    uint8_t flag = Context(s, n, pos);
+    for (;;) {
+      if (runq->dense.empty()) {
+        if (re_->anchored_begin_ && pos != 0) break;
+        if (matched_) break;
+        if (wins) {
+          // jump to the next allowed start (rune-aligned)
+          while (wi < wins->size() && (*wins)[wi].hi < pos) wi++;
+          if (wi >= wins->size()) break;
+          if ((*wins)[wi].lo > pos) {
+            int64_t t = Align(s, n, (*wins)[wi].lo);
+            if (t > pos) {
+              pos = t;
+              r = DecodeRune(s, n, pos);
+              r1 = r.r >= 0 ? DecodeRune(s, n, pos + r.width) : Rune{-1, 0};
+              flag = Context(s, n, pos);
+            }
+          }
+        }
+      }
+      bool allowed = true;
+      if (wins) {
+        while (wi < wins->size() && (*wins)[wi].hi < pos) wi++;
+        allowed = wi < wins->size() && (*wins)[wi].lo <= pos;
+      }
+      if (!matched_ && allowed && (pos == 0 || !re_->anchored_begin_)) {
+        if (ncap_ > 0) matchcap_[0] = pos;
+        Add(runq, re_->start_, pos, matchcap_.data(), flag, -1);
+      }
+      uint8_t nextflag = EmptyOpContext(r.r, r1.r);
+      Step(runq, nextq, pos, pos + r.width, r.r, nextflag);
+      if (r.width == 0) break;
+      if (ncap_ == 0 && matched_) break;
+      pos += r.width;
+      r = r1;
+      if (r.r >= 0) r1 = DecodeRune(s, n, pos + r.width);
+      flag = nextflag;
+      std::swap(runq, nextq);
+    }
+    Clear(nextq);
+    Clear(runq);
+    return matched_;
+  }
+
+  const std::vector<int64_t>& cap() const { return matchcap_; }
+
+  // Largest Go rune-chain position <= t (see goregex.h): only a continuation
+  // byte inside a valid multi-byte sequence is not a rune boundary.
+  static int64_t Align(const uint8_t* s, int64_t n, int64_t t) {
+    if (t >= n || t <= 0) return t;
+    if ((s[t] & 0xC0) != 0x80) return t;
+    for (int k = 1; k <= 3 && t - k >= 0; k++) {
+      uint8_t b = s[t - k];
+      if ((b & 0xC0) == 0x80) continue;
+      Rune r = DecodeRune(s, n, t - k);
+      if (r.width > k) return t - k;
+      return t;
+    }
+    return t;
+  }
+
+ private:
+  struct Entry {
+    uint32_t pc;
+    int t;  // thread index or -1
+  };
+  struct Queue {
+    std::vector<uint32_t> sparse;
+    std::vector<Entry> dense;
+  };
+  const Regex* re_;
+  int ncap_;
+  Queue q_[2];
+  bool matched_ = false;
+  std::vector<int64_t> matchcap_;
+  std::vector<int64_t> caps_;  // thread capture storage
+  std::vector<uint32_t> tinst_;
+  std::vector<int> free_;
+
+  int Alloc() {
+    if (!free_.empty()) {
+      int t = free_.back();
+      free_.pop_back();
+      return t;
+    }
+    int t = int(tinst_.size());
+    tinst_.push_back(0);
+    caps_.resize(caps_.size() + size_t(ncap_ > 0 ? ncap_ : 1));
+    return t;
+  }
+  int64_t* Cap(int t) { return caps_.data() + size_t(t) * size_t(ncap_ > 0 ? ncap_ : 1); }
+
+  static bool Contains(const Queue* q, uint32_t pc) {
+    uint32_t j = q->sparse[pc];
+    return j < q->dense.size() && q->dense[j].pc == pc;
+  }
+  void Clear(Queue* q) {
+    for (auto& e : q->dense)
+      if (e.t >= 0) free_.push_back(e.t);
+    q->dense.clear();
+  }
+
+  static uint8_t Context(const uint8_t* s, int64_t n, int64_t pos) {
+    int32_t r1 = -1, r2 = -1;
+    if (pos > 0 && pos <= n) {
+      uint8_t b = s[pos - 1];
+      r1 = b < 0x80 ? b : 0xFFFD;  // only ASCII word chars and '\n' matter
+    }
+    if (pos < n) {
+      uint8_t b = s[pos];
+      r2 = b < 0x80 ? b : 0xFFFD;
+    }
+    return EmptyOpContext(r1, r2);
+  }
+
+  // m.add: follow empty transitions; returns the (possibly unused) thread t.
+  int Add(Queue* q, uint32_t pc, int64_t pos, int64_t* cap, uint8_t cond, int t) {
+    if (pc == 0) return t;
+    if (Contains(q, pc)) return t;
+    uint32_t j = uint32_t(q->dense.size());
+    q->sparse[pc] = j;
+    q->dense.push_back({pc, -1});
+    const Inst& in = re_->prog_[pc];
+    switch (in.op) {
+      case kIFail: break;
+      case kIAlt:
+        t = Add(q, in.out, pos, cap, cond, t);
+        t = Add(q, in.arg, pos, cap, cond, t);
+        break;
+      case kIEmpty:
+        if ((in.empty & ~cond) == 0) t = Add(q, in.out, pos, cap, cond, t);
+        break;
+      case kINop: t = Add(q, in.out, pos, cap, cond, t); break;
+      case kICapture:
+        if (int(in.arg) < ncap_) {
+          int64_t opos = cap[in.arg];
+          cap[in.arg] = pos;
+          Add(q, in.out, pos, cap, cond, -1);
+          cap[in.arg] = opos;
+        } else {
+          t = Add(q, in.out, pos, cap, cond, t);
+        }
+        break;
+      default: {  // Match, Rune*, Any*
+        if (t < 0) t = Alloc();
+        tinst_[t] = pc;
+        if (ncap_ > 0 && Cap(t) != cap) std::memcpy(Cap(t), cap, sizeof(int64_t) * size_t(ncap_));
+        q->dense[j].t = t;
+        t = -1;
+      }
+    }
+    return t;
+  }
+
+  bool MatchRune(const Inst& in, int32_t c) const {
+    switch (in.op) {
+      case kIRune1: return c == int32_t(in.rune);
+      case kIRune: return c >= 0 && InRanges(re_->classes_[in.cls], uint32_t(c));
+      case kIAny: return c >= 0;
+      case kIAnyNotNL: return c >= 0 && c != '\n';
+      default: return false;
+    }
+  }
+
+  void Step(Queue* runq, Queue* nextq, int64_t pos, int64_t nextpos, int32_t c, uint8_t nextcond) {
+    for (size_t j = 0; j < runq->dense.size(); j++) {
+      int t = runq->dense[j].t;
+      if (t < 0) continue;
+      const Inst& in = re_->prog_[tinst_[t]];
+      bool add = false;
+      if (in.op == kIMatch) {
+        if (ncap_ > 0) {
+          Cap(t)[1] = pos;
+          std::memcpy(matchcap_.data(), Cap(t), sizeof(int64_t) * size_t(ncap_));
+        }
+        // first-match mode: cut off lower-priority threads
+        for (size_t k = j + 1; k < runq->dense.size(); k++)
+          if (runq->dense[k].t >= 0) free_.push_back(runq->dense[k].t);
+        runq->dense.resize(j + 1);
+        matched_ = true;
+      } else {
+        add = MatchRune(in, c);
+      }
+      if (add) t = Add(nextq, in.out, nextpos, ncap_ > 0 ? Cap(t) : nullptr, nextcond, t);
+      if (t >= 0) free_.push_back(t);
+      runq->dense[j].t = -1;
+    }
+    runq->dense.clear();
+  }
+};
+
+bool Regex::Match(const uint8_t* s, int64_t n) const {
+  Machine m(this, 0);
+  return m.Search(s, n, 0, nullptr);
+}
+
+void Regex::FindAll(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
+                    std::vector<int64_t>* out) const {
+  int ncap = submatch ? 2 * (num_cap_ + 1) : 2;
+  Machine m(this, ncap);
+  int64_t pos = 0, prev_end = -1;
+  while (pos <= n) {
+    if (!m.Search(s, n, pos, wins)) break;
+    const auto& c = m.cap();
+    bool accept = true;
+    if (c[1] == pos) {  // empty match
+      if (c[0] == prev_end) accept = false;
+      Rune r = DecodeRune(s, n, pos);
+      pos += r.width > 0 ? r.width : 1;
+    } else {
+      pos = c[1];
+    }
+    prev_end = c[1];
+    if (accept) out->insert(out->end(), c.begin(), c.end());
+  }
+}
+
+}  // namespace tsg
