@@ -27,6 +27,35 @@ int tsg_regex_match(const char* pattern, const uint8_t* text, uint64_t n);
 /* bytes.ToLower (Go semantics).  Writes up to out_cap bytes, returns the full length. */
 int64_t tsg_go_bytes_to_lower(const uint8_t* s, uint64_t n, uint8_t* out, uint64_t out_cap);
 
+/* ---- rule compiler inspection (tables the GPU kernels consume) ---- */
+struct tsg_global;
+typedef struct tsg_compiled tsg_compiled;
+struct tsg_table_info;
+typedef struct tsg_debug_rule_info {
+  uint32_t nfa_words;     /* 0: relaxed NFA empty */
+  uint32_t gate;          /* 0 always, 1 keyword bitset, 2 host-verified */
+  uint32_t anchored;      /* 1 anchor-driven, 0 full-scan */
+  uint32_t has_regex;
+  const uint64_t* nfa;    /* O[W] L[W] F[W] B[256][W] */
+  const uint32_t* kw_ids;
+  uint32_t n_kw;
+} tsg_debug_rule_info;
+int tsg_debug_compile(const struct tsg_global* g, tsg_compiled** out);
+void tsg_debug_compiled_free(tsg_compiled* c);
+int tsg_debug_compiled_info(const tsg_compiled* c, struct tsg_table_info* out);
+int tsg_debug_ac(const tsg_compiled* c, const uint8_t** cmap, const uint16_t** trans,
+                 const uint32_t** out_off, const uint32_t** out_items, uint32_t* n_out_items);
+int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out);
+int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t* lit_len,
+                     int32_t* off_lo, int32_t* off_hi);
+const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k);
+
+/* Test hook: the exact host tail (include/tsg_scanner.h) fed with whole-file
+ * candidate windows instead of the GPU's, on CPU.  Not a product path. */
+struct tsg_batch;
+struct tsg_result;
+int tsg_debug_host_tail(const struct tsg_global* g, const struct tsg_batch* b, struct tsg_result** out);
+
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);
 

@@ -1,0 +1,126 @@
+/* libtsg.so -- MI355X secret-scanning engine, C ABI (cgo / ctypes bindable).
+ *
+ * Drop-in boundary for pkg/fanal/secret (undistro/trivy @ 2024-12-20).  The
+ * host language keeps ParseConfig / NewScanner's rule-set assembly
+ * (pkg/fanal/secret/scanner.go:277-364) and hands the resulting *Global* to
+ * tsg_scanner_new; Scan(ScanArgs) (scanner.go:377-463) becomes a batched
+ * tsg_scan over a contiguous arena of CR-stripped file contents
+ * (pkg/fanal/analyzer/secret/secret.go:117-141 does the stripping).
+ *
+ * Entry point                 replaces (reference)
+ *   tsg_scanner_new           secret.NewScanner(config)            scanner.go:320-364
+ *   tsg_scanner_allow_path    (Global).AllowPath(path)             scanner.go:57-59
+ *   tsg_scan                  (*Scanner).Scan(ScanArgs), per file  scanner.go:377-463
+ *   tsg_result_*              types.Secret / SecretFinding / Code  pkg/fanal/types/secret.go:5-20,
+ *                                                                 misconf.go:48-61
+ * Conventions: all pointers are borrowed for the duration of the call;
+ * results are owned by the library until tsg_result_free.  Status: 0 = OK,
+ * <0 = error, text via tsg_last_error() (tsg_debug.h).  Thread-safety: one
+ * tsg_scan at a time per scanner (the engine owns one HIP stream).
+ */
+#ifndef TSG_SCANNER_H
+#define TSG_SCANNER_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tsg_allow_rule {  /* AllowRule, scanner.go:196-201 */
+  const char* id;
+  const char* regex;             /* NULL or "" = none */
+  const char* path;              /* NULL or "" = none */
+} tsg_allow_rule;
+
+typedef struct tsg_rule {        /* Rule, scanner.go:89-100 */
+  const char* id;
+  const char* category;
+  const char* title;
+  const char* severity;          /* already normalised by ParseConfig */
+  const char* regex;             /* NULL = rule without regex (never matches) */
+  const char* path;              /* NULL = any path */
+  const char* secret_group_name; /* "" = whole match */
+  const char* const* keywords;
+  uint32_t n_keywords;
+  const tsg_allow_rule* allow_rules;
+  uint32_t n_allow_rules;
+  const char* const* exclude_regexes; /* ExcludeBlock.Regexes */
+  uint32_t n_exclude_regexes;
+} tsg_rule;
+
+typedef struct tsg_global {      /* Global, scanner.go:45-49 (the assembled rule set) */
+  const tsg_rule* rules;
+  uint32_t n_rules;
+  const tsg_allow_rule* allow_rules;
+  uint32_t n_allow_rules;
+  const char* const* exclude_regexes;
+  uint32_t n_exclude_regexes;
+} tsg_global;
+
+typedef struct tsg_scanner tsg_scanner;
+typedef struct tsg_result tsg_result;
+
+/* Compile the rule set (keyword/anchor automaton + relaxed NFAs) and bind a HIP device. */
+int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out);
+void tsg_scanner_free(tsg_scanner* s);
+/* 1 if path is globally allowed (Global.AllowPath), else 0. */
+int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len);
+
+typedef struct tsg_batch {
+  uint32_t n_files;
+  const uint8_t* host_arena;     /* concatenated contents, required (exact pass) */
+  const uint64_t* host_offsets;  /* n_files + 1 */
+  const void* dev_arena;         /* optional: same bytes already in HBM (16-B aligned, +16 B pad) */
+  const void* dev_offsets;       /* optional: device copy of host_offsets */
+  const char* const* paths;      /* ScanArgs.FilePath per file */
+  const uint64_t* path_lens;     /* optional */
+  const uint8_t* binary;         /* optional ScanArgs.Binary per file */
+} tsg_batch;
+
+int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);
+void tsg_result_free(tsg_result* r);
+
+/* kind: 0 = types.Secret{} (no findings), 1 = Secret{FilePath} (allowed path), 2 = findings */
+int tsg_result_file(const tsg_result* r, uint32_t file, uint32_t* kind, uint32_t* n_findings);
+
+typedef struct tsg_finding {
+  uint32_t rule_index;           /* into tsg_global.rules */
+  int64_t start_line, end_line;
+  const char* match;
+  uint64_t match_len;
+  uint32_t n_lines;
+} tsg_finding;
+int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_finding* out);
+
+typedef struct tsg_line {
+  int64_t number;
+  const char* content;
+  uint64_t content_len;
+  uint8_t is_cause, first_cause, last_cause;
+} tsg_line;
+int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out);
+
+/* Whole batch as JSON ([{"kind":..,"findings":[..]}...], Go field names). */
+int tsg_result_json(const tsg_result* r, const char** json, uint64_t* len);
+
+/* Timings / counters of the batch (GPU ms from HIP events on the engine stream). */
+typedef struct tsg_stats {
+  uint64_t bytes, files, anchor_hits, candidates, special_files, findings;
+  double ms_scan_kernel, ms_verify_kernel, ms_fullscan_kernel, ms_gpu_total;
+  double ms_host_gpu_phase, ms_host_allow_path, ms_host_exact, ms_host_total;
+} tsg_stats;
+int tsg_result_stats(const tsg_result* r, tsg_stats* out);
+
+/* Compiled-table facts (for reports/tests). */
+typedef struct tsg_table_info {
+  uint32_t n_rules, n_keywords, n_anchors, ac_states, ac_classes, max_pattern_len;
+  uint32_t n_fullscan_rules, nfa_words_total;
+  uint64_t ac_table_bytes;
+} tsg_table_info;
+int tsg_scanner_table_info(const tsg_scanner* s, tsg_table_info* out);
+/* Anchor description of rule i ("[lo,hi] lit lit..." or "-"). */
+const char* tsg_scanner_rule_anchor(const tsg_scanner* s, uint32_t i);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,92 @@
+"""Exact host tail (libtsg.so) vs the oracle on CPU.
+
+Drives the C++ tail through the test hook ``tsg_debug_host_tail`` (whole-file
+candidate windows, keyword gate from Go's bytes.ToLower) so that allow rules,
+exclude blocks, group extraction, censoring, findLocation and the pdqsort
+order are checked without a GPU.  The GPU candidate stage is covered by
+tests/test_gpu_parity.py and tests/test_kernel_model.py.
+"""
+import ctypes as c
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import secret_scanner as osc
+from tests.corpus import make_corpus
+from trivy_amd import _lib
+from trivy_amd.secret import ParseConfig, builtin_allow_rules, builtin_rules
+from trivy_amd.secret.scanner import CGlobal, ScanResult, _CBatch, _declare, _b
+
+G = Path(__file__).resolve().parent / "golden"
+CASES = json.loads((G / "scanner_cases.json").read_text())["cases"]
+
+
+class _Owner:
+    def __init__(self, L):
+        self._L = L
+
+
+def _assemble(cfg):
+    b_rules, b_allow = builtin_rules(), builtin_allow_rules()
+    if cfg is None:
+        return b_rules, b_allow, []
+    enabled = b_rules
+    if cfg.EnableBuiltinRuleIDs:
+        enabled = [r for r in b_rules if r.ID in cfg.EnableBuiltinRuleIDs]
+    enabled = enabled + cfg.CustomRules
+    rules = [r for r in enabled if r.ID not in cfg.DisableRuleIDs]
+    allow = [a for a in b_allow + cfg.CustomAllowRules if a.ID not in cfg.DisableAllowRuleIDs]
+    return rules, allow, cfg.ExcludeBlock.Regexes
+
+
+def host_tail_scan(cfg, files):
+    L = _lib.lib()
+    _declare(L)
+    L.tsg_debug_host_tail.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_void_p)]
+    rules, allow, exclude = _assemble(cfg)
+    cg = CGlobal(rules, allow, exclude)
+    contents = [b for _, b in files]
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 16, dtype=np.uint8)
+    pb = [_b(p) for p, _ in files]
+    parr = (c.c_char_p * max(1, len(pb)))(*pb)
+    plen = np.array([len(p) for p in pb], dtype=np.uint64)
+    batch = _CBatch(len(files), arena.ctypes.data, offs.ctypes.data, None, None, parr, plen.ctypes.data, None)
+    h = c.c_void_p()
+    if L.tsg_debug_host_tail(c.byref(cg.g), c.byref(batch), c.byref(h)) != 0:
+        raise RuntimeError(_lib.last_error())
+    return ScanResult(_Owner(L), h).secrets([p for p, _ in files])
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] + "|" + c["config"] for c in CASES])
+def test_host_tail_golden(case):
+    cfg = ParseConfig(str(G / "scanner" / case["config"]))
+    content = (G / "scanner" / case["input"]).read_bytes().replace(b"\r", b"")
+    got = host_tail_scan(cfg, [(case["file_path"], content)])[0]
+    assert got.to_dict() == case["want"]
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_host_tail_corpus_vs_oracle(seed):
+    files = [(p, b.replace(b"\r", b"")) for p, b in make_corpus(seed, 150)]
+    got = host_tail_scan(None, files)
+    o = osc.new_scanner(None)
+    n = 0
+    for (p, b), g in zip(files, got):
+        want = o.scan(p, b)
+        assert g.to_dict() == want, p
+        n += len(want["Findings"] or [])
+    assert n > 5
+
+
+def test_host_tail_many_findings_sort_order():
+    # > 12 findings in one file exercises pdqsort beyond insertion sort
+    body = b"\n".join(b"tok%02d ghp_%036d AKIA%016d " % (i, i * 7919 % 1000, i) for i in range(40))
+    files = [("many.txt", body)]
+    got = host_tail_scan(None, files)[0]
+    want = osc.new_scanner(None).scan("many.txt", body)
+    assert got.to_dict() == want
+    assert len(want["Findings"]) > 12

@@ -1,0 +1,408 @@
+// C ABI of the drop-in scanner (include/tsg_scanner.h) and of the rule
+// compiler inspection hooks (include/tsg_debug.h).
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "scanner.h"
+#include "tsg_debug.h"
+#include "tsg_scanner.h"
+
+namespace tsg {
+void SetError(const std::string& e);
+}
+
+struct tsg_scanner {
+  std::unique_ptr<tsg::SecretScanner> s;
+};
+
+struct tsg_result {
+  std::vector<tsg::FileResult> files;
+  tsg_stats stats;
+  std::string json;
+  const tsg::SecretScanner* owner;
+  std::unique_ptr<tsg::SecretScanner> debug_owner;  // tsg_debug_host_tail only
+};
+
+struct tsg_compiled {
+  tsg::CompiledRules cr;
+};
+
+namespace {
+std::string Str(const char* s) { return s ? std::string(s) : std::string(); }
+
+bool MakeMatcher(const char* src, std::unique_ptr<tsg::Matcher>* out, std::string* err) {
+  if (!src || !*src) return true;
+  auto re = tsg::Regex::Compile(src, err);
+  if (!re) return false;
+  out->reset(new tsg::Matcher());
+  (*out)->lits = tsg::RequiredLiterals(*re);
+  (*out)->re = std::move(re);
+  return true;
+}
+
+bool MakeAllow(const tsg_allow_rule* a, uint32_t n, std::vector<tsg::AllowRuleSpec>* out, std::string* err) {
+  for (uint32_t i = 0; i < n; i++) {
+    tsg::AllowRuleSpec s;
+    s.id = Str(a[i].id);
+    if (!MakeMatcher(a[i].regex, &s.regex, err) || !MakeMatcher(a[i].path, &s.path, err)) return false;
+    out->push_back(std::move(s));
+  }
+  return true;
+}
+
+bool MakeExclude(const char* const* rx, uint32_t n, std::vector<std::unique_ptr<tsg::Regex>>* out,
+                 std::string* err) {
+  for (uint32_t i = 0; i < n; i++) {
+    auto re = tsg::Regex::Compile(Str(rx[i]), err);
+    if (!re) return false;
+    out->push_back(std::move(re));
+  }
+  return true;
+}
+
+bool MakeRules(const tsg_global* g, std::vector<tsg::RuleSpec>* rules, std::string* err) {
+  for (uint32_t i = 0; i < g->n_rules; i++) {
+    const tsg_rule& r = g->rules[i];
+    tsg::RuleSpec s;
+    s.id = Str(r.id);
+    s.category = Str(r.category);
+    s.title = Str(r.title);
+    s.severity = Str(r.severity);
+    s.secret_group_name = Str(r.secret_group_name);
+    s.regex_src = Str(r.regex);
+    for (uint32_t k = 0; k < r.n_keywords; k++) s.keywords.push_back(Str(r.keywords[k]));
+    if (!MakeMatcher(r.path, &s.path, err)) return false;
+    if (!MakeAllow(r.allow_rules, r.n_allow_rules, &s.allow_rules, err)) return false;
+    if (!MakeExclude(r.exclude_regexes, r.n_exclude_regexes, &s.exclude, err)) return false;
+    rules->push_back(std::move(s));
+  }
+  return true;
+}
+
+void JsonStr(std::string* o, const std::string& s) {
+  static const char* hex = "0123456789abcdef";
+  o->push_back('"');
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o->push_back('\\');
+      o->push_back(char(c));
+    } else if (c < 0x20) {
+      *o += "\\u00";
+      o->push_back(hex[c >> 4]);
+      o->push_back(hex[c & 15]);
+    } else if (c >= 0x80) {
+      // raw bytes are carried as \u00XX escapes of latin-1 code points so that
+      // non-UTF-8 content survives; the Python side re-encodes as latin-1.
+      *o += "\\u00";
+      o->push_back(hex[c >> 4]);
+      o->push_back(hex[c & 15]);
+    } else {
+      o->push_back(char(c));
+    }
+  }
+  o->push_back('"');
+}
+}  // namespace
+
+extern "C" {
+
+int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out) {
+  std::string err;
+  std::vector<tsg::RuleSpec> rules;
+  std::vector<tsg::AllowRuleSpec> allow;
+  std::vector<std::unique_ptr<tsg::Regex>> exclude;
+  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
+      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
+    tsg::SetError(err);
+    return -1;
+  }
+  std::unique_ptr<tsg_scanner> s(new tsg_scanner());
+  s->s.reset(new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), device, &err));
+  if (!s->s->ok()) {
+    tsg::SetError(err.empty() ? s->s->error() : err);
+    return -2;
+  }
+  *out = s.release();
+  return 0;
+}
+
+void tsg_scanner_free(tsg_scanner* s) { delete s; }
+
+int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len) {
+  return s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len)) ? 1 : 0;
+}
+
+int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
+  tsg::BatchInput in;
+  in.n_files = b->n_files;
+  in.host_arena = b->host_arena;
+  in.host_offsets = b->host_offsets;
+  in.dev_arena = static_cast<const uint8_t*>(b->dev_arena);
+  in.dev_offsets = static_cast<const uint64_t*>(b->dev_offsets);
+  in.paths = b->paths;
+  in.path_lens = b->path_lens;
+  in.binary = b->binary;
+  std::unique_ptr<tsg_result> r(new tsg_result());
+  r->owner = s->s.get();
+  tsg::BatchStats gs;
+  tsg::HostStats hs;
+  if (!s->s->Scan(in, &r->files, &gs, &hs)) {
+    tsg::SetError(s->s->error());
+    return -1;
+  }
+  tsg_stats& st = r->stats;
+  std::memset(&st, 0, sizeof(st));
+  st.bytes = gs.bytes;
+  st.files = gs.files;
+  st.anchor_hits = gs.hits;
+  st.candidates = gs.candidates;
+  st.special_files = gs.special_files;
+  st.findings = hs.findings;
+  st.ms_scan_kernel = gs.ms_scan;
+  st.ms_verify_kernel = gs.ms_verify;
+  st.ms_fullscan_kernel = gs.ms_fullscan;
+  st.ms_gpu_total = gs.ms_total;
+  st.ms_host_gpu_phase = hs.ms_gpu;
+  st.ms_host_allow_path = hs.ms_allow;
+  st.ms_host_exact = hs.ms_exact;
+  st.ms_host_total = hs.ms_total;
+  *out = r.release();
+  return 0;
+}
+
+void tsg_result_free(tsg_result* r) { delete r; }
+
+int tsg_result_file(const tsg_result* r, uint32_t file, uint32_t* kind, uint32_t* n) {
+  if (file >= r->files.size()) return -1;
+  *kind = r->files[file].kind;
+  *n = uint32_t(r->files[file].findings.size());
+  return 0;
+}
+
+int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_finding* out) {
+  if (file >= r->files.size() || k >= r->files[file].findings.size()) return -1;
+  const auto& f = r->files[file].findings[k];
+  out->rule_index = f.rule;
+  out->start_line = f.start_line;
+  out->end_line = f.end_line;
+  out->match = f.match.data();
+  out->match_len = f.match.size();
+  out->n_lines = uint32_t(f.lines.size());
+  return 0;
+}
+
+int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out) {
+  if (file >= r->files.size() || k >= r->files[file].findings.size()) return -1;
+  const auto& f = r->files[file].findings[k];
+  if (line >= f.lines.size()) return -1;
+  const auto& l = f.lines[line];
+  out->number = l.number;
+  out->content = l.content.data();
+  out->content_len = l.content.size();
+  out->is_cause = l.is_cause;
+  out->first_cause = l.first_cause;
+  out->last_cause = l.last_cause;
+  return 0;
+}
+
+int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
+  tsg_result* r = const_cast<tsg_result*>(rc);
+  if (r->json.empty()) {
+    const auto& rules = r->owner->rules();
+    std::string& o = r->json;
+    o.reserve(256 + r->stats.findings * 512);
+    o.push_back('[');
+    for (size_t i = 0; i < r->files.size(); i++) {
+      const auto& fr = r->files[i];
+      if (i) o.push_back(',');
+      o += "{\"kind\":" + std::to_string(int(fr.kind)) + ",\"findings\":[";
+      for (size_t k = 0; k < fr.findings.size(); k++) {
+        const auto& f = fr.findings[k];
+        const auto& R = rules[f.rule];
+        if (k) o.push_back(',');
+        o += "{\"RuleID\":";
+        JsonStr(&o, R.id);
+        o += ",\"Category\":";
+        JsonStr(&o, R.category);
+        o += ",\"Severity\":";
+        JsonStr(&o, R.severity.empty() ? std::string("UNKNOWN") : R.severity);
+        o += ",\"Title\":";
+        JsonStr(&o, R.title);
+        o += ",\"StartLine\":" + std::to_string(f.start_line) + ",\"EndLine\":" + std::to_string(f.end_line);
+        o += ",\"Code\":{\"Lines\":[";
+        for (size_t j = 0; j < f.lines.size(); j++) {
+          const auto& l = f.lines[j];
+          if (j) o.push_back(',');
+          o += "{\"Number\":" + std::to_string(l.number) + ",\"Content\":";
+          JsonStr(&o, l.content);
+          o += ",\"IsCause\":";
+          o += l.is_cause ? "true" : "false";
+          o += ",\"Annotation\":\"\",\"Truncated\":false,\"Highlighted\":";
+          JsonStr(&o, l.content);
+          o += ",\"FirstCause\":";
+          o += l.first_cause ? "true" : "false";
+          o += ",\"LastCause\":";
+          o += l.last_cause ? "true" : "false";
+          o.push_back('}');
+        }
+        o += "]},\"Match\":";
+        JsonStr(&o, f.match);
+        o.push_back('}');
+      }
+      o += "]}";
+    }
+    o.push_back(']');
+  }
+  *json = r->json.data();
+  *len = r->json.size();
+  return 0;
+}
+
+int tsg_result_stats(const tsg_result* r, tsg_stats* out) {
+  *out = r->stats;
+  return 0;
+}
+
+static void FillInfo(const tsg::CompiledRules& cr, tsg_table_info* out) {
+  out->n_rules = uint32_t(cr.rules.size());
+  out->n_keywords = uint32_t(cr.keywords.size());
+  out->n_anchors = uint32_t(cr.anchors.size());
+  out->ac_states = cr.n_states;
+  out->ac_classes = cr.n_classes;
+  out->max_pattern_len = cr.max_pat_len;
+  out->n_fullscan_rules = cr.n_fullscan_rules;
+  uint32_t w = 0;
+  for (auto& r : cr.rules) w += r.nfa_words;
+  out->nfa_words_total = w;
+  out->ac_table_bytes = uint64_t(cr.n_states) * cr.n_classes * 2;
+}
+
+int tsg_scanner_table_info(const tsg_scanner* s, tsg_table_info* out) {
+  FillInfo(s->s->compiled(), out);
+  return 0;
+}
+
+const char* tsg_scanner_rule_anchor(const tsg_scanner* s, uint32_t i) {
+  const auto& d = s->s->compiled().rule_anchor_desc;
+  return i < d.size() ? d[i].c_str() : "";
+}
+
+// ---- tsg_debug.h: rule compiler inspection (no GPU) ------------------------
+
+int tsg_debug_compile(const tsg_global* g, tsg_compiled** out) {
+  std::string err;
+  std::vector<tsg::RuleSrc> src;
+  for (uint32_t i = 0; i < g->n_rules; i++) {
+    const tsg_rule& r = g->rules[i];
+    tsg::RuleSrc s{Str(r.id), Str(r.regex), {}};
+    for (uint32_t k = 0; k < r.n_keywords; k++) s.keywords.push_back(Str(r.keywords[k]));
+    src.push_back(std::move(s));
+  }
+  std::unique_ptr<tsg_compiled> c(new tsg_compiled());
+  if (!tsg::CompileRules(src, &c->cr, &err)) {
+    tsg::SetError(err);
+    return -1;
+  }
+  *out = c.release();
+  return 0;
+}
+
+void tsg_debug_compiled_free(tsg_compiled* c) { delete c; }
+
+int tsg_debug_compiled_info(const tsg_compiled* c, tsg_table_info* out) {
+  FillInfo(c->cr, out);
+  return 0;
+}
+
+int tsg_debug_ac(const tsg_compiled* c, const uint8_t** cmap, const uint16_t** trans, const uint32_t** out_off,
+                 const uint32_t** out_items, uint32_t* n_out_items) {
+  *cmap = c->cr.cmap;
+  *trans = c->cr.trans.data();
+  *out_off = c->cr.out_off.data();
+  *out_items = c->cr.out_items.data();
+  *n_out_items = uint32_t(c->cr.out_items.size());
+  return 0;
+}
+
+int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out) {
+  if (i >= c->cr.rules.size()) return -1;
+  const auto& r = c->cr.rules[i];
+  out->nfa_words = r.nfa_words;
+  out->gate = r.gate;
+  out->anchored = r.anchored;
+  out->has_regex = r.has_regex;
+  out->nfa = c->cr.nfa.data() + r.nfa_off;
+  out->kw_ids = c->cr.rule_kw.data() + r.kw_off;
+  out->n_kw = r.kw_cnt;
+  return 0;
+}
+
+int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t* lit_len, int32_t* off_lo,
+                     int32_t* off_hi) {
+  if (j >= c->cr.anchors.size()) return -1;
+  const auto& a = c->cr.anchors[j];
+  *rule = a.rule;
+  *lit_len = a.lit_len;
+  *off_lo = a.off_lo;
+  *off_hi = a.off_hi;
+  return 0;
+}
+
+const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k) {
+  return k < c->cr.keywords.size() ? c->cr.keywords[k].c_str() : nullptr;
+}
+
+}  // extern "C"
+
+// ---- test hook: exact host tail with whole-file windows (no GPU) -----------
+// Candidates are every (file, rule with regex) whose keyword gate holds under
+// Go's bytes.ToLower, with the whole file as the start window.  This is NOT a
+// product path (tsg_scan always runs the GPU kernels first); it lets the CPU
+// test-suite check the exact tail against the oracle.
+extern "C" int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_result** out) {
+  std::string err;
+  std::vector<tsg::RuleSpec> rules;
+  std::vector<tsg::AllowRuleSpec> allow;
+  std::vector<std::unique_ptr<tsg::Regex>> exclude;
+  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
+      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
+    tsg::SetError(err);
+    return -1;
+  }
+  std::unique_ptr<tsg::SecretScanner> sc(
+      new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), -1, &err));
+  if (!sc->ok()) {
+    tsg::SetError(err);
+    return -2;
+  }
+  std::vector<tsg::Candidate> cands;
+  for (uint32_t f = 0; f < b->n_files; f++) {
+    uint64_t fs = b->host_offsets[f], fe = b->host_offsets[f + 1];
+    std::string lower = tsg::GoBytesToLower(b->host_arena + fs, size_t(fe - fs));
+    for (uint32_t r = 0; r < sc->rules().size(); r++) {
+      const auto& R = sc->rules()[r];
+      bool gate = R.keywords.empty();
+      for (auto& kw : R.kw_lower_host)
+        if (lower.find(kw) != std::string::npos) gate = true;
+      if (!gate || !sc->compiled().regex[r]) continue;
+      cands.push_back({f, r, 0, int64_t(fe - fs), 0});
+    }
+  }
+  tsg::BatchInput in;
+  in.n_files = b->n_files;
+  in.host_arena = b->host_arena;
+  in.host_offsets = b->host_offsets;
+  in.paths = b->paths;
+  in.path_lens = b->path_lens;
+  in.binary = b->binary;
+  std::unique_ptr<tsg_result> r(new tsg_result());
+  tsg::HostStats hs;
+  sc->HostTail(in, &cands, &r->files, &hs);
+  std::memset(&r->stats, 0, sizeof(r->stats));
+  r->stats.findings = hs.findings;
+  r->owner = sc.get();
+  r->debug_owner = std::move(sc);
+  *out = r.release();
+  return 0;
+}

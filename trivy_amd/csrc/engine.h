@@ -1,0 +1,87 @@
+// GPU candidate engine: one instance per HIP device.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rules.h"
+
+namespace tsg {
+
+constexpr uint32_t kChunk = 512;  // bytes per lane-chunk in the scan kernel
+
+struct Candidate {      // produced by the verify / full-scan kernels
+  uint32_t file;
+  uint32_t rule;
+  int64_t wlo, whi;     // allowed match-start window, file-relative, inclusive
+  int64_t nl_before;    // '\n' count in [file start, wlo)
+};
+
+struct BatchStats {
+  uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
+  float ms_scan = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
+  bool hit_overflow = false, cand_overflow = false;
+};
+
+class GpuEngine {
+ public:
+  GpuEngine(const CompiledRules& cr, int device);
+  ~GpuEngine();
+  bool ok() const { return err_.empty(); }
+  const std::string& error() const { return err_; }
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }
+
+  // Run the kernels over a device-resident arena.  Offsets: n_files+1 u64
+  // (device).  Results are copied back into `cands` / `special`.
+  bool Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
+           std::vector<Candidate>* cands, BatchStats* st);
+
+  // Host-pointer convenience: stages host arena + offsets through device
+  // buffers owned by the engine (PCIe-inclusive path).
+  bool RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
+               std::vector<Candidate>* cands, BatchStats* st);
+
+  // Device buffers of the last run (for tests / bench).
+  hipEvent_t ev_scan0() const { return ev_[0]; }
+  hipEvent_t ev_scan1() const { return ev_[1]; }
+
+ private:
+  bool Ensure(void** p, size_t* cap, size_t need);
+  std::string err_;
+  int device_ = 0;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_[4] = {};
+  // tables
+  uint8_t* d_cmap_ = nullptr;
+  uint16_t* d_trans_ = nullptr;
+  uint32_t* d_out_off_ = nullptr;
+  uint32_t* d_out_items_ = nullptr;
+  AnchorInfo* d_anchors_ = nullptr;
+  RuleGpu* d_rules_ = nullptr;
+  uint32_t* d_rule_kw_ = nullptr;
+  uint64_t* d_nfa_ = nullptr;
+  uint32_t* d_fullscan_rules_ = nullptr;
+  uint32_t n_states_ = 0, n_classes_ = 0, max_pat_len_ = 0, kw_words_ = 0, n_rules_ = 0;
+  uint32_t n_fullscan_rules_ = 0;
+  std::vector<uint32_t> fullscan_rules_, regex_rules_;
+  uint32_t* d_regex_rules_ = nullptr;
+  size_t lds_bytes_ = 0;
+  bool table_in_lds_ = true;
+  // per-batch buffers
+  void* d_chunk_file_ = nullptr; size_t cap_chunk_file_ = 0;
+  void* d_nl_ = nullptr; size_t cap_nl_ = 0;
+  void* d_kw_ = nullptr; size_t cap_kw_ = 0;
+  void* d_flags_ = nullptr; size_t cap_flags_ = 0;
+  void* d_hits_ = nullptr; size_t cap_hits_ = 0;
+  void* d_cands_ = nullptr; size_t cap_cands_ = 0;
+  void* d_special_ = nullptr; size_t cap_special_ = 0;
+  uint32_t* d_counters_ = nullptr;  // [0]=hits [1]=cands [2]=special [3]=hit overflow [4]=cand overflow
+  void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
+  void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
+  uint32_t hit_cap_ = 0, cand_cap_ = 0;
+};
+
+}  // namespace tsg

@@ -128,6 +128,70 @@ Rune DecodeRune(const uint8_t* s, int64_t n, int64_t pos) {
   return {0xFFFD, 1};
 }
 
+bool GoIsPrint(uint32_t r) {
+  if (r < 0x80) return r >= 0x20 && r < 0x7F;
+  size_t n = sizeof(kPrint) / sizeof(kPrint[0]);
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (r < kPrint[m][0]) hi = m;
+    else if (r > kPrint[m][1]) lo = m + 1;
+    else return true;
+  }
+  return false;
+}
+
+static void AppendUtf8(std::string* out, uint32_t r);
+
+std::string GoQuote(const std::string& s) {  // strconv.Quote
+  static const char* hex = "0123456789abcdef";
+  std::string o = "\"";
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(s.data());
+  int64_t n = int64_t(s.size()), pos = 0;
+  while (pos < n) {
+    Rune r = DecodeRune(p, n, pos);
+    if (r.r == 0xFFFD && r.width == 1) {
+      o += "\\x";
+      o.push_back(hex[p[pos] >> 4]);
+      o.push_back(hex[p[pos] & 15]);
+      pos += 1;
+      continue;
+    }
+    uint32_t c = uint32_t(r.r);
+    if (c == '"' || c == '\\') {
+      o.push_back('\\');
+      o.push_back(char(c));
+    } else if (GoIsPrint(c)) {
+      o.append(s, size_t(pos), size_t(r.width));
+    } else {
+      switch (c) {
+        case 7: o += "\\a"; break;
+        case 8: o += "\\b"; break;
+        case 12: o += "\\f"; break;
+        case 10: o += "\\n"; break;
+        case 13: o += "\\r"; break;
+        case 9: o += "\\t"; break;
+        case 11: o += "\\v"; break;
+        default:
+          if (c < 0x20 || c == 0x7F) {
+            o += "\\x";
+            o.push_back(hex[c >> 4]);
+            o.push_back(hex[c & 15]);
+          } else if (c < 0x10000) {
+            o += "\\u";
+            for (int k = 12; k >= 0; k -= 4) o.push_back(hex[(c >> k) & 15]);
+          } else {
+            o += "\\U";
+            for (int k = 28; k >= 0; k -= 4) o.push_back(hex[(c >> k) & 15]);
+          }
+      }
+    }
+    pos += r.width;
+  }
+  o.push_back('"');
+  return o;
+}
+
 static void AppendUtf8(std::string* out, uint32_t r) {
   if (r < 0x80) {
     out->push_back(char(r));

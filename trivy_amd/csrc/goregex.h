@@ -102,5 +102,8 @@ uint32_t SimpleFold(uint32_t r);
 uint32_t GoToLower(uint32_t r);
 // bytes.ToLower over a whole buffer (Go semantics, invalid byte -> EF BF BD).
 std::string GoBytesToLower(const uint8_t* s, size_t n);
+// unicode.IsPrint and strconv.Quote (fmt %q), scanner.go:442.
+bool GoIsPrint(uint32_t r);
+std::string GoQuote(const std::string& s);
 
 }  // namespace tsg

@@ -1,0 +1,565 @@
+// Rule compiler (see rules.h).  Superset arguments are in DESIGN.md §2-3.
+#include "rules.h"
+
+#include <algorithm>
+#include <array>
+#include <bitset>
+#include <deque>
+#include <map>
+#include <set>
+
+namespace tsg {
+
+namespace {
+constexpr int64_t kInf = int64_t(1) << 40;
+
+bool IsFoldOnlyRune(uint32_t r) { return r == 0x212A || r == 0x17F || r == 0x130; }
+
+int Utf8Len(uint32_t r) { return r < 0x80 ? 1 : r < 0x800 ? 2 : r < 0x10000 ? 3 : 4; }
+
+bool ClassHas(const RuneRanges& rr, uint32_t c) {
+  for (auto& p : rr)
+    if (c >= p.first && c <= p.second) return true;
+  return false;
+}
+
+// Byte-length range of one rune matched by the class, over the runes that can
+// appear in a non-special file (U+212A/U+017F/U+0130 only occur in files the
+// GPU routes to full-scan mode).
+void ClassBytes(const RuneRanges& rr, int64_t* mn, int64_t* mx) {
+  int lo = 5, hi = 0;
+  bool any = false;
+  for (auto& p : rr) {
+    uint32_t a = p.first, b = p.second;
+    // split across utf8 length boundaries
+    const uint32_t bounds[4][2] = {{0, 0x7F}, {0x80, 0x7FF}, {0x800, 0xFFFF}, {0x10000, 0x10FFFF}};
+    for (int k = 0; k < 4; k++) {
+      uint32_t x = std::max(a, bounds[k][0]), y = std::min(b, bounds[k][1]);
+      if (x > y) continue;
+      // skip the fold-only runes if they are the only members in this part
+      bool only_special = true;
+      for (uint32_t c = x; c <= y && only_special; c++) {
+        if (!IsFoldOnlyRune(c)) only_special = false;
+        if (c - x > 4) only_special = false;
+      }
+      if (only_special) continue;
+      any = true;
+      lo = std::min(lo, k + 1);
+      hi = std::max(hi, k + 1);
+    }
+  }
+  if (ClassHas(rr, 0xFFFD)) { lo = 1; hi = std::max(hi, 1); any = true; }
+  if (!any) { lo = 1; hi = 1; }
+  *mn = lo;
+  *mx = hi;
+}
+
+// A class that is one ASCII character, possibly case-folded (incl. its
+// U+212A/U+017F orbit members).  Returns the lowercased char or -1.
+int LitChar(const Node& n) {
+  if (n.op != NodeOp::Class) return -1;
+  std::vector<uint32_t> asc, uni;
+  uint64_t total = 0;
+  for (auto& p : n.ranges) {
+    total += uint64_t(p.second - p.first) + 1;
+    if (total > 4) return -1;
+    for (uint32_t c = p.first; c <= p.second; c++) (c < 0x80 ? asc : uni).push_back(c);
+  }
+  if (asc.empty() || asc.size() > 2) return -1;
+  uint32_t c = asc[0];
+  if (asc.size() == 2) {
+    uint32_t a = asc[0], b = asc[1];
+    if (!(a >= 'A' && a <= 'Z' && b == a + 32)) return -1;
+    c = b;
+  }
+  uint32_t lc = (c >= 'A' && c <= 'Z') ? c + 32 : c;
+  for (uint32_t u : uni) {
+    if (!((u == 0x212A && lc == 'k') || (u == 0x17F && lc == 's'))) return -1;
+  }
+  return int(lc);
+}
+
+struct Analyzer {
+  const std::vector<Node>& nodes;
+  std::map<int, std::pair<int64_t, int64_t>> memo;
+
+  explicit Analyzer(const std::vector<Node>& n) : nodes(n) {}
+
+  std::pair<int64_t, int64_t> Bytes(int i) {
+    auto it = memo.find(i);
+    if (it != memo.end()) return it->second;
+    const Node& n = nodes[i];
+    std::pair<int64_t, int64_t> r{0, 0};
+    switch (n.op) {
+      case NodeOp::Empty:
+      case NodeOp::NoMatch:
+      case NodeOp::Assert: break;
+      case NodeOp::Class: ClassBytes(n.ranges, &r.first, &r.second); break;
+      case NodeOp::Cat:
+        for (int s : n.subs) {
+          auto b = Bytes(s);
+          r.first += b.first;
+          r.second = (r.second >= kInf || b.second >= kInf) ? kInf : r.second + b.second;
+        }
+        break;
+      case NodeOp::Alt: {
+        r.first = kInf;
+        for (int s : n.subs) {
+          auto b = Bytes(s);
+          r.first = std::min(r.first, b.first);
+          r.second = std::max(r.second, b.second);
+        }
+        break;
+      }
+      case NodeOp::Capture: r = Bytes(n.subs[0]); break;
+      case NodeOp::Repeat: {
+        auto b = Bytes(n.subs[0]);
+        r.first = b.first * n.min;
+        if (n.max < 0 || b.second >= kInf) r.second = b.second == 0 ? 0 : kInf;
+        else r.second = b.second * n.max;
+        if (r.second > kInf) r.second = kInf;
+        break;
+      }
+    }
+    memo[i] = r;
+    return r;
+  }
+
+  void Flatten(int i, std::vector<int>* out) {
+    const Node& n = nodes[i];
+    if (n.op == NodeOp::Cat) {
+      for (int s : n.subs) Flatten(s, out);
+    } else if (n.op == NodeOp::Capture) {
+      Flatten(n.subs[0], out);
+    } else if (n.op == NodeOp::Empty || n.op == NodeOp::Assert) {
+      // zero-width: contributes no bytes, literal runs continue across it
+    } else {
+      out->push_back(i);
+    }
+  }
+
+  // Leading literal run of a node's flattened sequence ("" if none).
+  std::string LeadLiteral(int i) {
+    std::vector<int> items;
+    Flatten(i, &items);
+    std::string s;
+    for (int it : items) {
+      int c = LitChar(nodes[it]);
+      if (c < 0) break;
+      s.push_back(char(c));
+    }
+    return s;
+  }
+};
+
+struct Cand {
+  std::vector<std::string> lits;
+  int64_t olo, ohi;
+  size_t minlen() const {
+    size_t m = SIZE_MAX;
+    for (auto& l : lits) m = std::min(m, l.size());
+    return m;
+  }
+};
+
+bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
+  Analyzer an(re.nodes());
+  std::vector<int> items;
+  an.Flatten(re.root(), &items);
+  std::vector<Cand> cands;
+  int64_t olo = 0, ohi = 0;
+  for (size_t k = 0; k < items.size();) {
+    const Node& n = re.nodes()[items[k]];
+    int c = LitChar(n);
+    if (c >= 0) {
+      std::string s;
+      size_t j = k;
+      while (j < items.size()) {
+        int cj = LitChar(re.nodes()[items[j]]);
+        if (cj < 0) break;
+        s.push_back(char(cj));
+        j++;
+      }
+      if (ohi < kInf || !need_offset) cands.push_back({{s}, olo, ohi});
+      olo += int64_t(s.size());
+      if (ohi < kInf) ohi += int64_t(s.size());
+      k = j;
+      continue;
+    }
+    int alt = -1;
+    if (n.op == NodeOp::Alt) alt = items[k];
+    if (n.op == NodeOp::Repeat && n.min >= 1) {
+      int sub = n.subs[0];
+      while (re.nodes()[sub].op == NodeOp::Capture) sub = re.nodes()[sub].subs[0];
+      if (re.nodes()[sub].op == NodeOp::Alt) alt = sub;
+      else {
+        std::string s = an.LeadLiteral(sub);
+        if (!s.empty() && (ohi < kInf || !need_offset)) cands.push_back({{s}, olo, ohi});
+      }
+    }
+    if (alt >= 0 && (ohi < kInf || !need_offset)) {
+      Cand cd{{}, olo, ohi};
+      bool ok = true;
+      for (int b : re.nodes()[alt].subs) {
+        std::string s = an.LeadLiteral(b);
+        if (s.empty()) { ok = false; break; }
+        cd.lits.push_back(s);
+      }
+      if (ok) cands.push_back(cd);
+    }
+    auto b = an.Bytes(items[k]);
+    olo += b.first;
+    ohi = (ohi >= kInf || b.second >= kInf) ? kInf : ohi + b.second;
+    k++;
+  }
+  bool have = false;
+  for (auto& cd : cands) {
+    std::sort(cd.lits.begin(), cd.lits.end());
+    cd.lits.erase(std::unique(cd.lits.begin(), cd.lits.end()), cd.lits.end());
+    if (!have || cd.minlen() > best->minlen() ||
+        (cd.minlen() == best->minlen() && cd.lits.size() < best->lits.size())) {
+      *best = cd;
+      have = true;
+    }
+  }
+  return have && best->minlen() >= 2;
+}
+
+// ---------------------------------------------------------------------------
+// relaxed class-sequence NFA
+// ---------------------------------------------------------------------------
+using Reach = std::bitset<256>;
+
+Reach ByteReach(const RuneRanges& rr) {
+  Reach r;
+  for (uint32_t b = 0; b < 0x80; b++)
+    if (ClassHas(rr, b)) r.set(b);
+  bool fffd = ClassHas(rr, 0xFFFD);
+  auto any_in = [&](uint32_t lo, uint32_t hi) {
+    for (auto& p : rr)
+      if (p.first <= hi && p.second >= lo) return true;
+    return false;
+  };
+  for (uint32_t b = 0x80; b < 0x100; b++) {
+    bool on = fffd;  // invalid byte -> U+FFFD
+    if (b >= 0xC2 && b <= 0xDF) on = on || any_in((b & 0x1F) << 6, ((b & 0x1F) << 6) | 0x3F);
+    else if (b >= 0xE0 && b <= 0xEF) on = on || any_in((b & 0x0F) << 12, ((b & 0x0F) << 12) | 0xFFF);
+    else if (b >= 0xF0 && b <= 0xF4) on = on || any_in((b & 0x07) << 18, ((b & 0x07) << 18) | 0x3FFFF);
+    if (on) r.set(b);
+  }
+  return r;
+}
+
+struct Elem {
+  Reach reach;
+  int64_t min, max;  // max < 0: unbounded
+};
+
+int64_t SeqMin(const std::vector<Elem>& s) {
+  int64_t m = 0;
+  for (auto& e : s) m += e.min;
+  return m;
+}
+int64_t SeqMax(const std::vector<Elem>& s) {
+  int64_t m = 0;
+  for (auto& e : s) {
+    if (e.max < 0) return -1;
+    m += e.max;
+  }
+  return m;
+}
+Reach SeqUnion(const std::vector<Elem>& s) {
+  Reach r;
+  for (auto& e : s) r |= e.reach;
+  return r;
+}
+
+std::vector<Elem> Relax(const std::vector<Node>& nodes, int i) {
+  const Node& n = nodes[i];
+  switch (n.op) {
+    case NodeOp::Empty:
+    case NodeOp::NoMatch:
+    case NodeOp::Assert: return {};
+    case NodeOp::Class: return {{ByteReach(n.ranges), 1, 1}};
+    case NodeOp::Capture: return Relax(nodes, n.subs[0]);
+    case NodeOp::Cat: {
+      std::vector<Elem> out;
+      for (int s : n.subs) {
+        auto r = Relax(nodes, s);
+        out.insert(out.end(), r.begin(), r.end());
+      }
+      return out;
+    }
+    case NodeOp::Alt: {
+      std::vector<std::vector<Elem>> br;
+      for (int s : n.subs) br.push_back(Relax(nodes, s));
+      bool columns = true;
+      for (auto& b : br) {
+        if (b.size() != br[0].size()) columns = false;
+        for (auto& e : b)
+          if (e.min != 1 || e.max != 1) columns = false;
+      }
+      if (columns && !br[0].empty()) {
+        std::vector<Elem> out = br[0];
+        for (size_t k = 1; k < br.size(); k++)
+          for (size_t j = 0; j < out.size(); j++) out[j].reach |= br[k][j].reach;
+        return out;
+      }
+      Elem e{Reach(), kInf, 0};
+      for (auto& b : br) {
+        e.reach |= SeqUnion(b);
+        e.min = std::min(e.min, SeqMin(b));
+        int64_t mx = SeqMax(b);
+        if (mx < 0 || e.max < 0) e.max = -1;
+        else e.max = std::max(e.max, mx);
+      }
+      if (e.max == 0) return {};
+      return {e};
+    }
+    case NodeOp::Repeat: {
+      auto s = Relax(nodes, n.subs[0]);
+      if (s.empty()) return {};
+      if (s.size() == 1) {
+        Elem e = s[0];
+        e.min = e.min * n.min;
+        e.max = (n.max < 0 || e.max < 0) ? -1 : e.max * n.max;
+        if (e.max == 0) return {};
+        return {e};
+      }
+      if (n.max == 0) return {};
+      std::vector<Elem> out;
+      if (n.min >= 1) out = s;
+      Elem rest{SeqUnion(s), SeqMin(s) * std::max(0, n.min - 1), -1};
+      int64_t smax = SeqMax(s);
+      if (n.max >= 0 && smax >= 0) rest.max = smax * (n.min >= 1 ? n.max - 1 : n.max);
+      if (n.min == 0) rest.min = 0;
+      if (rest.max != 0) out.push_back(rest);
+      return out;
+    }
+  }
+  return {};
+}
+
+int64_t Positions(const Elem& e) { return e.max >= 0 ? e.max : std::max<int64_t>(e.min, 1); }
+
+void BuildNfa(std::vector<Elem> seq, std::vector<uint64_t>* nfa, RuleGpu* rg) {
+  // fit into kMaxNfaWords * 64 positions by relaxing the largest elements
+  for (;;) {
+    int64_t tot = 0;
+    for (auto& e : seq) tot += Positions(e);
+    if (tot <= 64 * kMaxNfaWords) break;
+    size_t big = 0;
+    for (size_t k = 1; k < seq.size(); k++)
+      if (Positions(seq[k]) > Positions(seq[big])) big = k;
+    Elem& e = seq[big];
+    if (e.max >= 0 && e.max > e.min) e.max = -1;
+    else { e.min = e.min / 2; e.max = -1; }
+  }
+  int64_t P = 0;
+  for (auto& e : seq) P += Positions(e);
+  rg->nfa_off = uint32_t(nfa->size());
+  if (P == 0) {
+    rg->nfa_words = 0;
+    return;
+  }
+  int W = int((P + 63) / 64);
+  rg->nfa_words = uint8_t(W);
+  std::vector<uint64_t> O(W, 0), L(W, 0), F(W, 0), B(256 * W, 0);
+  auto setb = [&](std::vector<uint64_t>& v, int64_t p) { v[p >> 6] |= uint64_t(1) << (p & 63); };
+  int64_t p = 0;
+  std::vector<bool> opt(P, false);
+  for (auto& e : seq) {
+    int64_t np = Positions(e);
+    for (int64_t j = 0; j < np; j++, p++) {
+      for (int b = 0; b < 256; b++)
+        if (e.reach.test(b)) B[size_t(b) * W + (p >> 6)] |= uint64_t(1) << (p & 63);
+      if (e.max >= 0) {
+        if (j >= e.min) { setb(O, p); opt[p] = true; }
+      } else {
+        if (j == np - 1) setb(L, p);
+        if (e.min == 0) { setb(O, p); opt[p] = true; }
+      }
+    }
+  }
+  setb(F, P - 1);
+  for (int64_t q = P - 1; q >= 1 && opt[q]; q--) setb(F, q - 1);
+  nfa->insert(nfa->end(), O.begin(), O.end());
+  nfa->insert(nfa->end(), L.begin(), L.end());
+  nfa->insert(nfa->end(), F.begin(), F.end());
+  nfa->insert(nfa->end(), B.begin(), B.end());
+}
+
+std::string AsciiLower(const std::string& s) {
+  std::string o = s;
+  for (auto& c : o)
+    if (c >= 'A' && c <= 'Z') c = char(c + 32);
+  return o;
+}
+
+bool IsAscii(const std::string& s) {
+  for (unsigned char c : s)
+    if (c >= 0x80) return false;
+  return true;
+}
+
+bool BuildAc(const std::vector<std::pair<std::string, uint32_t>>& pats, CompiledRules* out, std::string* err) {
+  // classes
+  int cls_of[256];
+  for (int b = 0; b < 256; b++) cls_of[b] = 0;
+  int nc = 1;
+  std::set<unsigned char> used;
+  for (auto& p : pats)
+    for (unsigned char c : p.first) used.insert(c);
+  for (unsigned char c : used) cls_of[c] = nc++;
+  for (int b = 'A'; b <= 'Z'; b++) cls_of[b] = cls_of[b + 32];
+  for (int b = 0; b < 256; b++) out->cmap[b] = uint8_t(cls_of[b]);
+  out->cmap[0xC4] = kClsFoldI;
+  out->cmap[0xE2] = kClsFoldK;
+  out->cmap[0xC5] = kClsFoldS;
+  if (nc >= 0xFD) {
+    *err = "too many distinct keyword/anchor characters";
+    return false;
+  }
+  // trie
+  std::vector<std::vector<int>> go;
+  std::vector<std::vector<uint32_t>> outs;
+  go.push_back(std::vector<int>(nc, -1));
+  outs.push_back({});
+  uint32_t maxlen = 0;
+  for (auto& p : pats) {
+    int s = 0;
+    for (unsigned char c : p.first) {
+      int k = cls_of[c];
+      if (go[s][k] < 0) {
+        go[s][k] = int(go.size());
+        go.push_back(std::vector<int>(nc, -1));
+        outs.push_back({});
+      }
+      s = go[s][k];
+    }
+    outs[s].push_back(p.second);
+    maxlen = std::max<uint32_t>(maxlen, uint32_t(p.first.size()));
+  }
+  size_t ns = go.size();
+  if (ns >= 0x8000) {
+    *err = "keyword automaton too large (" + std::to_string(ns) + " states)";
+    return false;
+  }
+  std::vector<int> fail(ns, 0);
+  std::deque<int> q;
+  for (int k = 0; k < nc; k++) {
+    if (go[0][k] < 0) go[0][k] = 0;
+    else {
+      fail[go[0][k]] = 0;
+      q.push_back(go[0][k]);
+    }
+  }
+  while (!q.empty()) {
+    int u = q.front();
+    q.pop_front();
+    for (int k = 0; k < nc; k++) {
+      int v = go[u][k];
+      if (v >= 0) {
+        fail[v] = go[fail[u]][k];
+        for (uint32_t o : outs[fail[v]]) outs[v].push_back(o);
+        q.push_back(v);
+      } else {
+        go[u][k] = go[fail[u]][k];
+      }
+    }
+  }
+  out->n_states = uint32_t(ns);
+  out->n_classes = uint32_t(nc);
+  out->max_pat_len = maxlen;
+  out->trans.assign(ns * nc, 0);
+  for (size_t s = 0; s < ns; s++)
+    for (int k = 0; k < nc; k++) {
+      int v = go[s][k];
+      out->trans[s * nc + k] = uint16_t(v | (outs[v].empty() ? 0 : kAcOutFlag));
+    }
+  out->out_off.assign(ns + 1, 0);
+  for (size_t s = 0; s < ns; s++) {
+    auto& o = outs[s];
+    std::sort(o.begin(), o.end());
+    o.erase(std::unique(o.begin(), o.end()), o.end());
+    out->out_off[s + 1] = out->out_off[s] + uint32_t(o.size());
+    out->out_items.insert(out->out_items.end(), o.begin(), o.end());
+  }
+  return true;
+}
+}  // namespace
+
+std::vector<std::string> RequiredLiterals(const Regex& re) {
+  Cand best{{}, 0, 0};
+  if (!ExtractAnchor(re, &best, false)) return {};
+  return best.lits;
+}
+
+bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err) {
+  std::map<std::string, uint32_t> kw_ids;
+  std::vector<std::pair<std::string, uint32_t>> pats;
+  out->rules.clear();
+  out->regex.clear();
+  for (size_t ri = 0; ri < src.size(); ri++) {
+    const RuleSrc& r = src[ri];
+    RuleGpu rg{};
+    std::unique_ptr<Regex> re;
+    if (!r.regex.empty()) {
+      re = Regex::Compile(r.regex, err);
+      if (!re) return false;
+      rg.has_regex = 1;
+    }
+    // keyword gate (strings.ToLower of each keyword)
+    rg.kw_off = uint32_t(out->rule_kw.size());
+    bool host_gate = false;
+    for (auto& kw : r.keywords) {
+      if (!IsAscii(kw)) {
+        host_gate = true;
+        continue;
+      }
+      std::string l = AsciiLower(kw);
+      auto it = kw_ids.find(l);
+      uint32_t id;
+      if (it == kw_ids.end()) {
+        id = uint32_t(out->keywords.size());
+        kw_ids[l] = id;
+        out->keywords.push_back(l);
+        if (!l.empty()) pats.push_back({l, kOutKeyword | id});
+      } else {
+        id = it->second;
+      }
+      out->rule_kw.push_back(id);
+    }
+    rg.kw_cnt = uint32_t(out->rule_kw.size()) - rg.kw_off;
+    bool empty_kw = false;
+    for (auto& kw : r.keywords)
+      if (kw.empty()) empty_kw = true;
+    if (r.keywords.empty() || empty_kw) rg.gate = kGateAlways;  // "" is a substring of anything
+    else rg.gate = host_gate ? kGateHost : kGateKeywords;
+    // anchor + relaxed NFA
+    std::string desc = "-";
+    if (re) {
+      Cand best{{}, 0, 0};
+      if (ExtractAnchor(*re, &best)) {
+        rg.anchored = 1;
+        desc = "[" + std::to_string(best.olo) + "," + std::to_string(best.ohi) + "]";
+        for (auto& l : best.lits) {
+          uint32_t aid = uint32_t(out->anchors.size());
+          out->anchors.push_back({uint32_t(ri), uint32_t(l.size()), int32_t(best.olo), int32_t(best.ohi)});
+          pats.push_back({l, kOutAnchor | aid});
+          desc += " " + l;
+        }
+      } else {
+        rg.anchored = 0;
+        out->n_fullscan_rules++;
+      }
+      BuildNfa(Relax(re->nodes(), re->root()), &out->nfa, &rg);
+    }
+    out->rule_anchor_desc.push_back(desc);
+    out->rules.push_back(rg);
+    out->regex.push_back(std::move(re));
+  }
+  return BuildAc(pats, out, err);
+}
+
+}  // namespace tsg

@@ -1,0 +1,88 @@
+// Rule compiler: secret rules -> GPU tables.
+//
+// Hooks where the reference assembles its rule list (NewScanner,
+// pkg/fanal/secret/scanner.go:320-364).  For the ordered rule list it builds
+//   * the keyword gate: unique strings.ToLower(keyword)s (scanner.go:174-186)
+//     and, per rule, the keyword ids whose presence enables it;
+//   * one anchor per rule: a set of ASCII literals every match contains, at a
+//     bounded byte offset [off_lo, off_hi] from the match start;
+//   * one case-folded Aho-Corasick DFA over keywords ∪ anchor literals ∪ the
+//     three fold-special UTF-8 sequences (U+0130, U+212A, U+017F);
+//   * a relaxed, byte-level "extended shift-and" NFA per rule whose language is
+//     a superset of the rule regex (captures dropped, assertions -> ε,
+//     alternations -> column unions / class runs, large repeats -> unbounded).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "goregex.h"
+
+namespace tsg {
+
+constexpr uint32_t kAcOutFlag = 0x8000;  // transition entry: target state has outputs
+constexpr uint8_t kClsFoldI = 0xFD;     // byte 0xC4 (maybe U+0130 -> 'i')
+constexpr uint8_t kClsFoldK = 0xFE;     // byte 0xE2 (maybe U+212A -> 'k')
+constexpr uint8_t kClsFoldS = 0xFF;     // byte 0xC5 (maybe U+017F, barrier)
+constexpr uint32_t kOutKeyword = 0u << 28;
+constexpr uint32_t kOutAnchor = 1u << 28;
+constexpr uint32_t kOutSpecial = 2u << 28;
+constexpr int kMaxNfaWords = 4;
+
+enum GateMode : uint8_t {
+  kGateAlways = 0,    // no keywords: MatchKeywords is true
+  kGateKeywords = 1,  // ASCII keywords: GPU bitset is exact
+  kGateHost = 2,      // a non-ASCII keyword: GPU treats as open, host verifies
+};
+
+struct RuleSrc {
+  std::string id;
+  std::string regex;  // empty: rule has no regex (never matches)
+  std::vector<std::string> keywords;
+};
+
+struct AnchorInfo {
+  uint32_t rule;
+  uint32_t lit_len;
+  int32_t off_lo, off_hi;  // literal start - match start, in bytes
+};
+
+struct RuleGpu {  // mirrored on the device
+  uint32_t nfa_off;     // index into nfa words (u64)
+  uint8_t nfa_words;    // 0: relaxed NFA is empty -> every anchor hit is a candidate
+  uint8_t gate;         // GateMode
+  uint8_t anchored;     // 1: anchor-driven; 0: full-scan rule
+  uint8_t has_regex;
+  uint32_t kw_off, kw_cnt;  // into rule_kw
+};
+
+struct CompiledRules {
+  // Aho-Corasick
+  uint32_t n_states = 0, n_classes = 0, max_pat_len = 0;
+  uint8_t cmap[256];
+  std::vector<uint16_t> trans;     // n_states * n_classes
+  std::vector<uint32_t> out_off;   // n_states + 1
+  std::vector<uint32_t> out_items; // kOut* | id
+  // keywords / anchors
+  std::vector<std::string> keywords;  // unique lowercased ASCII keywords
+  std::vector<AnchorInfo> anchors;
+  // rules
+  std::vector<RuleGpu> rules;
+  std::vector<uint32_t> rule_kw;  // keyword ids
+  std::vector<uint64_t> nfa;      // per rule: O[W] L[W] F[W] B[256][W]
+  std::vector<std::string> rule_anchor_desc;  // debug text
+  std::vector<std::unique_ptr<Regex>> regex;  // exact engines (host pass)
+  uint32_t n_fullscan_rules = 0;
+
+  uint32_t kw_words() const { return (uint32_t(keywords.size()) + 31) / 32; }
+};
+
+// A set of lowercased ASCII literals (len >= 2) one of which every match of
+// `re` contains, or empty if none is known.  Used as a MatchString prefilter.
+std::vector<std::string> RequiredLiterals(const Regex& re);
+
+// Compile; returns false with *err on a regex/limits error.
+bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err);
+
+}  // namespace tsg

@@ -1,0 +1,664 @@
+// Exact host tail of the drop-in Scanner (see scanner.h for the line map).
+#include "scanner.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+namespace tsg {
+
+namespace {
+
+double NowMs() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <typename F>
+void ParallelFor(size_t n, int threads, F fn) {
+  if (n == 0) return;
+  if (threads <= 1 || n < 2) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      size_t i = next.fetch_add(1);
+      if (i >= n) break;
+      fn(i);
+    }
+  };
+  int t = int(std::min<size_t>(size_t(threads), n));
+  std::vector<std::thread> pool;
+  for (int k = 1; k < t; k++) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+}
+
+bool AsciiContainsLower(const uint8_t* s, size_t n, const std::string& lit) {
+  // case-insensitive (ASCII) substring test; lit is lowercase
+  size_t m = lit.size();
+  if (m == 0) return true;
+  if (m > n) return false;
+  const uint8_t c0 = uint8_t(lit[0]);
+  const uint8_t c0u = (c0 >= 'a' && c0 <= 'z') ? uint8_t(c0 - 32) : c0;
+  for (size_t i = 0; i + m <= n; i++) {
+    uint8_t c = s[i];
+    if (c != c0 && c != c0u) continue;
+    size_t k = 1;
+    for (; k < m; k++) {
+      uint8_t x = s[i + k];
+      if (x >= 'A' && x <= 'Z') x = uint8_t(x + 32);
+      if (x != uint8_t(lit[k])) break;
+    }
+    if (k == m) return true;
+  }
+  return false;
+}
+
+struct Loc {
+  int64_t s, e;
+};
+
+// ---------------------------------------------------------------------------
+// Go sort.Slice = pdqsort_func (sort/zsortfunc.go), restated.
+// ---------------------------------------------------------------------------
+struct SortData {
+  std::vector<FindingOut>* v;
+  const std::vector<RuleSpec>* rules;
+  bool Less(int i, int j) const {
+    const FindingOut& a = (*v)[i];
+    const FindingOut& b = (*v)[j];
+    const std::string& ra = (*rules)[a.rule].id;
+    const std::string& rb = (*rules)[b.rule].id;
+    if (ra != rb) return ra < rb;
+    return a.match < b.match;
+  }
+  void Swap(int i, int j) { std::swap((*v)[i], (*v)[j]); }
+};
+
+void InsertionSort(SortData& d, int a, int b) {
+  for (int i = a + 1; i < b; i++)
+    for (int j = i; j > a && d.Less(j, j - 1); j--) d.Swap(j, j - 1);
+}
+
+void SiftDown(SortData& d, int lo, int hi, int first) {
+  int root = lo;
+  for (;;) {
+    int child = 2 * root + 1;
+    if (child >= hi) return;
+    if (child + 1 < hi && d.Less(first + child, first + child + 1)) child++;
+    if (!d.Less(first + root, first + child)) return;
+    d.Swap(first + root, first + child);
+    root = child;
+  }
+}
+
+void HeapSort(SortData& d, int a, int b) {
+  int first = a, lo = 0, hi = b - a;
+  for (int i = (hi - 1) / 2; i >= 0; i--) SiftDown(d, i, hi, first);
+  for (int i = hi - 1; i >= 0; i--) {
+    d.Swap(first, first + i);
+    SiftDown(d, lo, i, first);
+  }
+}
+
+int BitsLen(unsigned x) {
+  int n = 0;
+  while (x) {
+    n++;
+    x >>= 1;
+  }
+  return n;
+}
+
+void BreakPatterns(SortData& d, int a, int b) {
+  int length = b - a;
+  if (length >= 8) {
+    uint64_t r = uint64_t(length);
+    unsigned modulus = 1u << BitsLen(unsigned(length));
+    int idx = a + (length / 4) * 2 - 1;
+    for (int i = 0; i < 3; i++) {
+      r ^= r << 13;
+      r ^= r >> 7;
+      r ^= r << 17;
+      int other = int(unsigned(r) & (modulus - 1));
+      if (other >= length) other -= length;
+      d.Swap(idx - 1 + i, a + other);
+    }
+  }
+}
+
+enum { kHintUnknown = 0, kHintIncreasing = 1, kHintDecreasing = 2 };
+
+void Order2(SortData& d, int& a, int& b, int* swaps) {
+  if (d.Less(b, a)) {
+    (*swaps)++;
+    std::swap(a, b);
+  }
+}
+
+int Median(SortData& d, int a, int b, int c, int* swaps) {
+  Order2(d, a, b, swaps);
+  Order2(d, b, c, swaps);
+  Order2(d, a, b, swaps);
+  return b;
+}
+
+int ChoosePivot(SortData& d, int a, int b, int* hint) {
+  int l = b - a, swaps = 0;
+  int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+  if (l >= 8) {
+    if (l >= 50) {
+      i = Median(d, i - 1, i, i + 1, &swaps);
+      j = Median(d, j - 1, j, j + 1, &swaps);
+      k = Median(d, k - 1, k, k + 1, &swaps);
+    }
+    j = Median(d, i, j, k, &swaps);
+  }
+  *hint = swaps == 0 ? kHintIncreasing : swaps == 12 ? kHintDecreasing : kHintUnknown;
+  return j;
+}
+
+void ReverseRange(SortData& d, int a, int b) {
+  for (int i = a, j = b - 1; i < j; i++, j--) d.Swap(i, j);
+}
+
+bool PartialInsertionSort(SortData& d, int a, int b) {
+  int i = a + 1;
+  for (int step = 0; step < 5; step++) {
+    while (i < b && !d.Less(i, i - 1)) i++;
+    if (i == b) return true;
+    if (b - a < 50) return false;
+    d.Swap(i, i - 1);
+    if (i - a >= 2)
+      for (int j = i - 1; j >= 1; j--) {
+        if (!d.Less(j, j - 1)) break;
+        d.Swap(j, j - 1);
+      }
+    if (b - i >= 2)
+      for (int j = i + 1; j < b; j++) {
+        if (!d.Less(j, j - 1)) break;
+        d.Swap(j, j - 1);
+      }
+  }
+  return false;
+}
+
+int PartitionEqual(SortData& d, int a, int b, int pivot) {
+  d.Swap(a, pivot);
+  int i = a + 1, j = b - 1;
+  for (;;) {
+    while (i <= j && !d.Less(a, i)) i++;
+    while (i <= j && d.Less(a, j)) j--;
+    if (i > j) break;
+    d.Swap(i, j);
+    i++;
+    j--;
+  }
+  return i;
+}
+
+int Partition(SortData& d, int a, int b, int pivot, bool* already) {
+  d.Swap(a, pivot);
+  int i = a + 1, j = b - 1;
+  while (i <= j && d.Less(i, a)) i++;
+  while (i <= j && !d.Less(j, a)) j--;
+  if (i > j) {
+    d.Swap(j, a);
+    *already = true;
+    return j;
+  }
+  d.Swap(i, j);
+  i++;
+  j--;
+  for (;;) {
+    while (i <= j && d.Less(i, a)) i++;
+    while (i <= j && !d.Less(j, a)) j--;
+    if (i > j) break;
+    d.Swap(i, j);
+    i++;
+    j--;
+  }
+  d.Swap(j, a);
+  *already = false;
+  return j;
+}
+
+void Pdqsort(SortData& d, int a, int b, int limit) {
+  bool was_balanced = true, was_partitioned = true;
+  for (;;) {
+    int length = b - a;
+    if (length <= 12) {
+      InsertionSort(d, a, b);
+      return;
+    }
+    if (limit == 0) {
+      HeapSort(d, a, b);
+      return;
+    }
+    if (!was_balanced) {
+      BreakPatterns(d, a, b);
+      limit--;
+    }
+    int hint;
+    int pivot = ChoosePivot(d, a, b, &hint);
+    if (hint == kHintDecreasing) {
+      ReverseRange(d, a, b);
+      pivot = (b - 1) - (pivot - a);
+      hint = kHintIncreasing;
+    }
+    if (was_balanced && was_partitioned && hint == kHintIncreasing) {
+      if (PartialInsertionSort(d, a, b)) return;
+    }
+    if (a > 0 && !d.Less(a - 1, pivot)) {
+      a = PartitionEqual(d, a, b, pivot);
+      continue;
+    }
+    bool already;
+    int mid = Partition(d, a, b, pivot, &already);
+    was_partitioned = already;
+    int left = mid - a, right = b - mid, thr = length / 8;
+    if (left < right) {
+      was_balanced = left >= thr;
+      Pdqsort(d, a, mid, limit);
+      a = mid + 1;
+    } else {
+      was_balanced = right >= thr;
+      Pdqsort(d, mid + 1, b, limit);
+      b = mid;
+    }
+  }
+}
+
+}  // namespace
+
+void SortFindings(std::vector<FindingOut>* f, const std::vector<RuleSpec>& rules) {
+  SortData d{f, &rules};
+  int n = int(f->size());
+  Pdqsort(d, 0, n, BitsLen(unsigned(n)));
+}
+
+bool Matcher::Match(const uint8_t* s, size_t n) const {
+  if (!re) return false;
+  if (!lits.empty()) {
+    bool ascii = true;
+    for (size_t i = 0; i < n; i++)
+      if (s[i] >= 0x80) {
+        ascii = false;
+        break;
+      }
+    if (ascii) {
+      bool any = false;
+      for (auto& l : lits)
+        if (AsciiContainsLower(s, n, l)) {
+          any = true;
+          break;
+        }
+      if (!any) return false;
+    }
+  }
+  return re->Match(s, int64_t(n));
+}
+
+SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleSpec> allow,
+                             std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err)
+    : rules_(std::move(rules)), allow_(std::move(allow)), exclude_(std::move(exclude)) {
+  std::vector<RuleSrc> src;
+  for (auto& r : rules_) src.push_back({r.id, r.regex_src, r.keywords});
+  if (!CompileRules(src, &cr_, &err_)) {
+    *err = err_;
+    return;
+  }
+  compiled_ok_ = true;
+  for (size_t i = 0; i < rules_.size(); i++) {
+    auto& r = rules_[i];
+    if (cr_.regex[i] && !r.secret_group_name.empty()) {
+      const auto& names = cr_.regex[i]->cap_names();
+      for (size_t k = 0; k < names.size(); k++)
+        if (names[k] == r.secret_group_name) r.group_idx.push_back(int(k));
+    }
+    for (auto& kw : r.keywords) r.kw_lower_host.push_back(GoBytesToLower((const uint8_t*)kw.data(), kw.size()));
+  }
+  const char* ht = std::getenv("TSG_HOST_THREADS");
+  host_threads_ = ht ? std::atoi(ht) : 16;
+  if (host_threads_ <= 0) host_threads_ = 1;
+  if (device < 0) {
+    no_engine_ = true;
+    return;
+  }
+  engine_.reset(new GpuEngine(cr_, device));
+  if (!engine_->ok()) {
+    err_ = engine_->error();
+    *err = err_;
+  }
+}
+
+bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
+  for (auto& a : allow_)
+    if (a.path && a.path->Match(p, n)) return true;
+  return false;
+}
+
+namespace {
+bool AllowRulesAllow(const std::vector<AllowRuleSpec>& rules, const uint8_t* s, size_t n) {
+  for (auto& a : rules)
+    if (a.regex && a.regex->Match(s, n)) return true;
+  return false;
+}
+bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t* s, size_t n) {
+  for (auto& a : rules)
+    if (a.path && a.path->Match(s, n)) return true;
+  return false;
+}
+}  // namespace
+
+void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
+                             const Candidate* c, size_t nc, FileResult* out) const {
+  const uint8_t* P = reinterpret_cast<const uint8_t*>(path.data());
+  std::vector<std::pair<uint32_t, Loc>> matched;
+  std::vector<Loc> censor;
+  bool gblocks_done = false;
+  std::vector<Loc> gblocks;
+  std::string lowered;
+  bool lowered_done = false;
+  // (wlo, nl_before) anchors for line numbers
+  std::vector<std::pair<int64_t, int64_t>> nla;
+  for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
+  std::sort(nla.begin(), nla.end());
+
+  auto blocks_match = [&](const std::vector<std::unique_ptr<Regex>>& rx, std::vector<Loc>* cache, bool* done,
+                          Loc loc) {
+    if (!*done) {
+      *done = true;
+      for (auto& r : rx) {
+        std::vector<int64_t> m;
+        r->FindAll(content, len, false, nullptr, &m);
+        for (size_t k = 0; k + 1 < m.size(); k += 2) cache->push_back({m[k], m[k + 1]});
+      }
+    }
+    for (auto& b : *cache)
+      if (b.s <= loc.s && loc.e <= b.e) return true;
+    return false;
+  };
+
+  size_t i = 0;
+  while (i < nc) {
+    uint32_t r = c[i].rule;
+    size_t j = i;
+    std::vector<Window> wins;
+    while (j < nc && c[j].rule == r) {
+      Window w{c[j].wlo, c[j].whi};
+      if (!wins.empty() && w.lo <= wins.back().hi + 1) wins.back().hi = std::max(wins.back().hi, w.hi);
+      else wins.push_back(w);
+      j++;
+    }
+    i = j;
+    const RuleSpec& R = rules_[r];
+    const Regex* re = cr_.regex[r].get();
+    if (!re) continue;
+    if (R.path && !R.path->Match(P, path.size())) continue;                      // MatchPath :397
+    if (AllowRulesAllowPath(R.allow_rules, P, path.size())) continue;            // AllowPath :403
+    if (cr_.rules[r].gate == kGateHost) {                                       // MatchKeywords :409
+      if (!lowered_done) {
+        lowered = GoBytesToLower(content, size_t(len));
+        lowered_done = true;
+      }
+      bool hit = false;
+      for (auto& kw : R.kw_lower_host)
+        if (lowered.find(kw) != std::string::npos) {
+          hit = true;
+          break;
+        }
+      if (!hit) continue;
+    }
+    bool sub = !R.secret_group_name.empty();
+    std::vector<int64_t> m;
+    re->FindAll(content, len, sub, &wins, &m);
+    size_t stride = sub ? size_t(2 * (re->num_cap() + 1)) : 2;
+    std::vector<Loc> locs;
+    for (size_t k = 0; k + stride <= m.size(); k += stride) {
+      int64_t s = m[k], e = m[k + 1];
+      if (AllowRulesAllow(allow_, content + s, size_t(e - s)) ||
+          AllowRulesAllow(R.allow_rules, content + s, size_t(e - s)))  // AllowLocation :150-153
+        continue;
+      if (sub) {
+        for (int g : R.group_idx) locs.push_back({m[k + 2 * g], m[k + 2 * g + 1]});
+      } else {
+        locs.push_back({s, e});
+      }
+    }
+    if (locs.empty()) continue;
+    bool lblocks_done = false;
+    std::vector<Loc> lblocks;
+    for (auto& loc : locs) {
+      if (blocks_match(exclude_, &gblocks, &gblocks_done, loc) ||
+          blocks_match(R.exclude, &lblocks, &lblocks_done, loc))
+        continue;
+      if (loc.s < 0) continue;  // non-participating group: the reference would panic here
+      matched.push_back({r, loc});
+      censor.push_back(loc);
+    }
+  }
+  if (matched.empty()) {
+    out->kind = kNoFindings;
+    return;
+  }
+
+  // findLocation runs on the censored buffer (scanner.go:438-439): newlines
+  // inside a censored span are '*' there.  Spans merged and sorted:
+  std::vector<Loc> spans = censor;
+  std::sort(spans.begin(), spans.end(), [](const Loc& a, const Loc& b) { return a.s < b.s; });
+  {
+    std::vector<Loc> m;
+    for (auto& z : spans) {
+      if (z.e <= z.s) continue;
+      if (!m.empty() && z.s <= m.back().e) m.back().e = std::max(m.back().e, z.e);
+      else m.push_back(z);
+    }
+    spans.swap(m);
+  }
+  auto censored = [&](int64_t a, int64_t b) {
+    std::string s(reinterpret_cast<const char*>(content + a), size_t(b - a));
+    for (auto& cz : spans) {
+      int64_t x = std::max(a, cz.s), y = std::min(b, cz.e);
+      for (int64_t p = x; p < y; p++) s[size_t(p - a)] = '*';
+    }
+    return s;
+  };
+  auto count_nl_raw = [&](int64_t a, int64_t b) {
+    int64_t n = 0;
+    const uint8_t* p = content + a;
+    const uint8_t* e = content + b;
+    while (p < e) {
+      const void* q = std::memchr(p, '\n', size_t(e - p));
+      if (!q) break;
+      n++;
+      p = static_cast<const uint8_t*>(q) + 1;
+    }
+    return n;
+  };
+  auto censored_nl = [&](int64_t a, int64_t b) {  // '\n' bytes hidden by censoring in [a, b)
+    int64_t n = 0;
+    for (auto& z : spans) {
+      int64_t x = std::max(a, z.s), y = std::min(b, z.e);
+      if (x < y) n += count_nl_raw(x, y);
+    }
+    return n;
+  };
+  auto count_nl = [&](int64_t a, int64_t b) { return count_nl_raw(a, b) - censored_nl(a, b); };
+  auto nl_before = [&](int64_t pos) {
+    int64_t raw;
+    auto it = std::upper_bound(nla.begin(), nla.end(), std::make_pair(pos, INT64_MAX));
+    if (it == nla.begin()) {
+      raw = count_nl_raw(0, pos);
+    } else {
+      --it;
+      raw = it->second + count_nl_raw(it->first, pos);
+    }
+    return raw - censored_nl(0, pos);
+  };
+  auto in_span = [&](int64_t p) -> const Loc* {
+    auto it = std::upper_bound(spans.begin(), spans.end(), p, [](int64_t v, const Loc& z) { return v < z.s; });
+    if (it == spans.begin()) return nullptr;
+    --it;
+    return p < it->e ? &*it : nullptr;
+  };
+  auto line_start_of = [&](int64_t pos) {  // after the last visible '\n' before pos
+    int64_t p = pos - 1;
+    while (p >= 0) {
+      if (content[p] == '\n') {
+        const Loc* z = in_span(p);
+        if (!z) return p + 1;
+        p = z->s - 1;
+        continue;
+      }
+      p--;
+    }
+    return int64_t(0);
+  };
+  auto line_end_of = [&](int64_t pos) {  // first visible '\n' at or after pos, or len
+    int64_t p = pos;
+    while (p < len) {
+      const void* q = std::memchr(content + p, '\n', size_t(len - p));
+      if (!q) return len;
+      int64_t at = int64_t(static_cast<const uint8_t*>(q) - content);
+      const Loc* z = in_span(at);
+      if (!z) return at;
+      p = z->e;
+    }
+    return len;
+  };
+
+  out->kind = kHasFindings;
+  for (auto& mt : matched) {  // toFinding / findLocation :475-558
+    int64_t start = mt.second.s, end = mt.second.e;
+    FindingOut f;
+    f.rule = mt.first;
+    int64_t start_line_num = nl_before(start);
+    int64_t ls = line_start_of(start);
+    int64_t le = line_end_of(start);
+    int64_t mls = ls, mle = le;
+    if (le - ls > 100) {
+      mls = (start - ls - 30 < 0) ? ls : start - 30;
+      mle = (end + 20 > le) ? le : end + 20;
+    }
+    std::string match_line = censored(mls, mle);
+    int64_t end_line_num = start_line_num + count_nl(start, end);
+    int64_t code_start = std::max<int64_t>(start_line_num - 2, 0);
+    int64_t p = ls;
+    for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
+    bool found_first = false;
+    for (int64_t k = code_start; k < end_line_num + 2; k++) {
+      int64_t e = line_end_of(p);
+      bool in_cause = k >= start_line_num && k <= end_line_num;
+      std::string s;
+      if (e - p > 100) s = in_cause ? match_line : censored(p, p + 100);
+      else s = censored(p, e);
+      f.lines.push_back({k + 1, std::move(s), in_cause, !found_first && in_cause, false});
+      found_first = found_first || in_cause;
+      if (e >= len) break;  // last line of bytes.Split
+      p = e + 1;
+    }
+    for (auto it = f.lines.rbegin(); it != f.lines.rend(); ++it)
+      if (it->is_cause) {
+        it->last_cause = true;
+        break;
+      }
+    f.start_line = start_line_num + 1;
+    f.end_line = end_line_num + 1;
+    f.match = std::move(match_line);
+    if (binary) {
+      f.match = "Binary file " + GoQuote(path) + " matches a rule " + GoQuote(rules_[f.rule].title);
+      f.lines.clear();
+    }
+    out->findings.push_back(std::move(f));
+  }
+  SortFindings(&out->findings, rules_);
+}
+
+bool SecretScanner::Scan(const BatchInput& in, std::vector<FileResult>* out, BatchStats* gst, HostStats* hst) {
+  double t0 = NowMs();
+  HostStats hs;
+  std::vector<Candidate> cands;
+  uint64_t n_bytes = in.n_files ? in.host_offsets[in.n_files] : 0;
+  if (!engine_) {
+    err_ = "no GPU engine bound to this scanner";
+    return false;
+  }
+  bool ok;
+  if (in.dev_arena)
+    ok = engine_->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
+  else
+    ok = engine_->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
+  if (!ok) {
+    err_ = engine_->error();
+    return false;
+  }
+  double t1 = NowMs();
+  HostTail(in, &cands, out, &hs);
+  hs.ms_gpu = t1 - t0;
+  hs.ms_total = NowMs() - t0;
+  if (hst) *hst = hs;
+  return true;
+}
+
+void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, std::vector<FileResult>* out,
+                             HostStats* hs) const {
+  std::vector<Candidate>& cands = *cands_p;
+  out->assign(in.n_files, FileResult());
+  double t1 = NowMs();
+  // Global allow path (scanner.go:381-386) for every file
+  std::vector<uint8_t> allowed(in.n_files, 0);
+  {
+    bool any_path_rule = false;
+    for (auto& a : allow_)
+      if (a.path) any_path_rule = true;
+    if (any_path_rule) {
+      size_t blocks = (in.n_files + 4095) / 4096;
+      ParallelFor(blocks, host_threads_, [&](size_t b) {
+        size_t lo = b * 4096, hi = std::min<size_t>(lo + 4096, in.n_files);
+        for (size_t f = lo; f < hi; f++) {
+          const char* p = in.paths[f];
+          size_t n = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
+          allowed[f] = AllowPath(reinterpret_cast<const uint8_t*>(p), n) ? 1 : 0;
+        }
+      });
+    }
+  }
+  for (uint32_t f = 0; f < in.n_files; f++)
+    if (allowed[f]) (*out)[f].kind = kAllowedPath;
+  double t2 = NowMs();
+  std::sort(cands.begin(), cands.end(), [](const Candidate& a, const Candidate& b) {
+    if (a.file != b.file) return a.file < b.file;
+    if (a.rule != b.rule) return a.rule < b.rule;
+    return a.wlo < b.wlo;
+  });
+  std::vector<size_t> starts;
+  for (size_t i = 0; i < cands.size(); i++)
+    if (i == 0 || cands[i].file != cands[i - 1].file) starts.push_back(i);
+  starts.push_back(cands.size());
+  size_t nf = starts.size() - 1;
+  ParallelFor(nf, host_threads_, [&](size_t k) {
+    size_t a = starts[k], b = starts[k + 1];
+    uint32_t f = cands[a].file;
+    if (allowed[f]) return;
+    const char* p = in.paths[f];
+    size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
+    uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
+    ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string(p, pn), in.binary && in.binary[f], &cands[a],
+             b - a, &(*out)[f]);
+  });
+  double t3 = NowMs();
+  hs->ms_allow = t2 - t1;
+  hs->ms_exact = t3 - t2;
+  hs->candidates = cands.size();
+  hs->files_with_candidates = nf;
+  hs->findings = 0;
+  for (auto& r : *out) hs->findings += r.findings.size();
+}
+
+}  // namespace tsg

@@ -1,0 +1,118 @@
+// Host side of the drop-in Scanner (pkg/fanal/secret/scanner.go:377-558).
+//
+// The GPU engine returns candidate (file, rule, start-window) records; this
+// module runs the exact tail that the reference runs per rule per file:
+// path gates (:381, :397, :403), the exact keyword gate where the GPU bitset
+// is not exact (:409), leftmost-first FindAll[Submatch]Index restricted to
+// the candidate windows (:102-148), allow rules (:150-153, :214-221), exclude
+// blocks (:237-275, :419-425), censoring (:431-436, :465-473), findings
+// (:438-446, :475-558) and the final sort (:452-457).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "goregex.h"
+#include "rules.h"
+
+namespace tsg {
+
+// Regexp used as MatchString, with a required-literal prefilter.
+struct Matcher {
+  std::unique_ptr<Regex> re;
+  std::vector<std::string> lits;  // lowercased; empty = no prefilter
+  bool Match(const uint8_t* s, size_t n) const;
+};
+
+struct AllowRuleSpec {
+  std::string id;
+  std::unique_ptr<Matcher> regex, path;
+};
+
+struct RuleSpec {
+  std::string id, category, title, severity, secret_group_name;
+  std::string regex_src;
+  std::vector<std::string> keywords;
+  std::unique_ptr<Matcher> path;
+  std::vector<AllowRuleSpec> allow_rules;
+  std::vector<std::unique_ptr<Regex>> exclude;
+  std::vector<int> group_idx;  // capture indices named secret_group_name
+  std::vector<std::string> kw_lower_host;  // for host-verified gates
+};
+
+struct LineOut {
+  int64_t number;
+  std::string content;
+  bool is_cause, first_cause, last_cause;
+};
+
+struct FindingOut {
+  uint32_t rule;
+  int64_t start_line, end_line;
+  std::string match;
+  std::vector<LineOut> lines;
+};
+
+enum FileKind : uint32_t { kNoFindings = 0, kAllowedPath = 1, kHasFindings = 2 };
+
+struct FileResult {
+  FileKind kind = kNoFindings;
+  std::vector<FindingOut> findings;
+};
+
+struct BatchInput {
+  uint32_t n_files = 0;
+  const uint8_t* host_arena = nullptr;  // required: the exact pass reads it
+  const uint64_t* host_offsets = nullptr;
+  const uint8_t* dev_arena = nullptr;   // optional: resident in HBM already
+  const uint64_t* dev_offsets = nullptr;
+  const char* const* paths = nullptr;
+  const uint64_t* path_lens = nullptr;  // optional (else strlen)
+  const uint8_t* binary = nullptr;      // optional per-file Binary flag
+};
+
+struct HostStats {
+  double ms_gpu = 0, ms_allow = 0, ms_exact = 0, ms_total = 0;
+  uint64_t candidates = 0, files_with_candidates = 0, findings = 0;
+};
+
+class SecretScanner {
+ public:
+  // device < 0: no GPU engine (test hooks only: tsg_debug_host_tail)
+  SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleSpec> allow,
+                std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err);
+  bool ok() const { return compiled_ok_ && (no_engine_ || (engine_ && engine_->ok())); }
+  const std::string& error() const { return err_; }
+
+  bool Scan(const BatchInput& in, std::vector<FileResult>* out, BatchStats* gst, HostStats* hst);
+  // The exact host tail over a given candidate list (what Scan runs after the GPU).
+  void HostTail(const BatchInput& in, std::vector<Candidate>* cands, std::vector<FileResult>* out,
+                HostStats* hs) const;
+  // Global.AllowPath (scanner.go:57-59)
+  bool AllowPath(const uint8_t* p, size_t n) const;
+
+  const std::vector<RuleSpec>& rules() const { return rules_; }
+  const CompiledRules& compiled() const { return cr_; }
+  GpuEngine* engine() { return engine_.get(); }
+  void set_host_threads(int n) { host_threads_ = n; }
+
+ private:
+  void ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
+                const Candidate* c, size_t nc, FileResult* out) const;
+  std::vector<RuleSpec> rules_;
+  std::vector<AllowRuleSpec> allow_;
+  std::vector<std::unique_ptr<Regex>> exclude_;
+  CompiledRules cr_;
+  std::unique_ptr<GpuEngine> engine_;
+  std::string err_;
+  int host_threads_ = 0;
+  bool compiled_ok_ = false;
+  bool no_engine_ = false;
+};
+
+// Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.
+void SortFindings(std::vector<FindingOut>* f, const std::vector<RuleSpec>& rules);
+
+}  // namespace tsg

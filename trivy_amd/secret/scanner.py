@@ -1,0 +1,307 @@
+"""Scanner: pkg/fanal/secret/scanner.go:320-463 over the MI355X engine.
+
+``NewScanner`` assembles the rule set exactly as the reference does
+(scanner.go:320-364) and hands the resulting Global to ``tsg_scanner_new``;
+``Scan``/``ScanBatch`` submit contents through ``tsg_scan`` and decode the
+findings into ``types.Secret``-shaped objects (pkg/fanal/types/secret.go).
+"""
+import ctypes
+import json
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .. import _lib
+from .config import AllowRule, Config, Rule, builtin_allow_rules, builtin_rules
+
+c = ctypes
+
+
+class _CAllowRule(c.Structure):
+    _fields_ = [("id", c.c_char_p), ("regex", c.c_char_p), ("path", c.c_char_p)]
+
+
+class _CRule(c.Structure):
+    _fields_ = [("id", c.c_char_p), ("category", c.c_char_p), ("title", c.c_char_p),
+                ("severity", c.c_char_p), ("regex", c.c_char_p), ("path", c.c_char_p),
+                ("secret_group_name", c.c_char_p), ("keywords", c.POINTER(c.c_char_p)),
+                ("n_keywords", c.c_uint32), ("allow_rules", c.POINTER(_CAllowRule)),
+                ("n_allow_rules", c.c_uint32), ("exclude_regexes", c.POINTER(c.c_char_p)),
+                ("n_exclude_regexes", c.c_uint32)]
+
+
+class _CGlobal(c.Structure):
+    _fields_ = [("rules", c.POINTER(_CRule)), ("n_rules", c.c_uint32),
+                ("allow_rules", c.POINTER(_CAllowRule)), ("n_allow_rules", c.c_uint32),
+                ("exclude_regexes", c.POINTER(c.c_char_p)), ("n_exclude_regexes", c.c_uint32)]
+
+
+class _CBatch(c.Structure):
+    _fields_ = [("n_files", c.c_uint32), ("host_arena", c.c_void_p), ("host_offsets", c.c_void_p),
+                ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.POINTER(c.c_char_p)),
+                ("path_lens", c.c_void_p), ("binary", c.c_void_p)]
+
+
+class _CStats(c.Structure):
+    _fields_ = [(n, c.c_uint64) for n in ("bytes", "files", "anchor_hits", "candidates", "special_files",
+                                          "findings")] + \
+               [(n, c.c_double) for n in ("ms_scan_kernel", "ms_verify_kernel", "ms_fullscan_kernel",
+                                          "ms_gpu_total", "ms_host_gpu_phase", "ms_host_allow_path",
+                                          "ms_host_exact", "ms_host_total")]
+
+
+class _CTableInfo(c.Structure):
+    _fields_ = [(n, c.c_uint32) for n in ("n_rules", "n_keywords", "n_anchors", "ac_states", "ac_classes",
+                                          "max_pattern_len", "n_fullscan_rules", "nfa_words_total")] + \
+               [("ac_table_bytes", c.c_uint64)]
+
+
+def _declare(L):
+    if getattr(L, "_tsg_scanner_declared", False):
+        return
+    L.tsg_scanner_new.argtypes = [c.POINTER(_CGlobal), c.c_int, c.POINTER(c.c_void_p)]
+    L.tsg_scanner_free.argtypes = [c.c_void_p]
+    L.tsg_scanner_allow_path.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64]
+    L.tsg_scan.argtypes = [c.c_void_p, c.POINTER(_CBatch), c.POINTER(c.c_void_p)]
+    L.tsg_result_free.argtypes = [c.c_void_p]
+    L.tsg_result_json.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_uint64)]
+    L.tsg_result_stats.argtypes = [c.c_void_p, c.POINTER(_CStats)]
+    L.tsg_scanner_table_info.argtypes = [c.c_void_p, c.POINTER(_CTableInfo)]
+    L.tsg_scanner_rule_anchor.argtypes = [c.c_void_p, c.c_uint32]
+    L.tsg_scanner_rule_anchor.restype = c.c_char_p
+    L._tsg_scanner_declared = True
+
+
+def _b(s) -> Optional[bytes]:
+    if s is None:
+        return None
+    if isinstance(s, bytes):
+        return s
+    return str(s).encode("utf-8", "surrogateescape")
+
+
+def _s(latin: str) -> str:
+    """JSON strings from the library carry raw bytes as latin-1 code points."""
+    return latin.encode("latin-1").decode("utf-8", "surrogateescape")
+
+
+@dataclass
+class Line:  # pkg/fanal/types/misconf.go:52-61
+    Number: int = 0
+    Content: str = ""
+    IsCause: bool = False
+    Annotation: str = ""
+    Truncated: bool = False
+    Highlighted: str = ""
+    FirstCause: bool = False
+    LastCause: bool = False
+
+
+@dataclass
+class Code:  # misconf.go:48-50
+    Lines: List[Line] = field(default_factory=list)
+
+
+@dataclass
+class SecretFinding:  # pkg/fanal/types/secret.go:10-20
+    RuleID: str = ""
+    Category: str = ""
+    Severity: str = ""
+    Title: str = ""
+    StartLine: int = 0
+    EndLine: int = 0
+    Code: Code = field(default_factory=Code)
+    Match: str = ""
+
+    def to_dict(self):
+        return {"RuleID": self.RuleID, "Category": self.Category, "Severity": self.Severity,
+                "Title": self.Title, "StartLine": self.StartLine, "EndLine": self.EndLine,
+                "Code": {"Lines": [dict(l.__dict__) for l in self.Code.Lines]}, "Match": self.Match}
+
+
+@dataclass
+class Secret:  # pkg/fanal/types/secret.go:5-8
+    FilePath: str = ""
+    Findings: Optional[List[SecretFinding]] = None
+
+    def to_dict(self):
+        return {"FilePath": self.FilePath,
+                "Findings": None if self.Findings is None else [f.to_dict() for f in self.Findings]}
+
+
+@dataclass
+class ScanArgs:  # scanner.go:366-370
+    FilePath: str
+    Content: bytes
+    Binary: bool = False
+
+
+class CGlobal:
+    """tsg_global built from an assembled rule set (keeps the C strings alive)."""
+
+    def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude_regexes: Sequence[str]):
+        self.Rules = list(rules)
+        self.AllowRules = list(allow_rules)
+        self.ExcludeRegexes = list(exclude_regexes)
+        self._keep = []
+        self.g = self._build_global()
+
+    def _cstrs(self, items):
+        arr = (c.c_char_p * max(1, len(items)))(*[_b(x) for x in items])
+        self._keep.append(arr)
+        return arr
+
+    def _callow(self, items):
+        arr = (_CAllowRule * max(1, len(items)))()
+        for i, a in enumerate(items):
+            arr[i].id = _b(a.ID)
+            arr[i].regex = _b(a.Regex) if a.Regex else None
+            arr[i].path = _b(a.Path) if a.Path else None
+        self._keep.append(arr)
+        return arr
+
+    def _build_global(self):
+        rs = (_CRule * max(1, len(self.Rules)))()
+        for i, r in enumerate(self.Rules):
+            x = rs[i]
+            x.id, x.category, x.title, x.severity = _b(r.ID), _b(r.Category), _b(r.Title), _b(r.Severity)
+            x.regex = _b(r.Regex) if r.Regex else None
+            x.path = _b(r.Path) if r.Path else None
+            x.secret_group_name = _b(r.SecretGroupName or "")
+            x.keywords = self._cstrs(r.Keywords)
+            x.n_keywords = len(r.Keywords)
+            x.allow_rules = self._callow(r.AllowRules)
+            x.n_allow_rules = len(r.AllowRules)
+            x.exclude_regexes = self._cstrs(r.ExcludeBlock.Regexes)
+            x.n_exclude_regexes = len(r.ExcludeBlock.Regexes)
+        self._keep.append(rs)
+        return _CGlobal(rs, len(self.Rules), self._callow(self.AllowRules), len(self.AllowRules),
+                        self._cstrs(self.ExcludeRegexes), len(self.ExcludeRegexes))
+
+
+class Scanner:
+    """secret.Scanner: an assembled Global bound to one HIP device."""
+
+    def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude_regexes: Sequence[str],
+                 device: int = 0):
+        self.Rules = list(rules)
+        self.AllowRules = list(allow_rules)
+        self.ExcludeRegexes = list(exclude_regexes)
+        L = _lib.lib()
+        _declare(L)
+        self._L = L
+        self._cg = CGlobal(rules, allow_rules, exclude_regexes)
+        g = self._cg.g
+        h = c.c_void_p()
+        rc = L.tsg_scanner_new(c.byref(g), int(device), c.byref(h))
+        if rc != 0:
+            raise RuntimeError("tsg_scanner_new failed: %s" % _lib.last_error())
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.tsg_scanner_free(h)
+            self._h = None
+
+    # --- reference API -----------------------------------------------------
+    def AllowPath(self, path) -> bool:  # scanner.go:57-59
+        p = _b(path)
+        return self._L.tsg_scanner_allow_path(self._h, p, len(p)) == 1
+
+    def Scan(self, args: ScanArgs) -> Secret:  # scanner.go:377-463
+        return self.ScanBatch([args])[0]
+
+    def ScanBatch(self, args: Sequence[ScanArgs]) -> List[Secret]:
+        contents = [a.Content for a in args]
+        offs = np.zeros(len(contents) + 1, dtype=np.uint64)
+        if contents:
+            offs[1:] = np.cumsum([len(x) for x in contents], dtype=np.uint64)
+        arena = b"".join(contents) + b"\0" * 16
+        res = self.scan_arena(arena, offs, [a.FilePath for a in args],
+                              binary=[bool(a.Binary) for a in args])
+        return res.secrets([a.FilePath for a in args])
+
+    # --- batched arena API (analyzer / bench) -------------------------------
+    def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None):
+        n = len(offsets) - 1
+        arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        pb = [_b(p) for p in paths]
+        parr = (c.c_char_p * max(1, n))(*pb)
+        plen = np.array([len(p) for p in pb], dtype=np.uint64) if n else np.zeros(1, np.uint64)
+        bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
+        batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
+                        dev_arena, dev_offsets, parr, plen.ctypes.data,
+                        bin_arr.ctypes.data if bin_arr is not None else None)
+        h = c.c_void_p()
+        rc = self._L.tsg_scan(self._h, c.byref(batch), c.byref(h))
+        if rc != 0:
+            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
+        return ScanResult(self, h)
+
+    def table_info(self):
+        t = _CTableInfo()
+        self._L.tsg_scanner_table_info(self._h, c.byref(t))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+    def rule_anchor(self, i):
+        return self._L.tsg_scanner_rule_anchor(self._h, i).decode()
+
+
+class ScanResult:
+    def __init__(self, scanner, h):
+        self._sc = scanner
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._sc._L.tsg_result_free(self._h)
+            self._h = None
+
+    def stats(self):
+        s = _CStats()
+        self._sc._L.tsg_result_stats(self._h, c.byref(s))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def raw(self):
+        p = c.c_void_p()
+        n = c.c_uint64()
+        self._sc._L.tsg_result_json(self._h, c.byref(p), c.byref(n))
+        return json.loads(c.string_at(p, n.value).decode("ascii"))
+
+    def secrets(self, paths) -> List[Secret]:
+        out = []
+        for path, fr in zip(paths, self.raw()):
+            kind = fr["kind"]
+            if kind == 0:
+                out.append(Secret())
+            elif kind == 1:
+                out.append(Secret(FilePath=path))
+            else:
+                fs = []
+                for f in fr["findings"]:
+                    lines = [Line(Number=l["Number"], Content=_s(l["Content"]), IsCause=l["IsCause"],
+                                  Highlighted=_s(l["Highlighted"]), FirstCause=l["FirstCause"],
+                                  LastCause=l["LastCause"]) for l in f["Code"]["Lines"]]
+                    fs.append(SecretFinding(RuleID=_s(f["RuleID"]), Category=_s(f["Category"]),
+                                            Severity=_s(f["Severity"]), Title=_s(f["Title"]),
+                                            StartLine=f["StartLine"], EndLine=f["EndLine"],
+                                            Code=Code(Lines=lines), Match=_s(f["Match"])))
+                out.append(Secret(FilePath=path, Findings=fs))
+        return out
+
+
+def NewScanner(config: Optional[Config], device: int = 0) -> Scanner:  # scanner.go:320-364
+    b_rules, b_allow = builtin_rules(), builtin_allow_rules()
+    if config is None:
+        return Scanner(b_rules, b_allow, [], device)
+    enabled = b_rules
+    if config.EnableBuiltinRuleIDs:
+        enabled = [r for r in b_rules if r.ID in config.EnableBuiltinRuleIDs]
+    enabled = enabled + list(config.CustomRules)
+    rules = [r for r in enabled if r.ID not in config.DisableRuleIDs]
+    allow = b_allow + list(config.CustomAllowRules)
+    allow = [a for a in allow if a.ID not in config.DisableAllowRuleIDs]
+    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device)
