@@ -1,0 +1,21 @@
+/* Synthetic corpus generator (bench / large-size tests only; not the scan path).
+ * Deterministic: SplitMix64(seed ^ f(file index)); spec in SURVEY.md §8(d). */
+#ifndef TSG_CORPUS_H
+#define TSG_CORPUS_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* File sizes for target_bytes total; returns the file count and, when offsets
+ * is non-NULL, writes offsets[0..min(n, cap-1)]. */
+int64_t tsg_corpus_plan(uint64_t seed, uint64_t target_bytes, uint64_t* offsets, uint64_t cap);
+/* Fill arena (offsets[n_files] bytes) and paths (n_files * path_stride,
+ * NUL-terminated) using `threads` host threads.  Planted secrets are drawn
+ * from pool (concatenated strings, pool_off[n_pool+1]). */
+int tsg_corpus_fill(uint64_t seed, const uint64_t* offsets, uint64_t n_files, const char* pool,
+                    const uint64_t* pool_off, uint32_t n_pool, double secrets_per_byte, uint8_t* arena,
+                    char* paths, uint32_t path_stride, int threads);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -54,7 +54,8 @@ def host_tail_scan(cfg, files):
     pb = [_b(p) for p, _ in files]
     parr = (c.c_char_p * max(1, len(pb)))(*pb)
     plen = np.array([len(p) for p in pb], dtype=np.uint64)
-    batch = _CBatch(len(files), arena.ctypes.data, offs.ctypes.data, None, None, parr, plen.ctypes.data, None)
+    batch = _CBatch(len(files), arena.ctypes.data, offs.ctypes.data, None, None,
+                    c.cast(parr, c.c_void_p).value, plen.ctypes.data, None)
     h = c.c_void_p()
     if L.tsg_debug_host_tail(c.byref(cg.g), c.byref(batch), c.byref(h)) != 0:
         raise RuntimeError(_lib.last_error())

@@ -12,11 +12,15 @@ namespace tsg {
 
 constexpr uint32_t kChunk = 512;  // bytes per lane-chunk in the scan kernel
 
+constexpr uint32_t kCandHostGate = 1;  // keyword bits may over-approximate (file holds U+017F)
+
 struct Candidate {      // produced by the verify / full-scan kernels
   uint32_t file;
   uint32_t rule;
   int64_t wlo, whi;     // allowed match-start window, file-relative, inclusive
   int64_t nl_before;    // '\n' count in [file start, wlo)
+  uint32_t flags;       // kCand*
+  uint32_t pad;
 };
 
 struct BatchStats {
@@ -56,13 +60,16 @@ class GpuEngine {
   hipEvent_t ev_[4] = {};
   // tables
   uint8_t* d_cmap_ = nullptr;
-  uint16_t* d_trans_ = nullptr;
+  void* d_trans_ = nullptr;
+  bool wide_table_ = false;
+  uint32_t cls_fold_ = 0, cls_i_ = 0, cls_k_ = 0, cls_s_ = 0, div_magic_ = 0;
   uint32_t* d_out_off_ = nullptr;
   uint32_t* d_out_items_ = nullptr;
   AnchorInfo* d_anchors_ = nullptr;
   RuleGpu* d_rules_ = nullptr;
   uint32_t* d_rule_kw_ = nullptr;
   uint64_t* d_nfa_ = nullptr;
+  uint64_t* d_la_ = nullptr;
   uint32_t* d_fullscan_rules_ = nullptr;
   uint32_t n_states_ = 0, n_classes_ = 0, max_pat_len_ = 0, kw_words_ = 0, n_rules_ = 0;
   uint32_t n_fullscan_rules_ = 0;

@@ -24,9 +24,8 @@ namespace tsg {
 
 namespace {
 
-constexpr int kScanThreads = 512;
+constexpr int kScanThreads = 1024;
 constexpr int kHitBuf = 2048;  // records per workgroup LDS staging buffer
-constexpr uint32_t kKwCacheWords = 4;
 
 #define HIP_OK(x)                                                   \
   do {                                                              \
@@ -44,13 +43,18 @@ struct ScanParams {
   uint32_t n_files;
   const uint32_t* chunk_file;
   uint64_t n_chunks;
-  const uint8_t* cmap;
-  const uint16_t* trans;
+  const uint8_t* cmap;        // byte -> class; the fold-lead bytes C4/E2/C5 -> class n_cls_real
+  const void* trans;          // entry = next_state * n_classes | output flag (bit 0)
   const uint32_t* out_off;
   const uint32_t* out_items;
+  const AnchorInfo* anchors;
+  const uint64_t* la;         // lookahead ASCII masks (2 x u64 each)
   uint32_t n_states, n_classes, warm, kw_words;
+  uint32_t cls_fold;          // class id of the fold-lead bytes (largest id)
+  uint32_t cls_i, cls_k, cls_s;
+  uint32_t div_magic;         // ceil(2^32 / n_classes): state index = umulhi(entry, magic)
   uint32_t* kwbits;
-  uint32_t* flags;
+  uint32_t* flags;            // per file: bit0 fold rune seen, bit1 U+017F seen
   uint16_t* nl;
   uint32_t* hits;
   uint32_t hit_cap;
@@ -68,103 +72,114 @@ __global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_fi
   }
 }
 
-struct LaneState {
-  uint32_t state;
-  uint32_t skip;
-  uint32_t special;
-  uint32_t kw_cache[kKwCacheWords];
-};
-
-__device__ __noinline__ void emit_outputs(const ScanParams& P, uint32_t st, uint32_t f, uint64_t fs,
-                                          uint64_t end, LaneState& L, uint32_t* s_hits,
-                                          uint32_t* s_nhits) {
-  uint32_t a = P.out_off[st], b = P.out_off[st + 1];
+// Rare path: outputs of the DFA state whose table row starts at element `st`,
+// for a pattern ending at byte `end` (exclusive).  Keywords set the file's
+// gate bit; anchors pass the lookahead filter and are staged in LDS.
+__device__ __forceinline__ void emit_outputs(const ScanParams& P, uint32_t st, uint32_t f, uint64_t fs, uint64_t fe,
+                                             uint64_t end, uint32_t* s_hits, uint32_t* s_nhits) {
+  uint32_t sidx = __umulhi(st, P.div_magic);
+  uint32_t a = P.out_off[sidx], b = P.out_off[sidx + 1];
   for (uint32_t j = a; j < b; j++) {
     uint32_t item = P.out_items[j];
     uint32_t id = item & 0x0FFFFFFFu;
-    if ((item >> 28) == 0) {  // keyword
-      uint32_t w = id >> 5, bit = 1u << (id & 31);
-      if (P.kw_words <= kKwCacheWords) {
-        uint32_t cur = w == 0 ? L.kw_cache[0] : w == 1 ? L.kw_cache[1] : w == 2 ? L.kw_cache[2] : L.kw_cache[3];
-        if (!(cur & bit)) {
-          if (w == 0) L.kw_cache[0] |= bit;
-          else if (w == 1) L.kw_cache[1] |= bit;
-          else if (w == 2) L.kw_cache[2] |= bit;
-          else L.kw_cache[3] |= bit;
-          atomicOr(&P.kwbits[uint64_t(f) * P.kw_words + w], bit);
-        }
-      } else {
-        uint32_t* p = &P.kwbits[uint64_t(f) * P.kw_words + w];
-        if (!(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(p, bit);
+    if ((item >> 28) == 0) {  // keyword: set the file's gate bit once
+      uint32_t* w = &P.kwbits[uint64_t(f) * P.kw_words + (id >> 5)];
+      uint32_t bit = 1u << (id & 31);
+      if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
+      continue;
+    }
+    const AnchorInfo& an = P.anchors[id];
+    const uint32_t la_n = an.la_n, ext = an.ext;
+    uint32_t lac;
+    __builtin_memcpy(&lac, an.la_cls, 4);
+    const uint64_t lit_end = end - ext;  // the automaton already matched `ext` lookahead bytes
+    bool pass = true;
+    for (uint32_t q = ext; q < la_n; q++) {
+      uint64_t pos = lit_end + q;
+      if (pos >= fe) {
+        pass = false;
+        break;
       }
-    } else {  // anchor hit: (file, file-relative end, anchor id)
-      uint32_t k = atomicAdd(s_nhits, 1u);
-      uint32_t rel = uint32_t(end - fs);
-      if (k < uint32_t(kHitBuf)) {
-        s_hits[3 * k + 0] = f;
-        s_hits[3 * k + 1] = rel;
-        s_hits[3 * k + 2] = id;
-      } else {
-        uint32_t g = atomicAdd(&P.counters[0], 1u);
-        if (g < P.hit_cap) {
-          P.hits[3ull * g + 0] = f;
-          P.hits[3ull * g + 1] = rel;
-          P.hits[3ull * g + 2] = id;
-        } else {
-          P.counters[3] = 1;
-        }
+      uint32_t c = P.arena[pos];
+      if (c >= 0x80) break;  // multi-byte rune: positions no longer align, accept
+      uint64_t m = P.la[2 * ((lac >> (8 * q)) & 0xFFu) + (c >> 6)];
+      if (!((m >> (c & 63)) & 1)) {
+        pass = false;
+        break;
       }
     }
+    if (!pass) continue;
+    uint32_t k = atomicAdd(s_nhits, 1u);
+    uint32_t rel = uint32_t(lit_end - fs);
+    if (k < uint32_t(kHitBuf)) {
+      s_hits[3 * k + 0] = f;
+      s_hits[3 * k + 1] = rel;
+      s_hits[3 * k + 2] = id;
+    } else {
+      uint32_t g = atomicAdd(&P.counters[0], 1u);
+      if (g < P.hit_cap) {
+        P.hits[3ull * g + 0] = f;
+        P.hits[3ull * g + 1] = rel;
+        P.hits[3ull * g + 2] = id;
+      } else {
+        P.counters[3] = 1;
+      }
+    }
   }
 }
 
-// Resolve the three bytes whose multi-byte sequence can lower to / fold with ASCII.
-__device__ __noinline__ uint32_t fold_special(const ScanParams& P, const uint8_t* cmap, uint32_t cls,
-                                              uint64_t pos, uint64_t fe, LaneState& L) {
-  const uint8_t* a = P.arena;
-  if (cls == kClsFoldI) {  // C4 B0 = U+0130, bytes.ToLower -> 'i'
-    if (pos + 1 < fe && a[pos + 1] == 0xB0) {
-      L.skip = 1;
-      L.special = 1;
-      return cmap['i'];
+// Careful path for a segment holding a fold-lead byte (C4/E2/C5): the
+// multi-byte sequences U+0130 -> 'i' and U+212A -> 'k' lower to ASCII under
+// bytes.ToLower; U+017F folds with 's' under (?i) (used for anchors only;
+// the file is flagged so the host re-checks its keyword gates).
+template <typename TT>
+__device__ __forceinline__ uint32_t careful_segment(const ScanParams& P, const TT* T, const uint8_t* cmap,
+                                                    uint32_t f, uint64_t fs, uint64_t fe, uint64_t seg0,
+                                                    uint64_t seg1, uint32_t* s_hits, uint32_t* s_nhits) {
+  uint64_t w = seg0 - fs > 3ull * P.warm ? seg0 - 3ull * P.warm : fs;
+  uint32_t st = 0, skip = 0, fl = 0;
+  for (uint64_t p = w; p < seg1; p++) {
+    if (skip) {
+      skip--;
+      continue;
     }
-  } else if (cls == kClsFoldK) {  // E2 84 AA = U+212A, lowers to 'k'
-    if (pos + 2 < fe && a[pos + 1] == 0x84 && a[pos + 2] == 0xAA) {
-      L.skip = 2;
-      L.special = 1;
-      return cmap['k'];
+    uint32_t b = P.arena[p];
+    uint32_t cls = cmap[b];
+    if (cls == P.cls_fold) {
+      cls = 0;
+      if (b == 0xC4 && p + 1 < fe && P.arena[p + 1] == 0xB0) {
+        skip = 1;
+        cls = P.cls_i;
+        if (p >= seg0) fl |= 1;
+      } else if (b == 0xE2 && p + 2 < fe && P.arena[p + 1] == 0x84 && P.arena[p + 2] == 0xAA) {
+        skip = 2;
+        cls = P.cls_k;
+        if (p >= seg0) fl |= 1;
+      } else if (b == 0xC5 && p + 1 < fe && P.arena[p + 1] == 0xBF) {
+        skip = 1;
+        cls = P.cls_s;
+        if (p >= seg0) fl |= 3;
+      }
     }
-  } else {  // C5 BF = U+017F, folds with 's' under (?i) but lowers to itself
-    if (pos + 1 < fe && a[pos + 1] == 0xBF) {
-      L.skip = 1;
-      L.special = 1;
-      return 0;
-    }
+    uint32_t e = T[st + cls];
+    st = e & ~1u;
+    if ((e & 1u) && p >= seg0) emit_outputs(P, st, f, fs, fe, p + 1 + skip, s_hits, s_nhits);
   }
-  return 0;
+  return fl;
 }
 
-template <bool kOut>
-__device__ __forceinline__ void ac_step(const ScanParams& P, const uint16_t* __restrict__ T,
-                                        const uint8_t* __restrict__ cmap, uint32_t b, uint64_t pos,
-                                        uint32_t f, uint64_t fs, uint64_t fe, LaneState& L,
-                                        uint32_t* s_hits, uint32_t* s_nhits) {
-  if (L.skip) {
-    L.skip--;
-    return;
-  }
-  uint32_t cls = cmap[b];
-  if (cls >= kClsFoldI) cls = fold_special(P, cmap, cls, pos, fe, L);
-  uint32_t e = T[L.state * P.n_classes + cls];
-  L.state = e & 0x7FFFu;
-  if (kOut && (e & kAcOutFlag)) emit_outputs(P, L.state, f, fs, pos + 1 + L.skip, L, s_hits, s_nhits);
+// '\n' bytes in a 32-bit word (exact per byte)
+__device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
+  uint32_t x = w ^ 0x0A0A0A0Au;
+  uint32_t nz = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // bit7 set <=> byte != 0
+  return 4u - __popc(nz & 0x80808080u);
 }
 
-template <bool kLdsTable>
+template <typename TT, bool kLdsTable>
 __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  size_t tbytes = kLdsTable ? ((size_t(P.n_states) * P.n_classes * 2 + 15) & ~size_t(15)) : 0;
-  uint16_t* s_trans = reinterpret_cast<uint16_t*>(smem);
+  size_t tbytes = kLdsTable ? ((size_t(P.n_states) * P.n_classes * sizeof(TT) + 15) & ~size_t(15)) : 0;
+  TT* s_trans = reinterpret_cast<TT*>(smem);
   uint8_t* s_cmap = smem + tbytes;
   uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + tbytes + 256);
   uint32_t* s_nhits = s_hits + 3 * kHitBuf;
@@ -179,7 +194,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   for (int i = tid; i < 256; i += blockDim.x) s_cmap[i] = P.cmap[i];
   if (tid == 0) *s_nhits = 0;
   __syncthreads();
-  const uint16_t* T = kLdsTable ? s_trans : P.trans;
+  const TT* T = kLdsTable ? s_trans : reinterpret_cast<const TT*>(P.trans);
+  const uint32_t cls_fold = P.cls_fold;
 
   for (uint64_t tile = blockIdx.x; tile * blockDim.x < P.n_chunks; tile += gridDim.x) {
     uint64_t c = tile * blockDim.x + tid;
@@ -188,48 +204,72 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
       uint64_t b1 = b0 + kChunk < P.n_bytes ? b0 + kChunk : P.n_bytes;
       uint32_t f = P.chunk_file[c];
       uint32_t nl = 0;
-      LaneState L;
       while (f < P.n_files) {
         uint64_t fs = P.off[f], fe = P.off[f + 1];
         if (fs >= b1) break;
         uint64_t seg0 = fs > b0 ? fs : b0;
         uint64_t seg1 = fe < b1 ? fe : b1;
         if (seg0 < seg1) {
-          L.state = 0;
-          L.skip = 0;
-          L.special = 0;
-          L.kw_cache[0] = L.kw_cache[1] = L.kw_cache[2] = L.kw_cache[3] = 0;
-          if (seg0 > fs) {
-            // warm-up: the DFA state depends only on the last max_len-1 symbols
-            uint64_t w = seg0 - fs > P.warm ? seg0 - P.warm : fs;
-            for (uint64_t p = w; p < seg0; p++)
-              ac_step<false>(P, T, s_cmap, P.arena[p], p, f, fs, fe, L, s_hits, s_nhits);
-            if (L.special && w > fs) {  // folded runes shorten symbols: re-warm 3x longer
-              uint64_t w3 = seg0 - fs > 3ull * P.warm ? seg0 - 3ull * P.warm : fs;
-              L.state = 0;
-              L.skip = 0;
-              for (uint64_t p = w3; p < seg0; p++)
-                ac_step<false>(P, T, s_cmap, P.arena[p], p, f, fs, fe, L, s_hits, s_nhits);
-            }
-            L.special = 0;
+          uint32_t st = 0, spec = 0;
+          // warm-up: the DFA state depends only on the last max_len-1 symbols
+          for (uint64_t p = (seg0 - fs > P.warm ? seg0 - P.warm : fs); p < seg0; p++) {
+            uint32_t cl = s_cmap[P.arena[p]];
+            spec = spec > cl ? spec : cl;
+            st = T[st + cl] & ~1u;
           }
-          for (uint64_t p = seg0 & ~uint64_t(15); p < seg1; p += 16) {
-            uint4 v = *reinterpret_cast<const uint4*>(P.arena + p);
+          // main: 16-B loads with the next block in flight.  Hot loop = class
+          // lookup + transition; blocks whose states carry outputs are replayed
+          // with emission (outputs are rare: see DESIGN.md §4.1).
+          uint64_t p = seg0 & ~uint64_t(15);
+          uint4 v = *reinterpret_cast<const uint4*>(P.arena + p);
+          for (; p < seg1; p += 16) {
+            uint4 nv = *reinterpret_cast<const uint4*>(P.arena + p + 16);  // arena is padded
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t st0 = st;
+            uint32_t any = 0;
+            if (p >= seg0 && p + 16 <= seg1) {
+              nl += nl_in_word(v.x) + nl_in_word(v.y) + nl_in_word(v.z) + nl_in_word(v.w);
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-              uint64_t pos = p + k;
-              uint32_t b = (wd[k >> 2] >> ((k & 3) * 8)) & 0xFFu;
-              if (pos >= seg0 && pos < seg1) {
+              for (int k = 0; k < 16; k++) {
+                uint32_t cl = s_cmap[(wd[k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+                spec = spec > cl ? spec : cl;
+                uint32_t e = T[st + cl];
+                any |= e;
+                st = e & ~1u;
+              }
+            } else {
+              for (int k = 0; k < 16; k++) {
+                if (p + k < seg0 || p + k >= seg1) continue;
+                uint32_t b = P.arena[p + k];
                 nl += (b == '\n');
-                ac_step<true>(P, T, s_cmap, b, pos, f, fs, fe, L, s_hits, s_nhits);
+                uint32_t cl = s_cmap[b];
+                spec = spec > cl ? spec : cl;
+                uint32_t e = T[st + cl];
+                any |= e;
+                st = e & ~1u;
               }
             }
+            if (any & 1u) {  // replay the block, emitting outputs
+              st = st0;
+              for (int k = 0; k < 16; k++) {
+                uint64_t q = p + k;
+                if (q < seg0 || q >= seg1) continue;
+                uint32_t e = T[st + s_cmap[P.arena[q]]];
+                st = e & ~1u;
+                if (e & 1u) emit_outputs(P, st, f, fs, fe, q + 1, s_hits, s_nhits);
+              }
+            }
+            v = nv;
           }
-          if (L.special) {
-            if (atomicOr(&P.flags[f], 1u) == 0) {
-              uint32_t k = atomicAdd(&P.counters[2], 1u);
-              if (k < P.special_cap) P.special[k] = f;
+          if (spec >= cls_fold) {
+            // a fold-lead byte was seen: redo the segment on the careful path
+            uint32_t fl = careful_segment<TT>(P, T, s_cmap, f, fs, fe, seg0, seg1, s_hits, s_nhits);
+            if (fl) {
+              uint32_t old = atomicOr(&P.flags[f], fl);
+              if (old == 0) {
+                uint32_t k = atomicAdd(&P.counters[2], 1u);
+                if (k < P.special_cap) P.special[k] = f;
+              }
             }
           }
         }
@@ -373,7 +413,7 @@ __device__ int64_t count_nl(const NfaParams& P, uint64_t a, uint64_t b) {  // '\
 }
 
 __device__ void emit_candidate(const NfaParams& P, uint32_t f, uint32_t r, int64_t wlo, int64_t whi,
-                               int64_t nlb) {
+                               int64_t nlb, uint32_t flags) {
   uint32_t k = atomicAdd(&P.counters[1], 1u);
   if (k < P.cand_cap) {
     Candidate c;
@@ -382,6 +422,8 @@ __device__ void emit_candidate(const NfaParams& P, uint32_t f, uint32_t r, int64
     c.wlo = wlo;
     c.whi = whi;
     c.nl_before = nlb;
+    c.flags = flags;
+    c.pad = 0;
     P.cands[k] = c;
   } else {
     P.counters[4] = 1;
@@ -392,46 +434,42 @@ __global__ __launch_bounds__(256) void verify_kernel(NfaParams P) {
   uint32_t n = P.counters[0] < P.hit_cap ? P.counters[0] : P.hit_cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     uint32_t f = P.hits[3ull * i], end = P.hits[3ull * i + 1], aid = P.hits[3ull * i + 2];
-    if (P.flags[f] & 1u) continue;  // special file: handled by full-scan tasks
     AnchorInfo a = P.anchors[aid];
     RuleGpu rg = P.rules[a.rule];
     if (!gate_open(P, rg, f)) continue;
-    int64_t lit = int64_t(end) - int64_t(a.lit_len);
-    int64_t whi = lit - a.off_lo;
+    uint32_t ff = P.flags[f];
+    // literal start: lit_len bytes before the end, up to 3x when folded runes occur
+    int64_t lit_hi = int64_t(end) - int64_t(a.lit_len);
+    int64_t lit_lo = (ff & 1u) ? int64_t(end) - 3 * int64_t(a.lit_len) : lit_hi;
+    int64_t whi = lit_hi - a.off_lo;
     if (whi < 0) continue;
-    int64_t wlo = lit - a.off_hi;
+    int64_t wlo = lit_lo - ((ff & 1u) ? int64_t(a.off_hi_fold) : int64_t(a.off_hi));
     if (wlo < 0) wlo = 0;
     uint64_t fs = P.off[f];
     int64_t len = int64_t(P.off[f + 1] - fs);
     bool acc = rg.nfa_words == 0 ||
                nfa_dispatch(rg.nfa_words, P.arena + fs, len, wlo, whi, P.nfa + rg.nfa_off);
-    if (acc) emit_candidate(P, f, a.rule, wlo, whi, count_nl(P, fs, fs + uint64_t(wlo)));
+    if (acc)
+      emit_candidate(P, f, a.rule, wlo, whi, count_nl(P, fs, fs + uint64_t(wlo)),
+                     (ff & 2u) ? kCandHostGate : 0u);
   }
 }
 
+// Unanchored rules (no literal at a bounded offset): NFA with injection at
+// every byte of every gated file; an accept makes the whole file the window.
 __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
-  uint32_t ns = P.counters[2] < P.special_cap ? P.counters[2] : P.special_cap;
-  uint64_t t_special = uint64_t(ns) * P.n_regex_rules;
-  uint64_t total = t_special + uint64_t(P.n_files) * P.n_fullscan_rules;
+  uint64_t total = uint64_t(P.n_files) * P.n_fullscan_rules;
   for (uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; t < total;
        t += uint64_t(gridDim.x) * blockDim.x) {
-    uint32_t f, r;
-    if (t < t_special) {
-      f = P.special[t / P.n_regex_rules];
-      r = P.regex_rules[t % P.n_regex_rules];
-    } else {
-      uint64_t u = t - t_special;
-      f = uint32_t(u / P.n_fullscan_rules);
-      r = P.fullscan_rules[u % P.n_fullscan_rules];
-      if (P.flags[f] & 1u) continue;  // already covered by the special tasks
-    }
+    uint32_t f = uint32_t(t / P.n_fullscan_rules);
+    uint32_t r = P.fullscan_rules[t % P.n_fullscan_rules];
     RuleGpu rg = P.rules[r];
     if (!gate_open(P, rg, f)) continue;
     uint64_t fs = P.off[f];
     int64_t len = int64_t(P.off[f + 1] - fs);
     bool acc = rg.nfa_words == 0 ||
                nfa_dispatch(rg.nfa_words, P.arena + fs, len, 0, len, P.nfa + rg.nfa_off);
-    if (acc) emit_candidate(P, f, r, 0, len, 0);
+    if (acc) emit_candidate(P, f, r, 0, len, 0, (P.flags[f] & 2u) ? kCandHostGate : 0u);
   }
 }
 
@@ -472,39 +510,76 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (!cr.rules[r].anchored) fullscan_rules_.push_back(r);
   }
   n_fullscan_rules_ = uint32_t(fullscan_rules_.size());
-  // pad the transition table to 16 B for the vectorised LDS fill
-  std::vector<uint16_t> trans = cr.trans;
-  trans.resize(((trans.size() * 2 + 15) & ~size_t(15)) / 2, 0);
-  if (!Upload(&err_, &d_cmap_, cr.cmap, 256) || !Upload(&err_, &d_trans_, trans.data(), trans.size()) ||
+  // class columns: the real ones, then one for the fold-lead bytes (a copy
+  // of the "other" column 0, so the hot loop needs no branch), padded to even
+  uint32_t nc_real = n_classes_;
+  cls_fold_ = nc_real;
+  uint32_t nc = nc_real + 1;
+  if (nc & 1) nc++;
+  n_classes_ = nc;
+  if (nc >= 0xFF) {
+    err_ = "too many keyword character classes";
+    return;
+  }
+  uint8_t cmap[256];
+  for (int b = 0; b < 256; b++) {
+    uint8_t m = cr.cmap[b];
+    cmap[b] = m >= kClsFoldI ? uint8_t(cls_fold_) : m;
+  }
+  cls_i_ = cr.cmap['i'];
+  cls_k_ = cr.cmap['k'];
+  cls_s_ = cr.cmap['s'];
+  div_magic_ = uint32_t((uint64_t(1) << 32) / nc + 1);
+  // entry = next_state * nc | output flag (bit 0); nc is even so bit 0 is free
+  wide_table_ = uint64_t(n_states_) * nc >= 0x10000;
+  std::vector<uint8_t> tbuf;
+  size_t esz = wide_table_ ? 4 : 2;
+  size_t tbytes = (size_t(n_states_) * nc * esz + 15) & ~size_t(15);
+  tbuf.assign(tbytes + 16, 0);
+  for (size_t st = 0; st < n_states_; st++)
+    for (uint32_t col = 0; col < nc; col++) {
+      uint32_t src = col < nc_real ? col : 0;
+      uint32_t e = cr.trans[st * nc_real + src];
+      uint32_t v = (e & 0x7FFFu) * nc | ((e & kAcOutFlag) ? 1u : 0u);
+      size_t i = st * nc + col;
+      if (wide_table_) std::memcpy(&tbuf[i * 4], &v, 4);
+      else {
+        uint16_t h = uint16_t(v);
+        std::memcpy(&tbuf[i * 2], &h, 2);
+      }
+    }
+  uint8_t* d_tb = nullptr;
+  std::vector<uint64_t> la = cr.la_masks;
+  if (la.empty()) la.assign(2, 0);
+  if (!Upload(&err_, &d_cmap_, cmap, 256) || !Upload(&err_, &d_tb, tbuf.data(), tbuf.size()) ||
       !Upload(&err_, &d_out_off_, cr.out_off.data(), cr.out_off.size()) ||
       !Upload(&err_, &d_out_items_, cr.out_items.data(), cr.out_items.size()) ||
       !Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
+      !Upload(&err_, &d_la_, la.data(), la.size()) ||
       !Upload(&err_, &d_rules_, cr.rules.data(), cr.rules.size()) ||
       !Upload(&err_, &d_rule_kw_, cr.rule_kw.data(), cr.rule_kw.size()) ||
       !Upload(&err_, &d_nfa_, cr.nfa.data(), cr.nfa.size()) ||
       !Upload(&err_, &d_regex_rules_, regex_rules_.data(), regex_rules_.size()) ||
       !Upload(&err_, &d_fullscan_rules_, fullscan_rules_.data(), fullscan_rules_.size()))
     return;
+  d_trans_ = d_tb;
   if (hipMalloc(&d_counters_, 64) != hipSuccess) {
     err_ = "hipMalloc counters";
     return;
   }
-  size_t tbytes = (size_t(n_states_) * n_classes_ * 2 + 15) & ~size_t(15);
   size_t rest = 256 + size_t(3 * kHitBuf + 4) * 4;
   table_in_lds_ = tbytes + rest <= 150 * 1024;
   lds_bytes_ = (table_in_lds_ ? tbytes : 0) + rest;
-  if (table_in_lds_) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_kernel<true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes_));
-  } else {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_kernel<false>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes_));
-  }
+  const void* fn = wide_table_ ? (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint32_t, true>)
+                                                : reinterpret_cast<const void*>(&scan_kernel<uint32_t, false>))
+                               : (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint16_t, true>)
+                                                : reinterpret_cast<const void*>(&scan_kernel<uint16_t, false>));
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes_));
 }
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_rules_, d_rule_kw_, d_nfa_,
+  void* ps[] = {d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
                 d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
@@ -577,6 +652,13 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.trans = d_trans_;
     sp.out_off = d_out_off_;
     sp.out_items = d_out_items_;
+    sp.anchors = d_anchors_;
+    sp.la = d_la_;
+    sp.cls_fold = cls_fold_;
+    sp.cls_i = cls_i_;
+    sp.cls_k = cls_k_;
+    sp.cls_s = cls_s_;
+    sp.div_magic = div_magic_;
     sp.n_states = n_states_;
     sp.n_classes = n_classes_;
     sp.warm = max_pat_len_ > 0 ? max_pat_len_ - 1 : 0;
@@ -593,10 +675,13 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     uint32_t per_cu = std::max<uint32_t>(1, uint32_t((160 * 1024) / lds_bytes_));
     uint32_t grid = uint32_t(std::min<uint64_t>(tiles, uint64_t(256) * per_cu));
     HIP_OK(hipEventRecord(ev_[0], stream_));
-    if (table_in_lds_)
-      scan_kernel<true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-    else
-      scan_kernel<false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+    if (wide_table_) {
+      if (table_in_lds_) scan_kernel<uint32_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+      else scan_kernel<uint32_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+    } else {
+      if (table_in_lds_) scan_kernel<uint16_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+      else scan_kernel<uint16_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[1], stream_));
     NfaParams np;
@@ -625,7 +710,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     verify_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[2], stream_));
-    if (np.n_regex_rules > 0) {
+    if (np.n_fullscan_rules > 0) {
       fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
       HIP_OK(hipGetLastError());
     }

@@ -26,7 +26,7 @@ bool ClassHas(const RuneRanges& rr, uint32_t c) {
 // Byte-length range of one rune matched by the class, over the runes that can
 // appear in a non-special file (U+212A/U+017F/U+0130 only occur in files the
 // GPU routes to full-scan mode).
-void ClassBytes(const RuneRanges& rr, int64_t* mn, int64_t* mx) {
+void ClassBytes(const RuneRanges& rr, int64_t* mn, int64_t* mx, bool fold_runes) {
   int lo = 5, hi = 0;
   bool any = false;
   for (auto& p : rr) {
@@ -37,7 +37,7 @@ void ClassBytes(const RuneRanges& rr, int64_t* mn, int64_t* mx) {
       uint32_t x = std::max(a, bounds[k][0]), y = std::min(b, bounds[k][1]);
       if (x > y) continue;
       // skip the fold-only runes if they are the only members in this part
-      bool only_special = true;
+      bool only_special = !fold_runes;
       for (uint32_t c = x; c <= y && only_special; c++) {
         if (!IsFoldOnlyRune(c)) only_special = false;
         if (c - x > 4) only_special = false;
@@ -81,9 +81,10 @@ int LitChar(const Node& n) {
 
 struct Analyzer {
   const std::vector<Node>& nodes;
+  bool fold;
   std::map<int, std::pair<int64_t, int64_t>> memo;
 
-  explicit Analyzer(const std::vector<Node>& n) : nodes(n) {}
+  Analyzer(const std::vector<Node>& n, bool f) : nodes(n), fold(f) {}
 
   std::pair<int64_t, int64_t> Bytes(int i) {
     auto it = memo.find(i);
@@ -94,7 +95,7 @@ struct Analyzer {
       case NodeOp::Empty:
       case NodeOp::NoMatch:
       case NodeOp::Assert: break;
-      case NodeOp::Class: ClassBytes(n.ranges, &r.first, &r.second); break;
+      case NodeOp::Class: ClassBytes(n.ranges, &r.first, &r.second, fold); break;
       case NodeOp::Cat:
         for (int s : n.subs) {
           auto b = Bytes(s);
@@ -155,6 +156,8 @@ struct Analyzer {
 struct Cand {
   std::vector<std::string> lits;
   int64_t olo, ohi;
+  int64_t ohi_fold = 0;
+  std::vector<std::vector<int>> follow;  // per literal: flattened items after it
   size_t minlen() const {
     size_t m = SIZE_MAX;
     for (auto& l : lits) m = std::min(m, l.size());
@@ -163,11 +166,12 @@ struct Cand {
 };
 
 bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
-  Analyzer an(re.nodes());
+  Analyzer an(re.nodes(), false), anf(re.nodes(), true);
   std::vector<int> items;
   an.Flatten(re.root(), &items);
   std::vector<Cand> cands;
-  int64_t olo = 0, ohi = 0;
+  int64_t olo = 0, ohi = 0, ohf = 0;
+  auto tail = [&](size_t from) { return std::vector<int>(items.begin() + long(from), items.end()); };
   for (size_t k = 0; k < items.size();) {
     const Node& n = re.nodes()[items[k]];
     int c = LitChar(n);
@@ -180,9 +184,18 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
         s.push_back(char(cj));
         j++;
       }
-      if (ohi < kInf || !need_offset) cands.push_back({{s}, olo, ohi});
+      if (ohi < kInf || !need_offset) {
+        Cand cd{{s}, olo, ohi};
+        cd.ohi_fold = ohf;
+        cd.follow.push_back(tail(j));
+        cands.push_back(cd);
+      }
+      // the literal chars themselves are 1 byte each normally, up to 3 when folded
+      int64_t fb = 0;
+      for (size_t q = k; q < j; q++) fb += anf.Bytes(items[q]).second;
       olo += int64_t(s.size());
       if (ohi < kInf) ohi += int64_t(s.size());
+      if (ohf < kInf) ohf += fb;
       k = j;
       continue;
     }
@@ -191,31 +204,58 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
     if (n.op == NodeOp::Repeat && n.min >= 1) {
       int sub = n.subs[0];
       while (re.nodes()[sub].op == NodeOp::Capture) sub = re.nodes()[sub].subs[0];
-      if (re.nodes()[sub].op == NodeOp::Alt) alt = sub;
+      if (re.nodes()[sub].op == NodeOp::Alt) alt = -2 - sub;  // alternation inside a repeat: no lookahead
       else {
         std::string s = an.LeadLiteral(sub);
-        if (!s.empty() && (ohi < kInf || !need_offset)) cands.push_back({{s}, olo, ohi});
+        if (!s.empty() && (ohi < kInf || !need_offset)) {
+          Cand cd{{s}, olo, ohi};
+          cd.ohi_fold = ohf;
+          cd.follow.push_back({});
+          cands.push_back(cd);
+        }
       }
     }
-    if (alt >= 0 && (ohi < kInf || !need_offset)) {
+    if (alt != -1 && (ohi < kInf || !need_offset)) {
+      bool in_repeat = alt <= -2;
+      int an_node = in_repeat ? -2 - alt : alt;
       Cand cd{{}, olo, ohi};
+      cd.ohi_fold = ohf;
       bool ok = true;
-      for (int b : re.nodes()[alt].subs) {
+      for (int b : re.nodes()[an_node].subs) {
         std::string s = an.LeadLiteral(b);
         if (s.empty()) { ok = false; break; }
         cd.lits.push_back(s);
+        std::vector<int> bi;
+        an.Flatten(b, &bi);
+        std::vector<int> fol;
+        if (!in_repeat) {
+          fol.assign(bi.begin() + long(s.size()), bi.end());
+          auto t = tail(k + 1);
+          fol.insert(fol.end(), t.begin(), t.end());
+        }
+        cd.follow.push_back(fol);
       }
       if (ok) cands.push_back(cd);
     }
     auto b = an.Bytes(items[k]);
+    auto bf = anf.Bytes(items[k]);
     olo += b.first;
     ohi = (ohi >= kInf || b.second >= kInf) ? kInf : ohi + b.second;
+    ohf = (ohf >= kInf || bf.second >= kInf) ? kInf : ohf + bf.second;
     k++;
   }
   bool have = false;
   for (auto& cd : cands) {
-    std::sort(cd.lits.begin(), cd.lits.end());
-    cd.lits.erase(std::unique(cd.lits.begin(), cd.lits.end()), cd.lits.end());
+    // dedupe literals (keep the first follow list of each)
+    std::vector<std::string> L;
+    std::vector<std::vector<int>> F;
+    for (size_t i = 0; i < cd.lits.size(); i++) {
+      if (std::find(L.begin(), L.end(), cd.lits[i]) != L.end()) continue;
+      L.push_back(cd.lits[i]);
+      F.push_back(cd.follow[i]);
+    }
+    cd.lits = L;
+    cd.follow = F;
     if (!have || cd.minlen() > best->minlen() ||
         (cd.minlen() == best->minlen() && cd.lits.size() < best->lits.size())) {
       *best = cd;
@@ -223,6 +263,52 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
     }
   }
   return have && best->minlen() >= 2;
+}
+
+// Up to 4 mandatory single-rune classes at the start of `fol` (ASCII masks).
+// ascii_only[i]: the class holds no non-ASCII rune besides the fold-only ones.
+std::vector<std::pair<uint64_t, uint64_t>> Lookahead(const std::vector<Node>& nodes, const std::vector<int>& fol,
+                                                     std::vector<bool>* ascii_only = nullptr) {
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  auto asc_only = [&](const RuneRanges& rr) {
+    for (auto& p : rr) {
+      if (p.second < 0x80) continue;
+      for (uint32_t c = std::max<uint32_t>(p.first, 0x80); c <= p.second; c++) {
+        if (!IsFoldOnlyRune(c)) return false;
+        if (c - p.first > 8) return false;
+      }
+    }
+    return true;
+  };
+  auto mask = [&](const RuneRanges& rr) {
+    std::pair<uint64_t, uint64_t> m{0, 0};
+    for (uint32_t b = 0; b < 128; b++)
+      if (ClassHas(rr, b)) (b < 64 ? m.first : m.second) |= uint64_t(1) << (b & 63);
+    return m;
+  };
+  for (int it : fol) {
+    if (out.size() >= 4) break;
+    const Node& n = nodes[it];
+    if (n.op == NodeOp::Class) {
+      out.push_back(mask(n.ranges));
+      if (ascii_only) ascii_only->push_back(asc_only(n.ranges));
+      continue;
+    }
+    if (n.op == NodeOp::Repeat && n.min >= 1) {
+      int sub = n.subs[0];
+      while (nodes[sub].op == NodeOp::Capture) sub = nodes[sub].subs[0];
+      if (nodes[sub].op == NodeOp::Class) {
+        for (int r = 0; r < n.min && out.size() < 4; r++) {
+          out.push_back(mask(nodes[sub].ranges));
+          if (ascii_only) ascii_only->push_back(asc_only(nodes[sub].ranges));
+        }
+        if (n.max != n.min) break;  // what follows the repeat is not at a fixed position
+        continue;
+      }
+    }
+    break;
+  }
+  return out;
 }
 
 // ---------------------------------------------------------------------------
@@ -489,6 +575,67 @@ bool BuildAc(const std::vector<std::pair<std::string, uint32_t>>& pats, Compiled
 }
 }  // namespace
 
+bool KeywordImplied(const Regex& re, const std::string& kw) {
+  if (kw.empty()) return true;
+  Analyzer an(re.nodes(), false);
+  const auto& nodes = re.nodes();
+  // a run of literal chars with, per char, whether U+017F is in its class
+  auto contains = [&](const std::vector<int>& run) {
+    std::string s;
+    std::vector<bool> hz;
+    for (int it : run) {
+      s.push_back(char(LitChar(nodes[it])));
+      hz.push_back(ClassHas(nodes[it].ranges, 0x17F));
+    }
+    for (size_t o = 0; o + kw.size() <= s.size(); o++) {
+      bool ok = true;
+      for (size_t i = 0; i < kw.size() && ok; i++)
+        if (s[o + i] != kw[i] || (kw[i] == 's' && hz[o + i])) ok = false;
+      if (ok) return true;
+    }
+    return false;
+  };
+  auto lead_run = [&](int node) {
+    std::vector<int> items, run;
+    an.Flatten(node, &items);
+    for (int it : items) {
+      if (LitChar(nodes[it]) < 0) break;
+      run.push_back(it);
+    }
+    return run;
+  };
+  std::vector<int> items;
+  an.Flatten(re.root(), &items);
+  for (size_t k = 0; k < items.size();) {
+    if (LitChar(nodes[items[k]]) >= 0) {
+      std::vector<int> run;
+      while (k < items.size() && LitChar(nodes[items[k]]) >= 0) run.push_back(items[k++]);
+      if (contains(run)) return true;
+      continue;
+    }
+    const Node& n = nodes[items[k]];
+    int alt = -1;
+    if (n.op == NodeOp::Alt) alt = items[k];
+    if (n.op == NodeOp::Repeat && n.min >= 1) {
+      int sub = n.subs[0];
+      while (nodes[sub].op == NodeOp::Capture) sub = nodes[sub].subs[0];
+      if (nodes[sub].op == NodeOp::Alt) alt = sub;
+      else if (contains(lead_run(sub))) return true;
+    }
+    if (alt >= 0) {
+      bool all = true;
+      for (int b : nodes[alt].subs)
+        if (!contains(lead_run(b))) {
+          all = false;
+          break;
+        }
+      if (all) return true;
+    }
+    k++;
+  }
+  return false;
+}
+
 std::vector<std::string> RequiredLiterals(const Regex& re) {
   Cand best{{}, 0, 0};
   if (!ExtractAnchor(re, &best, false)) return {};
@@ -509,10 +656,18 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
       if (!re) return false;
       rg.has_regex = 1;
     }
-    // keyword gate (strings.ToLower of each keyword)
+    // keyword gate (strings.ToLower of each keyword); redundant when some
+    // keyword is implied by every match of the regex
     rg.kw_off = uint32_t(out->rule_kw.size());
     bool host_gate = false;
+    bool redundant = false;
+    if (re) {
+      for (auto& kw : r.keywords)
+        if (IsAscii(kw) && KeywordImplied(*re, AsciiLower(kw))) redundant = true;
+    }
+    if (redundant) out->n_redundant_gates++;
     for (auto& kw : r.keywords) {
+      if (redundant) break;
       if (!IsAscii(kw)) {
         host_gate = true;
         continue;
@@ -534,7 +689,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     bool empty_kw = false;
     for (auto& kw : r.keywords)
       if (kw.empty()) empty_kw = true;
-    if (r.keywords.empty() || empty_kw) rg.gate = kGateAlways;  // "" is a substring of anything
+    if (r.keywords.empty() || empty_kw || redundant) rg.gate = kGateAlways;  // "" is a substring of anything
     else rg.gate = host_gate ? kGateHost : kGateKeywords;
     // anchor + relaxed NFA
     std::string desc = "-";
@@ -543,11 +698,48 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
       if (ExtractAnchor(*re, &best)) {
         rg.anchored = 1;
         desc = "[" + std::to_string(best.olo) + "," + std::to_string(best.ohi) + "]";
-        for (auto& l : best.lits) {
+        for (size_t li = 0; li < best.lits.size(); li++) {
+          const std::string& l = best.lits[li];
           uint32_t aid = uint32_t(out->anchors.size());
-          out->anchors.push_back({uint32_t(ri), uint32_t(l.size()), int32_t(best.olo), int32_t(best.ohi)});
-          pats.push_back({l, kOutAnchor | aid});
-          desc += " " + l;
+          AnchorInfo ai{};
+          ai.rule = uint32_t(ri);
+          ai.lit_len = uint16_t(l.size());
+          ai.off_lo = int32_t(best.olo);
+          ai.off_hi = int32_t(best.ohi);
+          ai.off_hi_fold = int32_t(std::min<int64_t>(best.ohi_fold, 1 << 30));
+          std::vector<bool> la_ascii;
+          auto la = Lookahead(re->nodes(), best.follow[li], &la_ascii);
+          ai.la_n = uint8_t(la.size());
+          for (size_t q = 0; q < la.size(); q++) {
+            size_t id = 0;
+            for (; id < out->la_masks.size() / 2; id++)
+              if (out->la_masks[2 * id] == la[q].first && out->la_masks[2 * id + 1] == la[q].second) break;
+            if (id == out->la_masks.size() / 2) {
+              out->la_masks.push_back(la[q].first);
+              out->la_masks.push_back(la[q].second);
+            }
+            ai.la_cls[q] = uint8_t(id);
+          }
+          // weak (short) anchors: let the automaton match the first mandatory
+          // ASCII-only class after the literal too (patterns lit+c, c in class)
+          std::vector<char> ext_chars;
+          if (l.size() <= 3 && !la.empty() && la_ascii[0]) {
+            for (int b = 0; b < 128; b++) {
+              bool in = ((b < 64 ? la[0].first : la[0].second) >> (b & 63)) & 1;
+              if (!in) continue;
+              char lc = char((b >= 'A' && b <= 'Z') ? b + 32 : b);
+              if (std::find(ext_chars.begin(), ext_chars.end(), lc) == ext_chars.end()) ext_chars.push_back(lc);
+            }
+            if (ext_chars.size() > 40) ext_chars.clear();
+          }
+          ai.ext = ext_chars.empty() ? 0 : 1;
+          out->anchors.push_back(ai);
+          if (ext_chars.empty()) {
+            pats.push_back({l, kOutAnchor | aid});
+          } else {
+            for (char ch : ext_chars) pats.push_back({l + std::string(1, ch), kOutAnchor | aid});
+          }
+          desc += " " + l + (ai.ext ? "*" : "") + (la.empty() ? "" : "+" + std::to_string(la.size()));
         }
       } else {
         rg.anchored = 0;

@@ -36,6 +36,11 @@ enum GateMode : uint8_t {
   kGateHost = 2,      // a non-ASCII keyword: GPU treats as open, host verifies
 };
 
+// Gate redundancy: a keyword every regex match contains (ASCII case-folded,
+// and not through a (?i) 's' that U+017F could satisfy) makes MatchKeywords
+// unable to change Scan's result -- see DESIGN.md §2.1.
+bool KeywordImplied(const Regex& re, const std::string& kw_lower);
+
 struct RuleSrc {
   std::string id;
   std::string regex;  // empty: rule has no regex (never matches)
@@ -44,8 +49,12 @@ struct RuleSrc {
 
 struct AnchorInfo {
   uint32_t rule;
-  uint32_t lit_len;
-  int32_t off_lo, off_hi;  // literal start - match start, in bytes
+  uint16_t lit_len;
+  uint8_t la_n;            // mandatory classes checked right after the literal (0..4)
+  uint8_t ext;             // leading lookahead positions already matched by the automaton
+  int32_t off_lo, off_hi;  // literal start - match start, in bytes (non-special files)
+  int32_t off_hi_fold;     // the same when U+212A/U+017F/U+0130 may occur (special files)
+  uint8_t la_cls[4];       // indices into CompiledRules::la_masks
 };
 
 struct RuleGpu {  // mirrored on the device
@@ -67,6 +76,7 @@ struct CompiledRules {
   // keywords / anchors
   std::vector<std::string> keywords;  // unique lowercased ASCII keywords
   std::vector<AnchorInfo> anchors;
+  std::vector<uint64_t> la_masks;  // per lookahead class: 2 x u64 ASCII membership
   // rules
   std::vector<RuleGpu> rules;
   std::vector<uint32_t> rule_kw;  // keyword ids
@@ -74,6 +84,7 @@ struct CompiledRules {
   std::vector<std::string> rule_anchor_desc;  // debug text
   std::vector<std::unique_ptr<Regex>> regex;  // exact engines (host pass)
   uint32_t n_fullscan_rules = 0;
+  uint32_t n_redundant_gates = 0;
 
   uint32_t kw_words() const { return (uint32_t(keywords.size()) + 31) / 32; }
 };

@@ -390,7 +390,9 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     uint32_t r = c[i].rule;
     size_t j = i;
     std::vector<Window> wins;
+    bool cand_host_gate = false;
     while (j < nc && c[j].rule == r) {
+      if (c[j].flags & kCandHostGate) cand_host_gate = true;
       Window w{c[j].wlo, c[j].whi};
       if (!wins.empty() && w.lo <= wins.back().hi + 1) wins.back().hi = std::max(wins.back().hi, w.hi);
       else wins.push_back(w);
@@ -402,7 +404,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     if (!re) continue;
     if (R.path && !R.path->Match(P, path.size())) continue;                      // MatchPath :397
     if (AllowRulesAllowPath(R.allow_rules, P, path.size())) continue;            // AllowPath :403
-    if (cr_.rules[r].gate == kGateHost) {                                       // MatchKeywords :409
+    if (cr_.rules[r].gate == kGateHost ||
+        (cand_host_gate && cr_.rules[r].gate != kGateAlways)) {                   // MatchKeywords :409
       if (!lowered_done) {
         lowered = GoBytesToLower(content, size_t(len));
         lowered_done = true;

@@ -39,7 +39,7 @@ class _CGlobal(c.Structure):
 
 class _CBatch(c.Structure):
     _fields_ = [("n_files", c.c_uint32), ("host_arena", c.c_void_p), ("host_offsets", c.c_void_p),
-                ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.POINTER(c.c_char_p)),
+                ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.c_void_p),
                 ("path_lens", c.c_void_p), ("binary", c.c_void_p)]
 
 
@@ -228,12 +228,18 @@ class Scanner:
         n = len(offsets) - 1
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
-        pb = [_b(p) for p in paths]
-        parr = (c.c_char_p * max(1, n))(*pb)
-        plen = np.array([len(p) for p in pb], dtype=np.uint64) if n else np.zeros(1, np.uint64)
+        if isinstance(paths, np.ndarray) and paths.dtype == np.uint64:
+            parr, plen_ptr = paths, None  # char* table (caller keeps the strings alive)
+            paths_addr = paths.ctypes.data
+        else:
+            pb = [_b(p) for p in paths]
+            parr = (c.c_char_p * max(1, n))(*pb)
+            plen = np.array([len(p) for p in pb], dtype=np.uint64) if n else np.zeros(1, np.uint64)
+            paths_addr = c.cast(parr, c.c_void_p).value
+            plen_ptr = plen.ctypes.data
         bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
         batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
-                        dev_arena, dev_offsets, parr, plen.ctypes.data,
+                        dev_arena, dev_offsets, paths_addr, plen_ptr,
                         bin_arr.ctypes.data if bin_arr is not None else None)
         h = c.c_void_p()
         rc = self._L.tsg_scan(self._h, c.byref(batch), c.byref(h))
