@@ -17,7 +17,7 @@ struct tsg_scanner {
 };
 
 struct tsg_result {
-  std::vector<tsg::FileResult> files;
+  tsg::BatchResult files;
   tsg_stats stats;
   std::string json;
   const tsg::SecretScanner* owner;
@@ -174,15 +174,17 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
 void tsg_result_free(tsg_result* r) { delete r; }
 
 int tsg_result_file(const tsg_result* r, uint32_t file, uint32_t* kind, uint32_t* n) {
-  if (file >= r->files.size()) return -1;
-  *kind = r->files[file].kind;
-  *n = uint32_t(r->files[file].findings.size());
+  if (file >= r->files.kind.size()) return -1;
+  *kind = r->files.kind[file];
+  const auto* v = r->files.Findings(file);
+  *n = v ? uint32_t(v->size()) : 0;
   return 0;
 }
 
 int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_finding* out) {
-  if (file >= r->files.size() || k >= r->files[file].findings.size()) return -1;
-  const auto& f = r->files[file].findings[k];
+  const auto* v = file < r->files.kind.size() ? r->files.Findings(file) : nullptr;
+  if (!v || k >= v->size()) return -1;
+  const auto& f = (*v)[k];
   out->rule_index = f.rule;
   out->start_line = f.start_line;
   out->end_line = f.end_line;
@@ -193,8 +195,9 @@ int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_findi
 }
 
 int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out) {
-  if (file >= r->files.size() || k >= r->files[file].findings.size()) return -1;
-  const auto& f = r->files[file].findings[k];
+  const auto* v = file < r->files.kind.size() ? r->files.Findings(file) : nullptr;
+  if (!v || k >= v->size()) return -1;
+  const auto& f = (*v)[k];
   if (line >= f.lines.size()) return -1;
   const auto& l = f.lines[line];
   out->number = l.number;
@@ -213,12 +216,14 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
     std::string& o = r->json;
     o.reserve(256 + r->stats.findings * 512);
     o.push_back('[');
-    for (size_t i = 0; i < r->files.size(); i++) {
-      const auto& fr = r->files[i];
+    static const std::vector<tsg::FindingOut> kNone;
+    for (size_t i = 0; i < r->files.kind.size(); i++) {
+      const auto* fv = r->files.Findings(uint32_t(i));
+      const auto& findings = fv ? *fv : kNone;
       if (i) o.push_back(',');
-      o += "{\"kind\":" + std::to_string(int(fr.kind)) + ",\"findings\":[";
-      for (size_t k = 0; k < fr.findings.size(); k++) {
-        const auto& f = fr.findings[k];
+      o += "{\"kind\":" + std::to_string(int(r->files.kind[i])) + ",\"findings\":[";
+      for (size_t k = 0; k < findings.size(); k++) {
+        const auto& f = findings[k];
         const auto& R = rules[f.rule];
         if (k) o.push_back(',');
         o += "{\"RuleID\":";

@@ -211,23 +211,21 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
         uint64_t seg1 = fe < b1 ? fe : b1;
         if (seg0 < seg1) {
           uint32_t st = 0, spec = 0;
-          // warm-up: the DFA state depends only on the last max_len-1 symbols
-          for (uint64_t p = (seg0 - fs > P.warm ? seg0 - P.warm : fs); p < seg0; p++) {
-            uint32_t cl = s_cmap[P.arena[p]];
-            spec = spec > cl ? spec : cl;
-            st = T[st + cl] & ~1u;
-          }
-          // main: 16-B loads with the next block in flight.  Hot loop = class
-          // lookup + transition; blocks whose states carry outputs are replayed
-          // with emission (outputs are rare: see DESIGN.md §4.1).
-          uint64_t p = seg0 & ~uint64_t(15);
+          // warm-up starts max_len-1 bytes early: the DFA state depends only on
+          // the last max_len-1 symbols.  Bytes come from 16-B vector loads (next
+          // block in flight); the hot unrolled loop is class lookup + transition,
+          // blocks that touch the warm-up or the segment edges take the generic
+          // loop, and blocks whose states carry outputs are replayed with
+          // emission (outputs are rare: DESIGN.md §4.1).
+          const uint64_t ws = seg0 - fs > P.warm ? seg0 - P.warm : fs;
+          uint64_t p = ws & ~uint64_t(15);
           uint4 v = *reinterpret_cast<const uint4*>(P.arena + p);
           for (; p < seg1; p += 16) {
             uint4 nv = *reinterpret_cast<const uint4*>(P.arena + p + 16);  // arena is padded
-            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
             const uint32_t st0 = st;
             uint32_t any = 0;
             if (p >= seg0 && p + 16 <= seg1) {
+              const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
               nl += nl_in_word(v.x) + nl_in_word(v.y) + nl_in_word(v.z) + nl_in_word(v.w);
 #pragma unroll
               for (int k = 0; k < 16; k++) {
@@ -238,25 +236,30 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
                 st = e & ~1u;
               }
             } else {
-              for (int k = 0; k < 16; k++) {
-                if (p + k < seg0 || p + k >= seg1) continue;
-                uint32_t b = P.arena[p + k];
-                nl += (b == '\n');
+              for (uint32_t k = 0; k < 16; k++) {
+                uint64_t q = p + k;
+                if (q < ws || q >= seg1) continue;
+                uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+                uint32_t b = (w >> ((k & 3) * 8)) & 0xFFu;
                 uint32_t cl = s_cmap[b];
                 spec = spec > cl ? spec : cl;
                 uint32_t e = T[st + cl];
-                any |= e;
                 st = e & ~1u;
+                if (q >= seg0) {
+                  nl += (b == '\n');
+                  any |= e;
+                }
               }
             }
-            if (any & 1u) {  // replay the block, emitting outputs
+            if (any & 1u) {  // replay the block from st0, emitting outputs
               st = st0;
-              for (int k = 0; k < 16; k++) {
+              for (uint32_t k = 0; k < 16; k++) {
                 uint64_t q = p + k;
-                if (q < seg0 || q >= seg1) continue;
-                uint32_t e = T[st + s_cmap[P.arena[q]]];
+                if (q < ws || q >= seg1) continue;
+                uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+                uint32_t e = T[st + s_cmap[(w >> ((k & 3) * 8)) & 0xFFu]];
                 st = e & ~1u;
-                if (e & 1u) emit_outputs(P, st, f, fs, fe, q + 1, s_hits, s_nhits);
+                if ((e & 1u) && q >= seg0) emit_outputs(P, st, f, fs, fe, q + 1, s_hits, s_nhits);
               }
             }
             v = nv;

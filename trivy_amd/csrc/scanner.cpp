@@ -583,7 +583,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   SortFindings(&out->findings, rules_);
 }
 
-bool SecretScanner::Scan(const BatchInput& in, std::vector<FileResult>* out, BatchStats* gst, HostStats* hst) {
+bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst) {
   double t0 = NowMs();
   HostStats hs;
   std::vector<Candidate> cands;
@@ -609,10 +609,12 @@ bool SecretScanner::Scan(const BatchInput& in, std::vector<FileResult>* out, Bat
   return true;
 }
 
-void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, std::vector<FileResult>* out,
+void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, BatchResult* out,
                              HostStats* hs) const {
   std::vector<Candidate>& cands = *cands_p;
-  out->assign(in.n_files, FileResult());
+  out->kind.assign(in.n_files, uint8_t(kNoFindings));
+  out->found_files.clear();
+  out->found.clear();
   double t1 = NowMs();
   // Global allow path (scanner.go:381-386) for every file
   std::vector<uint8_t> allowed(in.n_files, 0);
@@ -633,7 +635,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     }
   }
   for (uint32_t f = 0; f < in.n_files; f++)
-    if (allowed[f]) (*out)[f].kind = kAllowedPath;
+    if (allowed[f]) out->kind[f] = uint8_t(kAllowedPath);
   double t2 = NowMs();
   std::sort(cands.begin(), cands.end(), [](const Candidate& a, const Candidate& b) {
     if (a.file != b.file) return a.file < b.file;
@@ -645,6 +647,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     if (i == 0 || cands[i].file != cands[i - 1].file) starts.push_back(i);
   starts.push_back(cands.size());
   size_t nf = starts.size() - 1;
+  std::vector<FileResult> tmp(nf);
   ParallelFor(nf, host_threads_, [&](size_t k) {
     size_t a = starts[k], b = starts[k + 1];
     uint32_t f = cands[a].file;
@@ -653,15 +656,21 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
     uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
     ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string(p, pn), in.binary && in.binary[f], &cands[a],
-             b - a, &(*out)[f]);
+             b - a, &tmp[k]);
   });
+  for (size_t k = 0; k < nf; k++) {
+    if (tmp[k].kind != kHasFindings) continue;
+    uint32_t f = cands[starts[k]].file;
+    out->kind[f] = uint8_t(kHasFindings);
+    out->found_files.push_back(f);
+    out->found.push_back(std::move(tmp[k].findings));
+  }
   double t3 = NowMs();
   hs->ms_allow = t2 - t1;
   hs->ms_exact = t3 - t2;
   hs->candidates = cands.size();
   hs->files_with_candidates = nf;
-  hs->findings = 0;
-  for (auto& r : *out) hs->findings += r.findings.size();
+  hs->findings = out->n_findings();
 }
 
 }  // namespace tsg

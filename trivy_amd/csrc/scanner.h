@@ -8,6 +8,7 @@
 // blocks (:237-275, :419-425), censoring (:431-436, :465-473), findings
 // (:438-446, :475-558) and the final sort (:452-457).
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -62,6 +63,23 @@ struct FileResult {
   std::vector<FindingOut> findings;
 };
 
+// Per-batch result, sparse: a kind byte per file, findings only where present.
+struct BatchResult {
+  std::vector<uint8_t> kind;              // FileKind per file
+  std::vector<uint32_t> found_files;      // ascending
+  std::vector<std::vector<FindingOut>> found;
+  const std::vector<FindingOut>* Findings(uint32_t f) const {
+    auto it = std::lower_bound(found_files.begin(), found_files.end(), f);
+    if (it == found_files.end() || *it != f) return nullptr;
+    return &found[size_t(it - found_files.begin())];
+  }
+  uint64_t n_findings() const {
+    uint64_t n = 0;
+    for (auto& v : found) n += v.size();
+    return n;
+  }
+};
+
 struct BatchInput {
   uint32_t n_files = 0;
   const uint8_t* host_arena = nullptr;  // required: the exact pass reads it
@@ -86,10 +104,9 @@ class SecretScanner {
   bool ok() const { return compiled_ok_ && (no_engine_ || (engine_ && engine_->ok())); }
   const std::string& error() const { return err_; }
 
-  bool Scan(const BatchInput& in, std::vector<FileResult>* out, BatchStats* gst, HostStats* hst);
+  bool Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst);
   // The exact host tail over a given candidate list (what Scan runs after the GPU).
-  void HostTail(const BatchInput& in, std::vector<Candidate>* cands, std::vector<FileResult>* out,
-                HostStats* hs) const;
+  void HostTail(const BatchInput& in, std::vector<Candidate>* cands, BatchResult* out, HostStats* hs) const;
   // Global.AllowPath (scanner.go:57-59)
   bool AllowPath(const uint8_t* p, size_t n) const;
 
