@@ -63,6 +63,9 @@ class GpuEngine {
   void* d_trans_ = nullptr;
   bool wide_table_ = false;
   uint32_t cls_fold_ = 0, cls_i_ = 0, cls_k_ = 0, cls_s_ = 0, div_magic_ = 0;
+  void* d_tabs_ = nullptr;
+  uint32_t diag_mode_ = 0;
+  uint32_t tabs_bytes_ = 0, tab_out_off_ = 0, tab_out_items_ = 0, tab_anchors_ = 0, tab_la_ = 0;
   uint32_t* d_out_off_ = nullptr;
   uint32_t* d_out_items_ = nullptr;
   AnchorInfo* d_anchors_ = nullptr;

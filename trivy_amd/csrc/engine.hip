@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "engine.h"
@@ -53,6 +54,9 @@ struct ScanParams {
   uint32_t cls_fold;          // class id of the fold-lead bytes (largest id)
   uint32_t cls_i, cls_k, cls_s;
   uint32_t div_magic;         // ceil(2^32 / n_classes): state index = umulhi(entry, magic)
+  uint32_t diag_mode;         // TSG_DIAG_SCAN=1: skip emission (timing diagnostics only)
+  const void* tabs;           // packed output tables for LDS staging
+  uint32_t tabs_bytes, tab_out_off, tab_out_items, tab_anchors, tab_la;
   uint32_t* kwbits;
   uint32_t* flags;            // per file: bit0 fold rune seen, bit1 U+017F seen
   uint16_t* nl;
@@ -72,15 +76,32 @@ __global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_fi
   }
 }
 
+struct EmitTabs {  // output tables (LDS when they fit, else global)
+  const uint32_t* out_off;
+  const uint32_t* out_items;
+  const AnchorInfo* anchors;
+  const uint64_t* la;
+};
+
+__device__ __forceinline__ uint32_t byte_of(uint4 a, uint4 b, uint32_t i) {  // byte i of the 32-B window a|b
+  uint4 x = i < 16 ? a : b;
+  uint32_t j = i & 15;
+  uint32_t w = j < 8 ? (j < 4 ? x.x : x.y) : (j < 12 ? x.z : x.w);
+  return (w >> ((j & 3) * 8)) & 0xFFu;
+}
+
 // Rare path: outputs of the DFA state whose table row starts at element `st`,
 // for a pattern ending at byte `end` (exclusive).  Keywords set the file's
-// gate bit; anchors pass the lookahead filter and are staged in LDS.
-__device__ __forceinline__ void emit_outputs(const ScanParams& P, uint32_t st, uint32_t f, uint64_t fs, uint64_t fe,
-                                             uint64_t end, uint32_t* s_hits, uint32_t* s_nhits) {
+// gate bit; anchors pass the lookahead filter and are staged in LDS.  When
+// `win` is set, the bytes after `end` are read from the 32-B register window
+// starting at `wbase` (v|nv) instead of memory.
+__device__ __forceinline__ void emit_outputs(const ScanParams& P, const EmitTabs& E, uint32_t st, uint32_t f,
+                                             uint64_t fs, uint64_t fe, uint64_t end, uint32_t* s_hits,
+                                             uint32_t* s_nhits, bool win, uint64_t wbase, uint4 v, uint4 nv) {
   uint32_t sidx = __umulhi(st, P.div_magic);
-  uint32_t a = P.out_off[sidx], b = P.out_off[sidx + 1];
+  uint32_t a = E.out_off[sidx], b = E.out_off[sidx + 1];
   for (uint32_t j = a; j < b; j++) {
-    uint32_t item = P.out_items[j];
+    uint32_t item = E.out_items[j];
     uint32_t id = item & 0x0FFFFFFFu;
     if ((item >> 28) == 0) {  // keyword: set the file's gate bit once
       uint32_t* w = &P.kwbits[uint64_t(f) * P.kw_words + (id >> 5)];
@@ -88,7 +109,7 @@ __device__ __forceinline__ void emit_outputs(const ScanParams& P, uint32_t st, u
       if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
       continue;
     }
-    const AnchorInfo& an = P.anchors[id];
+    const AnchorInfo& an = E.anchors[id];
     const uint32_t la_n = an.la_n, ext = an.ext;
     uint32_t lac;
     __builtin_memcpy(&lac, an.la_cls, 4);
@@ -100,9 +121,9 @@ __device__ __forceinline__ void emit_outputs(const ScanParams& P, uint32_t st, u
         pass = false;
         break;
       }
-      uint32_t c = P.arena[pos];
+      uint32_t c = win ? byte_of(v, nv, uint32_t(pos - wbase)) : uint32_t(P.arena[pos]);
       if (c >= 0x80) break;  // multi-byte rune: positions no longer align, accept
-      uint64_t m = P.la[2 * ((lac >> (8 * q)) & 0xFFu) + (c >> 6)];
+      uint64_t m = E.la[2 * ((lac >> (8 * q)) & 0xFFu) + (c >> 6)];
       if (!((m >> (c & 63)) & 1)) {
         pass = false;
         break;
@@ -133,9 +154,10 @@ __device__ __forceinline__ void emit_outputs(const ScanParams& P, uint32_t st, u
 // bytes.ToLower; U+017F folds with 's' under (?i) (used for anchors only;
 // the file is flagged so the host re-checks its keyword gates).
 template <typename TT>
-__device__ __forceinline__ uint32_t careful_segment(const ScanParams& P, const TT* T, const uint8_t* cmap,
-                                                    uint32_t f, uint64_t fs, uint64_t fe, uint64_t seg0,
-                                                    uint64_t seg1, uint32_t* s_hits, uint32_t* s_nhits) {
+__device__ __forceinline__ uint32_t careful_segment(const ScanParams& P, const EmitTabs& E, const TT* T,
+                                                    const uint8_t* cmap, uint32_t f, uint64_t fs, uint64_t fe,
+                                                    uint64_t seg0, uint64_t seg1, uint32_t* s_hits,
+                                                    uint32_t* s_nhits) {
   uint64_t w = seg0 - fs > 3ull * P.warm ? seg0 - 3ull * P.warm : fs;
   uint32_t st = 0, skip = 0, fl = 0;
   for (uint64_t p = w; p < seg1; p++) {
@@ -163,7 +185,8 @@ __device__ __forceinline__ uint32_t careful_segment(const ScanParams& P, const T
     }
     uint32_t e = T[st + cls];
     st = e & ~1u;
-    if ((e & 1u) && p >= seg0) emit_outputs(P, st, f, fs, fe, p + 1 + skip, s_hits, s_nhits);
+    if ((e & 1u) && p >= seg0)
+      emit_outputs(P, E, st, f, fs, fe, p + 1 + skip, s_hits, s_nhits, false, 0, uint4{}, uint4{});
   }
   return fl;
 }
@@ -184,17 +207,34 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + tbytes + 256);
   uint32_t* s_nhits = s_hits + 3 * kHitBuf;
   uint32_t* s_base = s_nhits + 1;
+  uint8_t* s_tabs = reinterpret_cast<uint8_t*>(s_nhits + 4);  // 16-B aligned (see host lds_bytes_)
   const int tid = threadIdx.x;
   if (kLdsTable) {
     const uint4* src = reinterpret_cast<const uint4*>(P.trans);
     uint4* dst = reinterpret_cast<uint4*>(s_trans);
     size_t n16 = tbytes / 16;
     for (size_t i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
+    // output tables: out_off | out_items | anchors | la  (sizes from the host, 16-B padded)
+    const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
+    uint4* d = reinterpret_cast<uint4*>(s_tabs);
+    for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
   }
   for (int i = tid; i < 256; i += blockDim.x) s_cmap[i] = P.cmap[i];
   if (tid == 0) *s_nhits = 0;
   __syncthreads();
   const TT* T = kLdsTable ? s_trans : reinterpret_cast<const TT*>(P.trans);
+  EmitTabs E;
+  if (kLdsTable) {
+    E.out_off = reinterpret_cast<const uint32_t*>(s_tabs + P.tab_out_off);
+    E.out_items = reinterpret_cast<const uint32_t*>(s_tabs + P.tab_out_items);
+    E.anchors = reinterpret_cast<const AnchorInfo*>(s_tabs + P.tab_anchors);
+    E.la = reinterpret_cast<const uint64_t*>(s_tabs + P.tab_la);
+  } else {
+    E.out_off = P.out_off;
+    E.out_items = P.out_items;
+    E.anchors = P.anchors;
+    E.la = P.la;
+  }
   const uint32_t cls_fold = P.cls_fold;
 
   for (uint64_t tile = blockIdx.x; tile * blockDim.x < P.n_chunks; tile += gridDim.x) {
@@ -251,7 +291,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
                 }
               }
             }
-            if (any & 1u) {  // replay the block from st0, emitting outputs
+            if ((any & 1u) && P.diag_mode == 0) {  // replay the block from st0, emitting outputs
               st = st0;
               for (uint32_t k = 0; k < 16; k++) {
                 uint64_t q = p + k;
@@ -259,14 +299,14 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
                 uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
                 uint32_t e = T[st + s_cmap[(w >> ((k & 3) * 8)) & 0xFFu]];
                 st = e & ~1u;
-                if ((e & 1u) && q >= seg0) emit_outputs(P, st, f, fs, fe, q + 1, s_hits, s_nhits);
+                if ((e & 1u) && q >= seg0) emit_outputs(P, E, st, f, fs, fe, q + 1, s_hits, s_nhits, true, p, v, nv);
               }
             }
             v = nv;
           }
           if (spec >= cls_fold) {
             // a fold-lead byte was seen: redo the segment on the careful path
-            uint32_t fl = careful_segment<TT>(P, T, s_cmap, f, fs, fe, seg0, seg1, s_hits, s_nhits);
+            uint32_t fl = careful_segment<TT>(P, E, T, s_cmap, f, fs, fe, seg0, seg1, s_hits, s_nhits);
             if (fl) {
               uint32_t old = atomicOr(&P.flags[f], fl);
               if (old == 0) {
@@ -502,6 +542,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     return;
   }
   for (auto& e : ev_) hipEventCreate(&e);
+  if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
   n_states_ = cr.n_states;
   n_classes_ = cr.n_classes;
   max_pat_len_ = cr.max_pat_len;
@@ -570,7 +611,28 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     err_ = "hipMalloc counters";
     return;
   }
-  size_t rest = 256 + size_t(3 * kHitBuf + 4) * 4;
+  // packed output tables (staged into LDS next to the DFA)
+  {
+    auto pad = [](std::vector<uint8_t>& v) { v.resize((v.size() + 15) & ~size_t(15), 0); };
+    std::vector<uint8_t> tb;
+    auto put = [&](const void* src, size_t n) {
+      size_t at = tb.size();
+      tb.resize(at + n);
+      if (n) std::memcpy(&tb[at], src, n);
+      pad(tb);
+      return uint32_t(at);
+    };
+    tab_out_off_ = put(cr.out_off.data(), cr.out_off.size() * 4);
+    tab_out_items_ = put(cr.out_items.data(), cr.out_items.size() * 4);
+    tab_anchors_ = put(cr.anchors.data(), cr.anchors.size() * sizeof(AnchorInfo));
+    tab_la_ = put(la.data(), la.size() * 8);
+    if (tb.empty()) tb.assign(16, 0);
+    tabs_bytes_ = uint32_t(tb.size());
+    uint8_t* d = nullptr;
+    if (!Upload(&err_, &d, tb.data(), tb.size())) return;
+    d_tabs_ = d;
+  }
+  size_t rest = 256 + size_t(3 * kHitBuf) * 4 + 16 + tabs_bytes_;
   table_in_lds_ = tbytes + rest <= 150 * 1024;
   lds_bytes_ = (table_in_lds_ ? tbytes : 0) + rest;
   const void* fn = wide_table_ ? (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint32_t, true>)
@@ -582,7 +644,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
+  void* ps[] = {d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
                 d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
@@ -662,6 +724,13 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.cls_k = cls_k_;
     sp.cls_s = cls_s_;
     sp.div_magic = div_magic_;
+    sp.diag_mode = diag_mode_;
+    sp.tabs = d_tabs_;
+    sp.tabs_bytes = tabs_bytes_;
+    sp.tab_out_off = tab_out_off_;
+    sp.tab_out_items = tab_out_items_;
+    sp.tab_anchors = tab_anchors_;
+    sp.tab_la = tab_la_;
     sp.n_states = n_states_;
     sp.n_classes = n_classes_;
     sp.warm = max_pat_len_ > 0 ? max_pat_len_ - 1 : 0;

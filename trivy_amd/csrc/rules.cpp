@@ -723,14 +723,15 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
           // weak (short) anchors: let the automaton match the first mandatory
           // ASCII-only class after the literal too (patterns lit+c, c in class)
           std::vector<char> ext_chars;
-          if (l.size() <= 3 && !la.empty() && la_ascii[0]) {
+          if (!la.empty() && la_ascii[0]) {
             for (int b = 0; b < 128; b++) {
               bool in = ((b < 64 ? la[0].first : la[0].second) >> (b & 63)) & 1;
               if (!in) continue;
               char lc = char((b >= 'A' && b <= 'Z') ? b + 32 : b);
               if (std::find(ext_chars.begin(), ext_chars.end(), lc) == ext_chars.end()) ext_chars.push_back(lc);
             }
-            if (ext_chars.size() > 40) ext_chars.clear();
+            // short literals take any class up to 40 chars; longer ones only small classes
+            if (ext_chars.size() > (l.size() <= 3 ? 40u : 4u)) ext_chars.clear();
           }
           ai.ext = ext_chars.empty() ? 0 : 1;
           out->anchors.push_back(ai);
