@@ -55,6 +55,10 @@ const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k);
 struct tsg_batch;
 struct tsg_result;
 int tsg_debug_host_tail(const struct tsg_global* g, const struct tsg_batch* b, struct tsg_result** out);
+/* The same tail over caller-supplied candidates (40-B records as written by a
+ * GPU run with TSG_DUMP_CANDS=<file>): profiles the exact pass without a GPU. */
+int tsg_debug_host_tail_cands(const struct tsg_global* g, const struct tsg_batch* b, const void* cands,
+                              uint64_t n_cands, struct tsg_result** out);
 
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);

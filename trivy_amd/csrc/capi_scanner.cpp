@@ -365,6 +365,31 @@ const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k) {
 // Go's bytes.ToLower, with the whole file as the start window.  This is NOT a
 // product path (tsg_scan always runs the GPU kernels first); it lets the CPU
 // test-suite check the exact tail against the oracle.
+namespace {
+int RunDebugTail(std::unique_ptr<tsg::SecretScanner> sc, const tsg_batch* b, std::vector<tsg::Candidate>* cands,
+                 tsg_result** out) {
+  tsg::BatchInput in;
+  in.n_files = b->n_files;
+  in.host_arena = b->host_arena;
+  in.host_offsets = b->host_offsets;
+  in.paths = b->paths;
+  in.path_lens = b->path_lens;
+  in.binary = b->binary;
+  std::unique_ptr<tsg_result> r(new tsg_result());
+  tsg::HostStats hs;
+  sc->HostTail(in, cands, &r->files, &hs);
+  std::memset(&r->stats, 0, sizeof(r->stats));
+  r->stats.findings = hs.findings;
+  r->stats.candidates = hs.candidates;
+  r->stats.ms_host_allow_path = hs.ms_allow;
+  r->stats.ms_host_exact = hs.ms_exact;
+  r->owner = sc.get();
+  r->debug_owner = std::move(sc);
+  *out = r.release();
+  return 0;
+}
+}  // namespace
+
 extern "C" int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_result** out) {
   std::string err;
   std::vector<tsg::RuleSpec> rules;
@@ -394,20 +419,34 @@ extern "C" int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_
       cands.push_back({f, r, 0, int64_t(fe - fs), 0});
     }
   }
-  tsg::BatchInput in;
-  in.n_files = b->n_files;
-  in.host_arena = b->host_arena;
-  in.host_offsets = b->host_offsets;
-  in.paths = b->paths;
-  in.path_lens = b->path_lens;
-  in.binary = b->binary;
-  std::unique_ptr<tsg_result> r(new tsg_result());
-  tsg::HostStats hs;
-  sc->HostTail(in, &cands, &r->files, &hs);
-  std::memset(&r->stats, 0, sizeof(r->stats));
-  r->stats.findings = hs.findings;
-  r->owner = sc.get();
-  r->debug_owner = std::move(sc);
-  *out = r.release();
-  return 0;
+  return RunDebugTail(std::move(sc), b, &cands, out);
+}
+
+// Host tail over caller-supplied candidates (e.g. dumped from a GPU run with
+// TSG_DUMP_CANDS): profiles the exact pass on CPU-only machines.
+extern "C" int tsg_debug_host_tail_cands(const tsg_global* g, const tsg_batch* b, const void* cands,
+                                         uint64_t n_cands, tsg_result** out) {
+  std::string err;
+  std::vector<tsg::RuleSpec> rules;
+  std::vector<tsg::AllowRuleSpec> allow;
+  std::vector<std::unique_ptr<tsg::Regex>> exclude;
+  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
+      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
+    tsg::SetError(err);
+    return -1;
+  }
+  std::unique_ptr<tsg::SecretScanner> sc(
+      new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), -1, &err));
+  if (!sc->ok()) {
+    tsg::SetError(err);
+    return -2;
+  }
+  std::vector<tsg::Candidate> cv(n_cands);
+  if (n_cands) std::memcpy(cv.data(), cands, n_cands * sizeof(tsg::Candidate));
+  for (const auto& c : cv)
+    if (c.file >= b->n_files || c.rule >= sc->rules().size()) {
+      tsg::SetError("candidate out of range");
+      return -3;
+    }
+  return RunDebugTail(std::move(sc), b, &cv, out);
 }

@@ -10,7 +10,7 @@
 
 namespace tsg {
 
-constexpr uint32_t kChunk = 512;  // bytes per lane-chunk in the scan kernel
+constexpr uint32_t kChunk = 1024;  // bytes per lane-chunk in the scan kernel
 
 constexpr uint32_t kCandHostGate = 1;  // keyword bits may over-approximate (file holds U+017F)
 
@@ -62,7 +62,7 @@ class GpuEngine {
   uint8_t* d_cmap_ = nullptr;
   void* d_trans_ = nullptr;
   bool wide_table_ = false;
-  uint32_t cls_fold_ = 0, cls_i_ = 0, cls_k_ = 0, cls_s_ = 0, div_magic_ = 0;
+  uint32_t thr_ = 0, fold_entry_ = 0, cls_i_ = 0, cls_k_ = 0, cls_s_ = 0, div_magic_ = 0;
   void* d_tabs_ = nullptr;
   uint32_t diag_mode_ = 0;
   uint32_t tabs_bytes_ = 0, tab_out_off_ = 0, tab_out_items_ = 0, tab_anchors_ = 0, tab_la_ = 0;
@@ -91,6 +91,7 @@ class GpuEngine {
   uint32_t* d_counters_ = nullptr;  // [0]=hits [1]=cands [2]=special [3]=hit overflow [4]=cand overflow
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
+  void* d_params_ = nullptr; size_t cap_params_ = 0;
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
 };
 

@@ -26,7 +26,11 @@ namespace tsg {
 namespace {
 
 constexpr int kScanThreads = 1024;
-constexpr int kHitBuf = 2048;  // records per workgroup LDS staging buffer
+constexpr int kScanWaves = kScanThreads / 64;
+constexpr int kQueue = 320;    // per-wave replay queue (entries): kFlushAt + 4 * 64 - 1 fit
+constexpr int kFlushAt = 64;   // drain when this many blocks wait (each iteration adds <= 64)
+constexpr int kGroup = 4;      // 16-B blocks per load group (64 B per lane, two groups in flight)
+constexpr int kWaveHits = 160; // per-wave LDS hit records
 
 #define HIP_OK(x)                                                   \
   do {                                                              \
@@ -44,17 +48,18 @@ struct ScanParams {
   uint32_t n_files;
   const uint32_t* chunk_file;
   uint64_t n_chunks;
-  const uint8_t* cmap;        // byte -> class; the fold-lead bytes C4/E2/C5 -> class n_cls_real
-  const void* trans;          // entry = next_state * n_classes | output flag (bit 0)
-  const uint32_t* out_off;
+  const uint8_t* cmap;        // byte -> class; the fold-lead bytes C4/E2/C5 -> the fold column
+  const void* trans;          // entry = next_state * n_classes (element offset of the target row)
+  const uint32_t* out_off;    // per (renumbered) state
   const uint32_t* out_items;
   const AnchorInfo* anchors;
   const uint64_t* la;         // lookahead ASCII masks (2 x u64 each)
-  uint32_t n_states, n_classes, warm, kw_words;
-  uint32_t cls_fold;          // class id of the fold-lead bytes (largest id)
+  uint32_t n_states, n_classes, warm, warm_blocks, kw_words;
+  uint32_t thr;               // entries >= thr: target state has outputs (or is the fold root)
+  uint32_t fold_entry;        // entry of the fold root (a flagged copy of the root)
   uint32_t cls_i, cls_k, cls_s;
   uint32_t div_magic;         // ceil(2^32 / n_classes): state index = umulhi(entry, magic)
-  uint32_t diag_mode;         // TSG_DIAG_SCAN=1: skip emission (timing diagnostics only)
+  uint32_t diag_mode;         // TSG_DIAG_SCAN: 1 skip replay/emission, 2 also skip the DFA (timing only)
   const void* tabs;           // packed output tables for LDS staging
   uint32_t tabs_bytes, tab_out_off, tab_out_items, tab_anchors, tab_la;
   uint32_t* kwbits;
@@ -76,11 +81,18 @@ __global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_fi
   }
 }
 
-struct EmitTabs {  // output tables (LDS when they fit, else global)
+struct EmitTabs {  // output tables (LDS when they fit, else global) + the wave's hit buffer (LDS)
   const uint32_t* out_off;
-  const uint32_t* out_items;
+  const uint32_t* out_items;  // kind (2 bits) | pattern length (10) | id (20), see DevItem()
   const AnchorInfo* anchors;
   const uint64_t* la;
+  uint32_t* hbuf;  // kWaveHits records of 3 words
+  uint32_t* hcnt;  // records in hbuf (beyond kWaveHits they went straight to global)
+};
+
+struct ReplayEntry {  // a 16-B block whose DFA path reaches a flagged state
+  uint32_t blk;       // block start / 16 (arenas < 64 GiB, checked on the host)
+  uint32_t st;        // entry (state) before the block
 };
 
 __device__ __forceinline__ uint32_t byte_of(uint4 a, uint4 b, uint32_t i) {  // byte i of the 32-B window a|b
@@ -90,25 +102,43 @@ __device__ __forceinline__ uint32_t byte_of(uint4 a, uint4 b, uint32_t i) {  // 
   return (w >> ((j & 3) * 8)) & 0xFFu;
 }
 
-// Rare path: outputs of the DFA state whose table row starts at element `st`,
-// for a pattern ending at byte `end` (exclusive).  Keywords set the file's
-// gate bit; anchors pass the lookahead filter and are staged in LDS.  When
-// `win` is set, the bytes after `end` are read from the 32-B register window
-// starting at `wbase` (v|nv) instead of memory.
-__device__ __forceinline__ void emit_outputs(const ScanParams& P, const EmitTabs& E, uint32_t st, uint32_t f,
-                                             uint64_t fs, uint64_t fe, uint64_t end, uint32_t* s_hits,
-                                             uint32_t* s_nhits, bool win, uint64_t wbase, uint4 v, uint4 nv) {
-  uint32_t sidx = __umulhi(st, P.div_magic);
-  uint32_t a = E.out_off[sidx], b = E.out_off[sidx + 1];
+__device__ __forceinline__ uint4 load16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Outputs of the state with entry `e`, for a pattern ending at byte `end`
+// (exclusive) in file [fs, fe).  The scan does not restart the automaton at
+// file starts: an Aho-Corasick state reports every pattern that is a suffix
+// of the stream, so the file's own outputs are exactly those no longer than
+// end - fs.  Keywords set the file's gate bit; anchors pass the lookahead
+// filter and go to the wave's LDS hit buffer.  When `win` is set, the bytes
+// after `end` come from the 32-B register window starting at `wbase`.
+constexpr uint32_t kEmitKeywords = 1, kEmitAnchors = 2, kEmitAll = 3;
+
+// `filter`: drop outputs longer than end - fs (the main stream, which runs
+// across file starts); off for careful passes, which start inside the file
+// and count fold runes as one symbol of 2-3 bytes.
+__device__ __forceinline__ void emit_outputs(const ScanParams& P, const EmitTabs& E, uint32_t e, uint32_t f,
+                                             uint64_t fs, uint64_t fe, uint64_t end, bool win, uint64_t wbase,
+                                             uint4 v, uint4 nv, uint32_t kinds = kEmitAll, bool filter = true) {
+  const uint32_t sidx = __umulhi(e, P.div_magic);
+  const uint32_t a = E.out_off[sidx], b = E.out_off[sidx + 1];
   for (uint32_t j = a; j < b; j++) {
-    uint32_t item = E.out_items[j];
-    uint32_t id = item & 0x0FFFFFFFu;
-    if ((item >> 28) == 0) {  // keyword: set the file's gate bit once
+    const uint32_t item = E.out_items[j];
+    const uint32_t id = item & 0xFFFFFu;
+    if (filter && end - fs < ((item >> 20) & 0x3FFu)) continue;  // starts in an earlier file
+    if ((item >> 30) == 0) {  // keyword: set the file's gate bit once
+      if (!(kinds & kEmitKeywords)) continue;
       uint32_t* w = &P.kwbits[uint64_t(f) * P.kw_words + (id >> 5)];
-      uint32_t bit = 1u << (id & 31);
+      const uint32_t bit = 1u << (id & 31);
       if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
       continue;
     }
+    if (!(kinds & kEmitAnchors)) continue;
     const AnchorInfo& an = E.anchors[id];
     const uint32_t la_n = an.la_n, ext = an.ext;
     uint32_t lac;
@@ -116,31 +146,30 @@ __device__ __forceinline__ void emit_outputs(const ScanParams& P, const EmitTabs
     const uint64_t lit_end = end - ext;  // the automaton already matched `ext` lookahead bytes
     bool pass = true;
     for (uint32_t q = ext; q < la_n; q++) {
-      uint64_t pos = lit_end + q;
+      const uint64_t pos = lit_end + q;
       if (pos >= fe) {
         pass = false;
         break;
       }
-      uint32_t c = win ? byte_of(v, nv, uint32_t(pos - wbase)) : uint32_t(P.arena[pos]);
+      const uint32_t c = win ? byte_of(v, nv, uint32_t(pos - wbase)) : uint32_t(P.arena[pos]);
       if (c >= 0x80) break;  // multi-byte rune: positions no longer align, accept
-      uint64_t m = E.la[2 * ((lac >> (8 * q)) & 0xFFu) + (c >> 6)];
+      const uint64_t m = E.la[2 * ((lac >> (8 * q)) & 0xFFu) + (c >> 6)];
       if (!((m >> (c & 63)) & 1)) {
         pass = false;
         break;
       }
     }
     if (!pass) continue;
-    uint32_t k = atomicAdd(s_nhits, 1u);
-    uint32_t rel = uint32_t(lit_end - fs);
-    if (k < uint32_t(kHitBuf)) {
-      s_hits[3 * k + 0] = f;
-      s_hits[3 * k + 1] = rel;
-      s_hits[3 * k + 2] = id;
+    const uint32_t k = atomicAdd(E.hcnt, 1u);  // LDS; copied out once per drain
+    if (k < uint32_t(kWaveHits)) {
+      E.hbuf[3 * k + 0] = f;
+      E.hbuf[3 * k + 1] = uint32_t(lit_end - fs);
+      E.hbuf[3 * k + 2] = id;
     } else {
-      uint32_t g = atomicAdd(&P.counters[0], 1u);
+      const uint32_t g = atomicAdd(&P.counters[0], 1u);
       if (g < P.hit_cap) {
         P.hits[3ull * g + 0] = f;
-        P.hits[3ull * g + 1] = rel;
+        P.hits[3ull * g + 1] = uint32_t(lit_end - fs);
         P.hits[3ull * g + 2] = id;
       } else {
         P.counters[3] = 1;
@@ -149,80 +178,183 @@ __device__ __forceinline__ void emit_outputs(const ScanParams& P, const EmitTabs
   }
 }
 
-// Careful path for a segment holding a fold-lead byte (C4/E2/C5): the
-// multi-byte sequences U+0130 -> 'i' and U+212A -> 'k' lower to ASCII under
-// bytes.ToLower; U+017F folds with 's' under (?i) (used for anchors only;
-// the file is flagged so the host re-checks its keyword gates).
-template <typename TT>
-__device__ __forceinline__ uint32_t careful_segment(const ScanParams& P, const EmitTabs& E, const TT* T,
-                                                    const uint8_t* cmap, uint32_t f, uint64_t fs, uint64_t fe,
-                                                    uint64_t seg0, uint64_t seg1, uint32_t* s_hits,
-                                                    uint32_t* s_nhits) {
-  uint64_t w = seg0 - fs > 3ull * P.warm ? seg0 - 3ull * P.warm : fs;
-  uint32_t st = 0, skip = 0, fl = 0;
-  for (uint64_t p = w; p < seg1; p++) {
-    if (skip) {
-      skip--;
-      continue;
-    }
-    uint32_t b = P.arena[p];
-    uint32_t cls = cmap[b];
-    if (cls == P.cls_fold) {
-      cls = 0;
-      if (b == 0xC4 && p + 1 < fe && P.arena[p + 1] == 0xB0) {
-        skip = 1;
-        cls = P.cls_i;
-        if (p >= seg0) fl |= 1;
-      } else if (b == 0xE2 && p + 2 < fe && P.arena[p + 1] == 0x84 && P.arena[p + 2] == 0xAA) {
-        skip = 2;
-        cls = P.cls_k;
-        if (p >= seg0) fl |= 1;
-      } else if (b == 0xC5 && p + 1 < fe && P.arena[p + 1] == 0xBF) {
-        skip = 1;
-        cls = P.cls_s;
-        if (p >= seg0) fl |= 3;
-      }
-    }
-    uint32_t e = T[st + cls];
-    st = e & ~1u;
-    if ((e & 1u) && p >= seg0)
-      emit_outputs(P, E, st, f, fs, fe, p + 1 + skip, s_hits, s_nhits, false, 0, uint4{}, uint4{});
+// Length of the fold sequence starting at `p` (U+0130 / U+212A / U+017F), 0 if none.
+__device__ __forceinline__ uint32_t fold_len(const ScanParams& P, uint64_t p, uint64_t fe, uint32_t* cls,
+                                             uint32_t* fl) {
+  const uint8_t* a = P.arena;
+  const uint32_t b = a[p];
+  if (b == 0xC4 && p + 1 < fe && a[p + 1] == 0xB0) {
+    *cls = P.cls_i;
+    *fl = 1;
+    return 2;
   }
-  return fl;
+  if (b == 0xE2 && p + 2 < fe && a[p + 1] == 0x84 && a[p + 2] == 0xAA) {
+    *cls = P.cls_k;
+    *fl = 1;
+    return 3;
+  }
+  if (b == 0xC5 && p + 1 < fe && a[p + 1] == 0xBF) {
+    *cls = P.cls_s;
+    *fl = 3;
+    return 2;
+  }
+  return 0;
+}
+
+// Careful pass around a fold sequence at `x` (file [fs, fe)).  Under
+// bytes.ToLower U+0130 -> 'i' and U+212A -> 'k' (keywords and anchors);
+// U+017F stays itself for keywords but folds with 's' under (?i) (anchors),
+// so keywords and anchors take one pass each and the keyword bits stay exact.
+// The main loop runs the fold-lead byte as a non-pattern byte, whose outputs
+// are a subset of the true stream's; a pass restarts 3*warm+2 bytes earlier
+// (>= warm whole symbols) on the true symbol stream and emits every output
+// ending after `x` until warm plain bytes follow the last fold sequence,
+// where both streams' states agree again.  Duplicated hits are harmless (the
+// host merges windows per rule).
+template <typename TT>
+__device__ __forceinline__ void careful_fold(const ScanParams& P, const EmitTabs& E, const TT* T, const uint8_t* cmap,
+                                             uint32_t f, uint64_t fs, uint64_t fe, uint64_t x) {
+  const uint8_t* a = P.arena;
+  const uint64_t back = 3ull * P.warm + 2;
+  uint32_t fl = 0;
+  for (uint32_t pass = 0; pass < 2; pass++) {
+    const uint32_t kinds = pass == 0 ? kEmitKeywords : kEmitAnchors;
+    uint64_t p = x - fs > back ? x - back : fs;
+    uint64_t stop = x + 3 + P.warm;
+    uint32_t st = 0;
+    while (p < fe && p < stop) {
+      uint32_t cls = cmap[a[p]], flx = 0;
+      uint32_t len = fold_len(P, p, fe, &cls, &flx);
+      if (len) {
+        fl |= flx;
+        if (pass == 0 && flx == 3) cls = 0;  // U+017F: not a letter for keywords
+        if (p + len + P.warm > stop) stop = p + len + P.warm;
+      } else {
+        len = 1;
+      }
+      const uint32_t e = T[st + cls];
+      st = e;
+      p += len;
+      if (e >= P.thr && e != P.fold_entry && p > x)
+        emit_outputs(P, E, e, f, fs, fe, p, false, 0, uint4{}, uint4{}, kinds, false);
+    }
+  }
+  if (fl) {
+    const uint32_t old = atomicOr(&P.flags[f], fl);
+    if (old == 0) {
+      const uint32_t k = atomicAdd(&P.counters[2], 1u);
+      if (k < P.special_cap) P.special[k] = f;
+    }
+  }
 }
 
 // '\n' bytes in a 32-bit word (exact per byte)
 __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
-  uint32_t x = w ^ 0x0A0A0A0Au;
-  uint32_t nz = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // bit7 set <=> byte != 0
+  const uint32_t x = w ^ 0x0A0A0A0Au;
+  const uint32_t nz = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // bit7 set <=> byte != 0
   return 4u - __popc(nz & 0x80808080u);
 }
 
+// Replays queue entries [0, n) of one wave (entry `lane` and `lane + 64`):
+// the block's 16 bytes are re-read (L2/MALL-warm), each flagged position is
+// attributed to its file and its outputs are emitted.
+template <typename TT>
+__device__ __forceinline__ void drain_queue(const ScanParams& P, const EmitTabs& E, const TT* T, const uint8_t* cmap,
+                                            const ReplayEntry* Q, uint32_t n, uint32_t lane) {
+  wave_sync();
+  for (uint32_t i = lane; i < n; i += 64) {
+    const ReplayEntry r = Q[i];
+    if (P.diag_mode) continue;
+    const uint64_t rp = uint64_t(r.blk) * 16;
+    uint32_t f = P.chunk_file[rp / kChunk];  // the file holding the chunk's first byte; walk forward
+    uint64_t fs = P.off[f], fe = P.off[f + 1];
+    const uint4 v = load16(P.arena + rp), nv = load16(P.arena + rp + 16);
+    uint32_t st = r.st;
+    for (uint32_t k = 0; k < 16; k++) {
+      const uint32_t e = T[st + cmap[byte_of(v, nv, k)]];
+      st = e;
+      if (e < P.thr) continue;
+      const uint64_t q = rp + k;
+      if (q >= P.n_bytes) break;
+      while (q >= fe) {  // q < n_bytes = off[n_files]: stays in range
+        f++;
+        fs = fe;
+        fe = P.off[f + 1];
+      }
+      if (q < fs) continue;  // before the first file
+      if (e == P.fold_entry) {
+        uint32_t cls, fl;
+        if (fold_len(P, q, fe, &cls, &fl)) careful_fold<TT>(P, E, T, cmap, f, fs, fe, q);
+      } else {
+        emit_outputs(P, E, e, f, fs, fe, q + 1, true, rp, v, nv);
+      }
+    }
+  }
+  wave_sync();
+}
+
+// Copies the wave's LDS hit records to the global list (one atomic per wave).
+__device__ __forceinline__ void flush_hits(const ScanParams& P, const EmitTabs& E, uint32_t lane) {
+  wave_sync();
+  const uint32_t n_all = __builtin_amdgcn_readfirstlane(*E.hcnt);
+  const uint32_t n = n_all < uint32_t(kWaveHits) ? n_all : uint32_t(kWaveHits);
+  if (n == 0) return;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(&P.counters[0], n);
+  base = __builtin_amdgcn_readfirstlane(base);
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t g = base + i;
+    if (g < P.hit_cap) {
+      P.hits[3ull * g + 0] = E.hbuf[3 * i + 0];
+      P.hits[3ull * g + 1] = E.hbuf[3 * i + 1];
+      P.hits[3ull * g + 2] = E.hbuf[3 * i + 2];
+    } else {
+      P.counters[3] = 1;
+    }
+  }
+  wave_sync();
+  if (lane == 0) *E.hcnt = 0;
+  wave_sync();
+}
+
+// K1.  One wave owns 64 consecutive kChunk-byte chunks (one per lane) at a
+// time.  Every lane walks the same number of 16-B blocks (warm-up + chunk,
+// padded to whole load groups), so the wave stays converged.  The automaton
+// runs straight across file boundaries (outputs are attributed and filtered
+// per file at emission, see emit_outputs), so the hot body is only class
+// lookup + transition from LDS plus one max per block for the flagged test
+// (flagged states are numbered last).  Each lane loads 64 contiguous bytes
+// at a time (4 x 16-B loads on the same lines) with the next 64 in flight.
+// A block that reached a flagged state is queued in LDS (ballot + mbcnt);
+// once 64 wait, the whole wave replays 64 of them in parallel, so emission
+// costs full-width work instead of a divergent replay per block.  Anchor
+// hits gather in a per-wave LDS buffer and leave with one atomic per drain.
 template <typename TT, bool kLdsTable>
 __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  size_t tbytes = kLdsTable ? ((size_t(P.n_states) * P.n_classes * sizeof(TT) + 15) & ~size_t(15)) : 0;
+  const size_t tbytes = kLdsTable ? ((size_t(P.n_states) * P.n_classes * sizeof(TT) + 15) & ~size_t(15)) : 0;
   TT* s_trans = reinterpret_cast<TT*>(smem);
   uint8_t* s_cmap = smem + tbytes;
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(smem + tbytes + 256);
-  uint32_t* s_nhits = s_hits + 3 * kHitBuf;
-  uint32_t* s_base = s_nhits + 1;
-  uint8_t* s_tabs = reinterpret_cast<uint8_t*>(s_nhits + 4);  // 16-B aligned (see host lds_bytes_)
+  uint8_t* s_tabs = smem + tbytes + 256;
+  ReplayEntry* s_queue = reinterpret_cast<ReplayEntry*>(s_tabs + (kLdsTable ? P.tabs_bytes : 0));
+  uint32_t* s_hits = reinterpret_cast<uint32_t*>(s_queue + kScanWaves * kQueue);
+  uint32_t* s_hcnt = s_hits + kScanWaves * kWaveHits * 3;
   const int tid = threadIdx.x;
   if (kLdsTable) {
     const uint4* src = reinterpret_cast<const uint4*>(P.trans);
     uint4* dst = reinterpret_cast<uint4*>(s_trans);
-    size_t n16 = tbytes / 16;
+    const size_t n16 = tbytes / 16;
     for (size_t i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
-    // output tables: out_off | out_items | anchors | la  (sizes from the host, 16-B padded)
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(s_tabs);
     for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
   }
   for (int i = tid; i < 256; i += blockDim.x) s_cmap[i] = P.cmap[i];
-  if (tid == 0) *s_nhits = 0;
+  if (tid < kScanWaves) s_hcnt[tid] = 0;
   __syncthreads();
   const TT* T = kLdsTable ? s_trans : reinterpret_cast<const TT*>(P.trans);
+  const uint8_t* Tb = reinterpret_cast<const uint8_t*>(T);
+  const uint32_t lane = tid & 63, wave = tid >> 6;
   EmitTabs E;
   if (kLdsTable) {
     E.out_off = reinterpret_cast<const uint32_t*>(s_tabs + P.tab_out_off);
@@ -235,113 +367,93 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
     E.anchors = P.anchors;
     E.la = P.la;
   }
-  const uint32_t cls_fold = P.cls_fold;
+  E.hbuf = s_hits + wave * kWaveHits * 3;
+  E.hcnt = s_hcnt + wave;
+  ReplayEntry* Q = s_queue + wave * kQueue;
+  uint32_t qn = 0;  // wave-uniform
+  const uint32_t thr = P.thr;
+  // load groups per lane, rounded up to an even count (blocks past b1 are skipped)
+  const uint32_t ngroups = ((P.warm_blocks + kChunk / 16 + kGroup - 1) / kGroup + 1) & ~1u;
+  const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
 
-  for (uint64_t tile = blockIdx.x; tile * blockDim.x < P.n_chunks; tile += gridDim.x) {
-    uint64_t c = tile * blockDim.x + tid;
-    if (c < P.n_chunks) {
-      uint64_t b0 = c * kChunk;
-      uint64_t b1 = b0 + kChunk < P.n_bytes ? b0 + kChunk : P.n_bytes;
-      uint32_t f = P.chunk_file[c];
-      uint32_t nl = 0;
-      while (f < P.n_files) {
-        uint64_t fs = P.off[f], fe = P.off[f + 1];
-        if (fs >= b1) break;
-        uint64_t seg0 = fs > b0 ? fs : b0;
-        uint64_t seg1 = fe < b1 ? fe : b1;
-        if (seg0 < seg1) {
-          uint32_t st = 0, spec = 0;
-          // warm-up starts max_len-1 bytes early: the DFA state depends only on
-          // the last max_len-1 symbols.  Bytes come from 16-B vector loads (next
-          // block in flight); the hot unrolled loop is class lookup + transition,
-          // blocks that touch the warm-up or the segment edges take the generic
-          // loop, and blocks whose states carry outputs are replayed with
-          // emission (outputs are rare: DESIGN.md §4.1).
-          const uint64_t ws = seg0 - fs > P.warm ? seg0 - P.warm : fs;
-          uint64_t p = ws & ~uint64_t(15);
-          uint4 v = *reinterpret_cast<const uint4*>(P.arena + p);
-          for (; p < seg1; p += 16) {
-            uint4 nv = *reinterpret_cast<const uint4*>(P.arena + p + 16);  // arena is padded
-            const uint32_t st0 = st;
-            uint32_t any = 0;
-            if (p >= seg0 && p + 16 <= seg1) {
-              const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-              nl += nl_in_word(v.x) + nl_in_word(v.y) + nl_in_word(v.z) + nl_in_word(v.w);
+  for (uint64_t tile = uint64_t(blockIdx.x) * kScanWaves + wave; tile * 64 < P.n_chunks; tile += n_waves) {
+    const uint64_t c = tile * 64 + lane;
+    const bool live = c < P.n_chunks;
+    const uint64_t b0 = c * kChunk;
+    const uint64_t b1 = live ? (b0 + kChunk < P.n_bytes ? b0 + kChunk : P.n_bytes) : 0;
+    const int64_t pstart = int64_t(b0) - int64_t(P.warm_blocks) * 16;
+    uint32_t st = 0, nl = 0;
+    // loads are unconditional (clamped address) so the waits stay countable
+    auto load_group = [&](uint4* g, int64_t gp) {
 #pragma unroll
-              for (int k = 0; k < 16; k++) {
-                uint32_t cl = s_cmap[(wd[k >> 2] >> ((k & 3) * 8)) & 0xFFu];
-                spec = spec > cl ? spec : cl;
-                uint32_t e = T[st + cl];
-                any |= e;
-                st = e & ~1u;
-              }
-            } else {
-              for (uint32_t k = 0; k < 16; k++) {
-                uint64_t q = p + k;
-                if (q < ws || q >= seg1) continue;
-                uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
-                uint32_t b = (w >> ((k & 3) * 8)) & 0xFFu;
-                uint32_t cl = s_cmap[b];
-                spec = spec > cl ? spec : cl;
-                uint32_t e = T[st + cl];
-                st = e & ~1u;
-                if (q >= seg0) {
-                  nl += (b == '\n');
-                  any |= e;
-                }
-              }
+      for (int j = 0; j < kGroup; j++) {
+        const int64_t p = gp + 16 * j;
+        g[j] = load16(P.arena + ((p >= 0 && uint64_t(p) < b1) ? uint64_t(p) : 0));
+      }
+    };
+    // one group of 4 blocks: transitions, then queue the flagged blocks
+    auto do_group = [&](const uint4* g, const int64_t gp) {
+      uint32_t st0[kGroup];
+      bool flg[kGroup];
+#pragma unroll
+      for (int j = 0; j < kGroup; j++) {
+        const int64_t p = gp + 16 * j;
+        const uint4 v = g[j];
+        st0[j] = st;
+        flg[j] = false;
+        if (p >= 0 && uint64_t(p) < b1) {
+          if (P.diag_mode < 2) {
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+            uint32_t mx = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+              const uint32_t cl = s_cmap[(wd[k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+              const uint32_t e = *reinterpret_cast<const TT*>(Tb + ((st + cl) * uint32_t(sizeof(TT))));
+              mx = mx > e ? mx : e;
+              st = e;
             }
-            if ((any & 1u) && P.diag_mode == 0) {  // replay the block from st0, emitting outputs
-              st = st0;
-              for (uint32_t k = 0; k < 16; k++) {
-                uint64_t q = p + k;
-                if (q < ws || q >= seg1) continue;
-                uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
-                uint32_t e = T[st + s_cmap[(w >> ((k & 3) * 8)) & 0xFFu]];
-                st = e & ~1u;
-                if ((e & 1u) && q >= seg0) emit_outputs(P, E, st, f, fs, fe, q + 1, s_hits, s_nhits, true, p, v, nv);
-              }
-            }
-            v = nv;
+            flg[j] = uint64_t(p) >= b0 && mx >= thr;
           }
-          if (spec >= cls_fold) {
-            // a fold-lead byte was seen: redo the segment on the careful path
-            uint32_t fl = careful_segment<TT>(P, E, T, s_cmap, f, fs, fe, seg0, seg1, s_hits, s_nhits);
-            if (fl) {
-              uint32_t old = atomicOr(&P.flags[f], fl);
-              if (old == 0) {
-                uint32_t k = atomicAdd(&P.counters[2], 1u);
-                if (k < P.special_cap) P.special[k] = f;
-              }
+          if (uint64_t(p) >= b0) {
+            if (uint64_t(p) + 16 <= b1) {
+              nl += nl_in_word(v.x) + nl_in_word(v.y) + nl_in_word(v.z) + nl_in_word(v.w);
+            } else {  // the arena's last, partial block
+              for (uint32_t k = 0; uint64_t(p) + k < b1; k++) nl += byte_of(v, v, k) == '\n';
             }
           }
         }
-        if (fe > b1) break;
-        f++;
       }
-      P.nl[c] = uint16_t(nl);
-    }
-    __syncthreads();
-    uint32_t nh = *s_nhits < uint32_t(kHitBuf) ? *s_nhits : uint32_t(kHitBuf);
-    if (nh) {
-      if (tid == 0) *s_base = atomicAdd(&P.counters[0], nh);
-      __syncthreads();
-      uint32_t base = *s_base;
-      for (uint32_t i = tid; i < nh; i += blockDim.x) {
-        uint32_t g = base + i;
-        if (g < P.hit_cap) {
-          P.hits[3ull * g + 0] = s_hits[3 * i + 0];
-          P.hits[3ull * g + 1] = s_hits[3 * i + 1];
-          P.hits[3ull * g + 2] = s_hits[3 * i + 2];
-        } else {
-          P.counters[3] = 1;
+#pragma unroll
+      for (int j = 0; j < kGroup; j++) {
+        const uint64_t m = __ballot(flg[j]);
+        if (m) {  // wave-uniform
+          const uint32_t below =
+              __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+          if (flg[j]) Q[qn + below] = ReplayEntry{uint32_t(uint64_t(gp + 16 * j) >> 4), st0[j]};
+          qn += uint32_t(__popcll(m));
         }
       }
+      if (qn >= uint32_t(kFlushAt)) {  // wave-uniform; qn < kFlushAt + 4 * 64 <= kQueue
+        drain_queue<TT>(P, E, T, s_cmap, Q, qn, lane);
+        flush_hits(P, E, lane);
+        qn = 0;
+      }
+    };
+    uint4 A[kGroup], B[kGroup];
+    load_group(A, pstart);
+    load_group(B, pstart + 16 * kGroup);
+    for (uint32_t g = 0; g < ngroups; g += 2) {
+      const int64_t ga = pstart + int64_t(g) * 16 * kGroup;
+      do_group(A, ga);
+      load_group(A, ga + 2 * 16 * kGroup);  // A's registers are dead: the loads land in place
+      const int64_t gb = ga + 16 * kGroup;
+      do_group(B, gb);
+      load_group(B, gb + 2 * 16 * kGroup);
     }
-    __syncthreads();
-    if (tid == 0) *s_nhits = 0;
-    __syncthreads();
+    if (live) P.nl[c] = uint16_t(nl);
   }
+  if (qn) drain_queue<TT>(P, E, T, s_cmap, Q, qn, lane);
+  flush_hits(P, E, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -493,8 +605,7 @@ __global__ __launch_bounds__(256) void verify_kernel(NfaParams P) {
     bool acc = rg.nfa_words == 0 ||
                nfa_dispatch(rg.nfa_words, P.arena + fs, len, wlo, whi, P.nfa + rg.nfa_off);
     if (acc)
-      emit_candidate(P, f, a.rule, wlo, whi, count_nl(P, fs, fs + uint64_t(wlo)),
-                     (ff & 2u) ? kCandHostGate : 0u);
+      emit_candidate(P, f, a.rule, wlo, whi, count_nl(P, fs, fs + uint64_t(wlo)), 0u);
   }
 }
 
@@ -512,7 +623,7 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
     int64_t len = int64_t(P.off[f + 1] - fs);
     bool acc = rg.nfa_words == 0 ||
                nfa_dispatch(rg.nfa_words, P.arena + fs, len, 0, len, P.nfa + rg.nfa_off);
-    if (acc) emit_candidate(P, f, r, 0, len, 0, (P.flags[f] & 2u) ? kCandHostGate : 0u);
+    if (acc) emit_candidate(P, f, r, 0, len, 0, 0u);
   }
 }
 
@@ -554,12 +665,15 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (!cr.rules[r].anchored) fullscan_rules_.push_back(r);
   }
   n_fullscan_rules_ = uint32_t(fullscan_rules_.size());
-  // class columns: the real ones, then one for the fold-lead bytes (a copy
-  // of the "other" column 0, so the hot loop needs no branch), padded to even
-  uint32_t nc_real = n_classes_;
-  cls_fold_ = nc_real;
-  uint32_t nc = nc_real + 1;
-  if (nc & 1) nc++;
+  // Device DFA: the real class columns plus one for the fold-lead bytes
+  // C4/E2/C5.  States are renumbered: plain states first (root = 0), then
+  // states with outputs, then the fold root (a copy of the root's row that
+  // every state enters on a fold-lead byte; class 0 always returns to the
+  // root, so the stream's states are unchanged).  An entry is the element
+  // offset of the target row, so "has outputs" is entry >= thr_.
+  const uint32_t nc_real = n_classes_;
+  const uint32_t cls_fold = nc_real;
+  const uint32_t nc = nc_real + 1;
   n_classes_ = nc;
   if (nc >= 0xFF) {
     err_ = "too many keyword character classes";
@@ -568,36 +682,94 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   uint8_t cmap[256];
   for (int b = 0; b < 256; b++) {
     uint8_t m = cr.cmap[b];
-    cmap[b] = m >= kClsFoldI ? uint8_t(cls_fold_) : m;
+    cmap[b] = m >= kClsFoldI ? uint8_t(cls_fold) : m;
   }
   cls_i_ = cr.cmap['i'];
   cls_k_ = cr.cmap['k'];
   cls_s_ = cr.cmap['s'];
+  const uint32_t ns = n_states_;
+  std::vector<uint32_t> perm(ns), inv;
+  {
+    uint32_t nid = 0;
+    for (int pass = 0; pass < 2; pass++)
+      for (uint32_t s = 0; s < ns; s++) {
+        bool out = cr.out_off[s + 1] > cr.out_off[s];
+        if (out == (pass == 1)) perm[s] = nid++;
+      }
+    inv.resize(ns);
+    for (uint32_t s = 0; s < ns; s++) inv[perm[s]] = s;
+    uint32_t n_plain = 0;
+    for (uint32_t s = 0; s < ns; s++) n_plain += cr.out_off[s + 1] == cr.out_off[s];
+    if (perm[0] != 0) {
+      err_ = "AC root has outputs";
+      return;
+    }
+    thr_ = n_plain * nc;
+  }
+  const uint32_t nsd = ns + 1;  // + fold root
+  n_states_ = nsd;
+  fold_entry_ = ns * nc;
   div_magic_ = uint32_t((uint64_t(1) << 32) / nc + 1);
-  // entry = next_state * nc | output flag (bit 0); nc is even so bit 0 is free
-  wide_table_ = uint64_t(n_states_) * nc >= 0x10000;
+  wide_table_ = uint64_t(nsd) * nc > 0x10000;
   std::vector<uint8_t> tbuf;
   size_t esz = wide_table_ ? 4 : 2;
-  size_t tbytes = (size_t(n_states_) * nc * esz + 15) & ~size_t(15);
+  size_t tbytes = (size_t(nsd) * nc * esz + 15) & ~size_t(15);
   tbuf.assign(tbytes + 16, 0);
-  for (size_t st = 0; st < n_states_; st++)
+  for (uint32_t ds = 0; ds < nsd; ds++) {
+    uint32_t src_state = ds < ns ? inv[ds] : 0;
     for (uint32_t col = 0; col < nc; col++) {
-      uint32_t src = col < nc_real ? col : 0;
-      uint32_t e = cr.trans[st * nc_real + src];
-      uint32_t v = (e & 0x7FFFu) * nc | ((e & kAcOutFlag) ? 1u : 0u);
-      size_t i = st * nc + col;
+      uint32_t v;
+      if (col == cls_fold) {
+        v = fold_entry_;
+      } else {
+        uint32_t e = cr.trans[size_t(src_state) * nc_real + col];
+        uint32_t tgt = e & 0x7FFFu;
+        if (col == 0 && tgt != 0) {
+          err_ = "AC class 0 does not return to the root";
+          return;
+        }
+        v = perm[tgt] * nc;
+      }
+      size_t i = size_t(ds) * nc + col;
       if (wide_table_) std::memcpy(&tbuf[i * 4], &v, 4);
       else {
         uint16_t h = uint16_t(v);
         std::memcpy(&tbuf[i * 2], &h, 2);
       }
     }
+  }
+  // output lists in the renumbered order (+ an empty list for the fold root)
+  // device item = kind (2 bits) | pattern length in bytes (10) | id (20): the
+  // length lets K1 drop outputs that start before the file (emit_outputs)
+  std::vector<uint32_t> out_off(nsd + 1, 0), out_items;
+  for (uint32_t ds = 0; ds < ns; ds++) {
+    uint32_t s = inv[ds];
+    out_off[ds] = uint32_t(out_items.size());
+    for (uint32_t j = cr.out_off[s]; j < cr.out_off[s + 1]; j++) {
+      const uint32_t item = cr.out_items[j], kind = item >> 28, id = item & 0x0FFFFFFFu;
+      size_t len;
+      if (kind == (kOutKeyword >> 28)) {
+        len = cr.keywords[id].size();
+      } else if (kind == (kOutAnchor >> 28)) {
+        len = size_t(cr.anchors[id].lit_len) + cr.anchors[id].ext;
+      } else {
+        err_ = "unexpected automaton output kind";
+        return;
+      }
+      if (id >= (1u << 20) || len >= (1u << 10)) {
+        err_ = "rule set exceeds the scan kernel's output encoding (ids < 2^20, patterns < 1024 bytes)";
+        return;
+      }
+      out_items.push_back((kind << 30) | (uint32_t(len) << 20) | id);
+    }
+  }
+  out_off[ns] = out_off[ns + 1] = uint32_t(out_items.size());
   uint8_t* d_tb = nullptr;
   std::vector<uint64_t> la = cr.la_masks;
   if (la.empty()) la.assign(2, 0);
   if (!Upload(&err_, &d_cmap_, cmap, 256) || !Upload(&err_, &d_tb, tbuf.data(), tbuf.size()) ||
-      !Upload(&err_, &d_out_off_, cr.out_off.data(), cr.out_off.size()) ||
-      !Upload(&err_, &d_out_items_, cr.out_items.data(), cr.out_items.size()) ||
+      !Upload(&err_, &d_out_off_, out_off.data(), out_off.size()) ||
+      !Upload(&err_, &d_out_items_, out_items.data(), out_items.size()) ||
       !Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
       !Upload(&err_, &d_la_, la.data(), la.size()) ||
       !Upload(&err_, &d_rules_, cr.rules.data(), cr.rules.size()) ||
@@ -622,8 +794,8 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       pad(tb);
       return uint32_t(at);
     };
-    tab_out_off_ = put(cr.out_off.data(), cr.out_off.size() * 4);
-    tab_out_items_ = put(cr.out_items.data(), cr.out_items.size() * 4);
+    tab_out_off_ = put(out_off.data(), out_off.size() * 4);
+    tab_out_items_ = put(out_items.data(), out_items.size() * 4);
     tab_anchors_ = put(cr.anchors.data(), cr.anchors.size() * sizeof(AnchorInfo));
     tab_la_ = put(la.data(), la.size() * 8);
     if (tb.empty()) tb.assign(16, 0);
@@ -632,9 +804,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_tabs_ = d;
   }
-  size_t rest = 256 + size_t(3 * kHitBuf) * 4 + 16 + tabs_bytes_;
-  table_in_lds_ = tbytes + rest <= 150 * 1024;
-  lds_bytes_ = (table_in_lds_ ? tbytes : 0) + rest;
+  const size_t queue_bytes = size_t(kScanWaves) * kQueue * sizeof(ReplayEntry) +
+                             size_t(kScanWaves) * kWaveHits * 12 + size_t(kScanWaves) * 4;
+  table_in_lds_ = tbytes + 256 + tabs_bytes_ + queue_bytes <= 156 * 1024;
+  lds_bytes_ = table_in_lds_ ? tbytes + 256 + tabs_bytes_ + queue_bytes : 256 + queue_bytes;
   const void* fn = wide_table_ ? (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint32_t, true>)
                                                 : reinterpret_cast<const void*>(&scan_kernel<uint32_t, false>))
                                : (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint16_t, true>)
@@ -646,7 +819,7 @@ GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
   void* ps[] = {d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
-                d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_};
+                d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_, d_params_};
   for (void* p : ps)
     if (p) hipFree(p);
   for (auto& e : ev_)
@@ -686,6 +859,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   st->bytes = n_bytes;
   st->files = n_files;
   if (n_files == 0) return true;
+  if (n_bytes >= (uint64_t(1) << 36) - 64) {
+    err_ = "batch arena must be < 64 GiB";
+    return false;
+  }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
   if (n_chunks == 0) n_chunks = 1;
   if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 64, 1 << 16), 1u << 30));
@@ -719,7 +896,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.out_items = d_out_items_;
     sp.anchors = d_anchors_;
     sp.la = d_la_;
-    sp.cls_fold = cls_fold_;
+    sp.thr = thr_;
+    sp.fold_entry = fold_entry_;
     sp.cls_i = cls_i_;
     sp.cls_k = cls_k_;
     sp.cls_s = cls_s_;
@@ -734,6 +912,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.n_states = n_states_;
     sp.n_classes = n_classes_;
     sp.warm = max_pat_len_ > 0 ? max_pat_len_ - 1 : 0;
+    sp.warm_blocks = (sp.warm + 15) / 16;
     sp.kw_words = kw_words_;
     sp.kwbits = static_cast<uint32_t*>(d_kw_);
     sp.flags = static_cast<uint32_t*>(d_flags_);

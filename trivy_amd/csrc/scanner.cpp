@@ -2,6 +2,8 @@
 #include "scanner.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -511,15 +513,14 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     return p < it->e ? &*it : nullptr;
   };
   auto line_start_of = [&](int64_t pos) {  // after the last visible '\n' before pos
-    int64_t p = pos - 1;
-    while (p >= 0) {
-      if (content[p] == '\n') {
-        const Loc* z = in_span(p);
-        if (!z) return p + 1;
-        p = z->s - 1;
-        continue;
-      }
-      p--;
+    int64_t p = pos;  // search [0, p)
+    while (p > 0) {
+      const void* q = memrchr(content, '\n', size_t(p));
+      if (!q) return int64_t(0);
+      int64_t at = int64_t(static_cast<const uint8_t*>(q) - content);
+      const Loc* z = in_span(at);
+      if (!z) return at + 1;
+      p = z->s;
     }
     return int64_t(0);
   };
@@ -592,48 +593,70 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     err_ = "no GPU engine bound to this scanner";
     return false;
   }
+  // the allow-path pass needs no GPU result: it runs on host threads while
+  // this thread drives the kernels
+  std::vector<uint8_t> allowed;
+  double ms_allow = 0;
+  std::thread allow_thread([&] {
+    double a0 = NowMs();
+    allowed = AllowedPaths(in);
+    ms_allow = NowMs() - a0;
+  });
   bool ok;
   if (in.dev_arena)
     ok = engine_->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
   else
     ok = engine_->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
+  allow_thread.join();
   if (!ok) {
     err_ = engine_->error();
     return false;
   }
   double t1 = NowMs();
-  HostTail(in, &cands, out, &hs);
+  if (const char* dump = std::getenv("TSG_DUMP_CANDS")) {  // profiling aid (tools/host_tail_bench.py)
+    if (FILE* fp = std::fopen(dump, "wb")) {
+      if (!cands.empty()) std::fwrite(cands.data(), sizeof(Candidate), cands.size(), fp);
+      std::fclose(fp);
+    }
+  }
+  HostTail(in, &cands, out, &hs, &allowed);
+  hs.ms_allow = ms_allow;  // overlapped with the GPU phase
   hs.ms_gpu = t1 - t0;
   hs.ms_total = NowMs() - t0;
   if (hst) *hst = hs;
   return true;
 }
 
+std::vector<uint8_t> SecretScanner::AllowedPaths(const BatchInput& in) const {
+  // Global allow path (scanner.go:381-386) for every file
+  std::vector<uint8_t> allowed(in.n_files, 0);
+  bool any_path_rule = false;
+  for (auto& a : allow_)
+    if (a.path) any_path_rule = true;
+  if (any_path_rule) {
+    size_t blocks = (in.n_files + 4095) / 4096;
+    ParallelFor(blocks, host_threads_, [&](size_t b) {
+      size_t lo = b * 4096, hi = std::min<size_t>(lo + 4096, in.n_files);
+      for (size_t f = lo; f < hi; f++) {
+        const char* p = in.paths[f];
+        size_t n = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
+        allowed[f] = AllowPath(reinterpret_cast<const uint8_t*>(p), n) ? 1 : 0;
+      }
+    });
+  }
+  return allowed;
+}
+
 void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, BatchResult* out,
-                             HostStats* hs) const {
+                             HostStats* hs, const std::vector<uint8_t>* allowed_pre) const {
   std::vector<Candidate>& cands = *cands_p;
   out->kind.assign(in.n_files, uint8_t(kNoFindings));
   out->found_files.clear();
   out->found.clear();
   double t1 = NowMs();
-  // Global allow path (scanner.go:381-386) for every file
-  std::vector<uint8_t> allowed(in.n_files, 0);
-  {
-    bool any_path_rule = false;
-    for (auto& a : allow_)
-      if (a.path) any_path_rule = true;
-    if (any_path_rule) {
-      size_t blocks = (in.n_files + 4095) / 4096;
-      ParallelFor(blocks, host_threads_, [&](size_t b) {
-        size_t lo = b * 4096, hi = std::min<size_t>(lo + 4096, in.n_files);
-        for (size_t f = lo; f < hi; f++) {
-          const char* p = in.paths[f];
-          size_t n = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
-          allowed[f] = AllowPath(reinterpret_cast<const uint8_t*>(p), n) ? 1 : 0;
-        }
-      });
-    }
-  }
+  std::vector<uint8_t> allowed_local;
+  if (!allowed_pre) allowed_local = AllowedPaths(in);
+  const std::vector<uint8_t>& allowed = allowed_pre ? *allowed_pre : allowed_local;
   for (uint32_t f = 0; f < in.n_files; f++)
     if (allowed[f]) out->kind[f] = uint8_t(kAllowedPath);
   double t2 = NowMs();

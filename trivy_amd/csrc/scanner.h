@@ -106,7 +106,11 @@ class SecretScanner {
 
   bool Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst);
   // The exact host tail over a given candidate list (what Scan runs after the GPU).
-  void HostTail(const BatchInput& in, std::vector<Candidate>* cands, BatchResult* out, HostStats* hs) const;
+  // The exact host pass over the GPU's candidates.  `allowed` (per-file
+  // global AllowPath results) is computed here when not supplied.
+  void HostTail(const BatchInput& in, std::vector<Candidate>* cands, BatchResult* out, HostStats* hs,
+                const std::vector<uint8_t>* allowed = nullptr) const;
+  std::vector<uint8_t> AllowedPaths(const BatchInput& in) const;
   // Global.AllowPath (scanner.go:57-59)
   bool AllowPath(const uint8_t* p, size_t n) const;
 
