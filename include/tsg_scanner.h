@@ -107,6 +107,8 @@ typedef struct tsg_stats {
   uint64_t bytes, files, anchor_hits, candidates, special_files, findings;
   double ms_scan_kernel, ms_verify_kernel, ms_fullscan_kernel, ms_gpu_total;
   double ms_host_gpu_phase, ms_host_allow_path, ms_host_exact, ms_host_total;
+  uint64_t flagged_blocks;   /* 16-B blocks the streaming filter sent to its exact confirm step */
+  double ms_careful_kernel;  /* fold-rune files' careful pass (part of ms_gpu_total) */
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 

@@ -1,0 +1,130 @@
+"""CPU model of the streaming prefilter K1 (test helper, not product code).
+
+Reads the compiled prefilter tables through include/tsg_debug.h
+(tsg_debug_filter) and replays K1's semantics with numpy: bucketed shift-or
+fires over the byte stream (window of 6 slots ending at each byte), then the
+exact confirm of every item of every fired bucket, file attribution and the
+emitted anchor hits / fold-rune files.  Used to check, without a GPU, that the
+prefilter's hits cover every true match of every rule.
+"""
+import ctypes as c
+
+import numpy as np
+
+from trivy_amd import _lib
+from trivy_amd.secret.scanner import CGlobal
+
+KIND_ANCHOR, KIND_FOLD = 1, 2
+WINDOW = 6
+
+
+class FilterModel:
+    def __init__(self, rules):
+        L = _lib.lib()
+        self._cg = CGlobal(rules, [], [])
+        h = c.c_void_p()
+        L.tsg_debug_compile.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+        if L.tsg_debug_compile(c.byref(self._cg.g), c.byref(h)) != 0:
+            raise ValueError(_lib.last_error())
+        self.h = h
+        L.tsg_debug_filter.argtypes = [c.c_void_p] + [c.c_void_p] * 9
+        shape = (c.c_uint32 * 3)()
+        reach, bo, bi, it, ic, cl = (c.c_void_p() for _ in range(6))
+        ni, fp = c.c_uint32(), c.c_double()
+        rc = L.tsg_debug_filter(h, shape, c.byref(reach), c.byref(bo), c.byref(bi), c.byref(it), c.byref(ni),
+                                c.byref(ic), c.byref(cl), c.byref(fp))
+        if rc != 0:
+            raise ValueError("no prefilter tables")
+        self.n_buckets, self.n_slots, self.n_words = shape[0], shape[1], shape[2]
+        W = self.n_words
+
+        def arr(ptr, ctype, n):
+            return np.ctypeslib.as_array((ctype * max(1, n)).from_address(ptr.value))[:n].copy()
+
+        self.reach = arr(reach, c.c_uint64, 256 * W).reshape(256, W)
+        self.bucket_off = arr(bo, c.c_uint32, self.n_buckets + 1)
+        self.bucket_items = arr(bi, c.c_uint32, int(self.bucket_off[-1]))
+        raw = arr(it, c.c_uint8, 16 * ni.value).reshape(ni.value, 16)
+        self.items = []
+        for r in raw:
+            u16 = r[:6].view(np.uint16)
+            u32 = r[8:16].view(np.uint32)
+            self.items.append({"n": int(u16[0]), "back": int(u16[1]), "lit_end": int(u16[2]), "kind": int(r[6]),
+                               "n_ids": int(r[7]), "ids_off": int(u32[0]), "cls_off": int(u32[1])})
+        n_cls_ref = sum(x["n"] for x in self.items)
+        self.item_cls = arr(ic, c.c_uint8, n_cls_ref)
+        n_cls = int(self.item_cls.max()) + 1 if n_cls_ref else 0
+        words = arr(cl, c.c_uint32, 8 * n_cls).reshape(n_cls, 8)
+        self.classes = np.zeros((n_cls, 256), dtype=bool)
+        for k in range(n_cls):
+            for b in range(256):
+                self.classes[k, b] = (words[k, b >> 5] >> (b & 31)) & 1
+        n_ids = sum(x["n_ids"] for x in self.items)
+        self.item_ids = self._item_ids(L, n_ids)
+        self.fp_est = fp.value
+
+    def _item_ids(self, L, n_ids):
+        L.tsg_debug_filter_ids.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_uint32)]
+        p, n = c.c_void_p(), c.c_uint32()
+        L.tsg_debug_filter_ids(self.h, c.byref(p), c.byref(n))
+        assert n.value == n_ids
+        return np.ctypeslib.as_array((c.c_uint32 * max(1, n.value)).from_address(p.value))[:n.value].copy()
+
+    def allowed(self, j, s):
+        """bool[256]: bytes allowed at slot s of bucket j."""
+        bpw = 64 // self.n_slots
+        w, jj = divmod(j, bpw)
+        bit = np.uint64(s * bpw + jj)
+        return ((self.reach[:, w] >> bit) & np.uint64(1)) == 0
+
+    def fires(self, a):
+        """bool[n_buckets, len(a)]: bucket j fires at window end t (zero bytes before the arena, as in K1)."""
+        a = np.concatenate([np.zeros(8, dtype=np.uint8), np.asarray(a, dtype=np.uint8)])
+        return self._fires(a)[:, 8:]
+
+    def _fires(self, a):
+        n = len(a)
+        out = np.zeros((self.n_buckets, n), dtype=bool)
+        for j in range(self.n_buckets):
+            ok = np.ones(n, dtype=bool)
+            for s in range(WINDOW):
+                col = self.allowed(j, s)[a]
+                sh = WINDOW - 1 - s
+                shifted = np.zeros(n, dtype=bool)
+                shifted[sh:] = col[:n - sh] if sh else col
+                ok &= shifted
+            out[j] = ok
+        return out
+
+    def item_match(self, a, it, start):
+        if start < 0 or start + it["n"] > len(a):
+            return False
+        cls = self.item_cls[it["cls_off"]:it["cls_off"] + it["n"]]
+        return bool(self.classes[cls, a[start:start + it["n"]]].all())
+
+    def run(self, arena, offsets):
+        """Returns (set of (file, literal end rel. to file, anchor id), set of (file, fold flag))."""
+        a = np.asarray(arena, dtype=np.uint8)
+        offs = np.asarray(offsets, dtype=np.int64)
+        hits, folds = set(), set()
+        fr = self.fires(a)
+        for j in range(self.n_buckets):
+            for t in np.nonzero(fr[j])[0]:
+                for x in self.bucket_items[self.bucket_off[j]:self.bucket_off[j + 1]]:
+                    it = self.items[int(x)]
+                    start = int(t) + 1 - it["back"]
+                    if not self.item_match(a, it, start):
+                        continue
+                    f = int(np.searchsorted(offs, start, side="right")) - 1
+                    while f + 1 < len(offs) and offs[f + 1] <= start:
+                        f += 1
+                    fs, fe = int(offs[f]), int(offs[f + 1])
+                    if start < fs or start + it["n"] > fe:
+                        continue
+                    ids = self.item_ids[it["ids_off"]:it["ids_off"] + it["n_ids"]]
+                    if it["kind"] == KIND_FOLD:
+                        folds.add((f, 3 if int(ids[0]) == 2 else 1))
+                        continue
+                    for aid in ids:
+                        hits.add((f, start - fs + it["lit_end"], int(aid)))
+        return hits, folds

@@ -1,0 +1,135 @@
+"""Streaming prefilter (K1) semantics on CPU: every true match is covered.
+
+The CPU model (tests/filter_model.py) replays the compiled bucketed shift-or
+tables and the exact confirm step.  For files without fold runes (U+0130,
+U+212A, U+017F: those go through the careful pass) every match of every rule
+regex -- found by the native Go-regexp engine over the whole file -- must start
+inside the window of some anchor hit of that rule, and files
+holding a fold rune must be flagged.  Rule sets: the builtin rules and the
+golden configs' custom rules.
+"""
+import ctypes as c
+import json
+import random
+from pathlib import Path
+
+import numpy as np
+import pytest
+import yaml
+
+from tests.corpus import make_corpus
+from tests.filter_model import FilterModel
+from tests.regex_sampler import sample_regex
+from trivy_amd import _lib
+from trivy_amd.secret import ParseConfig, builtin_rules
+
+ROOT = Path(__file__).resolve().parent.parent
+FOLDS = (b"\xc4\xb0", b"\xe2\x84\xaa", b"\xc5\xbf")
+NOISE = ["the quick brown fox ", "key=", "secret: ", "\n", "  ", "'", '"', "AKIA", "ghp_", "sk_live_",
+         "é", "日本", "\udcff", "-----BEGIN ", "=>", "xoxb-", "eyJ", ".", "hooks.slack.com", "\t", ",", "_",
+         "0123456789abcdef", "aws_", "live_", "test_", "SG.", "pk.", "linear ", "token: "]
+
+
+def _anchors(model):
+    L = _lib.lib()
+    L.tsg_debug_anchor.argtypes = [c.c_void_p, c.c_uint32] + [c.c_void_p] * 4
+    out = []
+    j = 0
+    while True:
+        r, ln, lo, hi = c.c_uint32(), c.c_uint32(), c.c_int32(), c.c_int32()
+        if L.tsg_debug_anchor(model.h, j, c.byref(r), c.byref(ln), c.byref(lo), c.byref(hi)) != 0:
+            return out
+        out.append((r.value, ln.value, lo.value, hi.value))
+        j += 1
+
+
+def _pack(contents):
+    offs = np.zeros(len(contents) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents), dtype=np.uint8)
+    return arena, offs
+
+
+def _check(rules, contents):
+    model = FilterModel(rules)
+    anchors = _anchors(model)
+    arena, offs = _pack(contents)
+    hits, folds = model.run(arena, offs)
+    special = {f for f, _ in folds}
+    windows = {}
+    for f, end, aid in hits:
+        r, lit_len, lo, hi = anchors[aid]
+        lit = end - lit_len
+        windows.setdefault((f, r), []).append((max(0, lit - hi), lit - lo))
+    n_matches = 0
+    for f, content in enumerate(contents):
+        has_fold = any(s in content for s in FOLDS)
+        assert has_fold == (f in special), (f, content)
+        if has_fold:
+            continue
+        for r, rule in enumerate(rules):
+            if not rule.Regex:
+                continue
+            for m in _lib.regex_find_all(rule.Regex, content):
+                if m[0] == m[1]:
+                    continue  # empty matches come from unanchored rules (full-scan path)
+                if not any(lo <= m[0] <= hi for lo, hi in windows.get((f, r), [])):
+                    raise AssertionError("rule %s match %r at %d not covered" % (rule.ID, content[m[0]:m[1]], m[0]))
+                n_matches += 1
+    return n_matches, len(hits)
+
+
+def _planted_texts(rng, rules, n):
+    out = []
+    for _ in range(n):
+        parts = []
+        for _ in range(rng.randint(1, 30)):
+            if rng.random() < 0.35:
+                rule = rng.choice(rules)
+                if rule.Regex:
+                    parts.append(sample_regex(rule.Regex, rng, maxrep=4))
+            else:
+                parts.append(rng.choice(NOISE).encode("utf-8", "surrogateescape"))
+        out.append(b"".join(parts))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_builtin_planted_matches_covered(seed):
+    rules = builtin_rules()
+    rng = random.Random(300 + seed)
+    n, _ = _check(rules, _planted_texts(rng, rules, 120))
+    assert n > 50
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_builtin_corpus_matches_covered(seed):
+    files = make_corpus(seed, 80)
+    contents = [b.replace(b"\r", b"") for _, b in files]
+    n, hits = _check(builtin_rules(), contents)
+    assert n > 0
+
+
+def test_fold_runes_flag_files():
+    rules = builtin_rules()
+    contents = [b"plain ascii\n", b"x\xc4\xb0y", b"\xe2\x84\xaa", b"ab\xc5\xbf", b"\xc4\xc4", b"\xe2\x84",
+                b"\xc5\xbf\xc5\xbf", b""]
+    model = FilterModel(rules)
+    arena, offs = _pack(contents)
+    _, folds = model.run(arena, offs)
+    assert folds == {(1, 1), (2, 1), (3, 3), (6, 3)}
+
+
+def test_golden_custom_rules_covered():
+    rng = random.Random(9)
+    for f in sorted((ROOT / "tests/golden/scanner").glob("*.yaml")):
+        d = yaml.safe_load(f.read_text()) or {}
+        if not d.get("rules"):
+            continue
+        try:
+            cfg = ParseConfig(str(f))
+        except ValueError:
+            continue
+        rules = builtin_rules() + list(cfg.CustomRules or [])
+        custom = [r for r in rules if r.Regex]
+        _check(rules, _planted_texts(rng, custom, 25))

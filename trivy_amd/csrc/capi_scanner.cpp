@@ -4,6 +4,7 @@
 #include <memory>
 #include <string>
 
+#include "filter.h"
 #include "scanner.h"
 #include "tsg_debug.h"
 #include "tsg_scanner.h"
@@ -167,6 +168,8 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.ms_host_allow_path = hs.ms_allow;
   st.ms_host_exact = hs.ms_exact;
   st.ms_host_total = hs.ms_total;
+  st.flagged_blocks = gs.flagged_blocks;
+  st.ms_careful_kernel = gs.ms_careful;
   *out = r.release();
   return 0;
 }
@@ -354,6 +357,38 @@ int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t
   return 0;
 }
 
+int tsg_debug_filter(const tsg_compiled* c, uint32_t* shape, const uint64_t** reach, const uint32_t** bucket_off,
+                     const uint32_t** bucket_items, const void** items, uint32_t* n_items, const uint8_t** item_cls,
+                     const uint32_t** classes, double* est_fp) {
+  const auto* f = c->cr.filter.get();
+  if (!f) return -1;
+  shape[0] = f->n_buckets;
+  shape[1] = f->n_slots;
+  shape[2] = f->n_words;
+  *reach = f->reach.data();
+  *bucket_off = f->bucket_off.data();
+  *bucket_items = f->bucket_items.data();
+  *items = f->items.data();
+  *n_items = uint32_t(f->items.size());
+  *item_cls = f->item_cls.data();
+  *classes = f->classes.data();
+  *est_fp = f->est_fp;
+  return 0;
+}
+
+int tsg_debug_filter_ids(const tsg_compiled* c, const uint32_t** ids, uint32_t* n) {
+  const auto* f = c->cr.filter.get();
+  if (!f) return -1;
+  *ids = f->item_ids.data();
+  *n = uint32_t(f->item_ids.size());
+  return 0;
+}
+
+const char* tsg_debug_rule_anchor(const tsg_compiled* c, uint32_t i) {
+  const auto& d = c->cr.rule_anchor_desc;
+  return i < d.size() ? d[i].c_str() : nullptr;
+}
+
 const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k) {
   return k < c->cr.keywords.size() ? c->cr.keywords[k].c_str() : nullptr;
 }
@@ -406,16 +441,13 @@ extern "C" int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_
     tsg::SetError(err);
     return -2;
   }
+  // every (file, rule with a regex) with the whole file as its window: the
+  // tail's lazy keyword gate decides (as it does for GPU candidates)
   std::vector<tsg::Candidate> cands;
   for (uint32_t f = 0; f < b->n_files; f++) {
     uint64_t fs = b->host_offsets[f], fe = b->host_offsets[f + 1];
-    std::string lower = tsg::GoBytesToLower(b->host_arena + fs, size_t(fe - fs));
     for (uint32_t r = 0; r < sc->rules().size(); r++) {
-      const auto& R = sc->rules()[r];
-      bool gate = R.keywords.empty();
-      for (auto& kw : R.kw_lower_host)
-        if (lower.find(kw) != std::string::npos) gate = true;
-      if (!gate || !sc->compiled().regex[r]) continue;
+      if (!sc->compiled().regex[r]) continue;
       cands.push_back({f, r, 0, int64_t(fe - fs), 0});
     }
   }

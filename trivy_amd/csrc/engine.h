@@ -12,8 +12,6 @@ namespace tsg {
 
 constexpr uint32_t kChunk = 1024;  // bytes per lane-chunk in the scan kernel
 
-constexpr uint32_t kCandHostGate = 1;  // keyword bits may over-approximate (file holds U+017F)
-
 struct Candidate {      // produced by the verify / full-scan kernels
   uint32_t file;
   uint32_t rule;
@@ -25,7 +23,8 @@ struct Candidate {      // produced by the verify / full-scan kernels
 
 struct BatchStats {
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
-  float ms_scan = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
+  uint64_t flagged_blocks = 0;
+  float ms_scan = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
   bool hit_overflow = false, cand_overflow = false;
 };
 
@@ -57,7 +56,7 @@ class GpuEngine {
   std::string err_;
   int device_ = 0;
   hipStream_t stream_ = nullptr;
-  hipEvent_t ev_[4] = {};
+  hipEvent_t ev_[5] = {};
   // tables
   uint8_t* d_cmap_ = nullptr;
   void* d_trans_ = nullptr;
@@ -80,6 +79,12 @@ class GpuEngine {
   uint32_t* d_regex_rules_ = nullptr;
   size_t lds_bytes_ = 0;
   bool table_in_lds_ = true;
+  // streaming prefilter (filter.h)
+  uint64_t* d_reach_ = nullptr;
+  void* d_ftabs_ = nullptr;
+  uint32_t f_words_ = 0, ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
+  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, filter_wg_per_cu_ = 1;
+  size_t f_lds_bytes_ = 0;
   // per-batch buffers
   void* d_chunk_file_ = nullptr; size_t cap_chunk_file_ = 0;
   void* d_nl_ = nullptr; size_t cap_nl_ = 0;
@@ -88,7 +93,9 @@ class GpuEngine {
   void* d_hits_ = nullptr; size_t cap_hits_ = 0;
   void* d_cands_ = nullptr; size_t cap_cands_ = 0;
   void* d_special_ = nullptr; size_t cap_special_ = 0;
-  uint32_t* d_counters_ = nullptr;  // [0]=hits [1]=cands [2]=special [3]=hit overflow [4]=cand overflow
+  void* d_chunk_list_ = nullptr; size_t cap_chunk_list_ = 0;
+  uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
+                                    // [5] careful chunk-list length [6] flagged blocks
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
   void* d_params_ = nullptr; size_t cap_params_ = 0;

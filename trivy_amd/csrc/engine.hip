@@ -20,6 +20,7 @@
 #include <cstring>
 
 #include "engine.h"
+#include "filter.h"
 
 namespace tsg {
 
@@ -70,6 +71,9 @@ struct ScanParams {
   uint32_t* counters;
   uint32_t* special;
   uint32_t special_cap;
+  const uint32_t* chunk_list;    // careful mode: chunks to scan (fold-rune files), count at *chunk_list_n
+  const uint32_t* chunk_list_n;
+  uint32_t chunk_list_cap;
 };
 
 __global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
@@ -332,6 +336,12 @@ __device__ __forceinline__ void flush_hits(const ScanParams& P, const EmitTabs& 
 template <typename TT, bool kLdsTable>
 __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t n_work = P.n_chunks;
+  if (P.chunk_list) {
+    const uint32_t n = *P.chunk_list_n;
+    n_work = n < P.chunk_list_cap ? n : P.chunk_list_cap;
+    if (n_work == 0) return;
+  }
   const size_t tbytes = kLdsTable ? ((size_t(P.n_states) * P.n_classes * sizeof(TT) + 15) & ~size_t(15)) : 0;
   TT* s_trans = reinterpret_cast<TT*>(smem);
   uint8_t* s_cmap = smem + tbytes;
@@ -376,9 +386,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   const uint32_t ngroups = ((P.warm_blocks + kChunk / 16 + kGroup - 1) / kGroup + 1) & ~1u;
   const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
 
-  for (uint64_t tile = uint64_t(blockIdx.x) * kScanWaves + wave; tile * 64 < P.n_chunks; tile += n_waves) {
-    const uint64_t c = tile * 64 + lane;
-    const bool live = c < P.n_chunks;
+  for (uint64_t tile = uint64_t(blockIdx.x) * kScanWaves + wave; tile * 64 < n_work; tile += n_waves) {
+    const uint64_t idx = tile * 64 + lane;
+    const bool live = idx < n_work;
+    const uint64_t c = P.chunk_list ? P.chunk_list[live ? idx : n_work - 1] : idx;
     const uint64_t b0 = c * kChunk;
     const uint64_t b1 = live ? (b0 + kChunk < P.n_bytes ? b0 + kChunk : P.n_bytes) : 0;
     const int64_t pstart = int64_t(b0) - int64_t(P.warm_blocks) * 16;
@@ -450,10 +461,348 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
       do_group(B, gb);
       load_group(B, gb + 2 * 16 * kGroup);
     }
-    if (live) P.nl[c] = uint16_t(nl);
+    if (live && !P.chunk_list) P.nl[c] = uint16_t(nl);
   }
   if (qn) drain_queue<TT>(P, E, T, s_cmap, Q, qn, lane);
   flush_hits(P, E, lane);
+}
+
+// ---------------------------------------------------------------------------
+// K1: streaming bucketed shift-or filter + exact confirm
+// ---------------------------------------------------------------------------
+constexpr int kFLaneBytes = 128;                 // bytes per lane per tile (8 blocks of 16 B)
+constexpr int kFBlocks = kFLaneBytes / 16;
+constexpr int kFTile = 64 * kFLaneBytes;         // 8 KiB per wave tile
+constexpr int kFQueue = 128;                     // per-wave flagged-block queue (drained at >= 64)
+constexpr int kFWaveHits = 128;                  // per-wave LDS hit records
+constexpr int kFWindow = 6;                      // filter window; checks every 9 - kFWindow = 3 bytes
+static_assert(kChunk % kFLaneBytes == 0, "a newline chunk must be whole lane chunks");
+
+struct FilterParams {
+  const uint8_t* arena;
+  uint64_t n_bytes;
+  const uint64_t* off;
+  uint32_t n_files;
+  const uint32_t* chunk_file;
+  uint64_t n_chunks;
+  const uint64_t* reach;      // 256 x W u64 (filter.h layout)
+  const void* tabs;           // bucket_off | bucket_items | items | item_ids | item_cls | classes
+  uint32_t tabs_bytes, t_bucket_off, t_bucket_items, t_items, t_item_ids, t_item_cls, t_classes;
+  uint32_t diag_mode;         // TSG_DIAG_SCAN: 1 skip the confirm drains, 2 also skip the filter
+  uint16_t* nl;
+  uint32_t* flags;            // per file: bit0 U+0130/U+212A seen, bit1 U+017F seen
+  uint32_t* special;
+  uint32_t special_cap;
+  uint32_t* hits;
+  uint32_t hit_cap;
+  uint32_t* counters;         // [0] hits [2] special files [3] hit overflow [6] flagged blocks
+};
+
+struct FilterTabs {  // LDS copies
+  const uint32_t* bucket_off;
+  const uint32_t* bucket_items;
+  const FilterItemGpu* items;
+  const uint32_t* item_ids;
+  const uint8_t* item_cls;
+  const uint32_t* classes;
+};
+
+// One shift-or step: S = (S << 8) | reach[b] for W 64-bit registers (lo, hi
+// u32 halves); the LDS table row of byte b is 256 B (16 copies of a 16-B
+// entry for W = 2, 32 copies of 8 B for W = 1), the copy chosen by lane, so a
+// wave's reads never conflict.  `laneoff` sits in the address's low byte.
+template <int W>
+__device__ __forceinline__ void fstep(uint32_t w, uint32_t k, uint32_t laneoff, const uint8_t* sb, uint32_t* st) {
+  const uint32_t addr = __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8));
+  if constexpr (W == 2) {
+    const uint4 m = *reinterpret_cast<const uint4*>(sb + addr);
+    st[1] = __builtin_amdgcn_alignbit(st[1], st[0], 24) | m.y;
+    st[0] = (st[0] << 8) | m.x;
+    st[3] = __builtin_amdgcn_alignbit(st[3], st[2], 24) | m.w;
+    st[2] = (st[2] << 8) | m.z;
+  } else {
+    const uint2 m = *reinterpret_cast<const uint2*>(sb + addr);
+    st[1] = __builtin_amdgcn_alignbit(st[1], st[0], 24) | m.y;
+    st[0] = (st[0] << 8) | m.x;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t ftop(const uint32_t* st) {  // AND of the registers' high halves
+  return W == 2 ? (st[1] & st[3]) : st[1];
+}
+
+__device__ __forceinline__ uint32_t word_of(uint4 v, uint32_t i) {
+  return i < 2 ? (i == 0 ? v.x : v.y) : (i == 2 ? v.z : v.w);
+}
+
+// Exact check of item `it` starting at arena byte `start` (every position's
+// byte in its class); 16-B loads, the item is at most 48 positions.
+__device__ bool item_match(const FilterParams& P, const FilterTabs& T, const FilterItemGpu& it, int64_t start) {
+  if (start < 0 || uint64_t(start) + it.n > P.n_bytes) return false;
+  uint64_t p = uint64_t(start);
+  uint4 cur = load16(P.arena + (p & ~uint64_t(15)));
+  for (uint32_t q = 0; q < it.n; q++, p++) {
+    if (q && (p & 15) == 0) cur = load16(P.arena + p);
+    const uint32_t b = (word_of(cur, uint32_t(p >> 2) & 3) >> ((p & 3) * 8)) & 0xFFu;
+    const uint32_t c = T.item_cls[it.cls_off + q];
+    if (!((T.classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u)) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ void push_hit(const FilterParams& P, uint32_t* hbuf, uint32_t* hcnt, uint32_t f, uint32_t end,
+                                         uint32_t id) {
+  const uint32_t k = atomicAdd(hcnt, 1u);
+  if (k < uint32_t(kFWaveHits)) {
+    hbuf[3 * k + 0] = f;
+    hbuf[3 * k + 1] = end;
+    hbuf[3 * k + 2] = id;
+    return;
+  }
+  const uint32_t g = atomicAdd(&P.counters[0], 1u);
+  if (g < P.hit_cap) {
+    P.hits[3ull * g + 0] = f;
+    P.hits[3ull * g + 1] = end;
+    P.hits[3ull * g + 2] = id;
+  } else {
+    P.counters[3] = 1;
+  }
+}
+
+// Confirm one flagged block: recompute the per-position bucket fires from
+// the 5 bytes before it, check every item of every fired bucket exactly,
+// attribute matches to their file and emit anchor hits / fold-rune flags.
+template <int W>
+__device__ void confirm_block(const FilterParams& P, const FilterTabs& T, const uint8_t* sb, uint32_t laneoff,
+                              uint32_t blk, uint32_t* hbuf, uint32_t* hcnt) {
+  const uint64_t base = uint64_t(blk) * 16;
+  const uint4 pv = base >= 16 ? load16(P.arena + base - 16) : uint4{0, 0, 0, 0};
+  const uint4 v = load16(P.arena + base);
+  uint32_t st[2 * W];
+#pragma unroll
+  for (int i = 0; i < 2 * W; i++) st[i] = ~0u;
+#pragma unroll
+  for (uint32_t k = 11; k < 16; k++) fstep<W>(word_of(pv, k >> 2), k & 3, laneoff, sb, st);
+  for (uint32_t k = 0; k < 16; k++) {
+    fstep<W>(word_of(v, k >> 2), k & 3, laneoff, sb, st);
+    // slot kFWindow-1 = bits 8..15 of each register's high half
+    uint32_t fm = (~st[1] >> 8) & 0xFFu;
+    if (W == 2) fm |= ((~st[3] >> 8) & 0xFFu) << 8;
+    while (fm) {
+      const uint32_t j = __builtin_ctz(fm);
+      fm &= fm - 1;
+      for (uint32_t x = T.bucket_off[j]; x < T.bucket_off[j + 1]; x++) {
+        const FilterItemGpu it = T.items[T.bucket_items[x]];
+        const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
+        if (!item_match(P, T, it, start)) continue;
+        const uint64_t s0 = uint64_t(start);
+        uint32_t f = P.chunk_file[s0 / kChunk];
+        uint64_t fs = P.off[f], fe = P.off[f + 1];
+        while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
+          f++;
+          fs = fe;
+          fe = P.off[f + 1];
+        }
+        if (s0 < fs || s0 + it.n > fe) continue;  // crosses a file boundary
+        if (it.kind == kItemFold) {
+          const uint32_t fl = T.item_ids[it.ids_off] == 2 ? 3u : 1u;
+          const uint32_t old = atomicOr(&P.flags[f], fl);
+          if (old == 0) {
+            const uint32_t q = atomicAdd(&P.counters[2], 1u);
+            if (q < P.special_cap) P.special[q] = f;
+          }
+          continue;
+        }
+        const uint32_t end = uint32_t(s0 - fs) + it.lit_end;
+        for (uint32_t d = 0; d < it.n_ids; d++) push_hit(P, hbuf, hcnt, f, end, T.item_ids[it.ids_off + d]);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void flush_wave_hits(const FilterParams& P, uint32_t* hbuf, uint32_t* hcnt, uint32_t lane) {
+  wave_sync();
+  const uint32_t n_all = __builtin_amdgcn_readfirstlane(*hcnt);
+  const uint32_t n = n_all < uint32_t(kFWaveHits) ? n_all : uint32_t(kFWaveHits);
+  if (n) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&P.counters[0], n);
+    base = __builtin_amdgcn_readfirstlane(base);
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t g = base + i;
+      if (g < P.hit_cap) {
+        P.hits[3ull * g + 0] = hbuf[3 * i + 0];
+        P.hits[3ull * g + 1] = hbuf[3 * i + 1];
+        P.hits[3ull * g + 2] = hbuf[3 * i + 2];
+      } else {
+        P.counters[3] = 1;
+      }
+    }
+  }
+  wave_sync();
+  if (lane == 0) *hcnt = 0;
+  wave_sync();
+}
+
+template <int W>
+__device__ __forceinline__ void drain_flagged(const FilterParams& P, const FilterTabs& T, const uint8_t* sb,
+                                              uint32_t laneoff, const uint32_t* Q, uint32_t n, uint32_t* hbuf,
+                                              uint32_t* hcnt, uint32_t lane) {
+  wave_sync();
+  if (lane == 0) atomicAdd(&P.counters[6], n);
+  if (P.diag_mode == 0)
+    for (uint32_t i = lane; i < n; i += 64) confirm_block<W>(P, T, sb, laneoff, Q[i], hbuf, hcnt);
+  flush_wave_hits(P, hbuf, hcnt, lane);
+}
+
+// K1.  A wave owns 8 KiB tiles (grid-strided); lane l streams its 128
+// contiguous bytes as 8 x 16-B loads with the next tile's loads in flight.
+// The 5 bytes before a lane's chunk come from lane l-1 (lane 0: an 8-B load).
+// Per byte: table address by v_perm, one conflict-free LDS read, shift-or on
+// W u64 registers.  Every 3 bytes the top three slots are AND-ed into the
+// block's accumulator (a fire at window end t is visible in slots 5..7 at
+// t..t+2), so the hot loop never branches.  Flagged blocks go through a
+// ballot/mbcnt-compacted per-wave LDS queue; at 64 the wave confirms them in
+// parallel (one block per lane).  '\n' is counted per 1-KiB chunk (SWAR +
+// an 8-lane reduction) for the verify kernel's line numbers.
+template <int W>
+__global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* s_reach = smem;                                        // 64 KiB
+  uint8_t* s_tabs = smem + 65536;
+  uint32_t* s_queue = reinterpret_cast<uint32_t*>(s_tabs + P.tabs_bytes);
+  uint32_t* s_hits = s_queue + kScanWaves * kFQueue;
+  uint32_t* s_hcnt = s_hits + kScanWaves * kFWaveHits * 3;
+  const int tid = threadIdx.x;
+  {
+    constexpr uint32_t esz = 8 * W, copies = 256 / esz;
+    for (uint32_t i = tid; i < 256 * copies; i += blockDim.x) {
+      const uint32_t b = i / copies;
+      const uint64_t* src = P.reach + size_t(b) * W;
+      uint64_t* dst = reinterpret_cast<uint64_t*>(s_reach + size_t(i) * esz);
+#pragma unroll
+      for (int w = 0; w < W; w++) dst[w] = src[w];
+    }
+    const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
+    uint4* d = reinterpret_cast<uint4*>(s_tabs);
+    for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
+    if (tid < kScanWaves) s_hcnt[tid] = 0;
+  }
+  __syncthreads();
+  FilterTabs T;
+  T.bucket_off = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_off);
+  T.bucket_items = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_items);
+  T.items = reinterpret_cast<const FilterItemGpu*>(s_tabs + P.t_items);
+  T.item_ids = reinterpret_cast<const uint32_t*>(s_tabs + P.t_item_ids);
+  T.item_cls = s_tabs + P.t_item_cls;
+  T.classes = reinterpret_cast<const uint32_t*>(s_tabs + P.t_classes);
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  const uint32_t laneoff = W == 2 ? (lane & 15) * 16 : (lane & 31) * 8;
+  uint32_t* Q = s_queue + wave * kFQueue;
+  uint32_t* hbuf = s_hits + wave * kFWaveHits * 3;
+  uint32_t* hcnt = s_hcnt + wave;
+  uint32_t qn = 0;  // wave-uniform
+  const uint64_t n_tiles = (P.n_bytes + kFTile - 1) / kFTile;
+  const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
+  uint64_t t = uint64_t(blockIdx.x) * kScanWaves + wave;
+  uint4 cur[kFBlocks], nxt[kFBlocks];
+  uint2 pre = make_uint2(0, 0), pnx = make_uint2(0, 0);
+  auto load_tile = [&](uint4* dst, uint2* pv, uint64_t tt) {
+    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLaneBytes;
+#pragma unroll
+    for (int j = 0; j < kFBlocks; j++) {
+      const uint64_t p = b0 + 16 * j;
+      dst[j] = load16(P.arena + (p < P.n_bytes ? p : 0));
+    }
+    if (lane == 0 && tt > 0) *pv = *reinterpret_cast<const uint2*>(P.arena + tt * kFTile - 8);
+  };
+  if (t < n_tiles) load_tile(cur, &pre, t);
+  for (; t < n_tiles; t += n_waves) {
+    if (t + n_waves < n_tiles) load_tile(nxt, &pnx, t + n_waves);
+    const uint64_t b0 = t * kFTile + uint64_t(lane) * kFLaneBytes;
+    // bytes past the arena end (last tile only) are zeroed
+    if (b0 + kFLaneBytes > P.n_bytes) {
+#pragma unroll
+      for (int j = 0; j < kFBlocks; j++) {
+        const uint64_t p = b0 + 16 * j;
+        uint32_t wd[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint64_t wp = p + 4 * q;
+          if (wp >= P.n_bytes) wd[q] = 0;
+          else if (wp + 4 > P.n_bytes) wd[q] &= (1u << (8 * (P.n_bytes - wp))) - 1u;
+        }
+        cur[j] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+      }
+    }
+    // the previous 8 bytes: lane l-1's last two words (lane 0: the extra load)
+    uint32_t p0 = __shfl(cur[kFBlocks - 1].z, int(lane) - 1), p1 = __shfl(cur[kFBlocks - 1].w, int(lane) - 1);
+    if (lane == 0) {
+      p0 = pre.x;
+      p1 = pre.y;
+    }
+    uint32_t flagged = 0, nl = 0;
+    if (P.diag_mode < 2) {
+      uint32_t st[2 * W];
+#pragma unroll
+      for (int i = 0; i < 2 * W; i++) st[i] = ~0u;
+      fstep<W>(p0, 3, laneoff, s_reach, st);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) fstep<W>(p1, k, laneoff, s_reach, st);
+#pragma unroll
+      for (int j = 0; j < kFBlocks; j++) {
+        const uint32_t wd[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+        uint32_t acc = ~0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+          fstep<W>(wd[k >> 2], k & 3, laneoff, s_reach, st);
+          if (k % 3 == 2 || k == 15) acc &= ftop<W>(st);
+        }
+        flagged |= uint32_t((acc | 0xFFu) != ~0u) << j;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kFBlocks; j++)
+      nl += nl_in_word(cur[j].x) + nl_in_word(cur[j].y) + nl_in_word(cur[j].z) + nl_in_word(cur[j].w);
+    nl += __shfl_xor(nl, 1);
+    nl += __shfl_xor(nl, 2);
+    nl += __shfl_xor(nl, 4);
+    if ((lane & 7) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
+    // queue the flagged blocks
+#pragma unroll
+    for (int j = 0; j < kFBlocks; j++) {
+      const bool fj = (flagged >> j) & 1u;
+      const uint64_t m = __ballot(fj);
+      if (m) {
+        const uint32_t below =
+            __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        if (fj) Q[qn + below] = uint32_t((b0 + 16 * j) >> 4);
+        qn += uint32_t(__popcll(m));
+        if (qn >= 64) {
+          drain_flagged<W>(P, T, s_reach, laneoff, Q, qn, hbuf, hcnt, lane);
+          qn = 0;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kFBlocks; j++) cur[j] = nxt[j];
+    pre = pnx;
+  }
+  if (qn) drain_flagged<W>(P, T, s_reach, laneoff, Q, qn, hbuf, hcnt, lane);
+}
+
+// Chunk list of the files K1 found fold runes in (for the careful pass).
+__global__ void special_chunks_kernel(const uint64_t* __restrict__ off, const uint32_t* __restrict__ special,
+                                      uint32_t* __restrict__ counters, uint32_t* __restrict__ list, uint32_t cap) {
+  const uint32_t n = counters[2];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t f = special[i];
+    const uint64_t c0 = off[f] / kChunk, c1 = (off[f + 1] - 1) / kChunk;
+    const uint32_t k = atomicAdd(&counters[5], uint32_t(c1 - c0 + 1));
+    for (uint64_t c = c0; c <= c1; c++)
+      if (k + (c - c0) < cap) list[k + (c - c0)] = uint32_t(c);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -544,16 +893,6 @@ __device__ bool nfa_dispatch(int words, const uint8_t* s, int64_t len, int64_t s
   }
 }
 
-__device__ bool gate_open(const NfaParams& P, const RuleGpu& rg, uint32_t f) {
-  if (rg.gate != kGateKeywords) return true;  // always / host-verified
-  const uint32_t* kb = P.kwbits + uint64_t(f) * P.kw_words;
-  for (uint32_t i = 0; i < rg.kw_cnt; i++) {
-    uint32_t id = P.rule_kw[rg.kw_off + i];
-    if (kb[id >> 5] & (1u << (id & 31))) return true;
-  }
-  return false;
-}
-
 __device__ int64_t count_nl(const NfaParams& P, uint64_t a, uint64_t b) {  // '\n' in arena [a, b)
   int64_t n = 0;
   uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
@@ -590,8 +929,7 @@ __global__ __launch_bounds__(256) void verify_kernel(NfaParams P) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     uint32_t f = P.hits[3ull * i], end = P.hits[3ull * i + 1], aid = P.hits[3ull * i + 2];
     AnchorInfo a = P.anchors[aid];
-    RuleGpu rg = P.rules[a.rule];
-    if (!gate_open(P, rg, f)) continue;
+    RuleGpu rg = P.rules[a.rule];  // keyword gates are evaluated lazily by the host tail
     uint32_t ff = P.flags[f];
     // literal start: lit_len bytes before the end, up to 3x when folded runes occur
     int64_t lit_hi = int64_t(end) - int64_t(a.lit_len);
@@ -618,7 +956,6 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
     uint32_t f = uint32_t(t / P.n_fullscan_rules);
     uint32_t r = P.fullscan_rules[t % P.n_fullscan_rules];
     RuleGpu rg = P.rules[r];
-    if (!gate_open(P, rg, f)) continue;
     uint64_t fs = P.off[f];
     int64_t len = int64_t(P.off[f + 1] - fs);
     bool acc = rg.nfa_words == 0 ||
@@ -813,11 +1150,55 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
                                : (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint16_t, true>)
                                                 : reinterpret_cast<const void*>(&scan_kernel<uint16_t, false>));
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes_));
+  // streaming prefilter tables (filter.h)
+  {
+    const FilterTables* ft = cr.filter.get();
+    if (!ft || ft->n_slots != 8 || ft->window != uint32_t(kFWindow) || (ft->n_words != 1 && ft->n_words != 2)) {
+      err_ = "prefilter shape not supported by the scan kernel (needs 8 slots, window 6, 8 or 16 buckets)";
+      return;
+    }
+    for (auto& it : ft->items)
+      if (it.n > 48) {
+        err_ = "prefilter item longer than 48 positions";
+        return;
+      }
+    f_words_ = ft->n_words;
+    if (!Upload(&err_, &d_reach_, ft->reach.data(), ft->reach.size())) return;
+    auto pad = [](std::vector<uint8_t>& v) { v.resize((v.size() + 15) & ~size_t(15), 0); };
+    std::vector<uint8_t> tb;
+    auto put = [&](const void* src, size_t n) {
+      size_t at = tb.size();
+      tb.resize(at + n);
+      if (n) std::memcpy(&tb[at], src, n);
+      pad(tb);
+      return uint32_t(at);
+    };
+    ft_bucket_off_ = put(ft->bucket_off.data(), ft->bucket_off.size() * 4);
+    ft_bucket_items_ = put(ft->bucket_items.data(), ft->bucket_items.size() * 4);
+    ft_items_ = put(ft->items.data(), ft->items.size() * sizeof(FilterItemGpu));
+    ft_item_ids_ = put(ft->item_ids.data(), ft->item_ids.size() * 4);
+    ft_item_cls_ = put(ft->item_cls.data(), ft->item_cls.size());
+    ft_classes_ = put(ft->classes.data(), ft->classes.size() * 4);
+    if (tb.empty()) tb.assign(16, 0);
+    ftabs_bytes_ = uint32_t(tb.size());
+    uint8_t* d = nullptr;
+    if (!Upload(&err_, &d, tb.data(), tb.size())) return;
+    d_ftabs_ = d;
+    f_lds_bytes_ = 65536 + ftabs_bytes_ + size_t(kScanWaves) * kFQueue * 4 + size_t(kScanWaves) * kFWaveHits * 12 +
+                   size_t(kScanWaves) * 4;
+    if (f_lds_bytes_ > 160 * 1024) {
+      err_ = "prefilter tables do not fit in LDS";
+      return;
+    }
+    const void* ff = f_words_ == 2 ? reinterpret_cast<const void*>(&filter_kernel<2>)
+                                   : reinterpret_cast<const void*>(&filter_kernel<1>);
+    hipFuncSetAttribute(ff, hipFuncAttributeMaxDynamicSharedMemorySize, int(f_lds_bytes_));
+  }
 }
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
+  void* ps[] = {d_reach_, d_ftabs_, d_chunk_list_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
                 d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_, d_params_};
   for (void* p : ps)
@@ -865,17 +1246,18 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
   if (n_chunks == 0) n_chunks = 1;
-  if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 64, 1 << 16), 1u << 30));
+  if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 256, 1 << 16), 1u << 30));
   if (cand_cap_ == 0) cand_cap_ = 1 << 16;
+  const uint32_t list_cap = uint32_t(std::min<uint64_t>(n_chunks + n_files, 0xFFFFFFF0u));
   for (int attempt = 0; attempt < 8; attempt++) {
     if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, n_chunks * 2) ||
         !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
         !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
         !Ensure(&d_special_, &cap_special_, size_t(n_files) * 4) ||
+        !Ensure(&d_chunk_list_, &cap_chunk_list_, size_t(list_cap) * 4) ||
         !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
         !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
       return false;
-    HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
     HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
     HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
     HIP_OK(hipMemsetAsync(d_chunk_file_, 0, n_chunks * 4, stream_));
@@ -883,6 +1265,42 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       uint32_t blocks = std::min<uint32_t>((n_files + 255) / 256, 4096);
       chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, static_cast<uint32_t*>(d_chunk_file_));
     }
+    // K1: streaming filter + confirm
+    FilterParams fp;
+    fp.arena = d_arena;
+    fp.n_bytes = n_bytes;
+    fp.off = d_offsets;
+    fp.n_files = n_files;
+    fp.chunk_file = static_cast<const uint32_t*>(d_chunk_file_);
+    fp.n_chunks = n_chunks;
+    fp.reach = d_reach_;
+    fp.tabs = d_ftabs_;
+    fp.tabs_bytes = ftabs_bytes_;
+    fp.t_bucket_off = ft_bucket_off_;
+    fp.t_bucket_items = ft_bucket_items_;
+    fp.t_items = ft_items_;
+    fp.t_item_ids = ft_item_ids_;
+    fp.t_item_cls = ft_item_cls_;
+    fp.t_classes = ft_classes_;
+    fp.diag_mode = diag_mode_;
+    fp.nl = static_cast<uint16_t*>(d_nl_);
+    fp.flags = static_cast<uint32_t*>(d_flags_);
+    fp.special = static_cast<uint32_t*>(d_special_);
+    fp.special_cap = n_files;
+    fp.hits = static_cast<uint32_t*>(d_hits_);
+    fp.hit_cap = hit_cap_;
+    fp.counters = d_counters_;
+    const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
+    const uint32_t f_grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves,
+                                                                            uint64_t(256) * filter_wg_per_cu_)));
+    HIP_OK(hipEventRecord(ev_[0], stream_));
+    if (f_words_ == 2) filter_kernel<2><<<f_grid, kScanThreads, f_lds_bytes_, stream_>>>(fp);
+    else filter_kernel<1><<<f_grid, kScanThreads, f_lds_bytes_, stream_>>>(fp);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev_[1], stream_));
+    // careful pass over the chunks of fold-rune files (Aho-Corasick on the bytes.ToLower symbol stream)
+    special_chunks_kernel<<<64, 256, 0, stream_>>>(d_offsets, static_cast<const uint32_t*>(d_special_), d_counters_,
+                                                   static_cast<uint32_t*>(d_chunk_list_), list_cap);
     ScanParams sp;
     sp.arena = d_arena;
     sp.n_bytes = n_bytes;
@@ -902,7 +1320,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.cls_k = cls_k_;
     sp.cls_s = cls_s_;
     sp.div_magic = div_magic_;
-    sp.diag_mode = diag_mode_;
+    sp.diag_mode = 0;
     sp.tabs = d_tabs_;
     sp.tabs_bytes = tabs_bytes_;
     sp.tab_out_off = tab_out_off_;
@@ -922,19 +1340,22 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.counters = d_counters_;
     sp.special = static_cast<uint32_t*>(d_special_);
     sp.special_cap = n_files;
-    uint64_t tiles = (n_chunks + kScanThreads - 1) / kScanThreads;
-    uint32_t per_cu = std::max<uint32_t>(1, uint32_t((160 * 1024) / lds_bytes_));
-    uint32_t grid = uint32_t(std::min<uint64_t>(tiles, uint64_t(256) * per_cu));
-    HIP_OK(hipEventRecord(ev_[0], stream_));
-    if (wide_table_) {
-      if (table_in_lds_) scan_kernel<uint32_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-      else scan_kernel<uint32_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-    } else {
-      if (table_in_lds_) scan_kernel<uint16_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-      else scan_kernel<uint16_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+    sp.chunk_list = static_cast<const uint32_t*>(d_chunk_list_);
+    sp.chunk_list_n = d_counters_ + 5;
+    sp.chunk_list_cap = list_cap;
+    {
+      uint32_t per_cu = std::max<uint32_t>(1, uint32_t((160 * 1024) / lds_bytes_));
+      uint32_t grid = 64 * per_cu;
+      if (wide_table_) {
+        if (table_in_lds_) scan_kernel<uint32_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+        else scan_kernel<uint32_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+      } else {
+        if (table_in_lds_) scan_kernel<uint16_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+        else scan_kernel<uint16_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
+      }
     }
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[1], stream_));
+    HIP_OK(hipEventRecord(ev_[2], stream_));
     NfaParams np;
     np.arena = d_arena;
     np.off = d_offsets;
@@ -960,21 +1381,26 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.n_fullscan_rules = n_fullscan_rules_;
     verify_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[2], stream_));
+    HIP_OK(hipEventRecord(ev_[3], stream_));
     if (np.n_fullscan_rules > 0) {
       fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
       HIP_OK(hipGetLastError());
     }
-    HIP_OK(hipEventRecord(ev_[3], stream_));
-    uint32_t cnt[8];
+    HIP_OK(hipEventRecord(ev_[4], stream_));
+    uint32_t cnt[16];
     HIP_OK(hipMemcpyAsync(cnt, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     st->hits = cnt[0];
     st->special_files = cnt[2];
+    st->flagged_blocks = cnt[6];
     st->hit_overflow = cnt[3] != 0;
     st->cand_overflow = cnt[4] != 0;
+    if (cnt[5] > list_cap) {
+      err_ = "careful chunk list overflow";
+      return false;
+    }
     if (st->hit_overflow) {  // grow and rescan (correctness first)
-      hit_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[0]) + cnt[0] / 4 + 1024, 0xFFFFFFF0u));
+      hit_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[0]) + cnt[0] / 4 + 1024, 0xFFFFFFF0u / 12));
       continue;
     }
     if (st->cand_overflow) {
@@ -989,9 +1415,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       HIP_OK(hipStreamSynchronize(stream_));
     }
     hipEventElapsedTime(&st->ms_scan, ev_[0], ev_[1]);
-    hipEventElapsedTime(&st->ms_verify, ev_[1], ev_[2]);
-    hipEventElapsedTime(&st->ms_fullscan, ev_[2], ev_[3]);
-    hipEventElapsedTime(&st->ms_total, ev_[0], ev_[3]);
+    hipEventElapsedTime(&st->ms_careful, ev_[1], ev_[2]);
+    hipEventElapsedTime(&st->ms_verify, ev_[2], ev_[3]);
+    hipEventElapsedTime(&st->ms_fullscan, ev_[3], ev_[4]);
+    hipEventElapsedTime(&st->ms_total, ev_[0], ev_[4]);
     return true;
   }
   err_ = "candidate buffers kept overflowing";

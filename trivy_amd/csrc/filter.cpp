@@ -1,0 +1,223 @@
+// Streaming prefilter tables (see filter.h).
+#include "filter.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <map>
+
+namespace tsg {
+
+const std::vector<double>& BytePrior() {
+  static const std::vector<double> prior = [] {
+    std::vector<double> f(256, 1e-6);
+    static const double en[26] = {8.2, 1.5, 2.8, 4.3, 12.7, 2.2, 2.0, 6.1, 7.0, 0.15, 0.8, 4.0, 2.4,
+                                  6.7, 7.5, 1.9, 0.1, 6.0, 6.3, 9.1, 2.8, 1.0, 2.4, 0.15, 2.0, 0.07};
+    double tot = 0;
+    for (double x : en) tot += x;
+    for (int i = 0; i < 26; i++) {
+      f['a' + i] = 0.50 * en[i] / tot;
+      f['A' + i] = 0.06 * en[i] / tot;
+    }
+    for (int d = '0'; d <= '9'; d++) f[d] = 0.006;
+    for (int c = 0x21; c < 0x7F; c++)
+      if (f[c] < 1e-4) f[c] = 0.001;
+    f[' '] = 0.14;
+    f['\n'] = 0.025;
+    f['\t'] = 0.005;
+    const std::pair<char, double> punct[] = {{'_', 0.015}, {'.', 0.012}, {',', 0.008}, {'"', 0.01}, {'\'', 0.006},
+                                             {'(', 0.008}, {')', 0.008}, {'=', 0.008}, {':', 0.006}, {'-', 0.006},
+                                             {'/', 0.005}, {';', 0.004}, {'{', 0.003}, {'}', 0.003}, {'[', 0.002},
+                                             {']', 0.002}};
+    for (auto& p : punct) f[uint8_t(p.first)] = p.second;
+    for (int b = 0x80; b < 0x100; b++) f[b] = 1e-4;
+    double s = 0;
+    for (double x : f) s += x;
+    for (double& x : f) x /= s;
+    return f;
+  }();
+  return prior;
+}
+
+namespace {
+
+double SetProb(const ByteSet& s) {
+  if (s.all()) return 1.0;
+  const auto& f = BytePrior();
+  double p = 0;
+  for (int b = 0; b < 256; b++)
+    if (s.test(b)) p += f[b];
+  return std::min(p, 1.0);
+}
+
+struct Cluster {
+  ByteSet u[kFilterSlots];
+  std::vector<uint32_t> members;
+  double cost = 0;
+};
+
+double Cost(const ByteSet* u) {
+  double c = 1.0;
+  for (int s = 0; s < kFilterSlots; s++) c *= SetProb(u[s]);  // unused slots stay "any" (P = 1)
+  return c;
+}
+
+}  // namespace
+
+bool BuildFilter(const std::vector<FilterItem>& items, uint32_t n_slots, uint32_t window, uint32_t n_buckets,
+                 FilterTables* out, std::string* err) {
+  if ((n_slots != 4 && n_slots != 8) || n_buckets == 0 || (n_slots * n_buckets) % 64 != 0 ||
+      n_slots * n_buckets > 256 || window == 0 || window > n_slots) {
+    *err = "unsupported prefilter shape";
+    return false;
+  }
+  *out = FilterTables();
+  out->n_buckets = n_buckets;
+  out->n_slots = n_slots;
+  out->n_words = n_slots * n_buckets / 64;
+  out->window = window;
+  const uint32_t S = window;
+  // identical byte-set sequences (rules sharing an anchor) become one item
+  std::vector<FilterItem> uniq;
+  std::vector<std::vector<uint32_t>> ids;
+  {
+    std::map<std::string, size_t> seen;
+    for (auto& it : items) {
+      std::string key(1, char(it.kind));
+      key += std::to_string(it.lit_end) + ":";
+      for (auto& b : it.sets) key += b.to_string();
+      auto f = seen.find(key);
+      if (f != seen.end() && ids[f->second].size() < 255) {
+        ids[f->second].push_back(it.id);
+        continue;
+      }
+      seen[key] = uniq.size();
+      uniq.push_back(it);
+      ids.push_back({it.id});
+    }
+  }
+  const size_t n = uniq.size();
+  // classes (deduplicated byte sets) and per-item windows
+  std::map<std::string, uint32_t> cls_ids;
+  std::vector<ByteSet> classes;
+  std::vector<Cluster> cl(n);
+  for (size_t i = 0; i < n; i++) {
+    const FilterItem& it = uniq[i];
+    if (it.sets.empty() || it.sets.size() > 0xFFFF) {
+      *err = "prefilter item with no (or too many) positions";
+      return false;
+    }
+    const size_t m = it.sets.size();
+    // least frequent window of <= kFilterSlots positions
+    size_t w = 0, wl = std::min<size_t>(m, S);
+    double best = std::numeric_limits<double>::infinity();
+    for (size_t s = 0; s + wl <= m; s++) {
+      double c = 1.0;
+      for (size_t q = s; q < s + wl; q++) c *= SetProb(it.sets[q]);
+      if (c < best) {
+        best = c;
+        w = s;
+      }
+    }
+    for (int s = 0; s < kFilterSlots; s++) cl[i].u[s].set();
+    for (size_t q = 0; q < wl; q++) cl[i].u[S - wl + q] = it.sets[w + q];
+    cl[i].members = {uint32_t(i)};
+    cl[i].cost = Cost(cl[i].u);
+    FilterItemGpu g{};
+    g.n = uint16_t(m);
+    g.back = uint16_t(w + wl);
+    g.lit_end = uint16_t(it.lit_end);
+    g.kind = it.kind;
+    g.n_ids = uint8_t(ids[i].size());
+    g.ids_off = uint32_t(out->item_ids.size());
+    out->item_ids.insert(out->item_ids.end(), ids[i].begin(), ids[i].end());
+    g.cls_off = uint32_t(out->item_cls.size());
+    out->max_after = std::max<uint32_t>(out->max_after, uint32_t(m - (w + wl)));
+    for (auto& b : it.sets) {
+      std::string key = b.to_string();
+      auto f = cls_ids.find(key);
+      uint32_t id;
+      if (f == cls_ids.end()) {
+        id = uint32_t(classes.size());
+        if (id >= 256) {
+          *err = "prefilter needs more than 256 distinct byte classes";
+          return false;
+        }
+        cls_ids[key] = id;
+        classes.push_back(b);
+      } else {
+        id = f->second;
+      }
+      out->item_cls.push_back(uint8_t(id));
+    }
+    out->items.push_back(g);
+  }
+  // agglomerative clustering down to n_buckets
+  std::vector<bool> alive(n, true);
+  size_t n_alive = n;
+  auto merged = [&](const Cluster& a, const Cluster& b, ByteSet* u) {
+    for (int s = 0; s < kFilterSlots; s++) u[s] = a.u[s] | b.u[s];
+    return Cost(u);
+  };
+  std::vector<std::vector<double>> delta(n, std::vector<double>(n, 0.0));
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = i + 1; j < n; j++) {
+      ByteSet u[kFilterSlots];
+      delta[i][j] = merged(cl[i], cl[j], u) - cl[i].cost - cl[j].cost;
+    }
+  while (n_alive > n_buckets) {
+    size_t bi = 0, bj = 0;
+    double bd = std::numeric_limits<double>::infinity();
+    for (size_t i = 0; i < n; i++) {
+      if (!alive[i]) continue;
+      for (size_t j = i + 1; j < n; j++)
+        if (alive[j] && delta[i][j] < bd) {
+          bd = delta[i][j];
+          bi = i;
+          bj = j;
+        }
+    }
+    ByteSet u[kFilterSlots];
+    double c = merged(cl[bi], cl[bj], u);
+    for (int s = 0; s < kFilterSlots; s++) cl[bi].u[s] = u[s];
+    cl[bi].cost = c;
+    cl[bi].members.insert(cl[bi].members.end(), cl[bj].members.begin(), cl[bj].members.end());
+    alive[bj] = false;
+    n_alive--;
+    for (size_t k = 0; k < n; k++) {
+      if (!alive[k] || k == bi) continue;
+      ByteSet v[kFilterSlots];
+      double d = merged(cl[bi], cl[k], v) - cl[bi].cost - cl[k].cost;
+      if (k < bi) delta[k][bi] = d;
+      else delta[bi][k] = d;
+    }
+  }
+  // reach table
+  const uint32_t W = out->n_words, bpw = 64 / n_slots;
+  out->reach.assign(256 * W, ~uint64_t(0));
+  out->bucket_off.push_back(0);
+  uint32_t j = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (!alive[i]) continue;
+    out->est_fp += cl[i].cost;
+    for (uint32_t s = 0; s < n_slots; s++)  // slots >= window: all bytes allowed (carry the fire)
+      for (int b = 0; b < 256; b++)
+        if (cl[i].u[s].test(b)) out->reach[size_t(b) * W + j / bpw] &= ~(uint64_t(1) << (s * bpw + (j % bpw)));
+    for (uint32_t m : cl[i].members) out->bucket_items.push_back(m);
+    out->bucket_off.push_back(uint32_t(out->bucket_items.size()));
+    j++;
+  }
+  while (j < n_buckets) {  // fewer items than buckets: empty buckets never fire
+    out->bucket_off.push_back(uint32_t(out->bucket_items.size()));
+    j++;
+  }
+  for (auto& b : classes) {
+    uint32_t w[8] = {};
+    for (int x = 0; x < 256; x++)
+      if (b.test(x)) w[x >> 5] |= 1u << (x & 31);
+    out->classes.insert(out->classes.end(), w, w + 8);
+  }
+  return true;
+}
+
+}  // namespace tsg

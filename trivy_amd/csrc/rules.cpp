@@ -1,6 +1,10 @@
 // Rule compiler (see rules.h).  Superset arguments are in DESIGN.md §2-3.
 #include "rules.h"
 
+#include <cstdlib>
+
+#include "filter.h"
+
 #include <algorithm>
 #include <array>
 #include <bitset>
@@ -139,6 +143,17 @@ struct Analyzer {
     }
   }
 
+  // Nodes of the leading literal run of a node's flattened sequence.
+  std::vector<int> LeadNodes(int i) {
+    std::vector<int> items, run;
+    Flatten(i, &items);
+    for (int it : items) {
+      if (LitChar(nodes[it]) < 0) break;
+      run.push_back(it);
+    }
+    return run;
+  }
+
   // Leading literal run of a node's flattened sequence ("" if none).
   std::string LeadLiteral(int i) {
     std::vector<int> items;
@@ -158,6 +173,9 @@ struct Cand {
   int64_t olo, ohi;
   int64_t ohi_fold = 0;
   std::vector<std::vector<int>> follow;  // per literal: flattened items after it
+  std::vector<std::vector<int>> lit_nodes;  // per literal: the class nodes of its chars
+  size_t pre_k = 0;                          // top-level flattened items before the literal(s)
+  std::vector<std::pair<std::string, std::vector<int>>> variants;  // every branch literal before dedupe
   size_t minlen() const {
     size_t m = SIZE_MAX;
     for (auto& l : lits) m = std::min(m, l.size());
@@ -188,6 +206,8 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
         Cand cd{{s}, olo, ohi};
         cd.ohi_fold = ohf;
         cd.follow.push_back(tail(j));
+        cd.lit_nodes.push_back(std::vector<int>(items.begin() + long(k), items.begin() + long(j)));
+        cd.pre_k = k;
         cands.push_back(cd);
       }
       // the literal chars themselves are 1 byte each normally, up to 3 when folded
@@ -211,6 +231,8 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
           Cand cd{{s}, olo, ohi};
           cd.ohi_fold = ohf;
           cd.follow.push_back({});
+          cd.lit_nodes.push_back(an.LeadNodes(sub));
+          cd.pre_k = k;
           cands.push_back(cd);
         }
       }
@@ -220,11 +242,13 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
       int an_node = in_repeat ? -2 - alt : alt;
       Cand cd{{}, olo, ohi};
       cd.ohi_fold = ohf;
+      cd.pre_k = k;
       bool ok = true;
       for (int b : re.nodes()[an_node].subs) {
         std::string s = an.LeadLiteral(b);
         if (s.empty()) { ok = false; break; }
         cd.lits.push_back(s);
+        cd.lit_nodes.push_back(an.LeadNodes(b));
         std::vector<int> bi;
         an.Flatten(b, &bi);
         std::vector<int> fol;
@@ -248,14 +272,22 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
   for (auto& cd : cands) {
     // dedupe literals (keep the first follow list of each)
     std::vector<std::string> L;
-    std::vector<std::vector<int>> F;
+    std::vector<std::vector<int>> F, N;
     for (size_t i = 0; i < cd.lits.size(); i++) {
-      if (std::find(L.begin(), L.end(), cd.lits[i]) != L.end()) continue;
+      cd.variants.push_back({cd.lits[i], cd.lit_nodes[i]});
+      auto it = std::find(L.begin(), L.end(), cd.lits[i]);
+      if (it != L.end()) {  // same case-folded literal in two branches: keep no lookahead
+        size_t at = size_t(it - L.begin());
+        if (F[at] != cd.follow[i]) F[at].clear();
+        continue;
+      }
       L.push_back(cd.lits[i]);
       F.push_back(cd.follow[i]);
+      N.push_back(cd.lit_nodes[i]);
     }
     cd.lits = L;
     cd.follow = F;
+    cd.lit_nodes = N;
     if (!have || cd.minlen() > best->minlen() ||
         (cd.minlen() == best->minlen() && cd.lits.size() < best->lits.size())) {
       *best = cd;
@@ -573,6 +605,111 @@ bool BuildAc(const std::vector<std::pair<std::string, uint32_t>>& pats, Compiled
   }
   return true;
 }
+// ---------------------------------------------------------------------------
+// prefilter items
+// ---------------------------------------------------------------------------
+// Byte set of a single-rune class as it can match in a file without fold
+// runes: its ASCII members.  False when the class has another non-ASCII member
+// (then the position's byte width is not fixed).
+bool ExactSet(const Node& n, ByteSet* out) {
+  if (n.op != NodeOp::Class) return false;
+  ByteSet s;
+  for (auto& p : n.ranges) {
+    for (uint32_t c = p.first; c <= p.second && c < 0x80; c++) s.set(c);
+    if (p.second >= 0x80) {
+      uint32_t a = std::max<uint32_t>(p.first, 0x80);
+      if (p.second - a > 0x10000) return false;
+      for (uint32_t c = a; c <= p.second; c++)
+        if (!IsFoldOnlyRune(c)) return false;
+    }
+  }
+  if (s.none()) return false;
+  *out = s;
+  return true;
+}
+
+// The fixed-width byte-set sequence of a node, if it has one (classes, fixed
+// repeats of them, concatenations, and alternations whose branches are such
+// sequences of one length -- the position-wise union).  `cap` bounds its length.
+bool FixedSets(const std::vector<Node>& nodes, int i, std::vector<ByteSet>* out, size_t cap) {
+  const Node& n = nodes[i];
+  switch (n.op) {
+    case NodeOp::Empty:
+    case NodeOp::Assert: return true;
+    case NodeOp::Class: {
+      ByteSet b;
+      if (!ExactSet(n, &b) || out->size() >= cap) return false;
+      out->push_back(b);
+      return true;
+    }
+    case NodeOp::Capture: return FixedSets(nodes, n.subs[0], out, cap);
+    case NodeOp::Cat:
+      for (int s : n.subs)
+        if (!FixedSets(nodes, s, out, cap)) return false;
+      return true;
+    case NodeOp::Repeat: {
+      if (n.max != n.min || n.min < 0) return false;
+      for (int r = 0; r < n.min; r++)
+        if (!FixedSets(nodes, n.subs[0], out, cap)) return false;
+      return true;
+    }
+    case NodeOp::Alt: {
+      std::vector<ByteSet> u;
+      bool first = true;
+      for (int s : n.subs) {
+        std::vector<ByteSet> b;
+        if (!FixedSets(nodes, s, &b, cap)) return false;
+        if (first) u = b;
+        else if (b.size() != u.size()) return false;
+        else
+          for (size_t k = 0; k < u.size(); k++) u[k] |= b[k];
+        first = false;
+      }
+      if (out->size() + u.size() > cap) return false;
+      out->insert(out->end(), u.begin(), u.end());
+      return true;
+    }
+    default: return false;
+  }
+}
+
+// Mandatory fixed-width sets right after a literal (up to `cap`): whole fixed
+// items, then the mandatory part of the first variable repeat of a class.
+std::vector<ByteSet> AfterSets(const std::vector<Node>& nodes, const std::vector<int>& fol, size_t cap) {
+  std::vector<ByteSet> out;
+  for (int it : fol) {
+    if (out.size() >= cap) break;
+    std::vector<ByteSet> b;
+    if (FixedSets(nodes, it, &b, cap - out.size())) {
+      out.insert(out.end(), b.begin(), b.end());
+      continue;
+    }
+    const Node& n = nodes[it];
+    if (n.op == NodeOp::Repeat && n.min >= 1) {
+      std::vector<ByteSet> one;
+      if (FixedSets(nodes, n.subs[0], &one, cap)) {
+        for (int r = 0; r < n.min && out.size() + one.size() <= cap; r++) out.insert(out.end(), one.begin(), one.end());
+      }
+    }
+    break;
+  }
+  if (out.size() > cap) out.resize(cap);
+  return out;
+}
+
+// Mandatory fixed-width sets right before top-level item `k` (up to `cap`).
+std::vector<ByteSet> BeforeSets(const std::vector<Node>& nodes, const std::vector<int>& items, size_t k, size_t cap) {
+  std::vector<ByteSet> out;  // reversed
+  for (size_t q = k; q-- > 0;) {
+    std::vector<ByteSet> b;
+    if (!FixedSets(nodes, items[q], &b, 64)) break;
+    for (size_t r = b.size(); r-- > 0 && out.size() < cap;) out.push_back(b[r]);
+    if (out.size() >= cap) break;
+  }
+  std::reverse(out.begin(), out.end());
+  return out;
+}
+
 }  // namespace
 
 bool KeywordImplied(const Regex& re, const std::string& kw) {
@@ -679,7 +816,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
         id = uint32_t(out->keywords.size());
         kw_ids[l] = id;
         out->keywords.push_back(l);
-        if (!l.empty()) pats.push_back({l, kOutKeyword | id});
+
       } else {
         id = it->second;
       }
@@ -735,6 +872,30 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
           }
           ai.ext = ext_chars.empty() ? 0 : 1;
           out->anchors.push_back(ai);
+          {  // prefilter item: prefix sets + literal sets (union over same-folded variants) + lookahead sets
+            FilterItem fi;
+            fi.kind = kItemAnchor;
+            fi.id = aid;
+            std::vector<int> top;
+            Analyzer(re->nodes(), false).Flatten(re->root(), &top);
+            fi.sets = BeforeSets(re->nodes(), top, best.pre_k, 16);
+            std::vector<ByteSet> lit(l.size());
+            for (auto& v : best.variants) {
+              if (v.first != l) continue;
+              for (size_t q = 0; q < l.size() && q < v.second.size(); q++) {
+                ByteSet b;
+                if (ExactSet(re->nodes()[v.second[q]], &b)) lit[q] |= b;
+                else lit[q].set();
+              }
+            }
+            for (auto& b : lit)
+              if (b.none()) b.set();
+            fi.sets.insert(fi.sets.end(), lit.begin(), lit.end());
+            fi.lit_end = uint32_t(fi.sets.size());
+            auto after = AfterSets(re->nodes(), best.follow[li], 16);
+            fi.sets.insert(fi.sets.end(), after.begin(), after.end());
+            out->items.push_back(std::move(fi));
+          }
           if (ext_chars.empty()) {
             pats.push_back({l, kOutAnchor | aid});
           } else {
@@ -751,6 +912,30 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     out->rule_anchor_desc.push_back(desc);
     out->rules.push_back(rg);
     out->regex.push_back(std::move(re));
+  }
+  {  // fold runes: files holding them take the careful path
+    const char* seqs[3] = {"\xC4\xB0", "\xE2\x84\xAA", "\xC5\xBF"};
+    for (uint32_t k = 0; k < 3; k++) {
+      FilterItem fi;
+      fi.kind = kItemFold;
+      fi.id = k;
+      for (const char* p = seqs[k]; *p; p++) {
+        ByteSet b;
+        b.set(uint8_t(*p));
+        fi.sets.push_back(b);
+      }
+      fi.lit_end = uint32_t(fi.sets.size());
+      out->items.push_back(std::move(fi));
+    }
+  }
+  {
+    uint32_t nb = 16, ns = 8, nw = 6;
+    if (const char* e = std::getenv("TSG_FILTER_BUCKETS")) nb = uint32_t(std::atoi(e));
+    if (const char* e = std::getenv("TSG_FILTER_SLOTS")) ns = uint32_t(std::atoi(e));
+    if (const char* e = std::getenv("TSG_FILTER_WINDOW")) nw = uint32_t(std::atoi(e));
+    auto ft = std::make_shared<FilterTables>();
+    if (!BuildFilter(out->items, ns, nw, nb, ft.get(), err)) return false;
+    out->filter = ft;
   }
   return BuildAc(pats, out, err);
 }

@@ -13,6 +13,7 @@
 //     alternations -> column unions / class runs, large repeats -> unbounded).
 #pragma once
 #include <cstdint>
+#include <bitset>
 #include <memory>
 #include <string>
 #include <vector>
@@ -66,6 +67,21 @@ struct RuleGpu {  // mirrored on the device
   uint32_t kw_off, kw_cnt;  // into rule_kw
 };
 
+// Prefilter item: a fixed-width sequence of byte sets that
+// every occurrence of a keyword (ASCII case-insensitive), an anchor literal
+// (with the mandatory single-width classes right before and after it) or a
+// fold rune (C4 B0 / E2 84 AA / C5 BF) matches byte for byte in files without
+// fold runes.  The streaming filter runs bucketed shift-or over windows of
+// these sequences; the confirm pass checks every position exactly.
+using ByteSet = std::bitset<256>;
+enum ItemKind : uint8_t { kItemKeyword = 0, kItemAnchor = 1, kItemFold = 2 };
+struct FilterItem {
+  uint8_t kind;
+  uint32_t id;       // keyword id / anchor id / fold rune (0 U+0130, 1 U+212A, 2 U+017F)
+  uint32_t lit_end;  // anchors: positions from the item start to the literal end
+  std::vector<ByteSet> sets;
+};
+
 struct CompiledRules {
   // Aho-Corasick
   uint32_t n_states = 0, n_classes = 0, max_pat_len = 0;
@@ -82,6 +98,8 @@ struct CompiledRules {
   std::vector<uint32_t> rule_kw;  // keyword ids
   std::vector<uint64_t> nfa;      // per rule: O[W] L[W] F[W] B[256][W]
   std::vector<std::string> rule_anchor_desc;  // debug text
+  std::vector<FilterItem> items;  // prefilter items (keywords, anchors, fold runes)
+  std::shared_ptr<const struct FilterTables> filter;  // built from items (filter.h)
   std::vector<std::unique_ptr<Regex>> regex;  // exact engines (host pass)
   uint32_t n_fullscan_rules = 0;
   uint32_t n_redundant_gates = 0;

@@ -392,9 +392,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     uint32_t r = c[i].rule;
     size_t j = i;
     std::vector<Window> wins;
-    bool cand_host_gate = false;
     while (j < nc && c[j].rule == r) {
-      if (c[j].flags & kCandHostGate) cand_host_gate = true;
       Window w{c[j].wlo, c[j].whi};
       if (!wins.empty() && w.lo <= wins.back().hi + 1) wins.back().hi = std::max(wins.back().hi, w.hi);
       else wins.push_back(w);
@@ -406,24 +404,38 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     if (!re) continue;
     if (R.path && !R.path->Match(P, path.size())) continue;                      // MatchPath :397
     if (AllowRulesAllowPath(R.allow_rules, P, path.size())) continue;            // AllowPath :403
-    if (cr_.rules[r].gate == kGateHost ||
-        (cand_host_gate && cr_.rules[r].gate != kGateAlways)) {                   // MatchKeywords :409
-      if (!lowered_done) {
-        lowered = GoBytesToLower(content, size_t(len));
-        lowered_done = true;
-      }
-      bool hit = false;
-      for (auto& kw : R.kw_lower_host)
-        if (lowered.find(kw) != std::string::npos) {
-          hit = true;
-          break;
-        }
-      if (!hit) continue;
-    }
     bool sub = !R.secret_group_name.empty();
     std::vector<int64_t> m;
     re->FindAll(content, len, sub, &wins, &m);
+    if (m.empty()) continue;
     size_t stride = sub ? size_t(2 * (re->num_cap() + 1)) : 2;
+    // MatchKeywords (:409), evaluated lazily: it only matters when FindLocations
+    // has matches.  A match is a run of whole runes of the content, so a
+    // keyword inside its lowered bytes is inside bytes.ToLower(content) too;
+    // otherwise the whole content is lowered and searched.
+    if (cr_.rules[r].gate != kGateAlways) {
+      bool hit = false;
+      for (size_t k = 0; k + stride <= m.size() && !hit; k += stride) {
+        std::string ml = GoBytesToLower(content + m[k], size_t(m[k + 1] - m[k]));
+        for (auto& kw : R.kw_lower_host)
+          if (ml.find(kw) != std::string::npos) {
+            hit = true;
+            break;
+          }
+      }
+      if (!hit) {
+        if (!lowered_done) {
+          lowered = GoBytesToLower(content, size_t(len));
+          lowered_done = true;
+        }
+        for (auto& kw : R.kw_lower_host)
+          if (lowered.find(kw) != std::string::npos) {
+            hit = true;
+            break;
+          }
+      }
+      if (!hit) continue;
+    }
     std::vector<Loc> locs;
     for (size_t k = 0; k + stride <= m.size(); k += stride) {
       int64_t s = m[k], e = m[k + 1];

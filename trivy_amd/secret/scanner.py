@@ -48,7 +48,8 @@ class _CStats(c.Structure):
                                           "findings")] + \
                [(n, c.c_double) for n in ("ms_scan_kernel", "ms_verify_kernel", "ms_fullscan_kernel",
                                           "ms_gpu_total", "ms_host_gpu_phase", "ms_host_allow_path",
-                                          "ms_host_exact", "ms_host_total")]
+                                          "ms_host_exact", "ms_host_total")] + \
+               [("flagged_blocks", c.c_uint64), ("ms_careful_kernel", c.c_double)]
 
 
 class _CTableInfo(c.Structure):
