@@ -4,7 +4,8 @@
 Workload (configs[1]): builtin ruleset (87 rules) over a synthetic mixed-text
 corpus of --gb GB per GPU (default 20), generated deterministically on the host
 (seed 0x5EC2E7), copied once into HBM.  A "step" is one full
-Scan of that corpus: K1 keyword/anchor scan + K2 NFA verify + full-scan tasks +
+Scan of that corpus: K1 streaming prefilter + confirm, the careful pass over fold-rune files,
+K2 NFA verify, full-scan tasks and
 the exact host pass (windowed Go-regexp, allow/exclude, censoring, findings,
 sort).  Inputs are resident in HBM when the timed region starts; findings
 come out as C++ structs (types.Secret equivalents).
@@ -178,15 +179,17 @@ def main():
             "config": {"workload": "builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per "
                                    "MI355X (BASELINE configs[1])" % args.gb,
                        "bytes_per_gpu": n_bytes, "files_per_gpu": C.n_files, "parallelism": "files sharded, dp%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "scan_kernel (K1)", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": "filter_kernel (K1)", "achieved": round(achieved, 2),
                          "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 4),
                          "traffic": traffic},
             "cpu_baseline": cpu,
-            "breakdown_ms": {k: round(last[k], 3) for k in ("ms_scan_kernel", "ms_verify_kernel",
-                                                           "ms_fullscan_kernel", "ms_gpu_total",
+            "breakdown_ms": {k: round(last[k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel",
+                                                           "ms_verify_kernel", "ms_fullscan_kernel",
+                                                           "ms_gpu_total",
                                                            "ms_host_gpu_phase", "ms_host_allow_path",
                                                            "ms_host_exact", "ms_host_total")},
-            "counts": {k: int(last[k]) for k in ("anchor_hits", "candidates", "special_files", "findings")},
+            "counts": {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "candidates", "special_files",
+                                                 "findings")},
             "gen_s": round(t_gen, 2),
         }
         print(json.dumps(out), flush=True)
