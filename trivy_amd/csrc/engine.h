@@ -83,7 +83,7 @@ class GpuEngine {
   uint64_t* d_reach_ = nullptr;
   void* d_ftabs_ = nullptr;
   uint32_t f_words_ = 0, ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
-  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, filter_wg_per_cu_ = 1;
+  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, filter_wg_per_cu_ = 1, f_lane_ = 64;
   size_t f_lds_bytes_ = 0;
   // per-batch buffers
   void* d_chunk_file_ = nullptr; size_t cap_chunk_file_ = 0;

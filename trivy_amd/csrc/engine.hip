@@ -470,13 +470,9 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
 // ---------------------------------------------------------------------------
 // K1: streaming bucketed shift-or filter + exact confirm
 // ---------------------------------------------------------------------------
-constexpr int kFLaneBytes = 128;                 // bytes per lane per tile (8 blocks of 16 B)
-constexpr int kFBlocks = kFLaneBytes / 16;
-constexpr int kFTile = 64 * kFLaneBytes;         // 8 KiB per wave tile
 constexpr int kFQueue = 128;                     // per-wave flagged-block queue (drained at >= 64)
 constexpr int kFWaveHits = 128;                  // per-wave LDS hit records
 constexpr int kFWindow = 6;                      // filter window; checks every 9 - kFWindow = 3 bytes
-static_assert(kChunk % kFLaneBytes == 0, "a newline chunk must be whole lane chunks");
 
 struct FilterParams {
   const uint8_t* arena;
@@ -511,19 +507,24 @@ struct FilterTabs {  // LDS copies
 // u32 halves); the LDS table row of byte b is 256 B (16 copies of a 16-B
 // entry for W = 2, 32 copies of 8 B for W = 1), the copy chosen by lane, so a
 // wave's reads never conflict.  `laneoff` sits in the address's low byte.
+__device__ __forceinline__ void shift_or(uint32_t& lo, uint32_t& hi, uint32_t mlo, uint32_t mhi) {
+  // hi = (hi << 8 | lo >> 24) | mhi ; lo = lo << 8 | mlo   (3 VALU ops)
+  uint32_t h;
+  asm("v_alignbit_b32 %0, %1, %2, 24" : "=v"(h) : "v"(hi), "v"(lo));
+  asm("v_or_b32 %0, %1, %2" : "=v"(hi) : "v"(h), "v"(mhi));
+  asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(lo) : "v"(lo), "v"(mlo));
+}
+
 template <int W>
 __device__ __forceinline__ void fstep(uint32_t w, uint32_t k, uint32_t laneoff, const uint8_t* sb, uint32_t* st) {
   const uint32_t addr = __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8));
   if constexpr (W == 2) {
     const uint4 m = *reinterpret_cast<const uint4*>(sb + addr);
-    st[1] = __builtin_amdgcn_alignbit(st[1], st[0], 24) | m.y;
-    st[0] = (st[0] << 8) | m.x;
-    st[3] = __builtin_amdgcn_alignbit(st[3], st[2], 24) | m.w;
-    st[2] = (st[2] << 8) | m.z;
+    shift_or(st[0], st[1], m.x, m.y);
+    shift_or(st[2], st[3], m.z, m.w);
   } else {
     const uint2 m = *reinterpret_cast<const uint2*>(sb + addr);
-    st[1] = __builtin_amdgcn_alignbit(st[1], st[0], 24) | m.y;
-    st[0] = (st[0] << 8) | m.x;
+    shift_or(st[0], st[1], m.x, m.y);
   }
 }
 
@@ -666,11 +667,15 @@ __device__ __forceinline__ void drain_flagged(const FilterParams& P, const Filte
 // ballot/mbcnt-compacted per-wave LDS queue; at 64 the wave confirms them in
 // parallel (one block per lane).  '\n' is counted per 1-KiB chunk (SWAR +
 // an 8-lane reduction) for the verify kernel's line numbers.
-template <int W>
+template <int W, int LB>
 __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
+  constexpr int kFBlocks = LB / 16;
+  constexpr int kFTile = 64 * LB;  // bytes per wave tile
+  static_assert(kChunk % LB == 0 && (kChunk / LB) <= 64, "a newline chunk must be whole lane chunks");
+  // the reach table sits at LDS address 0 (static), so table reads need no base add
+  __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* s_reach = smem;                                        // 64 KiB
-  uint8_t* s_tabs = smem + 65536;
+  uint8_t* s_tabs = smem;
   uint32_t* s_queue = reinterpret_cast<uint32_t*>(s_tabs + P.tabs_bytes);
   uint32_t* s_hits = s_queue + kScanWaves * kFQueue;
   uint32_t* s_hcnt = s_hits + kScanWaves * kFWaveHits * 3;
@@ -709,7 +714,7 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   uint4 cur[kFBlocks], nxt[kFBlocks];
   uint2 pre = make_uint2(0, 0), pnx = make_uint2(0, 0);
   auto load_tile = [&](uint4* dst, uint2* pv, uint64_t tt) {
-    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLaneBytes;
+    const uint64_t b0 = tt * kFTile + uint64_t(lane) * LB;
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
       const uint64_t p = b0 + 16 * j;
@@ -720,9 +725,9 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   if (t < n_tiles) load_tile(cur, &pre, t);
   for (; t < n_tiles; t += n_waves) {
     if (t + n_waves < n_tiles) load_tile(nxt, &pnx, t + n_waves);
-    const uint64_t b0 = t * kFTile + uint64_t(lane) * kFLaneBytes;
+    const uint64_t b0 = t * kFTile + uint64_t(lane) * LB;
     // bytes past the arena end (last tile only) are zeroed
-    if (b0 + kFLaneBytes > P.n_bytes) {
+    if (b0 + LB > P.n_bytes) {
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint64_t p = b0 + 16 * j;
@@ -765,10 +770,9 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++)
       nl += nl_in_word(cur[j].x) + nl_in_word(cur[j].y) + nl_in_word(cur[j].z) + nl_in_word(cur[j].w);
-    nl += __shfl_xor(nl, 1);
-    nl += __shfl_xor(nl, 2);
-    nl += __shfl_xor(nl, 4);
-    if ((lane & 7) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
+#pragma unroll
+    for (int x = 1; x < int(kChunk / LB); x <<= 1) nl += __shfl_xor(nl, x);
+    if ((lane & (kChunk / LB - 1)) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
     // queue the flagged blocks
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
@@ -792,16 +796,23 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   if (qn) drain_flagged<W>(P, T, s_reach, laneoff, Q, qn, hbuf, hcnt, lane);
 }
 
-// Chunk list of the files K1 found fold runes in (for the careful pass).
-__global__ void special_chunks_kernel(const uint64_t* __restrict__ off, const uint32_t* __restrict__ special,
-                                      uint32_t* __restrict__ counters, uint32_t* __restrict__ list, uint32_t cap) {
+// Chunk list of the files K1 found fold runes in (for the careful pass): one
+// workgroup per file reserves the file's chunk range, its threads fill it.
+__global__ __launch_bounds__(256) void special_chunks_kernel(const uint64_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ special,
+                                                             uint32_t* __restrict__ counters,
+                                                             uint32_t* __restrict__ list, uint32_t cap) {
+  __shared__ uint32_t s_base;
   const uint32_t n = counters[2];
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t f = special[i];
     const uint64_t c0 = off[f] / kChunk, c1 = (off[f + 1] - 1) / kChunk;
-    const uint32_t k = atomicAdd(&counters[5], uint32_t(c1 - c0 + 1));
-    for (uint64_t c = c0; c <= c1; c++)
+    if (threadIdx.x == 0) s_base = atomicAdd(&counters[5], uint32_t(c1 - c0 + 1));
+    __syncthreads();
+    const uint32_t k = s_base;
+    for (uint64_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x)
       if (k + (c - c0) < cap) list[k + (c - c0)] = uint32_t(c);
+    __syncthreads();
   }
 }
 
@@ -962,6 +973,14 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
                nfa_dispatch(rg.nfa_words, P.arena + fs, len, 0, len, P.nfa + rg.nfa_off);
     if (acc) emit_candidate(P, f, r, 0, len, 0, 0u);
   }
+}
+
+const void* FilterFn(uint32_t words, uint32_t lane_bytes) {
+  if (words == 2)
+    return lane_bytes == 128 ? reinterpret_cast<const void*>(&filter_kernel<2, 128>)
+                             : reinterpret_cast<const void*>(&filter_kernel<2, 64>);
+  return lane_bytes == 128 ? reinterpret_cast<const void*>(&filter_kernel<1, 128>)
+                           : reinterpret_cast<const void*>(&filter_kernel<1, 64>);
 }
 
 template <typename T>
@@ -1184,15 +1203,16 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     uint8_t* d = nullptr;
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_ftabs_ = d;
-    f_lds_bytes_ = 65536 + ftabs_bytes_ + size_t(kScanWaves) * kFQueue * 4 + size_t(kScanWaves) * kFWaveHits * 12 +
+    // dynamic LDS: tables + queues + hit buffers (the 64-KiB reach table is static)
+    f_lds_bytes_ = ftabs_bytes_ + size_t(kScanWaves) * kFQueue * 4 + size_t(kScanWaves) * kFWaveHits * 12 +
                    size_t(kScanWaves) * 4;
-    if (f_lds_bytes_ > 160 * 1024) {
+    if (65536 + f_lds_bytes_ > 160 * 1024) {
       err_ = "prefilter tables do not fit in LDS";
       return;
     }
-    const void* ff = f_words_ == 2 ? reinterpret_cast<const void*>(&filter_kernel<2>)
-                                   : reinterpret_cast<const void*>(&filter_kernel<1>);
-    hipFuncSetAttribute(ff, hipFuncAttributeMaxDynamicSharedMemorySize, int(f_lds_bytes_));
+    if (const char* e = std::getenv("TSG_FILTER_LANE")) f_lane_ = uint32_t(std::atoi(e));
+    if (f_lane_ != 64 && f_lane_ != 128) f_lane_ = 64;
+    hipFuncSetAttribute(FilterFn(f_words_, f_lane_), hipFuncAttributeMaxDynamicSharedMemorySize, int(f_lds_bytes_));
   }
 }
 
@@ -1290,16 +1310,18 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fp.hits = static_cast<uint32_t*>(d_hits_);
     fp.hit_cap = hit_cap_;
     fp.counters = d_counters_;
-    const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
+    const uint64_t f_tiles = (n_bytes + 64 * f_lane_ - 1) / (64 * f_lane_);
     const uint32_t f_grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves,
                                                                             uint64_t(256) * filter_wg_per_cu_)));
     HIP_OK(hipEventRecord(ev_[0], stream_));
-    if (f_words_ == 2) filter_kernel<2><<<f_grid, kScanThreads, f_lds_bytes_, stream_>>>(fp);
-    else filter_kernel<1><<<f_grid, kScanThreads, f_lds_bytes_, stream_>>>(fp);
-    HIP_OK(hipGetLastError());
+    {
+      void* kargs[] = {&fp};
+      HIP_OK(hipLaunchKernel(FilterFn(f_words_, f_lane_), dim3(f_grid), dim3(kScanThreads), kargs, f_lds_bytes_,
+                             stream_));
+    }
     HIP_OK(hipEventRecord(ev_[1], stream_));
     // careful pass over the chunks of fold-rune files (Aho-Corasick on the bytes.ToLower symbol stream)
-    special_chunks_kernel<<<64, 256, 0, stream_>>>(d_offsets, static_cast<const uint32_t*>(d_special_), d_counters_,
+    special_chunks_kernel<<<1024, 256, 0, stream_>>>(d_offsets, static_cast<const uint32_t*>(d_special_), d_counters_,
                                                    static_cast<uint32_t*>(d_chunk_list_), list_cap);
     ScanParams sp;
     sp.arena = d_arena;
@@ -1345,7 +1367,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     sp.chunk_list_cap = list_cap;
     {
       uint32_t per_cu = std::max<uint32_t>(1, uint32_t((160 * 1024) / lds_bytes_));
-      uint32_t grid = 64 * per_cu;
+      uint32_t grid = 256 * per_cu;
       if (wide_table_) {
         if (table_in_lds_) scan_kernel<uint32_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
         else scan_kernel<uint32_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
