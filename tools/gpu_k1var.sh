@@ -14,3 +14,7 @@ print("lane",sys.argv[2],"diag",sys.argv[3],"value",d["value"],"K1",d["breakdown
 PY
   done
 done
+if [ -n "${DUMP_GB:-}" ]; then
+  TSG_DUMP_CANDS=gpurun_out/cands_${DUMP_GB}g.bin timeout -k 10 300 python bench.py --gb $DUMP_GB --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dump.json 2> gpurun_out/dump.err || exit $?
+  cat gpurun_out/dump.json; ls -la gpurun_out/cands_${DUMP_GB}g.bin
+fi

@@ -27,6 +27,7 @@ namespace tsg {
 namespace {
 
 constexpr int kScanThreads = 1024;
+constexpr uint32_t kCarefulUnit = 256;  // bytes per lane in the careful pass
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kQueue = 320;    // per-wave replay queue (entries): kFlushAt + 4 * 64 - 1 fit
 constexpr int kFlushAt = 64;   // drain when this many blocks wait (each iteration adds <= 64)
@@ -383,15 +384,17 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
   uint32_t qn = 0;  // wave-uniform
   const uint32_t thr = P.thr;
   // load groups per lane, rounded up to an even count (blocks past b1 are skipped)
-  const uint32_t ngroups = ((P.warm_blocks + kChunk / 16 + kGroup - 1) / kGroup + 1) & ~1u;
+  // careful mode scans 256-B units (more lanes for the few fold-rune files); full mode 1-KiB chunks
+  const uint32_t unit = P.chunk_list ? kCarefulUnit : kChunk;
+  const uint32_t ngroups = ((P.warm_blocks + unit / 16 + kGroup - 1) / kGroup + 1) & ~1u;
   const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
 
   for (uint64_t tile = uint64_t(blockIdx.x) * kScanWaves + wave; tile * 64 < n_work; tile += n_waves) {
     const uint64_t idx = tile * 64 + lane;
     const bool live = idx < n_work;
     const uint64_t c = P.chunk_list ? P.chunk_list[live ? idx : n_work - 1] : idx;
-    const uint64_t b0 = c * kChunk;
-    const uint64_t b1 = live ? (b0 + kChunk < P.n_bytes ? b0 + kChunk : P.n_bytes) : 0;
+    const uint64_t b0 = c * unit;
+    const uint64_t b1 = live ? (b0 + unit < P.n_bytes ? b0 + unit : P.n_bytes) : 0;
     const int64_t pstart = int64_t(b0) - int64_t(P.warm_blocks) * 16;
     uint32_t st = 0, nl = 0;
     // loads are unconditional (clamped address) so the waits stay countable
@@ -526,6 +529,35 @@ __device__ __forceinline__ void fstep(uint32_t w, uint32_t k, uint32_t laneoff, 
     const uint2 m = *reinterpret_cast<const uint2*>(sb + addr);
     shift_or(st[0], st[1], m.x, m.y);
   }
+}
+
+template <int W>
+struct ReachVec;
+template <>
+struct ReachVec<2> {
+  using T = uint4;
+  static __device__ __forceinline__ T read(const uint8_t* sb, uint32_t w, uint32_t k, uint32_t laneoff) {
+    return *reinterpret_cast<const uint4*>(sb + __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8)));
+  }
+  static __device__ __forceinline__ void apply(const T& m, uint32_t* st) {
+    shift_or(st[0], st[1], m.x, m.y);
+    shift_or(st[2], st[3], m.z, m.w);
+  }
+};
+template <>
+struct ReachVec<1> {
+  using T = uint2;
+  static __device__ __forceinline__ T read(const uint8_t* sb, uint32_t w, uint32_t k, uint32_t laneoff) {
+    return *reinterpret_cast<const uint2*>(sb + __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8)));
+  }
+  static __device__ __forceinline__ void apply(const T& m, uint32_t* st) { shift_or(st[0], st[1], m.x, m.y); }
+};
+
+// '\n' bytes in a word: x = w ^ 0x0A.. is zero exactly in newline bytes; bit 7
+// of ((x & 0x7F..) + 0x7F..) | w marks the nonzero ones (bit 7 of x is w's).
+__device__ __forceinline__ uint32_t nl_count4(uint32_t w) {
+  const uint32_t a = ((w ^ 0x0A0A0A0Au) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return __popc(~(a | w) & 0x80808080u);
 }
 
 template <int W>
@@ -758,10 +790,14 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint32_t wd[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+        // all 16 table reads of the block first (independent of the state), then the chain
+        typename ReachVec<W>::T m[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) m[k] = ReachVec<W>::read(s_reach, wd[k >> 2], k & 3, laneoff);
         uint32_t acc = ~0u;
 #pragma unroll
         for (uint32_t k = 0; k < 16; k++) {
-          fstep<W>(wd[k >> 2], k & 3, laneoff, s_reach, st);
+          ReachVec<W>::apply(m[k], st);
           if (k % 3 == 2 || k == 15) acc &= ftop<W>(st);
         }
         flagged |= uint32_t((acc | 0xFFu) != ~0u) << j;
@@ -769,7 +805,7 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     }
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++)
-      nl += nl_in_word(cur[j].x) + nl_in_word(cur[j].y) + nl_in_word(cur[j].z) + nl_in_word(cur[j].w);
+      nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
 #pragma unroll
     for (int x = 1; x < int(kChunk / LB); x <<= 1) nl += __shfl_xor(nl, x);
     if ((lane & (kChunk / LB - 1)) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
@@ -806,7 +842,7 @@ __global__ __launch_bounds__(256) void special_chunks_kernel(const uint64_t* __r
   const uint32_t n = counters[2];
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t f = special[i];
-    const uint64_t c0 = off[f] / kChunk, c1 = (off[f + 1] - 1) / kChunk;
+    const uint64_t c0 = off[f] / kCarefulUnit, c1 = (off[f + 1] - 1) / kCarefulUnit;
     if (threadIdx.x == 0) s_base = atomicAdd(&counters[5], uint32_t(c1 - c0 + 1));
     __syncthreads();
     const uint32_t k = s_base;
@@ -1268,7 +1304,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   if (n_chunks == 0) n_chunks = 1;
   if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 256, 1 << 16), 1u << 30));
   if (cand_cap_ == 0) cand_cap_ = 1 << 16;
-  const uint32_t list_cap = uint32_t(std::min<uint64_t>(n_chunks + n_files, 0xFFFFFFF0u));
+  const uint32_t list_cap =
+      uint32_t(std::min<uint64_t>((n_bytes + kCarefulUnit - 1) / kCarefulUnit + n_files, 0xFFFFFFF0u));
   for (int attempt = 0; attempt < 8; attempt++) {
     if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, n_chunks * 2) ||
         !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
