@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 
 namespace tsg {
@@ -346,6 +347,98 @@ bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
 }
 
 namespace {
+bool HasSeq(const uint8_t* s, size_t n, const char* seq, size_t k) {  // memchr on the lead byte
+  const uint8_t* p = s;
+  const uint8_t* e = s + n;
+  while (p + k <= e) {
+    const void* q = std::memchr(p, uint8_t(seq[0]), size_t(e - p) - (k - 1));
+    if (!q) return false;
+    p = static_cast<const uint8_t*>(q);
+    if (std::memcmp(p, seq, k) == 0) return true;
+    p++;
+  }
+  return false;
+}
+
+// bytes.ToLower(content) contains the lowercase ASCII kw, for content holding
+// U+0130 / U+212A: every kw char matches an ASCII byte of either case, and
+// 'i' also C4 B0 (U+0130 lowers to 'i'), 'k' also E2 84 AA (U+212A lowers to
+// 'k'); no other rune lowers into ASCII and these byte sequences always decode
+// as those runes.
+bool FoldCaseContains(const uint8_t* s, size_t n, const std::string& kw) {
+  const size_t m = kw.size();
+  if (m == 0) return true;
+  for (size_t st = 0; st < n; st++) {
+    size_t p = st, i = 0;
+    for (; i < m && p < n; i++) {
+      uint8_t c = s[p];
+      if (c >= 'A' && c <= 'Z') c = uint8_t(c + 32);
+      if (c == uint8_t(kw[i])) {
+        p++;
+        continue;
+      }
+      if (kw[i] == 'i' && c == 0xC4 && p + 1 < n && s[p + 1] == 0xB0) {
+        p += 2;
+        continue;
+      }
+      if (kw[i] == 'k' && c == 0xE2 && p + 2 < n && s[p + 1] == 0x84 && s[p + 2] == 0xAA) {
+        p += 3;
+        continue;
+      }
+      break;
+    }
+    if (i == m) return true;
+  }
+  return false;
+}
+
+// Is the lowercase ASCII string kw a substring of the content with ASCII letters
+// case-folded?  Scans with memchr for kw's least frequent character (both cases).
+bool AsciiCaseContains(const uint8_t* s, size_t n, const std::string& kw) {
+  const size_t m = kw.size();
+  if (m == 0) return true;
+  if (n < m) return false;
+  static const char* kFreq = "etaoinshrdlcumwfgypbvkjxqz";  // English letter order
+  size_t best = 0;
+  int best_rank = -1;
+  for (size_t i = 0; i < m; i++) {
+    const char c = kw[i];
+    const char* f = (c >= 'a' && c <= 'z') ? std::strchr(kFreq, c) : nullptr;
+    const int rank = f ? int(f - kFreq) : 100;  // non-letters are rarest
+    if (rank > best_rank) {
+      best_rank = rank;
+      best = i;
+    }
+  }
+  auto eq_at = [&](const uint8_t* p) {  // p = candidate start
+    for (size_t i = 0; i < m; i++) {
+      uint8_t c = p[i];
+      if (c >= 'A' && c <= 'Z') c = uint8_t(c + 32);
+      if (c != uint8_t(kw[i])) return false;
+    }
+    return true;
+  };
+  const uint8_t c0 = uint8_t(kw[best]);
+  const int passes = (c0 >= 'a' && c0 <= 'z') ? 2 : 1;
+  for (int pass = 0; pass < passes; pass++) {
+    const uint8_t c = pass ? uint8_t(c0 - 32) : c0;
+    const uint8_t* p = s + best;
+    const uint8_t* e = s + n - (m - 1 - best);  // last valid position of the scanned char + 1
+    while (p < e) {
+      const void* q = std::memchr(p, c, size_t(e - p));
+      if (!q) break;
+      const uint8_t* hitp = static_cast<const uint8_t*>(q);
+      if (eq_at(hitp - best)) return true;
+      p = hitp + 1;
+    }
+  }
+  return false;
+}
+bool IsAsciiStr(const std::string& s) {
+  for (unsigned char c : s)
+    if (c >= 0x80) return false;
+  return true;
+}
 bool AllowRulesAllow(const std::vector<AllowRuleSpec>& rules, const uint8_t* s, size_t n) {
   for (auto& a : rules)
     if (a.regex && a.regex->Match(s, n)) return true;
@@ -358,6 +451,16 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 }
 }  // namespace
 
+std::atomic<int64_t> g_prof[8];
+struct PhaseTimer {
+  int k;
+  std::chrono::steady_clock::time_point t0;
+  explicit PhaseTimer(int kk) : k(kk), t0(std::chrono::steady_clock::now()) {}
+  ~PhaseTimer() {
+    g_prof[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  }
+};
+
 void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
                              const Candidate* c, size_t nc, FileResult* out) const {
   const uint8_t* P = reinterpret_cast<const uint8_t*>(path.data());
@@ -367,6 +470,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   std::vector<Loc> gblocks;
   std::string lowered;
   bool lowered_done = false;
+  bool fold_done = false, fold_runes = false;
   // (wlo, nl_before) anchors for line numbers
   std::vector<std::pair<int64_t, int64_t>> nla;
   for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
@@ -406,7 +510,10 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     if (AllowRulesAllowPath(R.allow_rules, P, path.size())) continue;            // AllowPath :403
     bool sub = !R.secret_group_name.empty();
     std::vector<int64_t> m;
-    re->FindAll(content, len, sub, &wins, &m);
+    {
+      PhaseTimer pt(0);
+      re->FindAll(content, len, sub, &wins, &m);
+    }
     if (m.empty()) continue;
     size_t stride = sub ? size_t(2 * (re->num_cap() + 1)) : 2;
     // MatchKeywords (:409), evaluated lazily: it only matters when FindLocations
@@ -414,6 +521,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     // keyword inside its lowered bytes is inside bytes.ToLower(content) too;
     // otherwise the whole content is lowered and searched.
     if (cr_.rules[r].gate != kGateAlways) {
+      PhaseTimer pt(1);
       bool hit = false;
       for (size_t k = 0; k + stride <= m.size() && !hit; k += stride) {
         std::string ml = GoBytesToLower(content + m[k], size_t(m[k + 1] - m[k]));
@@ -424,15 +532,40 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
           }
       }
       if (!hit) {
-        if (!lowered_done) {
-          lowered = GoBytesToLower(content, size_t(len));
-          lowered_done = true;
+        // ASCII keywords: an occurrence in the ASCII-lowered bytes is one in
+        // bytes.ToLower(content) (ASCII bytes are whole runes); the only other
+        // runes lowering into ASCII are U+0130 -> 'i' and U+212A -> 'k', so
+        // without them the ASCII search is exact.  Otherwise lower as Go does.
+        if (!fold_done) {
+          fold_runes = HasSeq(content, size_t(len), "\xC4\xB0", 2) || HasSeq(content, size_t(len), "\xE2\x84\xAA", 3);
+          fold_done = true;
         }
         for (auto& kw : R.kw_lower_host)
-          if (lowered.find(kw) != std::string::npos) {
+          if (IsAsciiStr(kw) && AsciiCaseContains(content, size_t(len), kw)) {
             hit = true;
             break;
           }
+        if (!hit && fold_runes)
+          for (auto& kw : R.kw_lower_host)
+            if (IsAsciiStr(kw) && FoldCaseContains(content, size_t(len), kw)) {
+              hit = true;
+              break;
+            }
+        bool need_go = false;
+        for (auto& kw : R.kw_lower_host)
+          if (!IsAsciiStr(kw)) need_go = true;
+        if (!hit && need_go) {
+          PhaseTimer p6(6);
+          if (!lowered_done) {
+            lowered = GoBytesToLower(content, size_t(len));
+            lowered_done = true;
+          }
+          for (auto& kw : R.kw_lower_host)
+            if (lowered.find(kw) != std::string::npos) {
+              hit = true;
+              break;
+            }
+        }
       }
       if (!hit) continue;
     }
@@ -449,6 +582,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       }
     }
     if (locs.empty()) continue;
+    PhaseTimer pt2(2);
     bool lblocks_done = false;
     std::vector<Loc> lblocks;
     for (auto& loc : locs) {
@@ -550,6 +684,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   };
 
   out->kind = kHasFindings;
+  PhaseTimer pt3(3);
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
@@ -593,6 +728,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     }
     out->findings.push_back(std::move(f));
   }
+  PhaseTimer pt4(4);
   SortFindings(&out->findings, rules_);
 }
 
@@ -683,6 +819,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   starts.push_back(cands.size());
   size_t nf = starts.size() - 1;
   std::vector<FileResult> tmp(nf);
+  for (auto& g : g_prof) g = 0;
   ParallelFor(nf, host_threads_, [&](size_t k) {
     size_t a = starts[k], b = starts[k + 1];
     uint32_t f = cands[a].file;
@@ -693,6 +830,10 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string(p, pn), in.binary && in.binary[f], &cands[a],
              b - a, &tmp[k]);
   });
+  if (std::getenv("TSG_TAIL_DEBUG"))
+    std::fprintf(stderr, "tail phases ms: findall %.1f gate %.1f locs %.1f findings %.1f sort %.1f ascii %.1f go %.1f\n",
+                 g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
+                 g_prof[5] / 1e6, g_prof[6] / 1e6);
   for (size_t k = 0; k < nf; k++) {
     if (tmp[k].kind != kHasFindings) continue;
     uint32_t f = cands[starts[k]].file;
