@@ -91,3 +91,38 @@ def test_host_tail_many_findings_sort_order():
     want = osc.new_scanner(None).scan("many.txt", body)
     assert got.to_dict() == want
     assert len(want["Findings"]) > 12
+
+
+def test_host_tail_lazy_keyword_gate(tmp_path):
+    """MatchKeywords is evaluated after the windowed search: keyword inside the match,
+    elsewhere in the file (either case), only via U+0130 / U+212A folding, inside a
+    longer word, or absent (scanner.go:174-186 semantics, checked against the oracle)."""
+    cfg_path = tmp_path / "trivy-secret.yaml"
+    cfg_path.write_text(
+        "rules:\n"
+        "  - id: gated\n    category: Custom\n    title: Gated\n    severity: HIGH\n"
+        "    regex: 'tok_[a-z0-9]{8}'\n    keywords: [Kilo, 'mi.x']\n"
+        "  - id: gated-in-match\n    category: Custom\n    title: In match\n    severity: LOW\n"
+        "    regex: '(?i)zz[a-z]{4}[0-9]{3}'\n    keywords: [zzab]\n")
+    cfg = ParseConfig(str(cfg_path))
+    body = b"x = tok_abcdef12\n"
+    files = [
+        ("none.txt", body),
+        ("lower.txt", body + b"kilo\n"),
+        ("upper.txt", b"KILO " + body),
+        ("mixed.txt", body + b"it is kIlO-ish\n"),
+        ("dot.txt", body + b"MI.X\n"),
+        ("dotmiss.txt", body + b"mixx mi_x\n"),
+        ("kelvin.txt", body + "Kilo\n".encode()),
+        ("dotless.txt", body + "Mİ.x\n".encode()),
+        ("longs.txt", body + "ſilo kilo\n".encode()),
+        ("partial.txt", body + b"kil\no\n"),
+        ("inmatch.txt", b"ZZAB"[:4] + b"cd123 zzabcd999 zzxyzw000\n"),
+        ("notinmatch.txt", b"zzxyzw000\n"),
+        ("end.txt", body + b"kil"),
+        ("start.txt", b"ilo" + body),
+    ]
+    got = host_tail_scan(cfg, files)
+    o = osc.new_scanner(osc.parse_config(str(cfg_path)))
+    for (p, b), g in zip(files, got):
+        assert g.to_dict() == o.scan(p, b), p
