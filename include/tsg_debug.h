@@ -49,10 +49,11 @@ int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out);
 int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t* lit_len,
                      int32_t* off_lo, int32_t* off_hi);
 const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k);
-/* The streaming prefilter's tables (trivy_amd/csrc/filter.h): shape = {buckets, slots, words},
- * reach[256 * words], bucket_off[buckets+1] -> bucket_items, items (16-B records), item_cls,
- * classes (8 u32 each). */
-int tsg_debug_filter(const tsg_compiled* c, uint32_t* shape, const uint64_t** reach, const uint32_t** bucket_off,
+/* The streaming prefilter's tables (trivy_amd/csrc/filter.h): shape = {buckets, window, words},
+ * reach[256 * words] (u32; bucket j in word j/4, slot s at bit 4s + j%4; the last bucket counts
+ * newlines), bucket_off[buckets+1] -> bucket_items, items (16-B records), item_cls, classes
+ * (8 u32 each). */
+int tsg_debug_filter(const tsg_compiled* c, uint32_t* shape, const uint32_t** reach, const uint32_t** bucket_off,
                      const uint32_t** bucket_items, const void** items, uint32_t* n_items, const uint8_t** item_cls,
                      const uint32_t** classes, double* est_fp);
 /* The anchor / fold ids of the prefilter items (items[k] owns ids[ids_off .. ids_off + n_ids)). */

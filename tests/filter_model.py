@@ -2,7 +2,8 @@
 
 Reads the compiled prefilter tables through include/tsg_debug.h
 (tsg_debug_filter) and replays K1's semantics with numpy: bucketed shift-or
-fires over the byte stream (window of 6 slots ending at each byte), then the
+fires over the byte stream (window of 6 slots ending at each byte; the last
+bucket only counts newlines and never fires), then the
 exact confirm of every item of every fired bucket, file attribution and the
 emitted anchor hits / fold-rune files.  Used to check, without a GPU, that the
 prefilter's hits cover every true match of every rule.
@@ -35,13 +36,14 @@ class FilterModel:
                                 c.byref(ic), c.byref(cl), c.byref(fp))
         if rc != 0:
             raise ValueError("no prefilter tables")
-        self.n_buckets, self.n_slots, self.n_words = shape[0], shape[1], shape[2]
+        self.n_buckets, self.window, self.n_words = shape[0], shape[1], shape[2]
+        assert self.window == WINDOW
         W = self.n_words
 
         def arr(ptr, ctype, n):
             return np.ctypeslib.as_array((ctype * max(1, n)).from_address(ptr.value))[:n].copy()
 
-        self.reach = arr(reach, c.c_uint64, 256 * W).reshape(256, W)
+        self.reach = arr(reach, c.c_uint32, 256 * W).reshape(256, W)
         self.bucket_off = arr(bo, c.c_uint32, self.n_buckets + 1)
         self.bucket_items = arr(bi, c.c_uint32, int(self.bucket_off[-1]))
         raw = arr(it, c.c_uint8, 16 * ni.value).reshape(ni.value, 16)
@@ -71,11 +73,9 @@ class FilterModel:
         return np.ctypeslib.as_array((c.c_uint32 * max(1, n.value)).from_address(p.value))[:n.value].copy()
 
     def allowed(self, j, s):
-        """bool[256]: bytes allowed at slot s of bucket j."""
-        bpw = 64 // self.n_slots
-        w, jj = divmod(j, bpw)
-        bit = np.uint64(s * bpw + jj)
-        return ((self.reach[:, w] >> bit) & np.uint64(1)) == 0
+        """bool[256]: bytes allowed at slot s of bucket j (register j // 4, bit 4 s + j % 4)."""
+        w, jj = divmod(j, 4)
+        return ((self.reach[:, w] >> np.uint32(4 * s + jj)) & np.uint32(1)) == 0
 
     def fires(self, a):
         """bool[n_buckets, len(a)]: bucket j fires at window end t (zero bytes before the arena, as in K1)."""

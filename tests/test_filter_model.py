@@ -133,3 +133,16 @@ def test_golden_custom_rules_covered():
         rules = builtin_rules() + list(cfg.CustomRules or [])
         custom = [r for r in rules if r.Regex]
         _check(rules, _planted_texts(rng, custom, 25))
+
+
+def test_newline_bucket_shape():
+    m = FilterModel(builtin_rules())
+    nlb = m.n_buckets - 1
+    assert m.bucket_off[nlb + 1] == m.bucket_off[nlb]  # no items
+    assert list(np.nonzero(m.allowed(nlb, 0))[0]) == [10]
+    for s in (1, 2, 3):
+        assert m.allowed(nlb, s).all()
+    for s in (4, 5, 6, 7):
+        assert not m.allowed(nlb, s).any()
+    for j in range(nlb):  # item buckets carry fires through slots 6, 7
+        assert m.allowed(j, 6).all() and m.allowed(j, 7).all()

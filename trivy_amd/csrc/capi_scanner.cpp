@@ -161,7 +161,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.special_files = gs.special_files;
   st.findings = hs.findings;
   st.ms_scan_kernel = gs.ms_scan;
-  st.ms_verify_kernel = gs.ms_verify;
+  st.ms_verify_kernel = gs.ms_confirm + gs.ms_verify;  // K2: confirm + NFA verify
   st.ms_fullscan_kernel = gs.ms_fullscan;
   st.ms_gpu_total = gs.ms_total;
   st.ms_host_gpu_phase = hs.ms_gpu;
@@ -357,13 +357,13 @@ int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t
   return 0;
 }
 
-int tsg_debug_filter(const tsg_compiled* c, uint32_t* shape, const uint64_t** reach, const uint32_t** bucket_off,
+int tsg_debug_filter(const tsg_compiled* c, uint32_t* shape, const uint32_t** reach, const uint32_t** bucket_off,
                      const uint32_t** bucket_items, const void** items, uint32_t* n_items, const uint8_t** item_cls,
                      const uint32_t** classes, double* est_fp) {
   const auto* f = c->cr.filter.get();
   if (!f) return -1;
   shape[0] = f->n_buckets;
-  shape[1] = f->n_slots;
+  shape[1] = f->window;
   shape[2] = f->n_words;
   *reach = f->reach.data();
   *bucket_off = f->bucket_off.data();

@@ -24,7 +24,7 @@ struct Candidate {      // produced by the verify / full-scan kernels
 struct BatchStats {
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
   uint64_t flagged_blocks = 0;
-  float ms_scan = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
+  float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
   bool hit_overflow = false, cand_overflow = false;
 };
 
@@ -80,11 +80,13 @@ class GpuEngine {
   size_t lds_bytes_ = 0;
   bool table_in_lds_ = true;
   // streaming prefilter (filter.h)
-  uint64_t* d_reach_ = nullptr;
+  uint32_t* d_reach_ = nullptr;
   void* d_ftabs_ = nullptr;
-  uint32_t f_words_ = 0, ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
-  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, filter_wg_per_cu_ = 1, f_lane_ = 64;
-  size_t f_lds_bytes_ = 0;
+  uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
+  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0;
+  size_t c_lds_bytes_ = 0;
+  void* d_recs_ = nullptr; size_t cap_recs_ = 0;
+  uint32_t rec_cap_ = 0;
   // per-batch buffers
   void* d_chunk_file_ = nullptr; size_t cap_chunk_file_ = 0;
   void* d_nl_ = nullptr; size_t cap_nl_ = 0;
@@ -95,7 +97,8 @@ class GpuEngine {
   void* d_special_ = nullptr; size_t cap_special_ = 0;
   void* d_chunk_list_ = nullptr; size_t cap_chunk_list_ = 0;
   uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
-                                    // [5] careful chunk-list length [6] flagged blocks
+                                    // [5] careful chunk-list length [7] flagged-block records
+                                    // [8] record overflow
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
   void* d_params_ = nullptr; size_t cap_params_ = 0;

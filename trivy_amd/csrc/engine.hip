@@ -471,87 +471,42 @@ __global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
 }
 
 // ---------------------------------------------------------------------------
-// K1: streaming bucketed shift-or filter + exact confirm
+// K1: streaming bucketed shift-or filter
 // ---------------------------------------------------------------------------
-constexpr int kFQueue = 128;                     // per-wave flagged-block queue (drained at >= 64)
-constexpr int kFWaveHits = 128;                  // per-wave LDS hit records
-constexpr int kFWindow = 6;                      // filter window; checks every 9 - kFWindow = 3 bytes
+constexpr int kFLane = 64;           // bytes per lane per tile (4 blocks of 16 B)
+constexpr int kFBlocks = kFLane / 16;
+constexpr int kFTile = 64 * kFLane;  // 4 KiB per wave tile
+constexpr int kFQueue = 64 + 64 * kFBlocks;  // per-wave flagged-block queue (flushed at >= 64 after a tile)
+constexpr int kFWindow = 6;          // filter window: a fire stays visible for 9 - 6 = 3 bytes
+constexpr int kFWords = 4;           // 16 buckets = 4 u32 registers of 8 slots x 4 buckets
+constexpr uint32_t kFireBits = 0xFFF00000u;  // slots 5..7 of a register
+constexpr uint32_t kNlBits = 0x8888u;        // newline bucket (15 = register 3, lane 3), slots 0..3
+static_assert(kChunk % kFLane == 0 && kChunk / kFLane <= 64, "a newline chunk must be whole lane chunks");
 
 struct FilterParams {
   const uint8_t* arena;
   uint64_t n_bytes;
-  const uint64_t* off;
-  uint32_t n_files;
-  const uint32_t* chunk_file;
-  uint64_t n_chunks;
-  const uint64_t* reach;      // 256 x W u64 (filter.h layout)
-  const void* tabs;           // bucket_off | bucket_items | items | item_ids | item_cls | classes
-  uint32_t tabs_bytes, t_bucket_off, t_bucket_items, t_items, t_item_ids, t_item_cls, t_classes;
-  uint32_t diag_mode;         // TSG_DIAG_SCAN: 1 skip the confirm drains, 2 also skip the filter
-  uint16_t* nl;
-  uint32_t* flags;            // per file: bit0 U+0130/U+212A seen, bit1 U+017F seen
-  uint32_t* special;
-  uint32_t special_cap;
-  uint32_t* hits;
-  uint32_t hit_cap;
-  uint32_t* counters;         // [0] hits [2] special files [3] hit overflow [6] flagged blocks
+  const uint32_t* reach;  // 256 x 4 u32 (filter.h layout)
+  uint32_t diag_mode;     // TSG_DIAG_SCAN: 2 skips the filter (loads + newline count only)
+  uint16_t* nl;           // '\n' per 1-KiB chunk
+  uint32_t* recs;         // flagged 16-B block indices
+  uint32_t rec_cap;
+  uint32_t* counters;     // [7] records [8] record overflow
 };
 
-struct FilterTabs {  // LDS copies
-  const uint32_t* bucket_off;
-  const uint32_t* bucket_items;
-  const FilterItemGpu* items;
-  const uint32_t* item_ids;
-  const uint8_t* item_cls;
-  const uint32_t* classes;
-};
-
-// One shift-or step: S = (S << 8) | reach[b] for W 64-bit registers (lo, hi
-// u32 halves); the LDS table row of byte b is 256 B (16 copies of a 16-B
-// entry for W = 2, 32 copies of 8 B for W = 1), the copy chosen by lane, so a
-// wave's reads never conflict.  `laneoff` sits in the address's low byte.
-__device__ __forceinline__ void shift_or(uint32_t& lo, uint32_t& hi, uint32_t mlo, uint32_t mhi) {
-  // hi = (hi << 8 | lo >> 24) | mhi ; lo = lo << 8 | mlo   (3 VALU ops)
-  uint32_t h;
-  asm("v_alignbit_b32 %0, %1, %2, 24" : "=v"(h) : "v"(hi), "v"(lo));
-  asm("v_or_b32 %0, %1, %2" : "=v"(hi) : "v"(h), "v"(mhi));
-  asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(lo) : "v"(lo), "v"(mlo));
+// The table row of byte b is 256 B: 16 copies of its 16-B entry, the copy
+// chosen by lane & 15, so a wave's ds_read_b128s never conflict.  v_perm puts
+// the byte in bits 8..15 and the lane offset in bits 0..7.
+__device__ __forceinline__ uint4 reach_read(const uint8_t* sb, uint32_t w, uint32_t k, uint32_t laneoff) {
+  return *reinterpret_cast<const uint4*>(sb + __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8)));
 }
 
-template <int W>
-__device__ __forceinline__ void fstep(uint32_t w, uint32_t k, uint32_t laneoff, const uint8_t* sb, uint32_t* st) {
-  const uint32_t addr = __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8));
-  if constexpr (W == 2) {
-    const uint4 m = *reinterpret_cast<const uint4*>(sb + addr);
-    shift_or(st[0], st[1], m.x, m.y);
-    shift_or(st[2], st[3], m.z, m.w);
-  } else {
-    const uint2 m = *reinterpret_cast<const uint2*>(sb + addr);
-    shift_or(st[0], st[1], m.x, m.y);
-  }
+__device__ __forceinline__ void reach_apply(const uint4& m, uint32_t* st) {  // R = R << 4 | m, per register
+  st[0] = (st[0] << 4) | m.x;
+  st[1] = (st[1] << 4) | m.y;
+  st[2] = (st[2] << 4) | m.z;
+  st[3] = (st[3] << 4) | m.w;
 }
-
-template <int W>
-struct ReachVec;
-template <>
-struct ReachVec<2> {
-  using T = uint4;
-  static __device__ __forceinline__ T read(const uint8_t* sb, uint32_t w, uint32_t k, uint32_t laneoff) {
-    return *reinterpret_cast<const uint4*>(sb + __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8)));
-  }
-  static __device__ __forceinline__ void apply(const T& m, uint32_t* st) {
-    shift_or(st[0], st[1], m.x, m.y);
-    shift_or(st[2], st[3], m.z, m.w);
-  }
-};
-template <>
-struct ReachVec<1> {
-  using T = uint2;
-  static __device__ __forceinline__ T read(const uint8_t* sb, uint32_t w, uint32_t k, uint32_t laneoff) {
-    return *reinterpret_cast<const uint2*>(sb + __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8)));
-  }
-  static __device__ __forceinline__ void apply(const T& m, uint32_t* st) { shift_or(st[0], st[1], m.x, m.y); }
-};
 
 // '\n' bytes in a word: x = w ^ 0x0A.. is zero exactly in newline bytes; bit 7
 // of ((x & 0x7F..) + 0x7F..) | w marks the nonzero ones (bit 7 of x is w's).
@@ -560,185 +515,36 @@ __device__ __forceinline__ uint32_t nl_count4(uint32_t w) {
   return __popc(~(a | w) & 0x80808080u);
 }
 
-template <int W>
-__device__ __forceinline__ uint32_t ftop(const uint32_t* st) {  // AND of the registers' high halves
-  return W == 2 ? (st[1] & st[3]) : st[1];
-}
-
 __device__ __forceinline__ uint32_t word_of(uint4 v, uint32_t i) {
   return i < 2 ? (i == 0 ? v.x : v.y) : (i == 2 ? v.z : v.w);
 }
 
-// Exact check of item `it` starting at arena byte `start` (every position's
-// byte in its class); 16-B loads, the item is at most 48 positions.
-__device__ bool item_match(const FilterParams& P, const FilterTabs& T, const FilterItemGpu& it, int64_t start) {
-  if (start < 0 || uint64_t(start) + it.n > P.n_bytes) return false;
-  uint64_t p = uint64_t(start);
-  uint4 cur = load16(P.arena + (p & ~uint64_t(15)));
-  for (uint32_t q = 0; q < it.n; q++, p++) {
-    if (q && (p & 15) == 0) cur = load16(P.arena + p);
-    const uint32_t b = (word_of(cur, uint32_t(p >> 2) & 3) >> ((p & 3) * 8)) & 0xFFu;
-    const uint32_t c = T.item_cls[it.cls_off + q];
-    if (!((T.classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u)) return false;
-  }
-  return true;
-}
-
-__device__ __forceinline__ void push_hit(const FilterParams& P, uint32_t* hbuf, uint32_t* hcnt, uint32_t f, uint32_t end,
-                                         uint32_t id) {
-  const uint32_t k = atomicAdd(hcnt, 1u);
-  if (k < uint32_t(kFWaveHits)) {
-    hbuf[3 * k + 0] = f;
-    hbuf[3 * k + 1] = end;
-    hbuf[3 * k + 2] = id;
-    return;
-  }
-  const uint32_t g = atomicAdd(&P.counters[0], 1u);
-  if (g < P.hit_cap) {
-    P.hits[3ull * g + 0] = f;
-    P.hits[3ull * g + 1] = end;
-    P.hits[3ull * g + 2] = id;
-  } else {
-    P.counters[3] = 1;
+__device__ __forceinline__ void load_reach_lds(uint8_t* s_reach, const uint32_t* reach, uint32_t copies, int tid,
+                                               int nthreads) {
+  for (uint32_t i = tid; i < 256 * copies; i += nthreads) {
+    const uint32_t b = i / copies;
+    reinterpret_cast<uint4*>(s_reach)[i] = reinterpret_cast<const uint4*>(reach)[b];
   }
 }
 
-// Confirm one flagged block: recompute the per-position bucket fires from
-// the 5 bytes before it, check every item of every fired bucket exactly,
-// attribute matches to their file and emit anchor hits / fold-rune flags.
-template <int W>
-__device__ void confirm_block(const FilterParams& P, const FilterTabs& T, const uint8_t* sb, uint32_t laneoff,
-                              uint32_t blk, uint32_t* hbuf, uint32_t* hcnt) {
-  const uint64_t base = uint64_t(blk) * 16;
-  const uint4 pv = base >= 16 ? load16(P.arena + base - 16) : uint4{0, 0, 0, 0};
-  const uint4 v = load16(P.arena + base);
-  uint32_t st[2 * W];
-#pragma unroll
-  for (int i = 0; i < 2 * W; i++) st[i] = ~0u;
-#pragma unroll
-  for (uint32_t k = 11; k < 16; k++) fstep<W>(word_of(pv, k >> 2), k & 3, laneoff, sb, st);
-  for (uint32_t k = 0; k < 16; k++) {
-    fstep<W>(word_of(v, k >> 2), k & 3, laneoff, sb, st);
-    // slot kFWindow-1 = bits 8..15 of each register's high half
-    uint32_t fm = (~st[1] >> 8) & 0xFFu;
-    if (W == 2) fm |= ((~st[3] >> 8) & 0xFFu) << 8;
-    while (fm) {
-      const uint32_t j = __builtin_ctz(fm);
-      fm &= fm - 1;
-      for (uint32_t x = T.bucket_off[j]; x < T.bucket_off[j + 1]; x++) {
-        const FilterItemGpu it = T.items[T.bucket_items[x]];
-        const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
-        if (!item_match(P, T, it, start)) continue;
-        const uint64_t s0 = uint64_t(start);
-        uint32_t f = P.chunk_file[s0 / kChunk];
-        uint64_t fs = P.off[f], fe = P.off[f + 1];
-        while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
-          f++;
-          fs = fe;
-          fe = P.off[f + 1];
-        }
-        if (s0 < fs || s0 + it.n > fe) continue;  // crosses a file boundary
-        if (it.kind == kItemFold) {
-          const uint32_t fl = T.item_ids[it.ids_off] == 2 ? 3u : 1u;
-          const uint32_t old = atomicOr(&P.flags[f], fl);
-          if (old == 0) {
-            const uint32_t q = atomicAdd(&P.counters[2], 1u);
-            if (q < P.special_cap) P.special[q] = f;
-          }
-          continue;
-        }
-        const uint32_t end = uint32_t(s0 - fs) + it.lit_end;
-        for (uint32_t d = 0; d < it.n_ids; d++) push_hit(P, hbuf, hcnt, f, end, T.item_ids[it.ids_off + d]);
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ void flush_wave_hits(const FilterParams& P, uint32_t* hbuf, uint32_t* hcnt, uint32_t lane) {
-  wave_sync();
-  const uint32_t n_all = __builtin_amdgcn_readfirstlane(*hcnt);
-  const uint32_t n = n_all < uint32_t(kFWaveHits) ? n_all : uint32_t(kFWaveHits);
-  if (n) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&P.counters[0], n);
-    base = __builtin_amdgcn_readfirstlane(base);
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t g = base + i;
-      if (g < P.hit_cap) {
-        P.hits[3ull * g + 0] = hbuf[3 * i + 0];
-        P.hits[3ull * g + 1] = hbuf[3 * i + 1];
-        P.hits[3ull * g + 2] = hbuf[3 * i + 2];
-      } else {
-        P.counters[3] = 1;
-      }
-    }
-  }
-  wave_sync();
-  if (lane == 0) *hcnt = 0;
-  wave_sync();
-}
-
-template <int W>
-__device__ __forceinline__ void drain_flagged(const FilterParams& P, const FilterTabs& T, const uint8_t* sb,
-                                              uint32_t laneoff, const uint32_t* Q, uint32_t n, uint32_t* hbuf,
-                                              uint32_t* hcnt, uint32_t lane) {
-  wave_sync();
-  if (lane == 0) atomicAdd(&P.counters[6], n);
-  if (P.diag_mode == 0)
-    for (uint32_t i = lane; i < n; i += 64) confirm_block<W>(P, T, sb, laneoff, Q[i], hbuf, hcnt);
-  flush_wave_hits(P, hbuf, hcnt, lane);
-}
-
-// K1.  A wave owns 8 KiB tiles (grid-strided); lane l streams its 128
-// contiguous bytes as 8 x 16-B loads with the next tile's loads in flight.
+// K1.  A wave owns 4-KiB tiles (grid-strided); lane l streams its 64
+// contiguous bytes as 4 x 16-B loads with the next tile's loads in flight.
 // The 5 bytes before a lane's chunk come from lane l-1 (lane 0: an 8-B load).
-// Per byte: table address by v_perm, one conflict-free LDS read, shift-or on
-// W u64 registers.  Every 3 bytes the top three slots are AND-ed into the
-// block's accumulator (a fire at window end t is visible in slots 5..7 at
-// t..t+2), so the hot loop never branches.  Flagged blocks go through a
-// ballot/mbcnt-compacted per-wave LDS queue; at 64 the wave confirms them in
-// parallel (one block per lane).  '\n' is counted per 1-KiB chunk (SWAR +
-// an 8-lane reduction) for the verify kernel's line numbers.
-template <int W, int LB>
+// Per byte: table address by v_perm, one conflict-free ds_read_b128 (issued a
+// block ahead of the chain), four v_lshl_or_b32.  Every 3 bytes the top slots
+// are AND-ed into the block's accumulator; every 4 bytes the newline bucket's
+// 4 slots are popcounted.  Flagged blocks go through a ballot/mbcnt-compacted
+// per-wave LDS queue to the global record list (one atomic per 64 records);
+// the confirm kernel (K2) checks them exactly.
 __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
-  constexpr int kFBlocks = LB / 16;
-  constexpr int kFTile = 64 * LB;  // bytes per wave tile
-  static_assert(kChunk % LB == 0 && (kChunk / LB) <= 64, "a newline chunk must be whole lane chunks");
-  // the reach table sits at LDS address 0 (static), so table reads need no base add
   __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* s_tabs = smem;
-  uint32_t* s_queue = reinterpret_cast<uint32_t*>(s_tabs + P.tabs_bytes);
-  uint32_t* s_hits = s_queue + kScanWaves * kFQueue;
-  uint32_t* s_hcnt = s_hits + kScanWaves * kFWaveHits * 3;
+  __shared__ uint32_t s_queue[kScanWaves * kFQueue];
   const int tid = threadIdx.x;
-  {
-    constexpr uint32_t esz = 8 * W, copies = 256 / esz;
-    for (uint32_t i = tid; i < 256 * copies; i += blockDim.x) {
-      const uint32_t b = i / copies;
-      const uint64_t* src = P.reach + size_t(b) * W;
-      uint64_t* dst = reinterpret_cast<uint64_t*>(s_reach + size_t(i) * esz);
-#pragma unroll
-      for (int w = 0; w < W; w++) dst[w] = src[w];
-    }
-    const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
-    uint4* d = reinterpret_cast<uint4*>(s_tabs);
-    for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
-    if (tid < kScanWaves) s_hcnt[tid] = 0;
-  }
+  load_reach_lds(s_reach, P.reach, 16, tid, blockDim.x);
   __syncthreads();
-  FilterTabs T;
-  T.bucket_off = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_off);
-  T.bucket_items = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_items);
-  T.items = reinterpret_cast<const FilterItemGpu*>(s_tabs + P.t_items);
-  T.item_ids = reinterpret_cast<const uint32_t*>(s_tabs + P.t_item_ids);
-  T.item_cls = s_tabs + P.t_item_cls;
-  T.classes = reinterpret_cast<const uint32_t*>(s_tabs + P.t_classes);
   const uint32_t lane = tid & 63, wave = tid >> 6;
-  const uint32_t laneoff = W == 2 ? (lane & 15) * 16 : (lane & 31) * 8;
+  const uint32_t laneoff = (lane & 15) * 16;
   uint32_t* Q = s_queue + wave * kFQueue;
-  uint32_t* hbuf = s_hits + wave * kFWaveHits * 3;
-  uint32_t* hcnt = s_hcnt + wave;
   uint32_t qn = 0;  // wave-uniform
   const uint64_t n_tiles = (P.n_bytes + kFTile - 1) / kFTile;
   const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
@@ -746,7 +552,7 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   uint4 cur[kFBlocks], nxt[kFBlocks];
   uint2 pre = make_uint2(0, 0), pnx = make_uint2(0, 0);
   auto load_tile = [&](uint4* dst, uint2* pv, uint64_t tt) {
-    const uint64_t b0 = tt * kFTile + uint64_t(lane) * LB;
+    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLane;
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
       const uint64_t p = b0 + 16 * j;
@@ -754,12 +560,21 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     }
     if (lane == 0 && tt > 0) *pv = *reinterpret_cast<const uint2*>(P.arena + tt * kFTile - 8);
   };
+  auto flush = [&]() {  // wave-uniform
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&P.counters[7], qn);
+    base = __builtin_amdgcn_readfirstlane(base);
+    for (uint32_t i = lane; i < qn; i += 64) {
+      if (base + i < P.rec_cap) P.recs[base + i] = Q[i];
+      else P.counters[8] = 1;
+    }
+    qn = 0;
+  };
   if (t < n_tiles) load_tile(cur, &pre, t);
   for (; t < n_tiles; t += n_waves) {
     if (t + n_waves < n_tiles) load_tile(nxt, &pnx, t + n_waves);
-    const uint64_t b0 = t * kFTile + uint64_t(lane) * LB;
-    // bytes past the arena end (last tile only) are zeroed
-    if (b0 + LB > P.n_bytes) {
+    const uint64_t b0 = t * kFTile + uint64_t(lane) * kFLane;
+    if (b0 + kFLane > P.n_bytes) {  // bytes past the arena end (last tile only) are zeroed
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint64_t p = b0 + 16 * j;
@@ -781,35 +596,33 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     }
     uint32_t flagged = 0, nl = 0;
     if (P.diag_mode < 2) {
-      uint32_t st[2 * W];
+      uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
+      reach_apply(reach_read(s_reach, p0, 3, laneoff), st);
 #pragma unroll
-      for (int i = 0; i < 2 * W; i++) st[i] = ~0u;
-      fstep<W>(p0, 3, laneoff, s_reach, st);
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) fstep<W>(p1, k, laneoff, s_reach, st);
+      for (uint32_t k = 0; k < 4; k++) reach_apply(reach_read(s_reach, p1, k, laneoff), st);
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint32_t wd[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
-        // all 16 table reads of the block first (independent of the state), then the chain
-        typename ReachVec<W>::T m[16];
+        uint4 m[16];  // a block's table reads first (independent of the state), then the chain
 #pragma unroll
-        for (uint32_t k = 0; k < 16; k++) m[k] = ReachVec<W>::read(s_reach, wd[k >> 2], k & 3, laneoff);
+        for (uint32_t k = 0; k < 16; k++) m[k] = reach_read(s_reach, wd[k >> 2], k & 3, laneoff);
         uint32_t acc = ~0u;
 #pragma unroll
         for (uint32_t k = 0; k < 16; k++) {
-          ReachVec<W>::apply(m[k], st);
-          if (k % 3 == 2 || k == 15) acc &= ftop<W>(st);
+          reach_apply(m[k], st);
+          if (k % 3 == 2 || k == 15) acc &= st[0] & st[1] & st[2] & st[3];
+          if (k % 4 == 3) nl += __popc(~st[3] & kNlBits);
         }
-        flagged |= uint32_t((acc | 0xFFu) != ~0u) << j;
+        flagged |= uint32_t((acc | ~kFireBits) != ~0u) << j;
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kFBlocks; j++)
+        nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
     }
 #pragma unroll
-    for (int j = 0; j < kFBlocks; j++)
-      nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
-#pragma unroll
-    for (int x = 1; x < int(kChunk / LB); x <<= 1) nl += __shfl_xor(nl, x);
-    if ((lane & (kChunk / LB - 1)) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
-    // queue the flagged blocks
+    for (int x = 1; x < int(kChunk / kFLane); x <<= 1) nl += __shfl_xor(nl, x);
+    if ((lane & (kChunk / kFLane - 1)) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
       const bool fj = (flagged >> j) & 1u;
@@ -819,17 +632,14 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
             __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
         if (fj) Q[qn + below] = uint32_t((b0 + 16 * j) >> 4);
         qn += uint32_t(__popcll(m));
-        if (qn >= 64) {
-          drain_flagged<W>(P, T, s_reach, laneoff, Q, qn, hbuf, hcnt, lane);
-          qn = 0;
-        }
       }
     }
+    if (qn >= 64) flush();
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) cur[j] = nxt[j];
     pre = pnx;
   }
-  if (qn) drain_flagged<W>(P, T, s_reach, laneoff, Q, qn, hbuf, hcnt, lane);
+  if (qn) flush();
 }
 
 // Chunk list of the files K1 found fold runes in (for the careful pass): one
@@ -1011,12 +821,232 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
   }
 }
 
-const void* FilterFn(uint32_t words, uint32_t lane_bytes) {
-  if (words == 2)
-    return lane_bytes == 128 ? reinterpret_cast<const void*>(&filter_kernel<2, 128>)
-                             : reinterpret_cast<const void*>(&filter_kernel<2, 64>);
-  return lane_bytes == 128 ? reinterpret_cast<const void*>(&filter_kernel<1, 128>)
-                           : reinterpret_cast<const void*>(&filter_kernel<1, 64>);
+// ---------------------------------------------------------------------------
+// K2: confirm flagged blocks exactly + verify the anchor hits
+// ---------------------------------------------------------------------------
+constexpr int kCThreads = 256;
+constexpr int kCWin = 64;  // per-lane LDS copy of arena bytes [base - 16, base + 48)
+
+struct ConfirmParams {
+  const uint8_t* arena;
+  uint64_t n_bytes;
+  const uint64_t* off;
+  const uint32_t* chunk_file;
+  const uint16_t* nl;
+  const uint32_t* reach;
+  const void* tabs;  // bucket_off | bucket_items | items | item_ids | item_cls | classes
+  uint32_t tabs_bytes, t_bucket_off, t_bucket_items, t_items, t_item_ids, t_item_cls, t_classes;
+  const AnchorInfo* anchors;
+  const RuleGpu* rules;
+  const uint64_t* nfa;
+  const uint32_t* recs;
+  uint32_t rec_cap;
+  uint32_t* flags;
+  uint32_t* special;
+  uint32_t special_cap;
+  uint32_t* counters;  // [1] candidates [2] special files [4] cand overflow [7] records
+  Candidate* cands;
+  uint32_t cand_cap;
+};
+
+// Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
+// (aligned) instead of one dependent load per byte.  As nfa_run otherwise.
+template <int W>
+__device__ bool nfa_run_abs(const uint8_t* __restrict arena, uint64_t fs, int64_t len, int64_t start, int64_t inj_hi,
+                            const uint64_t* __restrict tab) {
+  uint64_t O[W], Lp[W], F[W], D[W];
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    O[w] = tab[w];
+    Lp[w] = tab[W + w];
+    F[w] = tab[2 * W + w];
+    D[w] = 0;
+  }
+  const uint64_t* B = tab + 3 * W;
+  uint4 buf = make_uint4(0, 0, 0, 0);
+  uint64_t buf_at = ~uint64_t(0);
+  for (int64_t pos = start; pos < len; pos++) {
+    const uint64_t abs = fs + uint64_t(pos);
+    if ((abs & ~uint64_t(15)) != buf_at) {
+      buf_at = abs & ~uint64_t(15);
+      buf = load16(arena + buf_at);
+    }
+    const uint32_t b = (word_of(buf, uint32_t(abs >> 2) & 3) >> ((abs & 3) * 8)) & 0xFFu;
+    uint64_t carry = pos <= inj_hi ? 1 : 0;
+    uint64_t T[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      T[w] = (D[w] << 1) | carry | (D[w] & Lp[w]);
+      carry = D[w] >> 63;
+    }
+    uint64_t c = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      uint64_t x = T[w] & O[w];
+      uint64_t s1 = O[w] + x;
+      uint64_t c1 = s1 < O[w];
+      uint64_t s2 = s1 + c;
+      uint64_t c2 = s2 < s1;
+      T[w] |= s2 ^ O[w];
+      c = c1 | c2;
+    }
+    const uint64_t* Bb = B + size_t(b) * W;
+    const bool keep = (b & 0xC0u) == 0x80u;  // UTF-8 continuation: also stay
+    uint64_t acc = 0, alive = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      uint64_t nd = (T[w] & Bb[w]) | (keep ? D[w] : 0);
+      D[w] = nd;
+      acc |= nd & F[w];
+      alive |= nd;
+    }
+    if (acc) return true;
+    if (!alive && pos >= inj_hi) return false;
+  }
+  return false;
+}
+
+__device__ bool nfa_dispatch_abs(int words, const uint8_t* arena, uint64_t fs, int64_t len, int64_t start,
+                                 int64_t inj_hi, const uint64_t* tab) {
+  switch (words) {
+    case 1: return nfa_run_abs<1>(arena, fs, len, start, inj_hi, tab);
+    case 2: return nfa_run_abs<2>(arena, fs, len, start, inj_hi, tab);
+    case 3: return nfa_run_abs<3>(arena, fs, len, start, inj_hi, tab);
+    default: return nfa_run_abs<4>(arena, fs, len, start, inj_hi, tab);
+  }
+}
+
+__device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64_t a, uint64_t b) {  // arena [a, b)
+  int64_t n = 0;
+  const uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
+  if (ca >= cb) {
+    for (uint64_t p = a; p < b; p++) n += arena[p] == '\n';
+    return n;
+  }
+  for (uint64_t p = a; p < ca * kChunk; p++) n += arena[p] == '\n';
+  for (uint64_t c = ca; c < cb; c++) n += nl[c];
+  for (uint64_t p = cb * kChunk; p < b; p++) n += arena[p] == '\n';
+  return n;
+}
+
+// K2.  One lane per flagged block: the 64 arena bytes around it go to the
+// lane's LDS window; the bucket fires are recomputed from the 5 bytes before
+// the block; every item of a fired bucket is checked exactly (bytes from the
+// window, global beyond it); a matching item is attributed to its file
+// (chunk map) and, for each of its anchors, the rule's relaxed NFA runs from
+// the start window [wlo, whi] -- an accept emits the candidate, with the
+// line count before wlo from K1's per-chunk newline counts.  Fold-rune items
+// flag their file for the careful pass instead.
+__global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* s_reach = smem;                   // 4 KiB: one copy per byte (a few conflicts are fine here)
+  uint8_t* s_win = smem + 4096;              // kCThreads x 64 B
+  uint8_t* s_tabs = s_win + kCThreads * kCWin;
+  const int tid = threadIdx.x;
+  load_reach_lds(s_reach, P.reach, 1, tid, blockDim.x);
+  {
+    const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
+    uint4* d = reinterpret_cast<uint4*>(s_tabs);
+    for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
+  }
+  __syncthreads();
+  const uint32_t* bucket_off = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_off);
+  const uint32_t* bucket_items = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_items);
+  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(s_tabs + P.t_items);
+  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(s_tabs + P.t_item_ids);
+  const uint8_t* item_cls = s_tabs + P.t_item_cls;
+  const uint32_t* classes = reinterpret_cast<const uint32_t*>(s_tabs + P.t_classes);
+  uint8_t* win = s_win + tid * kCWin;
+  const uint32_t n_recs = P.counters[7] < P.rec_cap ? P.counters[7] : P.rec_cap;
+  for (uint32_t r = blockIdx.x * blockDim.x + tid; r < n_recs; r += gridDim.x * blockDim.x) {
+    const uint64_t base = uint64_t(P.recs[r]) * 16;
+    const uint64_t wbase = base >= 16 ? base - 16 : 0;  // window [wbase, wbase + 64)
+    const uint4 d0 = load16(P.arena + wbase), d1 = load16(P.arena + wbase + 16), d2 = load16(P.arena + wbase + 32),
+                d3 = load16(P.arena + wbase + 48);
+    reinterpret_cast<uint4*>(win)[0] = d0;
+    reinterpret_cast<uint4*>(win)[1] = d1;
+    reinterpret_cast<uint4*>(win)[2] = d2;
+    reinterpret_cast<uint4*>(win)[3] = d3;
+    const uint4 pv = base >= 16 ? d0 : make_uint4(0, 0, 0, 0);
+    const uint4 v = base >= 16 ? d1 : d0;
+    auto byte_at = [&](uint64_t pos) -> uint32_t {
+      return (pos >= wbase && pos < wbase + kCWin) ? uint32_t(win[pos - wbase]) : uint32_t(P.arena[pos]);
+    };
+    uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
+    auto rd1 = [&](uint32_t w, uint32_t k) {  // single-copy table: entry b at 16 * b
+      return *reinterpret_cast<const uint4*>(s_reach + (((w >> (8 * k)) & 0xFFu) << 4));
+    };
+    for (uint32_t k = 11; k < 16; k++) reach_apply(rd1(word_of(pv, k >> 2), k & 3), st);
+    for (uint32_t k = 0; k < 16; k++) {
+      reach_apply(rd1(word_of(v, k >> 2), k & 3), st);
+      // fires at window end base + k: slot 5 = bits 20..23 of each register
+      uint32_t fm = 0;
+#pragma unroll
+      for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
+      while (fm) {
+        const uint32_t j = __builtin_ctz(fm);
+        fm &= fm - 1;
+        for (uint32_t x = bucket_off[j]; x < bucket_off[j + 1]; x++) {
+          const FilterItemGpu it = items[bucket_items[x]];
+          const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
+          if (start < 0 || uint64_t(start) + it.n > P.n_bytes) continue;
+          bool ok = true;
+          for (uint32_t q = 0; q < it.n && ok; q++) {
+            const uint32_t bt = byte_at(uint64_t(start) + q);
+            const uint32_t c = item_cls[it.cls_off + q];
+            ok = (classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u;
+          }
+          if (!ok) continue;
+          const uint64_t s0 = uint64_t(start);
+          uint32_t f = P.chunk_file[s0 / kChunk];
+          uint64_t fs = P.off[f], fe = P.off[f + 1];
+          while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
+            f++;
+            fs = fe;
+            fe = P.off[f + 1];
+          }
+          if (s0 < fs || s0 + it.n > fe) continue;  // crosses a file boundary
+          if (it.kind == kItemFold) {
+            const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 1u;
+            const uint32_t old = atomicOr(&P.flags[f], fl);
+            if (old == 0) {
+              const uint32_t q = atomicAdd(&P.counters[2], 1u);
+              if (q < P.special_cap) P.special[q] = f;
+            }
+            continue;
+          }
+          const int64_t lit_end = int64_t(s0 - fs) + it.lit_end;
+          const int64_t len = int64_t(fe - fs);
+          for (uint32_t d = 0; d < it.n_ids; d++) {
+            const AnchorInfo an = P.anchors[item_ids[it.ids_off + d]];
+            const RuleGpu rg = P.rules[an.rule];
+            const int64_t lit_hi = lit_end - an.lit_len;
+            const int64_t whi = lit_hi - an.off_lo;
+            if (whi < 0) continue;
+            int64_t wlo = lit_hi - an.off_hi;
+            if (wlo < 0) wlo = 0;
+            const bool acc = rg.nfa_words == 0 ||
+                             nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off);
+            if (!acc) continue;
+            const uint32_t kc = atomicAdd(&P.counters[1], 1u);
+            if (kc < P.cand_cap) {
+              Candidate c;
+              c.file = f;
+              c.rule = an.rule;
+              c.wlo = wlo;
+              c.whi = whi;
+              c.nl_before = count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(wlo));
+              c.flags = 0;
+              c.pad = 0;
+              P.cands[kc] = c;
+            } else {
+              P.counters[4] = 1;
+            }
+          }
+        }
+      }
+    }
+  }
 }
 
 template <typename T>
@@ -1208,16 +1238,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   // streaming prefilter tables (filter.h)
   {
     const FilterTables* ft = cr.filter.get();
-    if (!ft || ft->n_slots != 8 || ft->window != uint32_t(kFWindow) || (ft->n_words != 1 && ft->n_words != 2)) {
-      err_ = "prefilter shape not supported by the scan kernel (needs 8 slots, window 6, 8 or 16 buckets)";
+    if (!ft || ft->n_words != uint32_t(kFWords) || ft->window != uint32_t(kFWindow) || ft->nl_bucket != 15) {
+      err_ = "prefilter shape not supported by the scan kernel (needs 16 buckets, window 6)";
       return;
     }
-    for (auto& it : ft->items)
-      if (it.n > 48) {
-        err_ = "prefilter item longer than 48 positions";
-        return;
-      }
-    f_words_ = ft->n_words;
     if (!Upload(&err_, &d_reach_, ft->reach.data(), ft->reach.size())) return;
     auto pad = [](std::vector<uint8_t>& v) { v.resize((v.size() + 15) & ~size_t(15), 0); };
     std::vector<uint8_t> tb;
@@ -1239,22 +1263,19 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     uint8_t* d = nullptr;
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_ftabs_ = d;
-    // dynamic LDS: tables + queues + hit buffers (the 64-KiB reach table is static)
-    f_lds_bytes_ = ftabs_bytes_ + size_t(kScanWaves) * kFQueue * 4 + size_t(kScanWaves) * kFWaveHits * 12 +
-                   size_t(kScanWaves) * 4;
-    if (65536 + f_lds_bytes_ > 160 * 1024) {
+    c_lds_bytes_ = 4096 + size_t(kCThreads) * kCWin + ftabs_bytes_;
+    if (c_lds_bytes_ > 64 * 1024) {
       err_ = "prefilter tables do not fit in LDS";
       return;
     }
-    if (const char* e = std::getenv("TSG_FILTER_LANE")) f_lane_ = uint32_t(std::atoi(e));
-    if (f_lane_ != 64 && f_lane_ != 128) f_lane_ = 64;
-    hipFuncSetAttribute(FilterFn(f_words_, f_lane_), hipFuncAttributeMaxDynamicSharedMemorySize, int(f_lds_bytes_));
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&confirm_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        int(c_lds_bytes_));
   }
 }
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_reach_, d_ftabs_, d_chunk_list_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
+  void* ps[] = {d_reach_, d_ftabs_, d_chunk_list_, d_recs_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
                 d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_, d_params_};
   for (void* p : ps)
@@ -1304,6 +1325,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   if (n_chunks == 0) n_chunks = 1;
   if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 256, 1 << 16), 1u << 30));
   if (cand_cap_ == 0) cand_cap_ = 1 << 16;
+  if (rec_cap_ == 0) rec_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 128, 1 << 16), 1u << 30));
   const uint32_t list_cap =
       uint32_t(std::min<uint64_t>((n_bytes + kCarefulUnit - 1) / kCarefulUnit + n_files, 0xFFFFFFF0u));
   for (int attempt = 0; attempt < 8; attempt++) {
@@ -1312,6 +1334,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
         !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
         !Ensure(&d_special_, &cap_special_, size_t(n_files) * 4) ||
         !Ensure(&d_chunk_list_, &cap_chunk_list_, size_t(list_cap) * 4) ||
+        !Ensure(&d_recs_, &cap_recs_, size_t(rec_cap_) * 4) ||
         !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
         !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
       return false;
@@ -1322,41 +1345,53 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       uint32_t blocks = std::min<uint32_t>((n_files + 255) / 256, 4096);
       chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, static_cast<uint32_t*>(d_chunk_file_));
     }
-    // K1: streaming filter + confirm
+    // K1: streaming filter -> flagged block records
     FilterParams fp;
     fp.arena = d_arena;
     fp.n_bytes = n_bytes;
-    fp.off = d_offsets;
-    fp.n_files = n_files;
-    fp.chunk_file = static_cast<const uint32_t*>(d_chunk_file_);
-    fp.n_chunks = n_chunks;
     fp.reach = d_reach_;
-    fp.tabs = d_ftabs_;
-    fp.tabs_bytes = ftabs_bytes_;
-    fp.t_bucket_off = ft_bucket_off_;
-    fp.t_bucket_items = ft_bucket_items_;
-    fp.t_items = ft_items_;
-    fp.t_item_ids = ft_item_ids_;
-    fp.t_item_cls = ft_item_cls_;
-    fp.t_classes = ft_classes_;
     fp.diag_mode = diag_mode_;
     fp.nl = static_cast<uint16_t*>(d_nl_);
-    fp.flags = static_cast<uint32_t*>(d_flags_);
-    fp.special = static_cast<uint32_t*>(d_special_);
-    fp.special_cap = n_files;
-    fp.hits = static_cast<uint32_t*>(d_hits_);
-    fp.hit_cap = hit_cap_;
+    fp.recs = static_cast<uint32_t*>(d_recs_);
+    fp.rec_cap = rec_cap_;
     fp.counters = d_counters_;
-    const uint64_t f_tiles = (n_bytes + 64 * f_lane_ - 1) / (64 * f_lane_);
-    const uint32_t f_grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves,
-                                                                            uint64_t(256) * filter_wg_per_cu_)));
+    const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
+    const uint32_t f_grid =
+        uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves, 256)));
     HIP_OK(hipEventRecord(ev_[0], stream_));
-    {
-      void* kargs[] = {&fp};
-      HIP_OK(hipLaunchKernel(FilterFn(f_words_, f_lane_), dim3(f_grid), dim3(kScanThreads), kargs, f_lds_bytes_,
-                             stream_));
-    }
+    filter_kernel<<<f_grid, kScanThreads, 0, stream_>>>(fp);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[1], stream_));
+    // K2: confirm + verify
+    ConfirmParams cp;
+    cp.arena = d_arena;
+    cp.n_bytes = n_bytes;
+    cp.off = d_offsets;
+    cp.chunk_file = static_cast<const uint32_t*>(d_chunk_file_);
+    cp.nl = static_cast<const uint16_t*>(d_nl_);
+    cp.reach = d_reach_;
+    cp.tabs = d_ftabs_;
+    cp.tabs_bytes = ftabs_bytes_;
+    cp.t_bucket_off = ft_bucket_off_;
+    cp.t_bucket_items = ft_bucket_items_;
+    cp.t_items = ft_items_;
+    cp.t_item_ids = ft_item_ids_;
+    cp.t_item_cls = ft_item_cls_;
+    cp.t_classes = ft_classes_;
+    cp.anchors = d_anchors_;
+    cp.rules = d_rules_;
+    cp.nfa = d_nfa_;
+    cp.recs = static_cast<const uint32_t*>(d_recs_);
+    cp.rec_cap = rec_cap_;
+    cp.flags = static_cast<uint32_t*>(d_flags_);
+    cp.special = static_cast<uint32_t*>(d_special_);
+    cp.special_cap = n_files;
+    cp.counters = d_counters_;
+    cp.cands = static_cast<Candidate*>(d_cands_);
+    cp.cand_cap = cand_cap_;
+    if (diag_mode_ == 0) confirm_kernel<<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev_[2], stream_));
     // careful pass over the chunks of fold-rune files (Aho-Corasick on the bytes.ToLower symbol stream)
     special_chunks_kernel<<<1024, 256, 0, stream_>>>(d_offsets, static_cast<const uint32_t*>(d_special_), d_counters_,
                                                    static_cast<uint32_t*>(d_chunk_list_), list_cap);
@@ -1414,7 +1449,6 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       }
     }
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[2], stream_));
     NfaParams np;
     np.arena = d_arena;
     np.off = d_offsets;
@@ -1438,7 +1472,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.n_regex_rules = uint32_t(regex_rules_.size());
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
-    verify_kernel<<<2048, 256, 0, stream_>>>(np);
+    verify_kernel<<<256, 256, 0, stream_>>>(np);  // hits of the careful pass
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[3], stream_));
     if (np.n_fullscan_rules > 0) {
@@ -1451,7 +1485,11 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     HIP_OK(hipStreamSynchronize(stream_));
     st->hits = cnt[0];
     st->special_files = cnt[2];
-    st->flagged_blocks = cnt[6];
+    st->flagged_blocks = cnt[7];
+    if (cnt[8]) {  // record list overflow: grow and rescan
+      rec_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[7]) + cnt[7] / 4 + 4096, 0xFFFFFFF0u / 4));
+      continue;
+    }
     st->hit_overflow = cnt[3] != 0;
     st->cand_overflow = cnt[4] != 0;
     if (cnt[5] > list_cap) {
@@ -1474,8 +1512,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       HIP_OK(hipStreamSynchronize(stream_));
     }
     hipEventElapsedTime(&st->ms_scan, ev_[0], ev_[1]);
-    hipEventElapsedTime(&st->ms_careful, ev_[1], ev_[2]);
-    hipEventElapsedTime(&st->ms_verify, ev_[2], ev_[3]);
+    hipEventElapsedTime(&st->ms_confirm, ev_[1], ev_[2]);
+    hipEventElapsedTime(&st->ms_careful, ev_[2], ev_[3]);
     hipEventElapsedTime(&st->ms_fullscan, ev_[3], ev_[4]);
     hipEventElapsedTime(&st->ms_total, ev_[0], ev_[4]);
     return true;

@@ -64,18 +64,18 @@ double Cost(const ByteSet* u) {
 
 }  // namespace
 
-bool BuildFilter(const std::vector<FilterItem>& items, uint32_t n_slots, uint32_t window, uint32_t n_buckets,
-                 FilterTables* out, std::string* err) {
-  if ((n_slots != 4 && n_slots != 8) || n_buckets == 0 || (n_slots * n_buckets) % 64 != 0 ||
-      n_slots * n_buckets > 256 || window == 0 || window > n_slots) {
+bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t n_buckets, FilterTables* out,
+                 std::string* err) {
+  if ((n_buckets != 8 && n_buckets != 16) || window < 2 || window > uint32_t(kFilterSlots)) {
     *err = "unsupported prefilter shape";
     return false;
   }
   *out = FilterTables();
   out->n_buckets = n_buckets;
-  out->n_slots = n_slots;
-  out->n_words = n_slots * n_buckets / 64;
+  out->n_words = n_buckets / 4;
   out->window = window;
+  out->nl_bucket = n_buckets - 1;
+  const uint32_t n_item_buckets = n_buckets - 1;
   const uint32_t S = window;
   // identical byte-set sequences (rules sharing an anchor) become one item
   std::vector<FilterItem> uniq;
@@ -165,7 +165,7 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t n_slots, uint32_
       ByteSet u[kFilterSlots];
       delta[i][j] = merged(cl[i], cl[j], u) - cl[i].cost - cl[j].cost;
     }
-  while (n_alive > n_buckets) {
+  while (n_alive > n_item_buckets) {
     size_t bi = 0, bj = 0;
     double bd = std::numeric_limits<double>::infinity();
     for (size_t i = 0; i < n; i++) {
@@ -193,23 +193,28 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t n_slots, uint32_
     }
   }
   // reach table
-  const uint32_t W = out->n_words, bpw = 64 / n_slots;
-  out->reach.assign(256 * W, ~uint64_t(0));
+  const uint32_t W = out->n_words;
+  out->reach.assign(256 * W, ~0u);
+  auto allow = [&](uint32_t b, uint32_t j, uint32_t slot) { out->reach[size_t(b) * W + j / 4] &= ~(1u << (4 * slot + j % 4)); };
   out->bucket_off.push_back(0);
   uint32_t j = 0;
   for (size_t i = 0; i < n; i++) {
     if (!alive[i]) continue;
     out->est_fp += cl[i].cost;
-    for (uint32_t s = 0; s < n_slots; s++)  // slots >= window: all bytes allowed (carry the fire)
+    for (uint32_t sl = 0; sl < uint32_t(kFilterSlots); sl++)  // slots >= window: all bytes allowed (carry the fire)
       for (int b = 0; b < 256; b++)
-        if (cl[i].u[s].test(b)) out->reach[size_t(b) * W + j / bpw] &= ~(uint64_t(1) << (s * bpw + (j % bpw)));
+        if (sl >= S || cl[i].u[sl].test(b)) allow(uint32_t(b), j, sl);
     for (uint32_t m : cl[i].members) out->bucket_items.push_back(m);
     out->bucket_off.push_back(uint32_t(out->bucket_items.size()));
     j++;
   }
-  while (j < n_buckets) {  // fewer items than buckets: empty buckets never fire
+  for (; j < n_buckets; j++) {  // empty item buckets never fire; the newline bucket allows '\n' at slot 0
+    if (j == out->nl_bucket) {  // slot 0: '\n' only; slots 1-3 carry; slots 4-7 never allow (no fires)
+      allow('\n', j, 0);
+      for (uint32_t sl = 1; sl < 4; sl++)
+        for (int b = 0; b < 256; b++) allow(uint32_t(b), j, sl);
+    }
     out->bucket_off.push_back(uint32_t(out->bucket_items.size()));
-    j++;
   }
   for (auto& b : classes) {
     uint32_t w[8] = {};

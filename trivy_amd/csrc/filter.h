@@ -1,15 +1,20 @@
 // Streaming prefilter tables: bucketed shift-or over windows
 // of the rule compiler's FilterItems.
 //
-// Each item is reduced to a window of at most kSlots consecutive byte sets
+// Each item is reduced to a window of at most `window` consecutive byte sets
 // (the least frequent one under a static byte-frequency prior); windows are
-// clustered into n_buckets buckets (agglomerative, minimising the estimated
-// false-positive rate Σ_bucket Π_slot P(union of the slot's sets)).  The
-// device reach table holds, per input byte, one bit per (slot, bucket): 0 when
-// the byte is allowed at that slot of that bucket.  State after byte t:
-//   S_t = (S_{t-1} << 8) | reach[b_t]      (8 buckets: u64; 16: two u64)
-// and bucket j fires at t when bit (8*7 + j) of S_t is 0.  The confirm pass
-// then checks each of the bucket's items exactly at every position.
+// clustered into the item buckets (agglomerative, minimising the estimated
+// false-positive rate Σ_bucket Π_slot P(union of the slot's sets)).
+//
+// State layout: n_words u32 registers of 8 slots x 4 buckets; bucket j lives
+// in register j / 4, slot s at bit 4*s + j % 4.  Per input byte b
+//   R_w = (R_w << 4) | reach[b][w]          (one v_lshl_or_b32 per register)
+// where a reach bit is 0 when b is allowed at that (slot, bucket).  Items end
+// at slot window-1; slots past it are all-allowed, so a fire stays visible in
+// slots window-1 .. 7 for 9 - window bytes and the top slots need checking
+// only that often.  The last bucket counts '\n': its slot 0 allows only '\n',
+// slots 1-3 carry and slots 4-7 allow nothing (it never fires), so after every
+// 4th byte its slots 0-3 hold the last 4 bytes' newline bits.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -19,7 +24,7 @@
 
 namespace tsg {
 
-constexpr int kFilterSlots = 8;  // maximum window length
+constexpr int kFilterSlots = 8;  // slots per register (4 bits each)
 
 struct FilterItemGpu {  // mirrored on the device (16 B)
   uint16_t n;        // positions (byte sets) of the item
@@ -32,15 +37,11 @@ struct FilterItemGpu {  // mirrored on the device (16 B)
 };
 
 struct FilterTables {
-  uint32_t n_buckets = 0;                // buckets
-  uint32_t n_slots = 0;                  // slots per register (4 or 8)
-  uint32_t window = 0;                   // window length L <= n_slots: items end at slot L-1; a fire
-                                         // stays visible in slots L-1..n_slots-1, so the top slots
-                                         // need checking only every n_slots - L + 1 bytes
-  uint32_t n_words = 0;                  // 64-bit state registers: n_slots * n_buckets / 64
-  // reach[b * n_words + w]: register w holds buckets [w*bpw, (w+1)*bpw), bpw = 64 / n_slots,
-  // bit s * bpw + (j % bpw) is 0 when byte b is allowed at slot s of bucket j
-  std::vector<uint64_t> reach;
+  uint32_t n_buckets = 0;                // buckets, including the newline bucket
+  uint32_t n_words = 0;                  // u32 state registers = n_buckets / 4
+  uint32_t window = 0;                   // window length (<= 8)
+  uint32_t nl_bucket = 0;                // the newline-counting bucket (n_buckets - 1)
+  std::vector<uint32_t> reach;           // reach[b * n_words + w]
   std::vector<uint32_t> bucket_off;      // n_buckets + 1 into bucket_items
   std::vector<uint32_t> bucket_items;    // item indices
   std::vector<FilterItemGpu> items;
@@ -49,12 +50,13 @@ struct FilterTables {
   std::vector<uint32_t> classes;         // 8 x u32 membership words per class
   uint32_t max_after = 0;                // max positions an item extends past its window end
   double est_fp = 0;                     // estimated bucket fires per input byte
+
 };
 
 // Static byte-frequency prior of source/text bytes (sums to 1).
 const std::vector<double>& BytePrior();
 
-bool BuildFilter(const std::vector<FilterItem>& items, uint32_t n_slots, uint32_t window, uint32_t n_buckets,
-                 FilterTables* out, std::string* err);
+bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t n_buckets, FilterTables* out,
+                 std::string* err);
 
 }  // namespace tsg

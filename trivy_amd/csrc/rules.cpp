@@ -929,12 +929,10 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     }
   }
   {
-    uint32_t nb = 16, ns = 8, nw = 6;
+    uint32_t nb = 16, nw = 6;
     if (const char* e = std::getenv("TSG_FILTER_BUCKETS")) nb = uint32_t(std::atoi(e));
-    if (const char* e = std::getenv("TSG_FILTER_SLOTS")) ns = uint32_t(std::atoi(e));
-    if (const char* e = std::getenv("TSG_FILTER_WINDOW")) nw = uint32_t(std::atoi(e));
     auto ft = std::make_shared<FilterTables>();
-    if (!BuildFilter(out->items, ns, nw, nb, ft.get(), err)) return false;
+    if (!BuildFilter(out->items, nw, nb, ft.get(), err)) return false;
     out->filter = ft;
   }
   return BuildAc(pats, out, err);
