@@ -63,7 +63,7 @@ class GpuEngine {
   bool wide_table_ = false;
   uint32_t thr_ = 0, fold_entry_ = 0, cls_i_ = 0, cls_k_ = 0, cls_s_ = 0, div_magic_ = 0;
   void* d_tabs_ = nullptr;
-  uint32_t diag_mode_ = 0;
+  uint32_t diag_mode_ = 0, diag_confirm_ = 0;
   uint32_t tabs_bytes_ = 0, tab_out_off_ = 0, tab_out_items_ = 0, tab_anchors_ = 0, tab_la_ = 0;
   uint32_t* d_out_off_ = nullptr;
   uint32_t* d_out_items_ = nullptr;
@@ -86,7 +86,7 @@ class GpuEngine {
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0;
   size_t c_lds_bytes_ = 0;
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;
-  uint32_t rec_cap_ = 0;
+  uint32_t rec_cap_ = 0, fold_cap_ = 0, n_fitems_ = 0;
   // per-batch buffers
   void* d_chunk_file_ = nullptr; size_t cap_chunk_file_ = 0;
   void* d_nl_ = nullptr; size_t cap_nl_ = 0;
@@ -95,10 +95,10 @@ class GpuEngine {
   void* d_hits_ = nullptr; size_t cap_hits_ = 0;
   void* d_cands_ = nullptr; size_t cap_cands_ = 0;
   void* d_special_ = nullptr; size_t cap_special_ = 0;
-  void* d_chunk_list_ = nullptr; size_t cap_chunk_list_ = 0;
+  void* d_folds_ = nullptr; size_t cap_folds_ = 0;
   uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
-                                    // [5] careful chunk-list length [7] flagged-block records
-                                    // [8] record overflow
+                                    // [7] flagged-block records [8] record overflow
+                                    // [9] fold sites [10] fold-site overflow
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
   void* d_params_ = nullptr; size_t cap_params_ = 0;

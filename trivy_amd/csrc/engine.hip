@@ -825,6 +825,36 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
 // K2: confirm flagged blocks exactly + verify the anchor hits
 // ---------------------------------------------------------------------------
 constexpr int kCThreads = 256;
+
+struct FoldSite {  // a fold rune (U+0130 / U+212A / U+017F) at arena byte x of file f
+  uint64_t x;
+  uint32_t f;
+  uint32_t len;
+};
+
+// One slot per active lane; one atomic per call per wave (divergence-safe:
+// the ballot covers exactly the lanes that call).
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
+  const uint64_t m = __ballot(1);
+  const uint32_t leader = uint32_t(__ffsll(static_cast<unsigned long long>(m)) - 1);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+  uint32_t base = 0;
+  if (rank == 0) base = atomicAdd(ctr, uint32_t(__popcll(m)));
+  base = __shfl(base, int(leader));
+  return base + rank;
+}
+
+__device__ __forceinline__ void put_hit(uint32_t* hits, uint32_t cap, uint32_t* counters, uint32_t f, uint32_t end,
+                                        uint32_t aid) {
+  const uint32_t g = wave_slot(&counters[0]);
+  if (g < cap) {
+    hits[3ull * g + 0] = f;
+    hits[3ull * g + 1] = end;
+    hits[3ull * g + 2] = aid;
+  } else {
+    counters[3] = 1;
+  }
+}
 constexpr int kCWin = 64;  // per-lane LDS copy of arena bytes [base - 16, base + 48)
 
 struct ConfirmParams {
@@ -844,9 +874,12 @@ struct ConfirmParams {
   uint32_t* flags;
   uint32_t* special;
   uint32_t special_cap;
-  uint32_t* counters;  // [1] candidates [2] special files [4] cand overflow [7] records
-  Candidate* cands;
-  uint32_t cand_cap;
+  uint32_t* counters;  // [0] hits [2] special files [3] hit overflow [7] records [9] folds [10] fold overflow
+  uint32_t* hits;      // (file, literal end in the file, anchor id)
+  uint32_t hit_cap;
+  FoldSite* folds;     // fold runes found (for the fold kernel)
+  uint32_t fold_cap;
+  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -916,16 +949,30 @@ __device__ bool nfa_dispatch_abs(int words, const uint8_t* arena, uint64_t fs, i
   }
 }
 
-__device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64_t a, uint64_t b) {  // arena [a, b)
+// '\n' in arena [a, b) with aligned 16-B loads (bytes outside the range masked to 0)
+__device__ int64_t count_nl_range(const uint8_t* arena, uint64_t a, uint64_t b) {
   int64_t n = 0;
-  const uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
-  if (ca >= cb) {
-    for (uint64_t p = a; p < b; p++) n += arena[p] == '\n';
-    return n;
+  for (uint64_t blk = a & ~uint64_t(15); blk < b; blk += 16) {
+    const uint4 v = load16(arena + blk);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint64_t wa = blk + 4 * q;
+      const uint32_t lo = a > wa ? uint32_t(a - wa < 4 ? a - wa : 4) : 0u;
+      const uint32_t hi = b < wa + 4 ? (b > wa ? uint32_t(b - wa) : 0u) : 4u;
+      if (hi <= lo) continue;
+      const uint32_t mhi = hi == 4 ? ~0u : (1u << (8 * hi)) - 1u;
+      const uint32_t mlo = ~((1u << (8 * lo)) - 1u);
+      n += nl_count4(word_of(v, q) & mhi & mlo);
+    }
   }
-  for (uint64_t p = a; p < ca * kChunk; p++) n += arena[p] == '\n';
+  return n;
+}
+
+__device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64_t a, uint64_t b) {  // arena [a, b)
+  const uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
+  if (ca >= cb) return count_nl_range(arena, a, b);
+  int64_t n = count_nl_range(arena, a, ca * kChunk) + count_nl_range(arena, cb * kChunk, b);
   for (uint64_t c = ca; c < cb; c++) n += nl[c];
-  for (uint64_t p = cb * kChunk; p < b; p++) n += arena[p] == '\n';
   return n;
 }
 
@@ -986,6 +1033,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
       while (fm) {
         const uint32_t j = __builtin_ctz(fm);
         fm &= fm - 1;
+        if (P.diag & 4) continue;
         for (uint32_t x = bucket_off[j]; x < bucket_off[j + 1]; x++) {
           const FilterItemGpu it = items[bucket_items[x]];
           const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
@@ -1013,39 +1061,113 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
               const uint32_t q = atomicAdd(&P.counters[2], 1u);
               if (q < P.special_cap) P.special[q] = f;
             }
+            const uint32_t q = wave_slot(&P.counters[9]);
+            if (q < P.fold_cap) P.folds[q] = FoldSite{s0, f, it.n};
+            else P.counters[10] = 1;
             continue;
           }
-          const int64_t lit_end = int64_t(s0 - fs) + it.lit_end;
-          const int64_t len = int64_t(fe - fs);
-          for (uint32_t d = 0; d < it.n_ids; d++) {
-            const AnchorInfo an = P.anchors[item_ids[it.ids_off + d]];
-            const RuleGpu rg = P.rules[an.rule];
-            const int64_t lit_hi = lit_end - an.lit_len;
-            const int64_t whi = lit_hi - an.off_lo;
-            if (whi < 0) continue;
-            int64_t wlo = lit_hi - an.off_hi;
-            if (wlo < 0) wlo = 0;
-            const bool acc = rg.nfa_words == 0 ||
-                             nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off);
-            if (!acc) continue;
-            const uint32_t kc = atomicAdd(&P.counters[1], 1u);
-            if (kc < P.cand_cap) {
-              Candidate c;
-              c.file = f;
-              c.rule = an.rule;
-              c.wlo = wlo;
-              c.whi = whi;
-              c.nl_before = count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(wlo));
-              c.flags = 0;
-              c.pad = 0;
-              P.cands[kc] = c;
-            } else {
-              P.counters[4] = 1;
-            }
-          }
+          const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
+          for (uint32_t d = 0; d < it.n_ids; d++)
+            put_hit(P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
         }
       }
     }
+  }
+}
+
+// Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
+// exact filter; for each fold site and each item, every item start that puts
+// the rune inside the item is tried with a fold-tolerant match: a position
+// also accepts U+212A (E2 84 AA) when its set holds k/K and U+017F (C5 BF)
+// when it holds s/S (the only non-ASCII runes (?i) folds onto ASCII letters),
+// advancing 3 / 2 bytes.  A superset of the true occurrences; hits carry the
+// literal end in bytes.  One thread per (site, item).
+struct FoldParams {
+  const uint8_t* arena;
+  const uint64_t* off;
+  const void* tabs;
+  uint32_t tabs_bytes, t_items, t_item_ids, t_item_cls, t_classes, n_items;
+  const FoldSite* folds;
+  uint32_t fold_cap;
+  uint32_t* hits;
+  uint32_t hit_cap;
+  uint32_t* counters;
+};
+
+__global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  {
+    const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
+    uint4* d = reinterpret_cast<uint4*>(smem);
+    for (uint32_t i = threadIdx.x; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
+  }
+  __syncthreads();
+  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(smem + P.t_items);
+  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(smem + P.t_item_ids);
+  const uint8_t* item_cls = smem + P.t_item_cls;
+  const uint32_t* classes = reinterpret_cast<const uint32_t*>(smem + P.t_classes);
+  const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
+  const uint64_t total = uint64_t(n_folds) * P.n_items;
+  auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
+  for (uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; t < total; t += uint64_t(gridDim.x) * blockDim.x) {
+    const FoldSite fsite = P.folds[t / P.n_items];
+    const FilterItemGpu it = items[t % P.n_items];
+    if (it.kind != kItemAnchor) continue;
+    const uint64_t fs = P.off[fsite.f], fe = P.off[fsite.f + 1];
+    const uint64_t lo = fsite.x > fs + 3ull * it.n ? fsite.x - 3ull * it.n : fs;
+    for (uint64_t st = lo; st <= fsite.x; st++) {
+      uint64_t p = st, lit_bytes_end = 0;
+      bool ok = true;
+      for (uint32_t q = 0; q < it.n && ok; q++) {
+        if (q == it.lit_end) lit_bytes_end = p;
+        if (p >= fe) {
+          ok = false;
+          break;
+        }
+        const uint32_t c = item_cls[it.cls_off + q];
+        const uint32_t b = P.arena[p];
+        if (b == 0xE2 && p + 2 < fe && P.arena[p + 1] == 0x84 && P.arena[p + 2] == 0xAA &&
+            (in_cls(c, 'k') || in_cls(c, 'K'))) {
+          p += 3;
+        } else if (b == 0xC5 && p + 1 < fe && P.arena[p + 1] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
+          p += 2;
+        } else if (in_cls(c, b)) {
+          p += 1;
+        } else {
+          ok = false;
+        }
+      }
+      if (!ok || p <= fsite.x) continue;  // the item must contain the fold rune
+      if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
+      for (uint32_t d = 0; d < it.n_ids; d++)
+        put_hit(P.hits, P.hit_cap, P.counters, fsite.f, uint32_t(lit_bytes_end - fs), item_ids[it.ids_off + d]);
+    }
+  }
+}
+
+// Verify kernel: one lane per anchor hit.  The start window comes from the
+// literal position and the anchor's offsets (wider in files with fold runes,
+// whose literal bytes may be up to 3x its length); the rule's relaxed NFA runs
+// from wlo with injection up to whi, reading the arena 16 B at a time; an
+// accept emits the candidate with the line count before wlo.
+__global__ __launch_bounds__(256) void verify_hits_kernel(NfaParams P) {
+  const uint32_t n = P.counters[0] < P.hit_cap ? P.counters[0] : P.hit_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t f = P.hits[3ull * i], end = P.hits[3ull * i + 1], aid = P.hits[3ull * i + 2];
+    const AnchorInfo a = P.anchors[aid];
+    const RuleGpu rg = P.rules[a.rule];  // keyword gates are evaluated lazily by the host tail
+    const uint32_t ff = P.flags[f];
+    const int64_t lit_hi = int64_t(end) - int64_t(a.lit_len);
+    const int64_t lit_lo = (ff & 1u) ? int64_t(end) - 3 * int64_t(a.lit_len) : lit_hi;
+    const int64_t whi = lit_hi - a.off_lo;
+    if (whi < 0) continue;
+    int64_t wlo = lit_lo - ((ff & 1u) ? int64_t(a.off_hi_fold) : int64_t(a.off_hi));
+    if (wlo < 0) wlo = 0;
+    const uint64_t fs = P.off[f];
+    const int64_t len = int64_t(P.off[f + 1] - fs);
+    const bool acc =
+        rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off);
+    if (acc) emit_candidate(P, f, a.rule, wlo, whi, count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(wlo)), 0u);
   }
 }
 
@@ -1076,6 +1198,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   }
   for (auto& e : ev_) hipEventCreate(&e);
   if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
+  if (const char* dc = std::getenv("TSG_DIAG_CONFIRM")) diag_confirm_ = uint32_t(std::atoi(dc));
   n_states_ = cr.n_states;
   n_classes_ = cr.n_classes;
   max_pat_len_ = cr.max_pat_len;
@@ -1260,6 +1383,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     ft_classes_ = put(ft->classes.data(), ft->classes.size() * 4);
     if (tb.empty()) tb.assign(16, 0);
     ftabs_bytes_ = uint32_t(tb.size());
+    n_fitems_ = uint32_t(ft->items.size());
     uint8_t* d = nullptr;
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_ftabs_ = d;
@@ -1275,7 +1399,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_reach_, d_ftabs_, d_chunk_list_, d_recs_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
+  void* ps[] = {d_reach_, d_ftabs_, d_folds_, d_recs_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
                 d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_, d_params_};
   for (void* p : ps)
@@ -1323,17 +1447,16 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
   if (n_chunks == 0) n_chunks = 1;
-  if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 256, 1 << 16), 1u << 30));
+  if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 512, 1 << 16), 1u << 28));
   if (cand_cap_ == 0) cand_cap_ = 1 << 16;
   if (rec_cap_ == 0) rec_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 128, 1 << 16), 1u << 30));
-  const uint32_t list_cap =
-      uint32_t(std::min<uint64_t>((n_bytes + kCarefulUnit - 1) / kCarefulUnit + n_files, 0xFFFFFFF0u));
+  if (fold_cap_ == 0) fold_cap_ = 1 << 16;
   for (int attempt = 0; attempt < 8; attempt++) {
     if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, n_chunks * 2) ||
         !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
         !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
         !Ensure(&d_special_, &cap_special_, size_t(n_files) * 4) ||
-        !Ensure(&d_chunk_list_, &cap_chunk_list_, size_t(list_cap) * 4) ||
+        !Ensure(&d_folds_, &cap_folds_, size_t(fold_cap_) * sizeof(FoldSite)) ||
         !Ensure(&d_recs_, &cap_recs_, size_t(rec_cap_) * 4) ||
         !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
         !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
@@ -1387,68 +1510,33 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.special = static_cast<uint32_t*>(d_special_);
     cp.special_cap = n_files;
     cp.counters = d_counters_;
-    cp.cands = static_cast<Candidate*>(d_cands_);
-    cp.cand_cap = cand_cap_;
+    cp.hits = static_cast<uint32_t*>(d_hits_);
+    cp.hit_cap = hit_cap_;
+    cp.folds = static_cast<FoldSite*>(d_folds_);
+    cp.fold_cap = fold_cap_;
+    cp.diag = diag_confirm_;
     if (diag_mode_ == 0) confirm_kernel<<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[2], stream_));
-    // careful pass over the chunks of fold-rune files (Aho-Corasick on the bytes.ToLower symbol stream)
-    special_chunks_kernel<<<1024, 256, 0, stream_>>>(d_offsets, static_cast<const uint32_t*>(d_special_), d_counters_,
-                                                   static_cast<uint32_t*>(d_chunk_list_), list_cap);
-    ScanParams sp;
-    sp.arena = d_arena;
-    sp.n_bytes = n_bytes;
-    sp.off = d_offsets;
-    sp.n_files = n_files;
-    sp.chunk_file = static_cast<const uint32_t*>(d_chunk_file_);
-    sp.n_chunks = n_chunks;
-    sp.cmap = d_cmap_;
-    sp.trans = d_trans_;
-    sp.out_off = d_out_off_;
-    sp.out_items = d_out_items_;
-    sp.anchors = d_anchors_;
-    sp.la = d_la_;
-    sp.thr = thr_;
-    sp.fold_entry = fold_entry_;
-    sp.cls_i = cls_i_;
-    sp.cls_k = cls_k_;
-    sp.cls_s = cls_s_;
-    sp.div_magic = div_magic_;
-    sp.diag_mode = 0;
-    sp.tabs = d_tabs_;
-    sp.tabs_bytes = tabs_bytes_;
-    sp.tab_out_off = tab_out_off_;
-    sp.tab_out_items = tab_out_items_;
-    sp.tab_anchors = tab_anchors_;
-    sp.tab_la = tab_la_;
-    sp.n_states = n_states_;
-    sp.n_classes = n_classes_;
-    sp.warm = max_pat_len_ > 0 ? max_pat_len_ - 1 : 0;
-    sp.warm_blocks = (sp.warm + 15) / 16;
-    sp.kw_words = kw_words_;
-    sp.kwbits = static_cast<uint32_t*>(d_kw_);
-    sp.flags = static_cast<uint32_t*>(d_flags_);
-    sp.nl = static_cast<uint16_t*>(d_nl_);
-    sp.hits = static_cast<uint32_t*>(d_hits_);
-    sp.hit_cap = hit_cap_;
-    sp.counters = d_counters_;
-    sp.special = static_cast<uint32_t*>(d_special_);
-    sp.special_cap = n_files;
-    sp.chunk_list = static_cast<const uint32_t*>(d_chunk_list_);
-    sp.chunk_list_n = d_counters_ + 5;
-    sp.chunk_list_cap = list_cap;
-    {
-      uint32_t per_cu = std::max<uint32_t>(1, uint32_t((160 * 1024) / lds_bytes_));
-      uint32_t grid = 256 * per_cu;
-      if (wide_table_) {
-        if (table_in_lds_) scan_kernel<uint32_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-        else scan_kernel<uint32_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-      } else {
-        if (table_in_lds_) scan_kernel<uint16_t, true><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-        else scan_kernel<uint16_t, false><<<grid, kScanThreads, lds_bytes_, stream_>>>(sp);
-      }
-    }
+    // fold runes: fold-tolerant item matching around each one
+    FoldParams fo;
+    fo.arena = d_arena;
+    fo.off = d_offsets;
+    fo.tabs = d_ftabs_;
+    fo.tabs_bytes = ftabs_bytes_;
+    fo.t_items = ft_items_;
+    fo.t_item_ids = ft_item_ids_;
+    fo.t_item_cls = ft_item_cls_;
+    fo.t_classes = ft_classes_;
+    fo.n_items = n_fitems_;
+    fo.folds = static_cast<const FoldSite*>(d_folds_);
+    fo.fold_cap = fold_cap_;
+    fo.hits = static_cast<uint32_t*>(d_hits_);
+    fo.hit_cap = hit_cap_;
+    fo.counters = d_counters_;
+    if (diag_mode_ == 0) fold_kernel<<<512, 256, ftabs_bytes_, stream_>>>(fo);
     HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev_[3], stream_));
     NfaParams np;
     np.arena = d_arena;
     np.off = d_offsets;
@@ -1472,9 +1560,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.n_regex_rules = uint32_t(regex_rules_.size());
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
-    verify_kernel<<<256, 256, 0, stream_>>>(np);  // hits of the careful pass
+    if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[3], stream_));
     if (np.n_fullscan_rules > 0) {
       fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
       HIP_OK(hipGetLastError());
@@ -1492,9 +1579,9 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     }
     st->hit_overflow = cnt[3] != 0;
     st->cand_overflow = cnt[4] != 0;
-    if (cnt[5] > list_cap) {
-      err_ = "careful chunk list overflow";
-      return false;
+    if (cnt[10]) {  // fold site list overflow
+      fold_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[9]) + cnt[9] / 4 + 1024, 0xFFFFFFF0u / 16));
+      continue;
     }
     if (st->hit_overflow) {  // grow and rescan (correctness first)
       hit_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[0]) + cnt[0] / 4 + 1024, 0xFFFFFFF0u / 12));
@@ -1513,7 +1600,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     }
     hipEventElapsedTime(&st->ms_scan, ev_[0], ev_[1]);
     hipEventElapsedTime(&st->ms_confirm, ev_[1], ev_[2]);
-    hipEventElapsedTime(&st->ms_careful, ev_[2], ev_[3]);
+    hipEventElapsedTime(&st->ms_careful, ev_[2], ev_[3]);  // fold kernel
+    hipEventElapsedTime(&st->ms_verify, ev_[3], ev_[4]);   // verify + full-scan
     hipEventElapsedTime(&st->ms_fullscan, ev_[3], ev_[4]);
     hipEventElapsedTime(&st->ms_total, ev_[0], ev_[4]);
     return true;

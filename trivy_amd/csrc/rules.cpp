@@ -673,26 +673,81 @@ bool FixedSets(const std::vector<Node>& nodes, int i, std::vector<ByteSet>* out,
   }
 }
 
-// Mandatory fixed-width sets right after a literal (up to `cap`): whole fixed
-// items, then the mandatory part of the first variable repeat of a class.
+// Byte sets at the first offsets after a literal, for any match: first the
+// exact (ASCII) sets of whole fixed-width items, then "continuation sets" from
+// the relaxed NFA of the remaining items -- offset i's set is the union of the
+// byte reaches of the positions the NFA can be in after i bytes.  A continuation
+// byte (0x80-0xBF) keeps the state (as in the NFA) and once the match may have
+// ended the offset is unconstrained, so every match satisfies every set: a
+// superset filter.  Trailing all-byte sets are dropped.
 std::vector<ByteSet> AfterSets(const std::vector<Node>& nodes, const std::vector<int>& fol, size_t cap) {
   std::vector<ByteSet> out;
-  for (int it : fol) {
-    if (out.size() >= cap) break;
+  size_t k = 0;
+  for (; k < fol.size() && out.size() < cap; k++) {
     std::vector<ByteSet> b;
-    if (FixedSets(nodes, it, &b, cap - out.size())) {
-      out.insert(out.end(), b.begin(), b.end());
-      continue;
-    }
-    const Node& n = nodes[it];
-    if (n.op == NodeOp::Repeat && n.min >= 1) {
-      std::vector<ByteSet> one;
-      if (FixedSets(nodes, n.subs[0], &one, cap)) {
-        for (int r = 0; r < n.min && out.size() + one.size() <= cap; r++) out.insert(out.end(), one.begin(), one.end());
-      }
-    }
-    break;
+    if (!FixedSets(nodes, fol[k], &b, cap - out.size())) break;
+    out.insert(out.end(), b.begin(), b.end());
   }
+  if (out.size() < cap && k < fol.size()) {
+    // expand the relaxed sequence into NFA positions (as BuildNfa): a run
+    // {min,max} gives min mandatory + (max-min) optional positions; an
+    // unbounded one max(min,1) positions, the last looping
+    struct P {
+      Reach r;
+      bool opt, loop;
+    };
+    std::vector<P> pos;
+    const size_t kMaxPos = 4 * cap + 8;  // enough to reach `cap` offsets; beyond: unconstrained
+    bool truncated = false;
+    for (size_t q = k; q < fol.size() && !truncated; q++)
+      for (const Elem& e : Relax(nodes, fol[q])) {
+        const int64_t np = Positions(e);
+        for (int64_t j = 0; j < np; j++) {
+          if (pos.size() >= kMaxPos) {
+            truncated = true;
+            break;
+          }
+          P x{e.reach, false, false};
+          if (e.max >= 0) x.opt = j >= e.min;
+          else {
+            x.opt = e.min == 0;
+            x.loop = j == np - 1;
+          }
+          pos.push_back(x);
+        }
+        if (truncated) break;
+      }
+    const size_t n = pos.size();  // index n = end of the (possibly truncated) sequence
+    std::vector<bool> act(n + 1, false);
+    auto activate = [&](std::vector<bool>& a, size_t i) {  // i and the optional positions after it
+      while (i <= n) {
+        a[i] = true;
+        if (i == n || !pos[i].opt) break;
+        i++;
+      }
+    };
+    activate(act, 0);
+    Reach cont;
+    for (int c = 0x80; c < 0xC0; c++) cont.set(size_t(c));
+    while (out.size() < cap) {
+      if (act[n]) break;  // the match may end here: nothing after is constrained
+      Reach set;
+      for (size_t i = 0; i < n; i++)
+        if (act[i]) set |= pos[i].r;
+      if (set.all() || set.none()) break;
+      out.push_back(set);
+      std::vector<bool> nx(n + 1, false);
+      const bool keep = (set & cont).any();
+      for (size_t i = 0; i < n; i++) {
+        if (!act[i]) continue;
+        if (keep) nx[i] = true;
+        if (pos[i].loop) nx[i] = true;
+        activate(nx, i + 1);
+      }
+      act.swap(nx);
+    }
+  }
+  while (!out.empty() && out.back().all()) out.pop_back();
   if (out.size() > cap) out.resize(cap);
   return out;
 }
