@@ -1156,8 +1156,14 @@ struct FoldParams {
   uint32_t* counters;
 };
 
+constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
+
+// One workgroup per fold site: the bytes [x - kFoldSpan, x + kFoldSpan) go to
+// LDS, the threads split the (item, start) pairs.  U+0130 sites only flag the
+// file (Go's (?i) does not fold U+0130 onto 'i').
 __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint8_t s_bytes[2 * kFoldSpan + 16];
   {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(smem);
@@ -1168,30 +1174,37 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
   const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(smem + P.t_item_ids);
   const uint8_t* item_cls = smem + P.t_item_cls;
   const uint32_t* classes = reinterpret_cast<const uint32_t*>(smem + P.t_classes);
-  const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
-  const uint64_t total = uint64_t(n_folds) * P.n_items;
   auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
-  for (uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; t < total; t += uint64_t(gridDim.x) * blockDim.x) {
-    const FoldSite fsite = P.folds[t / P.n_items];
-    const FilterItemGpu it = items[t % P.n_items];
-    if (it.kind != kItemAnchor) continue;
+  const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
+  for (uint32_t si = blockIdx.x; si < n_folds; si += gridDim.x) {
+    const FoldSite fsite = P.folds[si];
     const uint64_t fs = P.off[fsite.f], fe = P.off[fsite.f + 1];
-    const uint64_t lo = fsite.x > fs + 3ull * it.n ? fsite.x - 3ull * it.n : fs;
-    for (uint64_t st = lo; st <= fsite.x; st++) {
+    const uint64_t w0 = fsite.x > fs + kFoldSpan ? fsite.x - kFoldSpan : fs;
+    const uint64_t w1 = fsite.x + kFoldSpan < fe ? fsite.x + kFoldSpan : fe;  // window [w0, w1)
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < uint32_t(w1 - w0); i += blockDim.x) s_bytes[i] = P.arena[w0 + i];
+    __syncthreads();
+    if (P.arena[fsite.x] == 0xC4) continue;  // U+0130: uniform per block
+    const uint32_t span = uint32_t(fsite.x - w0) + 1;  // starts w0 .. x
+    const uint32_t total = P.n_items * span;
+    for (uint32_t t = threadIdx.x; t < total; t += blockDim.x) {
+      const FilterItemGpu it = items[t / span];
+      const uint64_t st = w0 + t % span;
+      if (it.kind != kItemAnchor || fsite.x - st > 3ull * it.n) continue;
       uint64_t p = st, lit_bytes_end = 0;
       bool ok = true;
       for (uint32_t q = 0; q < it.n && ok; q++) {
         if (q == it.lit_end) lit_bytes_end = p;
-        if (p >= fe) {
+        if (p >= w1) {
           ok = false;
           break;
         }
         const uint32_t c = item_cls[it.cls_off + q];
-        const uint32_t b = P.arena[p];
-        if (b == 0xE2 && p + 2 < fe && P.arena[p + 1] == 0x84 && P.arena[p + 2] == 0xAA &&
+        const uint32_t b = s_bytes[p - w0];
+        if (b == 0xE2 && p + 2 < w1 && s_bytes[p + 1 - w0] == 0x84 && s_bytes[p + 2 - w0] == 0xAA &&
             (in_cls(c, 'k') || in_cls(c, 'K'))) {
           p += 3;
-        } else if (b == 0xC5 && p + 1 < fe && P.arena[p + 1] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
+        } else if (b == 0xC5 && p + 1 < w1 && s_bytes[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
           p += 2;
         } else if (in_cls(c, b)) {
           p += 1;
