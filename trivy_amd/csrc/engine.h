@@ -81,6 +81,9 @@ class GpuEngine {
   bool table_in_lds_ = true;
   // streaming prefilter (filter.h)
   uint32_t* d_reach_ = nullptr;
+  uint64_t* d_core_ = nullptr;
+  uint32_t* d_group_items_ = nullptr;
+  uint32_t* d_bucket_groups_ = nullptr;
   void* d_ftabs_ = nullptr;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0;

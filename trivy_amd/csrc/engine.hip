@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "engine.h"
@@ -927,7 +928,10 @@ struct ConfirmParams {
   uint32_t hit_cap;
   FoldSite* folds;     // fold runes found (for the fold kernel)
   uint32_t fold_cap;
-  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks
+  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission
+  const uint64_t* core;           // filter.h core tables (n_groups x 256)
+  const uint32_t* group_items;    // n_groups x 8
+  const uint32_t* bucket_groups;  // n_buckets + 1
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -1095,17 +1099,37 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
         const uint32_t j = __builtin_ctz(fm);
         fm &= fm - 1;
         if (P.diag & 4) continue;
-        for (uint32_t x = bucket_off[j]; x < bucket_off[j + 1]; x++) {
-          const FilterItemGpu it = items[bucket_items[x]];
+        // the 8 bytes ending at the window end (before the arena: zero bytes, as in K1)
+        uint32_t cb[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const int64_t pos = int64_t(base + k) - 7 + q;
+          cb[q] = pos < 0 ? 0u : uint32_t(win[uint64_t(pos) - wbase]);
+        }
+        for (uint32_t g = P.bucket_groups[j]; g < P.bucket_groups[j + 1]; g++) {
+          uint64_t cm = ~uint64_t(0);
+          const uint64_t* ct = P.core + size_t(g) * 256;
+#pragma unroll
+          for (int q = 0; q < 8; q++) cm &= ct[cb[q]] >> (8 * q);
+          uint32_t im = uint32_t(cm) & 0xFFu;
+          while (im) {
+          const uint32_t gi = __builtin_ctz(im);
+          im &= im - 1;
+          const FilterItemGpu it = items[P.group_items[g * 8 + gi]];
           const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
           if (start < 0 || uint64_t(start) + it.n > P.n_bytes) continue;
           bool ok = true;
+          const uint32_t core_lo = it.back > 8 ? it.back - 8u : 0u;  // positions [core_lo, back) are verified
           for (uint32_t q = 0; q < it.n && ok; q++) {
+            if (q == core_lo) {
+              q = it.back - 1u;
+              continue;
+            }
             const uint32_t bt = byte_at(uint64_t(start) + q);
             const uint32_t c = item_cls[it.cls_off + q];
             ok = (classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u;
           }
-          if (!ok) continue;
+          if (!ok || (P.diag & 16)) continue;
           const uint64_t s0 = uint64_t(start);
           uint32_t f = P.chunk_file[s0 / kChunk];
           uint64_t fs = P.off[f], fe = P.off[f + 1];
@@ -1115,6 +1139,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
             fe = P.off[f + 1];
           }
           if (s0 < fs || s0 + it.n > fe) continue;  // crosses a file boundary
+          if (P.diag & 8) continue;
           if (it.kind == kItemFold) {
             const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 1u;
             const uint32_t old = atomicOr(&P.flags[f], fl);
@@ -1130,6 +1155,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
           const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
           for (uint32_t d = 0; d < it.n_ids; d++)
             stage_hit(hbuf, hcnt, P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
+          }
         }
       }
     }
@@ -1440,7 +1466,11 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       err_ = "prefilter shape not supported by the scan kernel (needs 16 buckets, window 6)";
       return;
     }
-    if (!Upload(&err_, &d_reach_, ft->reach.data(), ft->reach.size())) return;
+    if (!Upload(&err_, &d_reach_, ft->reach.data(), ft->reach.size()) ||
+        !Upload(&err_, &d_core_, ft->core.data(), ft->core.size()) ||
+        !Upload(&err_, &d_group_items_, ft->group_items.data(), ft->group_items.size()) ||
+        !Upload(&err_, &d_bucket_groups_, ft->bucket_groups.data(), ft->bucket_groups.size()))
+      return;
     auto pad = [](std::vector<uint8_t>& v) { v.resize((v.size() + 15) & ~size_t(15), 0); };
     std::vector<uint8_t> tb;
     auto put = [&](const void* src, size_t n) {
@@ -1474,7 +1504,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_reach_, d_ftabs_, d_folds_, d_recs_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
+  void* ps[] = {d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
                 d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
                 d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_, d_params_};
   for (void* p : ps)
@@ -1590,6 +1620,9 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.folds = static_cast<FoldSite*>(d_folds_);
     cp.fold_cap = fold_cap_;
     cp.diag = diag_confirm_;
+    cp.core = d_core_;
+    cp.group_items = d_group_items_;
+    cp.bucket_groups = d_bucket_groups_;
     if (diag_mode_ == 0) confirm_kernel<<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[2], stream_));
@@ -1645,6 +1678,9 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     uint32_t cnt[16];
     HIP_OK(hipMemcpyAsync(cnt, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
+    if (std::getenv("TSG_STATS_DEBUG"))
+      std::fprintf(stderr, "counters: hits %u cands %u special %u recs %u folds %u\n", cnt[0], cnt[1], cnt[2], cnt[7],
+                   cnt[9]);
     st->hits = cnt[0];
     st->special_files = cnt[2];
     st->flagged_blocks = cnt[7];

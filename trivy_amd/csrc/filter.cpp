@@ -216,6 +216,33 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     }
     out->bucket_off.push_back(uint32_t(out->bucket_items.size()));
   }
+  // core tables (filter.h)
+  out->bucket_groups.push_back(0);
+  uint32_t n_groups = 0;
+  for (uint32_t b = 0; b < n_buckets; b++) {
+    const uint32_t lo = out->bucket_off[b], hi = out->bucket_off[b + 1];
+    for (uint32_t g0 = lo; g0 < hi; g0 += 8) {
+      std::vector<uint64_t> tab(256, 0);
+      for (uint32_t i = 0; i < 8; i++) {
+        if (g0 + i >= hi) {
+          out->group_items.push_back(0xFFFFFFFFu);
+          continue;
+        }
+        const uint32_t item = out->bucket_items[g0 + i];
+        out->group_items.push_back(item);
+        const FilterItem& it = uniq[item];
+        const int back = out->items[item].back;
+        for (int sl = 0; sl < 8; sl++) {
+          const int q = back - 8 + sl;
+          for (int x = 0; x < 256; x++)
+            if (q < 0 || it.sets[size_t(q)].test(size_t(x))) tab[size_t(x)] |= uint64_t(1) << (8 * sl + i);
+        }
+      }
+      out->core.insert(out->core.end(), tab.begin(), tab.end());
+      n_groups++;
+    }
+    out->bucket_groups.push_back(n_groups);
+  }
   for (auto& b : classes) {
     uint32_t w[8] = {};
     for (int x = 0; x < 256; x++)

@@ -48,6 +48,15 @@ struct FilterTables {
   std::vector<uint32_t> item_ids;        // anchor / fold ids per item
   std::vector<uint8_t> item_cls;         // class id per item position (< 256)
   std::vector<uint32_t> classes;         // 8 x u32 membership words per class
+  // Core tables for the confirm step: a bucket's items in groups of 8; per
+  // group and byte b, bit 8*s + i of core[g * 256 + b] is 1 when b may stand at
+  // core slot s of the group's item i -- the item positions back-8 .. back-1,
+  // i.e. the 8 bytes ending at the window end (slots before the item start
+  // allow every byte).  One AND over 8 independent lookups gives the items
+  // whose core matches at a fire.
+  std::vector<uint64_t> core;            // n_groups x 256
+  std::vector<uint32_t> group_items;     // n_groups x 8 item indices (0xFFFFFFFF: none)
+  std::vector<uint32_t> bucket_groups;   // n_buckets + 1 into the groups
   uint32_t max_after = 0;                // max positions an item extends past its window end
   double est_fp = 0;                     // estimated bucket fires per input byte
 
