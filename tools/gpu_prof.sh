@@ -19,7 +19,7 @@ import csv, glob, sys, collections
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if "filter_kernel" in r.get("Kernel_Name", ""):
+        if __import__("os").environ.get("KNAME", "filter_kernel") in r.get("Kernel_Name", ""):
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
     print(sys.argv[1], dict(agg))
 PY

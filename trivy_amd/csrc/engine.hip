@@ -1028,21 +1028,32 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
   return n;
 }
 
-// K2.  One lane per flagged block: the 64 arena bytes around it go to the
-// lane's LDS window; the bucket fires are recomputed from the 5 bytes before
-// the block; every item of a fired bucket is checked exactly (bytes from the
-// window, global beyond it); a matching item is attributed to its file
-// (chunk map) and, for each of its anchors, the rule's relaxed NFA runs from
-// the start window [wlo, whi] -- an accept emits the candidate, with the
-// line count before wlo from K1's per-chunk newline counts.  Fold-rune items
-// flag their file for the careful pass instead.
+// K2.  Flagged blocks are confirmed in three wave-wide phases with LDS work
+// queues between them, so every phase runs on full waves instead of diverging
+// per lane:
+//   A  one block per lane: its 64 arena bytes [base-16, base+48) go to the
+//      lane's LDS window; the bucket fires are recomputed from the 5 bytes
+//      before it; each fire position queues (lane, k, bucket mask);
+//   B  one fire per lane: per fired bucket group, one AND over the 8 core-table
+//      lookups of the bytes ending at k gives the items whose core matches;
+//      each queues (lane, k, item);
+//   C  one candidate item per lane: the item's positions outside the core are
+//      checked, the start is attributed to its file (chunk map) and the anchor
+//      hits (or the fold site) are staged.
+constexpr uint32_t kCQ1 = 256;  // fires (overflow: handled in place)
+constexpr uint32_t kCQ2 = 256;  // candidate items (overflow: checked in place)
+
 __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* s_reach = smem;                   // 4 KiB: one copy per byte (a few conflicts are fine here)
-  uint8_t* s_win = smem + 4096;              // kCThreads x 64 B
-  uint32_t* s_hbuf = reinterpret_cast<uint32_t*>(s_win + kCThreads * kCWin);  // per wave kCWaveHits x 12 B
-  uint32_t* s_hcnt = s_hbuf + (kCThreads / 64) * kCWaveHits * 3;
-  uint8_t* s_tabs = reinterpret_cast<uint8_t*>(s_hcnt + 4);
+  constexpr uint32_t kWaves = kCThreads / 64;
+  uint8_t* s_reach = smem;                                                      // 4 KiB, one copy per byte
+  uint8_t* s_win = smem + 4096;                                                 // kCThreads x 64 B
+  uint64_t* s_base = reinterpret_cast<uint64_t*>(s_win + kCThreads * kCWin);    // kCThreads
+  uint32_t* s_q1 = reinterpret_cast<uint32_t*>(s_base + kCThreads);             // kWaves x kCQ1
+  uint32_t* s_q2 = s_q1 + kWaves * kCQ1;                                        // kWaves x kCQ2
+  uint32_t* s_hbuf = s_q2 + kWaves * kCQ2;                                      // kWaves x kCWaveHits x 3
+  uint32_t* s_cnt = s_hbuf + kWaves * kCWaveHits * 3;                           // kWaves x 4
+  uint8_t* s_tabs = reinterpret_cast<uint8_t*>(s_cnt + kWaves * 4);
   const int tid = threadIdx.x;
   load_reach_lds(s_reach, P.reach, 1, tid, blockDim.x);
   {
@@ -1050,117 +1061,166 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     uint4* d = reinterpret_cast<uint4*>(s_tabs);
     for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
   }
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2
+  if (lane < 4) cnt[lane] = 0;
   __syncthreads();
-  const uint32_t* bucket_off = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_off);
-  const uint32_t* bucket_items = reinterpret_cast<const uint32_t*>(s_tabs + P.t_bucket_items);
   const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(s_tabs + P.t_items);
   const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(s_tabs + P.t_item_ids);
   const uint8_t* item_cls = s_tabs + P.t_item_cls;
   const uint32_t* classes = reinterpret_cast<const uint32_t*>(s_tabs + P.t_classes);
-  uint8_t* win = s_win + tid * kCWin;
-  const uint32_t lane = tid & 63;
-  uint32_t* hbuf = s_hbuf + (tid >> 6) * kCWaveHits * 3;
-  uint32_t* hcnt = s_hcnt + (tid >> 6);
-  if (lane == 0) *hcnt = 0;
-  wave_sync();
+  uint8_t* wwin = s_win + wave * 64 * kCWin;  // the wave's 64 windows
+  uint64_t* wbase = s_base + wave * 64;      // block base per lane
+  uint32_t* q1 = s_q1 + wave * kCQ1;
+  uint32_t* q2 = s_q2 + wave * kCQ2;
+  uint32_t* hbuf = s_hbuf + wave * kCWaveHits * 3;
   const uint32_t n_recs = P.counters[7] < P.rec_cap ? P.counters[7] : P.rec_cap;
-  // wave-uniform trip count, so the hit flush between records is a wave-level step
-  const uint32_t stride = gridDim.x * blockDim.x;
-  const uint32_t first = blockIdx.x * blockDim.x + (tid & ~63u);
-  for (uint32_t r0 = first; r0 < n_recs; r0 += stride) {
-    if (__builtin_amdgcn_readfirstlane(*hcnt) >= 64) flush_staged(hbuf, hcnt, P.hits, P.hit_cap, P.counters, lane);
-    const uint32_t r = r0 + lane;
-    if (r >= n_recs) continue;
-    const uint64_t base = uint64_t(P.recs[r]) * 16;
-    const uint64_t wbase = base >= 16 ? base - 16 : 0;  // window [wbase, wbase + 64)
-    const uint4 d0 = load16(P.arena + wbase), d1 = load16(P.arena + wbase + 16), d2 = load16(P.arena + wbase + 32),
-                d3 = load16(P.arena + wbase + 48);
-    reinterpret_cast<uint4*>(win)[0] = d0;
-    reinterpret_cast<uint4*>(win)[1] = d1;
-    reinterpret_cast<uint4*>(win)[2] = d2;
-    reinterpret_cast<uint4*>(win)[3] = d3;
-    const uint4 pv = base >= 16 ? d0 : make_uint4(0, 0, 0, 0);
-    const uint4 v = base >= 16 ? d1 : d0;
-    auto byte_at = [&](uint64_t pos) -> uint32_t {
-      return (pos >= wbase && pos < wbase + kCWin) ? uint32_t(win[pos - wbase]) : uint32_t(P.arena[pos]);
-    };
-    uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
-    auto rd1 = [&](uint32_t w, uint32_t k) {  // single-copy table: entry b at 16 * b
-      return *reinterpret_cast<const uint4*>(s_reach + (((w >> (8 * k)) & 0xFFu) << 4));
-    };
-    for (uint32_t k = 11; k < 16; k++) reach_apply(rd1(word_of(pv, k >> 2), k & 3), st);
-    for (uint32_t k = 0; k < 16; k++) {
-      reach_apply(rd1(word_of(v, k >> 2), k & 3), st);
-      // fires at window end base + k: slot 5 = bits 20..23 of each register
-      uint32_t fm = 0;
+  auto win_byte = [&](uint32_t l, uint64_t pos) -> uint32_t {  // arena byte via lane l's window
+    const uint64_t b = wbase[l], w0 = b >= 16 ? b - 16 : 0;
+    return (pos >= w0 && pos < w0 + kCWin) ? uint32_t(wwin[l * kCWin + (pos - w0)]) : uint32_t(P.arena[pos]);
+  };
+  // phase C for one queued candidate: item `ix` whose window ends at lane l's block + k
+  auto check_item = [&](uint32_t l, uint32_t k, uint32_t ix) {
+    const FilterItemGpu it = items[ix];
+    const uint64_t base = wbase[l];
+    const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
+    if (start < 0 || uint64_t(start) + it.n > P.n_bytes) return;
+    const uint32_t core_lo = it.back > 8 ? it.back - 8u : 0u;  // [core_lo, back) verified by the core tables
+    for (uint32_t q = 0; q < it.n; q++) {
+      if (q == core_lo) {
+        q = it.back - 1u;
+        continue;
+      }
+      const uint32_t bt = win_byte(l, uint64_t(start) + q);
+      const uint32_t c = item_cls[it.cls_off + q];
+      if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return;
+    }
+    if (P.diag & 16) return;
+    const uint64_t s0 = uint64_t(start);
+    uint32_t f = P.chunk_file[s0 / kChunk];
+    uint64_t fs = P.off[f], fe = P.off[f + 1];
+    while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
+      f++;
+      fs = fe;
+      fe = P.off[f + 1];
+    }
+    if (s0 < fs || s0 + it.n > fe) return;  // crosses a file boundary
+    if (P.diag & 8) return;
+    if (it.kind == kItemFold) {
+      const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 1u;
+      const uint32_t old = atomicOr(&P.flags[f], fl);
+      if (old == 0) {
+        const uint32_t q = atomicAdd(&P.counters[2], 1u);
+        if (q < P.special_cap) P.special[q] = f;
+      }
+      const uint32_t q = atomicAdd(&P.counters[9], 1u);
+      if (q < P.fold_cap) P.folds[q] = FoldSite{s0, f, it.n};
+      else P.counters[10] = 1;
+      return;
+    }
+    const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
+    for (uint32_t d = 0; d < it.n_ids; d++)
+      stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
+  };
+  auto run_q2 = [&]() {  // wave-uniform: phase C over the queued candidates
+    wave_sync();
+    const uint32_t n2 = __builtin_amdgcn_readfirstlane(cnt[2]);
+    const uint32_t m2 = n2 < kCQ2 ? n2 : kCQ2;
+    for (uint32_t c2 = 0; c2 < m2; c2 += 64) {
+      if (c2 + lane < m2) {
+        const uint32_t e = q2[c2 + lane];
+        check_item(e & 63u, (e >> 6) & 15u, e >> 10);
+      }
+      if (__builtin_amdgcn_readfirstlane(cnt[0]) >= 64) flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
+    }
+    wave_sync();
+    if (lane == 0) cnt[2] = 0;
+    wave_sync();
+  };
+  // phase B for one fire entry (lane l, position k, bucket mask): queue the core-matching items
+  auto do_fire = [&](uint32_t e) {
+    const uint32_t l = e & 63u, k = (e >> 6) & 15u;
+    uint32_t fm = e >> 10;
+    const uint64_t base = wbase[l];
+    uint32_t cb[8];  // the 8 bytes ending at the window end (zero before the arena, as in K1)
 #pragma unroll
-      for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
-      while (fm) {
-        const uint32_t j = __builtin_ctz(fm);
-        fm &= fm - 1;
-        if (P.diag & 4) continue;
-        // the 8 bytes ending at the window end (before the arena: zero bytes, as in K1)
-        uint32_t cb[8];
+    for (int q = 0; q < 8; q++) {
+      const int64_t pos = int64_t(base + k) - 7 + q;
+      cb[q] = pos < 0 ? 0u : win_byte(l, uint64_t(pos));
+    }
+    while (fm) {
+      const uint32_t j = __builtin_ctz(fm);
+      fm &= fm - 1;
+      for (uint32_t g = P.bucket_groups[j]; g < P.bucket_groups[j + 1]; g++) {
+        const uint64_t* ct = P.core + size_t(g) * 256;
+        uint64_t cm = ~uint64_t(0);
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const int64_t pos = int64_t(base + k) - 7 + q;
-          cb[q] = pos < 0 ? 0u : uint32_t(win[uint64_t(pos) - wbase]);
-        }
-        for (uint32_t g = P.bucket_groups[j]; g < P.bucket_groups[j + 1]; g++) {
-          uint64_t cm = ~uint64_t(0);
-          const uint64_t* ct = P.core + size_t(g) * 256;
-#pragma unroll
-          for (int q = 0; q < 8; q++) cm &= ct[cb[q]] >> (8 * q);
-          uint32_t im = uint32_t(cm) & 0xFFu;
-          while (im) {
+        for (int q = 0; q < 8; q++) cm &= ct[cb[q]] >> (8 * q);
+        uint32_t im = uint32_t(cm) & 0xFFu;
+        while (im) {
           const uint32_t gi = __builtin_ctz(im);
           im &= im - 1;
-          const FilterItemGpu it = items[P.group_items[g * 8 + gi]];
-          const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
-          if (start < 0 || uint64_t(start) + it.n > P.n_bytes) continue;
-          bool ok = true;
-          const uint32_t core_lo = it.back > 8 ? it.back - 8u : 0u;  // positions [core_lo, back) are verified
-          for (uint32_t q = 0; q < it.n && ok; q++) {
-            if (q == core_lo) {
-              q = it.back - 1u;
-              continue;
-            }
-            const uint32_t bt = byte_at(uint64_t(start) + q);
-            const uint32_t c = item_cls[it.cls_off + q];
-            ok = (classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u;
-          }
-          if (!ok || (P.diag & 16)) continue;
-          const uint64_t s0 = uint64_t(start);
-          uint32_t f = P.chunk_file[s0 / kChunk];
-          uint64_t fs = P.off[f], fe = P.off[f + 1];
-          while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
-            f++;
-            fs = fe;
-            fe = P.off[f + 1];
-          }
-          if (s0 < fs || s0 + it.n > fe) continue;  // crosses a file boundary
-          if (P.diag & 8) continue;
-          if (it.kind == kItemFold) {
-            const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 1u;
-            const uint32_t old = atomicOr(&P.flags[f], fl);
-            if (old == 0) {
-              const uint32_t q = atomicAdd(&P.counters[2], 1u);
-              if (q < P.special_cap) P.special[q] = f;
-            }
-            const uint32_t q = wave_slot(&P.counters[9]);
-            if (q < P.fold_cap) P.folds[q] = FoldSite{s0, f, it.n};
-            else P.counters[10] = 1;
-            continue;
-          }
-          const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
-          for (uint32_t d = 0; d < it.n_ids; d++)
-            stage_hit(hbuf, hcnt, P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
-          }
+          const uint32_t ix = P.group_items[g * 8 + gi];
+          const uint32_t slot = atomicAdd(&cnt[2], 1u);
+          if (slot < kCQ2) q2[slot] = l | (k << 6) | (ix << 10);
+          else check_item(l, k, ix);  // queue full: check in place
         }
       }
     }
+  };
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x + wave * 64; r0 < n_recs; r0 += stride) {
+    // ---- A: one block per lane
+    const uint32_t r = r0 + lane;
+    if (r < n_recs) {
+      const uint64_t base = uint64_t(P.recs[r]) * 16;
+      const uint64_t w0 = base >= 16 ? base - 16 : 0;
+      const uint4 d0 = load16(P.arena + w0), d1 = load16(P.arena + w0 + 16), d2 = load16(P.arena + w0 + 32),
+                  d3 = load16(P.arena + w0 + 48);
+      uint4* wl = reinterpret_cast<uint4*>(wwin + lane * kCWin);
+      wl[0] = d0;
+      wl[1] = d1;
+      wl[2] = d2;
+      wl[3] = d3;
+      wbase[lane] = base;
+      const uint4 pv = base >= 16 ? d0 : make_uint4(0, 0, 0, 0);
+      const uint4 v = base >= 16 ? d1 : d0;
+      uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
+      auto rd1 = [&](uint32_t w, uint32_t k) {  // single-copy table: entry b at 16 * b
+        return *reinterpret_cast<const uint4*>(s_reach + (((w >> (8 * k)) & 0xFFu) << 4));
+      };
+#pragma unroll
+      for (uint32_t k = 11; k < 16; k++) reach_apply(rd1(word_of(pv, k >> 2), k & 3), st);
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++) {
+        reach_apply(rd1(word_of(v, k >> 2), k & 3), st);
+        uint32_t fm = 0;  // fires at window end base + k: slot 5 = bits 20..23 of each register
+#pragma unroll
+        for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
+        if (fm && !(P.diag & 4)) {
+          const uint32_t e = lane | (k << 6) | (fm << 10);
+          const uint32_t slot = atomicAdd(&cnt[1], 1u);
+          if (slot < kCQ1) q1[slot] = e;
+          else do_fire(e);  // queue full: handle in place
+        }
+      }
+    }
+    wave_sync();
+    // ---- B: one fire per lane
+    const uint32_t n1 = __builtin_amdgcn_readfirstlane(cnt[1]);
+    const uint32_t m1 = n1 < kCQ1 ? n1 : kCQ1;
+    for (uint32_t c1 = 0; c1 < m1; c1 += 64) {
+      if (c1 + lane < m1) do_fire(q1[c1 + lane]);
+      // ---- C: when enough candidates queued (or at the end)
+      const uint32_t n2 = __builtin_amdgcn_readfirstlane(cnt[2]);
+      if (n2 >= 64 || (c1 + 64 >= m1 && n2 > 0)) run_q2();
+    }
+    wave_sync();
+    if (lane == 0) cnt[1] = 0;
+    if (__builtin_amdgcn_readfirstlane(cnt[0]) >= 64) flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
+    wave_sync();
   }
-  flush_staged(hbuf, hcnt, P.hits, P.hit_cap, P.counters, lane);
+  flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
 }
 
 // Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
@@ -1492,7 +1552,8 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     uint8_t* d = nullptr;
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_ftabs_ = d;
-    c_lds_bytes_ = 4096 + size_t(kCThreads) * kCWin + size_t(kCThreads / 64) * kCWaveHits * 12 + 16 + ftabs_bytes_;
+    c_lds_bytes_ = 4096 + size_t(kCThreads) * (kCWin + 8) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
+                   size_t(kCThreads / 64) * kCWaveHits * 12 + size_t(kCThreads / 64) * 16 + ftabs_bytes_;
     if (c_lds_bytes_ > 64 * 1024) {
       err_ = "prefilter tables do not fit in LDS";
       return;
