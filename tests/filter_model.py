@@ -15,7 +15,7 @@ import numpy as np
 from trivy_amd import _lib
 from trivy_amd.secret.scanner import CGlobal
 
-KIND_ANCHOR, KIND_FOLD = 1, 2
+KIND_KEYWORD, KIND_ANCHOR, KIND_FOLD = 0, 1, 2
 WINDOW = 6
 
 
@@ -102,8 +102,9 @@ class FilterModel:
         cls = self.item_cls[it["cls_off"]:it["cls_off"] + it["n"]]
         return bool(self.classes[cls, a[start:start + it["n"]]].all())
 
-    def run(self, arena, offsets):
-        """Returns (set of (file, literal end rel. to file, anchor id), set of (file, fold flag))."""
+    def run(self, arena, offsets, keywords=None):
+        """Returns (set of (file, literal end rel. to file, anchor id), set of (file, fold flag));
+        keyword bits go to the optional set `keywords` as (file, keyword id)."""
         a = np.asarray(arena, dtype=np.uint8)
         offs = np.asarray(offsets, dtype=np.int64)
         hits, folds = set(), set()
@@ -123,7 +124,11 @@ class FilterModel:
                         continue
                     ids = self.item_ids[it["ids_off"]:it["ids_off"] + it["n_ids"]]
                     if it["kind"] == KIND_FOLD:
-                        folds.add((f, 3 if int(ids[0]) == 2 else 1))
+                        folds.add((f, 3 if int(ids[0]) == 2 else 5))
+                        continue
+                    if it["kind"] == KIND_KEYWORD:
+                        if keywords is not None:
+                            keywords.add((f, int(ids[0])))
                         continue
                     for aid in ids:
                         hits.add((f, start - fs + it["lit_end"], int(aid)))

@@ -43,6 +43,17 @@ def _anchors(model):
         j += 1
 
 
+def _rule_kw(model, i):
+    from tests.kernel_model import _RuleInfo
+    L = _lib.lib()
+    L.tsg_debug_rule.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p]
+    ri = _RuleInfo()
+    L.tsg_debug_rule(model.h, i, c.byref(ri))
+    if ri.gate != 1 or not ri.n_kw:
+        return []
+    return list(np.ctypeslib.as_array((c.c_uint32 * ri.n_kw).from_address(ri.kw_ids)))
+
+
 def _pack(contents):
     offs = np.zeros(len(contents) + 1, dtype=np.int64)
     offs[1:] = np.cumsum([len(x) for x in contents])
@@ -117,7 +128,7 @@ def test_fold_runes_flag_files():
     model = FilterModel(rules)
     arena, offs = _pack(contents)
     _, folds = model.run(arena, offs)
-    assert folds == {(1, 1), (2, 1), (3, 3), (6, 3)}
+    assert folds == {(1, 5), (2, 5), (3, 3), (6, 3)}
 
 
 def test_golden_custom_rules_covered():
@@ -146,3 +157,32 @@ def test_newline_bucket_shape():
         assert not m.allowed(nlb, s).any()
     for j in range(nlb):  # item buckets carry fires through slots 6, 7
         assert m.allowed(j, 6).all() and m.allowed(j, 7).all()
+
+
+def test_keyword_bits_exact_ascii():
+    """GPU keyword bits = ASCII case-insensitive keyword presence (files without U+0130/U+212A)."""
+    rules = builtin_rules()
+    m = FilterModel(rules)
+    L = _lib.lib()
+    L.tsg_debug_keyword.restype = c.c_char_p
+    L.tsg_debug_keyword.argtypes = [c.c_void_p, c.c_uint32]
+    kws = []
+    while True:
+        k = L.tsg_debug_keyword(m.h, len(kws))
+        if k is None:
+            break
+        kws.append(k)
+    rng = random.Random(5)
+    contents = _planted_texts(rng, rules, 60)
+    contents += [k.upper() + b" x" for k in kws] + [b"a" + k + b"b" for k in kws] + [kws[0][:-1]]
+    arena, offs = _pack(contents)
+    got = set()
+    m.run(arena, offs, got)
+    want = set()
+    for f, content in enumerate(contents):
+        low = content.lower()
+        for i, k in enumerate(kws):
+            if k in low:
+                want.add((f, i))
+    gated = {int(x) for r in range(len(rules)) for x in _rule_kw(m, r)}
+    assert {(f, i) for f, i in want if i in gated} == got

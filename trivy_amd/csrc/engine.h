@@ -12,6 +12,10 @@ namespace tsg {
 
 constexpr uint32_t kChunk = 1024;  // bytes per lane-chunk in the scan kernel
 
+constexpr uint32_t kCandGateOpen = 1;   // a keyword of the rule occurs in the file (ASCII, GPU bits)
+constexpr uint32_t kCandFoldFile = 2;   // the file holds U+0130 / U+212A (keywords may hide behind them)
+constexpr uint32_t kCandGateValid = 4;  // the two bits above were computed (GPU candidates)
+
 struct Candidate {      // produced by the verify / full-scan kernels
   uint32_t file;
   uint32_t rule;

@@ -929,6 +929,8 @@ struct ConfirmParams {
   FoldSite* folds;     // fold runes found (for the fold kernel)
   uint32_t fold_cap;
   uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission
+  uint32_t* kwbits;               // per file: kw_words x u32 keyword bits
+  uint32_t kw_words;
   const uint64_t* core;           // filter.h core tables (n_groups x 256)
   const uint32_t* group_items;    // n_groups x 8
   const uint32_t* bucket_groups;  // n_buckets + 1
@@ -1106,8 +1108,16 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     }
     if (s0 < fs || s0 + it.n > fe) return;  // crosses a file boundary
     if (P.diag & 8) return;
+    if (it.kind == kItemKeyword) {
+      const uint32_t id = item_ids[it.ids_off];
+      uint32_t* w = &P.kwbits[uint64_t(f) * P.kw_words + (id >> 5)];
+      const uint32_t bit = 1u << (id & 31);
+      if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
+      return;
+    }
     if (it.kind == kItemFold) {
-      const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 1u;
+      // bit0: widen anchor offsets; bit1: U+017F; bit2: U+0130 / U+212A (lower into ASCII)
+      const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 5u;
       const uint32_t old = atomicOr(&P.flags[f], fl);
       if (old == 0) {
         const uint32_t q = atomicAdd(&P.counters[2], 1u);
@@ -1306,6 +1316,22 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
   }
 }
 
+// Candidate flags for the host's lazy MatchKeywords (scanner.go:174-186).
+__device__ uint32_t gate_flags(const NfaParams& P, const RuleGpu& rg, uint32_t f) {
+  uint32_t fl = kCandGateValid | ((P.flags[f] & 4u) ? kCandFoldFile : 0u);
+  if (rg.gate == kGateKeywords) {
+    const uint32_t* kb = P.kwbits + uint64_t(f) * P.kw_words;
+    for (uint32_t i = 0; i < rg.kw_cnt; i++) {
+      const uint32_t id = P.rule_kw[rg.kw_off + i];
+      if (kb[id >> 5] & (1u << (id & 31))) {
+        fl |= kCandGateOpen;
+        break;
+      }
+    }
+  }
+  return fl;
+}
+
 // Verify kernel: one lane per anchor hit.  The start window comes from the
 // literal position and the anchor's offsets (wider in files with fold runes,
 // whose literal bytes may be up to 3x its length); the rule's relaxed NFA runs
@@ -1328,7 +1354,8 @@ __global__ __launch_bounds__(256) void verify_hits_kernel(NfaParams P) {
     const int64_t len = int64_t(P.off[f + 1] - fs);
     const bool acc =
         rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off);
-    if (acc) emit_candidate(P, f, a.rule, wlo, whi, count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(wlo)), 0u);
+    if (acc)
+      emit_candidate(P, f, a.rule, wlo, whi, count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(wlo)), gate_flags(P, rg, f));
   }
 }
 
@@ -1628,6 +1655,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
         !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
       return false;
     HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
+    HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
     HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
     HIP_OK(hipMemsetAsync(d_chunk_file_, 0, n_chunks * 4, stream_));
     {
@@ -1681,6 +1709,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.folds = static_cast<FoldSite*>(d_folds_);
     cp.fold_cap = fold_cap_;
     cp.diag = diag_confirm_;
+    cp.kwbits = static_cast<uint32_t*>(d_kw_);
+    cp.kw_words = kw_words_;
     cp.core = d_core_;
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;

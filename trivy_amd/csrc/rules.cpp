@@ -878,6 +878,26 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
       out->rule_kw.push_back(id);
     }
     rg.kw_cnt = uint32_t(out->rule_kw.size()) - rg.kw_off;
+    if (!redundant && !host_gate && rg.kw_cnt) {  // GPU keyword bits (file-level MatchKeywords for ASCII)
+      for (uint32_t q = rg.kw_off; q < rg.kw_off + rg.kw_cnt; q++) {
+        const uint32_t id = out->rule_kw[q];
+        bool have = false;
+        for (auto& it : out->items)
+          if (it.kind == kItemKeyword && it.id == id) have = true;
+        if (have) continue;
+        FilterItem fi;
+        fi.kind = kItemKeyword;
+        fi.id = id;
+        for (unsigned char ch : out->keywords[id]) {
+          ByteSet b;
+          b.set(ch);
+          if (ch >= 'a' && ch <= 'z') b.set(size_t(ch - 32));
+          fi.sets.push_back(b);
+        }
+        fi.lit_end = uint32_t(fi.sets.size());
+        if (!fi.sets.empty()) out->items.push_back(std::move(fi));
+      }
+    }
     bool empty_kw = false;
     for (auto& kw : r.keywords)
       if (kw.empty()) empty_kw = true;
