@@ -184,5 +184,7 @@ def test_keyword_bits_exact_ascii():
         for i, k in enumerate(kws):
             if k in low:
                 want.add((f, i))
+    with_items = {int(m.item_ids[it["ids_off"]]) for it in m.items if it["kind"] == 0}
     gated = {int(x) for r in range(len(rules)) for x in _rule_kw(m, r)}
-    assert {(f, i) for f, i in want if i in gated} == got
+    assert with_items and with_items <= gated
+    assert {(f, i) for f, i in want if i in with_items} == got

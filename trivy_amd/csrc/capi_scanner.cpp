@@ -187,25 +187,25 @@ int tsg_result_file(const tsg_result* r, uint32_t file, uint32_t* kind, uint32_t
 int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_finding* out) {
   const auto* v = file < r->files.kind.size() ? r->files.Findings(file) : nullptr;
   if (!v || k >= v->size()) return -1;
-  const auto& f = (*v)[k];
+  const auto& f = v->f[k];
   out->rule_index = f.rule;
   out->start_line = f.start_line;
   out->end_line = f.end_line;
-  out->match = f.match.data();
-  out->match_len = f.match.size();
-  out->n_lines = uint32_t(f.lines.size());
+  out->match = v->text.data() + f.match_off;
+  out->match_len = f.match_len;
+  out->n_lines = f.line_hi - f.line_lo;
   return 0;
 }
 
 int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out) {
   const auto* v = file < r->files.kind.size() ? r->files.Findings(file) : nullptr;
   if (!v || k >= v->size()) return -1;
-  const auto& f = (*v)[k];
-  if (line >= f.lines.size()) return -1;
-  const auto& l = f.lines[line];
+  const auto& f = v->f[k];
+  if (line >= f.line_hi - f.line_lo) return -1;
+  const auto& l = v->lines[f.line_lo + line];
   out->number = l.number;
-  out->content = l.content.data();
-  out->content_len = l.content.size();
+  out->content = v->text.data() + l.off;
+  out->content_len = l.len;
   out->is_cause = l.is_cause;
   out->first_cause = l.first_cause;
   out->last_cause = l.last_cause;
@@ -219,14 +219,14 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
     std::string& o = r->json;
     o.reserve(256 + r->stats.findings * 512);
     o.push_back('[');
-    static const std::vector<tsg::FindingOut> kNone;
+    static const tsg::FileFindings kNone;
     for (size_t i = 0; i < r->files.kind.size(); i++) {
       const auto* fv = r->files.Findings(uint32_t(i));
       const auto& findings = fv ? *fv : kNone;
       if (i) o.push_back(',');
       o += "{\"kind\":" + std::to_string(int(r->files.kind[i])) + ",\"findings\":[";
       for (size_t k = 0; k < findings.size(); k++) {
-        const auto& f = findings[k];
+        const auto& f = findings.f[k];
         const auto& R = rules[f.rule];
         if (k) o.push_back(',');
         o += "{\"RuleID\":";
@@ -239,15 +239,16 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
         JsonStr(&o, R.title);
         o += ",\"StartLine\":" + std::to_string(f.start_line) + ",\"EndLine\":" + std::to_string(f.end_line);
         o += ",\"Code\":{\"Lines\":[";
-        for (size_t j = 0; j < f.lines.size(); j++) {
-          const auto& l = f.lines[j];
-          if (j) o.push_back(',');
+        for (uint32_t j = f.line_lo; j < f.line_hi; j++) {
+          const auto& l = findings.lines[j];
+          const std::string content(findings.Str(l.off, l.len));
+          if (j > f.line_lo) o.push_back(',');
           o += "{\"Number\":" + std::to_string(l.number) + ",\"Content\":";
-          JsonStr(&o, l.content);
+          JsonStr(&o, content);
           o += ",\"IsCause\":";
           o += l.is_cause ? "true" : "false";
           o += ",\"Annotation\":\"\",\"Truncated\":false,\"Highlighted\":";
-          JsonStr(&o, l.content);
+          JsonStr(&o, content);
           o += ",\"FirstCause\":";
           o += l.first_cause ? "true" : "false";
           o += ",\"LastCause\":";
@@ -255,7 +256,7 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
           o.push_back('}');
         }
         o += "]},\"Match\":";
-        JsonStr(&o, f.match);
+        JsonStr(&o, std::string(findings.Match(f)));
         o.push_back('}');
       }
       o += "]}";

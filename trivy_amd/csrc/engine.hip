@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
 // Candidate flags for the host's lazy MatchKeywords (scanner.go:174-186).
 __device__ uint32_t gate_flags(const NfaParams& P, const RuleGpu& rg, uint32_t f) {
   uint32_t fl = kCandGateValid | ((P.flags[f] & 4u) ? kCandFoldFile : 0u);
-  if (rg.gate == kGateKeywords) {
+  if (rg.gate == kGateKeywords && !rg.kw_match_implied) {
     const uint32_t* kb = P.kwbits + uint64_t(f) * P.kw_words;
     for (uint32_t i = 0; i < rg.kw_cnt; i++) {
       const uint32_t id = P.rule_kw[rg.kw_off + i];

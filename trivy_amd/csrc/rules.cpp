@@ -767,44 +767,63 @@ std::vector<ByteSet> BeforeSets(const std::vector<Node>& nodes, const std::vecto
 
 }  // namespace
 
-bool KeywordImplied(const Regex& re, const std::string& kw) {
-  if (kw.empty()) return true;
+// Every match contains one of `kws` (lowercased ASCII), case-folded: found in
+// a required literal run, or in every branch of a required alternation (or
+// small class) together with the literal runs around it.  With long_s_ok a
+// (?i) 's' may be matched by U+017F (files holding it are checked exactly);
+// otherwise such positions do not count (bytes.ToLower keeps U+017F).
+bool KeywordsImplied(const Regex& re, const std::vector<std::string>& kws, bool long_s_ok) {
+  for (auto& kw : kws)
+    if (kw.empty()) return true;
   Analyzer an(re.nodes(), false);
   const auto& nodes = re.nodes();
-  // a run of literal chars with, per char, whether U+017F is in its class
-  auto contains = [&](const std::vector<int>& run) {
-    std::string s;
-    std::vector<bool> hz;
-    for (int it : run) {
-      s.push_back(char(LitChar(nodes[it])));
-      hz.push_back(ClassHas(nodes[it].ranges, 0x17F));
-    }
-    for (size_t o = 0; o + kw.size() <= s.size(); o++) {
-      bool ok = true;
-      for (size_t i = 0; i < kw.size() && ok; i++)
-        if (s[o + i] != kw[i] || (kw[i] == 's' && hz[o + i])) ok = false;
-      if (ok) return true;
-    }
+  struct Ch {
+    char c;
+    bool hz;  // U+017F in the class
+  };
+  auto ch_of = [&](int it) { return Ch{char(LitChar(nodes[it])), ClassHas(nodes[it].ranges, 0x17F)}; };
+  auto contains = [&](const std::vector<Ch>& s) {
+    for (auto& kw : kws)
+      for (size_t o = 0; o + kw.size() <= s.size(); o++) {
+        bool ok = true;
+        for (size_t i = 0; i < kw.size() && ok; i++)
+          if (s[o + i].c != kw[i] || (kw[i] == 's' && s[o + i].hz && !long_s_ok)) ok = false;
+        if (ok) return true;
+      }
     return false;
   };
-  auto lead_run = [&](int node) {
-    std::vector<int> items, run;
+  // branch alternatives as char sequences: the lead literal run, and whether it is the whole branch
+  auto lead = [&](int node, bool* whole) {
+    std::vector<int> items;
     an.Flatten(node, &items);
-    for (int it : items) {
-      if (LitChar(nodes[it]) < 0) break;
-      run.push_back(it);
-    }
+    std::vector<Ch> run;
+    size_t i = 0;
+    for (; i < items.size() && LitChar(nodes[items[i]]) >= 0; i++) run.push_back(ch_of(items[i]));
+    *whole = i == items.size();
     return run;
   };
   std::vector<int> items;
   an.Flatten(re.root(), &items);
-  for (size_t k = 0; k < items.size();) {
+  auto lit_run = [&](size_t from, size_t to) {  // literal chars items[from, to)
+    std::vector<Ch> r;
+    for (size_t q = from; q < to; q++) r.push_back(ch_of(items[q]));
+    return r;
+  };
+  for (size_t k = 0; k < items.size(); k++) {
     if (LitChar(nodes[items[k]]) >= 0) {
-      std::vector<int> run;
-      while (k < items.size() && LitChar(nodes[items[k]]) >= 0) run.push_back(items[k++]);
-      if (contains(run)) return true;
+      size_t e = k;
+      while (e < items.size() && LitChar(nodes[items[e]]) >= 0) e++;
+      if (contains(lit_run(k, e))) return true;
+      k = e - 1;
       continue;
     }
+    // the literal runs right before and after items[k]
+    size_t pb = k;
+    while (pb > 0 && LitChar(nodes[items[pb - 1]]) >= 0) pb--;
+    size_t ne = k + 1;
+    while (ne < items.size() && LitChar(nodes[items[ne]]) >= 0) ne++;
+    const std::vector<Ch> before = lit_run(pb, k), after = lit_run(k + 1, ne);
+    std::vector<std::vector<Ch>> alts;  // per alternative: its chars; `after` appended when whole
     const Node& n = nodes[items[k]];
     int alt = -1;
     if (n.op == NodeOp::Alt) alt = items[k];
@@ -812,21 +831,59 @@ bool KeywordImplied(const Regex& re, const std::string& kw) {
       int sub = n.subs[0];
       while (nodes[sub].op == NodeOp::Capture) sub = nodes[sub].subs[0];
       if (nodes[sub].op == NodeOp::Alt) alt = sub;
-      else if (contains(lead_run(sub))) return true;
+      else {
+        bool whole;
+        std::vector<Ch> r = lead(sub, &whole);
+        if (contains(r)) return true;
+      }
     }
     if (alt >= 0) {
+      for (int b : nodes[alt].subs) {
+        bool whole;
+        std::vector<Ch> r = before;
+        std::vector<Ch> l = lead(b, &whole);
+        r.insert(r.end(), l.begin(), l.end());
+        if (whole && n.op == NodeOp::Alt) r.insert(r.end(), after.begin(), after.end());
+        alts.push_back(r);
+      }
+    } else if (n.op == NodeOp::Class) {  // a small class: one alternative per case-folded char
+      std::vector<char> cs;
+      uint64_t total = 0;
+      for (auto& p : n.ranges) {
+        total += uint64_t(p.second - p.first) + 1;
+        if (total > 16) break;
+        for (uint32_t c = p.first; c <= p.second && c < 0x80; c++) {
+          char lc = char((c >= 'A' && c <= 'Z') ? c + 32 : c);
+          if (std::find(cs.begin(), cs.end(), lc) == cs.end()) cs.push_back(lc);
+        }
+      }
+      if (total <= 16 && !cs.empty()) {
+        bool nonascii = false;
+        for (auto& p : n.ranges)
+          if (p.second >= 0x80) nonascii = true;
+        if (!nonascii)
+          for (char c : cs) {
+            std::vector<Ch> r = before;
+            r.push_back(Ch{c, false});
+            r.insert(r.end(), after.begin(), after.end());
+            alts.push_back(r);
+          }
+      }
+    }
+    if (!alts.empty()) {
       bool all = true;
-      for (int b : nodes[alt].subs)
-        if (!contains(lead_run(b))) {
+      for (auto& r : alts)
+        if (!contains(r)) {
           all = false;
           break;
         }
       if (all) return true;
     }
-    k++;
   }
   return false;
 }
+
+bool KeywordImplied(const Regex& re, const std::string& kw) { return KeywordsImplied(re, {kw}, false); }
 
 std::vector<std::string> RequiredLiterals(const Regex& re) {
   Cand best{{}, 0, 0};
@@ -853,9 +910,18 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     rg.kw_off = uint32_t(out->rule_kw.size());
     bool host_gate = false;
     bool redundant = false;
+    bool ascii_implied = false;  // in files without U+017F every match holds a keyword
     if (re) {
-      for (auto& kw : r.keywords)
-        if (IsAscii(kw) && KeywordImplied(*re, AsciiLower(kw))) redundant = true;
+      std::vector<std::string> lows;
+      bool all_ascii = true;
+      for (auto& kw : r.keywords) {
+        if (!IsAscii(kw)) all_ascii = false;
+        lows.push_back(AsciiLower(kw));
+      }
+      if (all_ascii && !lows.empty()) {
+        redundant = KeywordsImplied(*re, lows, false);
+        ascii_implied = redundant || KeywordsImplied(*re, lows, true);
+      }
     }
     if (redundant) out->n_redundant_gates++;
     for (auto& kw : r.keywords) {
@@ -878,7 +944,8 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
       out->rule_kw.push_back(id);
     }
     rg.kw_cnt = uint32_t(out->rule_kw.size()) - rg.kw_off;
-    if (!redundant && !host_gate && rg.kw_cnt) {  // GPU keyword bits (file-level MatchKeywords for ASCII)
+    rg.kw_match_implied = ascii_implied ? 1 : 0;
+    if (!redundant && !host_gate && !ascii_implied && rg.kw_cnt) {  // GPU keyword bits (file-level, ASCII)
       for (uint32_t q = rg.kw_off; q < rg.kw_off + rg.kw_cnt; q++) {
         const uint32_t id = out->rule_kw[q];
         bool have = false;

@@ -41,6 +41,7 @@ enum GateMode : uint8_t {
 // and not through a (?i) 's' that U+017F could satisfy) makes MatchKeywords
 // unable to change Scan's result -- see DESIGN.md §2.1.
 bool KeywordImplied(const Regex& re, const std::string& kw_lower);
+bool KeywordsImplied(const Regex& re, const std::vector<std::string>& kws_lower, bool long_s_ok);
 
 struct RuleSrc {
   std::string id;
@@ -65,6 +66,7 @@ struct RuleGpu {  // mirrored on the device
   uint8_t anchored;     // 1: anchor-driven; 0: full-scan rule
   uint8_t has_regex;
   uint32_t kw_off, kw_cnt;  // into rule_kw
+  uint32_t kw_match_implied;  // every match holds a keyword unless the file has U+017F (no GPU bits)
 };
 
 // Prefilter item: a fixed-width sequence of byte sets that

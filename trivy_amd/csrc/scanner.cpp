@@ -70,17 +70,17 @@ struct Loc {
 // Go sort.Slice = pdqsort_func (sort/zsortfunc.go), restated.
 // ---------------------------------------------------------------------------
 struct SortData {
-  std::vector<FindingOut>* v;
+  FileFindings* v;
   const std::vector<RuleSpec>* rules;
   bool Less(int i, int j) const {
-    const FindingOut& a = (*v)[i];
-    const FindingOut& b = (*v)[j];
+    const FindingOut& a = v->f[size_t(i)];
+    const FindingOut& b = v->f[size_t(j)];
     const std::string& ra = (*rules)[a.rule].id;
     const std::string& rb = (*rules)[b.rule].id;
     if (ra != rb) return ra < rb;
-    return a.match < b.match;
+    return v->Match(a) < v->Match(b);
   }
-  void Swap(int i, int j) { std::swap((*v)[i], (*v)[j]); }
+  void Swap(int i, int j) { std::swap(v->f[size_t(i)], v->f[size_t(j)]); }
 };
 
 void InsertionSort(SortData& d, int a, int b) {
@@ -279,7 +279,7 @@ void Pdqsort(SortData& d, int a, int b, int limit) {
 
 }  // namespace
 
-void SortFindings(std::vector<FindingOut>* f, const std::vector<RuleSpec>& rules) {
+void SortFindings(FileFindings* f, const std::vector<RuleSpec>& rules) {
   SortData d{f, &rules};
   int n = int(f->size());
   Pdqsort(d, 0, n, BitsLen(unsigned(n)));
@@ -535,7 +535,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       }
       // GPU keyword bits (ASCII occurrences anywhere in the file) and the
       // file's U+0130/U+212A flag, when the candidates carry them
-      const bool gpu_bits = (group_flags & kCandGateValid) && cr_.rules[r].gate == kGateKeywords;
+      const bool gpu_bits = (group_flags & kCandGateValid) && cr_.rules[r].gate == kGateKeywords &&
+                            !cr_.rules[r].kw_match_implied;
       if (!hit && gpu_bits) {
         hit = (group_flags & kCandGateOpen) != 0;
         fold_done = true;
@@ -696,6 +697,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
 
   out->kind = kHasFindings;
   PhaseTimer pt3(3);
+  FileFindings& ff = out->findings;
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
@@ -708,36 +710,49 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       mls = (start - ls - 30 < 0) ? ls : start - 30;
       mle = (end + 20 > le) ? le : end + 20;
     }
-    std::string match_line = censored(mls, mle);
+    const std::string match_line = censored(mls, mle);
     int64_t end_line_num = start_line_num + count_nl(start, end);
     int64_t code_start = std::max<int64_t>(start_line_num - 2, 0);
     int64_t p = ls;
     for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
     bool found_first = false;
-    for (int64_t k = code_start; k < end_line_num + 2; k++) {
-      int64_t e = line_end_of(p);
-      bool in_cause = k >= start_line_num && k <= end_line_num;
-      std::string s;
-      if (e - p > 100) s = in_cause ? match_line : censored(p, p + 100);
-      else s = censored(p, e);
-      f.lines.push_back({k + 1, std::move(s), in_cause, !found_first && in_cause, false});
-      found_first = found_first || in_cause;
-      if (e >= len) break;  // last line of bytes.Split
-      p = e + 1;
+    f.line_lo = uint32_t(ff.lines.size());
+    if (!binary) {
+      for (int64_t k = code_start; k < end_line_num + 2; k++) {
+        int64_t e = line_end_of(p);
+        bool in_cause = k >= start_line_num && k <= end_line_num;
+        uint32_t off, n;
+        if (e - p > 100 && in_cause) {
+          n = uint32_t(match_line.size());
+          off = ff.Put(match_line);
+        } else {
+          const std::string s = censored(p, e - p > 100 ? p + 100 : e);
+          n = uint32_t(s.size());
+          off = ff.Put(s);
+        }
+        ff.lines.push_back({k + 1, off, n, in_cause, !found_first && in_cause, false});
+        found_first = found_first || in_cause;
+        if (e >= len) break;  // last line of bytes.Split
+        p = e + 1;
+      }
     }
-    for (auto it = f.lines.rbegin(); it != f.lines.rend(); ++it)
-      if (it->is_cause) {
-        it->last_cause = true;
+    f.line_hi = uint32_t(ff.lines.size());
+    for (uint32_t li = f.line_hi; li > f.line_lo; li--)
+      if (ff.lines[li - 1].is_cause) {
+        ff.lines[li - 1].last_cause = true;
         break;
       }
     f.start_line = start_line_num + 1;
     f.end_line = end_line_num + 1;
-    f.match = std::move(match_line);
     if (binary) {
-      f.match = "Binary file " + GoQuote(path) + " matches a rule " + GoQuote(rules_[f.rule].title);
-      f.lines.clear();
+      const std::string m = "Binary file " + GoQuote(path) + " matches a rule " + GoQuote(rules_[f.rule].title);
+      f.match_off = ff.Put(m);
+      f.match_len = uint32_t(m.size());
+    } else {
+      f.match_off = ff.Put(match_line);
+      f.match_len = uint32_t(match_line.size());
     }
-    out->findings.push_back(std::move(f));
+    ff.f.push_back(f);
   }
   PhaseTimer pt4(4);
   SortFindings(&out->findings, rules_);

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "engine.h"
@@ -43,32 +44,48 @@ struct RuleSpec {
   std::vector<std::string> kw_lower_host;  // for host-verified gates
 };
 
+// Findings of one file, flat: records plus one text pool for every match and
+// code line (three allocations per file, whatever the finding count).
 struct LineOut {
   int64_t number;
-  std::string content;
+  uint32_t off, len;  // content in FileFindings::text
   bool is_cause, first_cause, last_cause;
 };
 
 struct FindingOut {
   uint32_t rule;
   int64_t start_line, end_line;
-  std::string match;
+  uint32_t match_off, match_len;  // in FileFindings::text
+  uint32_t line_lo, line_hi;      // into FileFindings::lines
+};
+
+struct FileFindings {
+  std::vector<FindingOut> f;
   std::vector<LineOut> lines;
+  std::string text;
+  size_t size() const { return f.size(); }
+  std::string_view Str(uint32_t off, uint32_t len) const { return std::string_view(text).substr(off, len); }
+  std::string_view Match(const FindingOut& x) const { return Str(x.match_off, x.match_len); }
+  uint32_t Put(std::string_view s) {
+    const uint32_t at = uint32_t(text.size());
+    text.append(s.data(), s.size());
+    return at;
+  }
 };
 
 enum FileKind : uint32_t { kNoFindings = 0, kAllowedPath = 1, kHasFindings = 2 };
 
 struct FileResult {
   FileKind kind = kNoFindings;
-  std::vector<FindingOut> findings;
+  FileFindings findings;
 };
 
 // Per-batch result, sparse: a kind byte per file, findings only where present.
 struct BatchResult {
   std::vector<uint8_t> kind;              // FileKind per file
   std::vector<uint32_t> found_files;      // ascending
-  std::vector<std::vector<FindingOut>> found;
-  const std::vector<FindingOut>* Findings(uint32_t f) const {
+  std::vector<FileFindings> found;
+  const FileFindings* Findings(uint32_t f) const {
     auto it = std::lower_bound(found_files.begin(), found_files.end(), f);
     if (it == found_files.end() || *it != f) return nullptr;
     return &found[size_t(it - found_files.begin())];
@@ -134,6 +151,6 @@ class SecretScanner {
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.
-void SortFindings(std::vector<FindingOut>* f, const std::vector<RuleSpec>& rules);
+void SortFindings(FileFindings* f, const std::vector<RuleSpec>& rules);
 
 }  // namespace tsg
