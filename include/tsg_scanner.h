@@ -15,8 +15,9 @@
  *                                                                 misconf.go:48-61
  * Conventions: all pointers are borrowed for the duration of the call;
  * results are owned by the library until tsg_result_free.  Status: 0 = OK,
- * <0 = error, text via tsg_last_error() (tsg_debug.h).  Thread-safety: one
- * tsg_scan at a time per scanner (the engine owns one HIP stream).
+ * <0 = error, text via tsg_last_error() (tsg_debug.h).  Thread-safety: scans on
+ * one scanner may overlap (tsg_scan_submit); their GPU phases are serialized
+ * on the scanner's HIP stream, the exact host passes run concurrently.
  */
 #ifndef TSG_SCANNER_H
 #define TSG_SCANNER_H
@@ -69,7 +70,8 @@ typedef struct tsg_batch {
   uint32_t n_files;
   const uint8_t* host_arena;     /* concatenated contents, required (exact pass) */
   const uint64_t* host_offsets;  /* n_files + 1 */
-  const void* dev_arena;         /* optional: same bytes already in HBM (16-B aligned, +16 B pad) */
+  const void* dev_arena;         /* optional: same bytes already in HBM (16-B aligned, 64 readable
+                                    bytes past the end) */
   const void* dev_offsets;       /* optional: device copy of host_offsets */
   const char* const* paths;      /* ScanArgs.FilePath per file */
   const uint64_t* path_lens;     /* optional */
@@ -77,6 +79,13 @@ typedef struct tsg_batch {
 } tsg_batch;
 
 int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);
+/* Pipelined scanning: tsg_scan on a background thread.  The GPU phases of
+ * the scans in flight on one scanner run one after another (one HIP stream);
+ * a batch's exact host pass overlaps the next batch's kernels.  The batch's
+ * buffers stay borrowed until tsg_scan_wait returns. */
+typedef struct tsg_pending tsg_pending;
+int tsg_scan_submit(tsg_scanner* s, const tsg_batch* batch, tsg_pending** out);
+int tsg_scan_wait(tsg_pending* p, tsg_result** out); /* frees p */
 void tsg_result_free(tsg_result* r);
 
 /* kind: 0 = types.Secret{} (no findings), 1 = Secret{FilePath} (allowed path), 2 = findings */

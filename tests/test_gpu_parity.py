@@ -116,3 +116,21 @@ def test_fold_rune_files_multichunk(secret):
             parts.insert(rng.randint(0, len(parts)), rng.choice(secrets))
         files.append(("f%d.txt" % i, b"\n".join(parts)))
     _compare_corpus(secret, files)
+
+
+def test_pipelined_scans_match_sync(secret):
+    """tsg_scan_submit / tsg_scan_wait: overlapping scans give the synchronous results."""
+    import numpy as np
+    s = secret.NewScanner(None)
+    batches = []
+    for seed in (31, 32, 33):
+        files = [(p, _strip_cr(b)) for p, b in make_corpus(seed, 120)]
+        contents = [b for _, b in files]
+        offs = np.zeros(len(files) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(x) for x in contents])
+        arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+        batches.append((arena, offs, [p for p, _ in files]))
+    want = [s.scan_arena(a, o, p).raw() for a, o, p in batches]
+    pend = [s.scan_arena_async(a, o, p) for a, o, p in batches]
+    got = [pd.wait().raw() for pd in pend]
+    assert got == want

@@ -1,6 +1,10 @@
 // C ABI of the drop-in scanner (include/tsg_scanner.h) and of the rule
 // compiler inspection hooks (include/tsg_debug.h).
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <memory>
 #include <string>
 
@@ -28,6 +32,57 @@ struct tsg_result {
 struct tsg_compiled {
   tsg::CompiledRules cr;
 };
+
+namespace {
+// Results are destroyed on a background thread: a batch's findings are
+// thousands of small heap blocks written by the tail's worker threads, and
+// freeing them would otherwise sit on the caller's critical path.
+class ResultReaper {
+ public:
+  static ResultReaper& Get() {
+    static ResultReaper r;
+    return r;
+  }
+  void Push(tsg_result* r) {
+    if (!r) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(r);
+    }
+    cv_.notify_one();
+  }
+  ~ResultReaper() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_one();
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  ResultReaper() : th_([this] { Run(); }) {}
+  void Run() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      while (!q_.empty()) {
+        tsg_result* r = q_.front();
+        q_.pop_front();
+        lk.unlock();
+        delete r;
+        lk.lock();
+      }
+      if (stop_) return;
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<tsg_result*> q_;
+  bool stop_ = false;
+  std::thread th_;
+};
+}  // namespace
 
 namespace {
 std::string Str(const char* s) { return s ? std::string(s) : std::string(); }
@@ -134,6 +189,35 @@ int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len)
   return s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len)) ? 1 : 0;
 }
 
+struct tsg_pending {
+  std::thread th;
+  tsg_result* r = nullptr;
+  int rc = 0;
+  std::string err;
+};
+
+int tsg_scan_submit(tsg_scanner* s, const tsg_batch* b, tsg_pending** out) {
+  std::unique_ptr<tsg_pending> p(new tsg_pending());
+  const tsg_batch bc = *b;
+  tsg_pending* pp = p.get();
+  pp->th = std::thread([s, bc, pp] {
+    pp->rc = tsg_scan(s, &bc, &pp->r);
+    if (pp->rc != 0) pp->err = tsg_last_error();
+  });
+  *out = p.release();
+  return 0;
+}
+
+int tsg_scan_wait(tsg_pending* p, tsg_result** out) {
+  if (!p) return -1;
+  p->th.join();
+  const int rc = p->rc;
+  *out = p->r;
+  if (rc != 0) tsg::SetError(p->err);
+  delete p;
+  return rc;
+}
+
 int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   tsg::BatchInput in;
   in.n_files = b->n_files;
@@ -174,7 +258,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   return 0;
 }
 
-void tsg_result_free(tsg_result* r) { delete r; }
+void tsg_result_free(tsg_result* r) { ResultReaper::Get().Push(r); }
 
 int tsg_result_file(const tsg_result* r, uint32_t file, uint32_t* kind, uint32_t* n) {
   if (file >= r->files.kind.size()) return -1;

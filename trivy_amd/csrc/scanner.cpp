@@ -777,13 +777,18 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     ms_allow = NowMs() - a0;
   });
   bool ok;
-  if (in.dev_arena)
-    ok = engine_->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
-  else
-    ok = engine_->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
+  std::string gpu_err;
+  {
+    std::lock_guard<std::mutex> g(gpu_mu_);
+    if (in.dev_arena)
+      ok = engine_->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
+    else
+      ok = engine_->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
+    if (!ok) gpu_err = engine_->error();
+  }
   allow_thread.join();
   if (!ok) {
-    err_ = engine_->error();
+    err_ = gpu_err;
     return false;
   }
   double t1 = NowMs();
@@ -846,7 +851,18 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   size_t nf = starts.size() - 1;
   std::vector<FileResult> tmp(nf);
   for (auto& g : g_prof) g = 0;
-  ParallelFor(nf, host_threads_, [&](size_t k) {
+  // largest work first (candidates x file size) so one big file does not finish last
+  std::vector<uint32_t> order(nf);
+  for (size_t k = 0; k < nf; k++) order[k] = uint32_t(k);
+  auto work_of = [&](size_t k) {
+    const uint32_t f = cands[starts[k]].file;
+    return double(starts[k + 1] - starts[k]) * double(in.host_offsets[f + 1] - in.host_offsets[f] + 4096);
+  };
+  std::vector<double> w(nf);
+  for (size_t k = 0; k < nf; k++) w[k] = work_of(k);
+  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return w[x] > w[y]; });
+  ParallelFor(nf, host_threads_, [&](size_t kk) {
+    const size_t k = order[kk];
     size_t a = starts[k], b = starts[k + 1];
     uint32_t f = cands[a].file;
     if (allowed[f]) return;

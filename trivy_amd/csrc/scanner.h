@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -144,6 +145,7 @@ class SecretScanner {
   std::vector<std::unique_ptr<Regex>> exclude_;
   CompiledRules cr_;
   std::unique_ptr<GpuEngine> engine_;
+  std::mutex gpu_mu_;  // one GPU phase at a time (one HIP stream, per-batch device buffers)
   std::string err_;
   int host_threads_ = 0;
   bool compiled_ok_ = false;

@@ -65,6 +65,8 @@ def _declare(L):
     L.tsg_scanner_free.argtypes = [c.c_void_p]
     L.tsg_scanner_allow_path.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64]
     L.tsg_scan.argtypes = [c.c_void_p, c.POINTER(_CBatch), c.POINTER(c.c_void_p)]
+    L.tsg_scan_submit.argtypes = [c.c_void_p, c.POINTER(_CBatch), c.POINTER(c.c_void_p)]
+    L.tsg_scan_wait.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L.tsg_result_free.argtypes = [c.c_void_p]
     L.tsg_result_json.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_uint64)]
     L.tsg_result_stats.argtypes = [c.c_void_p, c.POINTER(_CStats)]
@@ -225,6 +227,36 @@ class Scanner:
         return res.secrets([a.FilePath for a in args])
 
     # --- batched arena API (analyzer / bench) -------------------------------
+    def scan_arena_async(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None):
+        """Pipelined scan (tsg_scan_submit): returns a PendingScan; .wait() gives the ScanResult.
+        The arrays passed must stay alive until then (the PendingScan keeps references)."""
+        keep, batch = self._batch(arena, offsets, paths, binary, dev_arena, dev_offsets)
+        h = c.c_void_p()
+        rc = self._L.tsg_scan_submit(self._h, c.byref(batch), c.byref(h))
+        if rc != 0:
+            raise RuntimeError("tsg_scan_submit failed: %s" % _lib.last_error())
+        return PendingScan(self, h, (keep, batch))
+
+    def _batch(self, arena, offsets, paths, binary, dev_arena, dev_offsets):
+        n = len(offsets) - 1
+        arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        plen = None
+        if isinstance(paths, np.ndarray) and paths.dtype == np.uint64:
+            parr, plen_ptr = paths, None  # char* table (caller keeps the strings alive)
+            paths_addr = paths.ctypes.data
+        else:
+            pb = [_b(p) for p in paths]
+            parr = (c.c_char_p * max(1, n))(*pb)
+            plen = np.array([len(p) for p in pb], dtype=np.uint64) if n else np.zeros(1, np.uint64)
+            paths_addr = c.cast(parr, c.c_void_p).value
+            plen_ptr = plen.ctypes.data
+        bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
+        batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
+                        dev_arena, dev_offsets, paths_addr, plen_ptr,
+                        bin_arr.ctypes.data if bin_arr is not None else None)
+        return (arena_buf, offs, parr, plen, bin_arr), batch
+
     def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None):
         n = len(offsets) - 1
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
@@ -255,6 +287,22 @@ class Scanner:
 
     def rule_anchor(self, i):
         return self._L.tsg_scanner_rule_anchor(self._h, i).decode()
+
+
+class PendingScan:
+    def __init__(self, scanner, h, keep):
+        self._sc = scanner
+        self._h = h
+        self._keep = keep
+
+    def wait(self):
+        r = c.c_void_p()
+        rc = self._sc._L.tsg_scan_wait(self._h, c.byref(r))
+        self._h = None
+        self._keep = None
+        if rc != 0:
+            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
+        return ScanResult(self._sc, r)
 
 
 class ScanResult:
