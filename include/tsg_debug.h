@@ -43,8 +43,6 @@ typedef struct tsg_debug_rule_info {
 int tsg_debug_compile(const struct tsg_global* g, tsg_compiled** out);
 void tsg_debug_compiled_free(tsg_compiled* c);
 int tsg_debug_compiled_info(const tsg_compiled* c, struct tsg_table_info* out);
-int tsg_debug_ac(const tsg_compiled* c, const uint8_t** cmap, const uint16_t** trans,
-                 const uint32_t** out_off, const uint32_t** out_items, uint32_t* n_out_items);
 int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out);
 int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t* lit_len,
                      int32_t* off_lo, int32_t* off_hi);

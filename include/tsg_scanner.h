@@ -123,9 +123,10 @@ int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 
 /* Compiled-table facts (for reports/tests). */
 typedef struct tsg_table_info {
-  uint32_t n_rules, n_keywords, n_anchors, ac_states, ac_classes, max_pattern_len;
+  uint32_t n_rules, n_keywords, n_anchors, n_filter_items, n_filter_buckets, filter_window;
   uint32_t n_fullscan_rules, nfa_words_total;
-  uint64_t ac_table_bytes;
+  uint64_t filter_table_bytes;  /* reach + item + class + core tables */
+  double filter_est_fp;         /* estimated bucket fires per input byte (static byte prior) */
 } tsg_table_info;
 int tsg_scanner_table_info(const tsg_scanner* s, tsg_table_info* out);
 /* Anchor description of rule i ("[lo,hi] lit lit..." or "-"). */

@@ -19,6 +19,11 @@ KIND_KEYWORD, KIND_ANCHOR, KIND_FOLD = 0, 1, 2
 WINDOW = 6
 
 
+class RuleInfo(c.Structure):  # tsg_debug_rule_info (include/tsg_debug.h)
+    _fields_ = [("nfa_words", c.c_uint32), ("gate", c.c_uint32), ("anchored", c.c_uint32),
+                ("has_regex", c.c_uint32), ("nfa", c.c_void_p), ("kw_ids", c.c_void_p), ("n_kw", c.c_uint32)]
+
+
 class FilterModel:
     def __init__(self, rules):
         L = _lib.lib()

@@ -18,7 +18,7 @@ import pytest
 import yaml
 
 from tests.corpus import make_corpus
-from tests.filter_model import FilterModel
+from tests.filter_model import FilterModel, RuleInfo
 from tests.regex_sampler import sample_regex
 from trivy_amd import _lib
 from trivy_amd.secret import ParseConfig, builtin_rules
@@ -44,10 +44,9 @@ def _anchors(model):
 
 
 def _rule_kw(model, i):
-    from tests.kernel_model import _RuleInfo
     L = _lib.lib()
     L.tsg_debug_rule.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p]
-    ri = _RuleInfo()
+    ri = RuleInfo()
     L.tsg_debug_rule(model.h, i, c.byref(ri))
     if ri.gate != 1 or not ri.n_kw:
         return []

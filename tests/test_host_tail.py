@@ -4,7 +4,7 @@ Drives the C++ tail through the test hook ``tsg_debug_host_tail`` (whole-file
 candidate windows, keyword gate from Go's bytes.ToLower) so that allow rules,
 exclude blocks, group extraction, censoring, findLocation and the pdqsort
 order are checked without a GPU.  The GPU candidate stage is covered by
-tests/test_gpu_parity.py and tests/test_kernel_model.py.
+tests/test_gpu_parity.py and tests/test_filter_model.py.
 """
 import ctypes as c
 import json

@@ -361,14 +361,20 @@ static void FillInfo(const tsg::CompiledRules& cr, tsg_table_info* out) {
   out->n_rules = uint32_t(cr.rules.size());
   out->n_keywords = uint32_t(cr.keywords.size());
   out->n_anchors = uint32_t(cr.anchors.size());
-  out->ac_states = cr.n_states;
-  out->ac_classes = cr.n_classes;
-  out->max_pattern_len = cr.max_pat_len;
+  const tsg::FilterTables* ft = cr.filter.get();
+  out->n_filter_items = ft ? uint32_t(ft->items.size()) : 0;
+  out->n_filter_buckets = ft ? ft->n_buckets : 0;
+  out->filter_window = ft ? ft->window : 0;
+  out->filter_table_bytes =
+      ft ? ft->reach.size() * 4 + ft->bucket_off.size() * 4 + ft->bucket_items.size() * 4 +
+               ft->items.size() * sizeof(tsg::FilterItemGpu) + ft->item_ids.size() * 4 + ft->item_cls.size() +
+               ft->classes.size() * 4 + ft->core.size() * 8 + ft->group_items.size() * 4 + ft->bucket_groups.size() * 4
+         : 0;
+  out->filter_est_fp = ft ? ft->est_fp : 0;
   out->n_fullscan_rules = cr.n_fullscan_rules;
   uint32_t w = 0;
   for (auto& r : cr.rules) w += r.nfa_words;
   out->nfa_words_total = w;
-  out->ac_table_bytes = uint64_t(cr.n_states) * cr.n_classes * 2;
 }
 
 int tsg_scanner_table_info(const tsg_scanner* s, tsg_table_info* out) {
@@ -408,15 +414,6 @@ int tsg_debug_compiled_info(const tsg_compiled* c, tsg_table_info* out) {
   return 0;
 }
 
-int tsg_debug_ac(const tsg_compiled* c, const uint8_t** cmap, const uint16_t** trans, const uint32_t** out_off,
-                 const uint32_t** out_items, uint32_t* n_out_items) {
-  *cmap = c->cr.cmap;
-  *trans = c->cr.trans.data();
-  *out_off = c->cr.out_off.data();
-  *out_items = c->cr.out_items.data();
-  *n_out_items = uint32_t(c->cr.out_items.size());
-  return 0;
-}
 
 int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out) {
   if (i >= c->cr.rules.size()) return -1;

@@ -10,7 +10,7 @@
 
 namespace tsg {
 
-constexpr uint32_t kChunk = 1024;  // bytes per lane-chunk in the scan kernel
+constexpr uint32_t kChunk = 1024;  // bytes per chunk of the per-chunk '\n' counts and chunk -> file map
 
 constexpr uint32_t kCandGateOpen = 1;   // a keyword of the rule occurs in the file (ASCII, GPU bits)
 constexpr uint32_t kCandFoldFile = 2;   // the file holds U+0130 / U+212A (keywords may hide behind them)
@@ -42,7 +42,8 @@ class GpuEngine {
   hipStream_t stream() const { return stream_; }
 
   // Run the kernels over a device-resident arena.  Offsets: n_files+1 u64
-  // (device).  Results are copied back into `cands` / `special`.
+  // (device); the arena must have 64 readable bytes past n_bytes.  The
+  // candidates are copied back into `cands`.
   bool Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
            std::vector<Candidate>* cands, BatchStats* st);
 
@@ -62,27 +63,14 @@ class GpuEngine {
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[5] = {};
   // tables
-  uint8_t* d_cmap_ = nullptr;
-  void* d_trans_ = nullptr;
-  bool wide_table_ = false;
-  uint32_t thr_ = 0, fold_entry_ = 0, cls_i_ = 0, cls_k_ = 0, cls_s_ = 0, div_magic_ = 0;
-  void* d_tabs_ = nullptr;
   uint32_t diag_mode_ = 0, diag_confirm_ = 0;
-  uint32_t tabs_bytes_ = 0, tab_out_off_ = 0, tab_out_items_ = 0, tab_anchors_ = 0, tab_la_ = 0;
-  uint32_t* d_out_off_ = nullptr;
-  uint32_t* d_out_items_ = nullptr;
   AnchorInfo* d_anchors_ = nullptr;
   RuleGpu* d_rules_ = nullptr;
   uint32_t* d_rule_kw_ = nullptr;
   uint64_t* d_nfa_ = nullptr;
-  uint64_t* d_la_ = nullptr;
   uint32_t* d_fullscan_rules_ = nullptr;
-  uint32_t n_states_ = 0, n_classes_ = 0, max_pat_len_ = 0, kw_words_ = 0, n_rules_ = 0;
-  uint32_t n_fullscan_rules_ = 0;
-  std::vector<uint32_t> fullscan_rules_, regex_rules_;
-  uint32_t* d_regex_rules_ = nullptr;
-  size_t lds_bytes_ = 0;
-  bool table_in_lds_ = true;
+  uint32_t kw_words_ = 0, n_rules_ = 0, n_fullscan_rules_ = 0;
+  std::vector<uint32_t> fullscan_rules_;
   // streaming prefilter (filter.h)
   uint32_t* d_reach_ = nullptr;
   uint64_t* d_core_ = nullptr;
@@ -101,14 +89,12 @@ class GpuEngine {
   void* d_flags_ = nullptr; size_t cap_flags_ = 0;
   void* d_hits_ = nullptr; size_t cap_hits_ = 0;
   void* d_cands_ = nullptr; size_t cap_cands_ = 0;
-  void* d_special_ = nullptr; size_t cap_special_ = 0;
   void* d_folds_ = nullptr; size_t cap_folds_ = 0;
   uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
                                     // [7] flagged-block records [8] record overflow
                                     // [9] fold sites [10] fold-site overflow
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
-  void* d_params_ = nullptr; size_t cap_params_ = 0;
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
 };
 

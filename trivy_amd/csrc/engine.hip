@@ -1,18 +1,22 @@
 // gfx950 kernels of the secret-scanning hot path.
 //
-//  K0 chunk_map   : chunk -> file index (one thread per file)
-//  K1 scan        : streams every arena byte once (16-B loads), runs the
-//                   case-folded Aho-Corasick DFA over keywords ∪ anchors held
-//                   in LDS, sets per-file keyword bits (exact MatchKeywords,
-//                   scanner.go:174-186), records anchor hits, counts '\n' per
-//                   chunk and flags files holding U+0130/U+212A/U+017F.
-//  K2 verify      : one lane per anchor hit; gate check, then the rule's
-//                   relaxed shift-and NFA from the hit's start window;
-//                   an accept emits a candidate window for the exact host pass
-//                   (replaces the whole-file regexp sweeps, scanner.go:102-148).
-//  K3 full-scan   : (special file x rule) and (file x unanchored rule) tasks:
-//                   NFA with injection at every byte; an accept makes the
-//                   whole file a candidate.
+//  K0 chunk_map   : 1-KiB chunk -> file index (one thread per file)
+//  K1 filter      : streams every arena byte once (64 B per lane per tile);
+//                   bucketed shift-or over 15 item buckets + a newline bucket
+//                   (reach table replicated 16x in LDS); records the flagged
+//                   16-B blocks and counts '\n' per chunk.
+//  K2 confirm     : three compacted wave phases over the flagged blocks:
+//                   fires -> core-table item candidates -> exact item check
+//                   with file attribution; staged anchor hits, fold-rune
+//                   sites and ASCII keyword bits.
+//  K2f fold       : one workgroup per fold-rune site (U+212A / U+017F / U+0130):
+//                   fold-tolerant item matching in an LDS byte window.
+//  K3 verify      : one lane per anchor hit: the rule's relaxed shift-and NFA
+//                   from the hit's start window; an accept emits a candidate
+//                   window for the exact host pass (replaces the whole-file
+//                   regexp sweeps, scanner.go:102-148).
+//  K4 full-scan   : (file x unanchored rule) tasks: NFA with injection at
+//                   every byte; an accept makes the whole file a candidate.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,12 +32,7 @@ namespace tsg {
 namespace {
 
 constexpr int kScanThreads = 1024;
-constexpr uint32_t kCarefulUnit = 256;  // bytes per lane in the careful pass
 constexpr int kScanWaves = kScanThreads / 64;
-constexpr int kQueue = 320;    // per-wave replay queue (entries): kFlushAt + 4 * 64 - 1 fit
-constexpr int kFlushAt = 64;   // drain when this many blocks wait (each iteration adds <= 64)
-constexpr int kGroup = 4;      // 16-B blocks per load group (64 B per lane, two groups in flight)
-constexpr int kWaveHits = 160; // per-wave LDS hit records
 
 #define HIP_OK(x)                                                   \
   do {                                                              \
@@ -44,39 +43,6 @@ constexpr int kWaveHits = 160; // per-wave LDS hit records
     }                                                               \
   } while (0)
 
-struct ScanParams {
-  const uint8_t* arena;
-  uint64_t n_bytes;
-  const uint64_t* off;
-  uint32_t n_files;
-  const uint32_t* chunk_file;
-  uint64_t n_chunks;
-  const uint8_t* cmap;        // byte -> class; the fold-lead bytes C4/E2/C5 -> the fold column
-  const void* trans;          // entry = next_state * n_classes (element offset of the target row)
-  const uint32_t* out_off;    // per (renumbered) state
-  const uint32_t* out_items;
-  const AnchorInfo* anchors;
-  const uint64_t* la;         // lookahead ASCII masks (2 x u64 each)
-  uint32_t n_states, n_classes, warm, warm_blocks, kw_words;
-  uint32_t thr;               // entries >= thr: target state has outputs (or is the fold root)
-  uint32_t fold_entry;        // entry of the fold root (a flagged copy of the root)
-  uint32_t cls_i, cls_k, cls_s;
-  uint32_t div_magic;         // ceil(2^32 / n_classes): state index = umulhi(entry, magic)
-  uint32_t diag_mode;         // TSG_DIAG_SCAN: 1 skip replay/emission, 2 also skip the DFA (timing only)
-  const void* tabs;           // packed output tables for LDS staging
-  uint32_t tabs_bytes, tab_out_off, tab_out_items, tab_anchors, tab_la;
-  uint32_t* kwbits;
-  uint32_t* flags;            // per file: bit0 fold rune seen, bit1 U+017F seen
-  uint16_t* nl;
-  uint32_t* hits;
-  uint32_t hit_cap;
-  uint32_t* counters;
-  uint32_t* special;
-  uint32_t special_cap;
-  const uint32_t* chunk_list;    // careful mode: chunks to scan (fold-rune files), count at *chunk_list_n
-  const uint32_t* chunk_list_n;
-  uint32_t chunk_list_cap;
-};
 
 __global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
                                  uint32_t* __restrict__ chunk_file) {
@@ -87,388 +53,12 @@ __global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_fi
   }
 }
 
-struct EmitTabs {  // output tables (LDS when they fit, else global) + the wave's hit buffer (LDS)
-  const uint32_t* out_off;
-  const uint32_t* out_items;  // kind (2 bits) | pattern length (10) | id (20), see DevItem()
-  const AnchorInfo* anchors;
-  const uint64_t* la;
-  uint32_t* hbuf;  // kWaveHits records of 3 words
-  uint32_t* hcnt;  // records in hbuf (beyond kWaveHits they went straight to global)
-};
-
-struct ReplayEntry {  // a 16-B block whose DFA path reaches a flagged state
-  uint32_t blk;       // block start / 16 (arenas < 64 GiB, checked on the host)
-  uint32_t st;        // entry (state) before the block
-};
-
-__device__ __forceinline__ uint32_t byte_of(uint4 a, uint4 b, uint32_t i) {  // byte i of the 32-B window a|b
-  uint4 x = i < 16 ? a : b;
-  uint32_t j = i & 15;
-  uint32_t w = j < 8 ? (j < 4 ? x.x : x.y) : (j < 12 ? x.z : x.w);
-  return (w >> ((j & 3) * 8)) & 0xFFu;
-}
-
 __device__ __forceinline__ uint4 load16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Outputs of the state with entry `e`, for a pattern ending at byte `end`
-// (exclusive) in file [fs, fe).  The scan does not restart the automaton at
-// file starts: an Aho-Corasick state reports every pattern that is a suffix
-// of the stream, so the file's own outputs are exactly those no longer than
-// end - fs.  Keywords set the file's gate bit; anchors pass the lookahead
-// filter and go to the wave's LDS hit buffer.  When `win` is set, the bytes
-// after `end` come from the 32-B register window starting at `wbase`.
-constexpr uint32_t kEmitKeywords = 1, kEmitAnchors = 2, kEmitAll = 3;
-
-// `filter`: drop outputs longer than end - fs (the main stream, which runs
-// across file starts); off for careful passes, which start inside the file
-// and count fold runes as one symbol of 2-3 bytes.
-__device__ __forceinline__ void emit_outputs(const ScanParams& P, const EmitTabs& E, uint32_t e, uint32_t f,
-                                             uint64_t fs, uint64_t fe, uint64_t end, bool win, uint64_t wbase,
-                                             uint4 v, uint4 nv, uint32_t kinds = kEmitAll, bool filter = true) {
-  const uint32_t sidx = __umulhi(e, P.div_magic);
-  const uint32_t a = E.out_off[sidx], b = E.out_off[sidx + 1];
-  for (uint32_t j = a; j < b; j++) {
-    const uint32_t item = E.out_items[j];
-    const uint32_t id = item & 0xFFFFFu;
-    if (filter && end - fs < ((item >> 20) & 0x3FFu)) continue;  // starts in an earlier file
-    if ((item >> 30) == 0) {  // keyword: set the file's gate bit once
-      if (!(kinds & kEmitKeywords)) continue;
-      uint32_t* w = &P.kwbits[uint64_t(f) * P.kw_words + (id >> 5)];
-      const uint32_t bit = 1u << (id & 31);
-      if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
-      continue;
-    }
-    if (!(kinds & kEmitAnchors)) continue;
-    const AnchorInfo& an = E.anchors[id];
-    const uint32_t la_n = an.la_n, ext = an.ext;
-    uint32_t lac;
-    __builtin_memcpy(&lac, an.la_cls, 4);
-    const uint64_t lit_end = end - ext;  // the automaton already matched `ext` lookahead bytes
-    bool pass = true;
-    for (uint32_t q = ext; q < la_n; q++) {
-      const uint64_t pos = lit_end + q;
-      if (pos >= fe) {
-        pass = false;
-        break;
-      }
-      const uint32_t c = win ? byte_of(v, nv, uint32_t(pos - wbase)) : uint32_t(P.arena[pos]);
-      if (c >= 0x80) break;  // multi-byte rune: positions no longer align, accept
-      const uint64_t m = E.la[2 * ((lac >> (8 * q)) & 0xFFu) + (c >> 6)];
-      if (!((m >> (c & 63)) & 1)) {
-        pass = false;
-        break;
-      }
-    }
-    if (!pass) continue;
-    const uint32_t k = atomicAdd(E.hcnt, 1u);  // LDS; copied out once per drain
-    if (k < uint32_t(kWaveHits)) {
-      E.hbuf[3 * k + 0] = f;
-      E.hbuf[3 * k + 1] = uint32_t(lit_end - fs);
-      E.hbuf[3 * k + 2] = id;
-    } else {
-      const uint32_t g = atomicAdd(&P.counters[0], 1u);
-      if (g < P.hit_cap) {
-        P.hits[3ull * g + 0] = f;
-        P.hits[3ull * g + 1] = uint32_t(lit_end - fs);
-        P.hits[3ull * g + 2] = id;
-      } else {
-        P.counters[3] = 1;
-      }
-    }
-  }
-}
-
-// Length of the fold sequence starting at `p` (U+0130 / U+212A / U+017F), 0 if none.
-__device__ __forceinline__ uint32_t fold_len(const ScanParams& P, uint64_t p, uint64_t fe, uint32_t* cls,
-                                             uint32_t* fl) {
-  const uint8_t* a = P.arena;
-  const uint32_t b = a[p];
-  if (b == 0xC4 && p + 1 < fe && a[p + 1] == 0xB0) {
-    *cls = P.cls_i;
-    *fl = 1;
-    return 2;
-  }
-  if (b == 0xE2 && p + 2 < fe && a[p + 1] == 0x84 && a[p + 2] == 0xAA) {
-    *cls = P.cls_k;
-    *fl = 1;
-    return 3;
-  }
-  if (b == 0xC5 && p + 1 < fe && a[p + 1] == 0xBF) {
-    *cls = P.cls_s;
-    *fl = 3;
-    return 2;
-  }
-  return 0;
-}
-
-// Careful pass around a fold sequence at `x` (file [fs, fe)).  Under
-// bytes.ToLower U+0130 -> 'i' and U+212A -> 'k' (keywords and anchors);
-// U+017F stays itself for keywords but folds with 's' under (?i) (anchors),
-// so keywords and anchors take one pass each and the keyword bits stay exact.
-// The main loop runs the fold-lead byte as a non-pattern byte, whose outputs
-// are a subset of the true stream's; a pass restarts 3*warm+2 bytes earlier
-// (>= warm whole symbols) on the true symbol stream and emits every output
-// ending after `x` until warm plain bytes follow the last fold sequence,
-// where both streams' states agree again.  Duplicated hits are harmless (the
-// host merges windows per rule).
-template <typename TT>
-__device__ __forceinline__ void careful_fold(const ScanParams& P, const EmitTabs& E, const TT* T, const uint8_t* cmap,
-                                             uint32_t f, uint64_t fs, uint64_t fe, uint64_t x) {
-  const uint8_t* a = P.arena;
-  const uint64_t back = 3ull * P.warm + 2;
-  uint32_t fl = 0;
-  for (uint32_t pass = 0; pass < 2; pass++) {
-    const uint32_t kinds = pass == 0 ? kEmitKeywords : kEmitAnchors;
-    uint64_t p = x - fs > back ? x - back : fs;
-    uint64_t stop = x + 3 + P.warm;
-    uint32_t st = 0;
-    while (p < fe && p < stop) {
-      uint32_t cls = cmap[a[p]], flx = 0;
-      uint32_t len = fold_len(P, p, fe, &cls, &flx);
-      if (len) {
-        fl |= flx;
-        if (pass == 0 && flx == 3) cls = 0;  // U+017F: not a letter for keywords
-        if (p + len + P.warm > stop) stop = p + len + P.warm;
-      } else {
-        len = 1;
-      }
-      const uint32_t e = T[st + cls];
-      st = e;
-      p += len;
-      if (e >= P.thr && e != P.fold_entry && p > x)
-        emit_outputs(P, E, e, f, fs, fe, p, false, 0, uint4{}, uint4{}, kinds, false);
-    }
-  }
-  if (fl) {
-    const uint32_t old = atomicOr(&P.flags[f], fl);
-    if (old == 0) {
-      const uint32_t k = atomicAdd(&P.counters[2], 1u);
-      if (k < P.special_cap) P.special[k] = f;
-    }
-  }
-}
-
-// '\n' bytes in a 32-bit word (exact per byte)
-__device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
-  const uint32_t x = w ^ 0x0A0A0A0Au;
-  const uint32_t nz = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // bit7 set <=> byte != 0
-  return 4u - __popc(nz & 0x80808080u);
-}
-
-// Replays queue entries [0, n) of one wave (entry `lane` and `lane + 64`):
-// the block's 16 bytes are re-read (L2/MALL-warm), each flagged position is
-// attributed to its file and its outputs are emitted.
-template <typename TT>
-__device__ __forceinline__ void drain_queue(const ScanParams& P, const EmitTabs& E, const TT* T, const uint8_t* cmap,
-                                            const ReplayEntry* Q, uint32_t n, uint32_t lane) {
-  wave_sync();
-  for (uint32_t i = lane; i < n; i += 64) {
-    const ReplayEntry r = Q[i];
-    if (P.diag_mode) continue;
-    const uint64_t rp = uint64_t(r.blk) * 16;
-    uint32_t f = P.chunk_file[rp / kChunk];  // the file holding the chunk's first byte; walk forward
-    uint64_t fs = P.off[f], fe = P.off[f + 1];
-    const uint4 v = load16(P.arena + rp), nv = load16(P.arena + rp + 16);
-    uint32_t st = r.st;
-    for (uint32_t k = 0; k < 16; k++) {
-      const uint32_t e = T[st + cmap[byte_of(v, nv, k)]];
-      st = e;
-      if (e < P.thr) continue;
-      const uint64_t q = rp + k;
-      if (q >= P.n_bytes) break;
-      while (q >= fe) {  // q < n_bytes = off[n_files]: stays in range
-        f++;
-        fs = fe;
-        fe = P.off[f + 1];
-      }
-      if (q < fs) continue;  // before the first file
-      if (e == P.fold_entry) {
-        uint32_t cls, fl;
-        if (fold_len(P, q, fe, &cls, &fl)) careful_fold<TT>(P, E, T, cmap, f, fs, fe, q);
-      } else {
-        emit_outputs(P, E, e, f, fs, fe, q + 1, true, rp, v, nv);
-      }
-    }
-  }
-  wave_sync();
-}
-
-// Copies the wave's LDS hit records to the global list (one atomic per wave).
-__device__ __forceinline__ void flush_hits(const ScanParams& P, const EmitTabs& E, uint32_t lane) {
-  wave_sync();
-  const uint32_t n_all = __builtin_amdgcn_readfirstlane(*E.hcnt);
-  const uint32_t n = n_all < uint32_t(kWaveHits) ? n_all : uint32_t(kWaveHits);
-  if (n == 0) return;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(&P.counters[0], n);
-  base = __builtin_amdgcn_readfirstlane(base);
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint32_t g = base + i;
-    if (g < P.hit_cap) {
-      P.hits[3ull * g + 0] = E.hbuf[3 * i + 0];
-      P.hits[3ull * g + 1] = E.hbuf[3 * i + 1];
-      P.hits[3ull * g + 2] = E.hbuf[3 * i + 2];
-    } else {
-      P.counters[3] = 1;
-    }
-  }
-  wave_sync();
-  if (lane == 0) *E.hcnt = 0;
-  wave_sync();
-}
-
-// K1.  One wave owns 64 consecutive kChunk-byte chunks (one per lane) at a
-// time.  Every lane walks the same number of 16-B blocks (warm-up + chunk,
-// padded to whole load groups), so the wave stays converged.  The automaton
-// runs straight across file boundaries (outputs are attributed and filtered
-// per file at emission, see emit_outputs), so the hot body is only class
-// lookup + transition from LDS plus one max per block for the flagged test
-// (flagged states are numbered last).  Each lane loads 64 contiguous bytes
-// at a time (4 x 16-B loads on the same lines) with the next 64 in flight.
-// A block that reached a flagged state is queued in LDS (ballot + mbcnt);
-// once 64 wait, the whole wave replays 64 of them in parallel, so emission
-// costs full-width work instead of a divergent replay per block.  Anchor
-// hits gather in a per-wave LDS buffer and leave with one atomic per drain.
-template <typename TT, bool kLdsTable>
-__global__ __launch_bounds__(kScanThreads) void scan_kernel(ScanParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint64_t n_work = P.n_chunks;
-  if (P.chunk_list) {
-    const uint32_t n = *P.chunk_list_n;
-    n_work = n < P.chunk_list_cap ? n : P.chunk_list_cap;
-    if (n_work == 0) return;
-  }
-  const size_t tbytes = kLdsTable ? ((size_t(P.n_states) * P.n_classes * sizeof(TT) + 15) & ~size_t(15)) : 0;
-  TT* s_trans = reinterpret_cast<TT*>(smem);
-  uint8_t* s_cmap = smem + tbytes;
-  uint8_t* s_tabs = smem + tbytes + 256;
-  ReplayEntry* s_queue = reinterpret_cast<ReplayEntry*>(s_tabs + (kLdsTable ? P.tabs_bytes : 0));
-  uint32_t* s_hits = reinterpret_cast<uint32_t*>(s_queue + kScanWaves * kQueue);
-  uint32_t* s_hcnt = s_hits + kScanWaves * kWaveHits * 3;
-  const int tid = threadIdx.x;
-  if (kLdsTable) {
-    const uint4* src = reinterpret_cast<const uint4*>(P.trans);
-    uint4* dst = reinterpret_cast<uint4*>(s_trans);
-    const size_t n16 = tbytes / 16;
-    for (size_t i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
-    const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
-    uint4* d = reinterpret_cast<uint4*>(s_tabs);
-    for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
-  }
-  for (int i = tid; i < 256; i += blockDim.x) s_cmap[i] = P.cmap[i];
-  if (tid < kScanWaves) s_hcnt[tid] = 0;
-  __syncthreads();
-  const TT* T = kLdsTable ? s_trans : reinterpret_cast<const TT*>(P.trans);
-  const uint8_t* Tb = reinterpret_cast<const uint8_t*>(T);
-  const uint32_t lane = tid & 63, wave = tid >> 6;
-  EmitTabs E;
-  if (kLdsTable) {
-    E.out_off = reinterpret_cast<const uint32_t*>(s_tabs + P.tab_out_off);
-    E.out_items = reinterpret_cast<const uint32_t*>(s_tabs + P.tab_out_items);
-    E.anchors = reinterpret_cast<const AnchorInfo*>(s_tabs + P.tab_anchors);
-    E.la = reinterpret_cast<const uint64_t*>(s_tabs + P.tab_la);
-  } else {
-    E.out_off = P.out_off;
-    E.out_items = P.out_items;
-    E.anchors = P.anchors;
-    E.la = P.la;
-  }
-  E.hbuf = s_hits + wave * kWaveHits * 3;
-  E.hcnt = s_hcnt + wave;
-  ReplayEntry* Q = s_queue + wave * kQueue;
-  uint32_t qn = 0;  // wave-uniform
-  const uint32_t thr = P.thr;
-  // load groups per lane, rounded up to an even count (blocks past b1 are skipped)
-  // careful mode scans 256-B units (more lanes for the few fold-rune files); full mode 1-KiB chunks
-  const uint32_t unit = P.chunk_list ? kCarefulUnit : kChunk;
-  const uint32_t ngroups = ((P.warm_blocks + unit / 16 + kGroup - 1) / kGroup + 1) & ~1u;
-  const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
-
-  for (uint64_t tile = uint64_t(blockIdx.x) * kScanWaves + wave; tile * 64 < n_work; tile += n_waves) {
-    const uint64_t idx = tile * 64 + lane;
-    const bool live = idx < n_work;
-    const uint64_t c = P.chunk_list ? P.chunk_list[live ? idx : n_work - 1] : idx;
-    const uint64_t b0 = c * unit;
-    const uint64_t b1 = live ? (b0 + unit < P.n_bytes ? b0 + unit : P.n_bytes) : 0;
-    const int64_t pstart = int64_t(b0) - int64_t(P.warm_blocks) * 16;
-    uint32_t st = 0, nl = 0;
-    // loads are unconditional (clamped address) so the waits stay countable
-    auto load_group = [&](uint4* g, int64_t gp) {
-#pragma unroll
-      for (int j = 0; j < kGroup; j++) {
-        const int64_t p = gp + 16 * j;
-        g[j] = load16(P.arena + ((p >= 0 && uint64_t(p) < b1) ? uint64_t(p) : 0));
-      }
-    };
-    // one group of 4 blocks: transitions, then queue the flagged blocks
-    auto do_group = [&](const uint4* g, const int64_t gp) {
-      uint32_t st0[kGroup];
-      bool flg[kGroup];
-#pragma unroll
-      for (int j = 0; j < kGroup; j++) {
-        const int64_t p = gp + 16 * j;
-        const uint4 v = g[j];
-        st0[j] = st;
-        flg[j] = false;
-        if (p >= 0 && uint64_t(p) < b1) {
-          if (P.diag_mode < 2) {
-            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-            uint32_t mx = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-              const uint32_t cl = s_cmap[(wd[k >> 2] >> ((k & 3) * 8)) & 0xFFu];
-              const uint32_t e = *reinterpret_cast<const TT*>(Tb + ((st + cl) * uint32_t(sizeof(TT))));
-              mx = mx > e ? mx : e;
-              st = e;
-            }
-            flg[j] = uint64_t(p) >= b0 && mx >= thr;
-          }
-          if (uint64_t(p) >= b0) {
-            if (uint64_t(p) + 16 <= b1) {
-              nl += nl_in_word(v.x) + nl_in_word(v.y) + nl_in_word(v.z) + nl_in_word(v.w);
-            } else {  // the arena's last, partial block
-              for (uint32_t k = 0; uint64_t(p) + k < b1; k++) nl += byte_of(v, v, k) == '\n';
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kGroup; j++) {
-        const uint64_t m = __ballot(flg[j]);
-        if (m) {  // wave-uniform
-          const uint32_t below =
-              __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-          if (flg[j]) Q[qn + below] = ReplayEntry{uint32_t(uint64_t(gp + 16 * j) >> 4), st0[j]};
-          qn += uint32_t(__popcll(m));
-        }
-      }
-      if (qn >= uint32_t(kFlushAt)) {  // wave-uniform; qn < kFlushAt + 4 * 64 <= kQueue
-        drain_queue<TT>(P, E, T, s_cmap, Q, qn, lane);
-        flush_hits(P, E, lane);
-        qn = 0;
-      }
-    };
-    uint4 A[kGroup], B[kGroup];
-    load_group(A, pstart);
-    load_group(B, pstart + 16 * kGroup);
-    for (uint32_t g = 0; g < ngroups; g += 2) {
-      const int64_t ga = pstart + int64_t(g) * 16 * kGroup;
-      do_group(A, ga);
-      load_group(A, ga + 2 * 16 * kGroup);  // A's registers are dead: the loads land in place
-      const int64_t gb = ga + 16 * kGroup;
-      do_group(B, gb);
-      load_group(B, gb + 2 * 16 * kGroup);
-    }
-    if (live && !P.chunk_list) P.nl[c] = uint16_t(nl);
-  }
-  if (qn) drain_queue<TT>(P, E, T, s_cmap, Q, qn, lane);
-  flush_hits(P, E, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -643,26 +233,6 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   if (qn) flush();
 }
 
-// Chunk list of the files K1 found fold runes in (for the careful pass): one
-// workgroup per file reserves the file's chunk range, its threads fill it.
-__global__ __launch_bounds__(256) void special_chunks_kernel(const uint64_t* __restrict__ off,
-                                                             const uint32_t* __restrict__ special,
-                                                             uint32_t* __restrict__ counters,
-                                                             uint32_t* __restrict__ list, uint32_t cap) {
-  __shared__ uint32_t s_base;
-  const uint32_t n = counters[2];
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    const uint32_t f = special[i];
-    const uint64_t c0 = off[f] / kCarefulUnit, c1 = (off[f + 1] - 1) / kCarefulUnit;
-    if (threadIdx.x == 0) s_base = atomicAdd(&counters[5], uint32_t(c1 - c0 + 1));
-    __syncthreads();
-    const uint32_t k = s_base;
-    for (uint64_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x)
-      if (k + (c - c0) < cap) list[k + (c - c0)] = uint32_t(c);
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------
 // relaxed NFA (extended shift-and)
 // ---------------------------------------------------------------------------
@@ -683,86 +253,9 @@ struct NfaParams {
   uint32_t* counters;
   Candidate* cands;
   uint32_t cand_cap;
-  const uint32_t* special;
-  uint32_t special_cap;
-  const uint32_t* regex_rules;
-  uint32_t n_regex_rules;
   const uint32_t* fullscan_rules;
   uint32_t n_fullscan_rules;
 };
-
-// Returns true at the first position whose state reaches a final position.
-// Injection (a match may start here) is on for positions in [start, inj_hi].
-template <int W>
-__device__ bool nfa_run(const uint8_t* __restrict__ s, int64_t len, int64_t start, int64_t inj_hi,
-                        const uint64_t* __restrict__ tab) {
-  uint64_t O[W], Lp[W], F[W], D[W];
-#pragma unroll
-  for (int w = 0; w < W; w++) {
-    O[w] = tab[w];
-    Lp[w] = tab[W + w];
-    F[w] = tab[2 * W + w];
-    D[w] = 0;
-  }
-  const uint64_t* B = tab + 3 * W;
-  for (int64_t pos = start; pos < len; pos++) {
-    uint32_t b = s[pos];
-    uint64_t carry = pos <= inj_hi ? 1 : 0;
-    uint64_t T[W];
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      T[w] = (D[w] << 1) | carry | (D[w] & Lp[w]);
-      carry = D[w] >> 63;
-    }
-    uint64_t c = 0;
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      uint64_t x = T[w] & O[w];
-      uint64_t s1 = O[w] + x;
-      uint64_t c1 = s1 < O[w];
-      uint64_t s2 = s1 + c;
-      uint64_t c2 = s2 < s1;
-      T[w] |= s2 ^ O[w];
-      c = c1 | c2;
-    }
-    const uint64_t* Bb = B + size_t(b) * W;
-    bool keep = (b & 0xC0u) == 0x80u;  // UTF-8 continuation: also stay
-    uint64_t acc = 0, alive = 0;
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      uint64_t nd = (T[w] & Bb[w]) | (keep ? D[w] : 0);
-      D[w] = nd;
-      acc |= nd & F[w];
-      alive |= nd;
-    }
-    if (acc) return true;
-    if (!alive && pos >= inj_hi) return false;
-  }
-  return false;
-}
-
-__device__ bool nfa_dispatch(int words, const uint8_t* s, int64_t len, int64_t start, int64_t inj_hi,
-                             const uint64_t* tab) {
-  switch (words) {
-    case 1: return nfa_run<1>(s, len, start, inj_hi, tab);
-    case 2: return nfa_run<2>(s, len, start, inj_hi, tab);
-    case 3: return nfa_run<3>(s, len, start, inj_hi, tab);
-    default: return nfa_run<4>(s, len, start, inj_hi, tab);
-  }
-}
-
-__device__ int64_t count_nl(const NfaParams& P, uint64_t a, uint64_t b) {  // '\n' in arena [a, b)
-  int64_t n = 0;
-  uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
-  if (ca >= cb) {
-    for (uint64_t p = a; p < b; p++) n += P.arena[p] == '\n';
-    return n;
-  }
-  for (uint64_t p = a; p < ca * kChunk; p++) n += P.arena[p] == '\n';
-  for (uint64_t c = ca; c < cb; c++) n += P.nl[c];
-  for (uint64_t p = cb * kChunk; p < b; p++) n += P.arena[p] == '\n';
-  return n;
-}
 
 __device__ void emit_candidate(const NfaParams& P, uint32_t f, uint32_t r, int64_t wlo, int64_t whi,
                                int64_t nlb, uint32_t flags) {
@@ -779,46 +272,6 @@ __device__ void emit_candidate(const NfaParams& P, uint32_t f, uint32_t r, int64
     P.cands[k] = c;
   } else {
     P.counters[4] = 1;
-  }
-}
-
-__global__ __launch_bounds__(256) void verify_kernel(NfaParams P) {
-  uint32_t n = P.counters[0] < P.hit_cap ? P.counters[0] : P.hit_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t f = P.hits[3ull * i], end = P.hits[3ull * i + 1], aid = P.hits[3ull * i + 2];
-    AnchorInfo a = P.anchors[aid];
-    RuleGpu rg = P.rules[a.rule];  // keyword gates are evaluated lazily by the host tail
-    uint32_t ff = P.flags[f];
-    // literal start: lit_len bytes before the end, up to 3x when folded runes occur
-    int64_t lit_hi = int64_t(end) - int64_t(a.lit_len);
-    int64_t lit_lo = (ff & 1u) ? int64_t(end) - 3 * int64_t(a.lit_len) : lit_hi;
-    int64_t whi = lit_hi - a.off_lo;
-    if (whi < 0) continue;
-    int64_t wlo = lit_lo - ((ff & 1u) ? int64_t(a.off_hi_fold) : int64_t(a.off_hi));
-    if (wlo < 0) wlo = 0;
-    uint64_t fs = P.off[f];
-    int64_t len = int64_t(P.off[f + 1] - fs);
-    bool acc = rg.nfa_words == 0 ||
-               nfa_dispatch(rg.nfa_words, P.arena + fs, len, wlo, whi, P.nfa + rg.nfa_off);
-    if (acc)
-      emit_candidate(P, f, a.rule, wlo, whi, count_nl(P, fs, fs + uint64_t(wlo)), 0u);
-  }
-}
-
-// Unanchored rules (no literal at a bounded offset): NFA with injection at
-// every byte of every gated file; an accept makes the whole file the window.
-__global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
-  uint64_t total = uint64_t(P.n_files) * P.n_fullscan_rules;
-  for (uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; t < total;
-       t += uint64_t(gridDim.x) * blockDim.x) {
-    uint32_t f = uint32_t(t / P.n_fullscan_rules);
-    uint32_t r = P.fullscan_rules[t % P.n_fullscan_rules];
-    RuleGpu rg = P.rules[r];
-    uint64_t fs = P.off[f];
-    int64_t len = int64_t(P.off[f + 1] - fs);
-    bool acc = rg.nfa_words == 0 ||
-               nfa_dispatch(rg.nfa_words, P.arena + fs, len, 0, len, P.nfa + rg.nfa_off);
-    if (acc) emit_candidate(P, f, r, 0, len, 0, 0u);
   }
 }
 
@@ -921,8 +374,6 @@ struct ConfirmParams {
   const uint32_t* recs;
   uint32_t rec_cap;
   uint32_t* flags;
-  uint32_t* special;
-  uint32_t special_cap;
   uint32_t* counters;  // [0] hits [2] special files [3] hit overflow [7] records [9] folds [10] fold overflow
   uint32_t* hits;      // (file, literal end in the file, anchor id)
   uint32_t hit_cap;
@@ -1118,11 +569,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     if (it.kind == kItemFold) {
       // bit0: widen anchor offsets; bit1: U+017F; bit2: U+0130 / U+212A (lower into ASCII)
       const uint32_t fl = item_ids[it.ids_off] == 2 ? 3u : 5u;
-      const uint32_t old = atomicOr(&P.flags[f], fl);
-      if (old == 0) {
-        const uint32_t q = atomicAdd(&P.counters[2], 1u);
-        if (q < P.special_cap) P.special[q] = f;
-      }
+      if (atomicOr(&P.flags[f], fl) == 0) atomicAdd(&P.counters[2], 1u);  // files with fold runes
       const uint32_t q = atomicAdd(&P.counters[9], 1u);
       if (q < P.fold_cap) P.folds[q] = FoldSite{s0, f, it.n};
       else P.counters[10] = 1;
@@ -1359,6 +806,22 @@ __global__ __launch_bounds__(256) void verify_hits_kernel(NfaParams P) {
   }
 }
 
+// Unanchored rules (no literal at a bounded offset): NFA with injection at
+// every byte of every file; an accept makes the whole file the window.
+__global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
+  const uint64_t total = uint64_t(P.n_files) * P.n_fullscan_rules;
+  for (uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; t < total;
+       t += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t f = uint32_t(t / P.n_fullscan_rules);
+    const uint32_t r = P.fullscan_rules[t % P.n_fullscan_rules];
+    const RuleGpu rg = P.rules[r];
+    const uint64_t fs = P.off[f];
+    const int64_t len = int64_t(P.off[f + 1] - fs);
+    const bool acc = rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, 0, len, P.nfa + rg.nfa_off);
+    if (acc) emit_candidate(P, f, r, 0, len, 0, 0u);  // gate checked exactly on the host
+  }
+}
+
 template <typename T>
 bool Upload(std::string* err, T** dst, const T* src, size_t n) {
   size_t bytes = std::max<size_t>(n * sizeof(T), 16);
@@ -1387,165 +850,21 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   for (auto& e : ev_) hipEventCreate(&e);
   if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
   if (const char* dc = std::getenv("TSG_DIAG_CONFIRM")) diag_confirm_ = uint32_t(std::atoi(dc));
-  n_states_ = cr.n_states;
-  n_classes_ = cr.n_classes;
-  max_pat_len_ = cr.max_pat_len;
   kw_words_ = std::max<uint32_t>(1, cr.kw_words());
   n_rules_ = uint32_t(cr.rules.size());
-  for (uint32_t r = 0; r < n_rules_; r++) {
-    if (!cr.rules[r].has_regex) continue;
-    regex_rules_.push_back(r);
-    if (!cr.rules[r].anchored) fullscan_rules_.push_back(r);
-  }
+  for (uint32_t r = 0; r < n_rules_; r++)
+    if (cr.rules[r].has_regex && !cr.rules[r].anchored) fullscan_rules_.push_back(r);
   n_fullscan_rules_ = uint32_t(fullscan_rules_.size());
-  // Device DFA: the real class columns plus one for the fold-lead bytes
-  // C4/E2/C5.  States are renumbered: plain states first (root = 0), then
-  // states with outputs, then the fold root (a copy of the root's row that
-  // every state enters on a fold-lead byte; class 0 always returns to the
-  // root, so the stream's states are unchanged).  An entry is the element
-  // offset of the target row, so "has outputs" is entry >= thr_.
-  const uint32_t nc_real = n_classes_;
-  const uint32_t cls_fold = nc_real;
-  const uint32_t nc = nc_real + 1;
-  n_classes_ = nc;
-  if (nc >= 0xFF) {
-    err_ = "too many keyword character classes";
-    return;
-  }
-  uint8_t cmap[256];
-  for (int b = 0; b < 256; b++) {
-    uint8_t m = cr.cmap[b];
-    cmap[b] = m >= kClsFoldI ? uint8_t(cls_fold) : m;
-  }
-  cls_i_ = cr.cmap['i'];
-  cls_k_ = cr.cmap['k'];
-  cls_s_ = cr.cmap['s'];
-  const uint32_t ns = n_states_;
-  std::vector<uint32_t> perm(ns), inv;
-  {
-    uint32_t nid = 0;
-    for (int pass = 0; pass < 2; pass++)
-      for (uint32_t s = 0; s < ns; s++) {
-        bool out = cr.out_off[s + 1] > cr.out_off[s];
-        if (out == (pass == 1)) perm[s] = nid++;
-      }
-    inv.resize(ns);
-    for (uint32_t s = 0; s < ns; s++) inv[perm[s]] = s;
-    uint32_t n_plain = 0;
-    for (uint32_t s = 0; s < ns; s++) n_plain += cr.out_off[s + 1] == cr.out_off[s];
-    if (perm[0] != 0) {
-      err_ = "AC root has outputs";
-      return;
-    }
-    thr_ = n_plain * nc;
-  }
-  const uint32_t nsd = ns + 1;  // + fold root
-  n_states_ = nsd;
-  fold_entry_ = ns * nc;
-  div_magic_ = uint32_t((uint64_t(1) << 32) / nc + 1);
-  wide_table_ = uint64_t(nsd) * nc > 0x10000;
-  std::vector<uint8_t> tbuf;
-  size_t esz = wide_table_ ? 4 : 2;
-  size_t tbytes = (size_t(nsd) * nc * esz + 15) & ~size_t(15);
-  tbuf.assign(tbytes + 16, 0);
-  for (uint32_t ds = 0; ds < nsd; ds++) {
-    uint32_t src_state = ds < ns ? inv[ds] : 0;
-    for (uint32_t col = 0; col < nc; col++) {
-      uint32_t v;
-      if (col == cls_fold) {
-        v = fold_entry_;
-      } else {
-        uint32_t e = cr.trans[size_t(src_state) * nc_real + col];
-        uint32_t tgt = e & 0x7FFFu;
-        if (col == 0 && tgt != 0) {
-          err_ = "AC class 0 does not return to the root";
-          return;
-        }
-        v = perm[tgt] * nc;
-      }
-      size_t i = size_t(ds) * nc + col;
-      if (wide_table_) std::memcpy(&tbuf[i * 4], &v, 4);
-      else {
-        uint16_t h = uint16_t(v);
-        std::memcpy(&tbuf[i * 2], &h, 2);
-      }
-    }
-  }
-  // output lists in the renumbered order (+ an empty list for the fold root)
-  // device item = kind (2 bits) | pattern length in bytes (10) | id (20): the
-  // length lets K1 drop outputs that start before the file (emit_outputs)
-  std::vector<uint32_t> out_off(nsd + 1, 0), out_items;
-  for (uint32_t ds = 0; ds < ns; ds++) {
-    uint32_t s = inv[ds];
-    out_off[ds] = uint32_t(out_items.size());
-    for (uint32_t j = cr.out_off[s]; j < cr.out_off[s + 1]; j++) {
-      const uint32_t item = cr.out_items[j], kind = item >> 28, id = item & 0x0FFFFFFFu;
-      size_t len;
-      if (kind == (kOutKeyword >> 28)) {
-        len = cr.keywords[id].size();
-      } else if (kind == (kOutAnchor >> 28)) {
-        len = size_t(cr.anchors[id].lit_len) + cr.anchors[id].ext;
-      } else {
-        err_ = "unexpected automaton output kind";
-        return;
-      }
-      if (id >= (1u << 20) || len >= (1u << 10)) {
-        err_ = "rule set exceeds the scan kernel's output encoding (ids < 2^20, patterns < 1024 bytes)";
-        return;
-      }
-      out_items.push_back((kind << 30) | (uint32_t(len) << 20) | id);
-    }
-  }
-  out_off[ns] = out_off[ns + 1] = uint32_t(out_items.size());
-  uint8_t* d_tb = nullptr;
-  std::vector<uint64_t> la = cr.la_masks;
-  if (la.empty()) la.assign(2, 0);
-  if (!Upload(&err_, &d_cmap_, cmap, 256) || !Upload(&err_, &d_tb, tbuf.data(), tbuf.size()) ||
-      !Upload(&err_, &d_out_off_, out_off.data(), out_off.size()) ||
-      !Upload(&err_, &d_out_items_, out_items.data(), out_items.size()) ||
-      !Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
-      !Upload(&err_, &d_la_, la.data(), la.size()) ||
+  if (!Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
       !Upload(&err_, &d_rules_, cr.rules.data(), cr.rules.size()) ||
       !Upload(&err_, &d_rule_kw_, cr.rule_kw.data(), cr.rule_kw.size()) ||
       !Upload(&err_, &d_nfa_, cr.nfa.data(), cr.nfa.size()) ||
-      !Upload(&err_, &d_regex_rules_, regex_rules_.data(), regex_rules_.size()) ||
       !Upload(&err_, &d_fullscan_rules_, fullscan_rules_.data(), fullscan_rules_.size()))
     return;
-  d_trans_ = d_tb;
   if (hipMalloc(&d_counters_, 64) != hipSuccess) {
     err_ = "hipMalloc counters";
     return;
   }
-  // packed output tables (staged into LDS next to the DFA)
-  {
-    auto pad = [](std::vector<uint8_t>& v) { v.resize((v.size() + 15) & ~size_t(15), 0); };
-    std::vector<uint8_t> tb;
-    auto put = [&](const void* src, size_t n) {
-      size_t at = tb.size();
-      tb.resize(at + n);
-      if (n) std::memcpy(&tb[at], src, n);
-      pad(tb);
-      return uint32_t(at);
-    };
-    tab_out_off_ = put(out_off.data(), out_off.size() * 4);
-    tab_out_items_ = put(out_items.data(), out_items.size() * 4);
-    tab_anchors_ = put(cr.anchors.data(), cr.anchors.size() * sizeof(AnchorInfo));
-    tab_la_ = put(la.data(), la.size() * 8);
-    if (tb.empty()) tb.assign(16, 0);
-    tabs_bytes_ = uint32_t(tb.size());
-    uint8_t* d = nullptr;
-    if (!Upload(&err_, &d, tb.data(), tb.size())) return;
-    d_tabs_ = d;
-  }
-  const size_t queue_bytes = size_t(kScanWaves) * kQueue * sizeof(ReplayEntry) +
-                             size_t(kScanWaves) * kWaveHits * 12 + size_t(kScanWaves) * 4;
-  table_in_lds_ = tbytes + 256 + tabs_bytes_ + queue_bytes <= 156 * 1024;
-  lds_bytes_ = table_in_lds_ ? tbytes + 256 + tabs_bytes_ + queue_bytes : 256 + queue_bytes;
-  const void* fn = wide_table_ ? (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint32_t, true>)
-                                                : reinterpret_cast<const void*>(&scan_kernel<uint32_t, false>))
-                               : (table_in_lds_ ? reinterpret_cast<const void*>(&scan_kernel<uint16_t, true>)
-                                                : reinterpret_cast<const void*>(&scan_kernel<uint16_t, false>));
-  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_bytes_));
   // streaming prefilter tables (filter.h)
   {
     const FilterTables* ft = cr.filter.get();
@@ -1592,9 +911,9 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_tabs_, d_cmap_, d_trans_, d_out_off_, d_out_items_, d_anchors_, d_la_, d_rules_, d_rule_kw_, d_nfa_,
-                d_regex_rules_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_, d_flags_,
-                d_hits_, d_cands_, d_special_, d_arena_stage_, d_off_stage_, d_params_};
+  void* ps[] = {d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+                d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
+                d_flags_, d_hits_, d_cands_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
     if (p) hipFree(p);
   for (auto& e : ev_)
@@ -1648,7 +967,6 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, n_chunks * 2) ||
         !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
         !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
-        !Ensure(&d_special_, &cap_special_, size_t(n_files) * 4) ||
         !Ensure(&d_folds_, &cap_folds_, size_t(fold_cap_) * sizeof(FoldSite)) ||
         !Ensure(&d_recs_, &cap_recs_, size_t(rec_cap_) * 4) ||
         !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
@@ -1701,8 +1019,6 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.recs = static_cast<const uint32_t*>(d_recs_);
     cp.rec_cap = rec_cap_;
     cp.flags = static_cast<uint32_t*>(d_flags_);
-    cp.special = static_cast<uint32_t*>(d_special_);
-    cp.special_cap = n_files;
     cp.counters = d_counters_;
     cp.hits = static_cast<uint32_t*>(d_hits_);
     cp.hit_cap = hit_cap_;
@@ -1753,10 +1069,6 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.counters = d_counters_;
     np.cands = static_cast<Candidate*>(d_cands_);
     np.cand_cap = cand_cap_;
-    np.special = static_cast<const uint32_t*>(d_special_);
-    np.special_cap = n_files;
-    np.regex_rules = d_regex_rules_;
-    np.n_regex_rules = uint32_t(regex_rules_.size());
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
     if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);

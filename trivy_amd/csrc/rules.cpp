@@ -297,52 +297,6 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
   return have && best->minlen() >= 2;
 }
 
-// Up to 4 mandatory single-rune classes at the start of `fol` (ASCII masks).
-// ascii_only[i]: the class holds no non-ASCII rune besides the fold-only ones.
-std::vector<std::pair<uint64_t, uint64_t>> Lookahead(const std::vector<Node>& nodes, const std::vector<int>& fol,
-                                                     std::vector<bool>* ascii_only = nullptr) {
-  std::vector<std::pair<uint64_t, uint64_t>> out;
-  auto asc_only = [&](const RuneRanges& rr) {
-    for (auto& p : rr) {
-      if (p.second < 0x80) continue;
-      for (uint32_t c = std::max<uint32_t>(p.first, 0x80); c <= p.second; c++) {
-        if (!IsFoldOnlyRune(c)) return false;
-        if (c - p.first > 8) return false;
-      }
-    }
-    return true;
-  };
-  auto mask = [&](const RuneRanges& rr) {
-    std::pair<uint64_t, uint64_t> m{0, 0};
-    for (uint32_t b = 0; b < 128; b++)
-      if (ClassHas(rr, b)) (b < 64 ? m.first : m.second) |= uint64_t(1) << (b & 63);
-    return m;
-  };
-  for (int it : fol) {
-    if (out.size() >= 4) break;
-    const Node& n = nodes[it];
-    if (n.op == NodeOp::Class) {
-      out.push_back(mask(n.ranges));
-      if (ascii_only) ascii_only->push_back(asc_only(n.ranges));
-      continue;
-    }
-    if (n.op == NodeOp::Repeat && n.min >= 1) {
-      int sub = n.subs[0];
-      while (nodes[sub].op == NodeOp::Capture) sub = nodes[sub].subs[0];
-      if (nodes[sub].op == NodeOp::Class) {
-        for (int r = 0; r < n.min && out.size() < 4; r++) {
-          out.push_back(mask(nodes[sub].ranges));
-          if (ascii_only) ascii_only->push_back(asc_only(nodes[sub].ranges));
-        }
-        if (n.max != n.min) break;  // what follows the repeat is not at a fixed position
-        continue;
-      }
-    }
-    break;
-  }
-  return out;
-}
-
 // ---------------------------------------------------------------------------
 // relaxed class-sequence NFA
 // ---------------------------------------------------------------------------
@@ -520,91 +474,6 @@ bool IsAscii(const std::string& s) {
   return true;
 }
 
-bool BuildAc(const std::vector<std::pair<std::string, uint32_t>>& pats, CompiledRules* out, std::string* err) {
-  // classes
-  int cls_of[256];
-  for (int b = 0; b < 256; b++) cls_of[b] = 0;
-  int nc = 1;
-  std::set<unsigned char> used;
-  for (auto& p : pats)
-    for (unsigned char c : p.first) used.insert(c);
-  for (unsigned char c : used) cls_of[c] = nc++;
-  for (int b = 'A'; b <= 'Z'; b++) cls_of[b] = cls_of[b + 32];
-  for (int b = 0; b < 256; b++) out->cmap[b] = uint8_t(cls_of[b]);
-  out->cmap[0xC4] = kClsFoldI;
-  out->cmap[0xE2] = kClsFoldK;
-  out->cmap[0xC5] = kClsFoldS;
-  if (nc >= 0xFD) {
-    *err = "too many distinct keyword/anchor characters";
-    return false;
-  }
-  // trie
-  std::vector<std::vector<int>> go;
-  std::vector<std::vector<uint32_t>> outs;
-  go.push_back(std::vector<int>(nc, -1));
-  outs.push_back({});
-  uint32_t maxlen = 0;
-  for (auto& p : pats) {
-    int s = 0;
-    for (unsigned char c : p.first) {
-      int k = cls_of[c];
-      if (go[s][k] < 0) {
-        go[s][k] = int(go.size());
-        go.push_back(std::vector<int>(nc, -1));
-        outs.push_back({});
-      }
-      s = go[s][k];
-    }
-    outs[s].push_back(p.second);
-    maxlen = std::max<uint32_t>(maxlen, uint32_t(p.first.size()));
-  }
-  size_t ns = go.size();
-  if (ns >= 0x8000) {
-    *err = "keyword automaton too large (" + std::to_string(ns) + " states)";
-    return false;
-  }
-  std::vector<int> fail(ns, 0);
-  std::deque<int> q;
-  for (int k = 0; k < nc; k++) {
-    if (go[0][k] < 0) go[0][k] = 0;
-    else {
-      fail[go[0][k]] = 0;
-      q.push_back(go[0][k]);
-    }
-  }
-  while (!q.empty()) {
-    int u = q.front();
-    q.pop_front();
-    for (int k = 0; k < nc; k++) {
-      int v = go[u][k];
-      if (v >= 0) {
-        fail[v] = go[fail[u]][k];
-        for (uint32_t o : outs[fail[v]]) outs[v].push_back(o);
-        q.push_back(v);
-      } else {
-        go[u][k] = go[fail[u]][k];
-      }
-    }
-  }
-  out->n_states = uint32_t(ns);
-  out->n_classes = uint32_t(nc);
-  out->max_pat_len = maxlen;
-  out->trans.assign(ns * nc, 0);
-  for (size_t s = 0; s < ns; s++)
-    for (int k = 0; k < nc; k++) {
-      int v = go[s][k];
-      out->trans[s * nc + k] = uint16_t(v | (outs[v].empty() ? 0 : kAcOutFlag));
-    }
-  out->out_off.assign(ns + 1, 0);
-  for (size_t s = 0; s < ns; s++) {
-    auto& o = outs[s];
-    std::sort(o.begin(), o.end());
-    o.erase(std::unique(o.begin(), o.end()), o.end());
-    out->out_off[s + 1] = out->out_off[s] + uint32_t(o.size());
-    out->out_items.insert(out->out_items.end(), o.begin(), o.end());
-  }
-  return true;
-}
 // ---------------------------------------------------------------------------
 // prefilter items
 // ---------------------------------------------------------------------------
@@ -893,7 +762,6 @@ std::vector<std::string> RequiredLiterals(const Regex& re) {
 
 bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err) {
   std::map<std::string, uint32_t> kw_ids;
-  std::vector<std::pair<std::string, uint32_t>> pats;
   out->rules.clear();
   out->regex.clear();
   for (size_t ri = 0; ri < src.size(); ri++) {
@@ -982,37 +850,10 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
           uint32_t aid = uint32_t(out->anchors.size());
           AnchorInfo ai{};
           ai.rule = uint32_t(ri);
-          ai.lit_len = uint16_t(l.size());
+          ai.lit_len = uint32_t(l.size());
           ai.off_lo = int32_t(best.olo);
           ai.off_hi = int32_t(best.ohi);
           ai.off_hi_fold = int32_t(std::min<int64_t>(best.ohi_fold, 1 << 30));
-          std::vector<bool> la_ascii;
-          auto la = Lookahead(re->nodes(), best.follow[li], &la_ascii);
-          ai.la_n = uint8_t(la.size());
-          for (size_t q = 0; q < la.size(); q++) {
-            size_t id = 0;
-            for (; id < out->la_masks.size() / 2; id++)
-              if (out->la_masks[2 * id] == la[q].first && out->la_masks[2 * id + 1] == la[q].second) break;
-            if (id == out->la_masks.size() / 2) {
-              out->la_masks.push_back(la[q].first);
-              out->la_masks.push_back(la[q].second);
-            }
-            ai.la_cls[q] = uint8_t(id);
-          }
-          // weak (short) anchors: let the automaton match the first mandatory
-          // ASCII-only class after the literal too (patterns lit+c, c in class)
-          std::vector<char> ext_chars;
-          if (!la.empty() && la_ascii[0]) {
-            for (int b = 0; b < 128; b++) {
-              bool in = ((b < 64 ? la[0].first : la[0].second) >> (b & 63)) & 1;
-              if (!in) continue;
-              char lc = char((b >= 'A' && b <= 'Z') ? b + 32 : b);
-              if (std::find(ext_chars.begin(), ext_chars.end(), lc) == ext_chars.end()) ext_chars.push_back(lc);
-            }
-            // short literals take any class up to 40 chars; longer ones only small classes
-            if (ext_chars.size() > (l.size() <= 3 ? 40u : 4u)) ext_chars.clear();
-          }
-          ai.ext = ext_chars.empty() ? 0 : 1;
           out->anchors.push_back(ai);
           {  // prefilter item: prefix sets + literal sets (union over same-folded variants) + lookahead sets
             FilterItem fi;
@@ -1038,12 +879,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
             fi.sets.insert(fi.sets.end(), after.begin(), after.end());
             out->items.push_back(std::move(fi));
           }
-          if (ext_chars.empty()) {
-            pats.push_back({l, kOutAnchor | aid});
-          } else {
-            for (char ch : ext_chars) pats.push_back({l + std::string(1, ch), kOutAnchor | aid});
-          }
-          desc += " " + l + (ai.ext ? "*" : "") + (la.empty() ? "" : "+" + std::to_string(la.size()));
+          desc += " " + l;
         }
       } else {
         rg.anchored = 0;
@@ -1077,7 +913,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     if (!BuildFilter(out->items, nw, nb, ft.get(), err)) return false;
     out->filter = ft;
   }
-  return BuildAc(pats, out, err);
+  return true;
 }
 
 }  // namespace tsg

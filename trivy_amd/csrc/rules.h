@@ -6,8 +6,9 @@
 //     and, per rule, the keyword ids whose presence enables it;
 //   * one anchor per rule: a set of ASCII literals every match contains, at a
 //     bounded byte offset [off_lo, off_hi] from the match start;
-//   * one case-folded Aho-Corasick DFA over keywords ∪ anchor literals ∪ the
-//     three fold-special UTF-8 sequences (U+0130, U+212A, U+017F);
+//   * the streaming prefilter's items (byte-set sequences around each anchor
+//     literal, keywords that need GPU bits, the fold runes U+0130 / U+212A /
+//     U+017F), bucketed into shift-or tables by filter.cpp;
 //   * a relaxed, byte-level "extended shift-and" NFA per rule whose language is
 //     a superset of the rule regex (captures dropped, assertions -> ε,
 //     alternations -> column unions / class runs, large repeats -> unbounded).
@@ -22,13 +23,6 @@
 
 namespace tsg {
 
-constexpr uint32_t kAcOutFlag = 0x8000;  // transition entry: target state has outputs
-constexpr uint8_t kClsFoldI = 0xFD;     // byte 0xC4 (maybe U+0130 -> 'i')
-constexpr uint8_t kClsFoldK = 0xFE;     // byte 0xE2 (maybe U+212A -> 'k')
-constexpr uint8_t kClsFoldS = 0xFF;     // byte 0xC5 (maybe U+017F, barrier)
-constexpr uint32_t kOutKeyword = 0u << 28;
-constexpr uint32_t kOutAnchor = 1u << 28;
-constexpr uint32_t kOutSpecial = 2u << 28;
 constexpr int kMaxNfaWords = 4;
 
 enum GateMode : uint8_t {
@@ -49,14 +43,11 @@ struct RuleSrc {
   std::vector<std::string> keywords;
 };
 
-struct AnchorInfo {
+struct AnchorInfo {  // mirrored on the device
   uint32_t rule;
-  uint16_t lit_len;
-  uint8_t la_n;            // mandatory classes checked right after the literal (0..4)
-  uint8_t ext;             // leading lookahead positions already matched by the automaton
+  uint32_t lit_len;
   int32_t off_lo, off_hi;  // literal start - match start, in bytes (non-special files)
   int32_t off_hi_fold;     // the same when U+212A/U+017F/U+0130 may occur (special files)
-  uint8_t la_cls[4];       // indices into CompiledRules::la_masks
 };
 
 struct RuleGpu {  // mirrored on the device
@@ -85,16 +76,9 @@ struct FilterItem {
 };
 
 struct CompiledRules {
-  // Aho-Corasick
-  uint32_t n_states = 0, n_classes = 0, max_pat_len = 0;
-  uint8_t cmap[256];
-  std::vector<uint16_t> trans;     // n_states * n_classes
-  std::vector<uint32_t> out_off;   // n_states + 1
-  std::vector<uint32_t> out_items; // kOut* | id
   // keywords / anchors
   std::vector<std::string> keywords;  // unique lowercased ASCII keywords
   std::vector<AnchorInfo> anchors;
-  std::vector<uint64_t> la_masks;  // per lookahead class: 2 x u64 ASCII membership
   // rules
   std::vector<RuleGpu> rules;
   std::vector<uint32_t> rule_kw;  // keyword ids

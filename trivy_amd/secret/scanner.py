@@ -53,9 +53,10 @@ class _CStats(c.Structure):
 
 
 class _CTableInfo(c.Structure):
-    _fields_ = [(n, c.c_uint32) for n in ("n_rules", "n_keywords", "n_anchors", "ac_states", "ac_classes",
-                                          "max_pattern_len", "n_fullscan_rules", "nfa_words_total")] + \
-               [("ac_table_bytes", c.c_uint64)]
+    _fields_ = [(n, c.c_uint32) for n in ("n_rules", "n_keywords", "n_anchors", "n_filter_items",
+                                          "n_filter_buckets", "filter_window", "n_fullscan_rules",
+                                          "nfa_words_total")] + \
+               [("filter_table_bytes", c.c_uint64), ("filter_est_fp", c.c_double)]
 
 
 def _declare(L):
