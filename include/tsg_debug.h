@@ -21,6 +21,10 @@ int tsg_regex_find_all(const char* pattern, const uint8_t* text, uint64_t n, int
                        const int64_t* windows, uint32_t n_windows, int64_t* out, uint64_t out_cap,
                        uint64_t* out_len, int32_t* num_cap);
 
+/* Engine selection for the exact pass's FindAll (tests only; process-wide):
+ * 0 auto (bit-state backtracker, Pike VM past its row budget), 1 Pike VM only,
+ * 2 backtracker with an 8-position budget (exercises the fallback). */
+void tsg_debug_regex_engine(int mode);
 /* regexp.MatchString: 1 = match, 0 = no match, <0 = compile error. */
 int tsg_regex_match(const char* pattern, const uint8_t* text, uint64_t n);
 

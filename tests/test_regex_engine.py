@@ -120,3 +120,26 @@ def test_compile_errors_agree():
             GoRegexp(p)
         with pytest.raises(ValueError):
             _lib.regex_find_all(p, b"abc")
+
+
+@pytest.mark.parametrize("idx", range(4))
+def test_backtracker_equals_pike_vm(idx):
+    """The bit-state backtracker, the Pike VM and the backtracker falling back to
+    the Pike VM mid-search (8-position budget) give the same FindAll result,
+    whole-text and windowed, for every builtin and golden custom regex."""
+    rng = random.Random(7000 + idx)
+    L = _lib.lib()
+    try:
+        for pat in PATTERNS + [r"(a|)+", r"(a*)+$", r"(?:(a)|b)*c"]:
+            text = _text(rng, [pat], n_parts=12)
+            wins = None
+            if rng.random() < 0.5 and text:
+                pts = sorted(rng.randrange(len(text)) for _ in range(6))
+                wins = [(pts[k], pts[k + 1]) for k in range(0, 6, 2)]
+            res = []
+            for mode in (0, 1, 2):
+                L.tsg_debug_regex_engine(mode)
+                res.append(_lib.regex_find_all(pat, text, submatch=True, windows=wins))
+            assert res[0] == res[1] == res[2], (pat, text, wins)
+    finally:
+        L.tsg_debug_regex_engine(0)

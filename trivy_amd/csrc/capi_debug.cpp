@@ -1,12 +1,14 @@
 // C-ABI for host-logic inspection (include/tsg_debug.h).
 #include "tsg_debug.h"
 
+#include <atomic>
 #include <cstring>
 #include <string>
 
 #include "goregex.h"
 
 namespace tsg {
+extern std::atomic<int> g_regex_engine;
 thread_local std::string g_last_error;
 void SetError(const std::string& e) { g_last_error = e; }
 }  // namespace tsg
@@ -33,6 +35,8 @@ int tsg_regex_find_all(const char* pattern, const uint8_t* text, uint64_t n, int
   std::memcpy(out, res.data(), sizeof(int64_t) * (res.size() < out_cap ? res.size() : out_cap));
   return 0;
 }
+
+void tsg_debug_regex_engine(int mode) { tsg::g_regex_engine.store(mode); }
 
 int tsg_regex_match(const char* pattern, const uint8_t* text, uint64_t n) {
   std::string err;

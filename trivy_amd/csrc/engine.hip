@@ -67,12 +67,16 @@ __device__ __forceinline__ void wave_sync() {
 constexpr int kFLane = 64;           // bytes per lane per tile (4 blocks of 16 B)
 constexpr int kFBlocks = kFLane / 16;
 constexpr int kFTile = 64 * kFLane;  // 4 KiB per wave tile
-constexpr int kFQueue = 64 + 64 * kFBlocks;  // per-wave flagged-block queue (flushed at >= 64 after a tile)
+constexpr int kFFlushAt = 256;                      // flush the flagged-block queue at >= this many
+constexpr int kFQueue = kFFlushAt + 64 * kFBlocks;  // per-wave queue entries
+constexpr int kFChunks = kFTile / 1024;             // newline chunks per tile (kChunk = 1 KiB)
+constexpr int kFNlTiles = 64;                       // tiles whose newline counts a wave stages in LDS
 constexpr int kFWindow = 6;          // filter window: a fire stays visible for 9 - 6 = 3 bytes
 constexpr int kFWords = 4;           // 16 buckets = 4 u32 registers of 8 slots x 4 buckets
 constexpr uint32_t kFireBits = 0xFFF00000u;  // slots 5..7 of a register
 constexpr uint32_t kNlBits = 0x8888u;        // newline bucket (15 = register 3, lane 3), slots 0..3
 static_assert(kChunk % kFLane == 0 && kChunk / kFLane <= 64, "a newline chunk must be whole lane chunks");
+static_assert(kFChunks * kChunk == kFTile && kFChunks == 4, "a tile's newline counts are one u64");
 
 struct FilterParams {
   const uint8_t* arena;
@@ -92,11 +96,14 @@ __device__ __forceinline__ uint4 reach_read(const uint8_t* sb, uint32_t w, uint3
   return *reinterpret_cast<const uint4*>(sb + __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + k) << 8)));
 }
 
-__device__ __forceinline__ void reach_apply(const uint4& m, uint32_t* st) {  // R = R << 4 | m, per register
-  st[0] = (st[0] << 4) | m.x;
-  st[1] = (st[1] << 4) | m.y;
-  st[2] = (st[2] << 4) | m.z;
-  st[3] = (st[3] << 4) | m.w;
+// R = R << 4 | m, per register: one v_lshl_or_b32 each.  Written as asm so the
+// compiler keeps the serial chain instead of re-associating it into shifted
+// copies of the table words (which costs ~1.6x the VALU instructions).
+__device__ __forceinline__ void reach_apply(const uint4& m, uint32_t* st) {
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(st[0]) : "v"(st[0]), "v"(m.x));
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(st[1]) : "v"(st[1]), "v"(m.y));
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(st[2]) : "v"(st[2]), "v"(m.z));
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(st[3]) : "v"(st[3]), "v"(m.w));
 }
 
 // '\n' bytes in a word: x = w ^ 0x0A.. is zero exactly in newline bytes; bit 7
@@ -130,12 +137,15 @@ __device__ __forceinline__ void load_reach_lds(uint8_t* s_reach, const uint32_t*
 __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
   __shared__ uint32_t s_queue[kScanWaves * kFQueue];
+  __shared__ uint64_t s_nl[kScanWaves * kFNlTiles];  // per wave: the last tiles' 4 chunk counts
   const int tid = threadIdx.x;
   load_reach_lds(s_reach, P.reach, 16, tid, blockDim.x);
   __syncthreads();
   const uint32_t lane = tid & 63, wave = tid >> 6;
   const uint32_t laneoff = (lane & 15) * 16;
   uint32_t* Q = s_queue + wave * kFQueue;
+  uint64_t* NL = s_nl + wave * kFNlTiles;
+  uint32_t nl_slots = 0;  // wave-uniform: tiles staged in NL
   uint32_t qn = 0;  // wave-uniform
   const uint64_t n_tiles = (P.n_bytes + kFTile - 1) / kFTile;
   const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
@@ -149,7 +159,10 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
       const uint64_t p = b0 + 16 * j;
       dst[j] = load16(P.arena + (p < P.n_bytes ? p : 0));
     }
-    if (lane == 0 && tt > 0) *pv = *reinterpret_cast<const uint2*>(P.arena + tt * kFTile - 8);
+    // the 8 bytes before the tile (lane 0's prefix): a uniform address, so one
+    // request; unconditional like the block loads, so the loads in flight stay
+    // a static count and the chain waits only for the current tile's.
+    *pv = *reinterpret_cast<const uint2*>(P.arena + (tt > 0 ? tt * kFTile - 8 : 0));
   };
   auto flush = [&]() {  // wave-uniform
     uint32_t base = 0;
@@ -161,9 +174,20 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     }
     qn = 0;
   };
+  // Global stores are rare on purpose: on gfx9 a store counts in vmcnt like
+  // the loads, so a store per tile would make the next tile's wait for its
+  // prefetched data also wait for the store's completion.
+  auto flush_nl = [&](uint64_t t_last) {  // wave-uniform; staged tiles are t_last - (nl_slots-1-i) * n_waves
+    wave_sync();
+    if (lane < nl_slots) {
+      const uint64_t tt = t_last - uint64_t(nl_slots - 1 - lane) * n_waves;
+      reinterpret_cast<uint64_t*>(P.nl)[tt] = NL[lane];  // chunks 4tt .. 4tt+3 (buffer padded past the end)
+    }
+    nl_slots = 0;
+  };
   if (t < n_tiles) load_tile(cur, &pre, t);
   for (; t < n_tiles; t += n_waves) {
-    if (t + n_waves < n_tiles) load_tile(nxt, &pnx, t + n_waves);
+    load_tile(nxt, &pnx, t + n_waves < n_tiles ? t + n_waves : t);  // past the end: a harmless reload
     const uint64_t b0 = t * kFTile + uint64_t(lane) * kFLane;
     if (b0 + kFLane > P.n_bytes) {  // bytes past the arena end (last tile only) are zeroed
 #pragma unroll
@@ -182,8 +206,8 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     // the previous 8 bytes: lane l-1's last two words (lane 0: the extra load)
     uint32_t p0 = __shfl(cur[kFBlocks - 1].z, int(lane) - 1), p1 = __shfl(cur[kFBlocks - 1].w, int(lane) - 1);
     if (lane == 0) {
-      p0 = pre.x;
-      p1 = pre.y;
+      p0 = t > 0 ? pre.x : 0u;
+      p1 = t > 0 ? pre.y : 0u;
     }
     uint32_t flagged = 0, nl = 0;
     if (P.diag_mode < 2) {
@@ -213,7 +237,9 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     }
 #pragma unroll
     for (int x = 1; x < int(kChunk / kFLane); x <<= 1) nl += __shfl_xor(nl, x);
-    if ((lane & (kChunk / kFLane - 1)) == 0 && b0 < P.n_bytes) P.nl[b0 / kChunk] = uint16_t(nl);
+    if ((lane & (kChunk / kFLane - 1)) == 0)
+      reinterpret_cast<uint16_t*>(NL + nl_slots)[lane / (kChunk / kFLane)] = uint16_t(nl);
+    if (++nl_slots == kFNlTiles) flush_nl(t);
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
       const bool fj = (flagged >> j) & 1u;
@@ -225,12 +251,13 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
         qn += uint32_t(__popcll(m));
       }
     }
-    if (qn >= 64) flush();
+    if (qn >= kFFlushAt) flush();
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) cur[j] = nxt[j];
     pre = pnx;
   }
   if (qn) flush();
+  if (nl_slots) flush_nl(t - n_waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -964,7 +991,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   if (rec_cap_ == 0) rec_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 128, 1 << 16), 1u << 30));
   if (fold_cap_ == 0) fold_cap_ = 1 << 16;
   for (int attempt = 0; attempt < 8; attempt++) {
-    if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, n_chunks * 2) ||
+    if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, (n_chunks + 8) * 2) ||
         !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
         !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
         !Ensure(&d_folds_, &cap_folds_, size_t(fold_cap_) * sizeof(FoldSite)) ||

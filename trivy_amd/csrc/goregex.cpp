@@ -5,6 +5,7 @@
 #include "goregex.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 
 namespace tsg {
@@ -854,6 +855,10 @@ class Compiler {
         uint32_t i = Emit(kIRune);
         re_->prog_[i].cls = int(re_->classes_.size());
         re_->classes_.push_back(n.ranges);
+        std::pair<uint64_t, uint64_t> a{0, 0};
+        for (uint32_t c = 0; c < 128; c++)
+          if (InRanges(n.ranges, c)) (c < 64 ? a.first : a.second) |= uint64_t(1) << (c & 63);
+        re_->class_ascii_.push_back(a);
         return {i, {i << 1}, false};
       }
       case NodeOp::Assert: {
@@ -1048,6 +1053,7 @@ class Machine {
     q->dense.clear();
   }
 
+  friend class Backtracker;
   static uint8_t Context(const uint8_t* s, int64_t n, int64_t pos) {
     int32_t r1 = -1, r2 = -1;
     if (pos > 0 && pos <= n) {
@@ -1100,15 +1106,7 @@ class Machine {
     return t;
   }
 
-  bool MatchRune(const Inst& in, int32_t c) const {
-    switch (in.op) {
-      case kIRune1: return c == int32_t(in.rune);
-      case kIRune: return c >= 0 && InRanges(re_->classes_[in.cls], uint32_t(c));
-      case kIAny: return c >= 0;
-      case kIAnyNotNL: return c >= 0 && c != '\n';
-      default: return false;
-    }
-  }
+  bool MatchRune(const Inst& in, int32_t c) const { return re_->RuneMatch(in, c); }
 
   void Step(Queue* runq, Queue* nextq, int64_t pos, int64_t nextpos, int32_t c, uint8_t nextcond) {
     for (size_t j = 0; j < runq->dense.size(); j++) {
@@ -1137,6 +1135,189 @@ class Machine {
   }
 };
 
+bool Regex::RuneMatch(const Inst& in, int32_t c) const {
+  switch (in.op) {
+    case kIRune1: return c == int32_t(in.rune);
+    case kIRune:
+      if (c < 0) return false;
+      if (c < 128) {
+        const auto& a = class_ascii_[in.cls];
+        return ((c < 64 ? a.first : a.second) >> (c & 63)) & 1;
+      }
+      return InRanges(classes_[in.cls], uint32_t(c));
+    case kIAny: return c >= 0;
+    case kIAnyNotNL: return c >= 0 && c != '\n';
+    default: return false;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Bit-state backtracker (regexp/backtrack.go): depth-first in priority order
+// from each allowed start position in turn, each (pc, pos) explored at most
+// once per search (a state that failed from an earlier start fails again).
+// The first Match reached is the leftmost-first match, as in the Pike VM.
+// The visited bits are rows of |prog| bits per text position from `base_`,
+// cleared lazily as the furthest position grows (paths only move forward), so
+// a search costs what it touches, not the file length.  Above kMaxRows
+// positions it gives up and the caller runs the Pike VM instead.
+// ---------------------------------------------------------------------------
+std::atomic<int> g_regex_engine{0};  // tests: 0 auto, 1 Pike VM only, 2 backtracker with an 8-row budget
+
+class Backtracker {
+ public:
+  static constexpr int64_t kMaxRows = 1 << 16;
+  int64_t max_rows_ = kMaxRows;
+
+  // Same contract as Machine::Search (returns the match in cap()).  *overflow:
+  // the search needed more than kMaxRows positions; the result is invalid.
+  bool Search(const Regex* re, const uint8_t* s, int64_t n, int64_t pos, const std::vector<Window>* wins, int ncap,
+              bool* overflow) {
+    re_ = re;
+    s_ = s;
+    n_ = n;
+    ncap_ = ncap;
+    overflow_ = false;
+    stride_ = (re->prog_.size() + 63) / 64;
+    cap_.assign(size_t(ncap > 0 ? ncap : 1), -1);
+    matchcap_.assign(size_t(ncap > 0 ? ncap : 1), -1);
+    top_ = -1;  // no rows yet
+    const bool anchored = re->anchored_begin_;
+    size_t wi = 0;
+    for (;;) {
+      if (wins) {
+        while (wi < wins->size() && (*wins)[wi].hi < pos) wi++;
+        if (wi >= wins->size()) break;
+        if ((*wins)[wi].lo > pos) {
+          const int64_t t = Machine::Align(s, n, (*wins)[wi].lo);
+          if (t > pos) pos = t;
+        }
+      }
+      const bool allowed = !wins || (*wins)[wi].lo <= pos;
+      if (anchored && pos != 0) break;
+      if (allowed) {
+        if (top_ < pos) Rebase(pos);  // states before pos are unreachable from here on
+        if (ncap_ > 0) cap_[0] = pos;
+        if (Try(re->start_, pos)) return true;
+        if (overflow_) {
+          *overflow = true;
+          return false;
+        }
+      }
+      if (pos >= n) break;
+      pos += DecodeRune(s, n, pos).width;
+    }
+    return false;
+  }
+  const std::vector<int64_t>& cap() const { return matchcap_; }
+
+ private:
+  struct Job {
+    uint32_t pc;
+    bool arg;
+    int64_t pos;  // capture-restore jobs: the saved capture value
+  };
+  const Regex* re_ = nullptr;
+  const uint8_t* s_ = nullptr;
+  int64_t n_ = 0;
+  int ncap_ = 0;
+  bool overflow_ = false;
+  size_t stride_ = 1;  // u64 words per position row
+  int64_t base_ = 0, top_ = -1;  // rows [base_, top_] are cleared / in use
+  std::vector<uint64_t> visited_;
+  std::vector<Job> jobs_;
+  std::vector<int64_t> cap_, matchcap_;
+
+  void Rebase(int64_t pos) {
+    base_ = pos;
+    top_ = pos - 1;
+  }
+  bool ShouldVisit(uint32_t pc, int64_t pos) {
+    if (pos > top_) {
+      if (pos - base_ >= max_rows_) {
+        overflow_ = true;
+        return false;
+      }
+      const size_t need = size_t(pos - base_ + 1) * stride_;
+      if (visited_.size() < need) visited_.resize(std::max(need, visited_.size() * 2));
+      std::fill(visited_.begin() + ptrdiff_t(size_t(top_ + 1 - base_) * stride_), visited_.begin() + ptrdiff_t(need),
+                uint64_t(0));
+      top_ = pos;
+    }
+    uint64_t& w = visited_[size_t(pos - base_) * stride_ + (pc >> 6)];
+    const uint64_t bit = uint64_t(1) << (pc & 63);
+    if (w & bit) return false;
+    w |= bit;
+    return true;
+  }
+  void Push(uint32_t pc, int64_t pos, bool arg) {
+    if (re_->prog_[pc].op != kIFail && (arg || ShouldVisit(pc, pos))) jobs_.push_back({pc, arg, pos});
+  }
+  bool Try(uint32_t pc0, int64_t pos0) {
+    const std::vector<Inst>& prog = re_->prog_;
+    jobs_.clear();
+    Push(pc0, pos0, false);
+    while (!jobs_.empty()) {
+      if (overflow_) return false;
+      const Job j = jobs_.back();
+      jobs_.pop_back();
+      uint32_t pc = j.pc;
+      int64_t pos = j.pos;
+      bool arg = j.arg;
+      goto skip;
+    check:
+      if (!ShouldVisit(pc, pos)) continue;
+    skip : {
+      const Inst& in = prog[pc];
+      switch (in.op) {
+        case kIFail: continue;
+        case kIAlt:
+          if (arg) {  // finished in.out; try in.arg
+            arg = false;
+            pc = in.arg;
+          } else {
+            Push(pc, pos, true);
+            pc = in.out;
+          }
+          goto check;
+        case kIRune:
+        case kIRune1:
+        case kIAny:
+        case kIAnyNotNL: {
+          const Rune r = DecodeRune(s_, n_, pos);
+          if (!re_->RuneMatch(in, r.r)) continue;
+          pos += r.width;
+          pc = in.out;
+          goto check;
+        }
+        case kICapture:
+          if (arg) {  // restore the saved value
+            cap_[in.arg] = pos;
+            continue;
+          }
+          if (int(in.arg) < ncap_) {
+            jobs_.push_back({pc, true, cap_[in.arg]});
+            cap_[in.arg] = pos;
+          }
+          pc = in.out;
+          goto check;
+        case kIEmpty:
+          if ((in.empty & ~Machine::Context(s_, n_, pos)) != 0) continue;
+          pc = in.out;
+          goto check;
+        case kINop:
+          pc = in.out;
+          goto check;
+        case kIMatch:
+          if (ncap_ > 1) cap_[1] = pos;
+          matchcap_ = cap_;
+          return true;
+      }
+    }
+    }
+    return false;
+  }
+};
+
 bool Regex::Match(const uint8_t* s, int64_t n) const {
   Machine m(this, 0);
   return m.Search(s, n, 0, nullptr);
@@ -1145,11 +1326,24 @@ bool Regex::Match(const uint8_t* s, int64_t n) const {
 void Regex::FindAll(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
                     std::vector<int64_t>* out) const {
   int ncap = submatch ? 2 * (num_cap_ + 1) : 2;
-  Machine m(this, ncap);
+  thread_local Backtracker bt;
+  const int mode = g_regex_engine.load(std::memory_order_relaxed);
+  bt.max_rows_ = mode == 2 ? 8 : Backtracker::kMaxRows;
+  std::unique_ptr<Machine> m;  // only when the backtracker's row budget runs out
+  if (mode == 1) m.reset(new Machine(this, ncap));
   int64_t pos = 0, prev_end = -1;
   while (pos <= n) {
-    if (!m.Search(s, n, pos, wins)) break;
-    const auto& c = m.cap();
+    bool overflow = false;
+    const std::vector<int64_t>* cp;
+    if (!m && bt.Search(this, s, n, pos, wins, ncap, &overflow)) {
+      cp = &bt.cap();
+    } else {
+      if (!overflow && !m) break;
+      if (!m) m.reset(new Machine(this, ncap));
+      if (!m->Search(s, n, pos, wins)) break;
+      cp = &m->cap();
+    }
+    const auto& c = *cp;
     bool accept = true;
     if (c[1] == pos) {  // empty match
       if (c[0] == prev_end) accept = false;

@@ -5,7 +5,9 @@
 // scoped (?imsU) flags, simplification of counted repeats, the Thompson
 // program layout (Alt priorities, (x+)? for nullable stars) and the
 // leftmost-first Pike VM with submatches over UTF-8 runes (invalid byte ->
-// U+FFFD width 1).  FindAll follows (*Regexp).allMatches (empty-match rules).
+// U+FFFD width 1), and the bit-state backtracker Go uses on small inputs
+// (regexp/backtrack.go; same leftmost-first result).  FindAll follows
+// (*Regexp).allMatches (empty-match rules).
 //
 // Extension for the GPU pipeline: FindAll can be restricted to a sorted list
 // of start windows (the GPU's candidate windows).  A thread is only started at
@@ -86,6 +88,8 @@ class Regex {
   friend class Parser;
   friend class Compiler;
   friend class Machine;
+  friend class Backtracker;
+  bool RuneMatch(const Inst& in, int32_t c) const;
   std::string pattern_;
   std::vector<Node> nodes_;
   int root_ = -1;
@@ -93,6 +97,7 @@ class Regex {
   std::vector<std::string> cap_names_;
   std::vector<Inst> prog_;
   std::vector<RuneRanges> classes_;
+  std::vector<std::pair<uint64_t, uint64_t>> class_ascii_;  // ASCII membership bitmap per class
   uint32_t start_ = 0;
   bool anchored_begin_ = false;  // program begins with \A (startCond has EmptyBeginText)
 };

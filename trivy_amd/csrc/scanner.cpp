@@ -451,18 +451,24 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 }
 }  // namespace
 
+// Host-tail phase profile (TSG_TAIL_DEBUG=1 only; otherwise the timers are inert).
+const bool g_tail_debug = std::getenv("TSG_TAIL_DEBUG") != nullptr;
 std::atomic<int64_t> g_prof[8];
 struct PhaseTimer {
   int k;
   std::chrono::steady_clock::time_point t0;
-  explicit PhaseTimer(int kk) : k(kk), t0(std::chrono::steady_clock::now()) {}
+  explicit PhaseTimer(int kk) : k(kk) {
+    if (g_tail_debug) t0 = std::chrono::steady_clock::now();
+  }
   ~PhaseTimer() {
-    g_prof[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (g_tail_debug)
+      g_prof[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   }
 };
 
 void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
                              const Candidate* c, size_t nc, FileResult* out) const {
+  PhaseTimer pt_all(7);
   const uint8_t* P = reinterpret_cast<const uint8_t*>(path.data());
   std::vector<std::pair<uint32_t, Loc>> matched;
   std::vector<Loc> censor;
@@ -526,12 +532,27 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       PhaseTimer pt(1);
       bool hit = false;
       for (size_t k = 0; k + stride <= m.size() && !hit; k += stride) {
-        std::string ml = GoBytesToLower(content + m[k], size_t(m[k + 1] - m[k]));
-        for (auto& kw : R.kw_lower_host)
-          if (ml.find(kw) != std::string::npos) {
+        const uint8_t* ms = content + m[k];
+        const size_t mn = size_t(m[k + 1] - m[k]);
+        // ASCII keywords in a match without U+0130 / U+212A: the ASCII
+        // case-insensitive search is exact (see the whole-content case below)
+        const bool fold = HasSeq(ms, mn, "\xC4\xB0", 2) || HasSeq(ms, mn, "\xE2\x84\xAA", 3);
+        bool go = fold;
+        for (auto& kw : R.kw_lower_host) {
+          if (!IsAsciiStr(kw)) go = true;
+          else if (!fold && AsciiCaseContains(ms, mn, kw)) {
             hit = true;
             break;
           }
+        }
+        if (!hit && go) {
+          std::string ml = GoBytesToLower(ms, mn);
+          for (auto& kw : R.kw_lower_host)
+            if (ml.find(kw) != std::string::npos) {
+              hit = true;
+              break;
+            }
+        }
       }
       // GPU keyword bits (ASCII occurrences anywhere in the file) and the
       // file's U+0130/U+212A flag, when the candidates carry them
@@ -582,6 +603,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       if (!hit) continue;
     }
     std::vector<Loc> locs;
+    PhaseTimer pt5(5);
     for (size_t k = 0; k + stride <= m.size(); k += stride) {
       int64_t s = m[k], e = m[k + 1];
       if (AllowRulesAllow(allow_, content + s, size_t(e - s)) ||
@@ -624,13 +646,19 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     }
     spans.swap(m);
   }
-  auto censored = [&](int64_t a, int64_t b) {
-    std::string s(reinterpret_cast<const char*>(content + a), size_t(b - a));
-    for (auto& cz : spans) {
-      int64_t x = std::max(a, cz.s), y = std::min(b, cz.e);
-      for (int64_t p = x; p < y; p++) s[size_t(p - a)] = '*';
+  auto first_span_after = [&](int64_t a) {  // first span with e > a (spans are disjoint and sorted)
+    return size_t(std::upper_bound(spans.begin(), spans.end(), a, [](int64_t v, const Loc& z) { return v < z.e; }) -
+                  spans.begin());
+  };
+  FileFindings& ff = out->findings;
+  auto put_censored = [&](int64_t a, int64_t b) {  // content [a, b) with censored bytes as '*', into ff.text
+    const uint32_t at = uint32_t(ff.text.size());
+    ff.text.append(reinterpret_cast<const char*>(content + a), size_t(b - a));
+    for (size_t k = first_span_after(a); k < spans.size() && spans[k].s < b; k++) {
+      int64_t x = std::max(a, spans[k].s), y = std::min(b, spans[k].e);
+      if (x < y) std::memset(&ff.text[at + size_t(x - a)], '*', size_t(y - x));
     }
-    return s;
+    return at;
   };
   auto count_nl_raw = [&](int64_t a, int64_t b) {
     int64_t n = 0;
@@ -646,10 +674,18 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   };
   auto censored_nl = [&](int64_t a, int64_t b) {  // '\n' bytes hidden by censoring in [a, b)
     int64_t n = 0;
-    for (auto& z : spans) {
-      int64_t x = std::max(a, z.s), y = std::min(b, z.e);
+    for (size_t k = first_span_after(a); k < spans.size() && spans[k].s < b; k++) {
+      int64_t x = std::max(a, spans[k].s), y = std::min(b, spans[k].e);
       if (x < y) n += count_nl_raw(x, y);
     }
+    return n;
+  };
+  std::vector<int64_t> span_nl(spans.size() + 1, 0);  // '\n' in spans[0 .. i)
+  for (size_t k = 0; k < spans.size(); k++) span_nl[k + 1] = span_nl[k] + count_nl_raw(spans[k].s, spans[k].e);
+  auto censored_nl_before = [&](int64_t pos) {  // censored_nl(0, pos)
+    const size_t k = first_span_after(pos);  // spans [0, k) end at or before pos
+    int64_t n = span_nl[k];
+    if (k < spans.size() && spans[k].s < pos) n += count_nl_raw(spans[k].s, pos);
     return n;
   };
   auto count_nl = [&](int64_t a, int64_t b) { return count_nl_raw(a, b) - censored_nl(a, b); };
@@ -662,7 +698,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       --it;
       raw = it->second + count_nl_raw(it->first, pos);
     }
-    return raw - censored_nl(0, pos);
+    return raw - censored_nl_before(pos);
   };
   auto in_span = [&](int64_t p) -> const Loc* {
     auto it = std::upper_bound(spans.begin(), spans.end(), p, [](int64_t v, const Loc& z) { return v < z.s; });
@@ -697,7 +733,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
 
   out->kind = kHasFindings;
   PhaseTimer pt3(3);
-  FileFindings& ff = out->findings;
+  ff.f.reserve(matched.size());
+  ff.lines.reserve(matched.size() * 5);
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
@@ -710,7 +747,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       mls = (start - ls - 30 < 0) ? ls : start - 30;
       mle = (end + 20 > le) ? le : end + 20;
     }
-    const std::string match_line = censored(mls, mle);
+    const uint32_t ml_off = put_censored(mls, mle), ml_len = uint32_t(mle - mls);
     int64_t end_line_num = start_line_num + count_nl(start, end);
     int64_t code_start = std::max<int64_t>(start_line_num - 2, 0);
     int64_t p = ls;
@@ -722,13 +759,13 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
         int64_t e = line_end_of(p);
         bool in_cause = k >= start_line_num && k <= end_line_num;
         uint32_t off, n;
-        if (e - p > 100 && in_cause) {
-          n = uint32_t(match_line.size());
-          off = ff.Put(match_line);
+        if (e - p > 100 && in_cause) {  // the match line (shared text)
+          n = ml_len;
+          off = ml_off;
         } else {
-          const std::string s = censored(p, e - p > 100 ? p + 100 : e);
-          n = uint32_t(s.size());
-          off = ff.Put(s);
+          const int64_t q = e - p > 100 ? p + 100 : e;
+          n = uint32_t(q - p);
+          off = put_censored(p, q);
         }
         ff.lines.push_back({k + 1, off, n, in_cause, !found_first && in_cause, false});
         found_first = found_first || in_cause;
@@ -749,8 +786,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       f.match_off = ff.Put(m);
       f.match_len = uint32_t(m.size());
     } else {
-      f.match_off = ff.Put(match_line);
-      f.match_len = uint32_t(match_line.size());
+      f.match_off = ml_off;
+      f.match_len = ml_len;
     }
     ff.f.push_back(f);
   }
@@ -851,6 +888,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   size_t nf = starts.size() - 1;
   std::vector<FileResult> tmp(nf);
   for (auto& g : g_prof) g = 0;
+  const double t_sorted = NowMs();
   // largest work first (candidates x file size) so one big file does not finish last
   std::vector<uint32_t> order(nf);
   for (size_t k = 0; k < nf; k++) order[k] = uint32_t(k);
@@ -872,10 +910,14 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string(p, pn), in.binary && in.binary[f], &cands[a],
              b - a, &tmp[k]);
   });
-  if (std::getenv("TSG_TAIL_DEBUG"))
-    std::fprintf(stderr, "tail phases ms: findall %.1f gate %.1f locs %.1f findings %.1f sort %.1f ascii %.1f go %.1f\n",
+  const double t_par = NowMs();
+  if (g_tail_debug)
+    std::fprintf(stderr, "tail serial ms: sort+setup %.1f parallel %.1f\n", t_sorted - t2, t_par - t_sorted);
+  if (g_tail_debug)
+    std::fprintf(stderr, "tail phases ms: findall %.1f gate %.1f blocks %.1f findings %.1f sort %.1f allow-loc %.1f go %.1f "
+                 "scanfile %.1f\n",
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
-                 g_prof[5] / 1e6, g_prof[6] / 1e6);
+                 g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
   for (size_t k = 0; k < nf; k++) {
     if (tmp[k].kind != kHasFindings) continue;
     uint32_t f = cands[starts[k]].file;
@@ -884,6 +926,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     out->found.push_back(std::move(tmp[k].findings));
   }
   double t3 = NowMs();
+  if (g_tail_debug) std::fprintf(stderr, "tail serial ms: collect %.1f\n", t3 - t_par);
   hs->ms_allow = t2 - t1;
   hs->ms_exact = t3 - t2;
   hs->candidates = cands.size();
