@@ -73,6 +73,11 @@ int tsg_debug_host_tail(const struct tsg_global* g, const struct tsg_batch* b, s
 int tsg_debug_host_tail_cands(const struct tsg_global* g, const struct tsg_batch* b, const void* cands,
                               uint64_t n_cands, struct tsg_result** out);
 
+/* A scanner without a GPU engine (tsg_scan on it fails): lets the CPU suite
+ * drive the analyzer's host logic (tsg_analyzer_required, collectors). */
+struct tsg_scanner;
+int tsg_debug_scanner_host_only(const struct tsg_global* g, struct tsg_scanner** out);
+
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);
 

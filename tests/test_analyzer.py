@@ -1,0 +1,223 @@
+"""The secret analyzer around Scan.
+
+CPU: the oracle restatement against the reference's own analyzer tests
+(pkg/fanal/analyzer/secret/secret_test.go, transcribed to tests/golden/), and
+the native ingest logic (IsBinary, ExtractPrintableBytes, CR strip, Required,
+the tar-layer walker packing collectors) against the oracle.
+GPU: Analyze / AnalyzeBatch / AnalyzeLayer end to end vs the oracle.
+"""
+import io
+import json
+import random
+import tarfile
+from pathlib import Path
+
+import pytest
+
+from oracle import analyzer as oan
+from tests.corpus import make_corpus
+from tests.layers import make_layer
+
+G = Path(__file__).resolve().parent / "golden"
+CASES = json.loads((G / "analyzer_cases.json").read_text())
+ADIR = G / "analyzer"
+
+
+def _norm_secret(s):
+    return s.to_dict() if hasattr(s, "to_dict") else s
+
+
+# ---- oracle pinned by the reference's golden tests ------------------------
+@pytest.mark.parametrize("case", CASES["analyze"], ids=[c["name"] for c in CASES["analyze"]])
+def test_oracle_analyze_golden(case, monkeypatch):
+    monkeypatch.chdir(ADIR)
+    a = oan.SecretAnalyzer(case["config"])
+    content = Path(case["file"]).read_bytes()
+    got = a.analyze(case["file"], case["dir"], content)
+    assert got == case["want"]
+
+
+@pytest.mark.parametrize("case", CASES["required"], ids=[c["name"] for c in CASES["required"]])
+def test_oracle_required_golden(case, monkeypatch):
+    monkeypatch.chdir(ADIR)
+    a = oan.SecretAnalyzer("testdata/skip-tests-config.yaml")
+    assert a.required(case["file"], Path(case["file"]).stat().st_size) == case["want"]
+
+
+# ---- native host logic vs the oracle (no GPU) -------------------------------
+def _rand_bytes(rng, n):
+    pool = [b"\r", b"\n", b"\r\n", b"\x00", b"\x07", b"\x0b", b"\x1b", b"\x7f", b"\xa0", b"\xad", b"\xa1",
+            b"\xff", b"abcde", b"hello world", b"\xc4\xb0", b"  ", b"\t"]
+    return b"".join(rng.choice(pool) for _ in range(n))
+
+
+def test_native_transforms_vs_oracle():
+    from trivy_amd.analyzer import ExtractPrintableBytes, IsBinary, StripCR
+    rng = random.Random(5)
+    for i in range(400):
+        b = _rand_bytes(rng, rng.randint(0, 120))
+        if i % 7 == 0:
+            b = b"x" * rng.randint(250, 320) + b  # control bytes past the 300-byte head
+        assert IsBinary(b, len(b)) == oan.is_binary(b, len(b)), b
+        assert ExtractPrintableBytes(b) == oan.extract_printable_bytes(b), b
+        assert StripCR(b) == b.replace(b"\r", b""), b
+    for b in (bytes(range(256)), bytes(range(256)) * 3, b""):
+        assert ExtractPrintableBytes(b) == oan.extract_printable_bytes(b)
+
+
+@pytest.fixture(scope="module")
+def host_analyzer():
+    from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer, SecretScannerOption
+    a = SecretAnalyzer(_host_only=True)
+    a.Init(AnalyzerOptions(SecretScannerOption(str(ADIR / "testdata/skip-tests-config.yaml"))))
+    return a
+
+
+@pytest.mark.parametrize("case", CASES["required"], ids=[c["name"] for c in CASES["required"]])
+def test_native_required_golden(case, monkeypatch):
+    from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer, SecretScannerOption, FileInfo
+    monkeypatch.chdir(ADIR)
+    a = SecretAnalyzer(_host_only=True)
+    a.Init(AnalyzerOptions(SecretScannerOption("testdata/skip-tests-config.yaml")))
+    assert a.Required(case["file"], FileInfo(Path(case["file"]).stat().st_size)) == case["want"]
+
+
+def test_native_required_vs_oracle(host_analyzer):
+    from trivy_amd.analyzer import FileInfo
+    o = oan.SecretAnalyzer(str(ADIR / "testdata/skip-tests-config.yaml"))
+    rng = random.Random(11)
+    parts = ["src", "node_modules", ".git", "test", "tests", "vendor", "a.git", "usr", "share", "doc", "x",
+             "testdata", "examples", "go.mod", "yarn.lock", "node_modules2", ""]
+    names = ["a.go", "go.sum", "x.md", "img.png", "f.tar", "f.tar.gz", "Pipfile.lock", "skip-tests-config.yaml",
+             "main_test.go", "f.", ".env", "noext", "a.pdf", "b.PNG", "c.socket"]
+    paths = ["skip-tests-config.yaml", str(ADIR / "testdata/skip-tests-config.yaml")]
+    for _ in range(600):
+        k = rng.randint(0, 4)
+        paths.append("/".join([rng.choice(parts) for _ in range(k)] + [rng.choice(names)]))
+    for p in paths:
+        for size in (0, 9, 10, 1 << 20):
+            assert host_analyzer.Required(p, FileInfo(size)) == o.required(p, size), (p, size)
+
+
+@pytest.mark.parametrize("fmt", [tarfile.GNU_FORMAT, tarfile.PAX_FORMAT, tarfile.USTAR_FORMAT])
+def test_native_tar_walk_vs_oracle(host_analyzer, fmt):
+    """The collector's batch (scan paths, transformed contents, binary flags) after
+    walking a layer equals the oracle's LayerTar.Walk + Required + Analyze prelude;
+    small arenas force resumption from the cursor."""
+    from trivy_amd.analyzer.secret import Collector, _CTarStats
+    import numpy as np
+    o = oan.SecretAnalyzer(str(ADIR / "testdata/skip-tests-config.yaml"))
+    layer = make_layer(100 + fmt, 150 if fmt != tarfile.USTAR_FORMAT else 0)
+    if fmt == tarfile.USTAR_FORMAT:  # USTAR cannot hold names > 255: build one with prefix-split names
+        buf = io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w", format=fmt) as tf:
+            for i, (p, b) in enumerate(make_corpus(77, 80)):
+                ti = tarfile.TarInfo("usr/share/some/long/prefix/dir/%s/%d/%s" % ("q" * 60, i, p))
+                ti.size = len(b)
+                tf.addfile(ti, io.BytesIO(b))
+        layer = buf.getvalue()
+    want = []
+    files, wh, opq = oan.walk_layer_tar(layer)
+    for fp, size, content in files:
+        if o.required(fp, size):
+            args = o.prepare(fp, "", content)
+            if args is not None:
+                want.append(args)
+    for arena in (1 << 20, 4096):
+        got = []
+        st = _CTarStats()
+        coll = Collector(host_analyzer, arena)
+        cursor = 0
+        buf = np.frombuffer(layer, dtype=np.uint8)
+        while True:
+            rc, cursor = coll.add_tar(buf, cursor, st)
+            got += [coll.file(i) for i in range(coll.files())]
+            coll.reset()
+            if rc == 0:
+                break
+        assert [(p, d, b) for p, d, b in got] == want
+        assert st.whiteouts == wh and st.opaque_dirs == opq
+        assert st.added == len(want)
+
+
+def test_native_tar_malformed(host_analyzer):
+    from trivy_amd.analyzer.secret import Collector, _CTarStats
+    layer = bytearray(make_layer(3, 20))
+    layer[148] ^= 0x01  # checksum of the first header
+    coll = Collector(host_analyzer, 1 << 20)
+    with pytest.raises(ValueError):
+        coll.add_tar(bytes(layer), 0, _CTarStats())
+    good = make_layer(4, 20)
+    with pytest.raises(ValueError):  # truncated mid-entry
+        coll.add_tar(good[:len(good) // 2 + 7], 0, _CTarStats())
+
+
+def test_scan_without_gpu_fails_loudly(host_analyzer):
+    from trivy_amd.analyzer.secret import Collector
+    coll = Collector(host_analyzer, 1 << 16)
+    assert coll.add("a.txt", ".", b"ghp_" + b"a" * 36) == 0
+    with pytest.raises(RuntimeError):
+        coll.submit().wait()
+
+
+# ---- GPU: end to end ------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES["analyze"], ids=[c["name"] for c in CASES["analyze"]])
+def test_gpu_analyze_golden(case, monkeypatch):
+    from trivy_amd.analyzer import AnalysisInput, AnalyzerOptions, FileInfo, SecretAnalyzer, SecretScannerOption
+    monkeypatch.chdir(ADIR)
+    a = SecretAnalyzer()
+    a.Init(AnalyzerOptions(SecretScannerOption(case["config"])))
+    content = Path(case["file"]).read_bytes()
+    got = a.Analyze(AnalysisInput(Dir=case["dir"], FilePath=case["file"], Info=FileInfo(len(content)),
+                                  Content=io.BytesIO(content)))
+    want = case["want"]
+    if want is None:
+        assert got is None
+    else:
+        assert [_norm_secret(s) for s in got.Secrets] == want["Secrets"]
+
+
+@pytest.mark.gpu
+def test_gpu_analyze_batch_vs_oracle():
+    from trivy_amd.analyzer import AnalysisInput, FileInfo, SecretAnalyzer, AnalyzerOptions
+    a = SecretAnalyzer()
+    a.Init(AnalyzerOptions())
+    o = oan.SecretAnalyzer("")
+    rng = random.Random(3)
+    inputs = []
+    for i, (p, b) in enumerate(make_corpus(31, 200)):
+        if i % 9 == 0:
+            b = b"\x00\x01" + b + b"\x02"  # binary: skipped unless .pyc
+            if i % 2 == 0:
+                p = p + ".pyc"
+        inputs.append(AnalysisInput(Dir=rng.choice(["", "."]), FilePath=p, Info=FileInfo(len(b)), Content=b))
+    got = a.AnalyzeBatch(inputs, arena_bytes=64 << 10)  # several batches
+    n = 0
+    for inp, g in zip(inputs, got):
+        w = o.analyze(inp.FilePath, inp.Dir, inp.Content)
+        if w is None:
+            assert g is None, inp.FilePath
+        else:
+            n += 1
+            assert [_norm_secret(s) for s in g.Secrets] == w["Secrets"], inp.FilePath
+    assert n > 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [tarfile.GNU_FORMAT, tarfile.PAX_FORMAT])
+def test_gpu_analyze_layer_vs_oracle(fmt):
+    from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
+    a = SecretAnalyzer()
+    a.Init(AnalyzerOptions())
+    o = oan.SecretAnalyzer("")
+    layer = make_layer(500 + fmt, 400, fmt)
+    st = {}
+    got = a.AnalyzeLayer(layer, arena_bytes=32 << 10, stats=st)  # many double-buffered batches
+    want = oan.analyze_layer(o, layer)
+    got.Sort()
+    want.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
+    for s in want:  # AnalysisResult.Sort (analyzer.go:225-234)
+        s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
+    assert [_norm_secret(s) for s in got.Secrets] == want
+    assert len(want) > 5 and st["added"] > 100

@@ -1,0 +1,352 @@
+"""SecretAnalyzer: pkg/fanal/analyzer/secret/secret.go over the MI355X engine.
+
+Same names and behaviour as the Go analyzer (undistro/trivy @ 2024-12-20):
+
+* ``SecretAnalyzer.Init(opt)``      -- secret.go:86-101 (ParseConfig + NewScanner)
+* ``SecretAnalyzer.Required(p, fi)`` -- secret.go:152-190 (tsg_analyzer_required)
+* ``SecretAnalyzer.Analyze(input)`` -- secret.go:103-150: binary gate, CR strip or
+  printable extraction, "/" prefix for image files, Scan, nil without findings
+* ``Type()`` = "secret" (analyzer/const.go:140), ``Version()`` = 1 (secret.go:26)
+
+and the batched forms the engine is built for (the analyzer group's goroutine
+per file, analyzer.go:403-455, becomes a batch collector feeding one arena):
+
+* ``AnalyzeBatch(inputs)``  -- Analyze for many files, one GPU submission per arena
+* ``AnalyzeLayer(tar)``     -- LayerTar.Walk (walker/tar.go:35-103) + AnalyzeFile's
+  Required gate + Analyze for every regular file of an uncompressed layer,
+  parsed natively into double-buffered pinned arenas (tsg_collector_add_tar)
+
+Every transform runs in libtsg.so (include/tsg_analyzer.h); there is no CPU
+fallback for the scan itself.
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+from .. import _lib
+from ..secret import NewScanner, ParseConfig, Secret
+from ..secret.scanner import ScanResult
+
+c = ctypes
+TypeSecret = "secret"  # pkg/fanal/analyzer/const.go:140
+version = 1            # secret.go:26
+TSG_SKIPPED, TSG_FULL = -1, -2
+
+
+class _CTarStats(c.Structure):
+    _fields_ = [(n, c.c_uint64) for n in ("entries", "regular", "required", "added", "skipped_binary",
+                                          "whiteouts", "opaque_dirs", "input_bytes")]
+
+
+def _declare(L):
+    if getattr(L, "_tsg_analyzer_declared", False):
+        return
+    L.tsg_is_binary.argtypes = [c.c_char_p, c.c_uint64]
+    L.tsg_extract_printable.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p]
+    L.tsg_extract_printable.restype = c.c_uint64
+    L.tsg_strip_cr.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p]
+    L.tsg_strip_cr.restype = c.c_uint64
+    L.tsg_analyzer_new.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_void_p)]
+    L.tsg_analyzer_free.argtypes = [c.c_void_p]
+    L.tsg_analyzer_required.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64, c.c_int64]
+    L.tsg_collector_new.argtypes = [c.c_void_p, c.c_uint64, c.POINTER(c.c_void_p)]
+    L.tsg_collector_free.argtypes = [c.c_void_p]
+    L.tsg_collector_add.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64, c.c_char_p, c.c_char_p, c.c_uint64]
+    L.tsg_collector_add.restype = c.c_int64
+    L.tsg_collector_add_tar.argtypes = [c.c_void_p, c.c_void_p, c.c_uint64, c.POINTER(c.c_uint64),
+                                        c.POINTER(_CTarStats)]
+    L.tsg_collector_files.argtypes = [c.c_void_p]
+    L.tsg_collector_files.restype = c.c_uint32
+    L.tsg_collector_bytes.argtypes = [c.c_void_p]
+    L.tsg_collector_bytes.restype = c.c_uint64
+    L.tsg_collector_input_bytes.argtypes = [c.c_void_p]
+    L.tsg_collector_input_bytes.restype = c.c_uint64
+    L.tsg_collector_file.argtypes = [c.c_void_p, c.c_uint32, c.POINTER(c.c_void_p), c.POINTER(c.c_uint64),
+                                     c.POINTER(c.c_void_p), c.POINTER(c.c_uint64), c.POINTER(c.c_int)]
+    L.tsg_collector_submit.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    L.tsg_collector_reset.argtypes = [c.c_void_p]
+    L.tsg_scan_wait.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    L._tsg_analyzer_declared = True
+
+
+def _b(s) -> bytes:
+    return s if isinstance(s, bytes) else str(s).encode("utf-8", "surrogateescape")
+
+
+# ---- utils (pkg/fanal/utils/utils.go) -------------------------------------
+def IsBinary(content: bytes, fileSize: int) -> bool:  # utils.go:85-103
+    L = _lib.lib()
+    _declare(L)
+    return L.tsg_is_binary(content, min(int(fileSize), len(content))) == 1
+
+
+def ExtractPrintableBytes(content: bytes) -> bytes:  # utils.go:128-160
+    L = _lib.lib()
+    _declare(L)
+    out = c.create_string_buffer(len(content) + len(content) // 5 + 2)
+    n = L.tsg_extract_printable(content, len(content), out)
+    return out.raw[:n]
+
+
+def StripCR(content: bytes) -> bytes:  # bytes.ReplaceAll(content, "\r", ""), secret.go:121
+    L = _lib.lib()
+    _declare(L)
+    out = c.create_string_buffer(max(1, len(content)))
+    n = L.tsg_strip_cr(content, len(content), out)
+    return out.raw[:n]
+
+
+# ---- analyzer types (pkg/fanal/analyzer/analyzer.go) -----------------------
+@dataclass
+class SecretScannerOption:  # analyzer.go:56-58
+    ConfigPath: str = ""
+
+
+@dataclass
+class AnalyzerOptions:  # analyzer.go:44-54 (the secret analyzer's part)
+    SecretScannerOption: SecretScannerOption = field(default_factory=SecretScannerOption)
+
+
+@dataclass
+class FileInfo:  # the os.FileInfo facts the analyzer reads
+    size: int
+
+    def Size(self) -> int:
+        return self.size
+
+
+@dataclass
+class AnalysisInput:  # analyzer.go:81-88
+    Dir: str
+    FilePath: str
+    Info: FileInfo
+    Content: bytes  # or a readable binary file object
+
+
+@dataclass
+class AnalysisResult:  # analyzer.go:99-136 (the Secrets part)
+    Secrets: List[Secret] = field(default_factory=list)
+
+    def Merge(self, other: Optional["AnalysisResult"]):  # analyzer.go:251-301
+        if other is not None:
+            self.Secrets.extend(other.Secrets)
+
+    def Sort(self):  # analyzer.go:225-234
+        self.Secrets.sort(key=lambda s: _b(s.FilePath))
+        for sec in self.Secrets:
+            if sec.Findings:
+                sec.Findings.sort(key=lambda f: (_b(f.RuleID), f.StartLine))
+
+
+def _read(content) -> bytes:
+    if isinstance(content, (bytes, bytearray, memoryview)):
+        return bytes(content)
+    data = content.read()
+    if hasattr(content, "seek"):
+        content.seek(0)
+    return data
+
+
+class Collector:
+    """A batch arena (tsg_collector): Analyze's pre-scan half for many files."""
+
+    def __init__(self, analyzer: "SecretAnalyzer", arena_bytes: int = 256 << 20):
+        self._L = analyzer._L
+        h = c.c_void_p()
+        if self._L.tsg_collector_new(analyzer._h, int(arena_bytes), c.byref(h)) != 0:
+            raise RuntimeError("tsg_collector_new failed: %s" % _lib.last_error())
+        self._h = h
+        self._keep = []
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.tsg_collector_free(self._h)
+            self._h = None
+
+    def add(self, path: str, dir_: str, content: bytes) -> int:
+        p = _b(path)
+        return self._L.tsg_collector_add(self._h, p, len(p), _b(dir_), content, len(content))
+
+    def add_tar(self, buf, cursor: int, stats: _CTarStats):
+        """Walk the layer from ``cursor``: (1 when full / 0 at the end, next cursor)."""
+        cur = c.c_uint64(cursor)
+        addr = buf.ctypes.data if hasattr(buf, "ctypes") else c.cast(c.c_char_p(buf), c.c_void_p).value
+        rc = self._L.tsg_collector_add_tar(self._h, addr, len(buf), c.byref(cur), c.byref(stats))
+        if rc < 0:
+            raise ValueError("tar layer: %s" % _lib.last_error())
+        return rc, cur.value
+
+    def files(self) -> int:
+        return self._L.tsg_collector_files(self._h)
+
+    def nbytes(self) -> int:
+        return self._L.tsg_collector_bytes(self._h)
+
+    def input_bytes(self) -> int:
+        return self._L.tsg_collector_input_bytes(self._h)
+
+    def file(self, i: int):
+        """(scan path, transformed content, binary) of batch file i."""
+        pp, pl, cp, cl, bn = c.c_void_p(), c.c_uint64(), c.c_void_p(), c.c_uint64(), c.c_int()
+        if self._L.tsg_collector_file(self._h, i, c.byref(pp), c.byref(pl), c.byref(cp), c.byref(cl),
+                                      c.byref(bn)) != 0:
+            raise IndexError(i)
+        path = c.string_at(pp, pl.value).decode("utf-8", "surrogateescape")
+        data = c.string_at(cp, cl.value) if cl.value else b""
+        return path, data, bool(bn.value)
+
+    def paths(self) -> List[str]:
+        return [self.file(i)[0] for i in range(self.files())]
+
+    def submit(self) -> "PendingBatch":
+        paths = self.paths()
+        h = c.c_void_p()
+        if self._L.tsg_collector_submit(self._h, c.byref(h)) != 0:
+            raise RuntimeError("tsg_collector_submit failed: %s" % _lib.last_error())
+        return PendingBatch(self, h, paths)
+
+    def reset(self):
+        self._L.tsg_collector_reset(self._h)
+
+
+class PendingBatch:
+    def __init__(self, coll: Collector, h, paths):
+        self.coll, self._h, self.paths = coll, h, paths
+
+    def wait(self) -> List[Optional[Secret]]:
+        """Per batch file: the Secret when it has findings (Analyze's result), else None."""
+        r = c.c_void_p()
+        rc = self.coll._L.tsg_scan_wait(self._h, c.byref(r))
+        self._h = None
+        if rc != 0:
+            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
+        res = ScanResult(_ScannerRef(self.coll._L), r)
+        out = [s if s.Findings else None for s in res.secrets(self.paths)]
+        del res
+        self.coll.reset()
+        return out
+
+
+class _ScannerRef:  # what ScanResult needs of its scanner
+    def __init__(self, L):
+        self._L = L
+
+
+class SecretAnalyzer:
+    """analyzer/secret.SecretAnalyzer bound to the MI355X engine."""
+
+    def __init__(self, scanner=None, configPath: str = "", device: int = 0, _host_only: bool = False):
+        self._L = _lib.lib()
+        _declare(self._L)
+        self.device = device
+        self._host_only = _host_only
+        self._h = None
+        self.scanner = None
+        self.configPath = configPath
+        if scanner is not None:
+            self._bind(scanner, configPath)
+
+    def _bind(self, scanner, configPath):
+        if self._h:
+            self._L.tsg_analyzer_free(self._h)
+        self.scanner = scanner
+        self.configPath = configPath
+        h = c.c_void_p()
+        if self._L.tsg_analyzer_new(scanner._h, _b(configPath), c.byref(h)) != 0:
+            raise RuntimeError("tsg_analyzer_new failed: %s" % _lib.last_error())
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.tsg_analyzer_free(self._h)
+            self._h = None
+
+    # --- reference API ------------------------------------------------------
+    def Init(self, opt: AnalyzerOptions):  # secret.go:86-101
+        path = opt.SecretScannerOption.ConfigPath
+        if self.scanner is not None and path == self.configPath:
+            return None
+        try:
+            cfg = ParseConfig(path)
+        except Exception as e:  # xerrors.Errorf("secret config error: %w", err)
+            raise RuntimeError("secret config error: %s" % e)
+        self._bind(NewScanner(cfg, device=self.device, _host_only=self._host_only), path)
+        return None
+
+    def Type(self) -> str:
+        return TypeSecret
+
+    def Version(self) -> int:
+        return version
+
+    def Required(self, filePath: str, fi) -> bool:  # secret.go:152-190
+        p = _b(filePath)
+        size = fi.Size() if hasattr(fi, "Size") else int(fi)
+        return self._L.tsg_analyzer_required(self._h, p, len(p), int(size)) == 1
+
+    def Analyze(self, input: AnalysisInput) -> Optional[AnalysisResult]:  # secret.go:103-150
+        return self.AnalyzeBatch([input])[0]
+
+    # --- batched forms ------------------------------------------------------
+    def AnalyzeBatch(self, inputs: Sequence[AnalysisInput], arena_bytes: int = 256 << 20
+                     ) -> List[Optional[AnalysisResult]]:
+        out: List[Optional[AnalysisResult]] = [None] * len(inputs)
+        coll = Collector(self, arena_bytes)
+        idx: List[int] = []
+
+        def flush():
+            if not idx:
+                return
+            for k, sec in zip(idx, coll.submit().wait()):
+                if sec is not None:
+                    out[k] = AnalysisResult(Secrets=[sec])
+            idx.clear()
+
+        for k, inp in enumerate(inputs):
+            data = _read(inp.Content)
+            for _ in range(2):
+                r = coll.add(inp.FilePath, inp.Dir, data)
+                if r == TSG_FULL:
+                    flush()
+                    continue
+                if r >= 0:
+                    idx.append(k)
+                elif r != TSG_SKIPPED:
+                    raise RuntimeError("tsg_collector_add failed: %s" % _lib.last_error())
+                break
+        flush()
+        return out
+
+    def AnalyzeLayer(self, layer, arena_bytes: int = 256 << 20, stats: Optional[dict] = None) -> AnalysisResult:
+        """Every regular file of an uncompressed tar layer (bytes or a uint8 numpy array),
+        as the image artifact's AnalyzeFile(dir="") would run it.  Two collectors alternate:
+        one is being filled while the other's batch is on the GPU."""
+        result = AnalysisResult()
+        st = _CTarStats()
+        colls = [Collector(self, arena_bytes), Collector(self, arena_bytes)]
+        pending = None
+        cursor, k, done = 0, 0, False
+        while not done:
+            coll = colls[k]
+            rc, cursor = coll.add_tar(layer, cursor, st)
+            done = rc == 0
+            if rc == 1 and coll.files() == 0:
+                raise RuntimeError("tar layer: an entry does not fit an empty collector")
+            nxt = coll.submit() if coll.files() else None
+            if pending is not None:
+                for sec in pending.wait():
+                    if sec is not None:
+                        result.Secrets.append(sec)
+            pending = nxt
+            k ^= 1
+        if pending is not None:
+            for sec in pending.wait():
+                if sec is not None:
+                    result.Secrets.append(sec)
+        if stats is not None:
+            stats.update({n: getattr(st, n) for n, _ in st._fields_})
+        return result
+
+
+def NewSecretAnalyzer(s=None, configPath: str = "") -> SecretAnalyzer:  # secret.go:79-84
+    return SecretAnalyzer(s, configPath)

@@ -1,0 +1,504 @@
+// The secret analyzer's ingest side (include/tsg_analyzer.h): the per-file
+// work pkg/fanal/analyzer/secret/secret.go does before Scanner.Scan, the
+// analyzer group's Required gate, and an uncompressed-tar layer walker
+// (pkg/fanal/walker/tar.go), all packing straight into one batch arena.
+#include "tsg_analyzer.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "capi_internal.h"
+
+namespace tsg {
+void SetError(const std::string& e);
+
+// utils.IsBinary (utils.go:85-103): the head is min(size, 300) bytes.
+bool IsBinaryHead(const uint8_t* p, uint64_t size) {
+  const uint64_t n = size < 300 ? size : 300;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t b = p[i];
+    if (b < 7 || b == 11 || (13 < b && b < 27) || (27 < b && b < 0x20) || b == 0x7f) return true;
+  }
+  return false;
+}
+
+// unicode.IsPrint(rune(b)) for a byte (Latin-1 code points): graphic
+// characters and the ASCII space; U+00A0 and the soft hyphen U+00AD are not.
+inline bool IsPrintByte(uint8_t b) { return (b >= 0x20 && b <= 0x7E) || (b >= 0xA1 && b != 0xAD); }
+
+// utils.ExtractPrintableBytes (utils.go:128-160): minLength = 4, a run is kept
+// when longer than that, each kept run is followed by '\n'.
+uint64_t ExtractPrintable(const uint8_t* in, uint64_t n, uint8_t* out) {
+  uint64_t w = 0, run = 0;  // the current run is in[i - run, i)
+  for (uint64_t i = 0; i <= n; i++) {
+    if (i < n && IsPrintByte(in[i])) {
+      run++;
+      continue;
+    }
+    if (run > 4) {
+      std::memmove(out + w, in + i - run, run);
+      w += run;
+      out[w++] = '\n';
+    }
+    run = 0;
+  }
+  return w;
+}
+
+// bytes.ReplaceAll(content, "\r", "") (secret.go:121), memchr-driven.
+uint64_t StripCR(const uint8_t* in, uint64_t n, uint8_t* out) {
+  uint64_t r = 0, w = 0;
+  while (r < n) {
+    const void* q = std::memchr(in + r, '\r', size_t(n - r));
+    const uint64_t e = q ? uint64_t(static_cast<const uint8_t*>(q) - in) : n;
+    if (out + w != in + r) std::memmove(out + w, in + r, size_t(e - r));
+    w += e - r;
+    r = e + (q ? 1 : 0);
+  }
+  return w;
+}
+
+// path.Clean (Go, slash-separated).
+std::string GoPathClean(const std::string& path) {
+  if (path.empty()) return ".";
+  const bool rooted = path[0] == '/';
+  const size_t n = path.size();
+  std::string out;
+  size_t r = 0, dotdot = 0;
+  if (rooted) {
+    out.push_back('/');
+    r = dotdot = 1;
+  }
+  while (r < n) {
+    if (path[r] == '/') {
+      r++;
+    } else if (path[r] == '.' && (r + 1 == n || path[r + 1] == '/')) {
+      r++;
+    } else if (path[r] == '.' && path[r + 1] == '.' && (r + 2 == n || path[r + 2] == '/')) {
+      r += 2;
+      if (out.size() > dotdot) {
+        out.pop_back();
+        while (out.size() > dotdot && out.back() != '/') out.pop_back();
+      } else if (!rooted) {
+        if (!out.empty()) out.push_back('/');
+        out += "..";
+        dotdot = out.size();
+      }
+    } else {
+      if ((rooted && out.size() != 1) || (!rooted && !out.empty())) out.push_back('/');
+      for (; r < n && path[r] != '/'; r++) out.push_back(path[r]);
+    }
+  }
+  if (out.empty()) return ".";
+  return out;
+}
+
+// filepath.Ext / filepath.Base (Unix).
+std::string GoExt(const std::string& p) {
+  for (size_t i = p.size(); i-- > 0 && p[i] != '/';)
+    if (p[i] == '.') return p.substr(i);
+  return "";
+}
+std::string GoBase(std::string p) {
+  if (p.empty()) return ".";
+  while (!p.empty() && p.back() == '/') p.pop_back();
+  if (p.empty()) return "/";
+  const size_t k = p.rfind('/');
+  return k == std::string::npos ? p : p.substr(k + 1);
+}
+
+// secret.go:28-62
+const char* const kSkipFiles[] = {"go.mod", "go.sum", "package-lock.json", "yarn.lock",
+                                  "pnpm-lock.yaml", "Pipfile.lock", "Gemfile.lock"};
+const char* const kSkipDirs[] = {".git", "node_modules"};
+const char* const kSkipExts[] = {".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg",
+                                 ".socket", ".deb", ".rpm", ".zip", ".gz", ".gzip", ".tar"};
+
+}  // namespace tsg
+
+struct tsg_analyzer {
+  const tsg_scanner* s = nullptr;
+  std::string config_base;  // filepath.Base(configPath)
+};
+
+struct tsg_collector {
+  tsg_analyzer* a = nullptr;
+  int device = -1;  // pinned arena on this device's host side; -1 plain memory
+  uint8_t* arena = nullptr;
+  uint64_t cap = 0, used = 0, input_bytes = 0;
+  uint64_t limit = 0;  // the batch size asked for
+  std::vector<uint64_t> offs{0};
+  std::string path_pool;
+  std::vector<uint64_t> path_off{0};
+  std::vector<uint8_t> binary;
+  // built at submit / file(): char* table over path_pool
+  std::vector<const char*> path_ptrs;
+  std::vector<uint64_t> path_lens;
+
+  ~tsg_collector() { Release(); }
+  void Release() {
+    if (!arena) return;
+    if (device >= 0)
+      (void)hipHostFree(arena);
+    else
+      std::free(arena);
+    arena = nullptr;
+    cap = 0;
+  }
+  bool Reserve(uint64_t need) {  // need: arena bytes incl. the 64-B pad
+    if (need <= cap) return true;
+    Release();
+    const uint64_t n = (need + 4095) & ~uint64_t(4095);
+    void* p = nullptr;
+    if (device >= 0) {
+      if (hipSetDevice(device) != hipSuccess || hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    } else if (posix_memalign(&p, 4096, n) != 0) {
+      p = nullptr;
+    }
+    if (!p) {
+      tsg::SetError("collector: cannot allocate a " + std::to_string(n) + "-byte arena");
+      return false;
+    }
+    arena = static_cast<uint8_t*>(p);
+    cap = n;
+    return true;
+  }
+  uint32_t files() const { return uint32_t(offs.size() - 1); }
+  void BuildPaths() {
+    const uint32_t n = files();
+    path_ptrs.resize(n);
+    path_lens.resize(n);
+    for (uint32_t i = 0; i < n; i++) {
+      path_ptrs[i] = path_pool.data() + path_off[i];
+      path_lens[i] = path_off[i + 1] - path_off[i];
+    }
+  }
+  void Reset() {
+    used = input_bytes = 0;
+    offs.assign(1, 0);
+    path_pool.clear();
+    path_off.assign(1, 0);
+    binary.clear();
+  }
+};
+
+namespace {
+bool Required(const tsg_analyzer* a, const char* path, uint64_t len, int64_t size) {  // secret.go:152-190
+  if (size < 10) return false;
+  const std::string fp(path, size_t(len));
+  const size_t slash = fp.rfind('/');
+  const std::string dir = slash == std::string::npos ? "" : fp.substr(0, slash + 1);
+  const std::string name = slash == std::string::npos ? fp : fp.substr(slash + 1);
+  // strings.Split(dir, "/") contains a skip dir
+  for (size_t b = 0;;) {
+    const size_t e = dir.find('/', b);
+    const std::string part = dir.substr(b, e == std::string::npos ? std::string::npos : e - b);
+    for (const char* d : tsg::kSkipDirs)
+      if (part == d) return false;
+    if (e == std::string::npos) break;
+    b = e + 1;
+  }
+  for (const char* f : tsg::kSkipFiles)
+    if (name == f) return false;
+  if (a->config_base == fp) return false;
+  const std::string ext = tsg::GoExt(name);
+  for (const char* x : tsg::kSkipExts)
+    if (ext == x) return false;
+  if (a->s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len))) return false;
+  return true;
+}
+
+// Analyze up to the Scan call (secret.go:103-136).
+int64_t Add(tsg_collector* c, const char* path, uint64_t plen, bool image, const uint8_t* content, uint64_t size) {
+  const bool bin = tsg::IsBinaryHead(content, size);
+  if (bin && tsg::GoExt(std::string(path, size_t(plen))) != ".pyc") return TSG_SKIPPED;
+  const uint64_t need = bin ? size + size / 5 + 1 : size;
+  if (c->files() > 0 && c->used + need > c->limit) return TSG_FULL;
+  if (c->used + need + 64 > c->cap) {  // only a lone file larger than the batch gets here
+    if (c->files() > 0) return TSG_FULL;
+    if (!c->Reserve(need + 64)) return -3;
+  }
+  uint8_t* dst = c->arena + c->used;
+  const uint64_t len = bin ? tsg::ExtractPrintable(content, size, dst) : tsg::StripCR(content, size, dst);
+  c->used += len;
+  std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
+  c->offs.push_back(c->used);
+  if (image) c->path_pool.push_back('/');  // files extracted from an image (secret.go:130-135)
+  c->path_pool.append(path, size_t(plen));
+  c->path_off.push_back(c->path_pool.size());
+  c->binary.push_back(bin ? 1 : 0);
+  c->input_bytes += size;
+  return int64_t(c->files() - 1);
+}
+
+// ---- archive/tar header reading (Go 1.22 archive/tar/reader.go semantics) ----
+bool AllZero(const uint8_t* b) {
+  for (int i = 0; i < 512; i++)
+    if (b[i]) return false;
+  return true;
+}
+std::string CStr(const uint8_t* b, size_t n) {  // parseString: up to the first NUL
+  size_t k = 0;
+  while (k < n && b[k]) k++;
+  return std::string(reinterpret_cast<const char*>(b), k);
+}
+bool ParseNumeric(const uint8_t* b, size_t n, int64_t* out) {  // parseNumeric
+  if (n > 0 && (b[0] & 0x80)) {  // base-256 (two's complement, big-endian)
+    const bool neg = b[0] & 0x40;
+    uint64_t v = 0;
+    for (size_t i = 0; i < n; i++) {
+      uint8_t c = i == 0 ? (b[0] & 0x7F) : b[i];
+      if (neg) c ^= 0xFF;
+      if (i == 0 && neg) c &= 0x7F;
+      if (v >> 56) return false;
+      v = (v << 8) | c;
+    }
+    if (v >> 63) return false;
+    *out = neg ? -int64_t(v) - 1 : int64_t(v);
+    return true;
+  }
+  // parseOctal: trim spaces and NULs at both ends
+  size_t lo = 0, hi = n;
+  while (lo < hi && (b[lo] == ' ' || b[lo] == 0)) lo++;
+  while (hi > lo && (b[hi - 1] == ' ' || b[hi - 1] == 0)) hi--;
+  int64_t v = 0;
+  for (size_t i = lo; i < hi; i++) {
+    if (b[i] < '0' || b[i] > '7') return false;
+    if (v >> 60) return false;
+    v = v * 8 + (b[i] - '0');
+  }
+  *out = v;
+  return true;
+}
+bool ChecksumOK(const uint8_t* b) {
+  int64_t want = 0;
+  if (!ParseNumeric(b + 148, 8, &want)) return false;
+  int64_t u = 0, s = 0;
+  for (int i = 0; i < 512; i++) {
+    const uint8_t c = (i >= 148 && i < 156) ? ' ' : b[i];
+    u += c;
+    s += int8_t(c);
+  }
+  return want == u || want == s;
+}
+// PAX records "%d %s=%s\n" (parsePAX): path, size and linkpath matter here.
+bool ParsePax(const uint8_t* d, uint64_t n, std::string* path, int64_t* size, bool* has_path, bool* has_size) {
+  uint64_t p = 0;
+  while (p < n) {
+    uint64_t sp = p;
+    while (sp < n && d[sp] != ' ') sp++;
+    if (sp >= n) return false;
+    uint64_t len = 0;
+    for (uint64_t i = p; i < sp; i++) {
+      if (d[i] < '0' || d[i] > '9') return false;
+      len = len * 10 + (d[i] - '0');
+    }
+    if (len < sp - p + 2 || p + len > n || d[p + len - 1] != '\n') return false;
+    const std::string rec(reinterpret_cast<const char*>(d + sp + 1), size_t(len - (sp + 1 - p) - 1));
+    const size_t eq = rec.find('=');
+    if (eq == std::string::npos) return false;
+    const std::string k = rec.substr(0, eq), v = rec.substr(eq + 1);
+    if (k == "path") {
+      *path = v;
+      *has_path = true;
+    } else if (k == "size") {
+      char* e = nullptr;
+      *size = std::strtoll(v.c_str(), &e, 10);
+      if (v.empty() || *e) return false;
+      *has_size = true;
+    }
+    p += len;
+  }
+  return true;
+}
+bool HeaderOnly(char t) { return t == '1' || t == '2' || t == '3' || t == '4' || t == '5' || t == '6'; }
+}  // namespace
+
+extern "C" {
+
+int tsg_is_binary(const uint8_t* content, uint64_t size) { return tsg::IsBinaryHead(content, size) ? 1 : 0; }
+uint64_t tsg_extract_printable(const uint8_t* in, uint64_t n, uint8_t* out) { return tsg::ExtractPrintable(in, n, out); }
+uint64_t tsg_strip_cr(const uint8_t* in, uint64_t n, uint8_t* out) { return tsg::StripCR(in, n, out); }
+
+int tsg_analyzer_new(const tsg_scanner* s, const char* config_path, tsg_analyzer** out) {
+  if (!s || !out) {
+    tsg::SetError("tsg_analyzer_new: null argument");
+    return -1;
+  }
+  auto* a = new tsg_analyzer();
+  a->s = s;
+  a->config_base = tsg::GoBase(config_path ? config_path : "");
+  *out = a;
+  return 0;
+}
+void tsg_analyzer_free(tsg_analyzer* a) { delete a; }
+
+int tsg_analyzer_required(const tsg_analyzer* a, const char* path, uint64_t path_len, int64_t size) {
+  return Required(a, path, path_len, size) ? 1 : 0;
+}
+
+int tsg_collector_new(tsg_analyzer* a, uint64_t arena_bytes, tsg_collector** out) {
+  auto* c = new tsg_collector();
+  c->a = a;
+  c->device = a->s->s->device();
+  c->limit = arena_bytes ? arena_bytes : (uint64_t(256) << 20);
+  if (!c->Reserve(c->limit + 64)) {
+    delete c;
+    return -1;
+  }
+  *out = c;
+  return 0;
+}
+void tsg_collector_free(tsg_collector* c) { delete c; }
+
+int64_t tsg_collector_add(tsg_collector* c, const char* path, uint64_t path_len, const char* dir,
+                          const uint8_t* content, uint64_t size) {
+  return Add(c, path, path_len, !dir || !*dir, content, size);
+}
+
+int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st) {
+  tsg_tar_stats local{};
+  if (!st) st = &local;
+  uint64_t p = *cursor;
+  for (;;) {
+    const uint64_t entry = p;  // where this entry's header chain starts
+    std::string long_name, pax_path;
+    bool has_long = false, has_pax_path = false, has_pax_size = false;
+    int64_t pax_size = 0;
+    const uint8_t* h = nullptr;
+    char type = 0;
+    int64_t size = 0;
+    for (;;) {  // extended headers, then the entry's own
+      if (p + 512 > n) {
+        if (p >= n) return 0;  // io.EOF without the zero blocks
+        tsg::SetError("tar: truncated header");
+        return -1;
+      }
+      h = tar + p;
+      if (AllZero(h)) return 0;  // end-of-archive marker
+      if (!ChecksumOK(h)) {
+        tsg::SetError("tar: invalid header checksum at offset " + std::to_string(p));
+        return -1;
+      }
+      type = char(h[156]);
+      if (!ParseNumeric(h + 124, 12, &size) || size < 0) {
+        tsg::SetError("tar: invalid size field");
+        return -1;
+      }
+      const uint64_t dsz = HeaderOnly(type) ? 0 : uint64_t(size);
+      const uint64_t data = p + 512;
+      if (data + dsz > n) {
+        tsg::SetError("tar: truncated entry data");
+        return -1;
+      }
+      if (type == 'x') {
+        if (!ParsePax(tar + data, dsz, &pax_path, &pax_size, &has_pax_path, &has_pax_size)) {
+          tsg::SetError("tar: invalid PAX record");
+          return -1;
+        }
+        p = data + ((dsz + 511) & ~uint64_t(511));
+        continue;
+      }
+      if (type == 'L') {
+        long_name = CStr(tar + data, size_t(dsz));
+        has_long = true;
+        p = data + ((dsz + 511) & ~uint64_t(511));
+        continue;
+      }
+      if (type == 'K') {  // GNU long link name
+        p = data + ((dsz + 511) & ~uint64_t(511));
+        continue;
+      }
+      break;
+    }
+    // the entry header at h
+    std::string name = CStr(h, 100);
+    const bool ustar = std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0;
+    if (ustar) {
+      const std::string prefix = CStr(h + 345, 155);
+      if (!prefix.empty()) name = prefix + "/" + name;
+    }
+    if (has_long) name = long_name;
+    if (has_pax_path) name = pax_path;
+    if (has_pax_size) size = pax_size;
+    if (type == '\0') type = (!name.empty() && name.back() == '/') ? '5' : '0';  // TypeRegA
+    const uint64_t dsz = HeaderOnly(type) ? 0 : uint64_t(size);
+    const uint64_t data = p + 512;
+    if (data + dsz > n) {
+      tsg::SetError("tar: truncated entry data");
+      return -1;
+    }
+    const uint64_t next = data + ((dsz + 511) & ~uint64_t(511));
+    st->entries++;
+    // LayerTar.Walk (walker/tar.go:41-84)
+    std::string fp = tsg::GoPathClean(name);
+    size_t t = 0;
+    while (t < fp.size() && fp[t] == '/') t++;
+    fp = fp.substr(t);
+    const size_t slash = fp.rfind('/');
+    const std::string file_name = slash == std::string::npos ? fp : fp.substr(slash + 1);
+    if (file_name == ".wh..wh..opq") {
+      st->opaque_dirs++;
+    } else if (file_name.compare(0, 4, ".wh.") == 0) {
+      st->whiteouts++;
+    } else if (type == '0') {
+      st->regular++;
+      // AnalyzeFile (analyzer.go:403-455): Required(cleanPath), then Analyze with Dir ""
+      if (Required(c->a, fp.data(), fp.size(), int64_t(dsz))) {
+        st->required++;
+        const int64_t r = Add(c, fp.data(), fp.size(), true, tar + data, dsz);
+        if (r == TSG_FULL) {
+          st->required--;
+          *cursor = entry;
+          return 1;
+        }
+        if (r == TSG_SKIPPED) {
+          st->skipped_binary++;
+        } else if (r < 0) {
+          return -1;
+        } else {
+          st->added++;
+          st->input_bytes += dsz;
+        }
+      }
+    }
+    p = next;
+    *cursor = p;
+  }
+}
+
+uint32_t tsg_collector_files(const tsg_collector* c) { return c->files(); }
+uint64_t tsg_collector_bytes(const tsg_collector* c) { return c->used; }
+uint64_t tsg_collector_input_bytes(const tsg_collector* c) { return c->input_bytes; }
+
+int tsg_collector_file(const tsg_collector* c, uint32_t i, const char** path, uint64_t* path_len,
+                       const uint8_t** content, uint64_t* len, int* binary) {
+  if (i >= c->files()) return -1;
+  *path = c->path_pool.data() + c->path_off[i];
+  *path_len = c->path_off[i + 1] - c->path_off[i];
+  *content = c->arena + c->offs[i];
+  *len = c->offs[i + 1] - c->offs[i];
+  *binary = c->binary[i];
+  return 0;
+}
+
+int tsg_collector_submit(tsg_collector* c, tsg_pending** out) {
+  c->BuildPaths();
+  tsg_batch b{};
+  b.n_files = c->files();
+  b.host_arena = c->arena;
+  b.host_offsets = c->offs.data();
+  b.paths = c->path_ptrs.data();
+  b.path_lens = c->path_lens.data();
+  b.binary = c->binary.data();
+  return tsg_scan_submit(const_cast<tsg_scanner*>(c->a->s), &b, out);
+}
+
+void tsg_collector_reset(tsg_collector* c) { c->Reset(); }
+
+}  // extern "C"

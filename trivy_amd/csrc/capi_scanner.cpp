@@ -8,6 +8,7 @@
 #include <memory>
 #include <string>
 
+#include "capi_internal.h"
 #include "filter.h"
 #include "scanner.h"
 #include "tsg_debug.h"
@@ -17,9 +18,6 @@ namespace tsg {
 void SetError(const std::string& e);
 }
 
-struct tsg_scanner {
-  std::unique_ptr<tsg::SecretScanner> s;
-};
 
 struct tsg_result {
   tsg::BatchResult files;
@@ -184,6 +182,26 @@ int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out) {
 }
 
 void tsg_scanner_free(tsg_scanner* s) { delete s; }
+
+int tsg_debug_scanner_host_only(const tsg_global* g, tsg_scanner** out) {
+  std::string err;
+  std::vector<tsg::RuleSpec> rules;
+  std::vector<tsg::AllowRuleSpec> allow;
+  std::vector<std::unique_ptr<tsg::Regex>> exclude;
+  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
+      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
+    tsg::SetError(err);
+    return -1;
+  }
+  std::unique_ptr<tsg_scanner> s(new tsg_scanner());
+  s->s.reset(new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), -1, &err));
+  if (!s->s->ok()) {
+    tsg::SetError(err.empty() ? s->s->error() : err);
+    return -2;
+  }
+  *out = s.release();
+  return 0;
+}
 
 int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len) {
   return s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len)) ? 1 : 0;

@@ -135,6 +135,7 @@ class SecretScanner {
   const std::vector<RuleSpec>& rules() const { return rules_; }
   const CompiledRules& compiled() const { return cr_; }
   GpuEngine* engine() { return engine_.get(); }
+  int device() const { return engine_ ? engine_->device() : -1; }  // -1: no GPU engine
   void set_host_threads(int n) { host_threads_ = n; }
 
  private:

@@ -188,7 +188,7 @@ class Scanner:
     """secret.Scanner: an assembled Global bound to one HIP device."""
 
     def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude_regexes: Sequence[str],
-                 device: int = 0):
+                 device: int = 0, _host_only: bool = False):
         self.Rules = list(rules)
         self.AllowRules = list(allow_rules)
         self.ExcludeRegexes = list(exclude_regexes)
@@ -198,7 +198,11 @@ class Scanner:
         self._cg = CGlobal(rules, allow_rules, exclude_regexes)
         g = self._cg.g
         h = c.c_void_p()
-        rc = L.tsg_scanner_new(c.byref(g), int(device), c.byref(h))
+        if _host_only:  # test hook (tsg_debug_scanner_host_only): host logic only, tsg_scan fails
+            L.tsg_debug_scanner_host_only.argtypes = [c.POINTER(_CGlobal), c.POINTER(c.c_void_p)]
+            rc = L.tsg_debug_scanner_host_only(c.byref(g), c.byref(h))
+        else:
+            rc = L.tsg_scanner_new(c.byref(g), int(device), c.byref(h))
         if rc != 0:
             raise RuntimeError("tsg_scanner_new failed: %s" % _lib.last_error())
         self._h = h
@@ -349,10 +353,10 @@ class ScanResult:
         return out
 
 
-def NewScanner(config: Optional[Config], device: int = 0) -> Scanner:  # scanner.go:320-364
+def NewScanner(config: Optional[Config], device: int = 0, _host_only: bool = False) -> Scanner:  # scanner.go:320-364
     b_rules, b_allow = builtin_rules(), builtin_allow_rules()
     if config is None:
-        return Scanner(b_rules, b_allow, [], device)
+        return Scanner(b_rules, b_allow, [], device, _host_only)
     enabled = b_rules
     if config.EnableBuiltinRuleIDs:
         enabled = [r for r in b_rules if r.ID in config.EnableBuiltinRuleIDs]
@@ -360,4 +364,4 @@ def NewScanner(config: Optional[Config], device: int = 0) -> Scanner:  # scanner
     rules = [r for r in enabled if r.ID not in config.DisableRuleIDs]
     allow = b_allow + list(config.CustomAllowRules)
     allow = [a for a in allow if a.ID not in config.DisableAllowRuleIDs]
-    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device)
+    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device, _host_only)
