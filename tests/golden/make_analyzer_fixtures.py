@@ -7,7 +7,7 @@ Source (read as data, in the build container only):
 
 Outputs (committed; the GPU box never reads /root/reference):
   tests/golden/analyzer/testdata/...  text inputs and YAML configs, copied verbatim
-  tests/golden/analyzer/testdata/secret.cpython-310.pyc
+  tests/golden/analyzer/testdata/secret.cpython-310.pyc.data (content of the case's .pyc path)
       NOT the reference's file: a synthetic binary made of the printable runs
       (> 4 bytes) that utils.ExtractPrintableBytes finds in it, separated by NUL
       bytes, so the extracted text -- all the analyzer scans -- is identical
@@ -88,7 +88,8 @@ def main():
                  "binaryfile", "emptyfile", "package-lock.json", "node_modules/secret.txt"]:
         shutil.copyfile(REF / name, OUT / name)
     runs = printable_runs((REF / "secret.cpython-310.pyc").read_bytes())
-    (OUT / "secret.cpython-310.pyc").write_bytes(b"\x00\x00\x00\x00" + b"\x00".join(runs) + b"\x00")
+    # stored under another name: *.pyc files are Python caches to git and gpurun
+    (OUT / "secret.cpython-310.pyc.data").write_bytes(b"\x00\x00\x00\x00" + b"\x00".join(runs) + b"\x00")
     (HERE / "analyzer_cases.json").write_text(json.dumps({"analyze": ANALYZE, "required": REQUIRED}, indent=1))
     print("wrote", OUT, "and analyzer_cases.json")
 

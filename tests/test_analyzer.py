@@ -23,6 +23,12 @@ CASES = json.loads((G / "analyzer_cases.json").read_text())
 ADIR = G / "analyzer"
 
 
+def _content(path):
+    """The fixture bytes of a case path (the .pyc stand-in is stored as <name>.data)."""
+    p = Path(path)
+    return (p.with_name(p.name + ".data") if p.suffix == ".pyc" else p).read_bytes()
+
+
 def _norm_secret(s):
     return s.to_dict() if hasattr(s, "to_dict") else s
 
@@ -32,7 +38,7 @@ def _norm_secret(s):
 def test_oracle_analyze_golden(case, monkeypatch):
     monkeypatch.chdir(ADIR)
     a = oan.SecretAnalyzer(case["config"])
-    content = Path(case["file"]).read_bytes()
+    content = _content(case["file"])
     got = a.analyze(case["file"], case["dir"], content)
     assert got == case["want"]
 
@@ -168,7 +174,7 @@ def test_gpu_analyze_golden(case, monkeypatch):
     monkeypatch.chdir(ADIR)
     a = SecretAnalyzer()
     a.Init(AnalyzerOptions(SecretScannerOption(case["config"])))
-    content = Path(case["file"]).read_bytes()
+    content = _content(case["file"])
     got = a.Analyze(AnalysisInput(Dir=case["dir"], FilePath=case["file"], Info=FileInfo(len(content)),
                                   Content=io.BytesIO(content)))
     want = case["want"]
