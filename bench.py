@@ -14,6 +14,14 @@ Multi-GPU (torchrun, one rank per GPU): files shard by content, each rank owns
 its own --gb GB shard (weak scaling); no data-path collective.  Timing uses a
 barrier + torch.cuda.synchronize() on both sides and the max over ranks.
 
+--workload selects the BASELINE config measured (default c2 = configs[1], the
+headline): c3 = configs[2] (2,000 generated custom rules appended to the
+builtins, C2-style corpus with their samples planted); c4 = configs[3] (an
+uncompressed image layer of millions of small files resident in host memory:
+native tar walk + Required + CR strip / printable extraction into double-
+buffered pinned arenas, H2D, kernels, exact tail -- the batching/arena packing
+path; value counts the input bytes of the files analyzed).
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -27,13 +35,13 @@ sys.path.insert(0, ROOT)
 
 
 def _cpu_sample_worker(args):
-    idx, arena_path, offs_path, paths_path = args
+    idx, arena_path, offs_path, paths_path, cfg_path = args
     import numpy as np
     from oracle import secret_scanner as osc
     arena = np.load(arena_path, mmap_mode="r")
     offs = np.load(offs_path)
     paths = np.load(paths_path)
-    sc = osc.new_scanner(None)
+    sc = osc.new_scanner(osc.parse_config(cfg_path) if cfg_path else None)
     nb = 0
     nf = 0
     for i in idx:
@@ -45,7 +53,43 @@ def _cpu_sample_worker(args):
     return nb, nf
 
 
-def cpu_baseline(C, sample_bytes, cores, tmpdir):
+def _cpu_layer_worker(args):
+    k, cores, layer_path = args
+    from oracle import analyzer as oan
+    data = open(layer_path, "rb").read()
+    a = oan.SecretAnalyzer("")
+    files, _, _ = oan.walk_layer_tar(data)
+    nb = nf = 0
+    for i, (fp, size, content) in enumerate(files):
+        if i % cores != k or not a.required(fp, size):
+            continue
+        r = a.analyze(fp, "", content)
+        if a.prepare(fp, "", content) is not None:
+            nb += size
+        nf += len(r["Secrets"][0]["Findings"]) if r else 0
+    return nb, nf
+
+
+def cpu_baseline_layer(layer, cores, tmpdir):
+    """Oracle analyzer (walk + Required + Analyze, 'port' of the reference CPU path) on a layer sample."""
+    import multiprocessing as mp
+    lp = os.path.join(tmpdir, "cpu_layer.tar")
+    layer.tofile(lp)
+    ctx = mp.get_context("spawn")
+    t0 = time.time()
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_layer_worker, [(k, cores, lp) for k in range(cores)])
+    dt = time.time() - t0
+    os.remove(lp)
+    nb = sum(r[0] for r in res)
+    nf = sum(r[1] for r in res)
+    return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": cores, "kind": "port",
+            "sample": "a %.1f MB layer of the same generator (its first files), oracle/analyzer.py (tarfile walk + "
+                      "Required + Analyze restated) in %d processes; %.1f MB of files analyzed; %d findings; "
+                      "%.1f s wall" % (layer.size / 1e6, cores, nb / 1e6, nf, dt)}
+
+
+def cpu_baseline(C, sample_bytes, cores, tmpdir, cfg_path=None):
     """Oracle ('port' of the reference CPU algorithm) on the first files of the corpus."""
     import multiprocessing as mp
     import numpy as np
@@ -65,7 +109,7 @@ def cpu_baseline(C, sample_bytes, cores, tmpdir):
     ctx = mp.get_context("spawn")
     t0 = time.time()
     with ctx.Pool(cores) as pool:
-        res = pool.map(_cpu_sample_worker, [(ch, ap, op, pp) for ch in chunks])
+        res = pool.map(_cpu_sample_worker, [(ch, ap, op, pp, cfg_path) for ch in chunks])
     dt = time.time() - t0
     nb = sum(r[0] for r in res)
     nf = sum(r[1] for r in res)
@@ -73,8 +117,18 @@ def cpu_baseline(C, sample_bytes, cores, tmpdir):
         os.remove(f)
     return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": cores, "kind": "port",
             "sample": "first %d files (%.1f MB) of the same corpus, oracle/secret_scanner.py "
-                      "(Python restatement of scanner.go) in %d processes; %d findings; %.1f s wall"
-                      % (n, nb / 1e6, cores, nf, dt)}
+                      "(Python restatement of scanner.go%s) in %d processes; %d findings; %.1f s wall"
+                      % (n, nb / 1e6, ", same rule set" if cfg_path else "", cores, nf, dt)}
+
+
+WORKLOADS = {
+    "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
+           20.0, 32.0),
+    "c3": ("2,000 generated custom rules (trivy-secret.yaml) + 87 builtins over a %g GB synthetic corpus per "
+           "MI355X (BASELINE configs[2])", 8.0, 2.0),
+    "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
+           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0),
+}
 
 
 def main():
@@ -82,12 +136,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--gb", type=float, default=20.0, help="corpus size per GPU (GB = 1e9 B)")
-    ap.add_argument("--cpu-sample-mb", type=float, default=32.0)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--gb", type=float, default=None, help="corpus size per GPU (GB = 1e9 B)")
+    ap.add_argument("--cpu-sample-mb", type=float, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=2, help="scans in flight (pipelined submission)")
+    ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     args = ap.parse_args()
+    wl_desc, gb_default, cpu_mb_default = WORKLOADS[args.workload]
+    if args.gb is None:
+        args.gb = gb_default
+    if args.cpu_sample_mb is None:
+        args.cpu_sample_mb = cpu_mb_default
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,24 +165,66 @@ def main():
     from trivy_amd import corpus
     import trivy_amd.secret as secret
 
+    tmpdir = os.environ.get("TMPDIR", "/tmp")
+    cfg_path = None
     t_gen = time.time()
-    C = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank)
+    C = layer = None
+    if args.workload == "c3":
+        y, samples = corpus.c3_rules()
+        cfg_path = os.path.join(tmpdir, "tsg-bench-c3-%d.yaml" % rank)
+        with open(cfg_path, "w") as f:
+            f.write(y)
+        C = corpus.generate_c3(int(args.gb * 1e9), samples, seed=corpus.SEED + rank)
+    elif args.workload == "c4":
+        layer = corpus.generate_layer(int(args.gb * 1e9), seed=corpus.SEED + rank)
+    else:
+        C = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank)
     t_gen = time.time() - t_gen
 
-    dev = torch.device("cuda", local)
-    d_arena = torch.from_numpy(C.arena).to(dev)
-    d_offs = torch.from_numpy(C.offsets.view(np.int64)).to(dev)
-    torch.cuda.synchronize()
+    if layer is None:
+        dev = torch.device("cuda", local)
+        d_arena = torch.from_numpy(C.arena).to(dev)
+        d_offs = torch.from_numpy(C.offsets.view(np.int64)).to(dev)
+        torch.cuda.synchronize()
+        t_c = time.time()
+        sc = secret.NewScanner(secret.ParseConfig(cfg_path) if cfg_path else None, device=local)
+        t_compile = time.time() - t_c
 
-    sc = secret.NewScanner(None, device=local)
+        def submit():
+            return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(),
+                                       dev_offsets=d_offs.data_ptr())
 
-    def submit():
-        return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(),
-                                   dev_offsets=d_offs.data_ptr())
+        def run_steps(n, stats):
+            # pipelined: step i+1's kernels run while step i's exact host pass finishes
+            # (tsg_scan_submit; --depth 1 runs the steps back to back)
+            inflight = []
+            for _ in range(n):
+                inflight.append(submit())
+                if len(inflight) >= args.depth:
+                    r = inflight.pop(0).wait()
+                    stats.append(r.stats())
+                    del r
+            while inflight:
+                r = inflight.pop(0).wait()
+                stats.append(r.stats())
+                del r
+    else:
+        from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
+        from trivy_amd.analyzer.secret import Collector
+        t_c = time.time()
+        an = SecretAnalyzer(device=local)
+        an.Init(AnalyzerOptions())
+        t_compile = time.time() - t_c
+        colls = [Collector(an, args.arena_mb << 20), Collector(an, args.arena_mb << 20)]
 
-    for _ in range(args.warmup):
-        r = submit().wait()
-        del r
+        def run_steps(n, stats):
+            for _ in range(n):
+                st = {}
+                an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
+                stats.append(st)
+
+    warm = []
+    run_steps(args.warmup, warm)
 
     def barrier():
         if dist is not None:
@@ -131,19 +234,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.time()
     stats = []
-    # pipelined: step i+1's kernels run while step i's exact host pass finishes
-    # (tsg_scan_submit; --depth 1 runs the steps back to back)
-    inflight = []
-    for _ in range(args.steps):
-        inflight.append(submit())
-        if len(inflight) >= args.depth:
-            r = inflight.pop(0).wait()
-            stats.append(r.stats())
-            del r
-    while inflight:
-        r = inflight.pop(0).wait()
-        stats.append(r.stats())
-        del r
+    run_steps(args.steps, stats)
     torch.cuda.synchronize()
     barrier()
     dt = time.time() - t0
@@ -152,14 +243,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    n_bytes = C.n_bytes
-    value = world * n_bytes * args.steps / dt / 1e9
     ms_step = dt / args.steps * 1e3
-    scan_ms = sum(s["ms_scan_kernel"] for s in stats) / len(stats)
-    alg_bytes = n_bytes + 16 * C.n_files  # 1 B/arena byte + 16 B/file
+    last = stats[-1]
+    if layer is None:
+        n_bytes, n_files = C.n_bytes, C.n_files
+        scan_ms = sum(s["ms_scan_kernel"] for s in stats) / len(stats)
+        arena_bytes = n_bytes
+        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "candidates", "special_files",
+                                            "findings")}
+        breakdown = {k: round(last[k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel", "ms_verify_kernel",
+                                                    "ms_fullscan_kernel", "ms_gpu_total", "ms_host_gpu_phase",
+                                                    "ms_host_allow_path", "ms_host_exact", "ms_host_total")}
+        config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth}
+    else:
+        n_bytes = int(last["input_bytes"])  # bytes of the files analyzed, as read from the layer
+        n_files = int(last["added"])
+        arena_bytes = int(last["scan_bytes"])
+        scan_ms = sum(s["scan_ms_scan_kernel"] for s in stats) / len(stats)
+        counts = {k: int(last[k]) for k in ("entries", "regular", "required", "added", "skipped_binary",
+                                            "whiteouts")}
+        counts.update({k: int(last["scan_" + k]) for k in ("candidates", "findings", "anchor_hits")})
+        breakdown = {k: round(last["scan_" + k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel",
+                                                              "ms_verify_kernel", "ms_gpu_total",
+                                                              "ms_host_gpu_phase", "ms_host_exact")}
+        config_extra = {"layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
+                        "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
+                        "arena_mb": args.arena_mb, "pipeline": "2 collectors (walk k+1 || scan k)",
+                        "layer_gbps": round(world * int(layer.size) * args.steps / dt / 1e9, 3)}
+    value = world * n_bytes * args.steps / dt / 1e9
+    alg_bytes = arena_bytes + 16 * n_files  # 1 B/arena byte + 16 B/file
     achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(args.traffic_file):
+    if os.path.exists(args.traffic_file) and args.workload == "c2":
         try:
             tj = json.load(open(args.traffic_file))
             if abs(tj.get("gb", -1) - args.gb) < 1e-6:
@@ -171,8 +286,11 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cores = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), cores, os.environ.get("TMPDIR", "/tmp"))
-        last = stats[-1]
+            if layer is None:
+                cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), cores, tmpdir, cfg_path)
+            else:
+                sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
+                cpu = cpu_baseline_layer(sample, cores, tmpdir)
         out = {
             "metric": "GB/s secret-scanned (whole node) at 1/2/4/8 MI355X; findings bit-exact vs CPU",
             "value": round(value, 3),
@@ -185,25 +303,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (deterministic generator, seed 0x5EC2E7+rank; planted builtin-rule secrets)",
-            "config": {"workload": "builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per "
-                                   "MI355X (BASELINE configs[1])" % args.gb,
-                       "bytes_per_gpu": n_bytes, "files_per_gpu": C.n_files, "parallelism": "files sharded, dp%d" % world,
-                       "pipeline_depth": args.depth},
+            "data": "synthetic (deterministic generator, seed 0x5EC2E7+rank; planted builtin-rule secrets%s)"
+                    % (" and generated-rule samples" if args.workload == "c3" else ""),
+            "config": dict({"workload": wl_desc % args.gb, "workload_id": args.workload,
+                            "parallelism": "files sharded, dp%d" % world,
+                            "rules_compile_s": round(t_compile, 2)}, **config_extra),
             "roofline": {"bound": "hbm", "kernel": "filter_kernel (K1)", "achieved": round(achieved, 2),
                          "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 4),
                          "traffic": traffic},
             "cpu_baseline": cpu,
-            "breakdown_ms": {k: round(last[k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel",
-                                                           "ms_verify_kernel", "ms_fullscan_kernel",
-                                                           "ms_gpu_total",
-                                                           "ms_host_gpu_phase", "ms_host_allow_path",
-                                                           "ms_host_exact", "ms_host_total")},
-            "counts": {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "candidates", "special_files",
-                                                 "findings")},
+            "breakdown_ms": breakdown,
+            "counts": counts,
             "gen_s": round(t_gen, 2),
         }
         print(json.dumps(out), flush=True)
+    if cfg_path:
+        os.remove(cfg_path)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -15,6 +15,14 @@ int64_t tsg_corpus_plan(uint64_t seed, uint64_t target_bytes, uint64_t* offsets,
 int tsg_corpus_fill(uint64_t seed, const uint64_t* offsets, uint64_t n_files, const char* pool,
                     const uint64_t* pool_off, uint32_t n_pool, double secrets_per_byte, uint8_t* arena,
                     char* paths, uint32_t path_stride, int threads);
+/* BASELINE configs[3] (C4): an uncompressed ustar image layer of many small
+ * files (log-normal sizes, median 1.5 KiB, sigma 1.2) with distro-like paths
+ * (allow-listed system dirs, executables, .pyc files, skipped extensions, app
+ * files with 5 % CRLF), directory / symlink / whiteout entries.  Returns the
+ * archive size (out == NULL: the size needed), -1 if cap is too small. */
+int64_t tsg_corpus_layer(uint64_t seed, uint64_t target_file_bytes, const char* pool, const uint64_t* pool_off,
+                         uint32_t n_pool, double secrets_per_byte, uint8_t* out, uint64_t cap, int threads,
+                         uint64_t* n_entries);
 #ifdef __cplusplus
 }
 #endif

@@ -227,3 +227,44 @@ def test_gpu_analyze_layer_vs_oracle(fmt):
         s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
     assert [_norm_secret(s) for s in got.Secrets] == want
     assert len(want) > 5 and st["added"] > 100
+
+
+# ---- BASELINE configs[3] (C4): the native layer generator's archives -----------
+def test_native_walk_generated_layer_vs_oracle(host_analyzer):
+    """The bench's C4 layers (native ustar writer, distro-like paths) walk identically."""
+    from trivy_amd import corpus
+    from trivy_amd.analyzer.secret import Collector, _CTarStats
+    layer = corpus.generate_layer(3_000_000, seed=corpus.SEED + 9)
+    o = oan.SecretAnalyzer(str(ADIR / "testdata/skip-tests-config.yaml"))
+    files, wh, opq = oan.walk_layer_tar(layer.tobytes())
+    want = [a for a in (o.prepare(fp, "", b) for fp, sz, b in files if o.required(fp, sz)) if a is not None]
+    st = _CTarStats()
+    coll = Collector(host_analyzer, 1 << 20)
+    got, cursor = [], 0
+    while True:
+        rc, cursor = coll.add_tar(layer, cursor, st)
+        got += [coll.file(i) for i in range(coll.files())]
+        coll.reset()
+        if rc == 0:
+            break
+    assert got == want
+    assert st.whiteouts == wh and len(want) > 300
+    assert any(b for _, _, b in want)  # .pyc-like binaries scanned through printable runs
+    assert any(b"\r" in f[2] for f in files)  # CRLF files present (stripped in want)
+
+
+@pytest.mark.gpu
+def test_gpu_analyze_generated_layer_vs_oracle():
+    from trivy_amd import corpus
+    from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
+    layer = corpus.generate_layer(1_500_000, seed=corpus.SEED + 4, secrets_per_byte=1.0 / 8192)
+    a = SecretAnalyzer()
+    a.Init(AnalyzerOptions())
+    got = a.AnalyzeLayer(layer, arena_bytes=256 << 10)
+    got.Sort()
+    want = oan.analyze_layer(oan.SecretAnalyzer(""), layer.tobytes())
+    want.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
+    for s in want:
+        s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
+    assert [_norm_secret(s) for s in got.Secrets] == want
+    assert len(want) > 20

@@ -134,3 +134,32 @@ def test_pipelined_scans_match_sync(secret):
     pend = [s.scan_arena_async(a, o, p) for a, o, p in batches]
     got = [pd.wait().raw() for pd in pend]
     assert got == want
+
+
+def _c3_files(samples, seed, n):
+    """C2-style files with C3 rule samples (and near-misses) planted."""
+    rng = random.Random(seed)
+    files = []
+    for p, b in make_corpus(seed, n):
+        parts = [_strip_cr(b)]
+        for _ in range(rng.randint(0, 3)):
+            s = rng.choice(samples)
+            r = rng.random()
+            if r < 0.2:
+                s = s[:len(s) // 2]  # truncated: no match
+            elif r < 0.3:
+                s = s.upper()
+            parts.insert(rng.randint(0, len(parts)), rng.choice([b" ", b"\n", b"x=", b""]) + s +
+                         rng.choice([b" ", b"\n", b'"', b""]))
+        files.append((p, b"".join(parts)))
+    return files
+
+
+def test_c3_generated_rules_corpus(secret, tmp_path):
+    """BASELINE configs[2]: 2,000 generated custom rules appended to the builtins."""
+    from trivy_amd.corpus import c3_rules
+    y, samples = c3_rules()
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(y)
+    n = _compare_corpus(secret, _c3_files(samples, 17, 150), str(cfg))
+    assert n > 50

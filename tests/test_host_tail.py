@@ -126,3 +126,21 @@ def test_host_tail_lazy_keyword_gate(tmp_path):
     o = osc.new_scanner(osc.parse_config(str(cfg_path)))
     for (p, b), g in zip(files, got):
         assert g.to_dict() == o.scan(p, b), p
+
+
+def test_host_tail_c3_generated_rules(tmp_path):
+    """The exact tail with 2,087 rules (BASELINE configs[2]) vs the oracle."""
+    from trivy_amd.corpus import c3_rules
+    from tests.test_gpu_parity import _c3_files
+    y, samples = c3_rules()
+    p = tmp_path / "trivy-secret.yaml"
+    p.write_text(y)
+    files = _c3_files(samples, 23, 40)
+    got = host_tail_scan(ParseConfig(str(p)), files)
+    o = osc.new_scanner(osc.parse_config(str(p)))
+    n = 0
+    for (path, b), g in zip(files, got):
+        want = o.scan(path, b)
+        assert g.to_dict() == want, path
+        n += len(want["Findings"] or [])
+    assert n > 10

@@ -199,29 +199,30 @@ class Collector:
         return [self.file(i)[0] for i in range(self.files())]
 
     def submit(self) -> "PendingBatch":
-        paths = self.paths()
         h = c.c_void_p()
         if self._L.tsg_collector_submit(self._h, c.byref(h)) != 0:
             raise RuntimeError("tsg_collector_submit failed: %s" % _lib.last_error())
-        return PendingBatch(self, h, paths)
+        return PendingBatch(self, h)
 
     def reset(self):
         self._L.tsg_collector_reset(self._h)
 
 
 class PendingBatch:
-    def __init__(self, coll: Collector, h, paths):
-        self.coll, self._h, self.paths = coll, h, paths
+    def __init__(self, coll: Collector, h):
+        self.coll, self._h = coll, h
 
-    def wait(self) -> List[Optional[Secret]]:
-        """Per batch file: the Secret when it has findings (Analyze's result), else None."""
+    def wait(self, materialize: bool = True):
+        """Per batch file: the Secret when it has findings (Analyze's result), else None.
+        materialize=False: only the batch's tsg_stats (dict), no per-file objects."""
         r = c.c_void_p()
         rc = self.coll._L.tsg_scan_wait(self._h, c.byref(r))
         self._h = None
         if rc != 0:
             raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
         res = ScanResult(_ScannerRef(self.coll._L), r)
-        out = [s if s.Findings else None for s in res.secrets(self.paths)]
+        out = ([s if s.Findings else None for s in res.secrets(self.coll.paths())] if materialize
+               else res.stats())
         del res
         self.coll.reset()
         return out
@@ -317,13 +318,24 @@ class SecretAnalyzer:
         flush()
         return out
 
-    def AnalyzeLayer(self, layer, arena_bytes: int = 256 << 20, stats: Optional[dict] = None) -> AnalysisResult:
+    def AnalyzeLayer(self, layer, arena_bytes: int = 256 << 20, stats: Optional[dict] = None,
+                     materialize: bool = True, colls: Optional[List[Collector]] = None) -> AnalysisResult:
         """Every regular file of an uncompressed tar layer (bytes or a uint8 numpy array),
         as the image artifact's AnalyzeFile(dir="") would run it.  Two collectors alternate:
-        one is being filled while the other's batch is on the GPU."""
+        one is being filled while the other's batch is on the GPU.  materialize=False
+        (bench): findings stay in the engine; stats gets the summed scan counters."""
         result = AnalysisResult()
+        scan_tot: dict = {}
+
+        def take(p):
+            out = p.wait(materialize)
+            if materialize:
+                result.Secrets.extend(sec for sec in out if sec is not None)
+            else:
+                for k2, v in out.items():
+                    scan_tot[k2] = scan_tot.get(k2, 0) + v
         st = _CTarStats()
-        colls = [Collector(self, arena_bytes), Collector(self, arena_bytes)]
+        colls = colls or [Collector(self, arena_bytes), Collector(self, arena_bytes)]
         pending = None
         cursor, k, done = 0, 0, False
         while not done:
@@ -334,17 +346,14 @@ class SecretAnalyzer:
                 raise RuntimeError("tar layer: an entry does not fit an empty collector")
             nxt = coll.submit() if coll.files() else None
             if pending is not None:
-                for sec in pending.wait():
-                    if sec is not None:
-                        result.Secrets.append(sec)
+                take(pending)
             pending = nxt
             k ^= 1
         if pending is not None:
-            for sec in pending.wait():
-                if sec is not None:
-                    result.Secrets.append(sec)
+            take(pending)
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
+            stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})
         return result
 
 

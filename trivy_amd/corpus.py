@@ -64,3 +64,96 @@ def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=Non
     L.tsg_corpus_fill(seed, offs.ctypes.data, n, blob, poff.ctypes.data, len(samples), float(secrets_per_byte),
                       arena.ctypes.data, paths.ctypes.data, PATH_STRIDE, threads)
     return Corpus(arena, offs, paths)
+
+
+# ---- BASELINE configs[2] (C3): 2,000 generated custom rules ----
+_C3_OPS = ["=", ">", ":=", "||:", "<=", "=>", ":"]
+
+
+def c3_rules(n_rules=2000, seed=SEED, planted_share=0.10):
+    """A trivy-secret.yaml text with n_rules custom rules and planted sample matches.
+
+    60 %: generic assignment form (secret group), 40 %: literal-prefix token form;
+    secret length L in [16, 64]; 1-3 keywords (4-12 chars, the first being the
+    rule's literal); samples for `planted_share` of the rules.  Returns
+    (yaml_text, [sample bytes])."""
+    import random
+    rng = random.Random(seed ^ 0xC3)
+    alnum = "abcdefghijklmnopqrstuvwxyz0123456789"
+    lines = ["rules:"]
+    samples = []
+    for i in range(n_rules):
+        L = rng.randint(16, 64)
+        generic = rng.random() < 0.6
+        lit = ("kw%04d" % i) if generic else ("pfx%04d_" % i)
+        kws = [lit] + ["".join(rng.choice(alnum) for _ in range(rng.randint(4, 12)))
+                       for _ in range(rng.randint(0, 2))]
+        if generic:
+            rx = (r"(?i)(?P<key>%s[a-z0-9_ .\-,]{0,25})(=|>|:=|\|\|:|<=|=>|:).{0,5}['\"]"
+                  r"(?P<secret>[a-z0-9]{%d})['\"]" % (lit, L))
+        else:
+            rx = r"%s[A-Za-z0-9]{%d}" % (lit, L)
+        lines += ["  - id: c3-rule-%04d" % i, "    category: Generated", "    title: Generated rule %d" % i,
+                  "    severity: %s" % rng.choice(["LOW", "MEDIUM", "HIGH", "CRITICAL"]),
+                  "    regex: '%s'" % rx.replace("'", "''"),
+                  "    keywords: [%s]" % ", ".join(kws)]
+        if generic:
+            lines.append("    secret-group-name: secret")
+        if rng.random() < planted_share:
+            for _ in range(3):
+                if generic:
+                    key = lit.upper() if rng.random() < 0.3 else lit
+                    key += "".join(rng.choice("abcdefghijklmnopqrstuvwxyz0123456789_ .-,")
+                                   for _ in range(rng.randint(0, 8)))
+                    q = rng.choice("'\"")
+                    s = "%s%s%s%s%s%s" % (key, rng.choice(_C3_OPS), " " * rng.randint(0, 3), q,
+                                          "".join(rng.choice(alnum) for _ in range(L)), q)
+                else:
+                    s = lit + "".join(rng.choice(alnum + alnum.upper()[:26]) for _ in range(L))
+                samples.append(s.encode())
+    return "\n".join(lines) + "\n", samples
+
+
+def generate_c3(target_bytes, rule_samples, seed=SEED, secrets_per_byte=1.0 / 262144, threads=None):
+    """The C2 generator with the C3 rules' samples added to the planted pool."""
+    L = _lib.lib()
+    _declare(L)
+    n = L.tsg_corpus_plan(seed, int(target_bytes), None, 0)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    L.tsg_corpus_plan(seed, int(target_bytes), offs.ctypes.data, n + 1)
+    pool = json.loads(POOL.read_text())
+    samples = [s.encode() for v in pool.values() for s in v] + list(rule_samples)
+    blob = b"".join(samples)
+    poff = np.zeros(len(samples) + 1, dtype=np.uint64)
+    poff[1:] = np.cumsum([len(s) for s in samples])
+    total = int(offs[-1])
+    arena = np.zeros(total + 64, dtype=np.uint8)
+    paths = np.zeros(n * PATH_STRIDE, dtype=np.uint8)
+    threads = threads or int(os.environ.get("TSG_HOST_THREADS", "16"))
+    L.tsg_corpus_fill(seed, offs.ctypes.data, n, blob, poff.ctypes.data, len(samples), float(secrets_per_byte),
+                      arena.ctypes.data, paths.ctypes.data, PATH_STRIDE, threads)
+    return Corpus(arena, offs, paths)
+
+
+# ---- BASELINE configs[3] (C4): image layers of millions of small files ----
+def generate_layer(target_file_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=None):
+    """An uncompressed ustar layer (uint8 numpy array) holding ~target_file_bytes of file data."""
+    L = _lib.lib()
+    L.tsg_corpus_layer.restype = c.c_int64
+    L.tsg_corpus_layer.argtypes = [c.c_uint64, c.c_uint64, c.c_char_p, c.c_void_p, c.c_uint32, c.c_double,
+                                   c.c_void_p, c.c_uint64, c.c_int, c.POINTER(c.c_uint64)]
+    pool = json.loads(POOL.read_text())
+    samples = [s.encode() for v in pool.values() for s in v]
+    blob = b"".join(samples)
+    poff = np.zeros(len(samples) + 1, dtype=np.uint64)
+    poff[1:] = np.cumsum([len(s) for s in samples])
+    ne = c.c_uint64()
+    total = L.tsg_corpus_layer(seed, int(target_file_bytes), blob, poff.ctypes.data, len(samples),
+                               float(secrets_per_byte), None, 0, 1, c.byref(ne))
+    out = np.empty(total, dtype=np.uint8)
+    threads = threads or int(os.environ.get("TSG_HOST_THREADS", "16"))
+    r = L.tsg_corpus_layer(seed, int(target_file_bytes), blob, poff.ctypes.data, len(samples),
+                           float(secrets_per_byte), out.ctypes.data, total, threads, c.byref(ne))
+    if r != total:
+        raise RuntimeError("tsg_corpus_layer failed")
+    return out

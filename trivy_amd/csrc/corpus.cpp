@@ -172,6 +172,154 @@ uint64_t FileSize(uint64_t seed, uint64_t i) {
   return uint64_t(s);
 }
 
+// One file's content (the class draw, planted secrets, lines) into o.
+void FillContent(Rng& r, Out& o, const char* pool, const uint64_t* pool_off, uint32_t n_pool,
+                 double secrets_per_byte) {
+  const uint64_t fs = 0, fe = o.cap;
+  uint32_t cls = r.Below(100);
+  // planted secrets: Poisson(size * rate) positions
+  double lam = double(fe - fs) * secrets_per_byte;
+  std::vector<uint64_t> plant;
+  {
+    double l = std::exp(-lam), p = 1.0;
+    int k = 0;
+    if (lam > 30) k = int(lam + std::sqrt(lam) * r.Normal());
+    else
+      for (;;) {
+        p *= r.U();
+        if (p < l) break;
+        k++;
+      }
+    for (int j = 0; j < k && n_pool; j++) plant.push_back(r.Next() % (fe - fs));
+    std::sort(plant.begin(), plant.end());
+  }
+  size_t pi = 0;
+  while (!o.Full()) {
+    while (pi < plant.size() && plant[pi] <= o.n) {
+      uint32_t s = r.Below(n_pool);
+      static const char* pre[] = {" ", "export TOKEN=", "key: \"", "\t", "= '", "", "(\""};
+      o.Put(pre[r.Below(7)]);
+      o.Put(pool + pool_off[s], size_t(pool_off[s + 1] - pool_off[s]));
+      o.C(r.Below(2) ? '\n' : ' ');
+      pi++;
+    }
+    uint32_t t = LineTarget(r);
+    if (cls < 70) SourceLine(o, r, t);
+    else if (cls < 90) ProseLine(o, r, t, false);
+    else if (cls < 98) BlobLine(o, r, cls % 3);
+    else ProseLine(o, r, t, true);
+  }
+}
+
+
+// ---- C4: an uncompressed image layer (ustar) of many small files ----------
+struct LayerEntry {
+  uint64_t hdr;   // header offset in the archive
+  uint64_t size;  // data bytes
+  uint8_t kind;   // 0 text, 1 CRLF text, 2 ELF-like binary, 3 .pyc-like, 4 dir, 5 symlink, 6 whiteout
+  std::string path;
+};
+
+const char* kPkgs[] = {"openssl", "curl", "bash", "coreutils", "nginx", "python3", "zlib", "libssl", "apt",
+                       "dpkg", "tzdata", "ca-certificates", "perl", "git", "node", "redis", "postgres", "sed"};
+const char* kAppDirs[] = {"opt/app/src", "srv/api/handlers", "home/app/project", "var/www/html", "app/services",
+                          "etc", "root", "opt/tools/scripts", "workspace/lib", "srv/config"};
+
+// Layer plan: per file SplitMix64(seed ^ i): size log-normal (median 1.5 KiB,
+// sigma 1.2, clipped [10 B, 10 MiB]) and a path mimicking a distro tree.
+std::vector<LayerEntry> PlanLayer(uint64_t seed, uint64_t target_file_bytes) {
+  std::vector<LayerEntry> v;
+  uint64_t total = 0, off = 0;
+  std::string last_dir;
+  Rng g(seed ^ 0xC4C4C4C4ull);  // directory groups: a new one every ~24 files
+  uint64_t group = 0;
+  for (uint64_t i = 0; total < target_file_bytes; i++) {
+    Rng r(seed ^ (i * 0xA24BAED4963EE407ull) ^ 0xC4C4C4C4ull);
+    if (g.Below(24) == 0) group++;
+    Rng gr(seed ^ (group * 0x9FB21C651E98DF25ull));
+    double z = r.Normal();
+    double sz = 1536.0 * std::exp(1.2 * z);
+    sz = std::min(std::max(sz, 10.0), 10485760.0);
+    uint64_t size = uint64_t(sz);
+    const uint32_t pk = gr.Below(1000);
+    const char* pkg = kPkgs[gr.Below(sizeof(kPkgs) / sizeof(kPkgs[0]))];
+    const char* ad = kAppDirs[gr.Below(sizeof(kAppDirs) / sizeof(kAppDirs[0]))];
+    const unsigned sub = unsigned(gr.Below(1000));
+    char buf[128];
+    uint8_t kind = 0;
+    std::string dir;
+    if (pk < 300) {  // allow-listed system dirs (Required skips them by path)
+      static const char* sys[] = {"usr/share/doc/", "usr/lib/x86_64-linux-gnu/", "usr/include/", "usr/share/zoneinfo/"};
+      dir = std::string(sys[pk % 4]) + pkg + "/d" + std::to_string(sub);
+      snprintf(buf, sizeof buf, "%s/f%llu.txt", dir.c_str(), (unsigned long long)i);
+    } else if (pk < 360) {  // executables
+      dir = std::string(pk < 330 ? "usr/bin" : "usr/sbin");
+      snprintf(buf, sizeof buf, "%s/%s-%llu", dir.c_str(), pkg, (unsigned long long)i);
+      kind = 2;
+    } else if (pk < 380) {  // compiled python (binary, scanned via printable runs)
+      dir = std::string("opt/app/venv/") + pkg + std::to_string(sub) + "/__pycache__";
+      snprintf(buf, sizeof buf, "%s/m%llu.cpython-311.pyc", dir.c_str(), (unsigned long long)i);
+      kind = 3;
+    } else if (pk < 410) {  // skipped extensions
+      dir = std::string("usr/local/share/") + pkg + "/img" + std::to_string(sub);
+      snprintf(buf, sizeof buf, "%s/i%llu%s", dir.c_str(), (unsigned long long)i, pk < 395 ? ".png" : ".gz");
+      kind = 2;
+    } else {
+      dir = std::string(ad) + "/" + pkg + "/m" + std::to_string(sub);
+      snprintf(buf, sizeof buf, "%s/file%llu%s", dir.c_str(), (unsigned long long)i,
+               kExt[r.Below(sizeof(kExt) / sizeof(kExt[0]))]);
+      kind = r.Below(100) < 5 ? 1 : 0;
+    }
+    if (dir != last_dir) {  // a directory entry when the walk changes directory
+      v.push_back({off, 0, 4, dir + "/"});
+      off += 512;
+      last_dir = dir;
+    }
+    if (r.Below(500) == 0) {  // whiteout / symlink entries
+      v.push_back({off, 0, uint8_t(r.Below(2) ? 5 : 6), dir + (r.Below(2) ? "/.wh.old" : "/link")});
+      off += 512;
+    }
+    if (total + size > target_file_bytes) size = target_file_bytes - total;
+    if (size == 0) break;
+    v.push_back({off, size, kind, std::string(buf)});
+    off += 512 + ((size + 511) & ~uint64_t(511));
+    total += size;
+  }
+  return v;
+}
+
+void Octal(char* dst, int width, uint64_t v) {  // width-1 octal digits + NUL
+  for (int k = width - 2; k >= 0; k--) {
+    dst[k] = char('0' + (v & 7));
+    v >>= 3;
+  }
+  dst[width - 1] = 0;
+}
+
+void WriteHeader(uint8_t* h, const LayerEntry& e) {
+  std::memset(h, 0, 512);
+  std::string name = e.path, prefix;
+  if (name.size() > 100) {  // ustar prefix split at a '/'
+    size_t k = name.rfind('/', 154);
+    prefix = name.substr(0, k);
+    name = name.substr(k + 1);
+  }
+  std::memcpy(h, name.data(), std::min<size_t>(name.size(), 100));
+  Octal(reinterpret_cast<char*>(h + 100), 8, e.kind == 4 ? 0755 : 0644);
+  Octal(reinterpret_cast<char*>(h + 108), 8, 0);
+  Octal(reinterpret_cast<char*>(h + 116), 8, 0);
+  Octal(reinterpret_cast<char*>(h + 124), 12, e.size);
+  Octal(reinterpret_cast<char*>(h + 136), 12, 1700000000);
+  h[156] = e.kind == 4 ? '5' : e.kind == 5 ? '2' : '0';
+  if (e.kind == 5) std::memcpy(h + 157, "../target", 9);
+  std::memcpy(h + 257, "ustar\0" "00", 8);
+  std::memcpy(h + 345, prefix.data(), std::min<size_t>(prefix.size(), 155));
+  std::memset(h + 148, ' ', 8);
+  uint32_t sum = 0;
+  for (int k = 0; k < 512; k++) sum += h[k];
+  Octal(reinterpret_cast<char*>(h + 148), 7, sum);
+  h[155] = ' ';
+}
 }  // namespace
 
 extern "C" {
@@ -203,39 +351,7 @@ int tsg_corpus_fill(uint64_t seed, const uint64_t* offsets, uint64_t n_files, co
         Rng r(seed ^ (i * 0x9E3779B97F4A7C15ull) ^ 0xA5A5A5A5ull);
         uint64_t fs = offsets[i], fe = offsets[i + 1];
         Out o{arena + fs, 0, fe - fs};
-        uint32_t cls = r.Below(100);
-        // planted secrets: Poisson(size * rate) positions
-        double lam = double(fe - fs) * secrets_per_byte;
-        std::vector<uint64_t> plant;
-        {
-          double l = std::exp(-lam), p = 1.0;
-          int k = 0;
-          if (lam > 30) k = int(lam + std::sqrt(lam) * r.Normal());
-          else
-            for (;;) {
-              p *= r.U();
-              if (p < l) break;
-              k++;
-            }
-          for (int j = 0; j < k && n_pool; j++) plant.push_back(r.Next() % (fe - fs));
-          std::sort(plant.begin(), plant.end());
-        }
-        size_t pi = 0;
-        while (!o.Full()) {
-          while (pi < plant.size() && plant[pi] <= o.n) {
-            uint32_t s = r.Below(n_pool);
-            static const char* pre[] = {" ", "export TOKEN=", "key: \"", "\t", "= '", "", "(\""};
-            o.Put(pre[r.Below(7)]);
-            o.Put(pool + pool_off[s], size_t(pool_off[s + 1] - pool_off[s]));
-            o.C(r.Below(2) ? '\n' : ' ');
-            pi++;
-          }
-          uint32_t t = LineTarget(r);
-          if (cls < 70) SourceLine(o, r, t);
-          else if (cls < 90) ProseLine(o, r, t, false);
-          else if (cls < 98) BlobLine(o, r, cls % 3);
-          else ProseLine(o, r, t, true);
-        }
+        FillContent(r, o, pool, pool_off, n_pool, secrets_per_byte);
         if (paths) {
           char* P = paths + i * path_stride;
           uint32_t pk = r.Below(100);
@@ -252,6 +368,68 @@ int tsg_corpus_fill(uint64_t seed, const uint64_t* offsets, uint64_t n_files, co
   work();
   for (auto& th : pool_t) th.join();
   return 0;
+}
+
+int64_t tsg_corpus_layer(uint64_t seed, uint64_t target_file_bytes, const char* pool, const uint64_t* pool_off,
+                         uint32_t n_pool, double secrets_per_byte, uint8_t* out, uint64_t cap, int threads,
+                         uint64_t* n_entries) {
+  const std::vector<LayerEntry> plan = PlanLayer(seed, target_file_bytes);
+  const uint64_t end = plan.empty() ? 0 : plan.back().hdr + 512 + ((plan.back().size + 511) & ~uint64_t(511));
+  const uint64_t total = end + 1024;  // two zero blocks
+  if (n_entries) *n_entries = plan.size();
+  if (!out) return int64_t(total);
+  if (cap < total) return -1;
+  if (threads <= 0) threads = 1;
+  std::atomic<uint64_t> next{0};
+  auto work = [&]() {
+    std::vector<uint8_t> tmp;
+    for (;;) {
+      const uint64_t lo = next.fetch_add(512);
+      if (lo >= plan.size()) break;
+      const uint64_t hi = std::min<uint64_t>(lo + 512, plan.size());
+      for (uint64_t i = lo; i < hi; i++) {
+        const LayerEntry& e = plan[i];
+        uint8_t* h = out + e.hdr;
+        WriteHeader(h, e);
+        uint8_t* d = h + 512;
+        const uint64_t padded = (e.size + 511) & ~uint64_t(511);
+        std::memset(d + e.size, 0, size_t(padded - e.size));
+        if (!e.size) continue;
+        Rng r(seed ^ (i * 0x9E3779B97F4A7C15ull) ^ 0x5A5A5A5Aull);
+        if (e.kind == 0 || e.kind == 3) {
+          Out o{d, 0, e.size};
+          FillContent(r, o, pool, pool_off, n_pool, secrets_per_byte);
+          if (e.kind == 3) {  // .pyc-like: a binary header and NULs between text runs
+            static const uint8_t magic[8] = {0xA7, 0x0D, 0x0D, 0x0A, 0, 0, 0, 0};
+            std::memcpy(d, magic, std::min<uint64_t>(8, e.size));
+            for (uint64_t k = 8; k < e.size; k += 16 + r.Below(48)) d[k] = 0;
+          }
+        } else if (e.kind == 1) {  // CRLF text: generate, then expand '\n' -> "\r\n" up to the size
+          tmp.assign(size_t(e.size), 0);
+          Out o{tmp.data(), 0, e.size};
+          FillContent(r, o, pool, pool_off, n_pool, secrets_per_byte);
+          uint64_t w = 0;
+          for (uint64_t k = 0; k < e.size && w < e.size; k++) {
+            if (tmp[k] == '\n') {
+              d[w++] = '\r';
+              if (w >= e.size) break;
+            }
+            d[w++] = tmp[k];
+          }
+        } else {  // ELF-like binary
+          static const uint8_t elf[8] = {0x7F, 'E', 'L', 'F', 2, 1, 1, 0};
+          for (uint64_t k = 0; k < e.size; k++) d[k] = uint8_t(r.Next());
+          std::memcpy(d, elf, std::min<uint64_t>(8, e.size));
+        }
+      }
+    }
+  };
+  std::vector<std::thread> pool_t;
+  for (int t = 1; t < threads; t++) pool_t.emplace_back(work);
+  work();
+  for (auto& th : pool_t) th.join();
+  std::memset(out + end, 0, 1024);
+  return int64_t(total);
 }
 
 }  // extern "C"

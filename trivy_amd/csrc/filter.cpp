@@ -41,22 +41,44 @@ const std::vector<double>& BytePrior() {
 
 namespace {
 
-double SetProb(const ByteSet& s) {
-  if (s.all()) return 1.0;
-  const auto& f = BytePrior();
-  double p = 0;
+// 256-bit byte set as four words (the clustering's working type).
+struct B256 {
+  uint64_t w[4];
+  void set_all() { w[0] = w[1] = w[2] = w[3] = ~uint64_t(0); }
+  bool test(int b) const { return (w[b >> 6] >> (b & 63)) & 1; }
+  bool all() const { return (w[0] & w[1] & w[2] & w[3]) == ~uint64_t(0); }
+};
+B256 ToB256(const ByteSet& s) {
+  B256 r{};
   for (int b = 0; b < 256; b++)
-    if (s.test(b)) p += f[b];
+    if (s.test(size_t(b))) r.w[b >> 6] |= uint64_t(1) << (b & 63);
+  return r;
+}
+
+// P(byte in s) under the prior: 32 lookups of 8-byte groups.
+double SetProb(const B256& s) {
+  static const std::vector<double> T = [] {  // T[g * 256 + m] = prior mass of mask m over bytes 8g..8g+7
+    const auto& f = BytePrior();
+    std::vector<double> t(32 * 256, 0.0);
+    for (int g = 0; g < 32; g++)
+      for (int m = 0; m < 256; m++)
+        for (int k = 0; k < 8; k++)
+          if ((m >> k) & 1) t[size_t(g) * 256 + size_t(m)] += f[size_t(8 * g + k)];
+    return t;
+  }();
+  if (s.all()) return 1.0;
+  double p = 0;
+  for (int g = 0; g < 32; g++) p += T[size_t(g) * 256 + ((s.w[g >> 3] >> (8 * (g & 7))) & 0xFF)];
   return std::min(p, 1.0);
 }
 
 struct Cluster {
-  ByteSet u[kFilterSlots];
+  B256 u[kFilterSlots];
   std::vector<uint32_t> members;
   double cost = 0;
 };
 
-double Cost(const ByteSet* u) {
+double Cost(const B256* u) {
   double c = 1.0;
   for (int s = 0; s < kFilterSlots; s++) c *= SetProb(u[s]);  // unused slots stay "any" (P = 1)
   return c;
@@ -113,14 +135,14 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     double best = std::numeric_limits<double>::infinity();
     for (size_t s = 0; s + wl <= m; s++) {
       double c = 1.0;
-      for (size_t q = s; q < s + wl; q++) c *= SetProb(it.sets[q]);
+      for (size_t q = s; q < s + wl; q++) c *= SetProb(ToB256(it.sets[q]));
       if (c < best) {
         best = c;
         w = s;
       }
     }
-    for (int s = 0; s < kFilterSlots; s++) cl[i].u[s].set();
-    for (size_t q = 0; q < wl; q++) cl[i].u[S - wl + q] = it.sets[w + q];
+    for (int s = 0; s < kFilterSlots; s++) cl[i].u[s].set_all();
+    for (size_t q = 0; q < wl; q++) cl[i].u[S - wl + q] = ToB256(it.sets[w + q]);
     cl[i].members = {uint32_t(i)};
     cl[i].cost = Cost(cl[i].u);
     FilterItemGpu g{};
@@ -152,32 +174,47 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     }
     out->items.push_back(g);
   }
-  // agglomerative clustering down to n_buckets
+  // agglomerative clustering down to n_buckets: always merge the pair whose
+  // union adds the least estimated fire rate.  Each row caches its best
+  // partner; after a merge only rows whose partner died are rescanned
+  // (O(n^2) in practice instead of a full O(n^2) scan per merge).
   std::vector<bool> alive(n, true);
   size_t n_alive = n;
-  auto merged = [&](const Cluster& a, const Cluster& b, ByteSet* u) {
-    for (int s = 0; s < kFilterSlots; s++) u[s] = a.u[s] | b.u[s];
+  auto merged = [&](const Cluster& a, const Cluster& b, B256* u) {
+    for (int s = 0; s < kFilterSlots; s++)
+      for (int k = 0; k < 4; k++) u[s].w[k] = a.u[s].w[k] | b.u[s].w[k];
     return Cost(u);
   };
-  std::vector<std::vector<double>> delta(n, std::vector<double>(n, 0.0));
+  auto delta_of = [&](size_t i, size_t j) {
+    B256 u[kFilterSlots];
+    return merged(cl[i], cl[j], u) - cl[i].cost - cl[j].cost;
+  };
+  std::vector<double> delta(n > 1 ? n * n : 1, 0.0);  // symmetric, rows of n
   for (size_t i = 0; i < n; i++)
-    for (size_t j = i + 1; j < n; j++) {
-      ByteSet u[kFilterSlots];
-      delta[i][j] = merged(cl[i], cl[j], u) - cl[i].cost - cl[j].cost;
-    }
+    for (size_t j = i + 1; j < n; j++) delta[i * n + j] = delta[j * n + i] = delta_of(i, j);
+  const double kInf = std::numeric_limits<double>::infinity();
+  std::vector<size_t> best(n, 0);
+  std::vector<double> best_d(n, kInf);
+  auto rescan = [&](size_t i) {
+    best_d[i] = kInf;
+    for (size_t j = 0; j < n; j++)
+      if (j != i && alive[j] && delta[i * n + j] < best_d[i]) {
+        best_d[i] = delta[i * n + j];
+        best[i] = j;
+      }
+  };
+  for (size_t i = 0; i < n; i++) rescan(i);
   while (n_alive > n_item_buckets) {
     size_t bi = 0, bj = 0;
-    double bd = std::numeric_limits<double>::infinity();
-    for (size_t i = 0; i < n; i++) {
-      if (!alive[i]) continue;
-      for (size_t j = i + 1; j < n; j++)
-        if (alive[j] && delta[i][j] < bd) {
-          bd = delta[i][j];
-          bi = i;
-          bj = j;
-        }
-    }
-    ByteSet u[kFilterSlots];
+    double bd = kInf;
+    for (size_t i = 0; i < n; i++)
+      if (alive[i] && best_d[i] < bd) {
+        bd = best_d[i];
+        bi = i;
+        bj = best[i];
+      }
+    if (bj < bi) std::swap(bi, bj);
+    B256 u[kFilterSlots];
     double c = merged(cl[bi], cl[bj], u);
     for (int s = 0; s < kFilterSlots; s++) cl[bi].u[s] = u[s];
     cl[bi].cost = c;
@@ -186,10 +223,18 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     n_alive--;
     for (size_t k = 0; k < n; k++) {
       if (!alive[k] || k == bi) continue;
-      ByteSet v[kFilterSlots];
-      double d = merged(cl[bi], cl[k], v) - cl[bi].cost - cl[k].cost;
-      if (k < bi) delta[k][bi] = d;
-      else delta[bi][k] = d;
+      const double d = delta_of(bi, k);
+      delta[k * n + bi] = delta[bi * n + k] = d;
+    }
+    rescan(bi);
+    for (size_t k = 0; k < n; k++) {
+      if (!alive[k] || k == bi) continue;
+      if (best[k] == bi || best[k] == bj) {
+        rescan(k);  // its partner changed or died
+      } else if (delta[k * n + bi] < best_d[k]) {
+        best_d[k] = delta[k * n + bi];
+        best[k] = bi;
+      }
     }
   }
   // reach table
