@@ -77,9 +77,12 @@ class GpuEngine {
   uint32_t* d_group_items_ = nullptr;
   uint32_t* d_bucket_groups_ = nullptr;
   void* d_ftabs_ = nullptr;
+  void* d_fold_pairs_ = nullptr;  // fold kernel work list
+  uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0;
   size_t c_lds_bytes_ = 0;
+  bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;
   uint32_t rec_cap_ = 0, fold_cap_ = 0, n_fitems_ = 0;
   // per-batch buffers

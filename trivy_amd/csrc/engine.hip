@@ -523,6 +523,10 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
 constexpr uint32_t kCQ1 = 256;  // fires (overflow: handled in place)
 constexpr uint32_t kCQ2 = 256;  // candidate items (overflow: checked in place)
 
+// kLdsTabs: the item tables are staged in LDS (they fit: builtin-sized rule
+// sets); otherwise they are read through the caches from global memory
+// (large custom rule sets, e.g. 2,000 generated rules).
+template <bool kLdsTabs>
 __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kCThreads / 64;
@@ -536,19 +540,20 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   uint8_t* s_tabs = reinterpret_cast<uint8_t*>(s_cnt + kWaves * 4);
   const int tid = threadIdx.x;
   load_reach_lds(s_reach, P.reach, 1, tid, blockDim.x);
-  {
+  if (kLdsTabs) {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(s_tabs);
     for (uint32_t i = tid; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
   }
+  const uint8_t* tabs = kLdsTabs ? s_tabs : static_cast<const uint8_t*>(P.tabs);
   const uint32_t lane = tid & 63, wave = tid >> 6;
   uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2
   if (lane < 4) cnt[lane] = 0;
   __syncthreads();
-  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(s_tabs + P.t_items);
-  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(s_tabs + P.t_item_ids);
-  const uint8_t* item_cls = s_tabs + P.t_item_cls;
-  const uint32_t* classes = reinterpret_cast<const uint32_t*>(s_tabs + P.t_classes);
+  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
+  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(tabs + P.t_item_ids);
+  const uint8_t* item_cls = tabs + P.t_item_cls;
+  const uint32_t* classes = reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
   uint8_t* wwin = s_win + wave * 64 * kCWin;  // the wave's 64 windows
   uint64_t* wbase = s_base + wave * 64;      // block base per lane
   uint32_t* q1 = s_q1 + wave * kCQ1;
@@ -713,12 +718,25 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
 // also accepts U+212A (E2 84 AA) when its set holds k/K and U+017F (C5 BF)
 // when it holds s/S (the only non-ASCII runes (?i) folds onto ASCII letters),
 // advancing 3 / 2 bytes.  A superset of the true occurrences; hits carry the
-// literal end in bytes.  One thread per (site, item).
+// literal end in bytes.
+//
+// Work list: a match holds the rune at x only if the position q covering byte
+// x can take it -- its set holds k/K (U+212A) or s/S (U+017F), or the lead
+// byte itself -- and then positions 0..q-1 span [q, max_before] bytes.  The
+// host lists those (item, q) pairs per rune kind; each pair tries only its
+// starts x - max_before .. x - q, and emits only when q is the covering
+// position (so an (item, start) is reported once).
+struct FoldPair {
+  uint32_t item;
+  uint16_t q, max_before;
+};
 struct FoldParams {
   const uint8_t* arena;
   const uint64_t* off;
   const void* tabs;
   uint32_t tabs_bytes, t_items, t_item_ids, t_item_cls, t_classes, n_items;
+  const FoldPair* pairs;  // [k-site pairs | s-site pairs]
+  uint32_t n_pairs_k, n_pairs_s;
   const FoldSite* folds;
   uint32_t fold_cap;
   uint32_t* hits;
@@ -731,19 +749,21 @@ constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each)
 // One workgroup per fold site: the bytes [x - kFoldSpan, x + kFoldSpan) go to
 // LDS, the threads split the (item, start) pairs.  U+0130 sites only flag the
 // file (Go's (?i) does not fold U+0130 onto 'i').
+template <bool kLdsTabs>  // as confirm_kernel
 __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint8_t s_bytes[2 * kFoldSpan + 16];
-  {
+  if (kLdsTabs) {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(smem);
     for (uint32_t i = threadIdx.x; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
   }
   __syncthreads();
-  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(smem + P.t_items);
-  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(smem + P.t_item_ids);
-  const uint8_t* item_cls = smem + P.t_item_cls;
-  const uint32_t* classes = reinterpret_cast<const uint32_t*>(smem + P.t_classes);
+  const uint8_t* tabs = kLdsTabs ? smem : static_cast<const uint8_t*>(P.tabs);
+  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
+  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(tabs + P.t_item_ids);
+  const uint8_t* item_cls = tabs + P.t_item_cls;
+  const uint32_t* classes = reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
   auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
   const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
   for (uint32_t si = blockIdx.x; si < n_folds; si += gridDim.x) {
@@ -755,37 +775,49 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
     for (uint32_t i = threadIdx.x; i < uint32_t(w1 - w0); i += blockDim.x) s_bytes[i] = P.arena[w0 + i];
     __syncthreads();
     if (P.arena[fsite.x] == 0xC4) continue;  // U+0130: uniform per block
-    const uint32_t span = uint32_t(fsite.x - w0) + 1;  // starts w0 .. x
-    const uint32_t total = P.n_items * span;
-    for (uint32_t t = threadIdx.x; t < total; t += blockDim.x) {
-      const FilterItemGpu it = items[t / span];
-      const uint64_t st = w0 + t % span;
-      if (it.kind != kItemAnchor || fsite.x - st > 3ull * it.n) continue;
-      uint64_t p = st, lit_bytes_end = 0;
-      bool ok = true;
-      for (uint32_t q = 0; q < it.n && ok; q++) {
-        if (q == it.lit_end) lit_bytes_end = p;
-        if (p >= w1) {
-          ok = false;
-          break;
+    const bool kay = P.arena[fsite.x] == 0xE2;  // U+212A, else U+017F
+    const FoldPair* pairs = P.pairs + (kay ? 0 : P.n_pairs_k);
+    const uint32_t n_pairs = kay ? P.n_pairs_k : P.n_pairs_s;
+    for (uint32_t t = threadIdx.x; t < n_pairs; t += blockDim.x) {
+      const FoldPair fp = pairs[t];
+      const FilterItemGpu it = items[fp.item];
+      for (uint32_t back = fp.q; back <= fp.max_before; back++) {
+        if (fsite.x < w0 + back) break;
+        const uint64_t st = fsite.x - back;
+        uint64_t p = st, lit_bytes_end = 0;
+        bool ok = true, covered = false;
+        for (uint32_t q = 0; q < it.n && ok; q++) {
+          if (q == it.lit_end) lit_bytes_end = p;
+          if (p >= w1) {
+            ok = false;
+            break;
+          }
+          if (p == fsite.x) {  // the position covering the rune
+            if (q != fp.q) {
+              ok = false;
+              break;
+            }
+            covered = true;
+          }
+          const uint32_t c = item_cls[it.cls_off + q];
+          const uint32_t b = s_bytes[p - w0];
+          if (b == 0xE2 && p + 2 < w1 && s_bytes[p + 1 - w0] == 0x84 && s_bytes[p + 2 - w0] == 0xAA &&
+              (in_cls(c, 'k') || in_cls(c, 'K'))) {
+            p += 3;
+          } else if (b == 0xC5 && p + 1 < w1 && s_bytes[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
+            p += 2;
+          } else if (in_cls(c, b)) {
+            p += 1;
+          } else {
+            ok = false;
+          }
+          if (p > fsite.x && !covered) ok = false;  // skipped over x inside a multi-byte step
         }
-        const uint32_t c = item_cls[it.cls_off + q];
-        const uint32_t b = s_bytes[p - w0];
-        if (b == 0xE2 && p + 2 < w1 && s_bytes[p + 1 - w0] == 0x84 && s_bytes[p + 2 - w0] == 0xAA &&
-            (in_cls(c, 'k') || in_cls(c, 'K'))) {
-          p += 3;
-        } else if (b == 0xC5 && p + 1 < w1 && s_bytes[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
-          p += 2;
-        } else if (in_cls(c, b)) {
-          p += 1;
-        } else {
-          ok = false;
-        }
+        if (!ok || !covered) continue;
+        if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
+        for (uint32_t d = 0; d < it.n_ids; d++)
+          put_hit(P.hits, P.hit_cap, P.counters, fsite.f, uint32_t(lit_bytes_end - fs), item_ids[it.ids_off + d]);
       }
-      if (!ok || p <= fsite.x) continue;  // the item must contain the fold rune
-      if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
-      for (uint32_t d = 0; d < it.n_ids; d++)
-        put_hit(P.hits, P.hit_cap, P.counters, fsite.f, uint32_t(lit_bytes_end - fs), item_ids[it.ids_off + d]);
     }
   }
 }
@@ -925,20 +957,41 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     uint8_t* d = nullptr;
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_ftabs_ = d;
-    c_lds_bytes_ = 4096 + size_t(kCThreads) * (kCWin + 8) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
-                   size_t(kCThreads / 64) * kCWaveHits * 12 + size_t(kCThreads / 64) * 16 + ftabs_bytes_;
-    if (c_lds_bytes_ > 64 * 1024) {
-      err_ = "prefilter tables do not fit in LDS";
-      return;
+    {  // fold work list (FoldParams): (item, q) pairs per rune kind, anchor items only
+      auto in_cls = [&](uint32_t c, uint32_t b) { return (ft->classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
+      std::vector<FoldPair> pk, ps;
+      for (uint32_t i = 0; i < uint32_t(ft->items.size()); i++) {
+        const FilterItemGpu& it = ft->items[i];
+        if (it.kind != kItemAnchor) continue;
+        uint32_t before = 0;  // max bytes of positions 0..q-1
+        for (uint32_t q = 0; q < it.n; q++) {
+          const uint32_t c = ft->item_cls[it.cls_off + q];
+          const bool k = in_cls(c, 'k') || in_cls(c, 'K'), sf = in_cls(c, 's') || in_cls(c, 'S');
+          if (before <= 0xFFFF && (k || in_cls(c, 0xE2))) pk.push_back({i, uint16_t(q), uint16_t(before)});
+          if (before <= 0xFFFF && (sf || in_cls(c, 0xC5))) ps.push_back({i, uint16_t(q), uint16_t(before)});
+          before += k ? 3 : sf ? 2 : 1;
+        }
+      }
+      n_fold_pairs_k_ = uint32_t(pk.size());
+      n_fold_pairs_s_ = uint32_t(ps.size());
+      pk.insert(pk.end(), ps.begin(), ps.end());
+      if (pk.empty()) pk.push_back({0, 0, 0});
+      uint8_t* dp = nullptr;
+      if (!Upload(&err_, &dp, reinterpret_cast<const uint8_t*>(pk.data()), pk.size() * sizeof(FoldPair))) return;
+      d_fold_pairs_ = dp;
     }
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&confirm_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        int(c_lds_bytes_));
+    const size_t fixed = 4096 + size_t(kCThreads) * (kCWin + 8) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
+                         size_t(kCThreads / 64) * kCWaveHits * 12 + size_t(kCThreads / 64) * 16;
+    lds_tabs_ = fixed + ftabs_bytes_ <= 64 * 1024;  // else the item tables stay in global memory
+    c_lds_bytes_ = fixed + (lds_tabs_ ? ftabs_bytes_ : 0);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
   }
 }
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_fold_pairs_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
@@ -1057,7 +1110,12 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.core = d_core_;
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;
-    if (diag_mode_ == 0) confirm_kernel<<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
+    if (diag_mode_ == 0) {
+      if (lds_tabs_)
+        confirm_kernel<true><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
+      else
+        confirm_kernel<false><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[2], stream_));
     // fold runes: fold-tolerant item matching around each one
@@ -1071,12 +1129,20 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.t_item_cls = ft_item_cls_;
     fo.t_classes = ft_classes_;
     fo.n_items = n_fitems_;
+    fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
+    fo.n_pairs_k = n_fold_pairs_k_;
+    fo.n_pairs_s = n_fold_pairs_s_;
     fo.folds = static_cast<const FoldSite*>(d_folds_);
     fo.fold_cap = fold_cap_;
     fo.hits = static_cast<uint32_t*>(d_hits_);
     fo.hit_cap = hit_cap_;
     fo.counters = d_counters_;
-    if (diag_mode_ == 0) fold_kernel<<<512, 256, ftabs_bytes_, stream_>>>(fo);
+    if (diag_mode_ == 0) {
+      if (lds_tabs_)
+        fold_kernel<true><<<512, 256, ftabs_bytes_, stream_>>>(fo);
+      else
+        fold_kernel<false><<<512, 256, 0, stream_>>>(fo);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[3], stream_));
     NfaParams np;
