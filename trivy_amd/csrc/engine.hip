@@ -722,14 +722,16 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
 //
 // Work list: a match holds the rune at x only if the position q covering byte
 // x can take it -- its set holds k/K (U+212A) or s/S (U+017F), or the lead
-// byte itself -- and then positions 0..q-1 span [q, max_before] bytes.  The
-// host lists those (item, q) pairs per rune kind; each pair tries only its
-// starts x - max_before .. x - q, and emits only when q is the covering
-// position (so an (item, start) is reported once).
+// byte itself -- and then positions 0..q-1 span at least q and at most
+// max_before(q) bytes.  The host lists, per rune kind, the items with such a
+// position and the start range [x - hi, x - lo] over all of them (lo = the
+// first capable q, hi = max_before of the last), cut into tasks of at most
+// kFoldTaskStarts starts; each start is tried once.
 struct FoldPair {
   uint32_t item;
-  uint16_t q, max_before;
+  uint16_t lo, hi;
 };
+constexpr int kFoldTaskStarts = 12;  // starts per fold task
 struct FoldParams {
   const uint8_t* arena;
   const uint64_t* off;
@@ -778,10 +780,12 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
     const bool kay = P.arena[fsite.x] == 0xE2;  // U+212A, else U+017F
     const FoldPair* pairs = P.pairs + (kay ? 0 : P.n_pairs_k);
     const uint32_t n_pairs = kay ? P.n_pairs_k : P.n_pairs_s;
+    // one task per (item, <= kFoldTaskStarts consecutive starts): bounded,
+    // balanced work without a per-start lookup of its item
     for (uint32_t t = threadIdx.x; t < n_pairs; t += blockDim.x) {
       const FoldPair fp = pairs[t];
       const FilterItemGpu it = items[fp.item];
-      for (uint32_t back = fp.q; back <= fp.max_before; back++) {
+      for (uint32_t back = fp.lo; back <= fp.hi; back++) {
         if (fsite.x < w0 + back) break;
         const uint64_t st = fsite.x - back;
         uint64_t p = st, lit_bytes_end = 0;
@@ -792,13 +796,7 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
             ok = false;
             break;
           }
-          if (p == fsite.x) {  // the position covering the rune
-            if (q != fp.q) {
-              ok = false;
-              break;
-            }
-            covered = true;
-          }
+          covered = covered || p == fsite.x;
           const uint32_t c = item_cls[it.cls_off + q];
           const uint32_t b = s_bytes[p - w0];
           if (b == 0xE2 && p + 2 < w1 && s_bytes[p + 1 - w0] == 0x84 && s_bytes[p + 2 - w0] == 0xAA &&
@@ -811,7 +809,6 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
           } else {
             ok = false;
           }
-          if (p > fsite.x && !covered) ok = false;  // skipped over x inside a multi-byte step
         }
         if (!ok || !covered) continue;
         if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
@@ -964,13 +961,27 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
         const FilterItemGpu& it = ft->items[i];
         if (it.kind != kItemAnchor) continue;
         uint32_t before = 0;  // max bytes of positions 0..q-1
+        int64_t klo = -1, khi = -1, slo = -1, shi = -1;
         for (uint32_t q = 0; q < it.n; q++) {
           const uint32_t c = ft->item_cls[it.cls_off + q];
           const bool k = in_cls(c, 'k') || in_cls(c, 'K'), sf = in_cls(c, 's') || in_cls(c, 'S');
-          if (before <= 0xFFFF && (k || in_cls(c, 0xE2))) pk.push_back({i, uint16_t(q), uint16_t(before)});
-          if (before <= 0xFFFF && (sf || in_cls(c, 0xC5))) ps.push_back({i, uint16_t(q), uint16_t(before)});
+          if (k || in_cls(c, 0xE2)) {
+            if (klo < 0) klo = q;
+            khi = before;
+          }
+          if (sf || in_cls(c, 0xC5)) {
+            if (slo < 0) slo = q;
+            shi = before;
+          }
           before += k ? 3 : sf ? 2 : 1;
         }
+        auto add = [&](std::vector<FoldPair>& v, int64_t lo, int64_t hi) {  // split into bounded tasks
+          hi = std::min<int64_t>(hi, 0xFFFF);
+          for (int64_t a = lo; a <= hi; a += kFoldTaskStarts)
+            v.push_back({i, uint16_t(a), uint16_t(std::min<int64_t>(a + kFoldTaskStarts - 1, hi))});
+        };
+        if (klo >= 0) add(pk, klo, khi);
+        if (slo >= 0) add(ps, slo, shi);
       }
       n_fold_pairs_k_ = uint32_t(pk.size());
       n_fold_pairs_s_ = uint32_t(ps.size());
