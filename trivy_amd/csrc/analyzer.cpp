@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "capi_internal.h"
+#include "parallel.h"
 
 namespace tsg {
 void SetError(const std::string& e);
@@ -48,6 +49,26 @@ uint64_t ExtractPrintable(const uint8_t* in, uint64_t n, uint8_t* out) {
     run = 0;
   }
   return w;
+}
+
+// Output length of ExtractPrintable without writing.
+uint64_t PrintableLen(const uint8_t* in, uint64_t n) {
+  uint64_t w = 0, run = 0;
+  for (uint64_t i = 0; i <= n; i++) {
+    if (i < n && IsPrintByte(in[i])) {
+      run++;
+      continue;
+    }
+    if (run > 4) w += run + 1;
+    run = 0;
+  }
+  return w;
+}
+
+uint64_t CountCR(const uint8_t* in, uint64_t n) {
+  uint64_t k = 0;
+  for (const uint8_t* p = in; (p = static_cast<const uint8_t*>(std::memchr(p, '\r', size_t(in + n - p)))); p++) k++;
+  return k;
 }
 
 // bytes.ReplaceAll(content, "\r", "") (secret.go:121), memchr-driven.
@@ -132,6 +153,7 @@ struct tsg_collector {
   uint8_t* arena = nullptr;
   uint64_t cap = 0, used = 0, input_bytes = 0;
   uint64_t limit = 0;  // the batch size asked for
+  int threads = 16;    // ingest threads (TSG_HOST_THREADS)
   std::vector<uint64_t> offs{0};
   std::string path_pool;
   std::vector<uint64_t> path_off{0};
@@ -238,9 +260,13 @@ int64_t Add(tsg_collector* c, const char* path, uint64_t plen, bool image, const
 
 // ---- archive/tar header reading (Go 1.22 archive/tar/reader.go semantics) ----
 bool AllZero(const uint8_t* b) {
-  for (int i = 0; i < 512; i++)
-    if (b[i]) return false;
-  return true;
+  uint64_t acc = 0;
+  for (int i = 0; i < 64; i++) {
+    uint64_t w;
+    std::memcpy(&w, b + 8 * i, 8);
+    acc |= w;
+  }
+  return acc == 0;
 }
 std::string CStr(const uint8_t* b, size_t n) {  // parseString: up to the first NUL
   size_t k = 0;
@@ -347,6 +373,7 @@ int tsg_collector_new(tsg_analyzer* a, uint64_t arena_bytes, tsg_collector** out
   c->a = a;
   c->device = a->s->s->device();
   c->limit = arena_bytes ? arena_bytes : (uint64_t(256) << 20);
+  if (const char* e = std::getenv("TSG_HOST_THREADS")) c->threads = std::max(1, std::atoi(e));
   if (!c->Reserve(c->limit + 64)) {
     delete c;
     return -1;
@@ -361,114 +388,198 @@ int64_t tsg_collector_add(tsg_collector* c, const char* path, uint64_t path_len,
   return Add(c, path, path_len, !dir || !*dir, content, size);
 }
 
-int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st) {
-  tsg_tar_stats local{};
-  if (!st) st = &local;
-  uint64_t p = *cursor;
-  for (;;) {
-    const uint64_t entry = p;  // where this entry's header chain starts
-    std::string long_name, pax_path;
-    bool has_long = false, has_pax_path = false, has_pax_size = false;
-    int64_t pax_size = 0;
-    const uint8_t* h = nullptr;
-    char type = 0;
-    int64_t size = 0;
-    for (;;) {  // extended headers, then the entry's own
-      if (p + 512 > n) {
-        if (p >= n) return 0;  // io.EOF without the zero blocks
-        tsg::SetError("tar: truncated header");
-        return -1;
-      }
-      h = tar + p;
-      if (AllZero(h)) return 0;  // end-of-archive marker
-      if (!ChecksumOK(h)) {
-        tsg::SetError("tar: invalid header checksum at offset " + std::to_string(p));
-        return -1;
-      }
-      type = char(h[156]);
-      if (!ParseNumeric(h + 124, 12, &size) || size < 0) {
-        tsg::SetError("tar: invalid size field");
-        return -1;
-      }
-      const uint64_t dsz = HeaderOnly(type) ? 0 : uint64_t(size);
-      const uint64_t data = p + 512;
-      if (data + dsz > n) {
-        tsg::SetError("tar: truncated entry data");
-        return -1;
-      }
-      if (type == 'x') {
-        if (!ParsePax(tar + data, dsz, &pax_path, &pax_size, &has_pax_path, &has_pax_size)) {
-          tsg::SetError("tar: invalid PAX record");
-          return -1;
-        }
-        p = data + ((dsz + 511) & ~uint64_t(511));
-        continue;
-      }
-      if (type == 'L') {
-        long_name = CStr(tar + data, size_t(dsz));
-        has_long = true;
-        p = data + ((dsz + 511) & ~uint64_t(511));
-        continue;
-      }
-      if (type == 'K') {  // GNU long link name
-        p = data + ((dsz + 511) & ~uint64_t(511));
-        continue;
-      }
-      break;
+}  // extern "C"
+
+namespace {
+// One archive entry as the walk sees it (header chain resolved).
+struct TarEntry {
+  uint64_t start, next;  // header chain start, next entry
+  uint64_t data, size;   // regular files: content
+  uint8_t what;          // 0 other, 1 whiteout, 2 opaque dir, 3 regular file
+  std::string fp;        // cleaned path (walker/tar.go:46-48)
+  // filled by the parallel pass
+  uint8_t state;         // 0 not required, 1 binary skipped, 2 add
+  uint8_t bin;
+  uint64_t out_len, out_off;
+};
+
+// Reads the entry whose header chain starts at p.  0 = entry read, 1 = end of
+// archive, <0 = malformed.
+int ReadEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
+  e->start = p;
+  std::string long_name, pax_path;
+  bool has_long = false, has_pax_path = false, has_pax_size = false;
+  int64_t pax_size = 0, size = 0;
+  const uint8_t* h = nullptr;
+  char type = 0;
+  for (;;) {  // extended headers, then the entry's own
+    if (p + 512 > n) {
+      if (p >= n) return 1;  // io.EOF without the zero blocks
+      tsg::SetError("tar: truncated header");
+      return -1;
     }
-    // the entry header at h
-    std::string name = CStr(h, 100);
-    const bool ustar = std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0;
-    if (ustar) {
-      const std::string prefix = CStr(h + 345, 155);
-      if (!prefix.empty()) name = prefix + "/" + name;
+    h = tar + p;
+    if (AllZero(h)) return 1;  // end-of-archive marker
+    if (!ChecksumOK(h)) {
+      tsg::SetError("tar: invalid header checksum at offset " + std::to_string(p));
+      return -1;
     }
-    if (has_long) name = long_name;
-    if (has_pax_path) name = pax_path;
-    if (has_pax_size) size = pax_size;
-    if (type == '\0') type = (!name.empty() && name.back() == '/') ? '5' : '0';  // TypeRegA
+    type = char(h[156]);
+    if (!ParseNumeric(h + 124, 12, &size) || size < 0) {
+      tsg::SetError("tar: invalid size field");
+      return -1;
+    }
     const uint64_t dsz = HeaderOnly(type) ? 0 : uint64_t(size);
     const uint64_t data = p + 512;
     if (data + dsz > n) {
       tsg::SetError("tar: truncated entry data");
       return -1;
     }
-    const uint64_t next = data + ((dsz + 511) & ~uint64_t(511));
-    st->entries++;
-    // LayerTar.Walk (walker/tar.go:41-84)
-    std::string fp = tsg::GoPathClean(name);
-    size_t t = 0;
-    while (t < fp.size() && fp[t] == '/') t++;
-    fp = fp.substr(t);
-    const size_t slash = fp.rfind('/');
-    const std::string file_name = slash == std::string::npos ? fp : fp.substr(slash + 1);
-    if (file_name == ".wh..wh..opq") {
-      st->opaque_dirs++;
-    } else if (file_name.compare(0, 4, ".wh.") == 0) {
-      st->whiteouts++;
-    } else if (type == '0') {
-      st->regular++;
-      // AnalyzeFile (analyzer.go:403-455): Required(cleanPath), then Analyze with Dir ""
-      if (Required(c->a, fp.data(), fp.size(), int64_t(dsz))) {
-        st->required++;
-        const int64_t r = Add(c, fp.data(), fp.size(), true, tar + data, dsz);
-        if (r == TSG_FULL) {
-          st->required--;
-          *cursor = entry;
-          return 1;
-        }
-        if (r == TSG_SKIPPED) {
-          st->skipped_binary++;
-        } else if (r < 0) {
-          return -1;
-        } else {
-          st->added++;
-          st->input_bytes += dsz;
-        }
+    if (type == 'x' || type == 'L' || type == 'K') {
+      if (type == 'x' && !ParsePax(tar + data, dsz, &pax_path, &pax_size, &has_pax_path, &has_pax_size)) {
+        tsg::SetError("tar: invalid PAX record");
+        return -1;
       }
+      if (type == 'L') {
+        long_name = CStr(tar + data, size_t(dsz));
+        has_long = true;
+      }
+      p = data + ((dsz + 511) & ~uint64_t(511));
+      continue;
     }
-    p = next;
+    break;
+  }
+  std::string name = CStr(h, 100);
+  const bool ustar = std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0;
+  if (ustar) {
+    const std::string prefix = CStr(h + 345, 155);
+    if (!prefix.empty()) name = prefix + "/" + name;
+  }
+  if (has_long) name = long_name;
+  if (has_pax_path) name = pax_path;
+  if (has_pax_size) size = pax_size;
+  if (type == '\0') type = (!name.empty() && name.back() == '/') ? '5' : '0';  // TypeRegA
+  const uint64_t dsz = HeaderOnly(type) ? 0 : uint64_t(size);
+  e->data = p + 512;
+  if (e->data + dsz > n) {
+    tsg::SetError("tar: truncated entry data");
+    return -1;
+  }
+  e->size = dsz;
+  e->next = e->data + ((dsz + 511) & ~uint64_t(511));
+  e->fp = std::move(name);  // raw name; Classify cleans it on the ingest threads
+  e->what = type == '0' ? 3 : 0;
+  return 0;
+}
+
+// LayerTar.Walk's per-entry path logic (walker/tar.go:41-84): clean the name,
+// classify whiteout / opaque markers.
+void Classify(TarEntry* e) {
+  std::string fp = tsg::GoPathClean(e->fp);
+  size_t t = 0;
+  while (t < fp.size() && fp[t] == '/') t++;
+  e->fp = fp.substr(t);
+  const size_t slash = e->fp.rfind('/');
+  const char* file_name = e->fp.c_str() + (slash == std::string::npos ? 0 : slash + 1);
+  if (std::strcmp(file_name, ".wh..wh..opq") == 0) e->what = 2;
+  else if (std::strncmp(file_name, ".wh.", 4) == 0) e->what = 1;
+}
+}  // namespace
+
+extern "C" {
+
+// The walk runs in rounds: index the entries ahead (headers only, ~1.5x the
+// room left in the batch), classify them on the ingest threads (Required,
+// binary gate, transformed length), accept the longest prefix that fits, copy
+// and transform the accepted contents on the threads.  Entries past the
+// accepted prefix are re-read from *cursor by the next call.
+int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st) {
+  tsg_tar_stats local{};
+  if (!st) st = &local;
+  uint64_t p = *cursor;
+  std::vector<TarEntry> ents;
+  for (;;) {
+    // 1. index
+    ents.clear();
+    const uint64_t room = c->limit > c->used ? c->limit - c->used : 0;
+    uint64_t ahead = 0;
+    bool at_end = false;
+    while (ahead <= room + room / 2 || ents.empty()) {
+      TarEntry e;
+      const int r = ReadEntry(tar, n, p, &e);
+      if (r < 0) return -1;
+      if (r == 1) {
+        at_end = true;
+        break;
+      }
+      p = e.next;
+      if (e.what == 3) ahead += e.size + 512;
+      ents.push_back(std::move(e));
+    }
+    // 2. classify (AnalyzeFile's Required + Analyze's binary gate)
+    const size_t kBlock = 64;
+    tsg::ParallelFor((ents.size() + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
+      for (size_t i = b * kBlock; i < std::min(ents.size(), (b + 1) * kBlock); i++) {
+        TarEntry& e = ents[i];
+        e.state = 0;
+        Classify(&e);
+        if (e.what != 3 || !Required(c->a, e.fp.data(), e.fp.size(), int64_t(e.size))) continue;
+        const uint8_t* d = tar + e.data;
+        e.bin = tsg::IsBinaryHead(d, e.size) ? 1 : 0;
+        if (e.bin && tsg::GoExt(e.fp) != ".pyc") {
+          e.state = 1;
+          continue;
+        }
+        e.state = 2;
+        e.out_len = e.bin ? tsg::PrintableLen(d, e.size) : e.size - tsg::CountCR(d, e.size);
+      }
+    });
+    // 3. accept in order
+    size_t k = 0;
+    bool full = false;
+    for (; k < ents.size(); k++) {
+      TarEntry& e = ents[k];
+      if (e.state == 2) {
+        if (c->files() > 0 && c->used + e.out_len > c->limit) {
+          full = true;
+          break;
+        }
+        if (c->used + e.out_len + 64 > c->cap && !c->Reserve(e.out_len + 64)) return -1;  // a lone large file
+        e.out_off = c->used;
+        c->used += e.out_len;
+        c->offs.push_back(c->used);
+        c->path_pool.push_back('/');  // Dir "" (image files, secret.go:130-135)
+        c->path_pool.append(e.fp);
+        c->path_off.push_back(c->path_pool.size());
+        c->binary.push_back(e.bin);
+        c->input_bytes += e.size;
+        st->added++;
+        st->input_bytes += e.size;
+      }
+      st->entries++;
+      st->whiteouts += e.what == 1;
+      st->opaque_dirs += e.what == 2;
+      st->regular += e.what == 3;
+      st->required += e.state != 0;
+      st->skipped_binary += e.state == 1;
+    }
+    // 4. copy / transform the accepted contents
+    tsg::ParallelFor((k + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
+      for (size_t i = b * kBlock; i < std::min(k, (b + 1) * kBlock); i++) {
+        const TarEntry& e = ents[i];
+        if (e.state != 2) continue;
+        uint8_t* dst = c->arena + e.out_off;
+        if (e.bin) tsg::ExtractPrintable(tar + e.data, e.size, dst);
+        else tsg::StripCR(tar + e.data, e.size, dst);
+      }
+    });
+    std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
+    if (full) {
+      *cursor = ents[k].start;
+      return 1;
+    }
     *cursor = p;
+    if (at_end) return 0;
   }
 }
 

@@ -993,10 +993,19 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     }
     const size_t fixed = 4096 + size_t(kCThreads) * (kCWin + 8) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
                          size_t(kCThreads / 64) * kCWaveHits * 12 + size_t(kCThreads / 64) * 16;
-    lds_tabs_ = fixed + ftabs_bytes_ <= 64 * 1024;  // else the item tables stay in global memory
+    // tables staged in LDS only while two 256-thread workgroups still fit a CU;
+    // larger ones are read from global memory (L2-resident).  c3 (103 KB of
+    // tables): LDS at 1 WG/CU 102 GB/s vs global at 4 WG/CU 164 GB/s.
+    // TSG_LDS_TABS_MAX overrides (tuning).
+    size_t lds_max = 64 * 1024;  // measured: 1 WG/CU with 160-KiB tables loses to 4 WGs/CU reading L2
+    if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
+    lds_tabs_ = fixed + ftabs_bytes_ <= lds_max && ftabs_bytes_ + 2 * kFoldSpan + 16 <= lds_max;
     c_lds_bytes_ = fixed + (lds_tabs_ ? ftabs_bytes_ : 0);
     hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
+    if (lds_tabs_)
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          int(ftabs_bytes_));
   }
 }
 

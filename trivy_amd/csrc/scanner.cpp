@@ -1,6 +1,8 @@
 // Exact host tail of the drop-in Scanner (see scanner.h for the line map).
 #include "scanner.h"
 
+#include "parallel.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -17,28 +19,6 @@ namespace {
 
 double NowMs() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-template <typename F>
-void ParallelFor(size_t n, int threads, F fn) {
-  if (n == 0) return;
-  if (threads <= 1 || n < 2) {
-    for (size_t i = 0; i < n; i++) fn(i);
-    return;
-  }
-  std::atomic<size_t> next{0};
-  auto work = [&]() {
-    for (;;) {
-      size_t i = next.fetch_add(1);
-      if (i >= n) break;
-      fn(i);
-    }
-  };
-  int t = int(std::min<size_t>(size_t(threads), n));
-  std::vector<std::thread> pool;
-  for (int k = 1; k < t; k++) pool.emplace_back(work);
-  work();
-  for (auto& th : pool) th.join();
 }
 
 bool AsciiContainsLower(const uint8_t* s, size_t n, const std::string& lit) {
