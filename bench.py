@@ -266,7 +266,8 @@ def main():
         breakdown = {k: round(last["scan_" + k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel",
                                                               "ms_verify_kernel", "ms_gpu_total",
                                                               "ms_host_gpu_phase", "ms_host_exact")}
-        config_extra = {"layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
+        config_extra = {"walk_s_per_step": round(last["walk_s"], 3), "wait_s_per_step": round(last["wait_s"], 3),
+                        "layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
                         "arena_mb": args.arena_mb, "pipeline": "2 collectors (walk k+1 || scan k)",
                         "layer_gbps": round(world * int(layer.size) * args.steps / dt / 1e9, 3)}

@@ -20,6 +20,7 @@ Every transform runs in libtsg.so (include/tsg_analyzer.h); there is no CPU
 fallback for the scan itself.
 """
 import ctypes
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -338,22 +339,30 @@ class SecretAnalyzer:
         colls = colls or [Collector(self, arena_bytes), Collector(self, arena_bytes)]
         pending = None
         cursor, k, done = 0, 0, False
+        t_walk = t_wait = 0.0
         while not done:
             coll = colls[k]
+            t0 = time.perf_counter()
             rc, cursor = coll.add_tar(layer, cursor, st)
+            t_walk += time.perf_counter() - t0
             done = rc == 0
             if rc == 1 and coll.files() == 0:
                 raise RuntimeError("tar layer: an entry does not fit an empty collector")
             nxt = coll.submit() if coll.files() else None
+            t0 = time.perf_counter()
             if pending is not None:
                 take(pending)
+            t_wait += time.perf_counter() - t0
             pending = nxt
             k ^= 1
+        t0 = time.perf_counter()
         if pending is not None:
             take(pending)
+        t_wait += time.perf_counter() - t0
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})
+            stats.update({"walk_s": t_walk, "wait_s": t_wait})
         return result
 
 

@@ -394,25 +394,34 @@ namespace {
 // One archive entry as the walk sees it (header chain resolved).
 struct TarEntry {
   uint64_t start, next;  // header chain start, next entry
-  uint64_t data, size;   // regular files: content
+  uint64_t hdr;          // the entry's own header
+  uint64_t data, size;   // content
+  uint64_t long_off, long_len;  // GNU 'L' long name data (long_len == ~0: none)
   uint8_t what;          // 0 other, 1 whiteout, 2 opaque dir, 3 regular file
-  std::string fp;        // cleaned path (walker/tar.go:46-48)
+  uint8_t has_pax_path;
+  uint8_t bad;           // the entry header's checksum is wrong (checked on the threads)
+  std::string fp;        // PAX path, then the cleaned path (walker/tar.go:46-48)
   // filled by the parallel pass
   uint8_t state;         // 0 not required, 1 binary skipped, 2 add
   uint8_t bin;
   uint64_t out_len, out_off;
 };
 
-// Reads the entry whose header chain starts at p.  0 = entry read, 1 = end of
-// archive, <0 = malformed.
-int ReadEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
+// Sequential step of the walk: hop over the header chain starting at p using
+// only what decides the next entry's position (zero block, typeflag, size,
+// PAX size).  Extended headers are checked here (rare); the entry header's
+// checksum and name are resolved later on the ingest threads (Resolve).
+// 0 = entry read, 1 = end of archive, <0 = malformed.
+int ChainEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
   e->start = p;
-  std::string long_name, pax_path;
-  bool has_long = false, has_pax_path = false, has_pax_size = false;
+  e->long_len = ~uint64_t(0);
+  e->has_pax_path = 0;
+  std::string pax_path;
+  bool has_pax_path = false, has_pax_size = false;
   int64_t pax_size = 0, size = 0;
   const uint8_t* h = nullptr;
   char type = 0;
-  for (;;) {  // extended headers, then the entry's own
+  for (;;) {
     if (p + 512 > n) {
       if (p >= n) return 1;  // io.EOF without the zero blocks
       tsg::SetError("tar: truncated header");
@@ -420,10 +429,6 @@ int ReadEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
     }
     h = tar + p;
     if (AllZero(h)) return 1;  // end-of-archive marker
-    if (!ChecksumOK(h)) {
-      tsg::SetError("tar: invalid header checksum at offset " + std::to_string(p));
-      return -1;
-    }
     type = char(h[156]);
     if (!ParseNumeric(h + 124, 12, &size) || size < 0) {
       tsg::SetError("tar: invalid size field");
@@ -435,30 +440,26 @@ int ReadEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
       tsg::SetError("tar: truncated entry data");
       return -1;
     }
-    if (type == 'x' || type == 'L' || type == 'K') {
-      if (type == 'x' && !ParsePax(tar + data, dsz, &pax_path, &pax_size, &has_pax_path, &has_pax_size)) {
-        tsg::SetError("tar: invalid PAX record");
-        return -1;
-      }
-      if (type == 'L') {
-        long_name = CStr(tar + data, size_t(dsz));
-        has_long = true;
-      }
-      p = data + ((dsz + 511) & ~uint64_t(511));
-      continue;
+    if (type != 'x' && type != 'L' && type != 'K') break;
+    if (!ChecksumOK(h)) {
+      tsg::SetError("tar: invalid header checksum at offset " + std::to_string(p));
+      return -1;
     }
-    break;
+    if (type == 'x' && !ParsePax(tar + data, dsz, &pax_path, &pax_size, &has_pax_path, &has_pax_size)) {
+      tsg::SetError("tar: invalid PAX record");
+      return -1;
+    }
+    if (type == 'L') {
+      e->long_off = data;
+      e->long_len = dsz;
+    }
+    p = data + ((dsz + 511) & ~uint64_t(511));
   }
-  std::string name = CStr(h, 100);
-  const bool ustar = std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0;
-  if (ustar) {
-    const std::string prefix = CStr(h + 345, 155);
-    if (!prefix.empty()) name = prefix + "/" + name;
-  }
-  if (has_long) name = long_name;
-  if (has_pax_path) name = pax_path;
+  e->hdr = p;
   if (has_pax_size) size = pax_size;
-  if (type == '\0') type = (!name.empty() && name.back() == '/') ? '5' : '0';  // TypeRegA
+  if (type == '\0') {  // TypeRegA: a directory when the name ends in '/' (resolved name: Resolve)
+    type = '0';
+  }
   const uint64_t dsz = HeaderOnly(type) ? 0 : uint64_t(size);
   e->data = p + 512;
   if (e->data + dsz > n) {
@@ -467,14 +468,35 @@ int ReadEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
   }
   e->size = dsz;
   e->next = e->data + ((dsz + 511) & ~uint64_t(511));
-  e->fp = std::move(name);  // raw name; Classify cleans it on the ingest threads
   e->what = type == '0' ? 3 : 0;
+  if (has_pax_path) {
+    e->fp = std::move(pax_path);
+    e->has_pax_path = 1;
+  }
   return 0;
+}
+
+// The entry's name (ustar prefix, GNU long name, PAX path) and header checksum.
+void Resolve(const uint8_t* tar, TarEntry* e) {
+  const uint8_t* h = tar + e->hdr;
+  e->bad = ChecksumOK(h) ? 0 : 1;
+  if (e->has_pax_path) return;
+  if (e->long_len != ~uint64_t(0)) {
+    e->fp = CStr(tar + e->long_off, size_t(e->long_len));
+  } else {
+    e->fp = CStr(h, 100);
+    if (std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0) {
+      const std::string prefix = CStr(h + 345, 155);
+      if (!prefix.empty()) e->fp = prefix + "/" + e->fp;
+    }
+  }
 }
 
 // LayerTar.Walk's per-entry path logic (walker/tar.go:41-84): clean the name,
 // classify whiteout / opaque markers.
-void Classify(TarEntry* e) {
+void Classify(const uint8_t* tar, TarEntry* e) {
+  Resolve(tar, e);
+  if (tar[e->hdr + 156] == '\0' && !e->fp.empty() && e->fp.back() == '/') e->what = 0;  // TypeRegA dir
   std::string fp = tsg::GoPathClean(e->fp);
   size_t t = 0;
   while (t < fp.size() && fp[t] == '/') t++;
@@ -506,7 +528,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     bool at_end = false;
     while (ahead <= room + room / 2 || ents.empty()) {
       TarEntry e;
-      const int r = ReadEntry(tar, n, p, &e);
+      const int r = ChainEntry(tar, n, p, &e);
       if (r < 0) return -1;
       if (r == 1) {
         at_end = true;
@@ -522,7 +544,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       for (size_t i = b * kBlock; i < std::min(ents.size(), (b + 1) * kBlock); i++) {
         TarEntry& e = ents[i];
         e.state = 0;
-        Classify(&e);
+        Classify(tar, &e);
         if (e.what != 3 || !Required(c->a, e.fp.data(), e.fp.size(), int64_t(e.size))) continue;
         const uint8_t* d = tar + e.data;
         e.bin = tsg::IsBinaryHead(d, e.size) ? 1 : 0;
@@ -539,6 +561,10 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     bool full = false;
     for (; k < ents.size(); k++) {
       TarEntry& e = ents[k];
+      if (e.bad) {
+        tsg::SetError("tar: invalid header checksum at offset " + std::to_string(e.hdr));
+        return -1;
+      }
       if (e.state == 2) {
         if (c->files() > 0 && c->used + e.out_len > c->limit) {
           full = true;
