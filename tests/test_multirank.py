@@ -1,0 +1,128 @@
+"""N>1 path: files shard across ranks, no data-path collective,
+findings gathered to rank 0 in the reference's order.
+
+CPU-only: world_size-2 gloo process group (127.0.0.1); each rank scans its LPT
+shard through the native exact host tail (tsg_debug_host_tail, the same C++ tail
+the GPU path feeds) and rank 0 compares the gathered, sorted result with the
+oracle's single-process scan of the whole corpus.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import secret_scanner as osc
+from tests.corpus import make_corpus
+from trivy_amd.shard import shard_files, shard_loads
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _files(seed, n):
+    # unique paths: secrets sort by FilePath only (analyzer.go:225-227), so equal paths would tie
+    return [("d%04d/%s" % (i, p), b.replace(b"\r", b"")) for i, (p, b) in enumerate(make_corpus(seed, n))]
+
+
+def _rank_main(rank, world, port, seed, n, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.test_host_tail import host_tail_scan
+        from trivy_amd.shard import scan_sharded
+        files = _files(seed, n)
+        res = scan_sharded(files, lambda fs: host_tail_scan(None, fs), rank, world)
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump([s.to_dict() for s in res.Secrets], f)
+        else:
+            assert res is None
+    finally:
+        dist.destroy_process_group()
+
+
+def _oracle_sorted(files):
+    o = osc.new_scanner(None)
+    secrets = [o.scan(p, b) for p, b in files]
+    secrets = [s for s in secrets if s["Findings"]]
+    secrets.sort(key=lambda s: s["FilePath"].encode("latin-1", "surrogateescape")
+                 if isinstance(s["FilePath"], str) else s["FilePath"])
+    for s in secrets:
+        s["Findings"].sort(key=lambda f: (f["RuleID"], f["StartLine"]))
+    return secrets
+
+
+def test_shard_files_partition_and_balance():
+    rng = np.random.default_rng(7)
+    sizes = np.clip(rng.lognormal(np.log(8192), 1.5, 5000).astype(np.int64), 10, 10 << 20)
+    for world in (1, 2, 3, 8):
+        shards = shard_files(sizes, world)
+        allidx = np.concatenate(shards)
+        assert sorted(allidx.tolist()) == list(range(sizes.size))
+        assert all(np.all(np.diff(s) > 0) for s in shards)
+        loads = shard_loads(sizes, shards)
+        # LPT: max load <= mean + largest item
+        assert max(loads) <= sizes.sum() / world + sizes.max()
+        assert shard_files(sizes, world)[0].tolist() == shards[0].tolist()  # deterministic
+
+
+def test_shard_files_edge_cases():
+    assert [s.tolist() for s in shard_files([], 2)] == [[], []]
+    assert [s.tolist() for s in shard_files([5], 3)] == [[0], [], []]
+    assert [s.tolist() for s in shard_files([1, 1, 1, 1], 2)] == [[0, 2], [1, 3]]
+    with pytest.raises(ValueError):
+        shard_files([1], 0)
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_scan_matches_single_process(tmp_path):
+    seed, n, world = 31, 160, 2
+    out = tmp_path / "rank0.json"
+    mp.start_processes(_rank_main, args=(world, _free_port(), seed, n, str(out)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = json.loads(out.read_text())
+    want = _oracle_sorted(_files(seed, n))
+    assert len(want) > 5
+    assert [s["FilePath"] for s in got] == [s["FilePath"] for s in want]
+    assert got == want
+
+
+def _rank_main_gpu(rank, world, port, seed, n, out_path):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import trivy_amd.secret as secret
+        from trivy_amd.shard import scan_sharded
+        dev = rank % torch.cuda.device_count()  # the 1-GPU box: both ranks share cuda:0
+        sc = secret.NewScanner(None, device=dev)
+        files = _files(seed, n)
+        res = scan_sharded(files, lambda fs: sc.ScanBatch([secret.ScanArgs(p, b) for p, b in fs]), rank, world)
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump([s.to_dict() for s in res.Secrets], f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_rank_gpu_scan_matches_single_process(tmp_path):
+    seed, n, world = 33, 160, 2
+    out = tmp_path / "rank0.json"
+    mp.start_processes(_rank_main_gpu, args=(world, _free_port(), seed, n, str(out)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = json.loads(out.read_text())
+    want = _oracle_sorted(_files(seed, n))
+    assert len(want) > 5
+    assert got == want
