@@ -306,6 +306,7 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
     }
     for (auto& kw : r.keywords) r.kw_lower_host.push_back(GoBytesToLower((const uint8_t*)kw.data(), kw.size()));
   }
+  BuildAllowPathFilter();
   const char* ht = std::getenv("TSG_HOST_THREADS");
   host_threads_ = ht ? std::atoi(ht) : 16;
   if (host_threads_ <= 0) host_threads_ = 1;
@@ -320,7 +321,50 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
   }
 }
 
+void SecretScanner::BuildAllowPathFilter() {
+  ap_fast_ = false;
+  if (allow_.size() > 64) return;
+  ap_pair_.assign(65536, 0);
+  ap_always_ = 0;
+  for (size_t i = 0; i < allow_.size(); i++) {
+    const Matcher* m = allow_[i].path.get();
+    if (!m || !m->re) continue;  // never matches
+    const uint64_t bit = uint64_t(1) << i;
+    bool always = m->lits.empty();
+    for (auto& l : m->lits)
+      if (l.size() < 2) always = true;
+    if (always) {
+      ap_always_ |= bit;
+      continue;
+    }
+    for (auto& l : m->lits) ap_pair_[(uint32_t(uint8_t(l[0])) << 8) | uint8_t(l[1])] |= bit;
+  }
+  ap_fast_ = true;
+}
+
 bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
+  // Matcher::Match rejects an ASCII path holding none of a rule's (lowercase)
+  // literals, so only the rules a byte pair of the lowered path can start a
+  // literal of (plus the unfiltered ones) can match: evaluate just those.
+  if (ap_fast_ && n <= 1024) {
+    uint8_t low[1024];
+    bool ascii = true;
+    for (size_t i = 0; i < n; i++) {
+      const uint8_t b = p[i];
+      ascii = ascii && b < 0x80;
+      low[i] = (b >= 'A' && b <= 'Z') ? uint8_t(b + 32) : b;
+    }
+    if (ascii) {
+      uint64_t mask = ap_always_;
+      for (size_t i = 0; i + 1 < n; i++) mask |= ap_pair_[(uint32_t(low[i]) << 8) | low[i + 1]];
+      while (mask) {
+        const int i = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        if (allow_[size_t(i)].path->Match(p, n)) return true;
+      }
+      return false;
+    }
+  }
   for (auto& a : allow_)
     if (a.path && a.path->Match(p, n)) return true;
   return false;

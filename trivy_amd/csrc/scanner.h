@@ -151,6 +151,13 @@ class SecretScanner {
   int host_threads_ = 0;
   bool compiled_ok_ = false;
   bool no_engine_ = false;
+  // Global AllowPath prefilter (exact): per ASCII-lowered byte pair, the allow
+  // rules that have a required literal starting with that pair; rules without
+  // a literal prefilter (or with a 1-byte literal) are always evaluated.
+  void BuildAllowPathFilter();
+  bool ap_fast_ = false;
+  uint64_t ap_always_ = 0;
+  std::vector<uint64_t> ap_pair_;  // 65536 rule masks
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.
