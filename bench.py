@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--gb", type=float, default=None, help="corpus size per GPU (GB = 1e9 B)")
     ap.add_argument("--cpu-sample-mb", type=float, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=2, help="scans in flight (pipelined submission)")
+    ap.add_argument("--depth", type=int, default=3, help="scans in flight (pipelined submission)")
     ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     args = ap.parse_args()
