@@ -847,6 +847,11 @@ __global__ __launch_bounds__(256) void verify_hits_kernel(NfaParams P) {
     const AnchorInfo a = P.anchors[aid];
     const RuleGpu rg = P.rules[a.rule];  // keyword gates are evaluated lazily by the host tail
     const uint32_t ff = P.flags[f];
+    // A closed ASCII keyword gate in a file without U+0130 / U+212A is exactly
+    // MatchKeywords == false (scanner.go:409): the host would drop every match
+    // of the rule, so its hits need no verification.
+    if (rg.gate == kGateKeywords && !rg.kw_match_implied && !(ff & 4u) && !(gate_flags(P, rg, f) & kCandGateOpen))
+      continue;
     const int64_t lit_hi = int64_t(end) - int64_t(a.lit_len);
     const int64_t lit_lo = (ff & 1u) ? int64_t(end) - 3 * int64_t(a.lit_len) : lit_hi;
     const int64_t whi = lit_hi - a.off_lo;

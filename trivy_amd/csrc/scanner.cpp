@@ -314,10 +314,18 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
     no_engine_ = true;
     return;
   }
-  engine_.reset(new GpuEngine(cr_, device));
-  if (!engine_->ok()) {
-    err_ = engine_->error();
-    *err = err_;
+  const char* slots_env = std::getenv("TSG_GPU_SLOTS");
+  int slots = slots_env ? std::atoi(slots_env) : 1;  // 2 measured slower at C2 (kernels interfere)
+  if (slots < 1) slots = 1;
+  if (slots > 4) slots = 4;
+  gpu_mu_.reset(new std::mutex[size_t(slots)]);
+  for (int k = 0; k < slots; k++) {
+    engines_.emplace_back(new GpuEngine(cr_, device));
+    if (!engines_.back()->ok()) {
+      err_ = engines_.back()->error();
+      *err = err_;
+      return;
+    }
   }
 }
 
@@ -824,10 +832,12 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   HostStats hs;
   std::vector<Candidate> cands;
   uint64_t n_bytes = in.n_files ? in.host_offsets[in.n_files] : 0;
-  if (!engine_) {
+  if (engines_.empty()) {
     err_ = "no GPU engine bound to this scanner";
     return false;
   }
+  const size_t slot = size_t(next_slot_.fetch_add(1) % engines_.size());
+  GpuEngine* engine = engines_[slot].get();
   // the allow-path pass needs no GPU result: it runs on host threads while
   // this thread drives the kernels
   std::vector<uint8_t> allowed;
@@ -840,12 +850,12 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   bool ok;
   std::string gpu_err;
   {
-    std::lock_guard<std::mutex> g(gpu_mu_);
+    std::lock_guard<std::mutex> g(gpu_mu_[slot]);
     if (in.dev_arena)
-      ok = engine_->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
+      ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
     else
-      ok = engine_->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
-    if (!ok) gpu_err = engine_->error();
+      ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
+    if (!ok) gpu_err = engine->error();
   }
   allow_thread.join();
   if (!ok) {

@@ -9,6 +9,7 @@
 // (:438-446, :475-558) and the final sort (:452-457).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -119,7 +120,14 @@ class SecretScanner {
   // device < 0: no GPU engine (test hooks only: tsg_debug_host_tail)
   SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleSpec> allow,
                 std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err);
-  bool ok() const { return compiled_ok_ && (no_engine_ || (engine_ && engine_->ok())); }
+  bool ok() const {
+    if (!compiled_ok_) return false;
+    if (no_engine_) return true;
+    if (engines_.empty()) return false;
+    for (auto& e : engines_)
+      if (!e->ok()) return false;
+    return true;
+  }
   const std::string& error() const { return err_; }
 
   bool Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst);
@@ -134,8 +142,8 @@ class SecretScanner {
 
   const std::vector<RuleSpec>& rules() const { return rules_; }
   const CompiledRules& compiled() const { return cr_; }
-  GpuEngine* engine() { return engine_.get(); }
-  int device() const { return engine_ ? engine_->device() : -1; }  // -1: no GPU engine
+  GpuEngine* engine() { return engines_.empty() ? nullptr : engines_[0].get(); }
+  int device() const { return engines_.empty() ? -1 : engines_[0]->device(); }  // -1: no GPU engine
   void set_host_threads(int n) { host_threads_ = n; }
 
  private:
@@ -145,8 +153,14 @@ class SecretScanner {
   std::vector<AllowRuleSpec> allow_;
   std::vector<std::unique_ptr<Regex>> exclude_;
   CompiledRules cr_;
-  std::unique_ptr<GpuEngine> engine_;
-  std::mutex gpu_mu_;  // one GPU phase at a time (one HIP stream, per-batch device buffers)
+  // GPU slots: each engine has its own HIP stream and per-batch device
+  // buffers; consecutive batches take the slots round robin, so one batch's
+  // latency-bound kernels (confirm / verify) overlap the next batch's
+  // streaming filter.  One GPU phase at a time per slot.  TSG_GPU_SLOTS,
+  // default 1 (2 measured slower at C2: the kernels of two batches interfere).
+  std::vector<std::unique_ptr<GpuEngine>> engines_;
+  std::unique_ptr<std::mutex[]> gpu_mu_;
+  std::atomic<uint32_t> next_slot_{0};
   std::string err_;
   int host_threads_ = 0;
   bool compiled_ok_ = false;
