@@ -333,27 +333,35 @@ void SecretScanner::BuildAllowPathFilter() {
   ap_fast_ = false;
   if (allow_.size() > 64) return;
   ap_pair_.assign(65536, 0);
+  ap_lits_.clear();
   ap_always_ = 0;
   for (size_t i = 0; i < allow_.size(); i++) {
     const Matcher* m = allow_[i].path.get();
     if (!m || !m->re) continue;  // never matches
-    const uint64_t bit = uint64_t(1) << i;
     bool always = m->lits.empty();
     for (auto& l : m->lits)
       if (l.size() < 2) always = true;
     if (always) {
-      ap_always_ |= bit;
+      ap_always_ |= uint64_t(1) << i;
       continue;
     }
-    for (auto& l : m->lits) ap_pair_[(uint32_t(uint8_t(l[0])) << 8) | uint8_t(l[1])] |= bit;
+    for (auto& l : m->lits) {
+      uint16_t& slot = ap_pair_[(uint32_t(uint8_t(l[0])) << 8) | uint8_t(l[1])];
+      if (!slot) {
+        ap_lits_.emplace_back();
+        slot = uint16_t(ap_lits_.size());
+      }
+      ap_lits_[slot - 1].push_back({l, uint32_t(i)});
+    }
   }
-  ap_fast_ = true;
+  ap_fast_ = ap_lits_.size() < 65535;
 }
 
 bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
   // Matcher::Match rejects an ASCII path holding none of a rule's (lowercase)
-  // literals, so only the rules a byte pair of the lowered path can start a
-  // literal of (plus the unfiltered ones) can match: evaluate just those.
+  // literals; here the literals are located in one pass over the lowered
+  // path (byte-pair table, then the whole literal), and only the rules with a
+  // literal present (plus the unfiltered ones) run their regex.
   if (ap_fast_ && n <= 1024) {
     uint8_t low[1024];
     bool ascii = true;
@@ -363,12 +371,21 @@ bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
       low[i] = (b >= 'A' && b <= 'Z') ? uint8_t(b + 32) : b;
     }
     if (ascii) {
-      uint64_t mask = ap_always_;
-      for (size_t i = 0; i + 1 < n; i++) mask |= ap_pair_[(uint32_t(low[i]) << 8) | low[i + 1]];
+      uint64_t lit_rules = 0;
+      for (size_t i = 0; i + 1 < n; i++) {
+        const uint16_t slot = ap_pair_[(uint32_t(low[i]) << 8) | low[i + 1]];
+        if (!slot) continue;
+        for (auto& lr : ap_lits_[slot - 1])
+          if (!(lit_rules >> lr.second & 1) && lr.first.size() <= n - i &&
+              std::memcmp(low + i, lr.first.data(), lr.first.size()) == 0)
+            lit_rules |= uint64_t(1) << lr.second;
+      }
+      uint64_t mask = ap_always_ | lit_rules;
       while (mask) {
         const int i = __builtin_ctzll(mask);
         mask &= mask - 1;
-        if (allow_[size_t(i)].path->Match(p, n)) return true;
+        const Matcher& m = *allow_[size_t(i)].path;
+        if ((lit_rules >> i & 1) ? m.re->Match(p, int64_t(n)) : m.Match(p, n)) return true;
       }
       return false;
     }

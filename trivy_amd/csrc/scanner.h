@@ -171,7 +171,8 @@ class SecretScanner {
   void BuildAllowPathFilter();
   bool ap_fast_ = false;
   uint64_t ap_always_ = 0;
-  std::vector<uint64_t> ap_pair_;  // 65536 rule masks
+  std::vector<uint16_t> ap_pair_;  // 65536: 1 + index into ap_lits_, 0 = no literal starts with the pair
+  std::vector<std::vector<std::pair<std::string, uint32_t>>> ap_lits_;  // (literal, allow rule) per pair
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.
