@@ -163,3 +163,51 @@ def test_c3_generated_rules_corpus(secret, tmp_path):
     cfg.write_text(y)
     n = _compare_corpus(secret, _c3_files(samples, 17, 150), str(cfg))
     assert n > 50
+
+
+def test_empty_batch(secret):
+    s = secret.NewScanner(None)
+    assert s.ScanBatch([]) == []
+
+
+def test_secrets_across_tile_and_chunk_boundaries(secret):
+    # K1 walks 4-KiB wave tiles of 64-B lane chunks and counts newlines per 1-KiB
+    # chunk; plant tokens straddling those boundaries at every small shift
+    rng = random.Random(5)
+    tokens = [b"ghp_" + b"a" * 36, b"AKIA" + b"B" * 16, b"xoxb-" + b"1" * 10 + b"-" + b"2" * 12 + b"-" + b"c" * 24,
+              b"glpat-" + b"d" * 20, b"sk_live_" + b"e" * 24]
+    buf = bytearray(b" " * (1 << 20))
+    for i in range(64, len(buf), 64):
+        buf[i - 1] = 0x0A  # a line every 64 B
+    k = 0
+    for base in range(4096, len(buf) - 128, 4096 + 1024 + 64 + 16):
+        t = tokens[k % len(tokens)]
+        st = base - (k % 40)
+        buf[st - 1:st] = b" "
+        buf[st:st + len(t)] = t
+        buf[st + len(t)] = 0x20
+        k += 1
+    files = [("big/a.txt", bytes(buf)), ("small.txt", b"x " + tokens[0])]
+    rng.shuffle(files)
+    n = _compare_corpus(secret, files)
+    assert n > 100
+
+
+def test_no_match_across_file_boundaries(secret):
+    # a token split over two adjacent files of the arena must not be found
+    tok = b"ghp_" + b"f" * 36
+    files = []
+    for cut in range(1, len(tok)):
+        files.append(("a%02d.txt" % cut, b"x " + tok[:cut]))
+        files.append(("b%02d.txt" % cut, tok[cut:] + b" y"))
+    files += [("tiny%04d.txt" % i, bytes([0x41 + i % 26]) * (i % 7)) for i in range(2000)]
+    assert _compare_corpus(secret, files) == 0
+
+
+def test_binary_files_match_message(secret):
+    files = [("bin/a.pyc", b"ghp_" + b"z" * 36 + b"\n"), ("bin/é.dat", b"AKIA" + b"Q" * 16)]
+    s = secret.NewScanner(None)
+    o = osc.new_scanner(None)
+    got = s.ScanBatch([secret.ScanArgs(FilePath=p, Content=b, Binary=True) for p, b in files])
+    for (p, b), g in zip(files, got):
+        assert g.to_dict() == o.scan(p, b, binary=True), p
