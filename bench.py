@@ -125,7 +125,7 @@ WORKLOADS = {
     "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
            20.0, 32.0),
     "c3": ("2,000 generated custom rules (trivy-secret.yaml) + 87 builtins over a %g GB synthetic corpus per "
-           "MI355X (BASELINE configs[2])", 8.0, 1.5),
+           "MI355X (BASELINE configs[2])", 8.0, 0.4),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
            "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0),
 }
