@@ -78,6 +78,7 @@ class GpuEngine {
   uint32_t* d_bucket_groups_ = nullptr;
   void* d_ftabs_ = nullptr;
   void* d_fold_pairs_ = nullptr;  // fold kernel work list
+  void* d_fold_first_ = nullptr;  // per item: bytes that can start it (fold kernel prefilter)
   uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0;

@@ -739,6 +739,7 @@ struct FoldParams {
   uint32_t tabs_bytes, t_items, t_item_ids, t_item_cls, t_classes, n_items;
   const FoldPair* pairs;  // [k-site pairs | s-site pairs]
   uint32_t n_pairs_k, n_pairs_s;
+  const uint32_t* first;  // per item 8 x u32: bytes its position 0 accepts (+ E2 / C5 fold leads)
   const FoldSite* folds;
   uint32_t fold_cap;
   uint32_t* hits;
@@ -785,9 +786,12 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
     for (uint32_t t = threadIdx.x; t < n_pairs; t += blockDim.x) {
       const FoldPair fp = pairs[t];
       const FilterItemGpu it = items[fp.item];
+      const uint32_t* first = P.first + 8ull * fp.item;
       for (uint32_t back = fp.lo; back <= fp.hi; back++) {
         if (fsite.x < w0 + back) break;
         const uint64_t st = fsite.x - back;
+        const uint32_t b0 = s_bytes[st - w0];
+        if (!((first[b0 >> 5] >> (b0 & 31)) & 1u)) continue;  // position 0 fails (superset test)
         uint64_t p = st, lit_bytes_end = 0;
         bool ok = true, covered = false;
         for (uint32_t q = 0; q < it.n && ok; q++) {
@@ -988,6 +992,19 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
         if (klo >= 0) add(pk, klo, khi);
         if (slo >= 0) add(ps, slo, shi);
       }
+      std::vector<uint32_t> first(8 * std::max<size_t>(ft->items.size(), 1), ~0u);
+      for (uint32_t i = 0; i < uint32_t(ft->items.size()); i++) {
+        const FilterItemGpu& it = ft->items[i];
+        if (it.n == 0) continue;
+        const uint32_t c = ft->item_cls[it.cls_off];
+        uint32_t* m = &first[8ull * i];
+        for (int w = 0; w < 8; w++) m[w] = ft->classes[c * 8 + w];
+        if (in_cls(c, 'k') || in_cls(c, 'K')) m[0xE2 >> 5] |= 1u << (0xE2 & 31);
+        if (in_cls(c, 's') || in_cls(c, 'S')) m[0xC5 >> 5] |= 1u << (0xC5 & 31);
+      }
+      uint8_t* dfm = nullptr;
+      if (!Upload(&err_, &dfm, reinterpret_cast<const uint8_t*>(first.data()), first.size() * sizeof(uint32_t))) return;
+      d_fold_first_ = dfm;
       n_fold_pairs_k_ = uint32_t(pk.size());
       n_fold_pairs_s_ = uint32_t(ps.size());
       pk.insert(pk.end(), ps.begin(), ps.end());
@@ -1016,7 +1033,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_fold_pairs_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
@@ -1155,6 +1172,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.t_classes = ft_classes_;
     fo.n_items = n_fitems_;
     fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
+    fo.first = static_cast<const uint32_t*>(d_fold_first_);
     fo.n_pairs_k = n_fold_pairs_k_;
     fo.n_pairs_s = n_fold_pairs_s_;
     fo.folds = static_cast<const FoldSite*>(d_folds_);
