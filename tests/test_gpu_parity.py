@@ -211,3 +211,33 @@ def test_binary_files_match_message(secret):
     got = s.ScanBatch([secret.ScanArgs(FilePath=p, Content=b, Binary=True) for p, b in files])
     for (p, b), g in zip(files, got):
         assert g.to_dict() == o.scan(p, b, binary=True), p
+
+
+def test_fold_runes_in_custom_rule_items(secret, tmp_path):
+    """U+212A / U+017F standing for k / s inside custom (?i) literals and inside class
+    positions of token rules (the fold kernel's position-0 byte prefilter and covering
+    starts), vs the oracle."""
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(
+        "rules:\n"
+        "  - id: kw-assign\n    category: Custom\n    title: KW\n    severity: HIGH\n"
+        "    regex: '(?i)(?P<key>kwsk01[a-z0-9_ .\\-,]{0,25})(=|:=|:).{0,5}[''\"](?P<secret>[a-z0-9]{16})[''\"]'\n"
+        "    secret-group-name: secret\n    keywords: [kwsk01]\n"
+        "  - id: pfx-token\n    category: Custom\n    title: PFX\n    severity: LOW\n"
+        "    regex: 'pfx42_[A-Za-z0-9]{12}'\n    keywords: [pfx42_]\n"
+        "  - id: ci-token\n    category: Custom\n    title: CI\n    severity: LOW\n"
+        "    regex: '(?i)sks_[a-z]{6}'\n")
+    K, S = "K", "ſ"
+    bodies = [
+        "kwsk01 = '0123456789abcdef'", K + "wsk01 = 'abcdefabcdef0123'", "kw" + S + "k01: \"0123456789abcdef\"",
+        "KWS" + K + "01_x := 'aaaaaaaaaaaaaaaa'", "pfx42_abcdefABCDEF", "pfx42_abc" + K + "defABCDE",
+        "pfx42_" + S + "abcdefABCDEF", S + "ks_abcdef", "s" + K + "s_ABCDEF", "SK" + S + "_abcdef x",
+        K * 3 + " " + S * 5, "İ kwsk01='0123456789abcdef'",
+    ]
+    rng = random.Random(9)
+    files = []
+    for i in range(60):
+        parts = [rng.choice(bodies) for _ in range(rng.randint(1, 5))]
+        pad = "x" * rng.randint(0, 300)
+        files.append(("c%02d.txt" % i, ("\n" + pad + " ").join(parts).encode()))
+    assert _compare_corpus(secret, files, str(cfg)) > 100
