@@ -844,7 +844,7 @@ __device__ uint32_t gate_flags(const NfaParams& P, const RuleGpu& rg, uint32_t f
 // whose literal bytes may be up to 3x its length); the rule's relaxed NFA runs
 // from wlo with injection up to whi, reading the arena 16 B at a time; an
 // accept emits the candidate with the line count before wlo.
-__global__ __launch_bounds__(256) void verify_hits_kernel(NfaParams P) {
+__global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
   const uint32_t n = P.counters[0] < P.hit_cap ? P.counters[0] : P.hit_cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t f = P.hits[3ull * i], end = P.hits[3ull * i + 1], aid = P.hits[3ull * i + 2];
