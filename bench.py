@@ -44,13 +44,15 @@ def _cpu_sample_worker(args):
     sc = osc.new_scanner(osc.parse_config(cfg_path) if cfg_path else None)
     nb = 0
     nf = 0
+    res = {}
     for i in idx:
         b = arena[int(offs[i]):int(offs[i + 1])].tobytes()
         p = paths[i * 64:(i + 1) * 64].tobytes().split(b"\0", 1)[0].decode()
         r = sc.scan(p, b)
         nb += len(b)
         nf += len(r["Findings"] or [])
-    return nb, nf
+        res[i] = r
+    return nb, nf, res
 
 
 def _cpu_layer_worker(args):
@@ -113,12 +115,26 @@ def cpu_baseline(C, sample_bytes, cores, tmpdir, cfg_path=None):
     dt = time.time() - t0
     nb = sum(r[0] for r in res)
     nf = sum(r[1] for r in res)
+    want = {}
+    for r in res:
+        want.update(r[2])
     for f in (ap, op, pp):
         os.remove(f)
     return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": cores, "kind": "port",
             "sample": "first %d files (%.1f MB) of the same corpus, oracle/secret_scanner.py "
                       "(Python restatement of scanner.go%s) in %d processes; %d findings; %.1f s wall"
-                      % (n, nb / 1e6, ", same rule set" if cfg_path else "", cores, nf, dt)}
+                      % (n, nb / 1e6, ", same rule set" if cfg_path else "", cores, nf, dt)}, want
+
+
+def parity_block(C, last_result, want):
+    """Findings of the GPU's last timed step vs the oracle, file by file (sample files)."""
+    n = len(want)
+    got = last_result.secrets([C.path(i) for i in range(n)], lo=0)
+    bad = [i for i in range(n) if got[i].to_dict() != want[i]]
+    return {"files": n, "findings": sum(len(w["Findings"] or []) for w in want.values()),
+            "mismatches": len(bad), "first_mismatch": (C.path(bad[0]) if bad else None),
+            "reference": "oracle/secret_scanner.py (scanner.go:377-463 restated, pinned by the reference's "
+                         "golden tests)"}
 
 
 WORKLOADS = {
@@ -198,16 +214,16 @@ def main():
             # pipelined: step i+1's kernels run while step i's exact host pass finishes
             # (tsg_scan_submit; --depth 1 runs the steps back to back)
             inflight = []
+            r = None
             for _ in range(n):
                 inflight.append(submit())
                 if len(inflight) >= args.depth:
                     r = inflight.pop(0).wait()
                     stats.append(r.stats())
-                    del r
             while inflight:
                 r = inflight.pop(0).wait()
                 stats.append(r.stats())
-                del r
+            last[0] = r
     else:
         from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
         from trivy_amd.analyzer.secret import Collector
@@ -223,6 +239,7 @@ def main():
                 an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
                 stats.append(st)
 
+    last = [None]  # the last step's ScanResult (findings checked against the oracle below)
     warm = []
     run_steps(args.warmup, warm)
 
@@ -285,10 +302,12 @@ def main():
 
     if rank == 0:
         cpu = None
+        parity = None
         if world == 1 and not args.no_cpu_baseline:
             cores = min(16, os.cpu_count() or 1)
             if layer is None:
-                cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), cores, tmpdir, cfg_path)
+                cpu, want = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), cores, tmpdir, cfg_path)
+                parity = parity_block(C, last[0], want)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
                 cpu = cpu_baseline_layer(sample, cores, tmpdir)
@@ -313,11 +332,15 @@ def main():
                          "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 4),
                          "traffic": traffic},
             "cpu_baseline": cpu,
+            "parity": parity,
             "breakdown_ms": breakdown,
             "counts": counts,
             "gen_s": round(t_gen, 2),
         }
         print(json.dumps(out), flush=True)
+        if parity is not None and parity["mismatches"]:
+            sys.exit("parity: %d of %d sample files differ from the oracle (first: %s)"
+                     % (parity["mismatches"], parity["files"], parity["first_mismatch"]))
     if cfg_path:
         os.remove(cfg_path)
     if dist is not None:

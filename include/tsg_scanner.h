@@ -28,8 +28,8 @@ extern "C" {
 
 typedef struct tsg_allow_rule {  /* AllowRule, scanner.go:196-201 */
   const char* id;
-  const char* regex;             /* NULL or "" = none */
-  const char* path;              /* NULL or "" = none */
+  const char* regex;             /* NULL = none; "" = matches everything (Go compiles "") */
+  const char* path;              /* NULL = none; "" = matches everything */
 } tsg_allow_rule;
 
 typedef struct tsg_rule {        /* Rule, scanner.go:89-100 */
@@ -37,8 +37,8 @@ typedef struct tsg_rule {        /* Rule, scanner.go:89-100 */
   const char* category;
   const char* title;
   const char* severity;          /* already normalised by ParseConfig */
-  const char* regex;             /* NULL = rule without regex (never matches) */
-  const char* path;              /* NULL = any path */
+  const char* regex;             /* NULL = rule without regex (never matches); "" = empty regex */
+  const char* path;              /* NULL = any path; "" = empty regex (matches every path) */
   const char* secret_group_name; /* "" = whole match */
   const char* const* keywords;
   uint32_t n_keywords;
@@ -110,6 +110,8 @@ int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t lin
 
 /* Whole batch as JSON ([{"kind":..,"findings":[..]}...], Go field names). */
 int tsg_result_json(const tsg_result* r, const char** json, uint64_t* len);
+/* Files [lo, hi) only (same format; the text stays valid until the next json call on r). */
+int tsg_result_json_range(const tsg_result* r, uint32_t lo, uint32_t hi, const char** json, uint64_t* len);
 
 /* Timings / counters of the batch (GPU ms from HIP events on the engine stream). */
 typedef struct tsg_stats {

@@ -256,7 +256,7 @@ class Scanner:
             f = to_finding(rule, loc, bytes(censored))
             if binary:
                 f["Match"] = "Binary file %s matches a rule %s" % (quote(path), quote(_b(rule.title)))
-                f["Code"] = {"Lines": []}
+                f["Code"] = {"Lines": None}  # types.Code{}: Lines is nil -> JSON null
             findings.append(f)
         if not findings:
             return {"FilePath": "", "Findings": None}

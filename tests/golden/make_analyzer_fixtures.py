@@ -44,7 +44,7 @@ WANT2 = _finding("rule1", "general", "Generic Rule", "HIGH", 4, 4, 'secret="****
 WANT_PAT = _finding("github-fine-grained-pat", "GitHub", "GitHub Fine-grained personal access tokens",  # :95-104
                     "CRITICAL", 1, 1,
                     'Binary file "/testdata/secret.cpython-310.pyc" matches a rule '
-                    '"GitHub Fine-grained personal access tokens"', [])
+                    '"GitHub Fine-grained personal access tokens"', None)  # types.Code{}: Lines nil
 
 ANALYZE = [  # secret_test.go:106-176
     {"name": "return results", "config": "testdata/config.yaml", "file": "testdata/secret.txt", "dir": ".",

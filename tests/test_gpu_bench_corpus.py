@@ -1,0 +1,109 @@
+"""GPU parity on the bench's own corpus generator (trivy_amd/csrc/corpus.cpp).
+
+The bench (BASELINE configs[1]/[2]) scans corpora made by the C++ generator:
+log-normal file sizes up to 10 MiB, 0.1 % minified lines over 10 KiB, 2 %
+UTF-8 files with fold runes and invalid bytes, planted secrets.  These tests
+scan a whole generated arena through the C-ABI (the same call the bench
+times) and compare every selected file -- the multi-MiB ones, files holding a
+> 10 KiB line, fold-rune files and a random sample -- field for field with
+the oracle (pkg/fanal/secret/scanner.go:377-463 restated).  The oracle runs
+in a process pool (it is pure Python).
+"""
+import multiprocessing as mp
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POOL = min(16, os.cpu_count() or 1)
+
+
+def _oracle_worker(args):
+    items, cfg_path = args
+    from oracle import secret_scanner as osc
+    sc = osc.new_scanner(osc.parse_config(cfg_path) if cfg_path else None)
+    return [(i, sc.scan(p, b)) for i, p, b in items]
+
+
+def _oracle(items, cfg_path=None):
+    """items: [(index, path, content)] -> {index: oracle result}, largest files spread first."""
+    items = sorted(items, key=lambda t: -len(t[2]))
+    shards = [items[k::POOL] for k in range(POOL)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(POOL) as pool:
+        out = {}
+        for part in pool.map(_oracle_worker, [(s, cfg_path) for s in shards if s]):
+            out.update(part)
+    return out
+
+
+def _select(C, rng, sample_bytes):
+    sizes = np.diff(C.offsets.astype(np.int64))
+    big = [int(i) for i in np.nonzero(sizes >= (1 << 20))[0]]
+    chosen = set(big)
+    long_line, fold = [], []
+    for i in range(C.n_files):
+        if len(long_line) >= 6 and len(fold) >= 12:
+            break
+        if sizes[i] > (1 << 20) or sizes[i] < 12 << 10:
+            continue
+        b = C.content(i)
+        if len(long_line) < 6 and max(len(x) for x in b.split(b"\n")) > 10240:
+            long_line.append(i)
+        elif len(fold) < 12 and (b"\xe2\x84\xaa" in b or b"\xc5\xbf" in b or b"\xc4\xb0" in b):
+            fold.append(i)
+    chosen.update(long_line + fold)
+    order = list(range(C.n_files))
+    rng.shuffle(order)
+    tot = 0
+    for i in order:
+        if tot >= sample_bytes:
+            break
+        if sizes[i] < (1 << 20):
+            chosen.add(i)
+            tot += int(sizes[i])
+    return sorted(chosen), big, long_line, fold
+
+
+def _check(C, res, chosen, want):
+    from trivy_amd.secret.scanner import Secret  # noqa: F401
+    n_find = 0
+    for i in chosen:
+        got = res.secrets([C.path(i)], lo=i)[0].to_dict()
+        assert got == want[i], (i, C.path(i))
+        n_find += len(want[i]["Findings"] or [])
+    return n_find
+
+
+def test_bench_corpus_c2_matches_oracle():
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    C = corpus.generate(int(160e6), seed=corpus.SEED + 7)
+    chosen, big, long_line, fold = _select(C, random.Random(3), 3e6)
+    assert len(big) >= 2 and long_line and fold, (len(big), len(long_line), len(fold))
+    s = secret.NewScanner(None)
+    res = s.scan_arena(C.arena, C.offsets, C.path_ptrs)
+    want = _oracle([(i, C.path(i), C.content(i)) for i in chosen])
+    n = _check(C, res, chosen, want)
+    assert n > 20
+
+
+def test_bench_corpus_c3_matches_oracle(tmp_path):
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    y, samples = corpus.c3_rules()
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(y)
+    C = corpus.generate_c3(int(24e6), samples, seed=corpus.SEED + 11, secrets_per_byte=1.0 / 16384)
+    rng = random.Random(4)
+    sizes = np.diff(C.offsets.astype(np.int64))
+    small = [i for i in range(C.n_files) if sizes[i] < 200000]
+    chosen = sorted(rng.sample(small, 160))
+    s = secret.NewScanner(secret.ParseConfig(str(cfg)))
+    res = s.scan_arena(C.arena, C.offsets, C.path_ptrs)
+    want = _oracle([(i, C.path(i), C.content(i)) for i in chosen], str(cfg))
+    n = _check(C, res, chosen, want)
+    assert n > 20

@@ -45,7 +45,8 @@ def go_string(tok: str) -> str:
 STR_TOK = r'(`[^`]*`|"(?:[^"\\]|\\.)*")'
 
 
-def main(ref_root: str) -> None:
+def extract(ref_root: str) -> dict:
+    """The builtin rule data of the reference tree at ref_root (what builtin_rules.json holds)."""
     src = Path(ref_root, "pkg/fanal/secret/builtin-rules.go").read_text()
     allow_src = Path(ref_root, "pkg/fanal/secret/builtin-allow-rules.go").read_text()
 
@@ -103,13 +104,20 @@ def main(ref_root: str) -> None:
         r["regex"] = go_string(rm.group(1)) if rm else None
         allow.append(r)
 
-    out = {
+    return {
         "source": "undistro/trivy@2024-12-20 pkg/fanal/secret/builtin-rules.go:101-849, "
                   "builtin-allow-rules.go:3-65 (expanded regex source strings)",
         "rules": rules,
         "allow_rules": allow,
     }
-    dst = Path(__file__).resolve().parent.parent / "trivy_amd/secret/builtin_rules.json"
+
+
+DST = Path(__file__).resolve().parent.parent / "trivy_amd/secret/builtin_rules.json"
+
+
+def main(ref_root: str) -> None:
+    out = extract(ref_root)
+    rules, allow, dst = out["rules"], out["allow_rules"], DST
     dst.write_text(json.dumps(out, indent=1, ensure_ascii=False) + "\n")
     print("wrote %d rules, %d allow rules -> %s" % (len(rules), len(allow), dst))
 

@@ -213,6 +213,18 @@ class PendingBatch:
     def __init__(self, coll: Collector, h):
         self.coll, self._h = coll, h
 
+    def __del__(self):
+        # dropped without wait() (e.g. an exception in the caller's loop): the
+        # scan thread still reads the collector's arena, so join it first
+        h = getattr(self, "_h", None)
+        if h:
+            r = c.c_void_p()
+            self.coll._L.tsg_scan_wait(h, c.byref(r))
+            self._h = None
+            if r:
+                self.coll._L.tsg_result_free(r)
+            self.coll.reset()
+
     def wait(self, materialize: bool = True):
         """Per batch file: the Secret when it has findings (Analyze's result), else None.
         materialize=False: only the batch's tsg_stats (dict), no per-file objects."""
@@ -340,25 +352,31 @@ class SecretAnalyzer:
         pending = None
         cursor, k, done = 0, 0, False
         t_walk = t_wait = 0.0
-        while not done:
-            coll = colls[k]
-            t0 = time.perf_counter()
-            rc, cursor = coll.add_tar(layer, cursor, st)
-            t_walk += time.perf_counter() - t0
-            done = rc == 0
-            if rc == 1 and coll.files() == 0:
-                raise RuntimeError("tar layer: an entry does not fit an empty collector")
-            nxt = coll.submit() if coll.files() else None
+        try:
+            while not done:
+                coll = colls[k]
+                t0 = time.perf_counter()
+                rc, cursor = coll.add_tar(layer, cursor, st)
+                t_walk += time.perf_counter() - t0
+                done = rc == 0
+                if rc == 1 and coll.files() == 0:
+                    raise RuntimeError("tar layer: an entry does not fit an empty collector")
+                nxt = coll.submit() if coll.files() else None
+                t0 = time.perf_counter()
+                if pending is not None:
+                    p, pending = pending, None
+                    take(p)
+                t_wait += time.perf_counter() - t0
+                pending = nxt
+                k ^= 1
             t0 = time.perf_counter()
             if pending is not None:
-                take(pending)
+                p, pending = pending, None
+                take(p)
             t_wait += time.perf_counter() - t0
-            pending = nxt
-            k ^= 1
-        t0 = time.perf_counter()
-        if pending is not None:
-            take(pending)
-        t_wait += time.perf_counter() - t0
+        finally:
+            if pending is not None:  # an error left a batch in flight: join it before the arenas go
+                pending.__del__()
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})

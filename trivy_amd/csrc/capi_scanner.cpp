@@ -85,8 +85,10 @@ class ResultReaper {
 namespace {
 std::string Str(const char* s) { return s ? std::string(s) : std::string(); }
 
+// NULL = no regex; "" is a regex that matches everywhere (Go compiles it,
+// Regexp.UnmarshalYAML, scanner.go:75-87).
 bool MakeMatcher(const char* src, std::unique_ptr<tsg::Matcher>* out, std::string* err) {
-  if (!src || !*src) return true;
+  if (!src) return true;
   auto re = tsg::Regex::Compile(src, err);
   if (!re) return false;
   out->reset(new tsg::Matcher());
@@ -125,6 +127,7 @@ bool MakeRules(const tsg_global* g, std::vector<tsg::RuleSpec>* rules, std::stri
     s.severity = Str(r.severity);
     s.secret_group_name = Str(r.secret_group_name);
     s.regex_src = Str(r.regex);
+    s.has_regex = r.regex != nullptr;
     for (uint32_t k = 0; k < r.n_keywords; k++) s.keywords.push_back(Str(r.keywords[k]));
     if (!MakeMatcher(r.path, &s.path, err)) return false;
     if (!MakeAllow(r.allow_rules, r.n_allow_rules, &s.allow_rules, err)) return false;
@@ -250,8 +253,9 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   r->owner = s->s.get();
   tsg::BatchStats gs;
   tsg::HostStats hs;
-  if (!s->s->Scan(in, &r->files, &gs, &hs)) {
-    tsg::SetError(s->s->error());
+  std::string err;
+  if (!s->s->Scan(in, &r->files, &gs, &hs, &err)) {
+    tsg::SetError(err);
     return -1;
   }
   tsg_stats& st = r->stats;
@@ -314,18 +318,18 @@ int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t lin
   return 0;
 }
 
-int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
-  tsg_result* r = const_cast<tsg_result*>(rc);
-  if (r->json.empty()) {
+namespace {
+void ResultJson(const tsg_result* r, uint32_t lo, uint32_t hi, std::string* out) {
+  {
     const auto& rules = r->owner->rules();
-    std::string& o = r->json;
-    o.reserve(256 + r->stats.findings * 512);
+    std::string& o = *out;
+    o.reserve(256 + size_t(hi - lo) * 32);
     o.push_back('[');
     static const tsg::FileFindings kNone;
-    for (size_t i = 0; i < r->files.kind.size(); i++) {
+    for (size_t i = lo; i < hi; i++) {
       const auto* fv = r->files.Findings(uint32_t(i));
       const auto& findings = fv ? *fv : kNone;
-      if (i) o.push_back(',');
+      if (i > lo) o.push_back(',');
       o += "{\"kind\":" + std::to_string(int(r->files.kind[i])) + ",\"findings\":[";
       for (size_t k = 0; k < findings.size(); k++) {
         const auto& f = findings.f[k];
@@ -340,7 +344,8 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
         o += ",\"Title\":";
         JsonStr(&o, R.title);
         o += ",\"StartLine\":" + std::to_string(f.start_line) + ",\"EndLine\":" + std::to_string(f.end_line);
-        o += ",\"Code\":{\"Lines\":[";
+        // binary files: types.Code{} -> "Lines":null (scanner.go:441-444)
+        o += findings.binary ? ",\"Code\":{\"Lines\":null" : ",\"Code\":{\"Lines\":[";
         for (uint32_t j = f.line_lo; j < f.line_hi; j++) {
           const auto& l = findings.lines[j];
           const std::string content(findings.Str(l.off, l.len));
@@ -357,7 +362,7 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
           o += l.last_cause ? "true" : "false";
           o.push_back('}');
         }
-        o += "]},\"Match\":";
+        o += findings.binary ? "},\"Match\":" : "]},\"Match\":";
         JsonStr(&o, std::string(findings.Match(f)));
         o.push_back('}');
       }
@@ -365,6 +370,22 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
     }
     o.push_back(']');
   }
+}
+}  // namespace
+
+int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
+  tsg_result* r = const_cast<tsg_result*>(rc);
+  if (r->json.empty()) ResultJson(r, 0, uint32_t(r->files.kind.size()), &r->json);
+  *json = r->json.data();
+  *len = r->json.size();
+  return 0;
+}
+
+int tsg_result_json_range(const tsg_result* rc, uint32_t lo, uint32_t hi, const char** json, uint64_t* len) {
+  tsg_result* r = const_cast<tsg_result*>(rc);
+  if (lo > hi || hi > r->files.kind.size()) return -1;
+  r->json.clear();
+  ResultJson(r, lo, hi, &r->json);
   *json = r->json.data();
   *len = r->json.size();
   return 0;
@@ -412,7 +433,7 @@ int tsg_debug_compile(const tsg_global* g, tsg_compiled** out) {
   std::vector<tsg::RuleSrc> src;
   for (uint32_t i = 0; i < g->n_rules; i++) {
     const tsg_rule& r = g->rules[i];
-    tsg::RuleSrc s{Str(r.id), Str(r.regex), {}};
+    tsg::RuleSrc s{Str(r.id), Str(r.regex), {}, r.regex != nullptr};
     for (uint32_t k = 0; k < r.n_keywords; k++) s.keywords.push_back(Str(r.keywords[k]));
     src.push_back(std::move(s));
   }

@@ -16,6 +16,7 @@ namespace tsg {
 
 namespace {
 constexpr int64_t kInf = int64_t(1) << 40;
+constexpr size_t kMaxAnchorLit = 32;
 
 bool IsFoldOnlyRune(uint32_t r) { return r == 0x212A || r == 0x17F || r == 0x130; }
 
@@ -148,7 +149,7 @@ struct Analyzer {
     std::vector<int> items, run;
     Flatten(i, &items);
     for (int it : items) {
-      if (LitChar(nodes[it]) < 0) break;
+      if (LitChar(nodes[it]) < 0 || run.size() >= kMaxAnchorLit) break;
       run.push_back(it);
     }
     return run;
@@ -161,7 +162,7 @@ struct Analyzer {
     std::string s;
     for (int it : items) {
       int c = LitChar(nodes[it]);
-      if (c < 0) break;
+      if (c < 0 || s.size() >= kMaxAnchorLit) break;
       s.push_back(char(c));
     }
     return s;
@@ -203,10 +204,14 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
         j++;
       }
       if (ohi < kInf || !need_offset) {
-        Cand cd{{s}, olo, ohi};
+        // an anchor literal is at most kMaxAnchorLit chars: the rest of a
+        // longer run stays in the follow sequence (the prefilter item and
+        // the fold kernel's window assume short items)
+        const size_t jl = std::min(j, k + kMaxAnchorLit);
+        Cand cd{{s.substr(0, jl - k)}, olo, ohi};
         cd.ohi_fold = ohf;
-        cd.follow.push_back(tail(j));
-        cd.lit_nodes.push_back(std::vector<int>(items.begin() + long(k), items.begin() + long(j)));
+        cd.follow.push_back(tail(jl));
+        cd.lit_nodes.push_back(std::vector<int>(items.begin() + long(k), items.begin() + long(jl)));
         cd.pre_k = k;
         cands.push_back(cd);
       }
@@ -414,19 +419,34 @@ std::vector<Elem> Relax(const std::vector<Node>& nodes, int i) {
 
 int64_t Positions(const Elem& e) { return e.max >= 0 ? e.max : std::max<int64_t>(e.min, 1); }
 
-void BuildNfa(std::vector<Elem> seq, std::vector<uint64_t>* nfa, RuleGpu* rg) {
-  // fit into kMaxNfaWords * 64 positions by relaxing the largest elements
+// Shrinks a relaxed sequence to at most `budget` NFA positions, keeping it a
+// superset: the largest element is relaxed first (X{m,n} -> X{m,}, then
+// X{m,} -> X{m/2,}); once every element is a single position, the last two
+// elements merge into one [X|Y]{0,} (X{a,b}Y{c,d} is inside it), so every
+// round strictly lowers the element count or the position total.
+void FitPositions(std::vector<Elem>* seq_p, int64_t budget) {
+  std::vector<Elem>& seq = *seq_p;
   for (;;) {
     int64_t tot = 0;
     for (auto& e : seq) tot += Positions(e);
-    if (tot <= 64 * kMaxNfaWords) break;
+    if (tot <= budget || seq.empty()) break;
     size_t big = 0;
     for (size_t k = 1; k < seq.size(); k++)
       if (Positions(seq[k]) > Positions(seq[big])) big = k;
     Elem& e = seq[big];
-    if (e.max >= 0 && e.max > e.min) e.max = -1;
-    else { e.min = e.min / 2; e.max = -1; }
+    if (Positions(e) > 1) {
+      if (e.max >= 0 && e.max > e.min) e.max = -1;
+      else { e.min = e.min / 2; e.max = -1; }
+      continue;
+    }
+    Elem m{seq[seq.size() - 2].reach | seq.back().reach, 0, -1};
+    seq.pop_back();
+    seq.back() = m;
   }
+}
+
+void BuildNfa(std::vector<Elem> seq, std::vector<uint64_t>* nfa, RuleGpu* rg) {
+  FitPositions(&seq, 64 * kMaxNfaWords);  // fit into kMaxNfaWords * 64 positions
   int64_t P = 0;
   for (auto& e : seq) P += Positions(e);
   rg->nfa_off = uint32_t(nfa->size());
@@ -768,7 +788,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     const RuleSrc& r = src[ri];
     RuleGpu rg{};
     std::unique_ptr<Regex> re;
-    if (!r.regex.empty()) {
+    if (r.has_regex) {
       re = Regex::Compile(r.regex, err);
       if (!re) return false;
       rg.has_regex = 1;

@@ -39,8 +39,9 @@ bool KeywordsImplied(const Regex& re, const std::vector<std::string>& kws_lower,
 
 struct RuleSrc {
   std::string id;
-  std::string regex;  // empty: rule has no regex (never matches)
+  std::string regex;
   std::vector<std::string> keywords;
+  bool has_regex = true;  // false: Rule.Regex == nil (never matches); "" is a regex
 };
 
 struct AnchorInfo {  // mirrored on the device

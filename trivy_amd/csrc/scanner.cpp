@@ -291,7 +291,7 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
                              std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err)
     : rules_(std::move(rules)), allow_(std::move(allow)), exclude_(std::move(exclude)) {
   std::vector<RuleSrc> src;
-  for (auto& r : rules_) src.push_back({r.id, r.regex_src, r.keywords});
+  for (auto& r : rules_) src.push_back({r.id, r.regex_src, r.keywords, r.has_regex});
   if (!CompileRules(src, &cr_, &err_)) {
     *err = err_;
     return;
@@ -781,6 +781,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   };
 
   out->kind = kHasFindings;
+  ff.binary = binary;
   PhaseTimer pt3(3);
   ff.f.reserve(matched.size());
   ff.lines.reserve(matched.size() * 5);
@@ -844,13 +845,13 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   SortFindings(&out->findings, rules_);
 }
 
-bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst) {
+bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst, std::string* err) {
   double t0 = NowMs();
   HostStats hs;
   std::vector<Candidate> cands;
   uint64_t n_bytes = in.n_files ? in.host_offsets[in.n_files] : 0;
   if (engines_.empty()) {
-    err_ = "no GPU engine bound to this scanner";
+    *err = "no GPU engine bound to this scanner";
     return false;
   }
   const size_t slot = size_t(next_slot_.fetch_add(1) % engines_.size());
@@ -876,7 +877,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   }
   allow_thread.join();
   if (!ok) {
-    err_ = gpu_err;
+    *err = gpu_err;
     return false;
   }
   double t1 = NowMs();

@@ -38,6 +38,7 @@ struct AllowRuleSpec {
 struct RuleSpec {
   std::string id, category, title, severity, secret_group_name;
   std::string regex_src;
+  bool has_regex = false;  // Rule.Regex != nil (an empty source is a regex)
   std::vector<std::string> keywords;
   std::unique_ptr<Matcher> path;
   std::vector<AllowRuleSpec> allow_rules;
@@ -65,6 +66,7 @@ struct FileFindings {
   std::vector<FindingOut> f;
   std::vector<LineOut> lines;
   std::string text;
+  bool binary = false;  // ScanArgs.Binary: findings carry Code{} (Lines nil, scanner.go:441-444)
   size_t size() const { return f.size(); }
   std::string_view Str(uint32_t off, uint32_t len) const { return std::string_view(text).substr(off, len); }
   std::string_view Match(const FindingOut& x) const { return Str(x.match_off, x.match_len); }
@@ -130,7 +132,8 @@ class SecretScanner {
   }
   const std::string& error() const { return err_; }
 
-  bool Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst);
+  // Thread-safe: concurrent scans report failures through *err only (no shared state).
+  bool Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst, std::string* err);
   // The exact host tail over a given candidate list (what Scan runs after the GPU).
   // The exact host pass over the GPU's candidates.  `allowed` (per-file
   // global AllowPath results) is computed here when not supplied.

@@ -70,6 +70,8 @@ def _declare(L):
     L.tsg_scan_wait.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L.tsg_result_free.argtypes = [c.c_void_p]
     L.tsg_result_json.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_uint64)]
+    L.tsg_result_json_range.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.POINTER(c.c_void_p),
+                                        c.POINTER(c.c_uint64)]
     L.tsg_result_stats.argtypes = [c.c_void_p, c.POINTER(_CStats)]
     L.tsg_scanner_table_info.argtypes = [c.c_void_p, c.POINTER(_CTableInfo)]
     L.tsg_scanner_rule_anchor.argtypes = [c.c_void_p, c.c_uint32]
@@ -103,8 +105,8 @@ class Line:  # pkg/fanal/types/misconf.go:52-61
 
 
 @dataclass
-class Code:  # misconf.go:48-50
-    Lines: List[Line] = field(default_factory=list)
+class Code:  # misconf.go:48-50 (Lines is None for binary files: types.Code{})
+    Lines: Optional[List[Line]] = field(default_factory=list)
 
 
 @dataclass
@@ -121,7 +123,8 @@ class SecretFinding:  # pkg/fanal/types/secret.go:10-20
     def to_dict(self):
         return {"RuleID": self.RuleID, "Category": self.Category, "Severity": self.Severity,
                 "Title": self.Title, "StartLine": self.StartLine, "EndLine": self.EndLine,
-                "Code": {"Lines": [dict(l.__dict__) for l in self.Code.Lines]}, "Match": self.Match}
+                "Code": {"Lines": None if self.Code.Lines is None else [dict(l.__dict__) for l in self.Code.Lines]},
+                "Match": self.Match}
 
 
 @dataclass
@@ -160,8 +163,8 @@ class CGlobal:
         arr = (_CAllowRule * max(1, len(items)))()
         for i, a in enumerate(items):
             arr[i].id = _b(a.ID)
-            arr[i].regex = _b(a.Regex) if a.Regex else None
-            arr[i].path = _b(a.Path) if a.Path else None
+            arr[i].regex = _b(a.Regex)  # None = no regex; "" is a regex (matches everything)
+            arr[i].path = _b(a.Path)
         self._keep.append(arr)
         return arr
 
@@ -170,8 +173,8 @@ class CGlobal:
         for i, r in enumerate(self.Rules):
             x = rs[i]
             x.id, x.category, x.title, x.severity = _b(r.ID), _b(r.Category), _b(r.Title), _b(r.Severity)
-            x.regex = _b(r.Regex) if r.Regex else None
-            x.path = _b(r.Path) if r.Path else None
+            x.regex = _b(r.Regex)
+            x.path = _b(r.Path)
             x.secret_group_name = _b(r.SecretGroupName or "")
             x.keywords = self._cstrs(r.Keywords)
             x.n_keywords = len(r.Keywords)
@@ -300,6 +303,17 @@ class PendingScan:
         self._h = h
         self._keep = keep
 
+    def __del__(self):
+        # dropped without wait(): the native scan thread still borrows the
+        # arena / offsets / paths kept here, so join it before they are freed
+        h = getattr(self, "_h", None)
+        if h:
+            r = c.c_void_p()
+            self._sc._L.tsg_scan_wait(h, c.byref(r))
+            self._h = None
+            if r:
+                self._sc._L.tsg_result_free(r)
+
     def wait(self):
         r = c.c_void_p()
         rc = self._sc._L.tsg_scan_wait(self._h, c.byref(r))
@@ -325,15 +339,20 @@ class ScanResult:
         self._sc._L.tsg_result_stats(self._h, c.byref(s))
         return {k: getattr(s, k) for k, _ in s._fields_}
 
-    def raw(self):
+    def raw(self, lo=None, hi=None):
         p = c.c_void_p()
         n = c.c_uint64()
-        self._sc._L.tsg_result_json(self._h, c.byref(p), c.byref(n))
+        if lo is None:
+            self._sc._L.tsg_result_json(self._h, c.byref(p), c.byref(n))
+        elif self._sc._L.tsg_result_json_range(self._h, lo, hi, c.byref(p), c.byref(n)) != 0:
+            raise IndexError((lo, hi))
         return json.loads(c.string_at(p, n.value).decode("ascii"))
 
-    def secrets(self, paths) -> List[Secret]:
+    def secrets(self, paths, lo=None) -> List[Secret]:
+        """types.Secret per file (files [lo, lo + len(paths)) when lo is given)."""
         out = []
-        for path, fr in zip(paths, self.raw()):
+        raw = self.raw() if lo is None else self.raw(lo, lo + len(paths))
+        for path, fr in zip(paths, raw):
             kind = fr["kind"]
             if kind == 0:
                 out.append(Secret())
@@ -342,9 +361,11 @@ class ScanResult:
             else:
                 fs = []
                 for f in fr["findings"]:
-                    lines = [Line(Number=l["Number"], Content=_s(l["Content"]), IsCause=l["IsCause"],
-                                  Highlighted=_s(l["Highlighted"]), FirstCause=l["FirstCause"],
-                                  LastCause=l["LastCause"]) for l in f["Code"]["Lines"]]
+                    raw = f["Code"]["Lines"]
+                    lines = None if raw is None else [
+                        Line(Number=l["Number"], Content=_s(l["Content"]), IsCause=l["IsCause"],
+                             Highlighted=_s(l["Highlighted"]), FirstCause=l["FirstCause"],
+                             LastCause=l["LastCause"]) for l in raw]
                     fs.append(SecretFinding(RuleID=_s(f["RuleID"]), Category=_s(f["Category"]),
                                             Severity=_s(f["Severity"]), Title=_s(f["Title"]),
                                             StartLine=f["StartLine"], EndLine=f["EndLine"],
