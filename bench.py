@@ -137,6 +137,12 @@ def parity_block(C, last_result, want):
                          "golden tests)"}
 
 
+PEAK_HBM = 8000.0  # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
+# kernels of one scan's GPU phase: (name, tsg_stats field); they add up to ms_gpu_total (+ buffer clears)
+KERNELS = [("chunk_map_kernel", "ms_chunkmap_kernel"), ("filter_kernel (K1)", "ms_scan_kernel"),
+           ("confirm_kernel (K2 + in-place NFA verify)", "ms_confirm_kernel"), ("fold_kernel", "ms_careful_kernel"),
+           ("verify_hits_kernel + fullscan_kernel", "ms_nfa_kernel"), ("finalize_kernel", "ms_finalize_kernel")]
+
 WORKLOADS = {
     "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
            20.0, 32.0),
@@ -158,7 +164,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=3, help="scans in flight (pipelined submission)")
     ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     args = ap.parse_args()
     wl_desc, gb_default, cpu_mb_default = WORKLOADS[args.workload]
     if args.gb is None:
@@ -223,7 +229,7 @@ def main():
             while inflight:
                 r = inflight.pop(0).wait()
                 stats.append(r.stats())
-            last[0] = r
+            last_res[0] = r
     else:
         from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
         from trivy_amd.analyzer.secret import Collector
@@ -239,7 +245,7 @@ def main():
                 an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
                 stats.append(st)
 
-    last = [None]  # the last step's ScanResult (findings checked against the oracle below)
+    last_res = [None]  # the last step's ScanResult (findings checked against the oracle below)
     warm = []
     run_steps(args.warmup, warm)
 
@@ -262,27 +268,30 @@ def main():
 
     ms_step = dt / args.steps * 1e3
     last = stats[-1]
+    pre = "" if layer is None else "scan_"
+
+    def avg(k):  # per-scan mean over the timed steps (c4 sums its batches per step)
+        return sum(s[pre + k] for s in stats) / len(stats)
+    kernels = {name: avg(k) for name, k in KERNELS}
+    gpu_ms = avg("ms_gpu_total")
+    scan_ms = kernels["filter_kernel (K1)"]
+    breakdown = {k: round(avg(k), 3) for _, k in KERNELS}
+    breakdown.update({k: round(avg(k), 3) for k in ("ms_gpu_total", "ms_host_gpu_phase", "ms_host_exact")})
     if layer is None:
         n_bytes, n_files = C.n_bytes, C.n_files
-        scan_ms = sum(s["ms_scan_kernel"] for s in stats) / len(stats)
         arena_bytes = n_bytes
-        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "candidates", "special_files",
-                                            "findings")}
-        breakdown = {k: round(last[k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel", "ms_verify_kernel",
-                                                    "ms_fullscan_kernel", "ms_gpu_total", "ms_host_gpu_phase",
-                                                    "ms_host_allow_path", "ms_host_exact", "ms_host_total")}
+        counts = {k: int(last[k]) for k in ("flagged_blocks", "confirmed_hits", "anchor_hits", "candidates",
+                                            "special_files", "findings")}
+        breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth}
     else:
         n_bytes = int(last["input_bytes"])  # bytes of the files analyzed, as read from the layer
         n_files = int(last["added"])
         arena_bytes = int(last["scan_bytes"])
-        scan_ms = sum(s["scan_ms_scan_kernel"] for s in stats) / len(stats)
         counts = {k: int(last[k]) for k in ("entries", "regular", "required", "added", "skipped_binary",
                                             "whiteouts")}
-        counts.update({k: int(last["scan_" + k]) for k in ("candidates", "findings", "anchor_hits")})
-        breakdown = {k: round(last["scan_" + k], 3) for k in ("ms_scan_kernel", "ms_careful_kernel",
-                                                              "ms_verify_kernel", "ms_gpu_total",
-                                                              "ms_host_gpu_phase", "ms_host_exact")}
+        counts.update({k: int(last["scan_" + k]) for k in ("candidates", "findings", "confirmed_hits",
+                                                            "anchor_hits")})
         config_extra = {"walk_s_per_step": round(last["walk_s"], 3), "wait_s_per_step": round(last["wait_s"], 3),
                         "layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
@@ -290,15 +299,27 @@ def main():
                         "layer_gbps": round(world * int(layer.size) * args.steps / dt / 1e9, 3)}
     value = world * n_bytes * args.steps / dt / 1e9
     alg_bytes = arena_bytes + 16 * n_files  # 1 B/arena byte + 16 B/file
-    achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_file) and args.workload == "c2":
+    phase = alg_bytes / (gpu_ms * 1e-3) / 1e9  # §8(d): (arena + 16 n_files) / (t_prefilter + t_nfa)
+    k1 = alg_bytes / (scan_ms * 1e-3) / 1e9
+    dom = max(kernels, key=kernels.get)
+    traffic = traffic_k1 = None
+    if os.path.exists(args.traffic_file):
         try:
             tj = json.load(open(args.traffic_file))
-            if abs(tj.get("gb", -1) - args.gb) < 1e-6:
-                traffic = tj.get("bytes_per_launch")
+            if tj.get("workload") == args.workload and abs(tj.get("gb", -1) - args.gb) < 1e-6:
+                traffic = tj.get("phase_bytes_per_scan")
+                traffic_k1 = tj.get("k1_bytes_per_launch")
         except Exception:
             traffic = None
+    roofline = {"bound": "hbm",
+                "kernel": "GPU phase per scan: %s (SURVEY.md §8(d) formula)" % " + ".join(kernels),
+                "achieved": round(phase, 2), "peak": PEAK_HBM, "unit": "GB/s", "frac": round(phase / PEAK_HBM, 4),
+                "traffic": traffic, "algorithmic_bytes": alg_bytes,
+                "dominant_kernel": {"name": dom, "ms": round(kernels[dom], 3),
+                                    "share": round(kernels[dom] / gpu_ms, 3) if gpu_ms else None},
+                "k1": {"kernel": "filter_kernel (K1, streams every arena byte)", "achieved": round(k1, 2),
+                       "frac": round(k1 / PEAK_HBM, 4), "traffic": traffic_k1},
+                "traffic_source": os.path.relpath(args.traffic_file, ROOT) if traffic else None}
 
     if rank == 0:
         cpu = None
@@ -307,7 +328,7 @@ def main():
             cores = min(16, os.cpu_count() or 1)
             if layer is None:
                 cpu, want = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), cores, tmpdir, cfg_path)
-                parity = parity_block(C, last[0], want)
+                parity = parity_block(C, last_res[0], want)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
                 cpu = cpu_baseline_layer(sample, cores, tmpdir)
@@ -328,9 +349,7 @@ def main():
             "config": dict({"workload": wl_desc % args.gb, "workload_id": args.workload,
                             "parallelism": "files sharded, dp%d" % world,
                             "rules_compile_s": round(t_compile, 2)}, **config_extra),
-            "roofline": {"bound": "hbm", "kernel": "filter_kernel (K1)", "achieved": round(achieved, 2),
-                         "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 4),
-                         "traffic": traffic},
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
             "breakdown_ms": breakdown,

@@ -120,6 +120,9 @@ typedef struct tsg_stats {
   double ms_host_gpu_phase, ms_host_allow_path, ms_host_exact, ms_host_total;
   uint64_t flagged_blocks;   /* 16-B blocks the streaming filter sent to its exact confirm step */
   double ms_careful_kernel;  /* fold-rune files' careful pass (part of ms_gpu_total) */
+  /* per-kernel split of ms_gpu_total (HIP events on the engine stream) */
+  uint64_t confirmed_hits;   /* exact anchor-item matches; anchor_hits = those deferred to the verify kernel */
+  double ms_chunkmap_kernel, ms_confirm_kernel, ms_nfa_kernel, ms_finalize_kernel;
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 

@@ -15,6 +15,7 @@ constexpr uint32_t kChunk = 1024;  // bytes per chunk of the per-chunk '\n' coun
 constexpr uint32_t kCandGateOpen = 1;   // a keyword of the rule occurs in the file (ASCII, GPU bits)
 constexpr uint32_t kCandFoldFile = 2;   // the file holds U+0130 / U+212A (keywords may hide behind them)
 constexpr uint32_t kCandGateValid = 4;  // the two bits above were computed (GPU candidates)
+constexpr uint32_t kCandDrop = 8;       // MatchKeywords is false for the rule in this file (never reaches the host)
 
 struct Candidate {      // produced by the verify / full-scan kernels
   uint32_t file;
@@ -28,7 +29,9 @@ struct Candidate {      // produced by the verify / full-scan kernels
 struct BatchStats {
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
   uint64_t flagged_blocks = 0;
+  uint64_t confirmed_hits = 0;  // exact anchor-item matches (hits = those deferred to the verify kernel)
   float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
+  float ms_finalize = 0, ms_chunkmap = 0;
   bool hit_overflow = false, cand_overflow = false;
 };
 
@@ -53,15 +56,18 @@ class GpuEngine {
                std::vector<Candidate>* cands, BatchStats* st);
 
   // Device buffers of the last run (for tests / bench).
-  hipEvent_t ev_scan0() const { return ev_[0]; }
-  hipEvent_t ev_scan1() const { return ev_[1]; }
+  hipEvent_t ev_scan0() const { return ev_[1]; }
+  hipEvent_t ev_scan1() const { return ev_[2]; }
 
  private:
   bool Ensure(void** p, size_t* cap, size_t need);
+  void DumpItemDiag();
+  std::vector<uint8_t> h_items_kind_;
+  std::vector<uint32_t> h_items_id_;
   std::string err_;
   int device_ = 0;
   hipStream_t stream_ = nullptr;
-  hipEvent_t ev_[5] = {};
+  hipEvent_t ev_[7] = {};  // K0 | K1 | confirm | fold | verify+fullscan | finalize
   // tables
   uint32_t diag_mode_ = 0, diag_confirm_ = 0;
   AnchorInfo* d_anchors_ = nullptr;
@@ -100,6 +106,9 @@ class GpuEngine {
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
+  uint32_t nfa_steps_ = 256;          // TSG_NFA_STEPS: in-place verify budget of the confirm kernel
+  uint32_t* d_item_diag_ = nullptr;   // TSG_DIAG_ITEMS=<file>: per-item counters dumped after each run
+  std::string item_diag_path_;
 };
 
 }  // namespace tsg

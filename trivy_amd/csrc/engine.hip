@@ -284,24 +284,6 @@ struct NfaParams {
   uint32_t n_fullscan_rules;
 };
 
-__device__ void emit_candidate(const NfaParams& P, uint32_t f, uint32_t r, int64_t wlo, int64_t whi,
-                               int64_t nlb, uint32_t flags) {
-  uint32_t k = atomicAdd(&P.counters[1], 1u);
-  if (k < P.cand_cap) {
-    Candidate c;
-    c.file = f;
-    c.rule = r;
-    c.wlo = wlo;
-    c.whi = whi;
-    c.nl_before = nlb;
-    c.flags = flags;
-    c.pad = 0;
-    P.cands[k] = c;
-  } else {
-    P.counters[4] = 1;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // K2: confirm flagged blocks exactly + verify the anchor hits
 // ---------------------------------------------------------------------------
@@ -412,13 +394,25 @@ struct ConfirmParams {
   const uint64_t* core;           // filter.h core tables (n_groups x 256)
   const uint32_t* group_items;    // n_groups x 8
   const uint32_t* bucket_groups;  // n_buckets + 1
+  Candidate* cands;               // anchor hits verified in place (NFA accepted)
+  uint32_t cand_cap;
+  uint32_t nfa_steps;             // in-place NFA budget per hit (bytes); longer runs go to K4
+  uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item {exact matches, hits passed on}
 };
 
+// Prefix bytes scanned for fold-rune lead bytes before verifying an anchor
+// hit in place (an anchor whose fold-widened prefix is longer goes to K4).
+constexpr int32_t kFoldPrefixScan = 96;
+
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
-// (aligned) instead of one dependent load per byte.  As nfa_run otherwise.
+// (aligned) instead of one dependent load per byte.  Injects the start state
+// at every position up to inj_hi.  Returns kNfaAccept when some position
+// accepts, kNfaReject when every thread died (or the file ended), and
+// kNfaUndecided after max_steps bytes with threads still alive.
+constexpr int kNfaReject = 0, kNfaAccept = 1, kNfaUndecided = 2;
 template <int W>
-__device__ bool nfa_run_abs(const uint8_t* __restrict arena, uint64_t fs, int64_t len, int64_t start, int64_t inj_hi,
-                            const uint64_t* __restrict tab) {
+__device__ int nfa_run_abs(const uint8_t* __restrict arena, uint64_t fs, int64_t len, int64_t start, int64_t inj_hi,
+                           const uint64_t* __restrict tab, int64_t max_steps) {
   uint64_t O[W], Lp[W], F[W], D[W];
 #pragma unroll
   for (int w = 0; w < W; w++) {
@@ -430,7 +424,8 @@ __device__ bool nfa_run_abs(const uint8_t* __restrict arena, uint64_t fs, int64_
   const uint64_t* B = tab + 3 * W;
   uint4 buf = make_uint4(0, 0, 0, 0);
   uint64_t buf_at = ~uint64_t(0);
-  for (int64_t pos = start; pos < len; pos++) {
+  const int64_t stop = len - start > max_steps ? start + max_steps : len;
+  for (int64_t pos = start; pos < stop; pos++) {
     const uint64_t abs = fs + uint64_t(pos);
     if ((abs & ~uint64_t(15)) != buf_at) {
       buf_at = abs & ~uint64_t(15);
@@ -465,19 +460,39 @@ __device__ bool nfa_run_abs(const uint8_t* __restrict arena, uint64_t fs, int64_
       acc |= nd & F[w];
       alive |= nd;
     }
-    if (acc) return true;
-    if (!alive && pos >= inj_hi) return false;
+    if (acc) return kNfaAccept;
+    if (!alive && pos >= inj_hi) return kNfaReject;
   }
-  return false;
+  return stop < len ? kNfaUndecided : kNfaReject;
 }
 
-__device__ bool nfa_dispatch_abs(int words, const uint8_t* arena, uint64_t fs, int64_t len, int64_t start,
-                                 int64_t inj_hi, const uint64_t* tab) {
+__device__ int nfa_dispatch_abs(int words, const uint8_t* arena, uint64_t fs, int64_t len, int64_t start,
+                                int64_t inj_hi, const uint64_t* tab, int64_t max_steps = INT64_MAX) {
   switch (words) {
-    case 1: return nfa_run_abs<1>(arena, fs, len, start, inj_hi, tab);
-    case 2: return nfa_run_abs<2>(arena, fs, len, start, inj_hi, tab);
-    case 3: return nfa_run_abs<3>(arena, fs, len, start, inj_hi, tab);
-    default: return nfa_run_abs<4>(arena, fs, len, start, inj_hi, tab);
+    case 1: return nfa_run_abs<1>(arena, fs, len, start, inj_hi, tab, max_steps);
+    case 2: return nfa_run_abs<2>(arena, fs, len, start, inj_hi, tab, max_steps);
+    case 3: return nfa_run_abs<3>(arena, fs, len, start, inj_hi, tab, max_steps);
+    default: return nfa_run_abs<4>(arena, fs, len, start, inj_hi, tab, max_steps);
+  }
+}
+
+// Candidate record (the host's exact pass input); nl_before < 0 and flags are
+// filled by the finalize kernel once the keyword bits are final.
+__device__ __forceinline__ void put_candidate(Candidate* cands, uint32_t cap, uint32_t* counters, uint32_t f,
+                                              uint32_t r, int64_t wlo, int64_t whi) {
+  const uint32_t k = atomicAdd(&counters[1], 1u);
+  if (k < cap) {
+    Candidate c;
+    c.file = f;
+    c.rule = r;
+    c.wlo = wlo;
+    c.whi = whi;
+    c.nl_before = -1;
+    c.flags = 0;
+    c.pad = 0;
+    cands[k] = c;
+  } else {
+    counters[4] = 1;
   }
 }
 
@@ -547,7 +562,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   }
   const uint8_t* tabs = kLdsTabs ? s_tabs : static_cast<const uint8_t*>(P.tabs);
   const uint32_t lane = tid & 63, wave = tid >> 6;
-  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2
+  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2 [3] confirmed anchor hits
   if (lane < 4) cnt[lane] = 0;
   __syncthreads();
   const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
@@ -607,9 +622,40 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
       else P.counters[10] = 1;
       return;
     }
+    if (P.item_diag) atomicAdd(&P.item_diag[2 * ix], 1u);
+    // Verify each anchor hit here, with the block's bytes still in cache: the
+    // rule's relaxed NFA from the start window the anchor's offsets give
+    // (exactly K4's check).  Deferred to K4 (the hit list) are hits whose
+    // fold-widened prefix may hold a fold rune (the window then depends on
+    // the file's fold flags, known only after this kernel) and runs longer
+    // than the in-place budget.
     const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
-    for (uint32_t d = 0; d < it.n_ids; d++)
-      stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
+    const int64_t flen = int64_t(fe - fs);
+    for (uint32_t d = 0; d < it.n_ids; d++) {
+      const uint32_t aid = item_ids[it.ids_off + d];
+      atomicAdd(&cnt[3], 1u);
+      const AnchorInfo a = P.anchors[aid];
+      const int64_t lit_hi = int64_t(lit_end) - int64_t(a.lit_len);  // literal start, file-relative
+      const int64_t whi = lit_hi - a.off_lo;
+      if (whi < 0) continue;  // no match can start before the file (as K4)
+      bool defer = a.off_hi_fold > kFoldPrefixScan;
+      for (int64_t q = lit_hi - a.off_hi_fold < 0 ? 0 : lit_hi - a.off_hi_fold; q < lit_hi && !defer; q++) {
+        const uint32_t b = win_byte(l, fs + uint64_t(q));
+        defer = b == 0xC4u || b == 0xC5u || b == 0xE2u;  // lead byte of U+0130 / U+017F / U+212A
+      }
+      int res = kNfaUndecided;
+      const int64_t wlo = lit_hi - a.off_hi < 0 ? 0 : lit_hi - a.off_hi;
+      if (!defer) {
+        const RuleGpu rg = P.rules[a.rule];
+        res = rg.nfa_words == 0 ? kNfaAccept
+                                : nfa_dispatch_abs(rg.nfa_words, P.arena, fs, flen, wlo, whi, P.nfa + rg.nfa_off,
+                                                   int64_t(P.nfa_steps));
+      }
+      if (res == kNfaReject) continue;
+      if (P.item_diag) atomicAdd(&P.item_diag[2 * ix + 1], 1u);
+      if (res == kNfaAccept) put_candidate(P.cands, P.cand_cap, P.counters, f, a.rule, wlo, whi);
+      else stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, aid);
+    }
   };
   auto run_q2 = [&]() {  // wave-uniform: phase C over the queued candidates
     wave_sync();
@@ -710,6 +756,8 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     wave_sync();
   }
   flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
+  wave_sync();
+  if (lane == 0 && cnt[3]) atomicAdd(&P.counters[11], cnt[3]);  // confirmed anchor hits (stats)
 }
 
 // Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
@@ -864,10 +912,9 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
     if (wlo < 0) wlo = 0;
     const uint64_t fs = P.off[f];
     const int64_t len = int64_t(P.off[f + 1] - fs);
-    const bool acc =
-        rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off);
-    if (acc)
-      emit_candidate(P, f, a.rule, wlo, whi, count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(wlo)), gate_flags(P, rg, f));
+    const bool acc = rg.nfa_words == 0 ||
+                     nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off) == kNfaAccept;
+    if (acc) put_candidate(P.cands, P.cand_cap, P.counters, f, a.rule, wlo, whi);
   }
 }
 
@@ -882,8 +929,28 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
     const RuleGpu rg = P.rules[r];
     const uint64_t fs = P.off[f];
     const int64_t len = int64_t(P.off[f + 1] - fs);
-    const bool acc = rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, 0, len, P.nfa + rg.nfa_off);
-    if (acc) emit_candidate(P, f, r, 0, len, 0, 0u);  // gate checked exactly on the host
+    const bool acc =
+        rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, 0, len, P.nfa + rg.nfa_off) == kNfaAccept;
+    if (acc) put_candidate(P.cands, P.cand_cap, P.counters, f, r, 0, len);
+  }
+}
+
+// Finalize: per candidate, the '\n' count before its window (per-chunk counts
+// from K1 + the partial chunks) and the keyword-gate flags for the host's
+// lazy MatchKeywords, now that every confirm / fold block has set its bits.
+// A closed ASCII gate in a file without U+0130 / U+212A is MatchKeywords ==
+// false (scanner.go:409): such candidates are marked for dropping.
+__global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
+  const uint32_t n = P.counters[1] < P.cand_cap ? P.counters[1] : P.cand_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    Candidate& c = P.cands[i];
+    const uint64_t fs = P.off[c.file];
+    if (c.nl_before < 0) c.nl_before = count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(c.wlo));
+    const RuleGpu rg = P.rules[c.rule];
+    uint32_t fl = gate_flags(P, rg, c.file);
+    if (rg.gate == kGateKeywords && !rg.kw_match_implied && !(P.flags[c.file] & 4u) && !(fl & kCandGateOpen))
+      fl |= kCandDrop;
+    c.flags = fl;
   }
 }
 
@@ -915,6 +982,8 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   for (auto& e : ev_) hipEventCreate(&e);
   if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
   if (const char* dc = std::getenv("TSG_DIAG_CONFIRM")) diag_confirm_ = uint32_t(std::atoi(dc));
+  if (const char* ns = std::getenv("TSG_NFA_STEPS")) nfa_steps_ = uint32_t(std::atoi(ns));
+  if (const char* di = std::getenv("TSG_DIAG_ITEMS")) item_diag_path_ = di;
   kw_words_ = std::max<uint32_t>(1, cr.kw_words());
   n_rules_ = uint32_t(cr.rules.size());
   for (uint32_t r = 0; r < n_rules_; r++)
@@ -960,6 +1029,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (tb.empty()) tb.assign(16, 0);
     ftabs_bytes_ = uint32_t(tb.size());
     n_fitems_ = uint32_t(ft->items.size());
+    for (auto& it : ft->items) {
+      h_items_kind_.push_back(it.kind);
+      h_items_id_.push_back(ft->item_ids[it.ids_off]);
+    }
     uint8_t* d = nullptr;
     if (!Upload(&err_, &d, tb.data(), tb.size())) return;
     d_ftabs_ = d;
@@ -1022,6 +1095,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     size_t lds_max = 64 * 1024;  // measured: 1 WG/CU with 160-KiB tables loses to 4 WGs/CU reading L2
     if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
     lds_tabs_ = fixed + ftabs_bytes_ <= lds_max && ftabs_bytes_ + 2 * kFoldSpan + 16 <= lds_max;
+    if (!item_diag_path_.empty() && hipMalloc(&d_item_diag_, 8 * std::max<size_t>(n_fitems_, 1)) != hipSuccess) {
+      err_ = "hipMalloc item diag";
+      return;
+    }
     c_lds_bytes_ = fixed + (lds_tabs_ ? ftabs_bytes_ : 0);
     hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
@@ -1033,7 +1110,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
@@ -1094,10 +1171,12 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
         !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
         !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
       return false;
+    HIP_OK(hipEventRecord(ev_[0], stream_));  // the GPU phase: clears, K0 .. finalize
     HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
     HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
     HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
     HIP_OK(hipMemsetAsync(d_chunk_file_, 0, n_chunks * 4, stream_));
+    if (d_item_diag_) HIP_OK(hipMemsetAsync(d_item_diag_, 0, 8 * std::max<size_t>(n_fitems_, 1), stream_));
     {
       uint32_t blocks = std::min<uint32_t>((n_files + 255) / 256, 4096);
       chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, static_cast<uint32_t*>(d_chunk_file_));
@@ -1115,10 +1194,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
     const uint32_t f_grid =
         uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves, 256)));
-    HIP_OK(hipEventRecord(ev_[0], stream_));
+    HIP_OK(hipEventRecord(ev_[1], stream_));
     filter_kernel<<<f_grid, kScanThreads, 0, stream_>>>(fp);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[1], stream_));
+    HIP_OK(hipEventRecord(ev_[2], stream_));
     // K2: confirm + verify
     ConfirmParams cp;
     cp.arena = d_arena;
@@ -1152,6 +1231,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.core = d_core_;
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;
+    cp.cands = static_cast<Candidate*>(d_cands_);
+    cp.cand_cap = cand_cap_;
+    cp.nfa_steps = nfa_steps_;
+    cp.item_diag = d_item_diag_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
         confirm_kernel<true><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
@@ -1159,7 +1242,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
         confirm_kernel<false><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
     }
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[2], stream_));
+    HIP_OK(hipEventRecord(ev_[3], stream_));
     // fold runes: fold-tolerant item matching around each one
     FoldParams fo;
     fo.arena = d_arena;
@@ -1187,7 +1270,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
         fold_kernel<false><<<512, 256, 0, stream_>>>(fo);
     }
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[3], stream_));
+    HIP_OK(hipEventRecord(ev_[4], stream_));
     NfaParams np;
     np.arena = d_arena;
     np.off = d_offsets;
@@ -1213,7 +1296,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
       HIP_OK(hipGetLastError());
     }
-    HIP_OK(hipEventRecord(ev_[4], stream_));
+    HIP_OK(hipEventRecord(ev_[5], stream_));
+    if (diag_mode_ == 0) finalize_kernel<<<256, 256, 0, stream_>>>(np);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev_[6], stream_));
     uint32_t cnt[16];
     HIP_OK(hipMemcpyAsync(cnt, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
@@ -1221,6 +1307,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       std::fprintf(stderr, "counters: hits %u cands %u special %u recs %u folds %u\n", cnt[0], cnt[1], cnt[2], cnt[7],
                    cnt[9]);
     st->hits = cnt[0];
+    st->confirmed_hits = cnt[11];
     st->special_files = cnt[2];
     st->flagged_blocks = cnt[7];
     if (cnt[8]) {  // record list overflow: grow and rescan
@@ -1241,22 +1328,41 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       cand_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[1]) + cnt[1] / 4 + 1024, 0xFFFFFFF0u));
       continue;
     }
-    st->candidates = cnt[1];
     cands->resize(cnt[1]);
     if (cnt[1]) {
       HIP_OK(hipMemcpyAsync(cands->data(), d_cands_, size_t(cnt[1]) * sizeof(Candidate), hipMemcpyDeviceToHost,
                             stream_));
       HIP_OK(hipStreamSynchronize(stream_));
     }
-    hipEventElapsedTime(&st->ms_scan, ev_[0], ev_[1]);
-    hipEventElapsedTime(&st->ms_confirm, ev_[1], ev_[2]);
-    hipEventElapsedTime(&st->ms_careful, ev_[2], ev_[3]);  // fold kernel
-    hipEventElapsedTime(&st->ms_verify, ev_[3], ev_[4]);   // verify + full-scan
-    hipEventElapsedTime(&st->ms_total, ev_[0], ev_[4]);
+    // closed keyword gates (finalize_kernel) never reach the host
+    cands->erase(std::remove_if(cands->begin(), cands->end(), [](const Candidate& c) { return c.flags & kCandDrop; }),
+                 cands->end());
+    st->candidates = cands->size();
+    if (d_item_diag_) DumpItemDiag();
+    hipEventElapsedTime(&st->ms_scan, ev_[1], ev_[2]);
+    hipEventElapsedTime(&st->ms_confirm, ev_[2], ev_[3]);
+    hipEventElapsedTime(&st->ms_careful, ev_[3], ev_[4]);  // fold kernel
+    hipEventElapsedTime(&st->ms_verify, ev_[4], ev_[5]);   // verify (deferred hits) + full-scan
+    hipEventElapsedTime(&st->ms_finalize, ev_[5], ev_[6]);
+    hipEventElapsedTime(&st->ms_chunkmap, ev_[0], ev_[1]);
+    hipEventElapsedTime(&st->ms_total, ev_[0], ev_[6]);
     return true;
   }
   err_ = "candidate buffers kept overflowing";
   return false;
+}
+
+// TSG_DIAG_ITEMS: appends "item kind first_id exact_matches passed_on" lines
+// (passed_on: anchor hits the in-place NFA did not reject).
+void GpuEngine::DumpItemDiag() {
+  std::vector<uint32_t> v(2 * std::max<size_t>(n_fitems_, 1));
+  if (hipMemcpy(v.data(), d_item_diag_, v.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
+  FILE* fp = std::fopen(item_diag_path_.c_str(), "a");
+  if (!fp) return;
+  for (uint32_t i = 0; i < n_fitems_; i++)
+    std::fprintf(fp, "%u %u %u %u %u\n", i, uint32_t(h_items_kind_[i]), h_items_id_[i], v[2 * i], v[2 * i + 1]);
+  std::fprintf(fp, "--\n");
+  std::fclose(fp);
 }
 
 }  // namespace tsg

@@ -446,11 +446,15 @@ void FitPositions(std::vector<Elem>* seq_p, int64_t budget) {
 }
 
 void BuildNfa(std::vector<Elem> seq, std::vector<uint64_t>* nfa, RuleGpu* rg) {
+  // A relaxed language holding the empty string: the kernels only accept after
+  // a byte, so such a rule makes every (anchor hit / file) a candidate instead
+  // (Go reports empty matches too; the exact pass finds them).
+  const bool nullable = SeqMin(seq) == 0;
   FitPositions(&seq, 64 * kMaxNfaWords);  // fit into kMaxNfaWords * 64 positions
   int64_t P = 0;
   for (auto& e : seq) P += Positions(e);
   rg->nfa_off = uint32_t(nfa->size());
-  if (P == 0) {
+  if (P == 0 || nullable) {
     rg->nfa_words = 0;
     return;
   }
