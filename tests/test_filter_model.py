@@ -66,8 +66,12 @@ def _check(rules, contents):
     arena, offs = _pack(contents)
     hits, folds = model.run(arena, offs)
     special = {f for f, _ in folds}
+    reqs = model.anchor_reqs()
     windows = {}
     for f, end, aid in hits:
+        # the confirm kernel drops hits failing the anchor's follow requirements
+        if not model.follow_possible(reqs[aid], contents[f], end):
+            continue
         r, lit_len, lo, hi = anchors[aid]
         lit = end - lit_len
         windows.setdefault((f, r), []).append((max(0, lit - hi), lit - lo))

@@ -515,6 +515,10 @@ const char* tsg_debug_rule_anchor(const tsg_compiled* c, uint32_t i) {
   return i < d.size() ? d[i].c_str() : nullptr;
 }
 
+const void* tsg_debug_anchor_req(const tsg_compiled* c, uint32_t j) {
+  return j < c->cr.anchor_req.size() ? &c->cr.anchor_req[j] : nullptr;
+}
+
 const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k) {
   return k < c->cr.keywords.size() ? c->cr.keywords[k].c_str() : nullptr;
 }

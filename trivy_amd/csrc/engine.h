@@ -71,6 +71,7 @@ class GpuEngine {
   // tables
   uint32_t diag_mode_ = 0, diag_confirm_ = 0;
   AnchorInfo* d_anchors_ = nullptr;
+  AnchorReq* d_anchor_req_ = nullptr;
   RuleGpu* d_rules_ = nullptr;
   uint32_t* d_rule_kw_ = nullptr;
   uint64_t* d_nfa_ = nullptr;

@@ -394,11 +394,53 @@ struct ConfirmParams {
   const uint64_t* core;           // filter.h core tables (n_groups x 256)
   const uint32_t* group_items;    // n_groups x 8
   const uint32_t* bucket_groups;  // n_buckets + 1
+  const AnchorReq* reqs;          // per anchor: follow requirements (rules.h)
   Candidate* cands;               // anchor hits verified in place (NFA accepted)
   uint32_t cand_cap;
   uint32_t nfa_steps;             // in-place NFA budget per hit (bytes); longer runs go to K4
   uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item {exact matches, hits passed on}
 };
+
+// The follow requirements of an anchor hit (rules.h AnchorReq) over the
+// bytes after its literal end e: false only when every byte up to the last
+// possible run end is ASCII and some requirement's run occurs at none of its
+// offsets, i.e. no match can continue from this literal occurrence.  One
+// shift-and pass per requirement (run position k in bit k).
+template <typename ByteAt>
+__device__ __forceinline__ bool follow_possible(const AnchorReq* __restrict rq, int64_t e, int64_t flen,
+                                                const ByteAt& byte_at) {
+#pragma unroll
+  for (int r = 0; r < kMaxReqs; r++) {
+    const uint32_t n = rq->n[r];
+    if (n == 0) break;
+    const int64_t lo = rq->lo[r], hi = rq->hi[r];
+    uint64_t m0[kMaxReqLen], m1[kMaxReqLen];
+#pragma unroll
+    for (int k = 0; k < kMaxReqLen; k++) {
+      m0[k] = rq->m[r][k][0];
+      m1[k] = rq->m[r][k][1];
+    }
+    const int64_t end = e + hi + int64_t(n) < flen ? e + hi + int64_t(n) : flen;
+    uint32_t D = 0;
+    bool found = false;
+    for (int64_t p = e; p < end; p++) {
+      const uint32_t b = byte_at(p);
+      if (b >= 0x80u) return true;  // a multi-byte rune or an invalid byte: offsets no longer fixed
+      const uint64_t bit = uint64_t(1) << (b & 63u);
+      uint32_t mk = 0;
+#pragma unroll
+      for (int k = 0; k < kMaxReqLen; k++) mk |= uint32_t((((b & 64u) ? m1[k] : m0[k]) & bit) != 0) << k;
+      const int64_t o = p - e;
+      D = ((D << 1) | uint32_t(o >= lo && o <= hi)) & mk;
+      if ((D >> (n - 1)) & 1u) {
+        found = true;
+        break;
+      }
+    }
+    if (!found) return false;
+  }
+  return true;
+}
 
 // Prefix bytes scanned for fold-rune lead bytes before verifying an anchor
 // hit in place (an anchor whose fold-widened prefix is longer goes to K4).
@@ -634,6 +676,8 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     for (uint32_t d = 0; d < it.n_ids; d++) {
       const uint32_t aid = item_ids[it.ids_off + d];
       atomicAdd(&cnt[3], 1u);
+      if (!follow_possible(P.reqs + aid, lit_end, flen, [&](int64_t q) { return win_byte(l, fs + uint64_t(q)); }))
+        continue;
       const AnchorInfo a = P.anchors[aid];
       const int64_t lit_hi = int64_t(lit_end) - int64_t(a.lit_len);  // literal start, file-relative
       const int64_t whi = lit_hi - a.off_lo;
@@ -940,17 +984,40 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
 // lazy MatchKeywords, now that every confirm / fold block has set its bits.
 // A closed ASCII gate in a file without U+0130 / U+212A is MatchKeywords ==
 // false (scanner.go:409): such candidates are marked for dropping.
+// One wave per candidate: the lanes sum the whole 1-KiB chunks' counts (a
+// window deep in a 10-MiB file spans ~10^4 chunks), lanes 0 / 1 the partial
+// chunks at either end.
 __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
   const uint32_t n = P.counters[1] < P.cand_cap ? P.counters[1] : P.cand_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n_waves = gridDim.x * (blockDim.x / 64);
+  for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += n_waves) {
     Candidate& c = P.cands[i];
-    const uint64_t fs = P.off[c.file];
-    if (c.nl_before < 0) c.nl_before = count_nl_abs(P.arena, P.nl, fs, fs + uint64_t(c.wlo));
-    const RuleGpu rg = P.rules[c.rule];
-    uint32_t fl = gate_flags(P, rg, c.file);
-    if (rg.gate == kGateKeywords && !rg.kw_match_implied && !(P.flags[c.file] & 4u) && !(fl & kCandGateOpen))
-      fl |= kCandDrop;
-    c.flags = fl;
+    const uint32_t file = c.file;
+    const uint64_t fs = P.off[file];
+    const int64_t nlb = c.nl_before;
+    if (nlb < 0) {
+      const uint64_t a = fs, b = fs + uint64_t(c.wlo);
+      const uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
+      int64_t part = 0;
+      if (ca >= cb) {
+        if (lane == 0) part = count_nl_range(P.arena, a, b);
+      } else {
+        if (lane == 0) part = count_nl_range(P.arena, a, ca * kChunk);
+        if (lane == 1) part = count_nl_range(P.arena, cb * kChunk, b);
+        for (uint64_t cc = ca + lane; cc < cb; cc += 64) part += P.nl[cc];
+      }
+#pragma unroll
+      for (int x = 1; x < 64; x <<= 1) part += __shfl_xor(part, x);
+      if (lane == 0) c.nl_before = part;
+    }
+    if (lane == 0) {
+      const RuleGpu rg = P.rules[c.rule];
+      uint32_t fl = gate_flags(P, rg, file);
+      if (rg.gate == kGateKeywords && !rg.kw_match_implied && !(P.flags[file] & 4u) && !(fl & kCandGateOpen))
+        fl |= kCandDrop;
+      c.flags = fl;
+    }
   }
 }
 
@@ -990,6 +1057,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (cr.rules[r].has_regex && !cr.rules[r].anchored) fullscan_rules_.push_back(r);
   n_fullscan_rules_ = uint32_t(fullscan_rules_.size());
   if (!Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
+      !Upload(&err_, &d_anchor_req_, cr.anchor_req.data(), cr.anchor_req.size()) ||
       !Upload(&err_, &d_rules_, cr.rules.data(), cr.rules.size()) ||
       !Upload(&err_, &d_rule_kw_, cr.rule_kw.data(), cr.rule_kw.size()) ||
       !Upload(&err_, &d_nfa_, cr.nfa.data(), cr.nfa.size()) ||
@@ -1110,7 +1178,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_anchor_req_, d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_arena_stage_, d_off_stage_};
   for (void* p : ps)
@@ -1231,6 +1299,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.core = d_core_;
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;
+    cp.reqs = d_anchor_req_;
     cp.cands = static_cast<Candidate*>(d_cands_);
     cp.cand_cap = cand_cap_;
     cp.nfa_steps = nfa_steps_;
@@ -1297,7 +1366,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(ev_[5], stream_));
-    if (diag_mode_ == 0) finalize_kernel<<<256, 256, 0, stream_>>>(np);
+    if (diag_mode_ == 0) finalize_kernel<<<1024, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[6], stream_));
     uint32_t cnt[16];

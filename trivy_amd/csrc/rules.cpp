@@ -658,6 +658,72 @@ std::vector<ByteSet> BeforeSets(const std::vector<Node>& nodes, const std::vecto
   return out;
 }
 
+// Follow requirements (rules.h AnchorReq) from the relaxed element sequence of
+// the items after an anchor literal.  A candidate run starts at a mandatory
+// element j (min >= 1) whose preceding elements have a bounded total length;
+// it holds j's mandatory positions and continues into the next elements while
+// they are fixed-length.  The (at most two, disjoint) runs with the fewest
+// expected chance occurrences over their offset range (static byte prior)
+// are kept.
+AnchorReq FollowReqs(const std::vector<Node>& nodes, const std::vector<int>& fol) {
+  AnchorReq rq{};
+  std::vector<Elem> seq;
+  for (int it : fol) {
+    auto r = Relax(nodes, it);
+    seq.insert(seq.end(), r.begin(), r.end());
+  }
+  const auto& prior = BytePrior();
+  struct Run {
+    int64_t lo, hi;
+    size_t j0, j1;  // elements covered [j0, j1)
+    std::vector<Reach> sets;
+    double score;
+  };
+  std::vector<Run> runs;
+  int64_t lo = 0, hi = 0;
+  for (size_t j = 0; j < seq.size() && hi < kInf; j++) {
+    if (seq[j].min >= 1 && hi <= 48) {
+      Run r{lo, hi, j, j, {}, 0};
+      for (size_t k = j; k < seq.size() && r.sets.size() < size_t(kMaxReqLen); k++) {
+        const Elem& e = seq[k];
+        if (e.min < 1) break;
+        for (int64_t c = 0; c < e.min && r.sets.size() < size_t(kMaxReqLen); c++) r.sets.push_back(e.reach);
+        r.j1 = k + 1;
+        if (e.max != e.min) break;  // the next element's offset is no longer fixed
+      }
+      double p = 1.0;
+      for (auto& s : r.sets) {
+        double q = 0;
+        for (int b = 0; b < 0x80; b++)
+          if (s.test(size_t(b))) q += prior[size_t(b)];
+        p *= q;
+      }
+      r.score = double(hi - lo + 1) * p;
+      if (r.score < 1.0) runs.push_back(r);
+    }
+    lo += seq[j].min;
+    hi = (seq[j].max < 0 || hi >= kInf) ? kInf : hi + seq[j].max;
+  }
+  std::sort(runs.begin(), runs.end(), [](const Run& a, const Run& b) { return a.score < b.score; });
+  int nr = 0;
+  std::vector<std::pair<size_t, size_t>> used;
+  for (auto& r : runs) {
+    bool overlap = false;
+    for (auto& u : used)
+      if (r.j0 < u.second && u.first < r.j1) overlap = true;
+    if (overlap) continue;
+    used.push_back({r.j0, r.j1});
+    rq.lo[nr] = uint16_t(r.lo);
+    rq.hi[nr] = uint16_t(r.hi);
+    rq.n[nr] = uint8_t(r.sets.size());
+    for (size_t k = 0; k < r.sets.size(); k++)
+      for (int b = 0; b < 0x80; b++)
+        if (r.sets[k].test(size_t(b))) rq.m[nr][k][b >> 6] |= uint64_t(1) << (b & 63);
+    if (++nr == kMaxReqs) break;
+  }
+  return rq;
+}
+
 }  // namespace
 
 // Every match contains one of `kws` (lowercased ASCII), case-folded: found in
@@ -879,6 +945,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
           ai.off_hi = int32_t(best.ohi);
           ai.off_hi_fold = int32_t(std::min<int64_t>(best.ohi_fold, 1 << 30));
           out->anchors.push_back(ai);
+          out->anchor_req.push_back(FollowReqs(re->nodes(), best.follow[li]));
           {  // prefilter item: prefix sets + literal sets (union over same-folded variants) + lookahead sets
             FilterItem fi;
             fi.kind = kItemAnchor;

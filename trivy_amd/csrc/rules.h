@@ -51,6 +51,21 @@ struct AnchorInfo {  // mirrored on the device
   int32_t off_hi_fold;     // the same when U+212A/U+017F/U+0130 may occur (special files)
 };
 
+// Follow requirements of an anchor (mirrored on the device): in ASCII text,
+// every match continues after the anchor literal with req r's run of n[r]
+// consecutive byte sets starting at a byte offset in [lo[r], hi[r]] from the
+// literal end (one relaxed-NFA position per ASCII byte).  A hit whose bytes
+// up to the last possible run end are ASCII and hold no such run cannot be a
+// match; any byte >= 0x80 in that range leaves the hit to the NFA.
+constexpr int kMaxReqs = 2, kMaxReqLen = 4;
+struct AnchorReq {
+  uint16_t lo[kMaxReqs], hi[kMaxReqs];
+  uint8_t n[kMaxReqs];                   // 0: no requirement
+  uint8_t pad[6];
+  uint64_t m[kMaxReqs][kMaxReqLen][2];   // ASCII members of each set (bit b of word b / 64)
+};
+static_assert(sizeof(AnchorReq) == 144, "AnchorReq layout (tests/filter_model.py reads it)");
+
 struct RuleGpu {  // mirrored on the device
   uint32_t nfa_off;     // index into nfa words (u64)
   uint8_t nfa_words;    // 0: relaxed NFA is empty -> every anchor hit is a candidate
@@ -80,6 +95,7 @@ struct CompiledRules {
   // keywords / anchors
   std::vector<std::string> keywords;  // unique lowercased ASCII keywords
   std::vector<AnchorInfo> anchors;
+  std::vector<AnchorReq> anchor_req;  // per anchor
   // rules
   std::vector<RuleGpu> rules;
   std::vector<uint32_t> rule_kw;  // keyword ids
