@@ -388,7 +388,8 @@ struct ConfirmParams {
   uint32_t hit_cap;
   FoldSite* folds;     // fold runes found (for the fold kernel)
   uint32_t fold_cap;
-  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission
+  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission,
+                       // 32 no follow requirements, 64 no in-place NFA (hits go to K4)
   uint32_t* kwbits;               // per file: kw_words x u32 keyword bits
   uint32_t kw_words;
   const uint64_t* core;           // filter.h core tables (n_groups x 256)
@@ -676,13 +677,14 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     for (uint32_t d = 0; d < it.n_ids; d++) {
       const uint32_t aid = item_ids[it.ids_off + d];
       atomicAdd(&cnt[3], 1u);
-      if (!follow_possible(P.reqs + aid, lit_end, flen, [&](int64_t q) { return win_byte(l, fs + uint64_t(q)); }))
+      if (!(P.diag & 32) &&
+          !follow_possible(P.reqs + aid, lit_end, flen, [&](int64_t q) { return win_byte(l, fs + uint64_t(q)); }))
         continue;
       const AnchorInfo a = P.anchors[aid];
       const int64_t lit_hi = int64_t(lit_end) - int64_t(a.lit_len);  // literal start, file-relative
       const int64_t whi = lit_hi - a.off_lo;
       if (whi < 0) continue;  // no match can start before the file (as K4)
-      bool defer = a.off_hi_fold > kFoldPrefixScan;
+      bool defer = a.off_hi_fold > kFoldPrefixScan || (P.diag & 64);
       for (int64_t q = lit_hi - a.off_hi_fold < 0 ? 0 : lit_hi - a.off_hi_fold; q < lit_hi && !defer; q++) {
         const uint32_t b = win_byte(l, fs + uint64_t(q));
         defer = b == 0xC4u || b == 0xC5u || b == 0xE2u;  // lead byte of U+0130 / U+017F / U+212A

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <cstdlib>
 #include <map>
 
 namespace tsg {
@@ -185,7 +186,18 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
       for (int k = 0; k < 4; k++) u[s].w[k] = a.u[s].w[k] | b.u[s].w[k];
     return Cost(u);
   };
+  std::vector<bool> solo(n, false);
+  if (const char* e = std::getenv("TSG_FILTER_SOLO")) {  // experiment: items kept in buckets of their own
+    for (const char* q = e; *q;) {
+      char* end = nullptr;
+      const unsigned long v = std::strtoul(q, &end, 10);
+      if (end == q) break;
+      if (v < n) solo[v] = true;
+      q = *end ? end + 1 : end;
+    }
+  }
   auto delta_of = [&](size_t i, size_t j) {
+    if (solo[i] || solo[j]) return std::numeric_limits<double>::infinity();
     B256 u[kFilterSlots];
     return merged(cl[i], cl[j], u) - cl[i].cost - cl[j].cost;
   };
