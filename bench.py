@@ -140,8 +140,9 @@ def parity_block(C, last_result, want):
 PEAK_HBM = 8000.0  # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
 # kernels of one scan's GPU phase: (name, tsg_stats field); they add up to ms_gpu_total (+ buffer clears)
 KERNELS = [("chunk_map_kernel", "ms_chunkmap_kernel"), ("filter_kernel (K1)", "ms_scan_kernel"),
-           ("confirm_kernel (K2 + in-place NFA verify)", "ms_confirm_kernel"), ("fold_kernel", "ms_careful_kernel"),
-           ("verify_hits_kernel + fullscan_kernel", "ms_nfa_kernel"), ("finalize_kernel", "ms_finalize_kernel")]
+           ("confirm_kernel (K2)", "ms_confirm_kernel"), ("fold_kernel", "ms_careful_kernel"),
+           ("verify_hits_kernel (follow check + NFA) + fullscan_kernel", "ms_nfa_kernel"),
+           ("finalize_kernel", "ms_finalize_kernel")]
 
 WORKLOADS = {
     "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
@@ -280,7 +281,7 @@ def main():
     if layer is None:
         n_bytes, n_files = C.n_bytes, C.n_files
         arena_bytes = n_bytes
-        counts = {k: int(last[k]) for k in ("flagged_blocks", "confirmed_hits", "anchor_hits", "candidates",
+        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "candidates",
                                             "special_files", "findings")}
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth}
@@ -290,8 +291,8 @@ def main():
         arena_bytes = int(last["scan_bytes"])
         counts = {k: int(last[k]) for k in ("entries", "regular", "required", "added", "skipped_binary",
                                             "whiteouts")}
-        counts.update({k: int(last["scan_" + k]) for k in ("candidates", "findings", "confirmed_hits",
-                                                            "anchor_hits")})
+        counts.update({k: int(last["scan_" + k]) for k in ("candidates", "findings", "anchor_hits",
+                                                            "follow_hits")})
         config_extra = {"walk_s_per_step": round(last["walk_s"], 3), "wait_s_per_step": round(last["wait_s"], 3),
                         "layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,

@@ -51,7 +51,7 @@ int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out);
 int tsg_debug_anchor(const tsg_compiled* c, uint32_t j, uint32_t* rule, uint32_t* lit_len,
                      int32_t* off_lo, int32_t* off_hi);
 const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k);
-/* Anchor j's follow requirements (trivy_amd/csrc/rules.h AnchorReq, 144 B), or NULL. */
+/* Anchor j's follow requirements (trivy_amd/csrc/rules.h FollowLut, 32 B), or NULL. */
 const void* tsg_debug_anchor_req(const tsg_compiled* c, uint32_t j);
 /* The streaming prefilter's tables (trivy_amd/csrc/filter.h): shape = {buckets, window, words},
  * reach[256 * words] (u32; bucket j in word j/4, slot s at bit 4s + j%4; the last bucket counts

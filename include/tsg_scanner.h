@@ -121,7 +121,7 @@ typedef struct tsg_stats {
   uint64_t flagged_blocks;   /* 16-B blocks the streaming filter sent to its exact confirm step */
   double ms_careful_kernel;  /* fold-rune files' careful pass (part of ms_gpu_total) */
   /* per-kernel split of ms_gpu_total (HIP events on the engine stream) */
-  uint64_t confirmed_hits;   /* exact anchor-item matches; anchor_hits = those deferred to the verify kernel */
+  uint64_t follow_hits;      /* anchor_hits (exact anchor-item matches) past the follow requirements */
   double ms_chunkmap_kernel, ms_confirm_kernel, ms_nfa_kernel, ms_finalize_kernel;
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);

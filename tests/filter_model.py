@@ -78,7 +78,8 @@ class FilterModel:
         return np.ctypeslib.as_array((c.c_uint32 * max(1, n.value)).from_address(p.value))[:n.value].copy()
 
     def anchor_reqs(self):
-        """Per anchor: [(lo, hi, [bool[128] per run position])] (rules.h AnchorReq)."""
+        """Per anchor: [(lo, hi, [bool[128] per run position])] -- the sets as the
+        verify kernel tests them (rules.h FollowLut nibble tables)."""
         L = _lib.lib()
         L.tsg_debug_anchor_req.restype = c.c_void_p
         L.tsg_debug_anchor_req.argtypes = [c.c_void_p, c.c_uint32]
@@ -87,30 +88,29 @@ class FilterModel:
             p = L.tsg_debug_anchor_req(self.h, len(out))
             if not p:
                 return out
-            raw = bytes((c.c_uint8 * 144).from_address(p))
-            lo = np.frombuffer(raw[0:4], np.uint16)
-            hi = np.frombuffer(raw[4:8], np.uint16)
-            n = raw[8:10]
-            m = np.frombuffer(raw[16:144], np.uint64).reshape(2, 4, 2)
+            raw = bytes((c.c_uint8 * 32).from_address(p))
+            lo_tab, hi_tab = raw[0:16], raw[16:24]
+            lo, hi, n = raw[24:26], raw[26:28], raw[28:30]
             reqs = []
             for r in range(2):
                 if n[r] == 0:
                     break
-                sets = []
-                for k in range(n[r]):
-                    sets.append(np.array([(int(m[r, k, b >> 6]) >> (b & 63)) & 1 for b in range(128)], dtype=bool))
-                reqs.append((int(lo[r]), int(hi[r]), sets))
+                sets = [np.array([(lo_tab[b & 15] & hi_tab[b >> 4]) >> (4 * r + k) & 1 for b in range(128)],
+                                 dtype=bool) for k in range(n[r])]
+                reqs.append((lo[r], hi[r], sets))
             out.append(reqs)
 
     @staticmethod
     def follow_possible(reqs, content, e):
-        """engine.hip follow_possible: can a match continue after a literal ending at e?"""
+        """engine.hip follow_lut_pass: can a match continue after a literal ending at e?"""
+        if not reqs:
+            return True
+        span = max(hi + len(sets) for lo, hi, sets in reqs)
+        if any(b >= 0x80 for b in content[e:e + span]):
+            return True
         for lo, hi, sets in reqs:
             n = len(sets)
-            end = min(e + hi + n, len(content))
-            if any(b >= 0x80 for b in content[e:end]):
-                return True
-            if not any(all(o + k < len(content) - e and sets[k][content[e + o + k]] for k in range(n))
+            if not any(all(sets[k][content[e + o + k]] for k in range(n))
                        for o in range(lo, hi + 1) if e + o + n <= len(content)):
                 return False
         return True

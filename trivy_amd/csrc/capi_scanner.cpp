@@ -276,7 +276,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.ms_host_total = hs.ms_total;
   st.flagged_blocks = gs.flagged_blocks;
   st.ms_careful_kernel = gs.ms_careful;
-  st.confirmed_hits = gs.confirmed_hits;
+  st.follow_hits = gs.follow_hits;
   st.ms_chunkmap_kernel = gs.ms_chunkmap;
   st.ms_confirm_kernel = gs.ms_confirm;
   st.ms_nfa_kernel = gs.ms_verify;

@@ -29,7 +29,7 @@ struct Candidate {      // produced by the verify / full-scan kernels
 struct BatchStats {
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
   uint64_t flagged_blocks = 0;
-  uint64_t confirmed_hits = 0;  // exact anchor-item matches (hits = those deferred to the verify kernel)
+  uint64_t follow_hits = 0;     // anchor hits past the follow requirements (the NFA runs on these)
   float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
   float ms_finalize = 0, ms_chunkmap = 0;
   bool hit_overflow = false, cand_overflow = false;
@@ -71,7 +71,7 @@ class GpuEngine {
   // tables
   uint32_t diag_mode_ = 0, diag_confirm_ = 0;
   AnchorInfo* d_anchors_ = nullptr;
-  AnchorReq* d_anchor_req_ = nullptr;
+  FollowLut* d_anchor_req_ = nullptr;
   RuleGpu* d_rules_ = nullptr;
   uint32_t* d_rule_kw_ = nullptr;
   uint64_t* d_nfa_ = nullptr;
@@ -107,7 +107,6 @@ class GpuEngine {
   void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
   void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
-  uint32_t nfa_steps_ = 256;          // TSG_NFA_STEPS: in-place verify budget of the confirm kernel
   uint32_t* d_item_diag_ = nullptr;   // TSG_DIAG_ITEMS=<file>: per-item counters dumped after each run
   std::string item_diag_path_;
 };

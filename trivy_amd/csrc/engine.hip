@@ -282,7 +282,91 @@ struct NfaParams {
   uint32_t cand_cap;
   const uint32_t* fullscan_rules;
   uint32_t n_fullscan_rules;
+  const FollowLut* luts;   // per anchor: follow requirements (rules.h)
+  uint64_t n_bytes;        // arena bytes (64 readable past the end)
 };
+
+// Follow requirements of an anchor hit (rules.h FollowLut), on registers.
+// X[0..12] hold the 52 bytes from the literal end (little-endian words);
+// avail = file bytes from there.  False only when every byte up to the last
+// possible run end is ASCII and some requirement's run starts at none of its
+// offsets -- then no match continues from this literal occurrence.
+// Per word: nibble-table set membership of 4 bytes with v_perm (bit 4r + k
+// of byte o = byte o is in run r's k-th set), runs by byte-aligned shifts
+// (bit 4r of Z[o] = the run starts at o), offsets by an interval mask.
+__device__ __forceinline__ bool follow_lut_pass(const FollowLut& L, const uint32_t* X, int64_t avail) {
+  const uint32_t n0 = L.n[0], n1 = L.n[1];
+  if (n0 == 0) return true;
+  const int64_t span0 = int64_t(L.hi[0]) + n0, span1 = n1 ? int64_t(L.hi[1]) + n1 : 0;
+  const int64_t lim = avail < (span0 > span1 ? span0 : span1) ? avail : (span0 > span1 ? span0 : span1);
+  uint32_t nonascii = 0;
+#pragma unroll
+  for (int j = 0; j < 13; j++) {
+    const int64_t v = lim - 4 * j;
+    const uint32_t vm = v >= 4 ? ~0u : (v <= 0 ? 0u : (1u << (8 * uint32_t(v))) - 1u);
+    nonascii |= X[j] & vm;
+  }
+  if (nonascii & 0x80808080u) return true;  // a multi-byte rune or invalid byte: offsets not fixed
+  uint32_t t[4], h[2];
+  __builtin_memcpy(t, L.lo_tab, 16);
+  __builtin_memcpy(h, L.hi_tab, 8);
+  uint32_t M[13];
+#pragma unroll
+  for (int j = 0; j < 13; j++) {
+    const uint32_t lo = X[j] & 0x0F0F0F0Fu, hi = (X[j] >> 4) & 0x07070707u;
+    const uint32_t sel = lo & 0x07070707u;
+    const uint32_t a0 = __builtin_amdgcn_perm(t[1], t[0], sel), a1 = __builtin_amdgcn_perm(t[3], t[2], sel);
+    const uint32_t m8 = ((lo >> 3) & 0x01010101u) * 0xFFu;
+    M[j] = ((a0 & ~m8) | (a1 & m8)) & __builtin_amdgcn_perm(h[1], h[0], hi);
+  }
+  // valid run starts: o in [lo_r, hi_r] with the run inside the file
+  auto interval = [&](int r, uint32_t n) -> uint64_t {
+    int64_t a = L.lo[r], b = L.hi[r];
+    if (avail - int64_t(n) < b) b = avail - int64_t(n);
+    if (b < a) return 0;
+    const uint64_t upto = b >= 63 ? ~uint64_t(0) : (uint64_t(1) << (b + 1)) - 1;
+    return upto & ~((uint64_t(1) << a) - 1);
+  };
+  const uint64_t R0 = interval(0, n0), R1 = n1 ? interval(1, n1) : 0;
+  uint32_t f0 = 0, f1 = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    const uint32_t y1 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 1);
+    const uint32_t y2 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 2);
+    const uint32_t y3 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 3);
+    const uint32_t Z = M[j] & (y1 >> 1) & (y2 >> 2) & (y3 >> 3);
+    const uint32_t s0 = ((uint32_t(R0 >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    const uint32_t s1 = ((uint32_t(R1 >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    f0 |= Z & s0;
+    f1 |= Z & (s1 << 4);
+  }
+  return f0 != 0 && (n1 == 0 || f1 != 0);
+}
+
+// The 52 bytes from arena position e (< n_bytes; the arena has 64 readable
+// bytes past its end) as 13 little-endian words: five aligned 16-B loads,
+// then a two-stage word select and v_alignbyte for the sub-word offset.
+__device__ __forceinline__ void load_follow_bytes(const uint8_t* __restrict arena, uint64_t e, uint32_t* X) {
+  const uint64_t base = e & ~uint64_t(15);
+  uint32_t D[20];
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const uint4 v = load16(arena + base + 16 * q);
+    D[4 * q] = v.x;
+    D[4 * q + 1] = v.y;
+    D[4 * q + 2] = v.z;
+    D[4 * q + 3] = v.w;
+  }
+  const uint32_t s = uint32_t(e & 15);
+  uint32_t R[14];
+#pragma unroll
+  for (int j = 0; j < 14; j++) {
+    const uint32_t r1a = (s & 4) ? D[j + 1] : D[j], r1b = (s & 4) ? D[j + 3] : D[j + 2];
+    R[j] = (s & 8) ? r1b : r1a;
+  }
+#pragma unroll
+  for (int j = 0; j < 13; j++) X[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], s & 3);
+}
 
 // ---------------------------------------------------------------------------
 // K2: confirm flagged blocks exactly + verify the anchor hits
@@ -388,64 +472,14 @@ struct ConfirmParams {
   uint32_t hit_cap;
   FoldSite* folds;     // fold runes found (for the fold kernel)
   uint32_t fold_cap;
-  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission,
-                       // 32 no follow requirements, 64 no in-place NFA (hits go to K4)
+  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission
   uint32_t* kwbits;               // per file: kw_words x u32 keyword bits
   uint32_t kw_words;
   const uint64_t* core;           // filter.h core tables (n_groups x 256)
   const uint32_t* group_items;    // n_groups x 8
   const uint32_t* bucket_groups;  // n_buckets + 1
-  const AnchorReq* reqs;          // per anchor: follow requirements (rules.h)
-  Candidate* cands;               // anchor hits verified in place (NFA accepted)
-  uint32_t cand_cap;
-  uint32_t nfa_steps;             // in-place NFA budget per hit (bytes); longer runs go to K4
-  uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item {exact matches, hits passed on}
+  uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item exact matches
 };
-
-// The follow requirements of an anchor hit (rules.h AnchorReq) over the
-// bytes after its literal end e: false only when every byte up to the last
-// possible run end is ASCII and some requirement's run occurs at none of its
-// offsets, i.e. no match can continue from this literal occurrence.  One
-// shift-and pass per requirement (run position k in bit k).
-template <typename ByteAt>
-__device__ __forceinline__ bool follow_possible(const AnchorReq* __restrict rq, int64_t e, int64_t flen,
-                                                const ByteAt& byte_at) {
-#pragma unroll
-  for (int r = 0; r < kMaxReqs; r++) {
-    const uint32_t n = rq->n[r];
-    if (n == 0) break;
-    const int64_t lo = rq->lo[r], hi = rq->hi[r];
-    uint64_t m0[kMaxReqLen], m1[kMaxReqLen];
-#pragma unroll
-    for (int k = 0; k < kMaxReqLen; k++) {
-      m0[k] = rq->m[r][k][0];
-      m1[k] = rq->m[r][k][1];
-    }
-    const int64_t end = e + hi + int64_t(n) < flen ? e + hi + int64_t(n) : flen;
-    uint32_t D = 0;
-    bool found = false;
-    for (int64_t p = e; p < end; p++) {
-      const uint32_t b = byte_at(p);
-      if (b >= 0x80u) return true;  // a multi-byte rune or an invalid byte: offsets no longer fixed
-      const uint64_t bit = uint64_t(1) << (b & 63u);
-      uint32_t mk = 0;
-#pragma unroll
-      for (int k = 0; k < kMaxReqLen; k++) mk |= uint32_t((((b & 64u) ? m1[k] : m0[k]) & bit) != 0) << k;
-      const int64_t o = p - e;
-      D = ((D << 1) | uint32_t(o >= lo && o <= hi)) & mk;
-      if ((D >> (n - 1)) & 1u) {
-        found = true;
-        break;
-      }
-    }
-    if (!found) return false;
-  }
-  return true;
-}
-
-// Prefix bytes scanned for fold-rune lead bytes before verifying an anchor
-// hit in place (an anchor whose fold-widened prefix is longer goes to K4).
-constexpr int32_t kFoldPrefixScan = 96;
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
 // (aligned) instead of one dependent load per byte.  Injects the start state
@@ -605,7 +639,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   }
   const uint8_t* tabs = kLdsTabs ? s_tabs : static_cast<const uint8_t*>(P.tabs);
   const uint32_t lane = tid & 63, wave = tid >> 6;
-  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2 [3] confirmed anchor hits
+  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2
   if (lane < 4) cnt[lane] = 0;
   __syncthreads();
   const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
@@ -666,42 +700,9 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
       return;
     }
     if (P.item_diag) atomicAdd(&P.item_diag[2 * ix], 1u);
-    // Verify each anchor hit here, with the block's bytes still in cache: the
-    // rule's relaxed NFA from the start window the anchor's offsets give
-    // (exactly K4's check).  Deferred to K4 (the hit list) are hits whose
-    // fold-widened prefix may hold a fold rune (the window then depends on
-    // the file's fold flags, known only after this kernel) and runs longer
-    // than the in-place budget.
     const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
-    const int64_t flen = int64_t(fe - fs);
-    for (uint32_t d = 0; d < it.n_ids; d++) {
-      const uint32_t aid = item_ids[it.ids_off + d];
-      atomicAdd(&cnt[3], 1u);
-      if (!(P.diag & 32) &&
-          !follow_possible(P.reqs + aid, lit_end, flen, [&](int64_t q) { return win_byte(l, fs + uint64_t(q)); }))
-        continue;
-      const AnchorInfo a = P.anchors[aid];
-      const int64_t lit_hi = int64_t(lit_end) - int64_t(a.lit_len);  // literal start, file-relative
-      const int64_t whi = lit_hi - a.off_lo;
-      if (whi < 0) continue;  // no match can start before the file (as K4)
-      bool defer = a.off_hi_fold > kFoldPrefixScan || (P.diag & 64);
-      for (int64_t q = lit_hi - a.off_hi_fold < 0 ? 0 : lit_hi - a.off_hi_fold; q < lit_hi && !defer; q++) {
-        const uint32_t b = win_byte(l, fs + uint64_t(q));
-        defer = b == 0xC4u || b == 0xC5u || b == 0xE2u;  // lead byte of U+0130 / U+017F / U+212A
-      }
-      int res = kNfaUndecided;
-      const int64_t wlo = lit_hi - a.off_hi < 0 ? 0 : lit_hi - a.off_hi;
-      if (!defer) {
-        const RuleGpu rg = P.rules[a.rule];
-        res = rg.nfa_words == 0 ? kNfaAccept
-                                : nfa_dispatch_abs(rg.nfa_words, P.arena, fs, flen, wlo, whi, P.nfa + rg.nfa_off,
-                                                   int64_t(P.nfa_steps));
-      }
-      if (res == kNfaReject) continue;
-      if (P.item_diag) atomicAdd(&P.item_diag[2 * ix + 1], 1u);
-      if (res == kNfaAccept) put_candidate(P.cands, P.cand_cap, P.counters, f, a.rule, wlo, whi);
-      else stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, aid);
-    }
+    for (uint32_t d = 0; d < it.n_ids; d++)
+      stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
   };
   auto run_q2 = [&]() {  // wave-uniform: phase C over the queued candidates
     wave_sync();
@@ -802,8 +803,6 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     wave_sync();
   }
   flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
-  wave_sync();
-  if (lane == 0 && cnt[3]) atomicAdd(&P.counters[11], cnt[3]);  // confirmed anchor hits (stats)
 }
 
 // Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
@@ -958,6 +957,23 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
     if (wlo < 0) wlo = 0;
     const uint64_t fs = P.off[f];
     const int64_t len = int64_t(P.off[f + 1] - fs);
+    if (!(ff & 1u)) {  // files without fold runes: the anchor's follow requirements first
+      const FollowLut lut = P.luts[aid];
+      if (lut.n[0]) {
+        bool pass = false;
+        if (fs + end < P.n_bytes) {
+          uint32_t X[13];
+          load_follow_bytes(P.arena, fs + end, X);
+          pass = follow_lut_pass(lut, X, len - int64_t(end));
+        }
+        if (!pass) continue;
+      }
+    }
+    {  // hits past the follow check (stats)
+      const uint64_t m = __ballot(1);
+      if (__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)) == 0)
+        atomicAdd(&P.counters[12], uint32_t(__popcll(m)));
+    }
     const bool acc = rg.nfa_words == 0 ||
                      nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off) == kNfaAccept;
     if (acc) put_candidate(P.cands, P.cand_cap, P.counters, f, a.rule, wlo, whi);
@@ -1002,11 +1018,16 @@ __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
       const uint64_t a = fs, b = fs + uint64_t(c.wlo);
       const uint64_t ca = (a + kChunk - 1) / kChunk, cb = b / kChunk;
       int64_t part = 0;
+      // partial ranges (< 1 KiB each, < 2 KiB unsplit): one 16-B block per lane
+      auto blocks = [&](uint64_t x, uint64_t y) {
+        for (uint64_t blk = (x & ~uint64_t(15)) + 16 * lane; blk < y; blk += 16 * 64)
+          part += count_nl_range(P.arena, blk > x ? blk : x, blk + 16 < y ? blk + 16 : y);
+      };
       if (ca >= cb) {
-        if (lane == 0) part = count_nl_range(P.arena, a, b);
+        blocks(a, b);
       } else {
-        if (lane == 0) part = count_nl_range(P.arena, a, ca * kChunk);
-        if (lane == 1) part = count_nl_range(P.arena, cb * kChunk, b);
+        blocks(a, ca * kChunk);
+        blocks(cb * kChunk, b);
         for (uint64_t cc = ca + lane; cc < cb; cc += 64) part += P.nl[cc];
       }
 #pragma unroll
@@ -1051,7 +1072,6 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   for (auto& e : ev_) hipEventCreate(&e);
   if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
   if (const char* dc = std::getenv("TSG_DIAG_CONFIRM")) diag_confirm_ = uint32_t(std::atoi(dc));
-  if (const char* ns = std::getenv("TSG_NFA_STEPS")) nfa_steps_ = uint32_t(std::atoi(ns));
   if (const char* di = std::getenv("TSG_DIAG_ITEMS")) item_diag_path_ = di;
   kw_words_ = std::max<uint32_t>(1, cr.kw_words());
   n_rules_ = uint32_t(cr.rules.size());
@@ -1301,10 +1321,6 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.core = d_core_;
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;
-    cp.reqs = d_anchor_req_;
-    cp.cands = static_cast<Candidate*>(d_cands_);
-    cp.cand_cap = cand_cap_;
-    cp.nfa_steps = nfa_steps_;
     cp.item_diag = d_item_diag_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
@@ -1361,6 +1377,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.cand_cap = cand_cap_;
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
+    np.luts = d_anchor_req_;
+    np.n_bytes = n_bytes;
     if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     if (np.n_fullscan_rules > 0) {
@@ -1378,7 +1396,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       std::fprintf(stderr, "counters: hits %u cands %u special %u recs %u folds %u\n", cnt[0], cnt[1], cnt[2], cnt[7],
                    cnt[9]);
     st->hits = cnt[0];
-    st->confirmed_hits = cnt[11];
+    st->follow_hits = cnt[12];
     st->special_files = cnt[2];
     st->flagged_blocks = cnt[7];
     if (cnt[8]) {  // record list overflow: grow and rescan

@@ -665,8 +665,12 @@ std::vector<ByteSet> BeforeSets(const std::vector<Node>& nodes, const std::vecto
 // they are fixed-length.  The (at most two, disjoint) runs with the fewest
 // expected chance occurrences over their offset range (static byte prior)
 // are kept.
-AnchorReq FollowReqs(const std::vector<Node>& nodes, const std::vector<int>& fol) {
-  AnchorReq rq{};
+FollowLut FollowReqs(const std::vector<Node>& nodes, const std::vector<int>& fol) {
+  FollowLut rq{};
+  for (int s = 0; s < 8; s++) {  // unused slots accept every ASCII byte
+    for (auto& x : rq.lo_tab) x |= uint8_t(1u << s);
+    for (auto& x : rq.hi_tab) x |= uint8_t(1u << s);
+  }
   std::vector<Elem> seq;
   for (int it : fol) {
     auto r = Relax(nodes, it);
@@ -699,7 +703,7 @@ AnchorReq FollowReqs(const std::vector<Node>& nodes, const std::vector<int>& fol
         p *= q;
       }
       r.score = double(hi - lo + 1) * p;
-      if (r.score < 1.0) runs.push_back(r);
+      if (r.score < 1.0 && hi + int64_t(r.sets.size()) <= kReqSpan) runs.push_back(r);
     }
     lo += seq[j].min;
     hi = (seq[j].max < 0 || hi >= kInf) ? kInf : hi + seq[j].max;
@@ -713,12 +717,19 @@ AnchorReq FollowReqs(const std::vector<Node>& nodes, const std::vector<int>& fol
       if (r.j0 < u.second && u.first < r.j1) overlap = true;
     if (overlap) continue;
     used.push_back({r.j0, r.j1});
-    rq.lo[nr] = uint16_t(r.lo);
-    rq.hi[nr] = uint16_t(r.hi);
+    rq.lo[nr] = uint8_t(r.lo);
+    rq.hi[nr] = uint8_t(r.hi);
     rq.n[nr] = uint8_t(r.sets.size());
-    for (size_t k = 0; k < r.sets.size(); k++)
+    for (size_t k = 0; k < r.sets.size(); k++) {
+      const uint8_t bit = uint8_t(1u << (4 * nr + int(k)));
+      for (auto& x : rq.lo_tab) x &= uint8_t(~bit);
+      for (auto& x : rq.hi_tab) x &= uint8_t(~bit);
       for (int b = 0; b < 0x80; b++)
-        if (r.sets[k].test(size_t(b))) rq.m[nr][k][b >> 6] |= uint64_t(1) << (b & 63);
+        if (r.sets[k].test(size_t(b))) {
+          rq.lo_tab[b & 15] |= bit;
+          rq.hi_tab[b >> 4] |= bit;
+        }
+    }
     if (++nr == kMaxReqs) break;
   }
   return rq;

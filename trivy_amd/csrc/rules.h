@@ -56,15 +56,19 @@ struct AnchorInfo {  // mirrored on the device
 // consecutive byte sets starting at a byte offset in [lo[r], hi[r]] from the
 // literal end (one relaxed-NFA position per ASCII byte).  A hit whose bytes
 // up to the last possible run end are ASCII and hold no such run cannot be a
-// match; any byte >= 0x80 in that range leaves the hit to the NFA.
-constexpr int kMaxReqs = 2, kMaxReqLen = 4;
-struct AnchorReq {
-  uint16_t lo[kMaxReqs], hi[kMaxReqs];
-  uint8_t n[kMaxReqs];                   // 0: no requirement
-  uint8_t pad[6];
-  uint64_t m[kMaxReqs][kMaxReqLen][2];   // ASCII members of each set (bit b of word b / 64)
+// match; any byte >= 0x80 in that range leaves the hit to the NFA.  Sets are
+// kept as nibble tables (slot 4r + k: run r, position k): byte b is in slot
+// s's set when bit s of lo_tab[b & 15] & hi_tab[b >> 4] is set -- the
+// product of the set's low- and high-nibble projections, a superset of it.
+constexpr int kMaxReqs = 2, kMaxReqLen = 4, kReqSpan = 48;  // hi + n <= kReqSpan
+struct FollowLut {
+  uint8_t lo_tab[16];
+  uint8_t hi_tab[8];       // ASCII high nibbles 0..7
+  uint8_t lo[kMaxReqs], hi[kMaxReqs];
+  uint8_t n[kMaxReqs];     // 0: no requirement
+  uint8_t pad[2];
 };
-static_assert(sizeof(AnchorReq) == 144, "AnchorReq layout (tests/filter_model.py reads it)");
+static_assert(sizeof(FollowLut) == 32, "FollowLut layout (tests/filter_model.py reads it)");
 
 struct RuleGpu {  // mirrored on the device
   uint32_t nfa_off;     // index into nfa words (u64)
@@ -95,7 +99,7 @@ struct CompiledRules {
   // keywords / anchors
   std::vector<std::string> keywords;  // unique lowercased ASCII keywords
   std::vector<AnchorInfo> anchors;
-  std::vector<AnchorReq> anchor_req;  // per anchor
+  std::vector<FollowLut> anchor_req;  // per anchor
   // rules
   std::vector<RuleGpu> rules;
   std::vector<uint32_t> rule_kw;  // keyword ids

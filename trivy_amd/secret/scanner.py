@@ -50,7 +50,7 @@ class _CStats(c.Structure):
                                           "ms_gpu_total", "ms_host_gpu_phase", "ms_host_allow_path",
                                           "ms_host_exact", "ms_host_total")] + \
                [("flagged_blocks", c.c_uint64), ("ms_careful_kernel", c.c_double),
-                ("confirmed_hits", c.c_uint64)] + \
+                ("follow_hits", c.c_uint64)] + \
                [(n, c.c_double) for n in ("ms_chunkmap_kernel", "ms_confirm_kernel", "ms_nfa_kernel",
                                           "ms_finalize_kernel")]
 
