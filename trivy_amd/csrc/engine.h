@@ -29,7 +29,7 @@ struct Candidate {      // produced by the verify / full-scan kernels
 struct BatchStats {
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
   uint64_t flagged_blocks = 0;
-  uint64_t follow_hits = 0;     // anchor hits past the follow requirements (the NFA runs on these)
+  uint64_t follow_hits = 0;     // anchor hits past the follow requirements + fold-kernel hits (the NFA runs on these)
   float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
   float ms_finalize = 0, ms_chunkmap = 0;
   bool hit_overflow = false, cand_overflow = false;

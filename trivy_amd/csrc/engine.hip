@@ -282,91 +282,9 @@ struct NfaParams {
   uint32_t cand_cap;
   const uint32_t* fullscan_rules;
   uint32_t n_fullscan_rules;
-  const FollowLut* luts;   // per anchor: follow requirements (rules.h)
-  uint64_t n_bytes;        // arena bytes (64 readable past the end)
 };
 
-// Follow requirements of an anchor hit (rules.h FollowLut), on registers.
-// X[0..12] hold the 52 bytes from the literal end (little-endian words);
-// avail = file bytes from there.  False only when every byte up to the last
-// possible run end is ASCII and some requirement's run starts at none of its
-// offsets -- then no match continues from this literal occurrence.
-// Per word: nibble-table set membership of 4 bytes with v_perm (bit 4r + k
-// of byte o = byte o is in run r's k-th set), runs by byte-aligned shifts
-// (bit 4r of Z[o] = the run starts at o), offsets by an interval mask.
-__device__ __forceinline__ bool follow_lut_pass(const FollowLut& L, const uint32_t* X, int64_t avail) {
-  const uint32_t n0 = L.n[0], n1 = L.n[1];
-  if (n0 == 0) return true;
-  const int64_t span0 = int64_t(L.hi[0]) + n0, span1 = n1 ? int64_t(L.hi[1]) + n1 : 0;
-  const int64_t lim = avail < (span0 > span1 ? span0 : span1) ? avail : (span0 > span1 ? span0 : span1);
-  uint32_t nonascii = 0;
-#pragma unroll
-  for (int j = 0; j < 13; j++) {
-    const int64_t v = lim - 4 * j;
-    const uint32_t vm = v >= 4 ? ~0u : (v <= 0 ? 0u : (1u << (8 * uint32_t(v))) - 1u);
-    nonascii |= X[j] & vm;
-  }
-  if (nonascii & 0x80808080u) return true;  // a multi-byte rune or invalid byte: offsets not fixed
-  uint32_t t[4], h[2];
-  __builtin_memcpy(t, L.lo_tab, 16);
-  __builtin_memcpy(h, L.hi_tab, 8);
-  uint32_t M[13];
-#pragma unroll
-  for (int j = 0; j < 13; j++) {
-    const uint32_t lo = X[j] & 0x0F0F0F0Fu, hi = (X[j] >> 4) & 0x07070707u;
-    const uint32_t sel = lo & 0x07070707u;
-    const uint32_t a0 = __builtin_amdgcn_perm(t[1], t[0], sel), a1 = __builtin_amdgcn_perm(t[3], t[2], sel);
-    const uint32_t m8 = ((lo >> 3) & 0x01010101u) * 0xFFu;
-    M[j] = ((a0 & ~m8) | (a1 & m8)) & __builtin_amdgcn_perm(h[1], h[0], hi);
-  }
-  // valid run starts: o in [lo_r, hi_r] with the run inside the file
-  auto interval = [&](int r, uint32_t n) -> uint64_t {
-    int64_t a = L.lo[r], b = L.hi[r];
-    if (avail - int64_t(n) < b) b = avail - int64_t(n);
-    if (b < a) return 0;
-    const uint64_t upto = b >= 63 ? ~uint64_t(0) : (uint64_t(1) << (b + 1)) - 1;
-    return upto & ~((uint64_t(1) << a) - 1);
-  };
-  const uint64_t R0 = interval(0, n0), R1 = n1 ? interval(1, n1) : 0;
-  uint32_t f0 = 0, f1 = 0;
-#pragma unroll
-  for (int j = 0; j < 12; j++) {
-    const uint32_t y1 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 1);
-    const uint32_t y2 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 2);
-    const uint32_t y3 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 3);
-    const uint32_t Z = M[j] & (y1 >> 1) & (y2 >> 2) & (y3 >> 3);
-    const uint32_t s0 = ((uint32_t(R0 >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    const uint32_t s1 = ((uint32_t(R1 >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    f0 |= Z & s0;
-    f1 |= Z & (s1 << 4);
-  }
-  return f0 != 0 && (n1 == 0 || f1 != 0);
-}
 
-// The 52 bytes from arena position e (< n_bytes; the arena has 64 readable
-// bytes past its end) as 13 little-endian words: five aligned 16-B loads,
-// then a two-stage word select and v_alignbyte for the sub-word offset.
-__device__ __forceinline__ void load_follow_bytes(const uint8_t* __restrict arena, uint64_t e, uint32_t* X) {
-  const uint64_t base = e & ~uint64_t(15);
-  uint32_t D[20];
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    const uint4 v = load16(arena + base + 16 * q);
-    D[4 * q] = v.x;
-    D[4 * q + 1] = v.y;
-    D[4 * q + 2] = v.z;
-    D[4 * q + 3] = v.w;
-  }
-  const uint32_t s = uint32_t(e & 15);
-  uint32_t R[14];
-#pragma unroll
-  for (int j = 0; j < 14; j++) {
-    const uint32_t r1a = (s & 4) ? D[j + 1] : D[j], r1b = (s & 4) ? D[j + 3] : D[j + 2];
-    R[j] = (s & 8) ? r1b : r1a;
-  }
-#pragma unroll
-  for (int j = 0; j < 13; j++) X[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], s & 3);
-}
 
 // ---------------------------------------------------------------------------
 // K2: confirm flagged blocks exactly + verify the anchor hits
@@ -450,7 +368,88 @@ __device__ __forceinline__ void put_hit(uint32_t* hits, uint32_t cap, uint32_t* 
     counters[3] = 1;
   }
 }
-constexpr int kCWin = 64;  // per-lane LDS copy of arena bytes [base - 16, base + 48)
+// Follow requirements of an anchor hit (rules.h FollowLut), on registers.
+// X[0..12] hold the 52 bytes from the literal end (little-endian words);
+// avail = file bytes from there.  False only when every byte up to the last
+// possible run end is ASCII and some requirement's run starts at none of its
+// offsets -- then no match continues from this literal occurrence.
+// Per word: nibble-table set membership of 4 bytes with v_perm (bit 4r + k
+// of byte o = byte o is in run r's k-th set), runs by byte-aligned shifts
+// (bit 4r of Z[o] = the run starts at o), offsets by an interval mask.
+__device__ __forceinline__ bool follow_lut_pass(const FollowLut& L, const uint32_t* X, int64_t avail) {
+  const uint32_t n0 = L.n[0], n1 = L.n[1];
+  if (n0 == 0) return true;
+  const int64_t span0 = int64_t(L.hi[0]) + n0, span1 = n1 ? int64_t(L.hi[1]) + n1 : 0;
+  const int64_t lim = avail < (span0 > span1 ? span0 : span1) ? avail : (span0 > span1 ? span0 : span1);
+  uint32_t nonascii = 0;
+#pragma unroll
+  for (int j = 0; j < 13; j++) {
+    const int64_t v = lim - 4 * j;
+    const uint32_t vm = v >= 4 ? ~0u : (v <= 0 ? 0u : (1u << (8 * uint32_t(v))) - 1u);
+    nonascii |= X[j] & vm;
+  }
+  if (nonascii & 0x80808080u) return true;  // a multi-byte rune or invalid byte: offsets not fixed
+  uint32_t t[4], h[2];
+  __builtin_memcpy(t, L.lo_tab, 16);
+  __builtin_memcpy(h, L.hi_tab, 8);
+  uint32_t M[13];
+#pragma unroll
+  for (int j = 0; j < 13; j++) {
+    const uint32_t lo = X[j] & 0x0F0F0F0Fu, hi = (X[j] >> 4) & 0x07070707u;
+    const uint32_t sel = lo & 0x07070707u;
+    const uint32_t a0 = __builtin_amdgcn_perm(t[1], t[0], sel), a1 = __builtin_amdgcn_perm(t[3], t[2], sel);
+    const uint32_t m8 = ((lo >> 3) & 0x01010101u) * 0xFFu;
+    M[j] = ((a0 & ~m8) | (a1 & m8)) & __builtin_amdgcn_perm(h[1], h[0], hi);
+  }
+  // valid run starts: o in [lo_r, hi_r] with the run inside the file
+  auto interval = [&](int r, uint32_t n) -> uint64_t {
+    int64_t a = L.lo[r], b = L.hi[r];
+    if (avail - int64_t(n) < b) b = avail - int64_t(n);
+    if (b < a) return 0;
+    const uint64_t upto = b >= 63 ? ~uint64_t(0) : (uint64_t(1) << (b + 1)) - 1;
+    return upto & ~((uint64_t(1) << a) - 1);
+  };
+  const uint64_t R0 = interval(0, n0), R1 = n1 ? interval(1, n1) : 0;
+  uint32_t f0 = 0, f1 = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    const uint32_t y1 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 1);
+    const uint32_t y2 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 2);
+    const uint32_t y3 = __builtin_amdgcn_alignbyte(M[j + 1], M[j], 3);
+    const uint32_t Z = M[j] & (y1 >> 1) & (y2 >> 2) & (y3 >> 3);
+    const uint32_t s0 = ((uint32_t(R0 >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    const uint32_t s1 = ((uint32_t(R1 >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    f0 |= Z & s0;
+    f1 |= Z & (s1 << 4);
+  }
+  return f0 != 0 && (n1 == 0 || f1 != 0);
+}
+
+// The 52 bytes from byte s (0..15) of the 16-B aligned pointer p16 as 13
+// little-endian words: five aligned 16-B loads (global memory or LDS), then a
+// two-stage word select and v_alignbyte for the sub-word offset.
+template <typename Ptr>
+__device__ __forceinline__ void follow_words(Ptr p16, uint32_t s, uint32_t* X) {
+  uint32_t D[20];
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p16 + 16 * q);
+    D[4 * q] = v.x;
+    D[4 * q + 1] = v.y;
+    D[4 * q + 2] = v.z;
+    D[4 * q + 3] = v.w;
+  }
+  uint32_t R[14];
+#pragma unroll
+  for (int j = 0; j < 14; j++) {
+    const uint32_t r1a = (s & 4) ? D[j + 1] : D[j], r1b = (s & 4) ? D[j + 3] : D[j + 2];
+    R[j] = (s & 8) ? r1b : r1a;
+  }
+#pragma unroll
+  for (int j = 0; j < 13; j++) X[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], s & 3);
+}
+
+constexpr int kCWin = 112;  // per-lane LDS copy of arena bytes [base - 16, base + 96)
 
 struct ConfirmParams {
   const uint8_t* arena;
@@ -479,6 +478,7 @@ struct ConfirmParams {
   const uint32_t* group_items;    // n_groups x 8
   const uint32_t* bucket_groups;  // n_buckets + 1
   uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item exact matches
+  const FollowLut* luts;          // per anchor: follow requirements (rules.h)
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   }
   const uint8_t* tabs = kLdsTabs ? s_tabs : static_cast<const uint8_t*>(P.tabs);
   const uint32_t lane = tid & 63, wave = tid >> 6;
-  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2
+  uint32_t* cnt = s_cnt + wave * 4;  // [0] staged hits [1] q1 [2] q2 [3] anchor-item matches
   if (lane < 4) cnt[lane] = 0;
   __syncthreads();
   const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
@@ -701,8 +701,31 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     }
     if (P.item_diag) atomicAdd(&P.item_diag[2 * ix], 1u);
     const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
-    for (uint32_t d = 0; d < it.n_ids; d++)
-      stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, item_ids[it.ids_off + d]);
+    // The anchor's follow requirements over the 52 bytes after the literal,
+    // read from the lane's LDS window when it holds them (else through the
+    // caches): most hits of frequent anchor words ("aws_region", prose
+    // "linear") end here instead of in the verify kernel's NFA.
+    const uint64_t e = s0 + it.lit_end;
+    const uint64_t w0 = wbase[l] >= 16 ? wbase[l] - 16 : 0;
+    uint32_t X[13];
+    bool have_x = false;
+    for (uint32_t d = 0; d < it.n_ids; d++) {
+      const uint32_t aid = item_ids[it.ids_off + d];
+      atomicAdd(&cnt[3], 1u);
+      const FollowLut lut = P.luts[aid];
+      if (lut.n[0] && e < P.n_bytes) {
+        if (!have_x) {
+          const uint64_t s = e - w0;
+          if (e >= w0 && (s & ~uint64_t(15)) + 80 <= uint64_t(kCWin))
+            follow_words(wwin + l * kCWin + (s & ~uint64_t(15)), uint32_t(s & 15), X);
+          else
+            follow_words(P.arena + (e & ~uint64_t(15)), uint32_t(e & 15), X);
+          have_x = true;
+        }
+        if (!follow_lut_pass(lut, X, int64_t(fe - e))) continue;
+      }
+      stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, aid);
+    }
   };
   auto run_q2 = [&]() {  // wave-uniform: phase C over the queued candidates
     wave_sync();
@@ -757,13 +780,14 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     if (r < n_recs) {
       const uint64_t base = uint64_t(P.recs[r]) * 16;
       const uint64_t w0 = base >= 16 ? base - 16 : 0;
-      const uint4 d0 = load16(P.arena + w0), d1 = load16(P.arena + w0 + 16), d2 = load16(P.arena + w0 + 32),
-                  d3 = load16(P.arena + w0 + 48);
+      uint4 dw[kCWin / 16];
+#pragma unroll
+      for (int q = 0; q < kCWin / 16; q++)  // the arena holds 64 readable bytes past n_bytes
+        dw[q] = w0 + 16 * q + 16 <= P.n_bytes + 64 ? load16(P.arena + w0 + 16 * q) : make_uint4(0, 0, 0, 0);
+      const uint4 d0 = dw[0], d1 = dw[1];
       uint4* wl = reinterpret_cast<uint4*>(wwin + lane * kCWin);
-      wl[0] = d0;
-      wl[1] = d1;
-      wl[2] = d2;
-      wl[3] = d3;
+#pragma unroll
+      for (int q = 0; q < kCWin / 16; q++) wl[q] = dw[q];
       wbase[lane] = base;
       const uint4 pv = base >= 16 ? d0 : make_uint4(0, 0, 0, 0);
       const uint4 v = base >= 16 ? d1 : d0;
@@ -803,6 +827,8 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     wave_sync();
   }
   flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
+  wave_sync();
+  if (lane == 0 && cnt[3]) atomicAdd(&P.counters[11], cnt[3]);  // anchor-item matches (stats)
 }
 
 // Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
@@ -957,23 +983,7 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
     if (wlo < 0) wlo = 0;
     const uint64_t fs = P.off[f];
     const int64_t len = int64_t(P.off[f + 1] - fs);
-    if (!(ff & 1u)) {  // files without fold runes: the anchor's follow requirements first
-      const FollowLut lut = P.luts[aid];
-      if (lut.n[0]) {
-        bool pass = false;
-        if (fs + end < P.n_bytes) {
-          uint32_t X[13];
-          load_follow_bytes(P.arena, fs + end, X);
-          pass = follow_lut_pass(lut, X, len - int64_t(end));
-        }
-        if (!pass) continue;
-      }
-    }
-    {  // hits past the follow check (stats)
-      const uint64_t m = __ballot(1);
-      if (__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)) == 0)
-        atomicAdd(&P.counters[12], uint32_t(__popcll(m)));
-    }
+
     const bool acc = rg.nfa_words == 0 ||
                      nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, wlo, whi, P.nfa + rg.nfa_off) == kNfaAccept;
     if (acc) put_candidate(P.cands, P.cand_cap, P.counters, f, a.rule, wlo, whi);
@@ -1182,7 +1192,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     // larger ones are read from global memory (L2-resident).  c3 (103 KB of
     // tables): LDS at 1 WG/CU 102 GB/s vs global at 4 WG/CU 164 GB/s.
     // TSG_LDS_TABS_MAX overrides (tuning).
-    size_t lds_max = 64 * 1024;  // measured: 1 WG/CU with 160-KiB tables loses to 4 WGs/CU reading L2
+    size_t lds_max = 80 * 1024;  // two workgroups per CU; measured: 1 WG/CU with 160-KiB tables loses to 4 WGs/CU reading L2
     if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
     lds_tabs_ = fixed + ftabs_bytes_ <= lds_max && ftabs_bytes_ + 2 * kFoldSpan + 16 <= lds_max;
     if (!item_diag_path_.empty() && hipMalloc(&d_item_diag_, 8 * std::max<size_t>(n_fitems_, 1)) != hipSuccess) {
@@ -1322,6 +1332,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;
     cp.item_diag = d_item_diag_;
+    cp.luts = d_anchor_req_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
         confirm_kernel<true><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
@@ -1377,8 +1388,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.cand_cap = cand_cap_;
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
-    np.luts = d_anchor_req_;
-    np.n_bytes = n_bytes;
+
     if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     if (np.n_fullscan_rules > 0) {
@@ -1395,8 +1405,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     if (std::getenv("TSG_STATS_DEBUG"))
       std::fprintf(stderr, "counters: hits %u cands %u special %u recs %u folds %u\n", cnt[0], cnt[1], cnt[2], cnt[7],
                    cnt[9]);
-    st->hits = cnt[0];
-    st->follow_hits = cnt[12];
+    st->hits = cnt[11];  // exact anchor-item matches in the confirm kernel
+    st->follow_hits = cnt[0];  // past the follow requirements (+ fold-kernel hits): the verify kernel's input
     st->special_files = cnt[2];
     st->flagged_blocks = cnt[7];
     if (cnt[8]) {  // record list overflow: grow and rescan
