@@ -91,14 +91,18 @@ def cpu_baseline_layer(layer, cores, tmpdir):
                       "%.1f s wall" % (layer.size / 1e6, cores, nb / 1e6, nf, dt)}
 
 
-def cpu_baseline(C, sample_bytes, cores, tmpdir, cfg_path=None):
-    """Oracle ('port' of the reference CPU algorithm) on the first files of the corpus."""
-    import multiprocessing as mp
-    import numpy as np
+def _first_files(C, sample_bytes):
     n = 0
     while n < C.n_files and int(C.offsets[n + 1]) <= sample_bytes:
         n += 1
-    n = max(n, 1)
+    return max(n, 1)
+
+
+def oracle_sample(C, sample_bytes, cores, tmpdir, cfg_path=None):
+    """The Python oracle (pinned by the reference's golden tests) on the first files: the parity reference."""
+    import multiprocessing as mp
+    import numpy as np
+    n = _first_files(C, sample_bytes)
     end = int(C.offsets[n])
     ap = os.path.join(tmpdir, "cpu_arena.npy")
     op = os.path.join(tmpdir, "cpu_offs.npy")
@@ -106,24 +110,68 @@ def cpu_baseline(C, sample_bytes, cores, tmpdir, cfg_path=None):
     np.save(ap, C.arena[:end])
     np.save(op, C.offsets[:n + 1])
     np.save(pp, C.path_buf[:n * 64])
-    # interleave files over workers for balance
-    chunks = [list(range(k, n, cores)) for k in range(cores)]
+    chunks = [list(range(k, n, cores)) for k in range(cores)]  # interleave files over workers for balance
     ctx = mp.get_context("spawn")
     t0 = time.time()
     with ctx.Pool(cores) as pool:
         res = pool.map(_cpu_sample_worker, [(ch, ap, op, pp, cfg_path) for ch in chunks])
     dt = time.time() - t0
-    nb = sum(r[0] for r in res)
-    nf = sum(r[1] for r in res)
     want = {}
     for r in res:
         want.update(r[2])
     for f in (ap, op, pp):
         os.remove(f)
-    return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": cores, "kind": "port",
-            "sample": "first %d files (%.1f MB) of the same corpus, oracle/secret_scanner.py "
-                      "(Python restatement of scanner.go%s) in %d processes; %d findings; %.1f s wall"
-                      % (n, nb / 1e6, ", same rule set" if cfg_path else "", cores, nf, dt)}, want
+    return want, dt
+
+
+def cpu_baseline(C, sample_bytes, threads, cfg_path, want):
+    """C++ restatement of the reference CPU algorithm (oracle/native/host_hooks.cpp tsg_cpuref_scan:
+    scanner.go:377-463 -- per file and rule bytes.ToLower + Contains, whole-file Go-regexp FindAll,
+    the same tail) on the first files of the corpus, timed on `threads` host threads per entry."""
+    import ctypes as c
+    import numpy as np
+    from oracle import hostlib
+    import trivy_amd.secret as secret
+    from trivy_amd.secret.scanner import ScanResult, _CBatch, _CStats
+    L = hostlib.lib()
+    sc = secret.NewScanner(secret.ParseConfig(cfg_path) if cfg_path else None, lib=L, host_only=True)
+    n = _first_files(C, sample_bytes)
+    offs = np.ascontiguousarray(C.offsets[:n + 1])
+    batch = _CBatch(n, C.arena.ctypes.data, offs.ctypes.data, None, None, C.path_ptrs.ctypes.data, None, None)
+    runs, res = [], None
+    for T in threads:
+        h = c.c_void_p()
+        t0 = time.time()
+        if L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), int(T), c.byref(h)) != 0:
+            raise RuntimeError("tsg_cpuref_scan: %s" % hostlib.last_error())
+        dt = time.time() - t0
+        st = _CStats()
+        L.tsg_result_stats(h, c.byref(st))
+        runs.append({"threads": int(T), "value": round(int(offs[-1]) / dt / 1e9, 6), "s": round(dt, 2),
+                     "findings": int(st.findings)})
+        if res is None:
+            res = ScanResult(sc, h)
+        else:
+            L.tsg_result_free(h)
+    nw = len(want)
+    got = res.secrets([C.path(i) for i in range(nw)], lo=0)
+    bad = sum(1 for i in range(nw) if got[i].to_dict() != want[i])
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": runs[0]["value"], "unit": "GB/s", "cores": runs[0]["threads"],
+            "kind": "port (restated reference CPU algorithm, C++)",
+            "sample": "first %d files (%.1f MB) of the same corpus, tsg_cpuref_scan (oracle/native/host_hooks.cpp: "
+                      "scanner.go:377-463 per file and rule -- bytes.ToLower + Contains gate, whole-file "
+                      "Go-regexp FindAll with the product's Go-semantics engine, same tail); %d findings"
+                      % (n, int(offs[-1]) / 1e6, runs[0]["findings"]),
+            "runs": runs, "cpu_model": cpu_model,
+            "parity_vs_oracle": {"files": nw, "mismatches": bad}}
 
 
 def parity_block(C, last_result, want):
@@ -145,12 +193,13 @@ KERNELS = [("chunk_map_kernel", "ms_chunkmap_kernel"), ("filter_kernel (K1)", "m
            ("finalize_kernel", "ms_finalize_kernel")]
 
 WORKLOADS = {
+    # (description, GB per GPU, CPU-baseline sample MB, oracle parity sample MB)
     "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
-           20.0, 32.0),
+           20.0, 64.0, 24.0),
     "c3": ("2,000 generated custom rules (trivy-secret.yaml) + 87 builtins over a %g GB synthetic corpus per "
-           "MI355X (BASELINE configs[2])", 8.0, 0.4),
+           "MI355X (BASELINE configs[2])", 8.0, 2.0, 0.4),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
-           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0),
+           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0, 0.0),
 }
 
 
@@ -161,13 +210,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--gb", type=float, default=None, help="corpus size per GPU (GB = 1e9 B)")
-    ap.add_argument("--cpu-sample-mb", type=float, default=None)
+    ap.add_argument("--cpu-sample-mb", type=float, default=None, help="CPU-baseline sample (first files)")
+    ap.add_argument("--parity-mb", type=float, default=None, help="oracle parity sample (first files)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=3, help="scans in flight (pipelined submission)")
     ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     args = ap.parse_args()
-    wl_desc, gb_default, cpu_mb_default = WORKLOADS[args.workload]
+    wl_desc, gb_default, cpu_mb_default, parity_mb_default = WORKLOADS[args.workload]
+    if args.parity_mb is None:
+        args.parity_mb = parity_mb_default
     if args.gb is None:
         args.gb = gb_default
     if args.cpu_sample_mb is None:
@@ -328,8 +380,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cores = min(16, os.cpu_count() or 1)
             if layer is None:
-                cpu, want = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), cores, tmpdir, cfg_path)
+                want, _ = oracle_sample(C, int(args.parity_mb * 1e6), cores, tmpdir, cfg_path)
                 parity = parity_block(C, last_res[0], want)
+                cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), [cores, 5], cfg_path, want)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
                 cpu = cpu_baseline_layer(sample, cores, tmpdir)

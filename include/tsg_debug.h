@@ -65,20 +65,9 @@ int tsg_debug_filter_ids(const tsg_compiled* c, const uint32_t** ids, uint32_t* 
 /* Rule i's anchor summary: "[off_lo,off_hi] lit[*][+la] ..." or "-" (no anchor). */
 const char* tsg_debug_rule_anchor(const tsg_compiled* c, uint32_t i);
 
-/* Test hook: the exact host tail (include/tsg_scanner.h) fed with whole-file
- * candidate windows instead of the GPU's, on CPU.  Not a product path. */
-struct tsg_batch;
-struct tsg_result;
-int tsg_debug_host_tail(const struct tsg_global* g, const struct tsg_batch* b, struct tsg_result** out);
-/* The same tail over caller-supplied candidates (40-B records as written by a
- * GPU run with TSG_DUMP_CANDS=<file>): profiles the exact pass without a GPU. */
-int tsg_debug_host_tail_cands(const struct tsg_global* g, const struct tsg_batch* b, const void* cands,
-                              uint64_t n_cands, struct tsg_result** out);
-
-/* A scanner without a GPU engine (tsg_scan on it fails): lets the CPU suite
- * drive the analyzer's host logic (tsg_analyzer_required, collectors). */
-struct tsg_scanner;
-int tsg_debug_scanner_host_only(const struct tsg_global* g, struct tsg_scanner** out);
+/* The CPU-only test hooks (host tail with whole-file windows, host-only
+ * scanners) and the CPU reference scan are NOT in libtsg.so: they live in the
+ * oracle's library (oracle/native/tsg_oracle.h, oracle/build/libtsg_host.so). */
 
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);

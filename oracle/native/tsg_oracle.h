@@ -1,0 +1,42 @@
+/* oracle/build/libtsg_host.so -- TEST INFRASTRUCTURE, not the product.
+ *
+ * Built from the product's host sources plus oracle/native/*.cpp by
+ * oracle/build_native.py.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load it.  It exports the whole libtsg.so C-ABI (its own
+ * copy, loaded RTLD_LOCAL) plus:
+ *
+ *   tsg_debug_host_tail / _cands   the exact host tail over whole-file / given
+ *                                  candidate windows (no GPU): checks the tail
+ *                                  against the oracle on CPU
+ *   tsg_debug_scanner_host_only    a scanner without a GPU engine (analyzer
+ *                                  host logic on CPU)
+ *   tsg_cpuref_scan                the reference CPU algorithm restated in C++
+ *                                  (pkg/fanal/secret/scanner.go:377-463: per file
+ *                                  and rule, bytes.ToLower + Contains keyword
+ *                                  gate, then whole-file regexp FindAll, then
+ *                                  the same exact tail) -- bench.py's CPU
+ *                                  baseline ("port", restated reference)
+ */
+#ifndef TSG_ORACLE_H
+#define TSG_ORACLE_H
+#include <stdint.h>
+
+#include "tsg_scanner.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_result** out);
+/* candidates: 40-B records (trivy_amd/csrc/engine.h Candidate), e.g. dumped by TSG_DUMP_CANDS */
+int tsg_debug_host_tail_cands(const tsg_global* g, const tsg_batch* b, const void* cands, uint64_t n_cands,
+                              tsg_result** out);
+int tsg_debug_scanner_host_only(const tsg_global* g, tsg_scanner** out);
+
+/* The reference algorithm on `threads` host threads (files in parallel, like
+ * the analyzer's --parallel goroutines).  Result: as tsg_scan. */
+int tsg_cpuref_scan(const tsg_global* g, const tsg_batch* b, int threads, tsg_result** out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -7,6 +7,7 @@ with 1-byte / no literals, mixed case, non-ASCII and over-long paths.
 """
 import random
 
+from oracle import hostlib
 from oracle import secret_scanner as osc
 from trivy_amd.secret import NewScanner, ParseConfig
 
@@ -31,7 +32,7 @@ def _paths(seed, n):
 
 
 def _check(cfg_path, paths):
-    sc = NewScanner(ParseConfig(cfg_path) if cfg_path else None, _host_only=True)
+    sc = NewScanner(ParseConfig(cfg_path) if cfg_path else None, lib=hostlib.lib(), host_only=True)
     o = osc.new_scanner(osc.parse_config(cfg_path) if cfg_path else None)
     for p in paths:
         assert sc.AllowPath(p) == o.allow_path(p), p

@@ -14,6 +14,8 @@ from pathlib import Path
 
 import pytest
 
+from oracle import hostlib
+
 from oracle import analyzer as oan
 from tests.corpus import make_corpus
 from tests.layers import make_layer
@@ -74,7 +76,7 @@ def test_native_transforms_vs_oracle():
 @pytest.fixture(scope="module")
 def host_analyzer():
     from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer, SecretScannerOption
-    a = SecretAnalyzer(_host_only=True)
+    a = SecretAnalyzer(lib=hostlib.lib(), host_only=True)
     a.Init(AnalyzerOptions(SecretScannerOption(str(ADIR / "testdata/skip-tests-config.yaml"))))
     return a
 
@@ -83,7 +85,7 @@ def host_analyzer():
 def test_native_required_golden(case, monkeypatch):
     from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer, SecretScannerOption, FileInfo
     monkeypatch.chdir(ADIR)
-    a = SecretAnalyzer(_host_only=True)
+    a = SecretAnalyzer(lib=hostlib.lib(), host_only=True)
     a.Init(AnalyzerOptions(SecretScannerOption("testdata/skip-tests-config.yaml")))
     assert a.Required(case["file"], FileInfo(Path(case["file"]).stat().st_size)) == case["want"]
 

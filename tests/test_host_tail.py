@@ -13,6 +13,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+from oracle import hostlib
 from oracle import secret_scanner as osc
 from tests.corpus import make_corpus
 from trivy_amd import _lib
@@ -42,9 +43,8 @@ def _assemble(cfg):
 
 
 def host_tail_scan(cfg, files):
-    L = _lib.lib()
+    L = hostlib.lib()
     _declare(L)
-    L.tsg_debug_host_tail.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_void_p)]
     rules, allow, exclude = _assemble(cfg)
     cg = CGlobal(rules, allow, exclude)
     contents = [b for _, b in files]
@@ -58,7 +58,7 @@ def host_tail_scan(cfg, files):
                     c.cast(parr, c.c_void_p).value, plen.ctypes.data, None)
     h = c.c_void_p()
     if L.tsg_debug_host_tail(c.byref(cg.g), c.byref(batch), c.byref(h)) != 0:
-        raise RuntimeError(_lib.last_error())
+        raise RuntimeError(hostlib.last_error())
     return ScanResult(_Owner(L), h).secrets([p for p, _ in files])
 
 

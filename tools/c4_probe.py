@@ -9,7 +9,8 @@ from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer  # noqa: E402
 from trivy_amd.analyzer.secret import Collector, _CTarStats  # noqa: E402
 
 layer = corpus.generate_layer(int(float(os.environ.get("GB", "4")) * 1e9))
-a = SecretAnalyzer(_host_only=True)
+from oracle import hostlib  # noqa: E402
+a = SecretAnalyzer(lib=hostlib.lib(), host_only=True)
 a.Init(AnalyzerOptions())
 coll = Collector(a, 256 << 20)
 st = _CTarStats()

@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--gb", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
-    L = _lib.lib()
+    from oracle import hostlib
+    L = hostlib.lib()
     cand = np.fromfile(args.cands, dtype=np.uint8)
     n_c = len(cand) // 40
     t = time.time()
@@ -33,14 +34,13 @@ def main():
     cg = CGlobal(builtin_rules(), builtin_allow_rules(), [])
     b = _CBatch(C.n_files, C.arena.ctypes.data, C.offsets.ctypes.data, None, None, C.path_ptrs.ctypes.data,
                 None, None)
-    L.tsg_debug_host_tail_cands.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64, c.c_void_p]
     for _ in range(args.reps):
         h = c.c_void_p()
         t = time.time()
         rc = L.tsg_debug_host_tail_cands(c.byref(cg.g), c.byref(b), cand.ctypes.data, n_c, c.byref(h))
         t1 = time.time()
         if rc != 0:
-            raise SystemExit(_lib.last_error())
+            raise SystemExit(hostlib.last_error())
         s = _CStats()
         L.tsg_result_stats(h, c.byref(s))
         L.tsg_result_free(h)

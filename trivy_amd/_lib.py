@@ -35,8 +35,11 @@ def _declare(L):
     L.tsg_go_bytes_to_lower.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p, c.c_uint64]
 
 
-def last_error():
-    e = lib().tsg_last_error()
+def last_error(L=None):
+    """Thread-local error text of library L (default libtsg.so)."""
+    L = L if L is not None else lib()
+    L.tsg_last_error.restype = ctypes.c_char_p
+    e = L.tsg_last_error()
     return e.decode("utf-8", "replace") if e else ""
 
 

@@ -155,7 +155,7 @@ class Collector:
         self._L = analyzer._L
         h = c.c_void_p()
         if self._L.tsg_collector_new(analyzer._h, int(arena_bytes), c.byref(h)) != 0:
-            raise RuntimeError("tsg_collector_new failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_collector_new failed: %s" % _lib.last_error(self._L))
         self._h = h
         self._keep = []
 
@@ -174,7 +174,7 @@ class Collector:
         addr = buf.ctypes.data if hasattr(buf, "ctypes") else c.cast(c.c_char_p(buf), c.c_void_p).value
         rc = self._L.tsg_collector_add_tar(self._h, addr, len(buf), c.byref(cur), c.byref(stats))
         if rc < 0:
-            raise ValueError("tar layer: %s" % _lib.last_error())
+            raise ValueError("tar layer: %s" % _lib.last_error(self._L))
         return rc, cur.value
 
     def files(self) -> int:
@@ -202,7 +202,7 @@ class Collector:
     def submit(self) -> "PendingBatch":
         h = c.c_void_p()
         if self._L.tsg_collector_submit(self._h, c.byref(h)) != 0:
-            raise RuntimeError("tsg_collector_submit failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_collector_submit failed: %s" % _lib.last_error(self._L))
         return PendingBatch(self, h)
 
     def reset(self):
@@ -232,7 +232,7 @@ class PendingBatch:
         rc = self.coll._L.tsg_scan_wait(self._h, c.byref(r))
         self._h = None
         if rc != 0:
-            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error(self.coll._L))
         res = ScanResult(_ScannerRef(self.coll._L), r)
         out = ([s if s.Findings else None for s in res.secrets(self.coll.paths())] if materialize
                else res.stats())
@@ -249,11 +249,12 @@ class _ScannerRef:  # what ScanResult needs of its scanner
 class SecretAnalyzer:
     """analyzer/secret.SecretAnalyzer bound to the MI355X engine."""
 
-    def __init__(self, scanner=None, configPath: str = "", device: int = 0, _host_only: bool = False):
-        self._L = _lib.lib()
+    def __init__(self, scanner=None, configPath: str = "", device: int = 0, lib=None, host_only: bool = False):
+        """lib / host_only: as trivy_amd.secret.Scanner (tests drive the host logic on CPU)."""
+        self._L = lib if lib is not None else _lib.lib()
         _declare(self._L)
         self.device = device
-        self._host_only = _host_only
+        self._host_only = host_only
         self._h = None
         self.scanner = None
         self.configPath = configPath
@@ -267,7 +268,7 @@ class SecretAnalyzer:
         self.configPath = configPath
         h = c.c_void_p()
         if self._L.tsg_analyzer_new(scanner._h, _b(configPath), c.byref(h)) != 0:
-            raise RuntimeError("tsg_analyzer_new failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_analyzer_new failed: %s" % _lib.last_error(self._L))
         self._h = h
 
     def __del__(self):
@@ -284,7 +285,7 @@ class SecretAnalyzer:
             cfg = ParseConfig(path)
         except Exception as e:  # xerrors.Errorf("secret config error: %w", err)
             raise RuntimeError("secret config error: %s" % e)
-        self._bind(NewScanner(cfg, device=self.device, _host_only=self._host_only), path)
+        self._bind(NewScanner(cfg, device=self.device, lib=self._L, host_only=self._host_only), path)
         return None
 
     def Type(self) -> str:
@@ -326,7 +327,7 @@ class SecretAnalyzer:
                 if r >= 0:
                     idx.append(k)
                 elif r != TSG_SKIPPED:
-                    raise RuntimeError("tsg_collector_add failed: %s" % _lib.last_error())
+                    raise RuntimeError("tsg_collector_add failed: %s" % _lib.last_error(self._L))
                 break
         flush()
         return out

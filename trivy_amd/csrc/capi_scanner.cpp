@@ -14,19 +14,6 @@
 #include "tsg_debug.h"
 #include "tsg_scanner.h"
 
-namespace tsg {
-void SetError(const std::string& e);
-}
-
-
-struct tsg_result {
-  tsg::BatchResult files;
-  tsg_stats stats;
-  std::string json;
-  const tsg::SecretScanner* owner;
-  std::unique_ptr<tsg::SecretScanner> debug_owner;  // tsg_debug_host_tail only
-};
-
 struct tsg_compiled {
   tsg::CompiledRules cr;
 };
@@ -84,6 +71,9 @@ class ResultReaper {
 
 namespace {
 std::string Str(const char* s) { return s ? std::string(s) : std::string(); }
+}  // namespace
+
+namespace tsg {
 
 // NULL = no regex; "" is a regex that matches everywhere (Go compiles it,
 // Regexp.UnmarshalYAML, scanner.go:75-87).
@@ -137,6 +127,13 @@ bool MakeRules(const tsg_global* g, std::vector<tsg::RuleSpec>* rules, std::stri
   return true;
 }
 
+}  // namespace tsg
+
+namespace {
+using tsg::MakeAllow;
+using tsg::MakeExclude;
+using tsg::MakeRules;
+
 void JsonStr(std::string* o, const std::string& s) {
   static const char* hex = "0123456789abcdef";
   o->push_back('"');
@@ -185,26 +182,6 @@ int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out) {
 }
 
 void tsg_scanner_free(tsg_scanner* s) { delete s; }
-
-int tsg_debug_scanner_host_only(const tsg_global* g, tsg_scanner** out) {
-  std::string err;
-  std::vector<tsg::RuleSpec> rules;
-  std::vector<tsg::AllowRuleSpec> allow;
-  std::vector<std::unique_ptr<tsg::Regex>> exclude;
-  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
-      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
-    tsg::SetError(err);
-    return -1;
-  }
-  std::unique_ptr<tsg_scanner> s(new tsg_scanner());
-  s->s.reset(new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), -1, &err));
-  if (!s->s->ok()) {
-    tsg::SetError(err.empty() ? s->s->error() : err);
-    return -2;
-  }
-  *out = s.release();
-  return 0;
-}
 
 int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len) {
   return s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len)) ? 1 : 0;
@@ -524,91 +501,3 @@ const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k) {
 }
 
 }  // extern "C"
-
-// ---- test hook: exact host tail with whole-file windows (no GPU) -----------
-// Candidates are every (file, rule with regex) whose keyword gate holds under
-// Go's bytes.ToLower, with the whole file as the start window.  This is NOT a
-// product path (tsg_scan always runs the GPU kernels first); it lets the CPU
-// test-suite check the exact tail against the oracle.
-namespace {
-int RunDebugTail(std::unique_ptr<tsg::SecretScanner> sc, const tsg_batch* b, std::vector<tsg::Candidate>* cands,
-                 tsg_result** out) {
-  tsg::BatchInput in;
-  in.n_files = b->n_files;
-  in.host_arena = b->host_arena;
-  in.host_offsets = b->host_offsets;
-  in.paths = b->paths;
-  in.path_lens = b->path_lens;
-  in.binary = b->binary;
-  std::unique_ptr<tsg_result> r(new tsg_result());
-  tsg::HostStats hs;
-  sc->HostTail(in, cands, &r->files, &hs);
-  std::memset(&r->stats, 0, sizeof(r->stats));
-  r->stats.findings = hs.findings;
-  r->stats.candidates = hs.candidates;
-  r->stats.ms_host_allow_path = hs.ms_allow;
-  r->stats.ms_host_exact = hs.ms_exact;
-  r->owner = sc.get();
-  r->debug_owner = std::move(sc);
-  *out = r.release();
-  return 0;
-}
-}  // namespace
-
-extern "C" int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_result** out) {
-  std::string err;
-  std::vector<tsg::RuleSpec> rules;
-  std::vector<tsg::AllowRuleSpec> allow;
-  std::vector<std::unique_ptr<tsg::Regex>> exclude;
-  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
-      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
-    tsg::SetError(err);
-    return -1;
-  }
-  std::unique_ptr<tsg::SecretScanner> sc(
-      new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), -1, &err));
-  if (!sc->ok()) {
-    tsg::SetError(err);
-    return -2;
-  }
-  // every (file, rule with a regex) with the whole file as its window: the
-  // tail's lazy keyword gate decides (as it does for GPU candidates)
-  std::vector<tsg::Candidate> cands;
-  for (uint32_t f = 0; f < b->n_files; f++) {
-    uint64_t fs = b->host_offsets[f], fe = b->host_offsets[f + 1];
-    for (uint32_t r = 0; r < sc->rules().size(); r++) {
-      if (!sc->compiled().regex[r]) continue;
-      cands.push_back({f, r, 0, int64_t(fe - fs), 0});
-    }
-  }
-  return RunDebugTail(std::move(sc), b, &cands, out);
-}
-
-// Host tail over caller-supplied candidates (e.g. dumped from a GPU run with
-// TSG_DUMP_CANDS): profiles the exact pass on CPU-only machines.
-extern "C" int tsg_debug_host_tail_cands(const tsg_global* g, const tsg_batch* b, const void* cands,
-                                         uint64_t n_cands, tsg_result** out) {
-  std::string err;
-  std::vector<tsg::RuleSpec> rules;
-  std::vector<tsg::AllowRuleSpec> allow;
-  std::vector<std::unique_ptr<tsg::Regex>> exclude;
-  if (!MakeRules(g, &rules, &err) || !MakeAllow(g->allow_rules, g->n_allow_rules, &allow, &err) ||
-      !MakeExclude(g->exclude_regexes, g->n_exclude_regexes, &exclude, &err)) {
-    tsg::SetError(err);
-    return -1;
-  }
-  std::unique_ptr<tsg::SecretScanner> sc(
-      new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), -1, &err));
-  if (!sc->ok()) {
-    tsg::SetError(err);
-    return -2;
-  }
-  std::vector<tsg::Candidate> cv(n_cands);
-  if (n_cands) std::memcpy(cv.data(), cands, n_cands * sizeof(tsg::Candidate));
-  for (const auto& c : cv)
-    if (c.file >= b->n_files || c.rule >= sc->rules().size()) {
-      tsg::SetError("candidate out of range");
-      return -3;
-    }
-  return RunDebugTail(std::move(sc), b, &cv, out);
-}

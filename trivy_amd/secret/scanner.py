@@ -194,23 +194,24 @@ class Scanner:
     """secret.Scanner: an assembled Global bound to one HIP device."""
 
     def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude_regexes: Sequence[str],
-                 device: int = 0, _host_only: bool = False):
+                 device: int = 0, lib=None, host_only: bool = False):
+        """lib: the C-ABI library (default libtsg.so).  host_only (tests): a scanner without a
+        GPU engine from the oracle's library (oracle/hostlib.py), whose tsg_scan fails."""
         self.Rules = list(rules)
         self.AllowRules = list(allow_rules)
         self.ExcludeRegexes = list(exclude_regexes)
-        L = _lib.lib()
+        L = lib if lib is not None else _lib.lib()
         _declare(L)
         self._L = L
         self._cg = CGlobal(rules, allow_rules, exclude_regexes)
         g = self._cg.g
         h = c.c_void_p()
-        if _host_only:  # test hook (tsg_debug_scanner_host_only): host logic only, tsg_scan fails
-            L.tsg_debug_scanner_host_only.argtypes = [c.POINTER(_CGlobal), c.POINTER(c.c_void_p)]
+        if host_only:
             rc = L.tsg_debug_scanner_host_only(c.byref(g), c.byref(h))
         else:
             rc = L.tsg_scanner_new(c.byref(g), int(device), c.byref(h))
         if rc != 0:
-            raise RuntimeError("tsg_scanner_new failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_scanner_new failed: %s" % _lib.last_error(L))
         self._h = h
 
     def __del__(self):
@@ -245,7 +246,7 @@ class Scanner:
         h = c.c_void_p()
         rc = self._L.tsg_scan_submit(self._h, c.byref(batch), c.byref(h))
         if rc != 0:
-            raise RuntimeError("tsg_scan_submit failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_scan_submit failed: %s" % _lib.last_error(self._L))
         return PendingScan(self, h, (keep, batch))
 
     def _batch(self, arena, offsets, paths, binary, dev_arena, dev_offsets):
@@ -288,7 +289,7 @@ class Scanner:
         h = c.c_void_p()
         rc = self._L.tsg_scan(self._h, c.byref(batch), c.byref(h))
         if rc != 0:
-            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error(self._L))
         return ScanResult(self, h)
 
     def table_info(self):
@@ -323,7 +324,7 @@ class PendingScan:
         self._h = None
         self._keep = None
         if rc != 0:
-            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error())
+            raise RuntimeError("tsg_scan failed: %s" % _lib.last_error(self._sc._L))
         return ScanResult(self._sc, r)
 
 
@@ -377,10 +378,11 @@ class ScanResult:
         return out
 
 
-def NewScanner(config: Optional[Config], device: int = 0, _host_only: bool = False) -> Scanner:  # scanner.go:320-364
+def NewScanner(config: Optional[Config], device: int = 0, lib=None, host_only: bool = False) -> Scanner:
+    """scanner.go:320-364."""
     b_rules, b_allow = builtin_rules(), builtin_allow_rules()
     if config is None:
-        return Scanner(b_rules, b_allow, [], device, _host_only)
+        return Scanner(b_rules, b_allow, [], device, lib, host_only)
     enabled = b_rules
     if config.EnableBuiltinRuleIDs:
         enabled = [r for r in b_rules if r.ID in config.EnableBuiltinRuleIDs]
@@ -388,4 +390,4 @@ def NewScanner(config: Optional[Config], device: int = 0, _host_only: bool = Fal
     rules = [r for r in enabled if r.ID not in config.DisableRuleIDs]
     allow = b_allow + list(config.CustomAllowRules)
     allow = [a for a in allow if a.ID not in config.DisableAllowRuleIDs]
-    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device, _host_only)
+    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device, lib, host_only)
