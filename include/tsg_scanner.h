@@ -123,8 +123,17 @@ typedef struct tsg_stats {
   /* per-kernel split of ms_gpu_total (HIP events on the engine stream) */
   uint64_t follow_hits;      /* anchor_hits (exact anchor-item matches) past the follow requirements */
   double ms_chunkmap_kernel, ms_confirm_kernel, ms_nfa_kernel, ms_finalize_kernel;
+  /* host-resident batches: copies + kernels from the first H2D to the last chunk (chunks streamed) */
+  double ms_h2d_span;
+  uint64_t h2d_chunks;
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
+
+/* Page-lock a caller's host buffer (hipHostRegister) so batches in it stream
+ * to the GPU asynchronously (two staging buffers, copies overlapping kernels):
+ * the Go caller's pinned arena pool.  Unregister before freeing it. */
+int tsg_host_register(void* p, uint64_t bytes);
+int tsg_host_unregister(void* p);
 
 /* Compiled-table facts (for reports/tests). */
 typedef struct tsg_table_info {

@@ -241,3 +241,30 @@ def test_fold_runes_in_custom_rule_items(secret, tmp_path):
         pad = "x" * rng.randint(0, 300)
         files.append(("c%02d.txt" % i, ("\n" + pad + " ").join(parts).encode()))
     assert _compare_corpus(secret, files, str(cfg)) > 100
+
+
+def test_host_batches_stream_in_chunks(secret, monkeypatch):
+    """Host-resident batches (RunHost) streamed through two staging buffers in many chunks
+    (TSG_INGEST_CHUNK_MB), pipelined submissions included, give the device-resident
+    results; the chunks really are many (h2d_chunks)."""
+    import numpy as np
+    import torch
+    from trivy_amd import corpus
+    C = corpus.generate(int(24e6), seed=corpus.SEED + 3)
+    d_arena = torch.from_numpy(C.arena).to("cuda:0")
+    d_offs = torch.from_numpy(C.offsets.view(np.int64)).to("cuda:0")
+    s = secret.NewScanner(None)
+    want = s.scan_arena(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(),
+                        dev_offsets=d_offs.data_ptr()).raw()
+    monkeypatch.setenv("TSG_INGEST_CHUNK_MB", "2")
+    s2 = secret.NewScanner(None)
+    unregister = secret.HostRegister(C.arena)
+    try:
+        r = s2.scan_arena(C.arena, C.offsets, C.path_ptrs)
+        assert r.stats()["h2d_chunks"] >= 10
+        assert r.raw() == want
+        pend = [s2.scan_arena_async(C.arena, C.offsets, C.path_ptrs) for _ in range(3)]
+        for p in pend:
+            assert p.wait().raw() == want
+    finally:
+        unregister()

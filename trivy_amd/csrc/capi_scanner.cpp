@@ -183,6 +183,26 @@ int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out) {
 
 void tsg_scanner_free(tsg_scanner* s) { delete s; }
 
+int tsg_host_register(void* p, uint64_t bytes) {
+  if (!p || !bytes) return 0;
+  const hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterDefault);
+  if (e != hipSuccess) {
+    tsg::SetError(std::string("hipHostRegister: ") + hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+int tsg_host_unregister(void* p) {
+  if (!p) return 0;
+  const hipError_t e = hipHostUnregister(p);
+  if (e != hipSuccess) {
+    tsg::SetError(std::string("hipHostUnregister: ") + hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len) {
   return s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len)) ? 1 : 0;
 }
@@ -258,6 +278,8 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.ms_confirm_kernel = gs.ms_confirm;
   st.ms_nfa_kernel = gs.ms_verify;
   st.ms_finalize_kernel = gs.ms_finalize;
+  st.ms_h2d_span = gs.ms_h2d_span;
+  st.h2d_chunks = gs.h2d_chunks;
   *out = r.release();
   return 0;
 }

@@ -32,6 +32,8 @@ struct BatchStats {
   uint64_t follow_hits = 0;     // anchor hits past the follow requirements + fold-kernel hits (the NFA runs on these)
   float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
   float ms_finalize = 0, ms_chunkmap = 0;
+  float ms_h2d_span = 0;  // RunHost: first copy issued -> last chunk done (the ingest-inclusive GPU time)
+  uint64_t h2d_chunks = 0;
   bool hit_overflow = false, cand_overflow = false;
 };
 
@@ -50,8 +52,8 @@ class GpuEngine {
   bool Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
            std::vector<Candidate>* cands, BatchStats* st);
 
-  // Host-pointer convenience: stages host arena + offsets through device
-  // buffers owned by the engine (PCIe-inclusive path).
+  // Host-resident batch (PCIe-inclusive path): streamed in chunks through two
+  // device staging buffers, copies overlapping the previous chunk's kernels.
   bool RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                std::vector<Candidate>* cands, BatchStats* st);
 
@@ -104,8 +106,13 @@ class GpuEngine {
   uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
                                     // [7] flagged-block records [8] record overflow
                                     // [9] fold sites [10] fold-site overflow
-  void* d_arena_stage_ = nullptr; size_t cap_arena_stage_ = 0;
-  void* d_off_stage_ = nullptr; size_t cap_off_stage_ = 0;
+  // host-batch streaming (RunHost): two staging buffers, a copy stream
+  hipStream_t copy_stream_ = nullptr;
+  hipEvent_t ev_copied_[2] = {}, ev_h2d_[2] = {};
+  void* d_stage_[2] = {}; size_t cap_stage_[2] = {};
+  void* d_stage_off_[2] = {}; size_t cap_stage_off_[2] = {};
+  uint64_t* h_off_[2] = {}; size_t cap_h_off_[2] = {};  // pinned, rebased chunk offsets
+  uint64_t chunk_bytes_ = uint64_t(1) << 30;             // TSG_INGEST_CHUNK_MB
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
   uint32_t* d_item_diag_ = nullptr;   // TSG_DIAG_ITEMS=<file>: per-item counters dumped after each run
   std::string item_diag_path_;

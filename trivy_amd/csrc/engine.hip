@@ -1075,10 +1075,15 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     err_ = "hipSetDevice failed (no HIP device?)";
     return;
   }
-  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking) != hipSuccess) {
     err_ = "hipStreamCreate failed";
     return;
   }
+  for (auto& e : ev_copied_) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : ev_h2d_) hipEventCreate(&e);
+  if (const char* cm = std::getenv("TSG_INGEST_CHUNK_MB")) chunk_bytes_ = uint64_t(std::atoll(cm)) << 20;
+  if (chunk_bytes_ < (uint64_t(1) << 20)) chunk_bytes_ = uint64_t(1) << 20;
   for (auto& e : ev_) hipEventCreate(&e);
   if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
   if (const char* dc = std::getenv("TSG_DIAG_CONFIRM")) diag_confirm_ = uint32_t(std::atoi(dc));
@@ -1212,11 +1217,18 @@ GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
   void* ps[] = {d_anchor_req_, d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
-                d_flags_, d_hits_, d_cands_, d_arena_stage_, d_off_stage_};
+                d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1]};
   for (void* p : ps)
     if (p) hipFree(p);
   for (auto& e : ev_)
     if (e) hipEventDestroy(e);
+  for (auto& e : ev_copied_)
+    if (e) hipEventDestroy(e);
+  for (auto& e : ev_h2d_)
+    if (e) hipEventDestroy(e);
+  for (auto* h : h_off_)
+    if (h) hipHostFree(h);
+  if (copy_stream_) hipStreamDestroy(copy_stream_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -1230,16 +1242,101 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
   return true;
 }
 
+// Host-resident batches (the analyzer's pinned arenas, a caller's registered
+// pool): the files are cut into chunks of at most chunk_bytes_ at file
+// boundaries and streamed through two device staging buffers.  The copy
+// stream moves chunk k+1 (arena + rebased offsets) while the kernels of chunk
+// k run on the scan stream (which waits on the chunk's copy event); Run()
+// returns only after chunk k's kernels finished, so the buffer it used is
+// free when chunk k+2's copy is issued.  Pinned host memory is required for
+// the copies to be asynchronous (hipHostMalloc / tsg_host_register).
 bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                         std::vector<Candidate>* cands, BatchStats* st) {
   HIP_OK(hipSetDevice(device_));
-  if (!Ensure(&d_arena_stage_, &cap_arena_stage_, n_bytes + 64)) return false;
-  if (!Ensure(&d_off_stage_, &cap_off_stage_, (size_t(n_files) + 1) * 8)) return false;
-  if (n_bytes) HIP_OK(hipMemcpyAsync(d_arena_stage_, h_arena, n_bytes, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemsetAsync(static_cast<uint8_t*>(d_arena_stage_) + n_bytes, 0, 64, stream_));
-  HIP_OK(hipMemcpyAsync(d_off_stage_, h_offsets, (size_t(n_files) + 1) * 8, hipMemcpyHostToDevice, stream_));
-  return Run(static_cast<const uint8_t*>(d_arena_stage_), n_bytes, static_cast<const uint64_t*>(d_off_stage_),
-             n_files, cands, st);
+  cands->clear();
+  BatchStats local;
+  if (!st) st = &local;
+  *st = BatchStats();
+  st->bytes = n_bytes;
+  st->files = n_files;
+  if (n_files == 0) return true;
+  // chunk boundaries (file indices)
+  std::vector<uint32_t> cut{0};
+  for (uint32_t f = 0; f < n_files; f++) {
+    const uint64_t c0 = h_offsets[cut.back()];
+    if (f > cut.back() && h_offsets[f + 1] - c0 > chunk_bytes_) cut.push_back(f);
+  }
+  cut.push_back(n_files);
+  const size_t n_chunks = cut.size() - 1;
+  uint64_t max_bytes = 0, max_files = 0;
+  for (size_t k = 0; k < n_chunks; k++) {
+    max_bytes = std::max<uint64_t>(max_bytes, h_offsets[cut[k + 1]] - h_offsets[cut[k]]);
+    max_files = std::max<uint64_t>(max_files, cut[k + 1] - cut[k]);
+  }
+  for (int b = 0; b < 2 && b < int(n_chunks); b++) {
+    if (!Ensure(&d_stage_[b], &cap_stage_[b], max_bytes + 64) ||
+        !Ensure(&d_stage_off_[b], &cap_stage_off_[b], (max_files + 1) * 8))
+      return false;
+    if (cap_h_off_[b] < max_files + 1) {
+      if (h_off_[b]) hipHostFree(h_off_[b]);
+      h_off_[b] = nullptr;
+      cap_h_off_[b] = 0;
+      HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&h_off_[b]), (max_files + 1) * 8, hipHostMallocDefault));
+      cap_h_off_[b] = max_files + 1;
+    }
+  }
+  auto copy = [&](size_t k) -> bool {  // chunk k -> staging buffer k % 2, on the copy stream
+    const int b = int(k % 2);
+    const uint32_t f0 = cut[k], f1 = cut[k + 1];
+    const uint64_t a = h_offsets[f0], e = h_offsets[f1];
+    for (uint32_t f = f0; f <= f1; f++) h_off_[b][f - f0] = h_offsets[f] - a;
+    uint8_t* d = static_cast<uint8_t*>(d_stage_[b]);
+    if (e > a) HIP_OK(hipMemcpyAsync(d, h_arena + a, e - a, hipMemcpyHostToDevice, copy_stream_));
+    HIP_OK(hipMemsetAsync(d + (e - a), 0, 64, copy_stream_));
+    HIP_OK(hipMemcpyAsync(d_stage_off_[b], h_off_[b], (size_t(f1 - f0) + 1) * 8, hipMemcpyHostToDevice,
+                          copy_stream_));
+    HIP_OK(hipEventRecord(ev_copied_[b], copy_stream_));
+    return true;
+  };
+  HIP_OK(hipEventRecord(ev_h2d_[0], copy_stream_));
+  if (!copy(0)) return false;
+  std::vector<Candidate> part;
+  for (size_t k = 0; k < n_chunks; k++) {
+    const int b = int(k % 2);
+    // h_off_[b ^ 1] was read by chunk k-1's offsets copy; that copy is done
+    // before chunk k-1's kernels ran (the scan stream waited on it)
+    if (k + 1 < n_chunks && !copy(k + 1)) return false;
+    HIP_OK(hipStreamWaitEvent(stream_, ev_copied_[b], 0));
+    const uint32_t f0 = cut[k], f1 = cut[k + 1];
+    BatchStats cs;
+    if (!Run(static_cast<const uint8_t*>(d_stage_[b]), h_offsets[f1] - h_offsets[f0],
+             static_cast<const uint64_t*>(d_stage_off_[b]), f1 - f0, &part, &cs))
+      return false;
+    for (auto c : part) {
+      c.file += f0;
+      cands->push_back(c);
+    }
+    st->hits += cs.hits;
+    st->follow_hits += cs.follow_hits;
+    st->candidates += cs.candidates;
+    st->special_files += cs.special_files;
+    st->flagged_blocks += cs.flagged_blocks;
+    st->hit_overflow = st->hit_overflow || cs.hit_overflow;
+    st->cand_overflow = st->cand_overflow || cs.cand_overflow;
+    st->ms_scan += cs.ms_scan;
+    st->ms_confirm += cs.ms_confirm;
+    st->ms_careful += cs.ms_careful;
+    st->ms_verify += cs.ms_verify;
+    st->ms_fullscan += cs.ms_fullscan;
+    st->ms_finalize += cs.ms_finalize;
+    st->ms_chunkmap += cs.ms_chunkmap;
+    st->ms_total += cs.ms_total;
+  }
+  HIP_OK(hipEventRecord(ev_h2d_[1], copy_stream_));
+  HIP_OK(hipEventSynchronize(ev_h2d_[1]));
+  hipEventElapsedTime(&st->ms_h2d_span, ev_h2d_[0], ev_h2d_[1]);
+  st->h2d_chunks = n_chunks;
+  return true;
 }
 
 bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,

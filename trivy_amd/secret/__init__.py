@@ -13,8 +13,8 @@ There is no CPU fallback: constructing a Scanner without a HIP device raises.
 """
 from .config import (AllowRule, Config, ExcludeBlock, Rule, ParseConfig, convert_severity,
                      builtin_rules, builtin_allow_rules)
-from .scanner import (ScanArgs, Scanner, NewScanner, Secret, SecretFinding, Code, Line)
+from .scanner import (ScanArgs, Scanner, NewScanner, Secret, SecretFinding, Code, Line, HostRegister)
 
 __all__ = ["AllowRule", "Config", "ExcludeBlock", "Rule", "ParseConfig", "convert_severity",
            "builtin_rules", "builtin_allow_rules", "ScanArgs", "Scanner", "NewScanner", "Secret",
-           "SecretFinding", "Code", "Line"]
+           "SecretFinding", "Code", "Line", "HostRegister"]

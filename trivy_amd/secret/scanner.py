@@ -52,7 +52,8 @@ class _CStats(c.Structure):
                [("flagged_blocks", c.c_uint64), ("ms_careful_kernel", c.c_double),
                 ("follow_hits", c.c_uint64)] + \
                [(n, c.c_double) for n in ("ms_chunkmap_kernel", "ms_confirm_kernel", "ms_nfa_kernel",
-                                          "ms_finalize_kernel")]
+                                          "ms_finalize_kernel", "ms_h2d_span")] + \
+               [("h2d_chunks", c.c_uint64)]
 
 
 class _CTableInfo(c.Structure):
@@ -79,6 +80,8 @@ def _declare(L):
     L.tsg_scanner_table_info.argtypes = [c.c_void_p, c.POINTER(_CTableInfo)]
     L.tsg_scanner_rule_anchor.argtypes = [c.c_void_p, c.c_uint32]
     L.tsg_scanner_rule_anchor.restype = c.c_char_p
+    L.tsg_host_register.argtypes = [c.c_void_p, c.c_uint64]
+    L.tsg_host_unregister.argtypes = [c.c_void_p]
     L._tsg_scanner_declared = True
 
 
@@ -376,6 +379,16 @@ class ScanResult:
                                             Code=Code(Lines=lines), Match=_s(f["Match"])))
                 out.append(Secret(FilePath=path, Findings=fs))
         return out
+
+
+def HostRegister(buf, lib=None):
+    """Page-lock a numpy buffer (tsg_host_register) so host-resident batches in it stream
+    asynchronously to the GPU; returns an unregister callable."""
+    L = lib if lib is not None else _lib.lib()
+    _declare(L)
+    if L.tsg_host_register(buf.ctypes.data, buf.nbytes) != 0:
+        raise RuntimeError("tsg_host_register failed: %s" % _lib.last_error(L))
+    return lambda: L.tsg_host_unregister(buf.ctypes.data)
 
 
 def NewScanner(config: Optional[Config], device: int = 0, lib=None, host_only: bool = False) -> Scanner:
