@@ -1,0 +1,51 @@
+"""Image-config secret analyzer (pkg/fanal/analyzer/imgconf/secret/secret.go:39-62).
+
+CPU: the MarshalIndent restatement scanned by the oracle reproduces the
+reference's golden cases (tests/golden/imgconf_cases.json, transcribed from
+secret_test.go:15-109).  GPU: the analyzer through the engine, field for field.
+"""
+import json
+from pathlib import Path
+
+import pytest
+
+from oracle import secret_scanner as osc
+from trivy_amd.analyzer.imgconf import ConfigAnalysisInput, MarshalIndentConfigFile
+
+CASES = json.loads((Path(__file__).resolve().parent / "golden/imgconf_cases.json").read_text())["cases"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_marshal_and_oracle_match_golden(case):
+    if case["config"] is None:
+        assert case["want"] is None
+        return
+    b = MarshalIndentConfigFile(case["config"], "  ", "")
+    assert b.startswith(b"{\n  \"architecture\": \"\",\n  \"created\": \"0001-01-01T00:00:00Z\",")
+    got = osc.new_scanner(None).scan("config.json", b)
+    if case["want"] is None:
+        assert not got["Findings"]
+    else:
+        assert got == case["want"]["Secret"]
+
+
+def test_marshal_shapes():
+    b = MarshalIndentConfigFile({"architecture": "amd64", "os": "linux",
+                                 "rootfs": {"type": "layers", "diff_ids": ["sha256:ab"]},
+                                 "config": {"Labels": {"b": "<x>", "a": "&"}, "Volumes": {"/data": {}},
+                                            "Cmd": ["sh"], "Tty": True}}).decode()
+    assert '"a": "\\u0026"' in b and '"b": "\\u003cx\\u003e"' in b  # HTML-safe, sorted map keys
+    assert '"/data": {}' in b and '"Tty": true' in b
+    assert b.index('"Cmd"') < b.index('"Labels"') < b.index('"Tty"') < b.index('"Volumes"')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_imgconf_analyzer_golden(case):
+    from trivy_amd.analyzer.imgconf import SecretAnalyzer
+    a = SecretAnalyzer("")
+    got = a.Analyze(ConfigAnalysisInput(Config=case["config"]))
+    if case["want"] is None:
+        assert got is None
+    else:
+        assert got.Secret.to_dict() == case["want"]["Secret"]

@@ -126,3 +126,29 @@ def test_two_rank_gpu_scan_matches_single_process(tmp_path):
     want = _oracle_sorted(_files(seed, n))
     assert len(want) > 5
     assert got == want
+
+
+@pytest.mark.gpu
+def test_two_scanners_one_process_concurrent():
+    """One process, two Scanners (device ids 0 and 0 on the 1-GPU box; 0 and 1 on a node),
+    shards scanned concurrently, merged and sorted as AnalysisResult.Sort vs the oracle."""
+    import torch
+    from oracle import secret_scanner as osc
+    import trivy_amd.secret as secret
+    from trivy_amd.analyzer.secret import AnalysisResult
+    from trivy_amd.shard import scan_devices
+    n_dev = torch.cuda.device_count()
+    scanners = [secret.NewScanner(None, device=0), secret.NewScanner(None, device=1 if n_dev > 1 else 0)]
+    files = [(p, b.replace(b"\r", b"")) for p, b in make_corpus(61, 240)]
+    got = scan_devices(files, scanners)
+    o = osc.new_scanner(None)
+    want = AnalysisResult()
+    for p, b in files:
+        r = o.scan(p, b)
+        if r["Findings"]:
+            want.Secrets.append(r)
+    want.Secrets.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
+    for s in want.Secrets:
+        s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
+    assert [s.to_dict() for s in got.Secrets] == want.Secrets
+    assert len(got.Secrets) > 5

@@ -79,3 +79,30 @@ def scan_sharded(files: Sequence[Tuple[str, bytes]], scan: Callable[[Sequence[Tu
             if s.Findings:
                 res.Secrets.append(s)
     return gather_results(res, dst=dst, group=group)
+
+
+def scan_devices(files: Sequence[Tuple[str, bytes]], scanners: Sequence) -> AnalysisResult:
+    """One process, one Scanner per device (the shape of a Go drop-in: a scanner per
+    GPU behind one analyzer): the LPT shards of `files` are
+    submitted to the scanners concurrently (tsg_scan_submit; each device's GPU
+    phase and host tail run on their own threads), then the secrets with
+    findings are merged and sorted as AnalysisResult.Merge/Sort do
+    (analyzer.go:251-301, :225-234)."""
+    shards = shard_files([len(b) for _, b in files], len(scanners))
+    pending = []
+    for sc, shard in zip(scanners, shards):
+        if len(shard) == 0:
+            continue
+        contents = [files[i][1] for i in shard]
+        offs = np.zeros(len(contents) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(x) for x in contents], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+        paths = [files[i][0] for i in shard]
+        pending.append((sc.scan_arena_async(arena, offs, paths), paths))
+    out = AnalysisResult()
+    for p, paths in pending:
+        for s in p.wait().secrets(paths):
+            if s.Findings:
+                out.Merge(AnalysisResult(Secrets=[s]))
+    out.Sort()
+    return out
