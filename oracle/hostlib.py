@@ -9,7 +9,8 @@ import ctypes as c
 import os
 from pathlib import Path
 
-_PATH = Path(__file__).resolve().parent / "build" / "libtsg_host.so"
+# TSG_HOSTLIB: an alternative build of the same library (tools/sanitize.sh: ASan/UBSan, TSan)
+_PATH = Path(os.environ.get("TSG_HOSTLIB") or Path(__file__).resolve().parent / "build" / "libtsg_host.so")
 _lib = None
 
 

@@ -1,0 +1,86 @@
+"""Host-side concurrency of the exact tail (CPU; the sanitizer runs drive this file).
+
+The tail's worker pool (parallel.h), concurrent scans on one scanner and the
+reference CPU algorithm's file fan-out must give the sequential results.
+tools/sanitize.sh runs these (and the host-tail / analyzer / allow-path tests)
+against ASan+UBSan and TSan builds of the host library.
+"""
+import ctypes as c
+import threading
+
+import numpy as np
+
+from oracle import hostlib
+from tests.corpus import make_corpus
+from trivy_amd.secret import NewScanner
+from trivy_amd.secret.scanner import ScanResult, _CBatch, _declare
+
+
+def _batch(files):
+    contents = [b for _, b in files]
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+    pb = [p.encode() for p, _ in files]
+    parr = (c.c_char_p * len(pb))(*pb)
+    plen = np.array([len(p) for p in pb], dtype=np.uint64)
+    keep = (arena, offs, parr, plen)
+    return keep, _CBatch(len(files), arena.ctypes.data, offs.ctypes.data, None, None,
+                         c.cast(parr, c.c_void_p).value, plen.ctypes.data, None)
+
+
+def _cpuref(sc, batch, threads):
+    L = hostlib.lib()
+    h = c.c_void_p()
+    assert L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), threads, c.byref(h)) == 0, hostlib.last_error()
+    return ScanResult(sc, h).raw()
+
+
+def test_cpuref_threads_agree():
+    L = hostlib.lib()
+    _declare(L)
+    sc = NewScanner(None, lib=L, host_only=True)
+    files = [(p, b.replace(b"\r", b"")) for p, b in make_corpus(71, 120)]
+    keep, batch = _batch(files)
+    one = _cpuref(sc, batch, 1)
+    assert _cpuref(sc, batch, 8) == one
+    assert sum(len(f["findings"]) for f in one) > 5
+
+
+def test_concurrent_host_tails():
+    """Several threads running the reference scan on one scanner at once (shared pool)."""
+    L = hostlib.lib()
+    _declare(L)
+    sc = NewScanner(None, lib=L, host_only=True)
+    batches = [_batch([(p, b.replace(b"\r", b"")) for p, b in make_corpus(80 + k, 60)]) for k in range(4)]
+    want = [_cpuref(sc, b, 1) for _, b in batches]
+    got = [None] * len(batches)
+
+    def run(i):
+        got[i] = _cpuref(sc, batches[i][1], 4)
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(batches))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert got == want
+
+
+def test_submit_without_gpu_reports_error():
+    """tsg_scan_submit / tsg_scan_wait on a host-only scanner: the scan thread fails cleanly."""
+    L = hostlib.lib()
+    _declare(L)
+    sc = NewScanner(None, lib=L, host_only=True)
+    files = [(p, b) for p, b in make_corpus(90, 10)]
+    contents = [b for _, b in files]
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+    pend = [sc.scan_arena_async(arena, offs, [p for p, _ in files]) for _ in range(3)]
+    for p in pend:
+        try:
+            p.wait()
+        except RuntimeError as e:
+            assert "no GPU engine" in str(e)
+        else:
+            raise AssertionError("scan without a GPU engine succeeded")
