@@ -23,6 +23,8 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <string>
+#include <thread>
 
 #include "engine.h"
 #include "filter.h"
@@ -1249,7 +1251,11 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
 // k run on the scan stream (which waits on the chunk's copy event); Run()
 // returns only after chunk k's kernels finished, so the buffer it used is
 // free when chunk k+2's copy is issued.  Pinned host memory is required for
-// the copies to be asynchronous (hipHostMalloc / tsg_host_register).
+// the copies to be asynchronous (hipHostMalloc / tsg_host_register).  The
+// copies are issued from a helper thread: on this runtime a 1-GiB
+// hipMemcpyAsync from registered memory returns only once the transfer is
+// done (measured, profiles/r02_ingest_trace_*), which would otherwise keep the
+// scan thread from launching chunk k's kernels during chunk k+1's copy.
 bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                         std::vector<Candidate>* cands, BatchStats* st) {
   HIP_OK(hipSetDevice(device_));
@@ -1286,6 +1292,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     }
   }
   auto copy = [&](size_t k) -> bool {  // chunk k -> staging buffer k % 2, on the copy stream
+    if (hipSetDevice(device_) != hipSuccess) return false;
     const int b = int(k % 2);
     const uint32_t f0 = cut[k], f1 = cut[k + 1];
     const uint64_t a = h_offsets[f0], e = h_offsets[f1];
@@ -1299,19 +1306,33 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     return true;
   };
   HIP_OK(hipEventRecord(ev_h2d_[0], copy_stream_));
-  if (!copy(0)) return false;
+  // copy(k) on the helper thread; joined before chunk k's kernels are queued
+  std::string copy_err;
+  auto start_copy = [&](size_t k) {
+    return std::thread([&, k] {
+      if (!copy(k) && copy_err.empty()) copy_err = err_.empty() ? "chunk copy failed" : err_;
+    });
+  };
+  std::thread copier = start_copy(0);
   std::vector<Candidate> part;
   for (size_t k = 0; k < n_chunks; k++) {
     const int b = int(k % 2);
-    // h_off_[b ^ 1] was read by chunk k-1's offsets copy; that copy is done
-    // before chunk k-1's kernels ran (the scan stream waited on it)
-    if (k + 1 < n_chunks && !copy(k + 1)) return false;
+    copier.join();  // chunk k's copy is queued (and its event recorded)
+    if (!copy_err.empty()) {
+      err_ = copy_err;
+      return false;
+    }
+    // chunk k+1 goes to the other buffer, last used by chunk k-1 (whose
+    // kernels are done: Run returned); its offsets staging too
+    if (k + 1 < n_chunks) copier = start_copy(k + 1);
     HIP_OK(hipStreamWaitEvent(stream_, ev_copied_[b], 0));
     const uint32_t f0 = cut[k], f1 = cut[k + 1];
     BatchStats cs;
     if (!Run(static_cast<const uint8_t*>(d_stage_[b]), h_offsets[f1] - h_offsets[f0],
-             static_cast<const uint64_t*>(d_stage_off_[b]), f1 - f0, &part, &cs))
+             static_cast<const uint64_t*>(d_stage_off_[b]), f1 - f0, &part, &cs)) {
+      if (copier.joinable()) copier.join();
       return false;
+    }
     for (auto c : part) {
       c.file += f0;
       cands->push_back(c);
