@@ -219,6 +219,9 @@ WORKLOADS = {
            20.0, 64.0, 24.0),
     "c3": ("2,000 generated custom rules (trivy-secret.yaml) + 87 builtins over a %g GB synthetic corpus per "
            "MI355X (BASELINE configs[2])", 8.0, 2.0, 0.4),
+    "c3u": ("C3 variant: 2,000 generated custom rules of which ~10 %% have no literal anchor (keyword-gated "
+            "full scan) + 87 builtins over a %g GB synthetic corpus per MI355X (BASELINE configs[2], VERDICT r01 #7)",
+            8.0, 2.0, 0.4),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
            "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0, 0.0),
 }
@@ -267,8 +270,8 @@ def main():
     cfg_path = None
     t_gen = time.time()
     C = layer = None
-    if args.workload == "c3":
-        y, samples = corpus.c3_rules()
+    if args.workload in ("c3", "c3u"):
+        y, samples = corpus.c3_rules(unanchored_share=0.1 if args.workload == "c3u" else 0.0)
         cfg_path = os.path.join(tmpdir, "tsg-bench-c3-%d.yaml" % rank)
         with open(cfg_path, "w") as f:
             f.write(y)
@@ -362,12 +365,13 @@ def main():
     gpu_ms = avg("ms_gpu_total")
     scan_ms = kernels["filter_kernel (K1)"]
     breakdown = {k: round(avg(k), 3) for _, k in KERNELS}
-    breakdown.update({k: round(avg(k), 3) for k in ("ms_gpu_total", "ms_host_gpu_phase", "ms_host_exact")})
+    breakdown.update({k: round(avg(k), 3) for k in ("ms_fullscan_kernel", "ms_gpu_total", "ms_host_gpu_phase",
+                                                     "ms_host_exact")})
     if layer is None:
         n_bytes, n_files = C.n_bytes, C.n_files
         arena_bytes = n_bytes
-        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "candidates",
-                                            "special_files", "findings")}
+        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs",
+                                            "candidates", "special_files", "findings")}
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
                         "resident": "host (page-locked), H2D in the timed region" if args.ingest
@@ -442,7 +446,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic generator, seed 0x5EC2E7+rank; planted builtin-rule secrets%s)"
-                    % (" and generated-rule samples" if args.workload == "c3" else ""),
+                    % (" and generated-rule samples" if args.workload in ("c3", "c3u") else ""),
             "config": dict({"workload": wl_desc % args.gb, "workload_id": args.workload,
                             "parallelism": "files sharded, dp%d" % world,
                             "rules_compile_s": round(t_compile, 2)}, **config_extra),

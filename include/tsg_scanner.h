@@ -126,6 +126,7 @@ typedef struct tsg_stats {
   /* host-resident batches: copies + kernels from the first H2D to the last chunk (chunks streamed) */
   double ms_h2d_span;
   uint64_t h2d_chunks;
+  uint64_t fullscan_pairs;   /* (file, unanchored rule) pairs with an open keyword gate, NFA-scanned */
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 

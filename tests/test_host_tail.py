@@ -144,3 +144,21 @@ def test_host_tail_c3_generated_rules(tmp_path):
         assert g.to_dict() == want, path
         n += len(want["Findings"] or [])
     assert n > 10
+
+
+def test_host_tail_c3u_unanchored_rules(tmp_path):
+    """The exact tail with the C3u rules (10 % without a literal anchor) vs the oracle."""
+    from trivy_amd.corpus import c3_rules
+    from tests.test_gpu_parity import _c3_files
+    y, samples = c3_rules(unanchored_share=0.1)
+    p = tmp_path / "trivy-secret.yaml"
+    p.write_text(y)
+    files = _c3_files([s for s in samples if s.startswith(b"kwu")], 29, 30)
+    got = host_tail_scan(ParseConfig(str(p)), files)
+    o = osc.new_scanner(osc.parse_config(str(p)))
+    n = 0
+    for (path, b), g in zip(files, got):
+        want = o.scan(path, b)
+        assert g.to_dict() == want, path
+        n += len(want["Findings"] or [])
+    assert n > 5

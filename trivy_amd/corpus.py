@@ -70,20 +70,36 @@ def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=Non
 _C3_OPS = ["=", ">", ":=", "||:", "<=", "=>", ":"]
 
 
-def c3_rules(n_rules=2000, seed=SEED, planted_share=0.10):
+def c3_rules(n_rules=2000, seed=SEED, planted_share=0.10, unanchored_share=0.0):
     """A trivy-secret.yaml text with n_rules custom rules and planted sample matches.
 
     60 %: generic assignment form (secret group), 40 %: literal-prefix token form;
     secret length L in [16, 64]; 1-3 keywords (4-12 chars, the first being the
-    rule's literal); samples for `planted_share` of the rules.  Returns
-    (yaml_text, [sample bytes])."""
+    rule's literal); samples for `planted_share` of the rules.  With
+    unanchored_share > 0 (the "C3u" variant) that share of
+    the rules has no literal at a bounded offset -- a token of classes only,
+    gated by its keyword -- so the engine full-scans the files where the gate is
+    open.  Returns (yaml_text, [sample bytes])."""
     import random
     rng = random.Random(seed ^ 0xC3)
     alnum = "abcdefghijklmnopqrstuvwxyz0123456789"
     lines = ["rules:"]
     samples = []
+    urng = random.Random(seed ^ 0xC3A)
     for i in range(n_rules):
         L = rng.randint(16, 64)
+        if unanchored_share and urng.random() < unanchored_share:
+            kw = "kwu%04d" % i
+            rx = r"(?i)\b[g-z]{3}[0-9]{3}[._-][a-z0-9]{%d}\b" % (L // 2)
+            lines += ["  - id: c3-unanchored-%04d" % i, "    category: Generated", "    title: Unanchored rule %d" % i,
+                      "    severity: MEDIUM", "    regex: '%s'" % rx, "    keywords: [%s]" % kw]
+            if urng.random() < planted_share * 3:
+                for _ in range(3):
+                    tok = "".join(urng.choice("ghijklmnopqrstuvwxyz") for _ in range(3)) + \
+                          "".join(urng.choice("0123456789") for _ in range(3)) + urng.choice("._-") + \
+                          "".join(urng.choice(alnum) for _ in range(L // 2))
+                    samples.append(("%s = %s" % (kw, tok)).encode())
+            continue
         generic = rng.random() < 0.6
         lit = ("kw%04d" % i) if generic else ("pfx%04d_" % i)
         kws = [lit] + ["".join(rng.choice(alnum) for _ in range(rng.randint(4, 12)))

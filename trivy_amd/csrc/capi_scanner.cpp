@@ -280,6 +280,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.ms_finalize_kernel = gs.ms_finalize;
   st.ms_h2d_span = gs.ms_h2d_span;
   st.h2d_chunks = gs.h2d_chunks;
+  st.fullscan_pairs = gs.fullscan_tasks;
   *out = r.release();
   return 0;
 }

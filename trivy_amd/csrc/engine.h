@@ -114,6 +114,8 @@ class GpuEngine {
   uint64_t* h_off_[2] = {}; size_t cap_h_off_[2] = {};  // pinned, rebased chunk offsets
   uint64_t chunk_bytes_ = uint64_t(1) << 30;             // TSG_INGEST_CHUNK_MB
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
+  uint32_t fs_chunk_ = 65536;         // TSG_FULLSCAN_CHUNK: full-scan bytes per lane (min)
+  hipEvent_t ev_fs_ = nullptr;
   uint32_t* d_item_diag_ = nullptr;   // TSG_DIAG_ITEMS=<file>: per-item counters dumped after each run
   std::string item_diag_path_;
 };

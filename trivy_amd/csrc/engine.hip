@@ -284,6 +284,7 @@ struct NfaParams {
   uint32_t cand_cap;
   const uint32_t* fullscan_rules;
   uint32_t n_fullscan_rules;
+  uint32_t fs_chunk;       // full-scan chunk bytes per lane (min; files of > 64 chunks use larger ones)
 };
 
 
@@ -992,20 +993,140 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
   }
 }
 
-// Unanchored rules (no literal at a bounded offset): NFA with injection at
-// every byte of every file; an accept makes the whole file the window.
+// Unanchored rules (no literal at a bounded offset): the relaxed NFA with
+// injection at every byte must find out whether any position of the file
+// accepts (then the whole file is the candidate window).
+//
+// Work: only (file, rule) pairs whose keyword gate can be open (the GPU
+// keyword bits are final here; scanner.go:409 skips the rest), one wave per
+// pair.  A file is cut into <= 64 chunks, one per lane; every lane runs its
+// chunk from the empty state, then the chunk entry states are iterated to the
+// fixpoint: lane c re-runs its chunk from lane c-1's exit state whenever that
+// state gained bits (shift-and is monotone, so exit states only grow and the
+// sequential result is reached; a state that dies stops mattering at once).
+// Any accept ends the pair.  More than kFsMaxRounds re-runs: the pair is
+// emitted unverified (a candidate is always safe -- the host pass is exact).
+constexpr int kFsMaxRounds = 6;
+
+template <int W>
+__device__ bool nfa_chunk(const uint8_t* __restrict arena, uint64_t a, uint64_t b, uint64_t* D,
+                          const uint64_t* __restrict tab) {  // arena [a, b), injection everywhere
+  uint64_t O[W], Lp[W], F[W];
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    O[w] = tab[w];
+    Lp[w] = tab[W + w];
+    F[w] = tab[2 * W + w];
+  }
+  const uint64_t* B = tab + 3 * W;
+  uint4 buf = make_uint4(0, 0, 0, 0);
+  uint64_t buf_at = ~uint64_t(0);
+  for (uint64_t abs = a; abs < b; abs++) {
+    if ((abs & ~uint64_t(15)) != buf_at) {
+      buf_at = abs & ~uint64_t(15);
+      buf = load16(arena + buf_at);
+    }
+    const uint32_t byte = (word_of(buf, uint32_t(abs >> 2) & 3) >> ((abs & 3) * 8)) & 0xFFu;
+    uint64_t carry = 1, T[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      T[w] = (D[w] << 1) | carry | (D[w] & Lp[w]);
+      carry = D[w] >> 63;
+    }
+    uint64_t c = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint64_t x = T[w] & O[w], s1 = O[w] + x, c1 = s1 < O[w], s2 = s1 + c, c2 = s2 < s1;
+      T[w] |= s2 ^ O[w];
+      c = c1 | c2;
+    }
+    const uint64_t* Bb = B + size_t(byte) * W;
+    const bool keep = (byte & 0xC0u) == 0x80u;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      D[w] = (T[w] & Bb[w]) | (keep ? D[w] : 0);
+      acc |= D[w] & F[w];
+    }
+    if (acc) return true;
+  }
+  return false;
+}
+
+template <int W>
+__device__ bool fullscan_pair(const NfaParams& P, const uint8_t* arena, uint64_t fs, uint64_t len,
+                              const uint64_t* tab, uint32_t lane) {
+  const uint64_t cs = (len + 63) / 64 > P.fs_chunk ? (len + 63) / 64 : uint64_t(P.fs_chunk);
+  const uint64_t a = fs + uint64_t(lane) * cs, b = a + cs < fs + len ? a + cs : fs + len;
+  const bool mine = a < fs + len;
+  uint64_t D[W] = {}, E[W] = {};  // exit state, the entry it came from
+  bool acc = mine && nfa_chunk<W>(arena, a, b, D, tab);
+  if (__ballot(acc)) return true;
+  for (int round = 0; round < kFsMaxRounds; round++) {
+    uint64_t in[W];
+    bool grow = false;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint32_t lo = __shfl_up(uint32_t(D[w]), 1), hi = __shfl_up(uint32_t(D[w] >> 32), 1);
+      in[w] = (uint64_t(hi) << 32) | lo;  // lane c-1's exit state
+      if (lane == 0) in[w] = 0;
+      grow = grow || (in[w] & ~E[w]) != 0;
+    }
+    if (!__ballot(grow && mine)) return false;  // fixpoint: no chunk's entry state changed
+    if (grow && mine) {
+      uint64_t S[W];
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        E[w] |= in[w];
+        S[w] = E[w];
+      }
+      acc = nfa_chunk<W>(arena, a, b, S, tab);
+#pragma unroll
+      for (int w = 0; w < W; w++) D[w] = S[w];
+    }
+    if (__ballot(acc)) return true;
+  }
+  return true;  // not settled: emit (always safe)
+}
+
 __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t n_waves = uint64_t(gridDim.x) * (blockDim.x / 64);
   const uint64_t total = uint64_t(P.n_files) * P.n_fullscan_rules;
-  for (uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; t < total;
-       t += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t f = uint32_t(t / P.n_fullscan_rules);
-    const uint32_t r = P.fullscan_rules[t % P.n_fullscan_rules];
-    const RuleGpu rg = P.rules[r];
-    const uint64_t fs = P.off[f];
-    const int64_t len = int64_t(P.off[f + 1] - fs);
-    const bool acc =
-        rg.nfa_words == 0 || nfa_dispatch_abs(rg.nfa_words, P.arena, fs, len, 0, len, P.nfa + rg.nfa_off) == kNfaAccept;
-    if (acc) put_candidate(P.cands, P.cand_cap, P.counters, f, r, 0, len);
+  for (uint64_t t0 = (uint64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; t0 < total;
+       t0 += n_waves * 64) {
+    // one (file, rule) pair per lane: can its keyword gate be open?
+    const uint64_t t = t0 + lane;
+    bool open = false;
+    uint32_t f = 0, r = 0;
+    if (t < total) {
+      f = uint32_t(t / P.n_fullscan_rules);
+      r = P.fullscan_rules[t % P.n_fullscan_rules];
+      const RuleGpu rg = P.rules[r];
+      open = rg.gate != kGateKeywords || rg.kw_match_implied || (P.flags[f] & 4u) ||
+             (gate_flags(P, rg, f) & kCandGateOpen);
+      open = open && P.off[f + 1] > P.off[f];
+    }
+    uint64_t m = __ballot(open);
+    while (m) {  // the open pairs, one at a time, wave-wide
+      const int src = __ffsll(static_cast<unsigned long long>(m)) - 1;
+      m &= m - 1;
+      const uint32_t pf = __shfl(f, src), pr = __shfl(r, src);
+      const RuleGpu rg = P.rules[pr];
+      const uint64_t fs = P.off[pf], len = P.off[pf + 1] - fs;
+      bool acc = true;
+      if (rg.nfa_words != 0) {
+        const uint64_t* tab = P.nfa + rg.nfa_off;
+        switch (rg.nfa_words) {
+          case 1: acc = fullscan_pair<1>(P, P.arena, fs, len, tab, lane); break;
+          case 2: acc = fullscan_pair<2>(P, P.arena, fs, len, tab, lane); break;
+          case 3: acc = fullscan_pair<3>(P, P.arena, fs, len, tab, lane); break;
+          default: acc = fullscan_pair<4>(P, P.arena, fs, len, tab, lane); break;
+        }
+      }
+      if (acc && lane == 0) put_candidate(P.cands, P.cand_cap, P.counters, pf, pr, 0, int64_t(len));
+      if (lane == 0) atomicAdd(&P.counters[13], 1u);  // pairs scanned (stats)
+    }
   }
 }
 
@@ -1090,6 +1211,9 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   if (const char* dm = std::getenv("TSG_DIAG_SCAN")) diag_mode_ = uint32_t(std::atoi(dm));
   if (const char* dc = std::getenv("TSG_DIAG_CONFIRM")) diag_confirm_ = uint32_t(std::atoi(dc));
   if (const char* di = std::getenv("TSG_DIAG_ITEMS")) item_diag_path_ = di;
+  if (const char* fc = std::getenv("TSG_FULLSCAN_CHUNK")) fs_chunk_ = uint32_t(std::atoi(fc));
+  if (fs_chunk_ < 64) fs_chunk_ = 64;
+  hipEventCreate(&ev_fs_);
   kw_words_ = std::max<uint32_t>(1, cr.kw_words());
   n_rules_ = uint32_t(cr.rules.size());
   for (uint32_t r = 0; r < n_rules_; r++)
@@ -1226,6 +1350,7 @@ GpuEngine::~GpuEngine() {
     if (e) hipEventDestroy(e);
   for (auto& e : ev_copied_)
     if (e) hipEventDestroy(e);
+  if (ev_fs_) hipEventDestroy(ev_fs_);
   for (auto& e : ev_h2d_)
     if (e) hipEventDestroy(e);
   for (auto* h : h_off_)
@@ -1349,6 +1474,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     st->ms_careful += cs.ms_careful;
     st->ms_verify += cs.ms_verify;
     st->ms_fullscan += cs.ms_fullscan;
+    st->fullscan_tasks += cs.fullscan_tasks;
     st->ms_finalize += cs.ms_finalize;
     st->ms_chunkmap += cs.ms_chunkmap;
     st->ms_total += cs.ms_total;
@@ -1506,10 +1632,12 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.cand_cap = cand_cap_;
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
+    np.fs_chunk = fs_chunk_;
 
     if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     if (np.n_fullscan_rules > 0) {
+      HIP_OK(hipEventRecord(ev_fs_, stream_));
       fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
       HIP_OK(hipGetLastError());
     }
@@ -1561,6 +1689,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     hipEventElapsedTime(&st->ms_careful, ev_[3], ev_[4]);  // fold kernel
     hipEventElapsedTime(&st->ms_verify, ev_[4], ev_[5]);   // verify (deferred hits) + full-scan
     hipEventElapsedTime(&st->ms_finalize, ev_[5], ev_[6]);
+    if (n_fullscan_rules_ > 0) hipEventElapsedTime(&st->ms_fullscan, ev_fs_, ev_[5]);
+    st->fullscan_tasks = cnt[13];
     hipEventElapsedTime(&st->ms_chunkmap, ev_[0], ev_[1]);
     hipEventElapsedTime(&st->ms_total, ev_[0], ev_[6]);
     return true;
