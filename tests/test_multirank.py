@@ -139,7 +139,8 @@ def test_two_scanners_one_process_concurrent():
     from trivy_amd.shard import scan_devices
     n_dev = torch.cuda.device_count()
     scanners = [secret.NewScanner(None, device=0), secret.NewScanner(None, device=1 if n_dev > 1 else 0)]
-    files = [(p, b.replace(b"\r", b"")) for p, b in make_corpus(61, 240)]
+    # unique paths: AnalysisResult.Sort orders secrets by FilePath only (ties keep no defined order)
+    files = [("d%04d/%s" % (i, p), b.replace(b"\r", b"")) for i, (p, b) in enumerate(make_corpus(61, 240))]
     got = scan_devices(files, scanners)
     o = osc.new_scanner(None)
     want = AnalysisResult()
