@@ -2,6 +2,8 @@
 // work pkg/fanal/analyzer/secret/secret.go does before Scanner.Scan, the
 // analyzer group's Required gate, and an uncompressed-tar layer walker
 // (pkg/fanal/walker/tar.go), all packing straight into one batch arena.
+#include <chrono>
+#include <cstdio>
 #include "tsg_analyzer.h"
 
 #include <hip/hip_runtime_api.h>
@@ -476,6 +478,93 @@ int ChainEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
   return 0;
 }
 
+// Entries of [p, ...) as the sequential walk reads them, the index found in
+// parallel: the window [p, p + window) is cut into segments; each segment's
+// thread starts at its first block that parses as a header (segment 0: at p)
+// and follows the header chain while it stays in the segment.  The merge then
+// takes a segment's entries from the one starting where the true chain
+// arrives (chains that meet coincide from there: ChainEntry depends on the
+// start position only); when no speculative entry starts there (a segment
+// start inside file data that looked like a header, or a header chain cut in
+// two) that segment is walked sequentially from the true position.  Stops
+// after `max_regular` bytes of regular files (at least one entry), at the end
+// of the archive (*at_end) or on a malformed header (-1).
+int IndexEntries(const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window, uint64_t max_regular, int threads,
+                 std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
+  out->clear();
+  *at_end = false;
+  const uint64_t end = std::min<uint64_t>(n, p + window);
+  const size_t n_seg = size_t(std::max(1, threads) * 4);
+  const uint64_t seg = std::max<uint64_t>(((end - p) / n_seg + 511) & ~uint64_t(511), 1 << 16);
+  const size_t segs = size_t(std::max<uint64_t>(1, (end - p + seg - 1) / seg));
+  std::vector<std::vector<TarEntry>> spec(segs);
+  tsg::ParallelFor(segs, threads, [&](size_t s) {
+    const uint64_t a = p + s * seg, b = std::min(end, a + seg);
+    uint64_t q = a;
+    if (s > 0) {  // first block that parses as a header (512-aligned from p)
+      while (q + 512 <= b && (AllZero(tar + q) || !ChecksumOK(tar + q))) q += 512;
+    }
+    while (q < b) {
+      TarEntry e;
+      if (ChainEntry(tar, n, q, &e) != 0) break;  // end marker or garbage: the merge decides
+      q = e.next;
+      spec[s].push_back(std::move(e));
+    }
+  });
+  uint64_t cur = p, regular = 0;
+  for (size_t s = 0; s < segs; s++) {
+    const uint64_t b = std::min(end, p + (s + 1) * seg);
+    if (cur >= b) continue;
+    auto& v = spec[s];
+    auto it = std::lower_bound(v.begin(), v.end(), cur, [](const TarEntry& e, uint64_t x) { return e.start < x; });
+    if (it != v.end() && it->start == cur) {
+      for (; it != v.end(); ++it) {
+        cur = it->next;
+        if (it->what == 3) regular += it->size + 512;
+        out->push_back(std::move(*it));
+        if (regular > max_regular) break;
+      }
+    }
+    while (cur < b && regular <= max_regular) {  // sequential from the true position
+      TarEntry e;
+      const int r = ChainEntry(tar, n, cur, &e);
+      if (r < 0) return -1;
+      if (r == 1) {
+        *at_end = true;
+        *next = cur;
+        return 0;
+      }
+      cur = e.next;
+      if (e.what == 3) regular += e.size + 512;
+      out->push_back(std::move(e));
+    }
+    if (regular > max_regular) break;
+  }
+  if (out->empty() || (cur >= n && !*at_end)) {  // nothing in the window (a huge entry) or the tail
+    while (out->empty() || (cur < n && regular <= max_regular && out->size() < 1)) {
+      TarEntry e;
+      const int r = ChainEntry(tar, n, cur, &e);
+      if (r < 0) return -1;
+      if (r == 1) {
+        *at_end = true;
+        break;
+      }
+      cur = e.next;
+      out->push_back(std::move(e));
+    }
+  }
+  if (!*at_end && cur >= n) *at_end = true;  // io.EOF without the zero blocks
+  if (!*at_end && regular <= max_regular && cur < n && end >= n) {
+    // window reached the archive's end region: check for the end marker at cur
+    TarEntry e;
+    const int r = ChainEntry(tar, n, cur, &e);
+    if (r < 0) return -1;
+    if (r == 1) *at_end = true;
+  }
+  *next = cur;
+  return 0;
+}
+
 // The entry's name (ustar prefix, GNU long name, PAX path) and header checksum.
 void Resolve(const uint8_t* tar, TarEntry* e) {
   const uint8_t* h = tar + e->hdr;
@@ -520,24 +609,17 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
   if (!st) st = &local;
   uint64_t p = *cursor;
   std::vector<TarEntry> ents;
+  static const bool dbg = std::getenv("TSG_WALK_DEBUG") != nullptr;
+  static double t_phase[4];
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   for (;;) {
     // 1. index
-    ents.clear();
+    double t0 = dbg ? now() : 0;
     const uint64_t room = c->limit > c->used ? c->limit - c->used : 0;
-    uint64_t ahead = 0;
     bool at_end = false;
-    while (ahead <= room + room / 2 || ents.empty()) {
-      TarEntry e;
-      const int r = ChainEntry(tar, n, p, &e);
-      if (r < 0) return -1;
-      if (r == 1) {
-        at_end = true;
-        break;
-      }
-      p = e.next;
-      if (e.what == 3) ahead += e.size + 512;
-      ents.push_back(std::move(e));
-    }
+    if (IndexEntries(tar, n, p, 2 * room + (1 << 20), room + room / 2, c->threads, &ents, &p, &at_end) < 0)
+      return -1;
+    double t1 = dbg ? now() : 0;
     // 2. classify (AnalyzeFile's Required + Analyze's binary gate)
     const size_t kBlock = 64;
     tsg::ParallelFor((ents.size() + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
@@ -556,6 +638,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         e.out_len = e.bin ? tsg::PrintableLen(d, e.size) : e.size - tsg::CountCR(d, e.size);
       }
     });
+    double t2 = dbg ? now() : 0;
     // 3. accept in order
     size_t k = 0;
     bool full = false;
@@ -589,6 +672,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       st->required += e.state != 0;
       st->skipped_binary += e.state == 1;
     }
+    double t3 = dbg ? now() : 0;
     // 4. copy / transform the accepted contents
     tsg::ParallelFor((k + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
       for (size_t i = b * kBlock; i < std::min(k, (b + 1) * kBlock); i++) {
@@ -600,6 +684,15 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       }
     });
     std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
+    if (dbg) {
+      const double t4 = now();
+      t_phase[0] += t1 - t0;
+      t_phase[1] += t2 - t1;
+      t_phase[2] += t3 - t2;
+      t_phase[3] += t4 - t3;
+      std::fprintf(stderr, "walk phases (cumulative s): index %.3f classify %.3f accept %.3f copy %.3f\n", t_phase[0],
+                   t_phase[1], t_phase[2], t_phase[3]);
+    }
     if (full) {
       *cursor = ents[k].start;
       return 1;
