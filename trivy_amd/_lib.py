@@ -8,7 +8,8 @@ import ctypes
 import os
 from pathlib import Path
 
-_PATH = Path(__file__).resolve().parent / "libtsg.so"
+# TSG_LIB: an alternative build of the same library (tools/build_variant.py, tuning runs)
+_PATH = Path(os.environ.get("TSG_LIB") or Path(__file__).resolve().parent / "libtsg.so")
 _lib = None
 
 

@@ -73,7 +73,6 @@ class GpuEngine {
   // tables
   uint32_t diag_mode_ = 0, diag_confirm_ = 0;
   AnchorInfo* d_anchors_ = nullptr;
-  FollowLut* d_anchor_req_ = nullptr;
   RuleGpu* d_rules_ = nullptr;
   uint32_t* d_rule_kw_ = nullptr;
   uint64_t* d_nfa_ = nullptr;
@@ -90,7 +89,7 @@ class GpuEngine {
   void* d_fold_first_ = nullptr;  // per item: bytes that can start it (fold kernel prefilter)
   uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
-  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0;
+  uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, ft_luts_ = 0;
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;

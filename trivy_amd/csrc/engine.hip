@@ -292,7 +292,18 @@ struct NfaParams {
 // ---------------------------------------------------------------------------
 // K2: confirm flagged blocks exactly + verify the anchor hits
 // ---------------------------------------------------------------------------
-constexpr int kCThreads = 256;
+// Confirm-kernel shape.  The kernel is latency-bound: occupancy decides its
+// time (C2, profiles/r02_confirm_variants.txt: 1 WG/CU 14.5 ms, 2 WG/CU
+// 8.2 ms, 4 WG/CU 5.6 ms; 5-6 waves/SIMD by forcing <= 80 VGPRs spills and
+// loses).  LDS per 256-thread workgroup: 4 KiB reach + 56 B per lane (48-B
+// window + base) + queues and hit buffer (8.2 KiB) + the item tables
+// (C2: 12.3 KiB) = 39 KiB: four workgroups per CU, as many as the 125 VGPRs
+// allow.  The TSG_C_* macros exist for those variant builds
+// (tools/build_variant.py).
+#ifndef TSG_C_THREADS
+#define TSG_C_THREADS 256
+#endif
+constexpr int kCThreads = TSG_C_THREADS;
 
 struct FoldSite {  // a fold rune (U+0130 / U+212A / U+017F) at arena byte x of file f
   uint64_t x;
@@ -312,7 +323,13 @@ __device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
   return base + rank;
 }
 
-constexpr uint32_t kCWaveHits = 192;  // per-wave LDS hit buffer of the confirm kernel (flushed at >= 64)
+// Per-wave LDS hit buffer of the confirm kernel, flushed at >= 64 entries with
+// one global atomic (emitting each hit with its own wave-aggregated atomic on
+// the one hit counter cost 2.3 ms on C2: the atomics serialise at one address).
+#ifndef TSG_C_HITS
+#define TSG_C_HITS 96
+#endif
+constexpr uint32_t kCWaveHits = TSG_C_HITS;
 
 // Appends a hit to the wave's LDS buffer (LDS atomic); a full buffer spills to
 // the global list directly.
@@ -428,31 +445,22 @@ __device__ __forceinline__ bool follow_lut_pass(const FollowLut& L, const uint32
   return f0 != 0 && (n1 == 0 || f1 != 0);
 }
 
-// The 52 bytes from byte s (0..15) of the 16-B aligned pointer p16 as 13
-// little-endian words: five aligned 16-B loads (global memory or LDS), then a
-// two-stage word select and v_alignbyte for the sub-word offset.
-template <typename Ptr>
-__device__ __forceinline__ void follow_words(Ptr p16, uint32_t s, uint32_t* X) {
-  uint32_t D[20];
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p16 + 16 * q);
-    D[4 * q] = v.x;
-    D[4 * q + 1] = v.y;
-    D[4 * q + 2] = v.z;
-    D[4 * q + 3] = v.w;
-  }
+// The 52 bytes from byte s (0..3) of the 4-B aligned pointer w as 13
+// little-endian words: 14 word loads (global memory or LDS) and v_alignbyte.
+// (Selecting words out of wider aligned loads by a per-lane offset made the
+// compiler index a private array: 96 B of scratch per lane.)
+__device__ __forceinline__ void follow_words(const uint32_t* w, uint32_t s, uint32_t* X) {
   uint32_t R[14];
 #pragma unroll
-  for (int j = 0; j < 14; j++) {
-    const uint32_t r1a = (s & 4) ? D[j + 1] : D[j], r1b = (s & 4) ? D[j + 3] : D[j + 2];
-    R[j] = (s & 8) ? r1b : r1a;
-  }
+  for (int j = 0; j < 14; j++) R[j] = w[j];
 #pragma unroll
   for (int j = 0; j < 13; j++) X[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], s & 3);
 }
 
-constexpr int kCWin = 112;  // per-lane LDS copy of arena bytes [base - 16, base + 96)
+#ifndef TSG_C_WIN
+#define TSG_C_WIN 48
+#endif
+constexpr int kCWin = TSG_C_WIN;  // per-lane LDS copy of arena bytes [base - 16, base + kCWin - 16)
 
 struct ConfirmParams {
   const uint8_t* arena;
@@ -474,14 +482,14 @@ struct ConfirmParams {
   uint32_t hit_cap;
   FoldSite* folds;     // fold runes found (for the fold kernel)
   uint32_t fold_cap;
-  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission
+  uint32_t diag;       // TSG_DIAG_CONFIRM bits: 4 no item checks, 8 no attribution, 16 no emission, 32 follow first
   uint32_t* kwbits;               // per file: kw_words x u32 keyword bits
   uint32_t kw_words;
   const uint64_t* core;           // filter.h core tables (n_groups x 256)
   const uint32_t* group_items;    // n_groups x 8
   const uint32_t* bucket_groups;  // n_buckets + 1
   uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item exact matches
-  const FollowLut* luts;          // per anchor: follow requirements (rules.h)
+  uint32_t t_luts;                // tabs offset of the per-anchor follow requirements (rules.h FollowLut)
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -615,20 +623,35 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
 //   C  one candidate item per lane: the item's positions outside the core are
 //      checked, the start is attributed to its file (chunk map) and the anchor
 //      hits (or the fold site) are staged.
-constexpr uint32_t kCQ1 = 256;  // fires (overflow: handled in place)
-constexpr uint32_t kCQ2 = 256;  // candidate items (overflow: checked in place)
+#ifndef TSG_C_Q1
+#define TSG_C_Q1 128
+#endif
+#ifndef TSG_C_Q2
+#define TSG_C_Q2 96
+#endif
+#ifndef TSG_C_FSE
+#define TSG_C_FSE 0
+#endif
+constexpr bool kCFse = TSG_C_FSE;     // cache each block's file in LDS in phase A (-0.2 ms at equal occupancy; costs 20 B/lane)
+constexpr uint32_t kCQ1 = TSG_C_Q1;  // fires (overflow: handled in place)
+constexpr uint32_t kCQ2 = TSG_C_Q2;  // candidate items (overflow: checked in place)
 
 // kLdsTabs: the item tables are staged in LDS (they fit: builtin-sized rule
 // sets); otherwise they are read through the caches from global memory
 // (large custom rule sets, e.g. 2,000 generated rules).
 template <bool kLdsTabs>
-__global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
+#ifndef TSG_C_MINW
+#define TSG_C_MINW 1
+#endif
+__global__ __launch_bounds__(kCThreads, TSG_C_MINW) void confirm_kernel(ConfirmParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr uint32_t kWaves = kCThreads / 64;
   uint8_t* s_reach = smem;                                                      // 4 KiB, one copy per byte
   uint8_t* s_win = smem + 4096;                                                 // kCThreads x 64 B
   uint64_t* s_base = reinterpret_cast<uint64_t*>(s_win + kCThreads * kCWin);    // kCThreads
-  uint32_t* s_q1 = reinterpret_cast<uint32_t*>(s_base + kCThreads);             // kWaves x kCQ1
+  uint64_t* s_fse = s_base + kCThreads;                                         // kCThreads x 2: block's file [fs, fe)
+  uint32_t* s_file = reinterpret_cast<uint32_t*>(s_fse + (kCFse ? 2 * kCThreads : 0));  // kCThreads: block's file
+  uint32_t* s_q1 = s_file + (kCFse ? kCThreads : 0);                            // kWaves x kCQ1
   uint32_t* s_q2 = s_q1 + kWaves * kCQ1;                                        // kWaves x kCQ2
   uint32_t* s_hbuf = s_q2 + kWaves * kCQ2;                                      // kWaves x kCWaveHits x 3
   uint32_t* s_cnt = s_hbuf + kWaves * kCWaveHits * 3;                           // kWaves x 4
@@ -651,6 +674,8 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
   const uint32_t* classes = reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
   uint8_t* wwin = s_win + wave * 64 * kCWin;  // the wave's 64 windows
   uint64_t* wbase = s_base + wave * 64;      // block base per lane
+  uint64_t* wfse = s_fse + wave * 128;       // the file holding the block's first byte, per lane
+  uint32_t* wfile = s_file + wave * 64;
   uint32_t* q1 = s_q1 + wave * kCQ1;
   uint32_t* q2 = s_q2 + wave * kCQ2;
   uint32_t* hbuf = s_hbuf + wave * kCWaveHits * 3;
@@ -666,23 +691,39 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
     if (start < 0 || uint64_t(start) + it.n > P.n_bytes) return;
     const uint32_t core_lo = it.back > 8 ? it.back - 8u : 0u;  // [core_lo, back) verified by the core tables
-    for (uint32_t q = 0; q < it.n; q++) {
-      if (q == core_lo) {
-        q = it.back - 1u;
-        continue;
+    // Positions [q0, q1) outside the core range, checked exactly: all of them,
+    // before the follow requirements (measured on C2: checking the lookahead
+    // sets only after a follow requirement passed, TSG_DIAG_CONFIRM=32, costs
+    // 0.35 ms more -- the sets reject half the literal hits at a lower cost).
+    auto sets_ok = [&](uint32_t q0, uint32_t q1) {
+      for (uint32_t q = q0; q < q1; q++) {
+        if (q >= core_lo && q < it.back) continue;
+        const uint32_t bt = win_byte(l, uint64_t(start) + q);
+        const uint32_t c = item_cls[it.cls_off + q];
+        if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return false;
       }
-      const uint32_t bt = win_byte(l, uint64_t(start) + q);
-      const uint32_t c = item_cls[it.cls_off + q];
-      if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return;
-    }
+      return true;
+    };
+    const uint32_t check_to = it.lit_end < it.n && (P.diag & 32) ? it.lit_end : it.n;  // diag 32: follow first
+    if (!sets_ok(0, check_to)) return;
     if (P.diag & 16) return;
     const uint64_t s0 = uint64_t(start);
-    uint32_t f = P.chunk_file[s0 / kChunk];
-    uint64_t fs = P.off[f], fe = P.off[f + 1];
-    while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
-      f++;
-      fs = fe;
+    uint32_t f = 0;
+    uint64_t fs = 1, fe = 0;
+    if (kCFse) {  // phase A's attribution of the block start, when the item lies in that file
+      f = wfile[l];
+      fs = wfse[2 * l];
+      fe = wfse[2 * l + 1];
+    }
+    if (s0 < fs || s0 >= fe) {
+      f = P.chunk_file[s0 / kChunk];
+      fs = P.off[f];
       fe = P.off[f + 1];
+      while (s0 >= fe) {  // s0 < n_bytes = off[n_files]
+        f++;
+        fs = fe;
+        fe = P.off[f + 1];
+      }
     }
     if (s0 < fs || s0 + it.n > fe) return;  // crosses a file boundary
     if (P.diag & 8) return;
@@ -712,21 +753,24 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
     const uint64_t w0 = wbase[l] >= 16 ? wbase[l] - 16 : 0;
     uint32_t X[13];
     bool have_x = false;
+    int after = check_to < it.n ? -1 : 1;  // lookahead sets: -1 unchecked, 0 fail, 1 pass
     for (uint32_t d = 0; d < it.n_ids; d++) {
       const uint32_t aid = item_ids[it.ids_off + d];
       atomicAdd(&cnt[3], 1u);
-      const FollowLut lut = P.luts[aid];
+      const FollowLut lut = reinterpret_cast<const FollowLut*>(tabs + P.t_luts)[aid];
       if (lut.n[0] && e < P.n_bytes) {
         if (!have_x) {
           const uint64_t s = e - w0;
-          if (e >= w0 && (s & ~uint64_t(15)) + 80 <= uint64_t(kCWin))
-            follow_words(wwin + l * kCWin + (s & ~uint64_t(15)), uint32_t(s & 15), X);
+          if (e >= w0 && (s & ~uint64_t(3)) + 56 <= uint64_t(kCWin))
+            follow_words(reinterpret_cast<const uint32_t*>(wwin + l * kCWin + (s & ~uint64_t(3))), uint32_t(s), X);
           else
-            follow_words(P.arena + (e & ~uint64_t(15)), uint32_t(e & 15), X);
+            follow_words(reinterpret_cast<const uint32_t*>(P.arena + (e & ~uint64_t(3))), uint32_t(e), X);
           have_x = true;
         }
         if (!follow_lut_pass(lut, X, int64_t(fe - e))) continue;
       }
+      if (after < 0) after = sets_ok(check_to, it.n) ? 1 : 0;
+      if (!after) return;
       stage_hit(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, f, lit_end, aid);
     }
   };
@@ -792,6 +836,18 @@ __global__ __launch_bounds__(kCThreads) void confirm_kernel(ConfirmParams P) {
 #pragma unroll
       for (int q = 0; q < kCWin / 16; q++) wl[q] = dw[q];
       wbase[lane] = base;
+      if (kCFse) {  // the file holding the block's first byte (check_item's attribution, usually)
+        uint32_t f = P.chunk_file[base / kChunk];
+        uint64_t fs = P.off[f], fe = P.off[f + 1];
+        while (base >= fe) {
+          f++;
+          fs = fe;
+          fe = P.off[f + 1];
+        }
+        wfile[lane] = f;
+        wfse[2 * lane] = fs;
+        wfse[2 * lane + 1] = fe;
+      }
       const uint4 pv = base >= 16 ? d0 : make_uint4(0, 0, 0, 0);
       const uint4 v = base >= 16 ? d1 : d0;
       uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
@@ -1220,7 +1276,6 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (cr.rules[r].has_regex && !cr.rules[r].anchored) fullscan_rules_.push_back(r);
   n_fullscan_rules_ = uint32_t(fullscan_rules_.size());
   if (!Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
-      !Upload(&err_, &d_anchor_req_, cr.anchor_req.data(), cr.anchor_req.size()) ||
       !Upload(&err_, &d_rules_, cr.rules.data(), cr.rules.size()) ||
       !Upload(&err_, &d_rule_kw_, cr.rule_kw.data(), cr.rule_kw.size()) ||
       !Upload(&err_, &d_nfa_, cr.nfa.data(), cr.nfa.size()) ||
@@ -1257,6 +1312,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     ft_item_ids_ = put(ft->item_ids.data(), ft->item_ids.size() * 4);
     ft_item_cls_ = put(ft->item_cls.data(), ft->item_cls.size());
     ft_classes_ = put(ft->classes.data(), ft->classes.size() * 4);
+    ft_luts_ = put(cr.anchor_req.data(), cr.anchor_req.size() * sizeof(FollowLut));
     if (tb.empty()) tb.assign(16, 0);
     ftabs_bytes_ = uint32_t(tb.size());
     n_fitems_ = uint32_t(ft->items.size());
@@ -1317,13 +1373,15 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       if (!Upload(&err_, &dp, reinterpret_cast<const uint8_t*>(pk.data()), pk.size() * sizeof(FoldPair))) return;
       d_fold_pairs_ = dp;
     }
-    const size_t fixed = 4096 + size_t(kCThreads) * (kCWin + 8) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
+    const size_t fixed = 4096 + size_t(kCThreads) * (kCWin + 8 + (kCFse ? 20 : 0)) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
                          size_t(kCThreads / 64) * kCWaveHits * 12 + size_t(kCThreads / 64) * 16;
-    // tables staged in LDS only while two 256-thread workgroups still fit a CU;
-    // larger ones are read from global memory (L2-resident).  c3 (103 KB of
-    // tables): LDS at 1 WG/CU 102 GB/s vs global at 4 WG/CU 164 GB/s.
-    // TSG_LDS_TABS_MAX overrides (tuning).
-    size_t lds_max = 80 * 1024;  // two workgroups per CU; measured: 1 WG/CU with 160-KiB tables loses to 4 WGs/CU reading L2
+    // Tables staged in LDS only while four workgroups still fit a CU (the
+    // register-bound maximum); larger ones are read from global memory
+    // (L2-resident).  Measured on C2: LDS tables beat global ones by 17% at
+    // equal occupancy, 4 WG/CU beats 2 by 32%; c3 (103 KB of tables): LDS at
+    // 1 WG/CU 102 GB/s vs global at 4 WG/CU 164 GB/s.  TSG_LDS_TABS_MAX
+    // overrides (tuning).
+    size_t lds_max = 160 * 1024 / 4;
     if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
     lds_tabs_ = fixed + ftabs_bytes_ <= lds_max && ftabs_bytes_ + 2 * kFoldSpan + 16 <= lds_max;
     if (!item_diag_path_.empty() && hipMalloc(&d_item_diag_, 8 * std::max<size_t>(n_fitems_, 1)) != hipSuccess) {
@@ -1331,6 +1389,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       return;
     }
     c_lds_bytes_ = fixed + (lds_tabs_ ? ftabs_bytes_ : 0);
+    if (const char* e = std::getenv("TSG_CONFIRM_LDS_PAD")) c_lds_bytes_ += size_t(std::strtoull(e, nullptr, 10));  // occupancy experiments
     hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
     if (lds_tabs_)
@@ -1341,7 +1400,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_anchor_req_, d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1]};
   for (void* p : ps)
@@ -1576,7 +1635,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.group_items = d_group_items_;
     cp.bucket_groups = d_bucket_groups_;
     cp.item_diag = d_item_diag_;
-    cp.luts = d_anchor_req_;
+    cp.t_luts = ft_luts_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
         confirm_kernel<true><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
