@@ -370,7 +370,7 @@ def main():
     if layer is None:
         n_bytes, n_files = C.n_bytes, C.n_files
         arena_bytes = n_bytes
-        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs",
+        counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs", "fold_sites",
                                             "candidates", "special_files", "findings")}
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,

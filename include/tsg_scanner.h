@@ -127,6 +127,7 @@ typedef struct tsg_stats {
   double ms_h2d_span;
   uint64_t h2d_chunks;
   uint64_t fullscan_pairs;   /* (file, unanchored rule) pairs with an open keyword gate, NFA-scanned */
+  uint64_t fold_sites;       /* U+212A / U+017F / U+0130 occurrences the fold kernel examined */
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 

@@ -281,6 +281,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.ms_h2d_span = gs.ms_h2d_span;
   st.h2d_chunks = gs.h2d_chunks;
   st.fullscan_pairs = gs.fullscan_tasks;
+  st.fold_sites = gs.fold_sites;
   *out = r.release();
   return 0;
 }

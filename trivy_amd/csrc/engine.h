@@ -27,7 +27,7 @@ struct Candidate {      // produced by the verify / full-scan kernels
 };
 
 struct BatchStats {
-  uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0;
+  uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0, fold_sites = 0;
   uint64_t flagged_blocks = 0;
   uint64_t follow_hits = 0;     // anchor hits past the follow requirements + fold-kernel hits (the NFA runs on these)
   float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
@@ -87,7 +87,7 @@ class GpuEngine {
   void* d_ftabs_ = nullptr;
   void* d_fold_pairs_ = nullptr;  // fold kernel work list
   void* d_fold_first_ = nullptr;  // per item: bytes that can start it (fold kernel prefilter)
-  uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0;
+  uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0, n_fold_cap_k_ = 0, n_fold_cap_s_ = 0;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, ft_luts_ = 0;
   size_t c_lds_bytes_ = 0;

@@ -898,25 +898,27 @@ __global__ __launch_bounds__(kCThreads, TSG_C_MINW) void confirm_kernel(ConfirmP
 // advancing 3 / 2 bytes.  A superset of the true occurrences; hits carry the
 // literal end in bytes.
 //
-// Work list: a match holds the rune at x only if the position q covering byte
-// x can take it -- its set holds k/K (U+212A) or s/S (U+017F), or the lead
-// byte itself -- and then positions 0..q-1 span at least q and at most
-// max_before(q) bytes.  The host lists, per rune kind, the items with such a
-// position and the start range [x - hi, x - lo] over all of them (lo = the
-// first capable q, hi = max_before of the last), cut into tasks of at most
-// kFoldTaskStarts starts; each start is tried once.
+// Work lists (per rune kind): a match holds the rune at x only if the position
+// q covering byte x can take it -- its set holds k/K (U+212A) or s/S (U+017F),
+// or the lead byte itself.  When no other fold rune precedes x in the window,
+// every position before q spans one byte, so the start is exactly x - q: the
+// "capable" list holds one task per (item, capable q).  Otherwise positions
+// 0..q-1 span at least q and at most max_before(q) bytes, and the "range" list
+// holds the start range [x - hi, x - lo] per item (lo = the first capable q,
+// hi = max_before of the last), cut into tasks of at most kFoldTaskStarts
+// starts.  Each start is tried once either way.
 struct FoldPair {
   uint32_t item;
   uint16_t lo, hi;
 };
-constexpr int kFoldTaskStarts = 12;  // starts per fold task
+constexpr int kFoldTaskStarts = 12;  // starts per range task
 struct FoldParams {
   const uint8_t* arena;
   const uint64_t* off;
   const void* tabs;
   uint32_t tabs_bytes, t_items, t_item_ids, t_item_cls, t_classes, n_items;
-  const FoldPair* pairs;  // [k-site pairs | s-site pairs]
-  uint32_t n_pairs_k, n_pairs_s;
+  const FoldPair* pairs;  // [k ranges | s ranges | k capable | s capable]
+  uint32_t n_pairs_k, n_pairs_s, n_cap_k, n_cap_s;
   const uint32_t* first;  // per item 8 x u32: bytes its position 0 accepts (+ E2 / C5 fold leads)
   const FoldSite* folds;
   uint32_t fold_cap;
@@ -926,49 +928,66 @@ struct FoldParams {
 };
 
 constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
+constexpr int kFoldWin = 2 * kFoldSpan + 16;
+constexpr int kFoldWaves = 4;
 
-// One workgroup per fold site: the bytes [x - kFoldSpan, x + kFoldSpan) go to
-// LDS, the threads split the (item, start) pairs.  U+0130 sites only flag the
-// file (Go's (?i) does not fold U+0130 onto 'i').
+// One wave per fold site (no workgroup barriers): the bytes [x - kFoldSpan,
+// x + kFoldSpan) go to the wave's LDS window, the lanes split the tasks.  With
+// kLdsTabs the item tables and the position-0 byte sets are staged in LDS.
+// U+0130 sites only flag the file (Go's (?i) does not fold U+0130 onto 'i').
 template <bool kLdsTabs>  // as confirm_kernel
-__global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
+__global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ uint8_t s_bytes[2 * kFoldSpan + 16];
+  __shared__ uint8_t s_win[kFoldWaves][kFoldWin];
   if (kLdsTabs) {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(smem);
     for (uint32_t i = threadIdx.x; i < P.tabs_bytes / 16; i += blockDim.x) d[i] = t[i];
+    const uint4* f = reinterpret_cast<const uint4*>(P.first);
+    uint4* df = reinterpret_cast<uint4*>(smem + P.tabs_bytes);
+    for (uint32_t i = threadIdx.x; i < P.n_items * 2; i += blockDim.x) df[i] = f[i];
   }
   __syncthreads();
   const uint8_t* tabs = kLdsTabs ? smem : static_cast<const uint8_t*>(P.tabs);
+  const uint32_t* firsts = kLdsTabs ? reinterpret_cast<const uint32_t*>(smem + P.tabs_bytes) : P.first;
   const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
   const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(tabs + P.t_item_ids);
   const uint8_t* item_cls = tabs + P.t_item_cls;
   const uint32_t* classes = reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
   auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* wb = s_win[wave];
   const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
-  for (uint32_t si = blockIdx.x; si < n_folds; si += gridDim.x) {
+  for (uint32_t si = blockIdx.x * kFoldWaves + wave; si < n_folds; si += gridDim.x * kFoldWaves) {
     const FoldSite fsite = P.folds[si];
     const uint64_t fs = P.off[fsite.f], fe = P.off[fsite.f + 1];
     const uint64_t w0 = fsite.x > fs + kFoldSpan ? fsite.x - kFoldSpan : fs;
     const uint64_t w1 = fsite.x + kFoldSpan < fe ? fsite.x + kFoldSpan : fe;  // window [w0, w1)
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < uint32_t(w1 - w0); i += blockDim.x) s_bytes[i] = P.arena[w0 + i];
-    __syncthreads();
-    if (P.arena[fsite.x] == 0xC4) continue;  // U+0130: uniform per block
-    const bool kay = P.arena[fsite.x] == 0xE2;  // U+212A, else U+017F
-    const FoldPair* pairs = P.pairs + (kay ? 0 : P.n_pairs_k);
-    const uint32_t n_pairs = kay ? P.n_pairs_k : P.n_pairs_s;
-    // one task per (item, <= kFoldTaskStarts consecutive starts): bounded,
-    // balanced work without a per-start lookup of its item
-    for (uint32_t t = threadIdx.x; t < n_pairs; t += blockDim.x) {
+    wave_sync();
+    for (uint32_t i = lane; i < uint32_t(w1 - w0); i += 64) wb[i] = P.arena[w0 + i];
+    wave_sync();
+    const uint32_t lead = wb[fsite.x - w0];
+    if (lead == 0xC4) continue;  // U+0130: uniform per wave
+    const bool kay = lead == 0xE2;  // U+212A, else U+017F
+    bool other = false;  // another foldable rune before x (then starts are not x - q)
+    for (uint64_t p = w0 + lane; p < fsite.x; p += 64) {
+      const uint32_t b = wb[p - w0];
+      if ((b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA) ||
+          (b == 0xC5 && p + 1 < w1 && wb[p + 1 - w0] == 0xBF))
+        other = true;
+    }
+    other = __ballot(other) != 0;
+    const FoldPair* pairs = P.pairs + (other ? (kay ? 0 : P.n_pairs_k)
+                                             : P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k));
+    const uint32_t n_pairs = other ? (kay ? P.n_pairs_k : P.n_pairs_s) : (kay ? P.n_cap_k : P.n_cap_s);
+    for (uint32_t t = lane; t < n_pairs; t += 64) {
       const FoldPair fp = pairs[t];
       const FilterItemGpu it = items[fp.item];
-      const uint32_t* first = P.first + 8ull * fp.item;
+      const uint32_t* first = firsts + 8ull * fp.item;
       for (uint32_t back = fp.lo; back <= fp.hi; back++) {
         if (fsite.x < w0 + back) break;
         const uint64_t st = fsite.x - back;
-        const uint32_t b0 = s_bytes[st - w0];
+        const uint32_t b0 = wb[st - w0];
         if (!((first[b0 >> 5] >> (b0 & 31)) & 1u)) continue;  // position 0 fails (superset test)
         uint64_t p = st, lit_bytes_end = 0;
         bool ok = true, covered = false;
@@ -980,11 +999,11 @@ __global__ __launch_bounds__(256) void fold_kernel(FoldParams P) {
           }
           covered = covered || p == fsite.x;
           const uint32_t c = item_cls[it.cls_off + q];
-          const uint32_t b = s_bytes[p - w0];
-          if (b == 0xE2 && p + 2 < w1 && s_bytes[p + 1 - w0] == 0x84 && s_bytes[p + 2 - w0] == 0xAA &&
+          const uint32_t b = wb[p - w0];
+          if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
               (in_cls(c, 'k') || in_cls(c, 'K'))) {
             p += 3;
-          } else if (b == 0xC5 && p + 1 < w1 && s_bytes[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
+          } else if (b == 0xC5 && p + 1 < w1 && wb[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
             p += 2;
           } else if (in_cls(c, b)) {
             p += 1;
@@ -1325,7 +1344,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     d_ftabs_ = d;
     {  // fold work list (FoldParams): (item, q) pairs per rune kind, anchor items only
       auto in_cls = [&](uint32_t c, uint32_t b) { return (ft->classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
-      std::vector<FoldPair> pk, ps;
+      std::vector<FoldPair> pk, ps, ck, cs;  // start ranges / capable positions, per rune kind
       for (uint32_t i = 0; i < uint32_t(ft->items.size()); i++) {
         const FilterItemGpu& it = ft->items[i];
         if (it.kind != kItemAnchor) continue;
@@ -1337,10 +1356,12 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
           if (k || in_cls(c, 0xE2)) {
             if (klo < 0) klo = q;
             khi = before;
+            if (q <= 0xFFFF) ck.push_back({i, uint16_t(q), uint16_t(q)});
           }
           if (sf || in_cls(c, 0xC5)) {
             if (slo < 0) slo = q;
             shi = before;
+            if (q <= 0xFFFF) cs.push_back({i, uint16_t(q), uint16_t(q)});
           }
           before += k ? 3 : sf ? 2 : 1;
         }
@@ -1367,7 +1388,11 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       d_fold_first_ = dfm;
       n_fold_pairs_k_ = uint32_t(pk.size());
       n_fold_pairs_s_ = uint32_t(ps.size());
+      n_fold_cap_k_ = uint32_t(ck.size());
+      n_fold_cap_s_ = uint32_t(cs.size());
       pk.insert(pk.end(), ps.begin(), ps.end());
+      pk.insert(pk.end(), ck.begin(), ck.end());
+      pk.insert(pk.end(), cs.begin(), cs.end());
       if (pk.empty()) pk.push_back({0, 0, 0});
       uint8_t* dp = nullptr;
       if (!Upload(&err_, &dp, reinterpret_cast<const uint8_t*>(pk.data()), pk.size() * sizeof(FoldPair))) return;
@@ -1383,7 +1408,8 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     // overrides (tuning).
     size_t lds_max = 160 * 1024 / 4;
     if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
-    lds_tabs_ = fixed + ftabs_bytes_ <= lds_max && ftabs_bytes_ + 2 * kFoldSpan + 16 <= lds_max;
+    lds_tabs_ = fixed + ftabs_bytes_ <= lds_max &&
+                ftabs_bytes_ + 32 * size_t(n_fitems_) + kFoldWaves * kFoldWin <= 64 * 1024;  // fold kernel too
     if (!item_diag_path_.empty() && hipMalloc(&d_item_diag_, 8 * std::max<size_t>(n_fitems_, 1)) != hipSuccess) {
       err_ = "hipMalloc item diag";
       return;
@@ -1394,7 +1420,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
     if (lds_tabs_)
       hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          int(ftabs_bytes_));
+                          int(ftabs_bytes_ + 32 * n_fitems_));
   }
 }
 
@@ -1534,6 +1560,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     st->ms_verify += cs.ms_verify;
     st->ms_fullscan += cs.ms_fullscan;
     st->fullscan_tasks += cs.fullscan_tasks;
+    st->fold_sites += cs.fold_sites;
     st->ms_finalize += cs.ms_finalize;
     st->ms_chunkmap += cs.ms_chunkmap;
     st->ms_total += cs.ms_total;
@@ -1659,6 +1686,8 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.first = static_cast<const uint32_t*>(d_fold_first_);
     fo.n_pairs_k = n_fold_pairs_k_;
     fo.n_pairs_s = n_fold_pairs_s_;
+    fo.n_cap_k = n_fold_cap_k_;
+    fo.n_cap_s = n_fold_cap_s_;
     fo.folds = static_cast<const FoldSite*>(d_folds_);
     fo.fold_cap = fold_cap_;
     fo.hits = static_cast<uint32_t*>(d_hits_);
@@ -1666,9 +1695,9 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.counters = d_counters_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
-        fold_kernel<true><<<512, 256, ftabs_bytes_, stream_>>>(fo);
+        fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_bytes_ + 32 * n_fitems_, stream_>>>(fo);
       else
-        fold_kernel<false><<<512, 256, 0, stream_>>>(fo);
+        fold_kernel<false><<<2048, 64 * kFoldWaves, 0, stream_>>>(fo);
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[4], stream_));
@@ -1750,6 +1779,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     hipEventElapsedTime(&st->ms_finalize, ev_[5], ev_[6]);
     if (n_fullscan_rules_ > 0) hipEventElapsedTime(&st->ms_fullscan, ev_fs_, ev_[5]);
     st->fullscan_tasks = cnt[13];
+    st->fold_sites = cnt[9];
     hipEventElapsedTime(&st->ms_chunkmap, ev_[0], ev_[1]);
     hipEventElapsedTime(&st->ms_total, ev_[0], ev_[6]);
     return true;

@@ -53,7 +53,7 @@ class _CStats(c.Structure):
                 ("follow_hits", c.c_uint64)] + \
                [(n, c.c_double) for n in ("ms_chunkmap_kernel", "ms_confirm_kernel", "ms_nfa_kernel",
                                           "ms_finalize_kernel", "ms_h2d_span")] + \
-               [("h2d_chunks", c.c_uint64), ("fullscan_pairs", c.c_uint64)]
+               [("h2d_chunks", c.c_uint64), ("fullscan_pairs", c.c_uint64), ("fold_sites", c.c_uint64)]
 
 
 class _CTableInfo(c.Structure):
