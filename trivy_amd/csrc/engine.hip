@@ -66,6 +66,12 @@ __device__ __forceinline__ void wave_sync() {
 // ---------------------------------------------------------------------------
 // K1: streaming bucketed shift-or filter
 // ---------------------------------------------------------------------------
+#ifndef TSG_K1_PINGPONG
+#define TSG_K1_PINGPONG 1
+#endif
+#ifndef TSG_K1_DPP
+#define TSG_K1_DPP 1
+#endif
 constexpr int kFLane = 64;           // bytes per lane per tile (4 blocks of 16 B)
 constexpr int kFBlocks = kFLane / 16;
 constexpr int kFTile = 64 * kFLane;  // 4 KiB per wave tile
@@ -152,19 +158,21 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   const uint64_t n_tiles = (P.n_bytes + kFTile - 1) / kFTile;
   const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
   uint64_t t = uint64_t(blockIdx.x) * kScanWaves + wave;
-  uint4 cur[kFBlocks], nxt[kFBlocks];
-  uint2 pre = make_uint2(0, 0), pnx = make_uint2(0, 0);
+  uint4 bufA[kFBlocks], bufB[kFBlocks];
+  uint2 preA = make_uint2(0, 0), preB = make_uint2(0, 0);
   auto load_tile = [&](uint4* dst, uint2* pv, uint64_t tt) {
-    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLane;
+    const uint64_t t0 = tt * kFTile;
+    // One clamp per lane, no branch (a wave-uniform full-tile branch around
+    // the loads cost 1.4 ms on C2): a lane chunk starting inside the arena is
+    // readable whole (64 readable bytes past n_bytes), one past it reloads 0.
+    const uint64_t b0 = t0 + uint64_t(lane) * kFLane;
+    const uint8_t* lp = P.arena + (b0 < P.n_bytes ? b0 : 0);
 #pragma unroll
-    for (int j = 0; j < kFBlocks; j++) {
-      const uint64_t p = b0 + 16 * j;
-      dst[j] = load16(P.arena + (p < P.n_bytes ? p : 0));
-    }
+    for (int j = 0; j < kFBlocks; j++) dst[j] = load16(lp + 16 * j);
     // the 8 bytes before the tile (lane 0's prefix): a uniform address, so one
     // request; unconditional like the block loads, so the loads in flight stay
     // a static count and the chain waits only for the current tile's.
-    *pv = *reinterpret_cast<const uint2*>(P.arena + (tt > 0 ? tt * kFTile - 8 : 0));
+    *pv = *reinterpret_cast<const uint2*>(P.arena + (tt > 0 ? t0 - 8 : 0));
   };
   auto flush = [&]() {  // wave-uniform
     uint32_t base = 0;
@@ -187,11 +195,10 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     }
     nl_slots = 0;
   };
-  if (t < n_tiles) load_tile(cur, &pre, t);
-  for (; t < n_tiles; t += n_waves) {
-    load_tile(nxt, &pnx, t + n_waves < n_tiles ? t + n_waves : t);  // past the end: a harmless reload
-    const uint64_t b0 = t * kFTile + uint64_t(lane) * kFLane;
-    if (b0 + kFLane > P.n_bytes) {  // bytes past the arena end (last tile only) are zeroed
+  // One tile: `cur` holds its 64 bytes per lane, `pre` lane 0's prefix.
+  auto tile = [&](uint4* cur, uint2 pre, uint64_t tt) {
+    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLane;
+    if (tt * kFTile + kFTile > P.n_bytes) {  // wave-uniform: bytes past the arena end (last tile only) are zeroed
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint64_t p = b0 + 16 * j;
@@ -205,12 +212,20 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
         cur[j] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
       }
     }
-    // the previous 8 bytes: lane l-1's last two words (lane 0: the extra load)
+    // the previous 8 bytes: lane l-1's last two words by a DPP wave shift
+    // (lane 0 takes the extra load: the tile before, or zeros at the arena start)
+#if TSG_K1_DPP
+    const uint32_t p0 = uint32_t(__builtin_amdgcn_update_dpp(int(tt > 0 ? pre.x : 0u), int(cur[kFBlocks - 1].z),
+                                                             0x138, 0xF, 0xF, false));
+    const uint32_t p1 = uint32_t(__builtin_amdgcn_update_dpp(int(tt > 0 ? pre.y : 0u), int(cur[kFBlocks - 1].w),
+                                                             0x138, 0xF, 0xF, false));
+#else
     uint32_t p0 = __shfl(cur[kFBlocks - 1].z, int(lane) - 1), p1 = __shfl(cur[kFBlocks - 1].w, int(lane) - 1);
     if (lane == 0) {
-      p0 = t > 0 ? pre.x : 0u;
-      p1 = t > 0 ? pre.y : 0u;
+      p0 = tt > 0 ? pre.x : 0u;
+      p1 = tt > 0 ? pre.y : 0u;
     }
+#endif
     uint32_t flagged = 0, nl = 0;
     if (P.diag_mode < 2) {
       uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
@@ -237,11 +252,21 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
       for (int j = 0; j < kFBlocks; j++)
         nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
     }
+#if TSG_K1_DPP
+    // newlines per 1-KiB chunk = per 16-lane DPP row: a row_shr 1/2/4/8 sum puts it in the row's last lane
+    nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x111, 0xF, 0xF, true));
+    nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x112, 0xF, 0xF, true));
+    nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x114, 0xF, 0xF, true));
+    nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x118, 0xF, 0xF, true));
+    static_assert(kChunk / kFLane == 16, "one newline chunk per DPP row");
+    if ((lane & 15) == 15) reinterpret_cast<uint16_t*>(NL + nl_slots)[lane >> 4] = uint16_t(nl);
+#else
 #pragma unroll
     for (int x = 1; x < int(kChunk / kFLane); x <<= 1) nl += __shfl_xor(nl, x);
     if ((lane & (kChunk / kFLane - 1)) == 0)
       reinterpret_cast<uint16_t*>(NL + nl_slots)[lane / (kChunk / kFLane)] = uint16_t(nl);
-    if (++nl_slots == kFNlTiles) flush_nl(t);
+#endif
+    if (++nl_slots == kFNlTiles) flush_nl(tt);
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
       const bool fj = (flagged >> j) & 1u;
@@ -254,10 +279,29 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
       }
     }
     if (qn >= kFFlushAt) flush();
-#pragma unroll
-    for (int j = 0; j < kFBlocks; j++) cur[j] = nxt[j];
-    pre = pnx;
+  };
+#if TSG_K1_PINGPONG
+  // two register buffers alternate roles (no copies): tile t in A while t + n_waves loads into B
+  if (t < n_tiles) load_tile(bufA, &preA, t);
+  while (t < n_tiles) {
+    load_tile(bufB, &preB, t + n_waves < n_tiles ? t + n_waves : t);  // past the end: a harmless reload
+    tile(bufA, preA, t);
+    t += n_waves;
+    if (t >= n_tiles) break;
+    load_tile(bufA, &preA, t + n_waves < n_tiles ? t + n_waves : t);
+    tile(bufB, preB, t);
+    t += n_waves;
   }
+#else
+  if (t < n_tiles) load_tile(bufA, &preA, t);
+  for (; t < n_tiles; t += n_waves) {
+    load_tile(bufB, &preB, t + n_waves < n_tiles ? t + n_waves : t);
+    tile(bufA, preA, t);
+#pragma unroll
+    for (int j = 0; j < kFBlocks; j++) bufA[j] = bufB[j];
+    preA = preB;
+  }
+#endif
   if (qn) flush();
   if (nl_slots) flush_nl(t - n_waves);
 }
