@@ -211,7 +211,8 @@ PEAK_HBM = 8000.0  # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
 KERNELS = [("chunk_map_kernel", "ms_chunkmap_kernel"), ("filter_kernel (K1)", "ms_scan_kernel"),
            ("confirm_kernel (K2)", "ms_confirm_kernel"), ("fold_kernel", "ms_careful_kernel"),
            ("verify_hits_kernel (follow check + NFA) + fullscan_kernel", "ms_nfa_kernel"),
-           ("finalize_kernel", "ms_finalize_kernel")]
+           ("finalize_kernel", "ms_finalize_kernel"),
+           ("xform kernels (c4 GPU pre-transform: lengths, scan, compaction)", "ms_xform_kernel")]
 
 WORKLOADS = {
     # (description, GB per GPU, CPU-baseline sample MB, oracle parity sample MB)
@@ -241,6 +242,9 @@ def main():
     ap.add_argument("--ingest", action="store_true",
                     help="c2/c3: host-resident corpus (page-locked), H2D inside the timed region")
     ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
+    ap.add_argument("--transform", choices=["gpu", "host"], default="gpu",
+                    help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
+                         "the walk's host threads")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     args = ap.parse_args()
     wl_desc, gb_default, cpu_mb_default, parity_mb_default = WORKLOADS[args.workload]
@@ -326,7 +330,8 @@ def main():
         an = SecretAnalyzer(device=local)
         an.Init(AnalyzerOptions())
         t_compile = time.time() - t_c
-        colls = [Collector(an, args.arena_mb << 20), Collector(an, args.arena_mb << 20)]
+        gx = args.transform == "gpu"
+        colls = [Collector(an, args.arena_mb << 20, gx), Collector(an, args.arena_mb << 20, gx)]
 
         def run_steps(n, stats):
             for _ in range(n):
@@ -388,6 +393,7 @@ def main():
                         "layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
                         "arena_mb": args.arena_mb, "pipeline": "2 collectors (walk k+1 || scan k)",
+                        "pre_transform": args.transform,
                         "layer_gbps": round(world * int(layer.size) * args.steps / dt / 1e9, 3)}
     value = world * n_bytes * args.steps / dt / 1e9
     alg_bytes = arena_bytes + 16 * n_files  # 1 B/arena byte + 16 B/file

@@ -72,8 +72,13 @@ typedef struct tsg_tar_stats {
  * archive.  Whiteout (.wh.) and opaque-dir entries are counted, not added. */
 int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st);
 
+/* GPU pre-transform mode (empty collector only): files go into the arena as
+ * read, and the CR strip / printable extraction runs on the GPU at scan time
+ * (tsg_batch.transform).  The batch limit then counts each file's largest
+ * transformed size. */
+int tsg_collector_set_gpu_transform(tsg_collector* c, int on);
 uint32_t tsg_collector_files(const tsg_collector* c);
-uint64_t tsg_collector_bytes(const tsg_collector* c);       /* transformed (arena) bytes */
+uint64_t tsg_collector_bytes(const tsg_collector* c);       /* arena bytes (transformed; as read in GPU mode) */
 uint64_t tsg_collector_input_bytes(const tsg_collector* c); /* bytes as read, added files only */
 /* The ScanArgs of file i as they will be scanned (tests / host-language mirror). */
 int tsg_collector_file(const tsg_collector* c, uint32_t i, const char** path, uint64_t* path_len,

@@ -76,6 +76,11 @@ typedef struct tsg_batch {
   const char* const* paths;      /* ScanArgs.FilePath per file */
   const uint64_t* path_lens;     /* optional */
   const uint8_t* binary;         /* optional ScanArgs.Binary per file */
+  /* optional, per file: the analyzer's pre-scan transform, run on the GPU
+   * (then host_arena / host_offsets hold the bytes as read, and dev_arena
+   * must be NULL): 0 as is, 1 every '\r' removed (secret.go:121), 2
+   * utils.ExtractPrintableBytes (.pyc, secret.go:112-117, utils.go:128-160) */
+  const uint8_t* transform;
 } tsg_batch;
 
 int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);
@@ -128,6 +133,7 @@ typedef struct tsg_stats {
   uint64_t h2d_chunks;
   uint64_t fullscan_pairs;   /* (file, unanchored rule) pairs with an open keyword gate, NFA-scanned */
   uint64_t fold_sites;       /* U+212A / U+017F / U+0130 occurrences the fold kernel examined */
+  double ms_xform_kernel;    /* GPU pre-transform (batch.transform; part of ms_gpu_total) */
 } tsg_stats;
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 

@@ -41,6 +41,8 @@ def make_layer(seed: int, n_files: int, fmt=tarfile.GNU_FORMAT) -> bytes:
                 path = "./" + path
             if rng.random() < 0.03:
                 path = "/" + path
+            if rng.random() < 0.02:  # names path.Clean rewrites: "//", "/./", "/../"
+                path = path.replace("/", rng.choice(["//", "/./", "/x/../"]), 1)
             r = rng.random()
             if r < 0.04:
                 ti = tarfile.TarInfo(d + "/.wh." + name)  # whiteout

@@ -187,7 +187,8 @@ def test_gpu_analyze_golden(case, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_analyze_batch_vs_oracle():
+@pytest.mark.parametrize("gpu_transform", [False, True])
+def test_gpu_analyze_batch_vs_oracle(gpu_transform):
     from trivy_amd.analyzer import AnalysisInput, FileInfo, SecretAnalyzer, AnalyzerOptions
     a = SecretAnalyzer()
     a.Init(AnalyzerOptions())
@@ -200,7 +201,7 @@ def test_gpu_analyze_batch_vs_oracle():
             if i % 2 == 0:
                 p = p + ".pyc"
         inputs.append(AnalysisInput(Dir=rng.choice(["", "."]), FilePath=p, Info=FileInfo(len(b)), Content=b))
-    got = a.AnalyzeBatch(inputs, arena_bytes=64 << 10)  # several batches
+    got = a.AnalyzeBatch(inputs, arena_bytes=64 << 10, gpu_transform=gpu_transform)  # several batches
     n = 0
     for inp, g in zip(inputs, got):
         w = o.analyze(inp.FilePath, inp.Dir, inp.Content)
@@ -213,15 +214,16 @@ def test_gpu_analyze_batch_vs_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gpu_transform", [False, True])
 @pytest.mark.parametrize("fmt", [tarfile.GNU_FORMAT, tarfile.PAX_FORMAT])
-def test_gpu_analyze_layer_vs_oracle(fmt):
+def test_gpu_analyze_layer_vs_oracle(fmt, gpu_transform):
     from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
     a = SecretAnalyzer()
     a.Init(AnalyzerOptions())
     o = oan.SecretAnalyzer("")
     layer = make_layer(500 + fmt, 400, fmt)
     st = {}
-    got = a.AnalyzeLayer(layer, arena_bytes=32 << 10, stats=st)  # many double-buffered batches
+    got = a.AnalyzeLayer(layer, arena_bytes=32 << 10, stats=st, gpu_transform=gpu_transform)  # many batches
     want = oan.analyze_layer(o, layer)
     got.Sort()
     want.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
@@ -232,8 +234,10 @@ def test_gpu_analyze_layer_vs_oracle(fmt):
 
 
 # ---- BASELINE configs[3] (C4): the native layer generator's archives -----------
-def test_native_walk_generated_layer_vs_oracle(host_analyzer):
-    """The bench's C4 layers (native ustar writer, distro-like paths) walk identically."""
+@pytest.mark.parametrize("gpu_transform", [False, True])
+def test_native_walk_generated_layer_vs_oracle(host_analyzer, gpu_transform):
+    """The bench's C4 layers (native ustar writer, distro-like paths) walk identically
+    (GPU-transform mode: the arena holds the bytes as read; file() transforms them)."""
     from trivy_amd import corpus
     from trivy_amd.analyzer.secret import Collector, _CTarStats
     layer = corpus.generate_layer(3_000_000, seed=corpus.SEED + 9)
@@ -241,7 +245,7 @@ def test_native_walk_generated_layer_vs_oracle(host_analyzer):
     files, wh, opq = oan.walk_layer_tar(layer.tobytes())
     want = [a for a in (o.prepare(fp, "", b) for fp, sz, b in files if o.required(fp, sz)) if a is not None]
     st = _CTarStats()
-    coll = Collector(host_analyzer, 1 << 20)
+    coll = Collector(host_analyzer, 1 << 20, gpu_transform)
     got, cursor = [], 0
     while True:
         rc, cursor = coll.add_tar(layer, cursor, st)
@@ -256,13 +260,14 @@ def test_native_walk_generated_layer_vs_oracle(host_analyzer):
 
 
 @pytest.mark.gpu
-def test_gpu_analyze_generated_layer_vs_oracle():
+@pytest.mark.parametrize("gpu_transform", [False, True])
+def test_gpu_analyze_generated_layer_vs_oracle(gpu_transform):
     from trivy_amd import corpus
     from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
     layer = corpus.generate_layer(1_500_000, seed=corpus.SEED + 4, secrets_per_byte=1.0 / 8192)
     a = SecretAnalyzer()
     a.Init(AnalyzerOptions())
-    got = a.AnalyzeLayer(layer, arena_bytes=256 << 10)
+    got = a.AnalyzeLayer(layer, arena_bytes=256 << 10, gpu_transform=gpu_transform)
     got.Sort()
     want = oan.analyze_layer(oan.SecretAnalyzer(""), layer.tobytes())
     want.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
@@ -270,3 +275,61 @@ def test_gpu_analyze_generated_layer_vs_oracle():
         s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
     assert [_norm_secret(s) for s in got.Secrets] == want
     assert len(want) > 20
+
+
+def test_native_tar_walk_cleans_names(host_analyzer):
+    """path.Clean on archive names (walker/tar.go:46-48): "//", "/./", "..", leading "/" and "./"."""
+    from trivy_amd.analyzer.secret import Collector, _CTarStats
+    import numpy as np
+    names = ["etc//app/a.txt", "a/./b.txt", "x/y/../z.txt", "/abs//p.txt", "./rel/q.txt", "u/v/w/../../t.txt",
+             "../up/s.txt", "m/../../n.txt", "k/l/.."]
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        for n in names:
+            b = b"hello world, some text\n"
+            ti = tarfile.TarInfo(n)
+            ti.size = len(b)
+            tf.addfile(ti, io.BytesIO(b))
+    layer = buf.getvalue()
+    want = ["/" + fp for fp, _, _ in oan.walk_layer_tar(layer)[0]]
+    coll = Collector(host_analyzer, 1 << 20)
+    rc, _ = coll.add_tar(np.frombuffer(layer, dtype=np.uint8), 0, _CTarStats())
+    got = [coll.file(i)[0] for i in range(coll.files())]
+    assert got == want
+    assert "/x/z.txt" in got and "/etc/app/a.txt" in got
+
+
+@pytest.mark.gpu
+def test_gpu_transform_edges_vs_oracle():
+    """The GPU pre-transform kernels (trivy_amd/csrc/xform.hip) on the cases the tiles
+    and lanes cut: CR at 16-B / 1-KiB boundaries, CR-only and empty-after-strip files,
+    CRLF secrets, .pyc printable runs of length 4 / 5 / long, runs crossing tiles."""
+    from trivy_amd.analyzer import AnalysisInput, FileInfo, SecretAnalyzer, AnalyzerOptions
+    a = SecretAnalyzer()
+    a.Init(AnalyzerOptions())
+    o = oan.SecretAnalyzer("")
+    key = b"AKIA" + b"Z" * 12 + b"QWER"
+    texts = []
+    for n in (10, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 3000):
+        for pos in (0, 15, 16, 1023, 1024, n - 1):
+            b = bytearray(b"x" * n)
+            if 0 <= pos < n:
+                b[pos] = 13
+            texts.append(bytes(b) + b"\r\naws_key = " + key + b"\r\n")
+    texts += [b"\r" * 40, b"\r\r\r\r\r\r\r\r\r\rAKIA" + b"Q" * 16 + b"\r\r", (b"line\r\n" * 700) + key]
+    bins = [b"\x00\x01abcd\x00abcde\x00" + key + b"\x00" + b"y" * 2000 + b"\x07" + b"zz" * 600 + key,
+            b"\x00" * 50 + b"\xa1\xa2\xad\xa3\xa4\xa5\xa6" + b"\x00" + key]
+    inputs = [AnalysisInput(Dir="", FilePath="t/%d.txt" % i, Info=FileInfo(len(b)), Content=b)
+              for i, b in enumerate(texts)]
+    inputs += [AnalysisInput(Dir="", FilePath="b/%d.pyc" % i, Info=FileInfo(len(b)), Content=b)
+               for i, b in enumerate(bins)]
+    got = a.AnalyzeBatch(inputs, arena_bytes=16 << 10, gpu_transform=True)
+    n = 0
+    for inp, g in zip(inputs, got):
+        w = o.analyze(inp.FilePath, inp.Dir, inp.Content)
+        if w is None:
+            assert g is None, inp.FilePath
+        else:
+            n += 1
+            assert [_norm_secret(s) for s in g.Secrets] == w["Secrets"], inp.FilePath
+    assert n > 40

@@ -66,6 +66,7 @@ def _declare(L):
                                      c.POINTER(c.c_void_p), c.POINTER(c.c_uint64), c.POINTER(c.c_int)]
     L.tsg_collector_submit.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L.tsg_collector_reset.argtypes = [c.c_void_p]
+    L.tsg_collector_set_gpu_transform.argtypes = [c.c_void_p, c.c_int]
     L.tsg_scan_wait.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L._tsg_analyzer_declared = True
 
@@ -151,12 +152,16 @@ def _read(content) -> bytes:
 class Collector:
     """A batch arena (tsg_collector): Analyze's pre-scan half for many files."""
 
-    def __init__(self, analyzer: "SecretAnalyzer", arena_bytes: int = 256 << 20):
+    def __init__(self, analyzer: "SecretAnalyzer", arena_bytes: int = 256 << 20, gpu_transform: bool = False):
+        """gpu_transform: files enter the arena as read and the CR strip / printable
+        extraction runs on the GPU at scan time (tsg_collector_set_gpu_transform)."""
         self._L = analyzer._L
         h = c.c_void_p()
         if self._L.tsg_collector_new(analyzer._h, int(arena_bytes), c.byref(h)) != 0:
             raise RuntimeError("tsg_collector_new failed: %s" % _lib.last_error(self._L))
         self._h = h
+        if gpu_transform and self._L.tsg_collector_set_gpu_transform(h, 1) != 0:
+            raise RuntimeError("tsg_collector_set_gpu_transform failed: %s" % _lib.last_error(self._L))
         self._keep = []
 
     def __del__(self):
@@ -303,10 +308,10 @@ class SecretAnalyzer:
         return self.AnalyzeBatch([input])[0]
 
     # --- batched forms ------------------------------------------------------
-    def AnalyzeBatch(self, inputs: Sequence[AnalysisInput], arena_bytes: int = 256 << 20
-                     ) -> List[Optional[AnalysisResult]]:
+    def AnalyzeBatch(self, inputs: Sequence[AnalysisInput], arena_bytes: int = 256 << 20,
+                     gpu_transform: bool = False) -> List[Optional[AnalysisResult]]:
         out: List[Optional[AnalysisResult]] = [None] * len(inputs)
-        coll = Collector(self, arena_bytes)
+        coll = Collector(self, arena_bytes, gpu_transform)
         idx: List[int] = []
 
         def flush():
@@ -333,7 +338,8 @@ class SecretAnalyzer:
         return out
 
     def AnalyzeLayer(self, layer, arena_bytes: int = 256 << 20, stats: Optional[dict] = None,
-                     materialize: bool = True, colls: Optional[List[Collector]] = None) -> AnalysisResult:
+                     materialize: bool = True, colls: Optional[List[Collector]] = None,
+                     gpu_transform: bool = False) -> AnalysisResult:
         """Every regular file of an uncompressed tar layer (bytes or a uint8 numpy array),
         as the image artifact's AnalyzeFile(dir="") would run it.  Two collectors alternate:
         one is being filled while the other's batch is on the GPU.  materialize=False
@@ -349,7 +355,7 @@ class SecretAnalyzer:
                 for k2, v in out.items():
                     scan_tot[k2] = scan_tot.get(k2, 0) + v
         st = _CTarStats()
-        colls = colls or [Collector(self, arena_bytes), Collector(self, arena_bytes)]
+        colls = colls or [Collector(self, arena_bytes, gpu_transform), Collector(self, arena_bytes, gpu_transform)]
         pending = None
         cursor, k, done = 0, 0, False
         t_walk = t_wait = 0.0

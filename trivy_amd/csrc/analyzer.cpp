@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "capi_internal.h"
@@ -86,12 +87,32 @@ uint64_t StripCR(const uint8_t* in, uint64_t n, uint8_t* out) {
   return w;
 }
 
+// True when path.Clean(p) == p: no empty, "." or ".." element, no trailing
+// slash (other than the root itself).  Most archive names already are clean.
+inline bool GoPathIsClean(const char* p, size_t n) {
+  if (n == 0) return false;
+  if (n == 1) return p[0] != '.';
+  if (p[n - 1] == '/') return false;
+  size_t s = 0;  // element start
+  for (size_t i = 0; i <= n; i++) {
+    if (i < n && p[i] != '/') continue;
+    const size_t len = i - s;
+    if (len == 0 && i != 0) return false;                      // "//" (a leading '/' is the root)
+    if (len == 1 && p[s] == '.') return false;                 // "."
+    if (len == 2 && p[s] == '.' && p[s + 1] == '.') return false;  // ".."
+    s = i + 1;
+  }
+  return true;
+}
+
 // path.Clean (Go, slash-separated).
 std::string GoPathClean(const std::string& path) {
   if (path.empty()) return ".";
+  if (GoPathIsClean(path.data(), path.size())) return path;
   const bool rooted = path[0] == '/';
   const size_t n = path.size();
   std::string out;
+  out.reserve(n + 1);
   size_t r = 0, dotdot = 0;
   if (rooted) {
     out.push_back('/');
@@ -104,9 +125,10 @@ std::string GoPathClean(const std::string& path) {
       r++;
     } else if (path[r] == '.' && path[r + 1] == '.' && (r + 2 == n || path[r + 2] == '/')) {
       r += 2;
-      if (out.size() > dotdot) {
-        out.pop_back();
-        while (out.size() > dotdot && out.back() != '/') out.pop_back();
+      if (out.size() > dotdot) {  // back to the last '/' at or after dotdot (Go: w--, then while out[w] != '/')
+        size_t w = out.size() - 1;
+        while (w > dotdot && out[w] != '/') w--;
+        out.resize(w);
       } else if (!rooted) {
         if (!out.empty()) out.push_back('/');
         out += "..";
@@ -155,6 +177,13 @@ struct tsg_collector {
   uint8_t* arena = nullptr;
   uint64_t cap = 0, used = 0, input_bytes = 0;
   uint64_t limit = 0;  // the batch size asked for
+  // GPU pre-transform mode (tsg_collector_set_gpu_transform): the arena holds
+  // the bytes as read, kinds[] the transform per file (xform.h), and the batch
+  // limit counts each file's largest transformed size (bound).
+  bool gpu_xform = false;
+  uint64_t bound = 0;
+  std::vector<uint8_t> kinds;
+  mutable std::vector<uint8_t> scratch;  // tsg_collector_file's transformed copy (GPU mode)
   int threads = 16;    // ingest threads (TSG_HOST_THREADS)
   std::vector<uint64_t> offs{0};
   std::string path_pool;
@@ -202,8 +231,10 @@ struct tsg_collector {
       path_lens[i] = path_off[i + 1] - path_off[i];
     }
   }
+  uint64_t acct() const { return gpu_xform ? bound : used; }  // bytes counted against the limit
   void Reset() {
-    used = input_bytes = 0;
+    used = input_bytes = bound = 0;
+    kinds.clear();
     offs.assign(1, 0);
     path_pool.clear();
     path_off.assign(1, 0);
@@ -214,23 +245,28 @@ struct tsg_collector {
 namespace {
 bool Required(const tsg_analyzer* a, const char* path, uint64_t len, int64_t size) {  // secret.go:152-190
   if (size < 10) return false;
-  const std::string fp(path, size_t(len));
+  const std::string_view fp(path, size_t(len));
   const size_t slash = fp.rfind('/');
-  const std::string dir = slash == std::string::npos ? "" : fp.substr(0, slash + 1);
-  const std::string name = slash == std::string::npos ? fp : fp.substr(slash + 1);
+  const std::string_view dir = slash == std::string_view::npos ? std::string_view() : fp.substr(0, slash + 1);
+  const std::string_view name = slash == std::string_view::npos ? fp : fp.substr(slash + 1);
   // strings.Split(dir, "/") contains a skip dir
   for (size_t b = 0;;) {
     const size_t e = dir.find('/', b);
-    const std::string part = dir.substr(b, e == std::string::npos ? std::string::npos : e - b);
+    const std::string_view part = dir.substr(b, e == std::string_view::npos ? std::string_view::npos : e - b);
     for (const char* d : tsg::kSkipDirs)
       if (part == d) return false;
-    if (e == std::string::npos) break;
+    if (e == std::string_view::npos) break;
     b = e + 1;
   }
   for (const char* f : tsg::kSkipFiles)
     if (name == f) return false;
   if (a->config_base == fp) return false;
-  const std::string ext = tsg::GoExt(name);
+  std::string_view ext;  // filepath.Ext
+  for (size_t i = name.size(); i-- > 0;)
+    if (name[i] == '.') {
+      ext = name.substr(i);
+      break;
+    }
   for (const char* x : tsg::kSkipExts)
     if (ext == x) return false;
   if (a->s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len))) return false;
@@ -242,13 +278,21 @@ int64_t Add(tsg_collector* c, const char* path, uint64_t plen, bool image, const
   const bool bin = tsg::IsBinaryHead(content, size);
   if (bin && tsg::GoExt(std::string(path, size_t(plen))) != ".pyc") return TSG_SKIPPED;
   const uint64_t need = bin ? size + size / 5 + 1 : size;
-  if (c->files() > 0 && c->used + need > c->limit) return TSG_FULL;
+  if (c->files() > 0 && c->acct() + need > c->limit) return TSG_FULL;
   if (c->used + need + 64 > c->cap) {  // only a lone file larger than the batch gets here
     if (c->files() > 0) return TSG_FULL;
     if (!c->Reserve(need + 64)) return -3;
   }
   uint8_t* dst = c->arena + c->used;
-  const uint64_t len = bin ? tsg::ExtractPrintable(content, size, dst) : tsg::StripCR(content, size, dst);
+  uint64_t len;
+  if (c->gpu_xform) {  // as read; the GPU transforms it
+    std::memcpy(dst, content, size);
+    len = size;
+    c->bound += need;
+    c->kinds.push_back(bin ? 2 : 1);
+  } else {
+    len = bin ? tsg::ExtractPrintable(content, size, dst) : tsg::StripCR(content, size, dst);
+  }
   c->used += len;
   std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
   c->offs.push_back(c->used);
@@ -306,11 +350,14 @@ bool ParseNumeric(const uint8_t* b, size_t n, int64_t* out) {  // parseNumeric
 bool ChecksumOK(const uint8_t* b) {
   int64_t want = 0;
   if (!ParseNumeric(b + 148, 8, &want)) return false;
-  int64_t u = 0, s = 0;
-  for (int i = 0; i < 512; i++) {
-    const uint8_t c = (i >= 148 && i < 156) ? ' ' : b[i];
-    u += c;
-    s += int8_t(c);
+  // unsigned and signed byte sums with the checksum field read as spaces
+  // (two plain loops: the compiler vectorises them)
+  int32_t u = 0, s = 0;
+  for (int i = 0; i < 512; i++) u += b[i];
+  for (int i = 0; i < 512; i++) s += int8_t(b[i]);
+  for (int i = 148; i < 156; i++) {
+    u += ' ' - b[i];
+    s += ' ' - int8_t(b[i]);
   }
   return want == u || want == s;
 }
@@ -478,6 +525,28 @@ int ChainEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
   return 0;
 }
 
+void Classify(const uint8_t* tar, TarEntry* e);
+
+// Everything the walk decides about one entry, on the thread that indexed it
+// (its header and path are still in that core's cache): the name (Classify),
+// AnalyzeFile's Required, Analyze's binary gate and the transformed length.
+void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
+  Classify(tar, e);
+  e->state = 0;
+  if (e->what != 3 || !Required(c->a, e->fp.data(), e->fp.size(), int64_t(e->size))) return;
+  const uint8_t* d = tar + e->data;
+  e->bin = tsg::IsBinaryHead(d, e->size) ? 1 : 0;
+  if (e->bin && tsg::GoExt(e->fp) != ".pyc") {
+    e->state = 1;
+    return;
+  }
+  e->state = 2;
+  if (c->gpu_xform)  // the largest transformed size: the batch limit counts it, the GPU transforms
+    e->out_len = e->bin ? e->size + e->size / 5 + 1 : e->size;
+  else
+    e->out_len = e->bin ? tsg::PrintableLen(d, e->size) : e->size - tsg::CountCR(d, e->size);
+}
+
 // Entries of [p, ...) as the sequential walk reads them, the index found in
 // parallel: the window [p, p + window) is cut into segments; each segment's
 // thread starts at its first block that parses as a header (segment 0: at p)
@@ -489,8 +558,8 @@ int ChainEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
 // two) that segment is walked sequentially from the true position.  Stops
 // after `max_regular` bytes of regular files (at least one entry), at the end
 // of the archive (*at_end) or on a malformed header (-1).
-int IndexEntries(const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window, uint64_t max_regular, int threads,
-                 std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
+int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
+                 uint64_t max_regular, int threads, std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
   out->clear();
   *at_end = false;
   const uint64_t end = std::min<uint64_t>(n, p + window);
@@ -500,6 +569,7 @@ int IndexEntries(const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window, ui
   std::vector<std::vector<TarEntry>> spec(segs);
   tsg::ParallelFor(segs, threads, [&](size_t s) {
     const uint64_t a = p + s * seg, b = std::min(end, a + seg);
+    spec[s].reserve(size_t(seg / 2048) + 8);
     uint64_t q = a;
     if (s > 0) {  // first block that parses as a header (512-aligned from p)
       while (q + 512 <= b && (AllZero(tar + q) || !ChecksumOK(tar + q))) q += 512;
@@ -508,37 +578,70 @@ int IndexEntries(const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window, ui
       TarEntry e;
       if (ChainEntry(tar, n, q, &e) != 0) break;  // end marker or garbage: the merge decides
       q = e.next;
+      Evaluate(c, tar, &e);
       spec[s].push_back(std::move(e));
     }
   });
+  // The merge plans ranges of the speculative vectors (and of the rare
+  // sequential fallbacks) first, reading only positions and sizes; the
+  // entries are then moved into *out in parallel.
+  struct Range {
+    std::vector<TarEntry>* v;
+    size_t lo, hi;
+  };
+  std::vector<Range> plan;
+  std::vector<std::vector<TarEntry>> fallback;
+  fallback.reserve(segs);
   uint64_t cur = p, regular = 0;
-  for (size_t s = 0; s < segs; s++) {
+  bool ended = false;
+  for (size_t s = 0; s < segs && !ended; s++) {
     const uint64_t b = std::min(end, p + (s + 1) * seg);
     if (cur >= b) continue;
     auto& v = spec[s];
     auto it = std::lower_bound(v.begin(), v.end(), cur, [](const TarEntry& e, uint64_t x) { return e.start < x; });
     if (it != v.end() && it->start == cur) {
-      for (; it != v.end(); ++it) {
-        cur = it->next;
-        if (it->what == 3) regular += it->size + 512;
-        out->push_back(std::move(*it));
+      const size_t lo = size_t(it - v.begin());
+      size_t i = lo;
+      for (; i < v.size();) {
+        cur = v[i].next;
+        if (v[i].what == 3) regular += v[i].size + 512;
+        i++;
         if (regular > max_regular) break;
       }
+      plan.push_back({&v, lo, i});
     }
-    while (cur < b && regular <= max_regular) {  // sequential from the true position
-      TarEntry e;
-      const int r = ChainEntry(tar, n, cur, &e);
-      if (r < 0) return -1;
-      if (r == 1) {
-        *at_end = true;
-        *next = cur;
-        return 0;
+    if (cur < b && regular <= max_regular) {  // sequential from the true position
+      fallback.emplace_back();
+      auto& fb = fallback.back();
+      while (cur < b && regular <= max_regular) {
+        TarEntry e;
+        const int r = ChainEntry(tar, n, cur, &e);
+        if (r < 0) return -1;
+        if (r == 1) {
+          *at_end = true;
+          ended = true;
+          break;
+        }
+        cur = e.next;
+        Evaluate(c, tar, &e);
+        if (e.what == 3) regular += e.size + 512;
+        fb.push_back(std::move(e));
       }
-      cur = e.next;
-      if (e.what == 3) regular += e.size + 512;
-      out->push_back(std::move(e));
+      plan.push_back({&fb, 0, fb.size()});
     }
     if (regular > max_regular) break;
+  }
+  {
+    std::vector<size_t> at(plan.size() + 1, 0);
+    for (size_t k = 0; k < plan.size(); k++) at[k + 1] = at[k] + (plan[k].hi - plan[k].lo);
+    out->resize(at.back());
+    tsg::ParallelFor(plan.size(), threads, [&](size_t k) {
+      for (size_t i = plan[k].lo; i < plan[k].hi; i++) (*out)[at[k] + (i - plan[k].lo)] = std::move((*plan[k].v)[i]);
+    });
+  }
+  if (ended) {
+    *next = cur;
+    return 0;
   }
   if (out->empty() || (cur >= n && !*at_end)) {  // nothing in the window (a huge entry) or the tail
     while (out->empty() || (cur < n && regular <= max_regular && out->size() < 1)) {
@@ -550,6 +653,7 @@ int IndexEntries(const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window, ui
         break;
       }
       cur = e.next;
+      Evaluate(c, tar, &e);
       out->push_back(std::move(e));
     }
   }
@@ -573,11 +677,21 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
   if (e->long_len != ~uint64_t(0)) {
     e->fp = CStr(tar + e->long_off, size_t(e->long_len));
   } else {
-    e->fp = CStr(h, 100);
-    if (std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0) {
-      const std::string prefix = CStr(h + 345, 155);
-      if (!prefix.empty()) e->fp = prefix + "/" + e->fp;
+    auto clen = [](const uint8_t* b, size_t n) {
+      size_t k = 0;
+      while (k < n && b[k]) k++;
+      return k;
+    };
+    const size_t nl = clen(h, 100);
+    size_t pl = 0;
+    if (std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0) pl = clen(h + 345, 155);
+    e->fp.clear();
+    e->fp.reserve(pl + 1 + nl);
+    if (pl) {
+      e->fp.append(reinterpret_cast<const char*>(h + 345), pl);
+      e->fp.push_back('/');
     }
+    e->fp.append(reinterpret_cast<const char*>(h), nl);
   }
 }
 
@@ -586,10 +700,10 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
 void Classify(const uint8_t* tar, TarEntry* e) {
   Resolve(tar, e);
   if (tar[e->hdr + 156] == '\0' && !e->fp.empty() && e->fp.back() == '/') e->what = 0;  // TypeRegA dir
-  std::string fp = tsg::GoPathClean(e->fp);
+  if (!tsg::GoPathIsClean(e->fp.data(), e->fp.size())) e->fp = tsg::GoPathClean(e->fp);
   size_t t = 0;
-  while (t < fp.size() && fp[t] == '/') t++;
-  e->fp = fp.substr(t);
+  while (t < e->fp.size() && e->fp[t] == '/') t++;
+  if (t) e->fp.erase(0, t);
   const size_t slash = e->fp.rfind('/');
   const char* file_name = e->fp.c_str() + (slash == std::string::npos ? 0 : slash + 1);
   if (std::strcmp(file_name, ".wh..wh..opq") == 0) e->what = 2;
@@ -599,8 +713,8 @@ void Classify(const uint8_t* tar, TarEntry* e) {
 
 extern "C" {
 
-// The walk runs in rounds: index the entries ahead (headers only, ~1.5x the
-// room left in the batch), classify them on the ingest threads (Required,
+// The walk runs in rounds: index the entries ahead (~1.5x the room left in
+// the batch) and evaluate each on the thread that found it (name, Required,
 // binary gate, transformed length), accept the longest prefix that fits, copy
 // and transform the accepted contents on the threads.  Entries past the
 // accepted prefix are re-read from *cursor by the next call.
@@ -617,28 +731,11 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     double t0 = dbg ? now() : 0;
     const uint64_t room = c->limit > c->used ? c->limit - c->used : 0;
     bool at_end = false;
-    if (IndexEntries(tar, n, p, 2 * room + (1 << 20), room + room / 2, c->threads, &ents, &p, &at_end) < 0)
+    if (IndexEntries(c, tar, n, p, 2 * room + (1 << 20), room + room / 2, c->threads, &ents, &p, &at_end) < 0)
       return -1;
     double t1 = dbg ? now() : 0;
-    // 2. classify (AnalyzeFile's Required + Analyze's binary gate)
-    const size_t kBlock = 64;
-    tsg::ParallelFor((ents.size() + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
-      for (size_t i = b * kBlock; i < std::min(ents.size(), (b + 1) * kBlock); i++) {
-        TarEntry& e = ents[i];
-        e.state = 0;
-        Classify(tar, &e);
-        if (e.what != 3 || !Required(c->a, e.fp.data(), e.fp.size(), int64_t(e.size))) continue;
-        const uint8_t* d = tar + e.data;
-        e.bin = tsg::IsBinaryHead(d, e.size) ? 1 : 0;
-        if (e.bin && tsg::GoExt(e.fp) != ".pyc") {
-          e.state = 1;
-          continue;
-        }
-        e.state = 2;
-        e.out_len = e.bin ? tsg::PrintableLen(d, e.size) : e.size - tsg::CountCR(d, e.size);
-      }
-    });
     double t2 = dbg ? now() : 0;
+    const size_t kBlock = 64;
     // 3. accept in order
     size_t k = 0;
     bool full = false;
@@ -649,13 +746,19 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         return -1;
       }
       if (e.state == 2) {
-        if (c->files() > 0 && c->used + e.out_len > c->limit) {
+        if (c->files() > 0 && c->acct() + e.out_len > c->limit) {
           full = true;
           break;
         }
         if (c->used + e.out_len + 64 > c->cap && !c->Reserve(e.out_len + 64)) return -1;  // a lone large file
         e.out_off = c->used;
-        c->used += e.out_len;
+        if (c->gpu_xform) {
+          c->used += e.size;
+          c->bound += e.out_len;
+          c->kinds.push_back(e.bin ? 2 : 1);
+        } else {
+          c->used += e.out_len;
+        }
         c->offs.push_back(c->used);
         c->path_pool.push_back('/');  // Dir "" (image files, secret.go:130-135)
         c->path_pool.append(e.fp);
@@ -679,7 +782,8 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         const TarEntry& e = ents[i];
         if (e.state != 2) continue;
         uint8_t* dst = c->arena + e.out_off;
-        if (e.bin) tsg::ExtractPrintable(tar + e.data, e.size, dst);
+        if (c->gpu_xform) std::memcpy(dst, tar + e.data, e.size);
+        else if (e.bin) tsg::ExtractPrintable(tar + e.data, e.size, dst);
         else tsg::StripCR(tar + e.data, e.size, dst);
       }
     });
@@ -714,6 +818,22 @@ int tsg_collector_file(const tsg_collector* c, uint32_t i, const char** path, ui
   *content = c->arena + c->offs[i];
   *len = c->offs[i + 1] - c->offs[i];
   *binary = c->binary[i];
+  if (c->gpu_xform) {  // as it will be scanned: transformed here (tests / host-language mirror only)
+    const uint64_t n = *len;
+    c->scratch.resize(size_t(n + n / 5 + 2));
+    *len = c->kinds[i] == 2 ? tsg::ExtractPrintable(*content, n, c->scratch.data())
+                            : tsg::StripCR(*content, n, c->scratch.data());
+    *content = c->scratch.data();
+  }
+  return 0;
+}
+
+int tsg_collector_set_gpu_transform(tsg_collector* c, int on) {
+  if (c->files() > 0) {
+    tsg::SetError("tsg_collector_set_gpu_transform: the batch is not empty");
+    return -1;
+  }
+  c->gpu_xform = on != 0;
   return 0;
 }
 
@@ -726,6 +846,7 @@ int tsg_collector_submit(tsg_collector* c, tsg_pending** out) {
   b.paths = c->path_ptrs.data();
   b.path_lens = c->path_lens.data();
   b.binary = c->binary.data();
+  b.transform = c->gpu_xform ? c->kinds.data() : nullptr;
   return tsg_scan_submit(const_cast<tsg_scanner*>(c->a->s), &b, out);
 }
 

@@ -246,6 +246,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   in.paths = b->paths;
   in.path_lens = b->path_lens;
   in.binary = b->binary;
+  in.transform = b->transform;
   std::unique_ptr<tsg_result> r(new tsg_result());
   r->owner = s->s.get();
   tsg::BatchStats gs;
@@ -282,6 +283,7 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   st.h2d_chunks = gs.h2d_chunks;
   st.fullscan_pairs = gs.fullscan_tasks;
   st.fold_sites = gs.fold_sites;
+  st.ms_xform_kernel = gs.ms_xform;
   *out = r.release();
   return 0;
 }

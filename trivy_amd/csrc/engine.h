@@ -26,6 +26,15 @@ struct Candidate {      // produced by the verify / full-scan kernels
   uint32_t pad;
 };
 
+// The transformed bytes of chosen files of a host batch whose transform ran
+// on the GPU (RunHost with kinds): buf holds them in file order, off is a
+// full n_files+1 offset table into buf (files not chosen are empty).
+struct TailOut {
+  std::vector<uint8_t> buf;
+  std::vector<uint64_t> off;
+  uint64_t xform_bytes = 0;  // transformed arena bytes of the whole batch
+};
+
 struct BatchStats {
   uint64_t bytes = 0, files = 0, hits = 0, candidates = 0, special_files = 0, fullscan_tasks = 0, fold_sites = 0;
   uint64_t flagged_blocks = 0;
@@ -33,6 +42,7 @@ struct BatchStats {
   float ms_scan = 0, ms_confirm = 0, ms_careful = 0, ms_verify = 0, ms_fullscan = 0, ms_total = 0;
   float ms_finalize = 0, ms_chunkmap = 0;
   float ms_h2d_span = 0;  // RunHost: first copy issued -> last chunk done (the ingest-inclusive GPU time)
+  float ms_xform = 0;     // RunHost with kinds: pre-transform kernels (part of ms_total)
   uint64_t h2d_chunks = 0;
   bool hit_overflow = false, cand_overflow = false;
 };
@@ -54,8 +64,12 @@ class GpuEngine {
 
   // Host-resident batch (PCIe-inclusive path): streamed in chunks through two
   // device staging buffers, copies overlapping the previous chunk's kernels.
+  // With kinds (per file, xform.h), h_arena holds the bytes as read: each
+  // chunk is transformed on the GPU before the scan, and the transformed
+  // bytes of the files that got candidates come back in *tail.
   bool RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
-               std::vector<Candidate>* cands, BatchStats* st);
+               std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds = nullptr,
+               TailOut* tail = nullptr);
 
   // Device buffers of the last run (for tests / bench).
   hipEvent_t ev_scan0() const { return ev_[1]; }
@@ -63,6 +77,10 @@ class GpuEngine {
 
  private:
   bool Ensure(void** p, size_t* cap, size_t need);
+  bool Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
+                 std::vector<uint64_t>* xoff, float* ms);
+  bool GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf, const std::vector<uint64_t>& xoff,
+                  std::vector<uint64_t>* tail_len, TailOut* tail);
   void DumpItemDiag();
   std::vector<uint8_t> h_items_kind_;
   std::vector<uint32_t> h_items_id_;
@@ -111,6 +129,16 @@ class GpuEngine {
   void* d_stage_[2] = {}; size_t cap_stage_[2] = {};
   void* d_stage_off_[2] = {}; size_t cap_stage_off_[2] = {};
   uint64_t* h_off_[2] = {}; size_t cap_h_off_[2] = {};  // pinned, rebased chunk offsets
+  // GPU pre-transform (xform.h): per-chunk kinds, lengths, transformed offsets and bytes, the gather
+  void* d_kind_[2] = {}; size_t cap_kind_[2] = {};
+  void* d_xlen_ = nullptr; size_t cap_xlen_ = 0;
+  void* d_xoff_ = nullptr; size_t cap_xoff_ = 0;
+  void* d_xscan_ = nullptr; size_t cap_xscan_ = 0;
+  void* d_xf_ = nullptr; size_t cap_xf_ = 0;
+  void* d_gfiles_ = nullptr; size_t cap_gfiles_ = 0;
+  void* d_gdst_ = nullptr; size_t cap_gdst_ = 0;
+  void* d_gbuf_ = nullptr; size_t cap_gbuf_ = 0;
+  hipEvent_t ev_x_[2] = {};
   uint64_t chunk_bytes_ = uint64_t(1) << 30;             // TSG_INGEST_CHUNK_MB
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
   uint32_t fs_chunk_ = 65536;         // TSG_FULLSCAN_CHUNK: full-scan bytes per lane (min)

@@ -27,6 +27,7 @@
 #include <thread>
 
 #include "engine.h"
+#include "xform.h"
 #include "filter.h"
 
 namespace tsg {
@@ -1324,6 +1325,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   }
   for (auto& e : ev_copied_) hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : ev_h2d_) hipEventCreate(&e);
+  for (auto& e : ev_x_) hipEventCreate(&e);
   if (const char* cm = std::getenv("TSG_INGEST_CHUNK_MB")) chunk_bytes_ = uint64_t(std::atoll(cm)) << 20;
   if (chunk_bytes_ < (uint64_t(1) << 20)) chunk_bytes_ = uint64_t(1) << 20;
   for (auto& e : ev_) hipEventCreate(&e);
@@ -1472,7 +1474,8 @@ GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
   void* ps[] = {d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
-                d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1]};
+                d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1],
+                d_kind_[0], d_kind_[1], d_xlen_, d_xoff_, d_xscan_, d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
   for (void* p : ps)
     if (p) hipFree(p);
   for (auto& e : ev_)
@@ -1481,6 +1484,8 @@ GpuEngine::~GpuEngine() {
     if (e) hipEventDestroy(e);
   if (ev_fs_) hipEventDestroy(ev_fs_);
   for (auto& e : ev_h2d_)
+    if (e) hipEventDestroy(e);
+  for (auto& e : ev_x_)
     if (e) hipEventDestroy(e);
   for (auto* h : h_off_)
     if (h) hipHostFree(h);
@@ -1511,7 +1516,7 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
 // done (measured, profiles/r02_ingest_trace_*), which would otherwise keep the
 // scan thread from launching chunk k's kernels during chunk k+1's copy.
 bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
-                        std::vector<Candidate>* cands, BatchStats* st) {
+                        std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail) {
   HIP_OK(hipSetDevice(device_));
   cands->clear();
   BatchStats local;
@@ -1519,7 +1524,18 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
   *st = BatchStats();
   st->bytes = n_bytes;
   st->files = n_files;
+  if (tail) {
+    tail->buf.clear();
+    tail->off.assign(size_t(n_files) + 1, 0);
+    tail->xform_bytes = 0;
+  }
+  if (kinds && !tail) {
+    err_ = "RunHost: a transformed batch needs a tail output";
+    return false;
+  }
   if (n_files == 0) return true;
+  std::vector<uint64_t> tail_len;  // per file: transformed bytes kept for the host (0: not a candidate file)
+  if (kinds) tail_len.assign(n_files, 0);
   // chunk boundaries (file indices)
   std::vector<uint32_t> cut{0};
   for (uint32_t f = 0; f < n_files; f++) {
@@ -1535,7 +1551,8 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
   }
   for (int b = 0; b < 2 && b < int(n_chunks); b++) {
     if (!Ensure(&d_stage_[b], &cap_stage_[b], max_bytes + 64) ||
-        !Ensure(&d_stage_off_[b], &cap_stage_off_[b], (max_files + 1) * 8))
+        !Ensure(&d_stage_off_[b], &cap_stage_off_[b], (max_files + 1) * 8) ||
+        (kinds && !Ensure(&d_kind_[b], &cap_kind_[b], max_files + 1)))
       return false;
     if (cap_h_off_[b] < max_files + 1) {
       if (h_off_[b]) hipHostFree(h_off_[b]);
@@ -1556,6 +1573,8 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     HIP_OK(hipMemsetAsync(d + (e - a), 0, 64, copy_stream_));
     HIP_OK(hipMemcpyAsync(d_stage_off_[b], h_off_[b], (size_t(f1 - f0) + 1) * 8, hipMemcpyHostToDevice,
                           copy_stream_));
+    if (kinds)
+      HIP_OK(hipMemcpyAsync(d_kind_[b], kinds + f0, size_t(f1 - f0), hipMemcpyHostToDevice, copy_stream_));
     HIP_OK(hipEventRecord(ev_copied_[b], copy_stream_));
     return true;
   };
@@ -1582,10 +1601,27 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     HIP_OK(hipStreamWaitEvent(stream_, ev_copied_[b], 0));
     const uint32_t f0 = cut[k], f1 = cut[k + 1];
     BatchStats cs;
-    if (!Run(static_cast<const uint8_t*>(d_stage_[b]), h_offsets[f1] - h_offsets[f0],
-             static_cast<const uint64_t*>(d_stage_off_[b]), f1 - f0, &part, &cs)) {
+    const uint8_t* scan_arena = static_cast<const uint8_t*>(d_stage_[b]);
+    const uint64_t* scan_off = static_cast<const uint64_t*>(d_stage_off_[b]);
+    uint64_t scan_bytes = h_offsets[f1] - h_offsets[f0];
+    std::vector<uint64_t> xoff;
+    float ms_x = 0;
+    if (kinds && !Transform(b, f1 - f0, &scan_arena, &scan_off, &scan_bytes, &xoff, &ms_x)) {
       if (copier.joinable()) copier.join();
       return false;
+    }
+    if (!Run(scan_arena, scan_bytes, scan_off, f1 - f0, &part, &cs)) {
+      if (copier.joinable()) copier.join();
+      return false;
+    }
+    if (kinds) {
+      st->ms_xform += ms_x;
+      cs.ms_total += ms_x;
+      tail->xform_bytes += scan_bytes;
+      if (!GatherTail(part, f0, f1 - f0, xoff, &tail_len, tail)) {
+        if (copier.joinable()) copier.join();
+        return false;
+      }
     }
     for (auto c : part) {
       c.file += f0;
@@ -1613,6 +1649,79 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
   HIP_OK(hipEventSynchronize(ev_h2d_[1]));
   hipEventElapsedTime(&st->ms_h2d_span, ev_h2d_[0], ev_h2d_[1]);
   st->h2d_chunks = n_chunks;
+  if (kinds)
+    for (uint32_t f = 0; f < n_files; f++) tail->off[f + 1] = tail->off[f] + tail_len[f];
+  return true;
+}
+
+// Pre-transform of the chunk in staging buffer b (xform.h): lengths, their
+// prefix sums (the transformed offsets, also copied back to *xoff), the
+// compaction into d_xf_.  Points the scan at the transformed arena.
+bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
+                          std::vector<uint64_t>* xoff, float* ms) {
+  size_t scan_bytes = 0;
+  HIP_OK(XformScanBytes(nf, &scan_bytes));
+  if (!Ensure(&d_xlen_, &cap_xlen_, (size_t(nf) + 1) * 8) || !Ensure(&d_xoff_, &cap_xoff_, (size_t(nf) + 1) * 8) ||
+      !Ensure(&d_xscan_, &cap_xscan_, scan_bytes + 16))
+    return false;
+  const uint8_t* raw = static_cast<const uint8_t*>(d_stage_[b]);
+  const uint64_t* off = static_cast<const uint64_t*>(d_stage_off_[b]);
+  const uint8_t* kd = static_cast<const uint8_t*>(d_kind_[b]);
+  uint64_t* xo = static_cast<uint64_t*>(d_xoff_);
+  HIP_OK(hipEventRecord(ev_x_[0], stream_));
+  HIP_OK(XformLengths(raw, off, kd, nf, static_cast<uint64_t*>(d_xlen_), stream_));
+  HIP_OK(XformScan(d_xscan_, scan_bytes, static_cast<const uint64_t*>(d_xlen_), xo, nf, stream_));
+  xoff->resize(size_t(nf) + 1);
+  HIP_OK(hipMemcpyAsync(xoff->data(), xo, (size_t(nf) + 1) * 8, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  const uint64_t total = (*xoff)[nf];
+  if (!Ensure(&d_xf_, &cap_xf_, total + 64)) return false;
+  uint8_t* out = static_cast<uint8_t*>(d_xf_);
+  HIP_OK(XformCopy(raw, off, kd, nf, xo, out, stream_));
+  HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));
+  HIP_OK(hipEventRecord(ev_x_[1], stream_));
+  HIP_OK(hipEventSynchronize(ev_x_[1]));
+  hipEventElapsedTime(ms, ev_x_[0], ev_x_[1]);
+  *arena = out;
+  *offsets = xo;
+  *n_bytes = total;
+  return true;
+}
+
+// The transformed bytes of the chunk's files with candidates -> tail->buf
+// (appended in file order); their lengths -> (*tail_len)[f0 + f].
+bool GpuEngine::GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf,
+                           const std::vector<uint64_t>& xoff, std::vector<uint64_t>* tail_len, TailOut* tail) {
+  std::vector<uint32_t> files;
+  files.reserve(part.size());
+  for (const auto& c : part) files.push_back(c.file);
+  std::sort(files.begin(), files.end());
+  files.erase(std::unique(files.begin(), files.end()), files.end());
+  if (files.empty()) return true;
+  std::vector<uint64_t> dst(files.size());
+  uint64_t total = 0;
+  for (size_t i = 0; i < files.size(); i++) {
+    if (files[i] >= nf) {
+      err_ = "candidate file outside its chunk";
+      return false;
+    }
+    dst[i] = total;
+    const uint64_t len = xoff[files[i] + 1] - xoff[files[i]];
+    (*tail_len)[f0 + files[i]] = len;
+    total += len;
+  }
+  if (!Ensure(&d_gfiles_, &cap_gfiles_, files.size() * 4) || !Ensure(&d_gdst_, &cap_gdst_, files.size() * 8) ||
+      !Ensure(&d_gbuf_, &cap_gbuf_, total + 64))
+    return false;
+  HIP_OK(hipMemcpyAsync(d_gfiles_, files.data(), files.size() * 4, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_gdst_, dst.data(), dst.size() * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(GatherFiles(static_cast<const uint8_t*>(d_xf_), static_cast<const uint64_t*>(d_xoff_),
+                     static_cast<const uint32_t*>(d_gfiles_), static_cast<const uint64_t*>(d_gdst_),
+                     uint32_t(files.size()), static_cast<uint8_t*>(d_gbuf_), stream_));
+  const size_t at = tail->buf.size();
+  tail->buf.resize(at + total);
+  HIP_OK(hipMemcpyAsync(tail->buf.data() + at, d_gbuf_, total, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
   return true;
 }
 

@@ -867,18 +867,30 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   });
   bool ok;
   std::string gpu_err;
+  TailOut tail;  // GPU pre-transform: the transformed bytes of the files with candidates
+  if (in.transform && in.dev_arena) {
+    allow_thread.join();
+    *err = "a pre-transformed batch must be host-resident";
+    return false;
+  }
   {
     std::lock_guard<std::mutex> g(gpu_mu_[slot]);
     if (in.dev_arena)
       ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
     else
-      ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst);
+      ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
+                           in.transform ? &tail : nullptr);
     if (!ok) gpu_err = engine->error();
   }
   allow_thread.join();
   if (!ok) {
     *err = gpu_err;
     return false;
+  }
+  BatchInput tin = in;  // the exact pass reads the transformed bytes
+  if (in.transform) {
+    tin.host_arena = tail.buf.data();
+    tin.host_offsets = tail.off.data();
   }
   double t1 = NowMs();
   if (const char* dump = std::getenv("TSG_DUMP_CANDS")) {  // profiling aid (tools/host_tail_bench.py)
@@ -887,7 +899,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
       std::fclose(fp);
     }
   }
-  HostTail(in, &cands, out, &hs, &allowed);
+  HostTail(tin, &cands, out, &hs, &allowed);
   hs.ms_allow = ms_allow;  // overlapped with the GPU phase
   hs.ms_gpu = t1 - t0;
   hs.ms_total = NowMs() - t0;

@@ -110,6 +110,8 @@ struct BatchInput {
   const char* const* paths = nullptr;
   const uint64_t* path_lens = nullptr;  // optional (else strlen)
   const uint8_t* binary = nullptr;      // optional per-file Binary flag
+  const uint8_t* transform = nullptr;   // optional per-file pre-transform (xform.h) run on the GPU: then
+                                        // host_arena holds the bytes as read (host-resident batches only)
 };
 
 struct HostStats {

@@ -40,7 +40,7 @@ class _CGlobal(c.Structure):
 class _CBatch(c.Structure):
     _fields_ = [("n_files", c.c_uint32), ("host_arena", c.c_void_p), ("host_offsets", c.c_void_p),
                 ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.c_void_p),
-                ("path_lens", c.c_void_p), ("binary", c.c_void_p)]
+                ("path_lens", c.c_void_p), ("binary", c.c_void_p), ("transform", c.c_void_p)]
 
 
 class _CStats(c.Structure):
@@ -53,7 +53,8 @@ class _CStats(c.Structure):
                 ("follow_hits", c.c_uint64)] + \
                [(n, c.c_double) for n in ("ms_chunkmap_kernel", "ms_confirm_kernel", "ms_nfa_kernel",
                                           "ms_finalize_kernel", "ms_h2d_span")] + \
-               [("h2d_chunks", c.c_uint64), ("fullscan_pairs", c.c_uint64), ("fold_sites", c.c_uint64)]
+               [("h2d_chunks", c.c_uint64), ("fullscan_pairs", c.c_uint64), ("fold_sites", c.c_uint64),
+                ("ms_xform_kernel", c.c_double)]
 
 
 class _CTableInfo(c.Structure):
