@@ -794,7 +794,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       t_phase[1] += t2 - t1;
       t_phase[2] += t3 - t2;
       t_phase[3] += t4 - t3;
-      std::fprintf(stderr, "walk phases (cumulative s): index %.3f classify %.3f accept %.3f copy %.3f\n", t_phase[0],
+      std::fprintf(stderr, "walk phases (cumulative s): index+evaluate %.3f (classify %.3f) accept %.3f copy %.3f\n", t_phase[0],
                    t_phase[1], t_phase[2], t_phase[3]);
     }
     if (full) {
