@@ -292,6 +292,17 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
     : rules_(std::move(rules)), allow_(std::move(allow)), exclude_(std::move(exclude)) {
   std::vector<RuleSrc> src;
   for (auto& r : rules_) src.push_back({r.id, r.regex_src, r.keywords, r.has_regex});
+  for (size_t g = 0; g < exclude_.size(); g++) {
+    ex_global_rule_.push_back(uint32_t(src.size()));
+    src.push_back({"exclude-block:global:" + std::to_string(g), exclude_[g]->pattern(), {}, true});
+  }
+  ex_rule_.resize(rules_.size());
+  for (size_t r = 0; r < rules_.size(); r++)
+    for (size_t k = 0; k < rules_[r].exclude.size(); k++) {
+      ex_rule_[r].push_back(uint32_t(src.size()));
+      src.push_back({"exclude-block:" + rules_[r].id + ":" + std::to_string(k), rules_[r].exclude[k]->pattern(), {},
+                     true});
+    }
   if (!CompileRules(src, &cr_, &err_)) {
     *err = err_;
     return;
@@ -516,7 +527,7 @@ struct PhaseTimer {
 };
 
 void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
-                             const Candidate* c, size_t nc, FileResult* out) const {
+                             const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const {
   PhaseTimer pt_all(7);
   const uint8_t* P = reinterpret_cast<const uint8_t*>(path.data());
   std::vector<std::pair<uint32_t, Loc>> matched;
@@ -531,13 +542,32 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
   std::sort(nla.begin(), nla.end());
 
-  auto blocks_match = [&](const std::vector<std::unique_ptr<Regex>>& rx, std::vector<Loc>* cache, bool* done,
-                          Loc loc) {
+  // the candidates are sorted by rule: real rules first, then the exclude-block rules
+  const uint32_t n_real = uint32_t(rules_.size());
+  size_t nc_real = 0;
+  while (nc_real < nc && c[nc_real].rule < n_real) nc_real++;
+  auto block_windows = [&](uint32_t rule, std::vector<Window>* wins) {  // merged candidate windows of a block rule
+    for (size_t k = nc_real; k < nc; k++) {
+      if (c[k].rule != rule) continue;
+      Window w{c[k].wlo, c[k].whi};
+      if (!wins->empty() && w.lo <= wins->back().hi + 1) wins->back().hi = std::max(wins->back().hi, w.hi);
+      else wins->push_back(w);
+    }
+  };
+  auto blocks_match = [&](const std::vector<std::unique_ptr<Regex>>& rx, const std::vector<uint32_t>& rx_rule,
+                          std::vector<Loc>* cache, bool* done, Loc loc) {
     if (!*done) {
       *done = true;
-      for (auto& r : rx) {
+      for (size_t q = 0; q < rx.size(); q++) {
         std::vector<int64_t> m;
-        r->FindAll(content, len, false, nullptr, &m);
+        if (gpu_windows) {  // Blocks.find (scanner.go:262-275) where a block can start
+          std::vector<Window> wins;
+          block_windows(rx_rule[q], &wins);
+          if (wins.empty()) continue;
+          rx[q]->FindAll(content, len, false, &wins, &m);
+        } else {
+          rx[q]->FindAll(content, len, false, nullptr, &m);
+        }
         for (size_t k = 0; k + 1 < m.size(); k += 2) cache->push_back({m[k], m[k + 1]});
       }
     }
@@ -547,12 +577,12 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   };
 
   size_t i = 0;
-  while (i < nc) {
+  while (i < nc_real) {
     uint32_t r = c[i].rule;
     size_t j = i;
     std::vector<Window> wins;
     uint32_t group_flags = ~0u;  // AND over the group's candidates (file-level bits agree)
-    while (j < nc && c[j].rule == r) {
+    while (j < nc_real && c[j].rule == r) {
       group_flags &= c[j].flags;
       Window w{c[j].wlo, c[j].whi};
       if (!wins.empty() && w.lo <= wins.back().hi + 1) wins.back().hi = std::max(wins.back().hi, w.hi);
@@ -669,8 +699,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     bool lblocks_done = false;
     std::vector<Loc> lblocks;
     for (auto& loc : locs) {
-      if (blocks_match(exclude_, &gblocks, &gblocks_done, loc) ||
-          blocks_match(R.exclude, &lblocks, &lblocks_done, loc))
+      if (blocks_match(exclude_, ex_global_rule_, &gblocks, &gblocks_done, loc) ||
+          blocks_match(R.exclude, ex_rule_[r], &lblocks, &lblocks_done, loc))
         continue;
       if (loc.s < 0) continue;  // non-participating group: the reference would panic here
       matched.push_back({r, loc});
@@ -899,7 +929,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
       std::fclose(fp);
     }
   }
-  HostTail(tin, &cands, out, &hs, &allowed);
+  HostTail(tin, &cands, out, &hs, &allowed, true);
   hs.ms_allow = ms_allow;  // overlapped with the GPU phase
   hs.ms_gpu = t1 - t0;
   hs.ms_total = NowMs() - t0;
@@ -928,7 +958,7 @@ std::vector<uint8_t> SecretScanner::AllowedPaths(const BatchInput& in) const {
 }
 
 void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, BatchResult* out,
-                             HostStats* hs, const std::vector<uint8_t>* allowed_pre) const {
+                             HostStats* hs, const std::vector<uint8_t>* allowed_pre, bool gpu_windows) const {
   std::vector<Candidate>& cands = *cands_p;
   out->kind.assign(in.n_files, uint8_t(kNoFindings));
   out->found_files.clear();
@@ -972,7 +1002,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
     uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
     ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string(p, pn), in.binary && in.binary[f], &cands[a],
-             b - a, &tmp[k]);
+             b - a, &tmp[k], gpu_windows);
   });
   const double t_par = NowMs();
   if (g_tail_debug)

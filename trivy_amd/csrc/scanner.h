@@ -139,8 +139,11 @@ class SecretScanner {
   // The exact host tail over a given candidate list (what Scan runs after the GPU).
   // The exact host pass over the GPU's candidates.  `allowed` (per-file
   // global AllowPath results) is computed here when not supplied.
+  // gpu_windows: the candidates came from the GPU engine, so the exclude-block
+  // regexes (compiled as extra rules) have candidate windows too; otherwise
+  // (host-only callers) each exclude regex sweeps the whole file.
   void HostTail(const BatchInput& in, std::vector<Candidate>* cands, BatchResult* out, HostStats* hs,
-                const std::vector<uint8_t>* allowed = nullptr) const;
+                const std::vector<uint8_t>* allowed = nullptr, bool gpu_windows = false) const;
   std::vector<uint8_t> AllowedPaths(const BatchInput& in) const;
   // Global.AllowPath (scanner.go:57-59)
   bool AllowPath(const uint8_t* p, size_t n) const;
@@ -153,8 +156,14 @@ class SecretScanner {
 
  private:
   void ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
-                const Candidate* c, size_t nc, FileResult* out) const;
+                const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const;
   std::vector<RuleSpec> rules_;
+  // Exclude-block regexes (scanner.go:237-275) are compiled after the rules as
+  // extra GPU rules without keywords: their candidates bound where a block can
+  // start, so the host's FindAll of each block regex runs on windows instead
+  // of the whole file.  Rule index of global block regex g / rule r's k-th.
+  std::vector<uint32_t> ex_global_rule_;
+  std::vector<std::vector<uint32_t>> ex_rule_;
   std::vector<AllowRuleSpec> allow_;
   std::vector<std::unique_ptr<Regex>> exclude_;
   CompiledRules cr_;
