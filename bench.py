@@ -218,6 +218,8 @@ WORKLOADS = {
     # (description, GB per GPU, CPU-baseline sample MB, oracle parity sample MB)
     "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
            20.0, 64.0, 24.0),
+    "c5": ("%g GB per MI355X per step (1 TB over 8 GPUs) streamed host->HBM from a page-locked pool of "
+           "mean-64-KiB files re-emitted with distinct ids, builtin rules (BASELINE configs[4])", 125.0, 64.0, 24.0),
     "c3": ("2,000 generated custom rules (trivy-secret.yaml) + 87 builtins over a %g GB synthetic corpus per "
            "MI355X (BASELINE configs[2])", 8.0, 2.0, 0.4),
     "c3u": ("C3 variant: 2,000 generated custom rules of which ~10 %% have no literal anchor (keyword-gated "
@@ -245,6 +247,7 @@ def main():
     ap.add_argument("--transform", choices=["gpu", "host"], default="gpu",
                     help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
                          "the walk's host threads")
+    ap.add_argument("--pool-gb", type=float, default=64.0, help="c5: page-locked host pool size")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     args = ap.parse_args()
     wl_desc, gb_default, cpu_mb_default, parity_mb_default = WORKLOADS[args.workload]
@@ -282,11 +285,16 @@ def main():
         C = corpus.generate_c3(int(args.gb * 1e9), samples, seed=corpus.SEED + rank)
     elif args.workload == "c4":
         layer = corpus.generate_layer(int(args.gb * 1e9), seed=corpus.SEED + rank)
+    elif args.workload == "c5":  # the pool, emitted `emissions` times per step through the ingest path
+        pool_gb = min(args.pool_gb, args.gb)
+        C = corpus.generate(int(pool_gb * 1e9), seed=corpus.SEED + rank, size_scale=2.6)
+        args.ingest = True
     else:
         C = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank)
     t_gen = time.time() - t_gen
 
     h2d_peak = None
+    emissions = 1
     if layer is None:
         dev = torch.device("cuda", local)
         if args.ingest:
@@ -309,12 +317,14 @@ def main():
             return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(),
                                        dev_offsets=d_offs.data_ptr())
 
+        emissions = max(1, int(round(args.gb * 1e9 / C.n_bytes))) if args.workload == "c5" else 1
+
         def run_steps(n, stats):
             # pipelined: step i+1's kernels run while step i's exact host pass finishes
             # (tsg_scan_submit; --depth 1 runs the steps back to back)
             inflight = []
             r = None
-            for _ in range(n):
+            for _ in range(n * emissions):  # c5: the pool once per emission (distinct ids: emission, file)
                 inflight.append(submit())
                 if len(inflight) >= args.depth:
                     r = inflight.pop(0).wait()
@@ -373,12 +383,13 @@ def main():
     breakdown.update({k: round(avg(k), 3) for k in ("ms_fullscan_kernel", "ms_gpu_total", "ms_host_gpu_phase",
                                                      "ms_host_exact")})
     if layer is None:
-        n_bytes, n_files = C.n_bytes, C.n_files
-        arena_bytes = n_bytes
+        n_bytes, n_files = C.n_bytes * emissions, C.n_files * emissions  # per step
+        arena_bytes = C.n_bytes  # per scan
         counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs", "fold_sites",
                                             "candidates", "special_files", "findings")}
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
+                        "emissions_per_step": emissions, "pool_bytes": C.n_bytes,
                         "resident": "host (page-locked), H2D in the timed region" if args.ingest
                         else "HBM (copied once before timing)"}
     else:
@@ -396,7 +407,7 @@ def main():
                         "pre_transform": args.transform,
                         "layer_gbps": round(world * int(layer.size) * args.steps / dt / 1e9, 3)}
     value = world * n_bytes * args.steps / dt / 1e9
-    alg_bytes = arena_bytes + 16 * n_files  # 1 B/arena byte + 16 B/file
+    alg_bytes = arena_bytes + 16 * (n_files // emissions)  # 1 B/arena byte + 16 B/file, per scan
     phase = alg_bytes / (gpu_ms * 1e-3) / 1e9  # §8(d): (arena + 16 n_files) / (t_prefilter + t_nfa)
     k1 = alg_bytes / (scan_ms * 1e-3) / 1e9
     dom = max(kernels, key=kernels.get)

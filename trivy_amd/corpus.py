@@ -46,12 +46,21 @@ class Corpus:
         return self.arena[int(self.offsets[i]):int(self.offsets[i + 1])].tobytes()
 
 
-def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=None):
+def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=None, size_scale=1.0):
+    """The C1/C2 generator; size_scale multiplies every planned file size (clipped at
+    10 MiB, the total cut at target_bytes): C5's mean-64-KiB files use 2.6."""
     L = _lib.lib()
     _declare(L)
     n = L.tsg_corpus_plan(seed, int(target_bytes), None, 0)
     offs = np.zeros(n + 1, dtype=np.uint64)
     L.tsg_corpus_plan(seed, int(target_bytes), offs.ctypes.data, n + 1)
+    if size_scale != 1.0:
+        sizes = np.minimum(np.diff(offs).astype(np.float64) * size_scale, 10 << 20).astype(np.uint64)
+        cum = np.cumsum(sizes)
+        n = int(np.searchsorted(cum, int(target_bytes))) + 1
+        n = min(n, len(sizes))
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        offs[1:] = np.minimum(cum[:n], int(target_bytes))
     pool = json.loads(POOL.read_text())
     samples = [s.encode() for v in pool.values() for s in v]
     blob = b"".join(samples)
