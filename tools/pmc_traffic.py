@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--kernel", default="filter_kernel")
     ap.add_argument("--out", required=True)
     ap.add_argument("--csv-out", default=None, help="per-kernel summary CSV")
+    ap.add_argument("--workload", default="c2", help="bench workload id the pass ran (bench.py matches it)")
+    ap.add_argument("--note", default="")
     args = ap.parse_args()
     per = collections.defaultdict(list)
     for f in glob.glob(args.dir + "/**/*counter_collection.csv", recursive=True):
@@ -42,8 +44,15 @@ def main():
     if not hit:
         raise SystemExit("no FETCH_SIZE rows for " + args.kernel)
     k, n, kb, raw, x2 = hit[0]
-    json.dump({"gb": args.gb, "kernel": k, "dispatches": n, "bytes_per_launch": round(x2),
-               "fetch_size_kb": kb, "correction": "x2 (gfx950 FETCH_SIZE counts half of wide streaming reads)"},
+    # the whole GPU phase of one scan: every tsg kernel, each averaged per dispatch
+    phase = {r[0]: round(r[4]) for r in rows if "tsg::" in r[0]}
+    json.dump({"workload": args.workload, "gb": args.gb, "kernel": k, "dispatches": n,
+               "bytes_per_launch": round(x2), "k1_bytes_per_launch": round(x2),
+               "phase_bytes_per_scan": sum(phase.values()), "phase_kernels_bytes": phase,
+               "fetch_size_kb": kb,
+               "correction": "x2 (gfx950 FETCH_SIZE counts half of wide streaming reads); calibrated for K1's "
+                             "16-B/lane stream, an upper bound for the other kernels' gathers",
+               "note": args.note},
               open(args.out, "w"), indent=1)
     print(json.dumps(json.load(open(args.out))))
 

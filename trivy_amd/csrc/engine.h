@@ -108,6 +108,9 @@ class GpuEngine {
   uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0, n_fold_cap_k_ = 0, n_fold_cap_s_ = 0;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, ft_luts_ = 0;
+  // confirm-only part of the table blob (after the fold kernel's prefix): the
+  // core tables over byte classes (filter.h core, columns deduplicated)
+  uint32_t ftabs_fold_bytes_ = 0, ft_cmap_ = 0, ft_ccore_ = 0, ft_gitems_ = 0, ft_bgroups_ = 0, n_core_cls_ = 0;
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;

@@ -346,7 +346,7 @@ struct NfaParams {
 // allow.  The TSG_C_* macros exist for those variant builds
 // (tools/build_variant.py).
 #ifndef TSG_C_THREADS
-#define TSG_C_THREADS 256
+#define TSG_C_THREADS 512
 #endif
 constexpr int kCThreads = TSG_C_THREADS;
 
@@ -535,6 +535,9 @@ struct ConfirmParams {
   const uint32_t* bucket_groups;  // n_buckets + 1
   uint32_t* item_diag;            // TSG_DIAG_ITEMS: per item exact matches
   uint32_t t_luts;                // tabs offset of the per-anchor follow requirements (rules.h FollowLut)
+  // LDS tables only: the core tables over byte classes -- class of byte b at
+  // tabs[t_cmap + b], group g's column of class c at u64 [t_ccore/8 + g * n_cls + c]
+  uint32_t t_cmap, t_ccore, t_gitems, t_bgroups, n_cls;
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -686,7 +689,7 @@ constexpr uint32_t kCQ2 = TSG_C_Q2;  // candidate items (overflow: checked in pl
 // (large custom rule sets, e.g. 2,000 generated rules).
 template <bool kLdsTabs>
 #ifndef TSG_C_MINW
-#define TSG_C_MINW 1
+#define TSG_C_MINW 4  // <= 128 VGPRs: 4 waves per SIMD
 #endif
 __global__ __launch_bounds__(kCThreads, TSG_C_MINW) void confirm_kernel(ConfirmParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -845,11 +848,20 @@ __global__ __launch_bounds__(kCThreads, TSG_C_MINW) void confirm_kernel(ConfirmP
       const int64_t pos = int64_t(base + k) - 7 + q;
       cb[q] = pos < 0 ? 0u : win_byte(l, uint64_t(pos));
     }
+    // LDS tables: the bytes' classes once per fire, then one ds_read_b64 per
+    // byte and group (the global tables cost an L2 round trip per group)
+    const uint32_t* bgroups = kLdsTabs ? reinterpret_cast<const uint32_t*>(tabs + P.t_bgroups) : P.bucket_groups;
+    const uint32_t* gitems = kLdsTabs ? reinterpret_cast<const uint32_t*>(tabs + P.t_gitems) : P.group_items;
+    if (kLdsTabs) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) cb[q] = tabs[P.t_cmap + cb[q]];
+    }
     while (fm) {
       const uint32_t j = __builtin_ctz(fm);
       fm &= fm - 1;
-      for (uint32_t g = P.bucket_groups[j]; g < P.bucket_groups[j + 1]; g++) {
-        const uint64_t* ct = P.core + size_t(g) * 256;
+      for (uint32_t g = bgroups[j]; g < bgroups[j + 1]; g++) {
+        const uint64_t* ct = kLdsTabs ? reinterpret_cast<const uint64_t*>(tabs + P.t_ccore) + size_t(g) * P.n_cls
+                                      : P.core + size_t(g) * 256;
         uint64_t cm = ~uint64_t(0);
 #pragma unroll
         for (int q = 0; q < 8; q++) cm &= ct[cb[q]] >> (8 * q);
@@ -857,7 +869,7 @@ __global__ __launch_bounds__(kCThreads, TSG_C_MINW) void confirm_kernel(ConfirmP
         while (im) {
           const uint32_t gi = __builtin_ctz(im);
           im &= im - 1;
-          const uint32_t ix = P.group_items[g * 8 + gi];
+          const uint32_t ix = gitems[g * 8 + gi];
           const uint32_t slot = atomicAdd(&cnt[2], 1u);
           if (slot < kCQ2) q2[slot] = l | (k << 6) | (ix << 10);
           else check_item(l, k, ix);  // queue full: check in place
@@ -1379,6 +1391,30 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     ft_classes_ = put(ft->classes.data(), ft->classes.size() * 4);
     ft_luts_ = put(cr.anchor_req.data(), cr.anchor_req.size() * sizeof(FollowLut));
     if (tb.empty()) tb.assign(16, 0);
+    ftabs_fold_bytes_ = uint32_t(tb.size());  // the fold kernel stages this prefix
+    {  // core tables over byte classes (bytes with equal columns in every group share one)
+      const size_t n_groups = ft->bucket_groups.empty() ? 0 : ft->bucket_groups.back();
+      std::vector<uint8_t> cmap(256, 0);
+      std::vector<uint32_t> rep;  // representative byte per class
+      for (uint32_t b = 0; b < 256; b++) {
+        uint32_t c = 0;
+        for (; c < rep.size(); c++) {
+          bool same = true;
+          for (size_t g = 0; g < n_groups && same; g++) same = ft->core[g * 256 + b] == ft->core[g * 256 + rep[c]];
+          if (same) break;
+        }
+        if (c == rep.size()) rep.push_back(b);
+        cmap[b] = uint8_t(c);
+      }
+      n_core_cls_ = uint32_t(rep.size());
+      std::vector<uint64_t> cc(n_groups * rep.size());
+      for (size_t g = 0; g < n_groups; g++)
+        for (size_t c = 0; c < rep.size(); c++) cc[g * rep.size() + c] = ft->core[g * 256 + rep[c]];
+      ft_cmap_ = put(cmap.data(), cmap.size());
+      ft_ccore_ = put(cc.data(), cc.size() * sizeof(uint64_t));
+      ft_gitems_ = put(ft->group_items.data(), ft->group_items.size() * 4);
+      ft_bgroups_ = put(ft->bucket_groups.data(), ft->bucket_groups.size() * 4);
+    }
     ftabs_bytes_ = uint32_t(tb.size());
     n_fitems_ = uint32_t(ft->items.size());
     for (auto& it : ft->items) {
@@ -1452,10 +1488,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     // equal occupancy, 4 WG/CU beats 2 by 32%; c3 (103 KB of tables): LDS at
     // 1 WG/CU 102 GB/s vs global at 4 WG/CU 164 GB/s.  TSG_LDS_TABS_MAX
     // overrides (tuning).
-    size_t lds_max = 160 * 1024 / 4;
+    size_t lds_max = 160 * 1024 * size_t(kCThreads) / 1024;  // 16 waves per CU
     if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
     lds_tabs_ = fixed + ftabs_bytes_ <= lds_max &&
-                ftabs_bytes_ + 32 * size_t(n_fitems_) + kFoldWaves * kFoldWin <= 64 * 1024;  // fold kernel too
+                ftabs_fold_bytes_ + 32 * size_t(n_fitems_) + kFoldWaves * kFoldWin <= 64 * 1024;  // fold kernel too
     if (!item_diag_path_.empty() && hipMalloc(&d_item_diag_, 8 * std::max<size_t>(n_fitems_, 1)) != hipSuccess) {
       err_ = "hipMalloc item diag";
       return;
@@ -1466,7 +1502,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
     if (lds_tabs_)
       hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          int(ftabs_bytes_ + 32 * n_fitems_));
+                          int(ftabs_fold_bytes_ + 32 * n_fitems_));
   }
 }
 
@@ -1816,11 +1852,16 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.bucket_groups = d_bucket_groups_;
     cp.item_diag = d_item_diag_;
     cp.t_luts = ft_luts_;
+    cp.t_cmap = ft_cmap_;
+    cp.t_ccore = ft_ccore_;
+    cp.t_gitems = ft_gitems_;
+    cp.t_bgroups = ft_bgroups_;
+    cp.n_cls = n_core_cls_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
-        confirm_kernel<true><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
+        confirm_kernel<true><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
       else
-        confirm_kernel<false><<<2048, kCThreads, c_lds_bytes_, stream_>>>(cp);
+        confirm_kernel<false><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[3], stream_));
@@ -1829,7 +1870,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.arena = d_arena;
     fo.off = d_offsets;
     fo.tabs = d_ftabs_;
-    fo.tabs_bytes = ftabs_bytes_;
+    fo.tabs_bytes = ftabs_fold_bytes_;
     fo.t_items = ft_items_;
     fo.t_item_ids = ft_item_ids_;
     fo.t_item_cls = ft_item_cls_;
@@ -1848,7 +1889,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.counters = d_counters_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
-        fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_bytes_ + 32 * n_fitems_, stream_>>>(fo);
+        fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
       else
         fold_kernel<false><<<2048, 64 * kFoldWaves, 0, stream_>>>(fo);
     }

@@ -914,7 +914,50 @@ std::unique_ptr<Regex> Regex::Compile(const std::string& pattern, std::string* e
       break;
     }
   }
+  re->ComputeFirstBytes();
   return re;
+}
+
+void Regex::ComputeFirstBytes() {
+  uint64_t f[4] = {};
+  bool all = false;
+  auto add = [&](uint32_t b) { f[b >> 6] |= uint64_t(1) << (b & 63); };
+  auto lead = [](uint32_t r) -> uint32_t {
+    return r < 0x80 ? r : r < 0x800 ? 0xC0 | (r >> 6) : r < 0x10000 ? 0xE0 | (r >> 12) : 0xF0 | (r >> 18);
+  };
+  auto add_range = [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t b = lo; b <= hi && b < 0x80; b++) add(b);
+    if (hi < 0x80) return;
+    if (lo <= 0xFFFD && 0xFFFD <= hi) {  // invalid bytes decode to U+FFFD (width 1)
+      for (uint32_t b = 0x80; b < 0x100; b++) add(b);
+      return;
+    }
+    for (uint32_t b = lead(lo < 0x80 ? 0x80 : lo); b <= lead(hi); b++) add(b);
+  };
+  std::vector<uint32_t> stack{start_};
+  std::vector<uint8_t> seen(prog_.size(), 0);
+  while (!stack.empty() && !all) {
+    const uint32_t pc = stack.back();
+    stack.pop_back();
+    if (seen[pc]) continue;
+    seen[pc] = 1;
+    const Inst& in = prog_[pc];
+    switch (in.op) {
+      case kIFail: break;
+      case kIAlt: stack.push_back(in.out); stack.push_back(in.arg); break;
+      case kICapture: case kIEmpty: case kINop: stack.push_back(in.out); break;  // assertions: superset
+      case kIMatch: all = true; break;  // an empty match
+      case kIRune1: add_range(in.rune, in.rune); break;
+      case kIRune: for (auto& rg : classes_[size_t(in.cls)]) add_range(rg.first, rg.second); break;
+      case kIAny: all = true; break;
+      case kIAnyNotNL:
+        for (uint32_t b = 0; b < 256; b++)
+          if (b != '\n') add(b);
+        break;
+    }
+  }
+  first_all_ = all;
+  for (int k = 0; k < 4; k++) first_[k] = f[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1194,7 +1237,7 @@ class Backtracker {
       }
       const bool allowed = !wins || (*wins)[wi].lo <= pos;
       if (anchored && pos != 0) break;
-      if (allowed) {
+      if (allowed && re->FirstOk(s, n, pos)) {
         if (top_ < pos) Rebase(pos);  // states before pos are unreachable from here on
         if (ncap_ > 0) cap_[0] = pos;
         if (Try(re->start_, pos)) return true;
@@ -1318,7 +1361,22 @@ class Backtracker {
   }
 };
 
+namespace {
+thread_local Backtracker t_bt;  // per host thread: its visited rows and job stack are reused
+}
+
+// MatchString: any match at all.  The bit-state backtracker answers it without
+// allocating (a Pike VM per call cost 15% of the host tail, mostly in the
+// allow-path regexes); the Pike VM only past its row budget.
 bool Regex::Match(const uint8_t* s, int64_t n) const {
+  Backtracker& bt = t_bt;
+  const int mode = g_regex_engine.load(std::memory_order_relaxed);
+  if (mode != 1) {
+    bt.max_rows_ = mode == 2 ? 8 : Backtracker::kMaxRows;
+    bool overflow = false;
+    if (bt.Search(this, s, n, 0, nullptr, 0, &overflow)) return true;
+    if (!overflow) return false;
+  }
   Machine m(this, 0);
   return m.Search(s, n, 0, nullptr);
 }
@@ -1326,7 +1384,7 @@ bool Regex::Match(const uint8_t* s, int64_t n) const {
 void Regex::FindAll(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
                     std::vector<int64_t>* out) const {
   int ncap = submatch ? 2 * (num_cap_ + 1) : 2;
-  thread_local Backtracker bt;
+  Backtracker& bt = t_bt;
   const int mode = g_regex_engine.load(std::memory_order_relaxed);
   bt.max_rows_ = mode == 2 ? 8 : Backtracker::kMaxRows;
   std::unique_ptr<Machine> m;  // only when the backtracker's row budget runs out

@@ -100,6 +100,15 @@ class Regex {
   std::vector<std::pair<uint64_t, uint64_t>> class_ascii_;  // ASCII membership bitmap per class
   uint32_t start_ = 0;
   bool anchored_begin_ = false;  // program begins with \A (startCond has EmptyBeginText)
+  // Bytes that can begin a match (the first byte of its first rune), from the
+  // program's start closure; first_all_ when a match can be empty or start
+  // with any byte.  Starts at other bytes are skipped (an exact pruning).
+  uint64_t first_[4] = {};
+  bool first_all_ = true;
+  void ComputeFirstBytes();
+  bool FirstOk(const uint8_t* s, int64_t n, int64_t pos) const {
+    return first_all_ || (pos < n && ((first_[s[pos] >> 6] >> (s[pos] & 63)) & 1));
+  }
 };
 
 // unicode.SimpleFold and unicode.ToLower (generated tables, Unicode 13 data).

@@ -514,6 +514,7 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 // Host-tail phase profile (TSG_TAIL_DEBUG=1 only; otherwise the timers are inert).
 const bool g_tail_debug = std::getenv("TSG_TAIL_DEBUG") != nullptr;
 std::atomic<int64_t> g_prof[8];
+std::atomic<int64_t> g_wholefile_bytes{0}, g_wholefile_calls{0};  // TSG_TAIL_DEBUG: whole-content gate scans
 struct PhaseTimer {
   int k;
   std::chrono::steady_clock::time_point t0;
@@ -526,19 +527,36 @@ struct PhaseTimer {
   }
 };
 
-void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
+namespace {
+// Per host thread scratch of ScanFile: cleared per file, never freed, so the
+// per-file vectors cost no allocation (malloc was ~14% of the host tail).
+struct ScanScratch {
+  std::vector<std::pair<uint32_t, Loc>> matched;
+  std::vector<Loc> censor, locs, spans, merged;
+  std::vector<std::pair<int64_t, int64_t>> nla;
+  std::vector<Window> wins;
+  std::vector<int64_t> m, span_nl;
+};
+thread_local ScanScratch t_scan;
+}  // namespace
+
+void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_view path, bool binary,
                              const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const {
   PhaseTimer pt_all(7);
   const uint8_t* P = reinterpret_cast<const uint8_t*>(path.data());
-  std::vector<std::pair<uint32_t, Loc>> matched;
-  std::vector<Loc> censor;
+  ScanScratch& S = t_scan;
+  std::vector<std::pair<uint32_t, Loc>>& matched = S.matched;
+  std::vector<Loc>& censor = S.censor;
+  matched.clear();
+  censor.clear();
   bool gblocks_done = false;
   std::vector<Loc> gblocks;
   std::string lowered;
   bool lowered_done = false;
   bool fold_done = false, fold_runes = false;
   // (wlo, nl_before) anchors for line numbers
-  std::vector<std::pair<int64_t, int64_t>> nla;
+  std::vector<std::pair<int64_t, int64_t>>& nla = S.nla;
+  nla.clear();
   for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
   std::sort(nla.begin(), nla.end());
 
@@ -580,7 +598,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   while (i < nc_real) {
     uint32_t r = c[i].rule;
     size_t j = i;
-    std::vector<Window> wins;
+    std::vector<Window>& wins = S.wins;
+    wins.clear();
     uint32_t group_flags = ~0u;  // AND over the group's candidates (file-level bits agree)
     while (j < nc_real && c[j].rule == r) {
       group_flags &= c[j].flags;
@@ -596,7 +615,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     if (R.path && !R.path->Match(P, path.size())) continue;                      // MatchPath :397
     if (AllowRulesAllowPath(R.allow_rules, P, path.size())) continue;            // AllowPath :403
     bool sub = !R.secret_group_name.empty();
-    std::vector<int64_t> m;
+    std::vector<int64_t>& m = S.m;
+    m.clear();
     {
       PhaseTimer pt(0);
       re->FindAll(content, len, sub, &wins, &m);
@@ -648,6 +668,10 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
         // runes lowering into ASCII are U+0130 -> 'i' and U+212A -> 'k', so
         // without them the ASCII search is exact.  Otherwise lower as Go does.
         if (!fold_done) {
+          if (g_tail_debug) {
+            g_wholefile_bytes += len;
+            g_wholefile_calls += 1;
+          }
           fold_runes = HasSeq(content, size_t(len), "\xC4\xB0", 2) || HasSeq(content, size_t(len), "\xE2\x84\xAA", 3);
           fold_done = true;
         }
@@ -681,7 +705,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
       }
       if (!hit) continue;
     }
-    std::vector<Loc> locs;
+    std::vector<Loc>& locs = S.locs;
+    locs.clear();
     PhaseTimer pt5(5);
     for (size_t k = 0; k + stride <= m.size(); k += stride) {
       int64_t s = m[k], e = m[k + 1];
@@ -714,10 +739,12 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
 
   // findLocation runs on the censored buffer (scanner.go:438-439): newlines
   // inside a censored span are '*' there.  Spans merged and sorted:
-  std::vector<Loc> spans = censor;
+  std::vector<Loc>& spans = S.spans;
+  spans.assign(censor.begin(), censor.end());
   std::sort(spans.begin(), spans.end(), [](const Loc& a, const Loc& b) { return a.s < b.s; });
   {
-    std::vector<Loc> m;
+    std::vector<Loc>& m = S.merged;
+    m.clear();
     for (auto& z : spans) {
       if (z.e <= z.s) continue;
       if (!m.empty() && z.s <= m.back().e) m.back().e = std::max(m.back().e, z.e);
@@ -759,7 +786,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     }
     return n;
   };
-  std::vector<int64_t> span_nl(spans.size() + 1, 0);  // '\n' in spans[0 .. i)
+  std::vector<int64_t>& span_nl = S.span_nl;  // '\n' in spans[0 .. i)
+  span_nl.assign(spans.size() + 1, 0);
   for (size_t k = 0; k < spans.size(); k++) span_nl[k + 1] = span_nl[k] + count_nl_raw(spans[k].s, spans[k].e);
   auto censored_nl_before = [&](int64_t pos) {  // censored_nl(0, pos)
     const size_t k = first_span_after(pos);  // spans [0, k) end at or before pos
@@ -815,6 +843,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
   PhaseTimer pt3(3);
   ff.f.reserve(matched.size());
   ff.lines.reserve(matched.size() * 5);
+  ff.text.reserve(matched.size() * 512);  // match line + 4 lines of <= 100 B, typically
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
@@ -862,7 +891,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, const std::str
     f.start_line = start_line_num + 1;
     f.end_line = end_line_num + 1;
     if (binary) {
-      const std::string m = "Binary file " + GoQuote(path) + " matches a rule " + GoQuote(rules_[f.rule].title);
+      const std::string m = "Binary file " + GoQuote(std::string(path)) + " matches a rule " + GoQuote(rules_[f.rule].title);
       f.match_off = ff.Put(m);
       f.match_len = uint32_t(m.size());
     } else {
@@ -1001,7 +1030,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     const char* p = in.paths[f];
     size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
     uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
-    ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string(p, pn), in.binary && in.binary[f], &cands[a],
+    ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string_view(p, pn), in.binary && in.binary[f], &cands[a],
              b - a, &tmp[k], gpu_windows);
   });
   const double t_par = NowMs();
@@ -1012,6 +1041,9 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
                  "scanfile %.1f\n",
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
                  g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
+  if (g_tail_debug)
+    std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB\n", (long long)g_wholefile_calls.load(),
+                 g_wholefile_bytes.load() / 1e6);
   for (size_t k = 0; k < nf; k++) {
     if (tmp[k].kind != kHasFindings) continue;
     uint32_t f = cands[starts[k]].file;

@@ -155,7 +155,7 @@ class SecretScanner {
   void set_host_threads(int n) { host_threads_ = n; }
 
  private:
-  void ScanFile(const uint8_t* content, int64_t len, const std::string& path, bool binary,
+  void ScanFile(const uint8_t* content, int64_t len, std::string_view path, bool binary,
                 const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const;
   std::vector<RuleSpec> rules_;
   // Exclude-block regexes (scanner.go:237-275) are compiled after the rules as
