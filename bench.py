@@ -424,6 +424,10 @@ def main():
         arena_bytes = C.n_bytes  # per scan
         counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs", "fold_sites",
                                             "candidates", "special_files", "findings")}
+        # plain names: anchor_hits counts K2's exact anchor-item matches, follow_hits the hits
+        # past the follow requirements that K2 emits to the verify kernel's NFA
+        counts["anchor_item_matches"] = counts["anchor_hits"]
+        counts["hits_to_verify"] = counts["follow_hits"]
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
                         "emissions_per_step": emissions, "pool_bytes": C.n_bytes,

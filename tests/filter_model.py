@@ -16,7 +16,7 @@ from trivy_amd import _lib
 from trivy_amd.secret.scanner import CGlobal
 
 KIND_KEYWORD, KIND_ANCHOR, KIND_FOLD = 0, 1, 2
-WINDOW = 6
+WINDOW = 6  # default filter window (the compiled tables carry theirs: FilterModel.window)
 
 
 class RuleInfo(c.Structure):  # tsg_debug_rule_info (include/tsg_debug.h)
@@ -42,7 +42,6 @@ class FilterModel:
         if rc != 0:
             raise ValueError("no prefilter tables")
         self.n_buckets, self.window, self.n_words = shape[0], shape[1], shape[2]
-        assert self.window == WINDOW
         W = self.n_words
 
         def arr(ptr, ctype, n):
@@ -130,9 +129,9 @@ class FilterModel:
         out = np.zeros((self.n_buckets, n), dtype=bool)
         for j in range(self.n_buckets):
             ok = np.ones(n, dtype=bool)
-            for s in range(WINDOW):
+            for s in range(self.window):
                 col = self.allowed(j, s)[a]
-                sh = WINDOW - 1 - s
+                sh = self.window - 1 - s
                 shifted = np.zeros(n, dtype=bool)
                 shifted[sh:] = col[:n - sh] if sh else col
                 ok &= shifted

@@ -191,3 +191,28 @@ def test_keyword_bits_exact_ascii():
     gated = {int(x) for r in range(len(rules)) for x in _rule_kw(m, r)}
     assert with_items and with_items <= gated
     assert {(f, i) for f, i in want if i in with_items} == got
+
+
+def test_class_run_anchors_cover_matches():
+    """Rules without a required literal anchored on a run of one-byte classes
+    (rules.cpp ExtractClassRun): every match holds the run at its bounded offset,
+    so K1/K2 + the follow requirements still cover every match."""
+    from trivy_amd.secret.config import Rule
+    import re as _re
+    srcs = [r"(?i)\b[g-z]{3}[0-9]{3}[._-][a-z0-9]{12}\b",
+            r"[a-f]{2}[0-9]{2}_[a-z]+_end[0-9]",
+            r"[0-9]{3}-[0-9]{4}-[0-9]{3}",
+            r"(?i)(?:^|\s)[k-s]{2}[0-9]{4}[:=][A-Z0-9]{8}",
+            r"x?[0-9]{2}\.[0-9]{2}\.[0-9]{4}-[a-z]{2}"]
+    rules = builtin_rules() + [Rule(ID="cr%d" % i, Category="C", Title="t", Severity="LOW",
+                                    Regex=s)
+                               for i, s in enumerate(srcs)]
+    m = FilterModel(rules)
+    L = _lib.lib()
+    L.tsg_debug_rule_anchor.restype = c.c_char_p
+    L.tsg_debug_rule_anchor.argtypes = [c.c_void_p, c.c_uint32]
+    descs = [L.tsg_debug_rule_anchor(m.h, len(rules) - len(srcs) + i).decode() for i in range(len(srcs))]
+    assert all("classes" in d for d in descs), descs
+    rng = random.Random(11)
+    n, _ = _check(rules, _planted_texts(rng, rules[-len(srcs):], 60))
+    assert n > 40

@@ -62,19 +62,24 @@ def _compare(secret, files, cfg):
     return n
 
 
-@pytest.mark.parametrize("chunk", ["4096", "65536"])
-def test_fullscan_chunks_vs_oracle(tmp_path, monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,class_runs", [("4096", "0"), ("65536", "0"), ("4096", "1")])
+def test_fullscan_chunks_vs_oracle(tmp_path, monkeypatch, chunk, class_runs):
+    """class_runs 0: no literal anchors, the rules run in full-scan mode; 1: they are
+    anchored on their runs of one-byte classes (rules.cpp ExtractClassRun)."""
     import trivy_amd.secret as secret
     monkeypatch.setenv("TSG_FULLSCAN_CHUNK", chunk)
+    monkeypatch.setenv("TSG_CLASS_RUNS", class_runs)
     cfg = tmp_path / "trivy-secret.yaml"
     cfg.write_text(RULES)
     n = _compare(secret, _files(random.Random(7)), str(cfg))
     assert n > 100
 
 
-def test_c3u_unanchored_rules_vs_oracle(tmp_path):
+@pytest.mark.parametrize("class_runs", ["0", "1"])
+def test_c3u_unanchored_rules_vs_oracle(tmp_path, monkeypatch, class_runs):
     """The C3u rule set (10 % of 2,000 generated rules without a literal anchor)."""
     import trivy_amd.secret as secret
+    monkeypatch.setenv("TSG_CLASS_RUNS", class_runs)
     from trivy_amd.corpus import c3_rules
     from tests.test_gpu_parity import _c3_files
     y, samples = c3_rules(unanchored_share=0.1)
@@ -82,3 +87,43 @@ def test_c3u_unanchored_rules_vs_oracle(tmp_path):
     cfg.write_text(y)
     files = _c3_files([s for s in samples if s.startswith(b"kwu")] + samples[:50], 19, 120)
     assert _compare(secret, files, str(cfg)) > 20
+
+
+FOLD_RULES = (
+    "rules:\n"
+    "  - id: tok-kw\n    category: Custom\n    title: Token gated by a k/i keyword\n    severity: HIGH\n"
+    "    regex: '(?i)\\b[g-z]{3}[0-9]{3}[._-][a-z0-9]{12}\\b'\n    keywords: [kwink]\n"
+    "  - id: anchored-kw\n    category: Custom\n    title: Anchored, gated\n    severity: LOW\n"
+    "    regex: 'pfxtok_[a-z0-9]{10}'\n    keywords: [tikki]\n")
+
+
+@pytest.mark.parametrize("class_runs", ["0", "1"])
+def test_keyword_gate_through_fold_runes_vs_oracle(tmp_path, monkeypatch, class_runs):
+    """bytes.ToLower maps U+212A to 'k' and U+0130 to 'i': keywords spelled with
+    them open the gate (kwfold_kernel sets the bits); files holding the runes
+    but not the keyword stay gated out of the full scan."""
+    import trivy_amd.secret as secret
+    monkeypatch.setenv("TSG_CLASS_RUNS", class_runs)
+    K, I = "K".encode(), "İ".encode()
+    tok = b" ghi123_abcdef123456 "
+    atok = b" pfxtok_abcdefghij "
+    pad = b"filler text 0123 " * 300 + b"\n"
+    variants = [
+        b"kwink",                       # ASCII
+        K + b"w" + I + b"n" + K,        # every k / i through a fold rune
+        b"KW" + I + b"NK",              # upper case + U+0130
+        K + b"wink",                    # the rune at the start
+        b"kwin" + K,                    # ... at the end
+        b"kw" + K + b"nk",              # U+212A where 'i' belongs: no match
+        b"kwi" + I + b"k",              # an extra rune: no match
+    ]
+    files = []
+    for i, v in enumerate(variants):
+        files.append(("v%d.txt" % i, pad + v + b"\n" + pad + tok + pad))
+        files.append(("a%d.txt" % i, pad + b"t" + I + b"kk" + I + b" " + v + atok + pad))
+    files.append(("runes-no-kw.txt", pad + K + I + b" x " + tok + pad))  # runes, keyword absent
+    files.append(("deep.txt", pad * 40 + K + b"w" + I + b"nk" + pad * 40 + tok))
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(FOLD_RULES)
+    n = _compare(secret, files, str(cfg))
+    assert n >= 8

@@ -106,6 +106,9 @@ class GpuEngine {
   void* d_fold_pairs_ = nullptr;  // fold kernel work list
   void* d_fold_first_ = nullptr;  // per item: bytes that can start it (fold kernel prefilter)
   uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0, n_fold_cap_k_ = 0, n_fold_cap_s_ = 0;
+  void* d_kwfold_pairs_ = nullptr;  // kwfold kernel work list (keyword items through U+0130 / U+212A)
+  uint32_t n_kwf_ri_ = 0, n_kwf_rk_ = 0, n_kwf_ci_ = 0, n_kwf_ck_ = 0;
+  bool kw_fold_ = false;
   uint32_t ftabs_bytes_ = 0, ft_bucket_off_ = 0, ft_bucket_items_ = 0, ft_items_ = 0;
   uint32_t ft_item_ids_ = 0, ft_item_cls_ = 0, ft_classes_ = 0, ft_luts_ = 0;
   // confirm-only part of the table blob (after the fold kernel's prefix): the

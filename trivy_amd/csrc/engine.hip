@@ -330,7 +330,15 @@ struct NfaParams {
   const uint32_t* fullscan_rules;
   uint32_t n_fullscan_rules;
   uint32_t fs_chunk;       // full-scan chunk bytes per lane (min; files of > 64 chunks use larger ones)
+  uint32_t kw_fold;        // kwfold_kernel ran: with no fold-site overflow the keyword bits are exact in every file
 };
+
+// The keyword bits of file f may miss occurrences through U+0130 / U+212A
+// (then a closed gate is not MatchKeywords == false): files holding them,
+// unless kwfold_kernel covered every fold site.
+__device__ __forceinline__ bool kw_bits_inexact(const NfaParams& P, uint32_t f) {
+  return (P.flags[f] & 4u) && !(P.kw_fold && P.counters[10] == 0);
+}
 
 
 
@@ -348,7 +356,15 @@ struct NfaParams {
 #ifndef TSG_C_THREADS
 #define TSG_C_THREADS 512
 #endif
-constexpr int kCThreads = TSG_C_THREADS;
+constexpr int kCThreads = TSG_C_THREADS;  // LDS-table variant (builtin-sized rule sets)
+#ifndef TSG_C_THREADS_G
+#define TSG_C_THREADS_G 256
+#endif
+// global-table variant (large custom sets): C3 confirm 22.5 ms at 256 threads x 4 WG/CU vs
+// 32.7 ms at 512 x 2 (profiles/r02d_*)
+constexpr int kCThreadsG = TSG_C_THREADS_G;
+template <bool kLdsTabs>
+constexpr int ConfirmThreads() { return kLdsTabs ? kCThreads : kCThreadsG; }
 
 struct FoldSite {  // a fold rune (U+0130 / U+212A / U+017F) at arena byte x of file f
   uint64_t x;
@@ -683,6 +699,10 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
 constexpr bool kCFse = TSG_C_FSE;     // cache each block's file in LDS in phase A (-0.2 ms at equal occupancy; costs 20 B/lane)
 constexpr uint32_t kCQ1 = TSG_C_Q1;  // fires (overflow: handled in place)
 constexpr uint32_t kCQ2 = TSG_C_Q2;  // candidate items (overflow: checked in place)
+constexpr size_t ConfirmFixedLds(int t) {  // LDS of a t-thread workgroup besides the staged tables
+  return 4096 + size_t(t) * (kCWin + 8 + (kCFse ? 20 : 0)) + size_t(t / 64) * (kCQ1 + kCQ2) * 4 +
+         size_t(t / 64) * kCWaveHits * 12 + size_t(t / 64) * 16;
+}
 
 // kLdsTabs: the item tables are staged in LDS (they fit: builtin-sized rule
 // sets); otherwise they are read through the caches from global memory
@@ -691,8 +711,9 @@ template <bool kLdsTabs>
 #ifndef TSG_C_MINW
 #define TSG_C_MINW 4  // <= 128 VGPRs: 4 waves per SIMD
 #endif
-__global__ __launch_bounds__(kCThreads, TSG_C_MINW) void confirm_kernel(ConfirmParams P) {
+__global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confirm_kernel(ConfirmParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int kCThreads = ConfirmThreads<kLdsTabs>();  // shadows the file-scope constant
   constexpr uint32_t kWaves = kCThreads / 64;
   uint8_t* s_reach = smem;                                                      // 4 KiB, one copy per byte
   uint8_t* s_win = smem + 4096;                                                 // kCThreads x 64 B
@@ -1077,6 +1098,99 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
   }
 }
 
+// Keyword occurrences through fold runes.  bytes.ToLower maps exactly two
+// non-ASCII runes into ASCII: U+0130 (C4 B0) -> 'i' and U+212A (E2 84 AA) ->
+// 'k' (SURVEY.md §8 A7), so `kw` is in bytes.ToLower(content) iff some
+// occurrence matches each keyword position by an ASCII byte of either case, by
+// C4 B0 where the position is 'i' or by E2 84 AA where it is 'k'.  K2 sets the
+// bits of the all-ASCII occurrences; an occurrence holding a fold rune covers a
+// fold site, so trying, at every U+0130 / U+212A site, each keyword that can
+// take the rune at each start putting the rune inside it finds the rest.  After
+// this kernel the keyword bits are MatchKeywords exactly (unless the fold-site
+// list overflowed), and the full-scan and verify kernels need not open the gates
+// of files holding those runes.  Work lists as the fold kernel's: "capable"
+// (item, q) tasks with start x - q when no other such rune precedes x within
+// the span, else start ranges.
+struct KwFoldParams {
+  const uint8_t* arena;
+  const uint64_t* off;
+  const uint8_t* tabs;  // global table blob (filter items)
+  uint32_t t_items, t_item_ids, t_item_cls, t_classes;
+  const FoldPair* pairs;  // [i ranges | k ranges | i capable | k capable]
+  uint32_t n_rng_i, n_rng_k, n_cap_i, n_cap_k;
+  const FoldSite* folds;
+  uint32_t fold_cap;
+  uint32_t* counters;
+  uint32_t* kwbits;
+  uint32_t kw_words;
+};
+
+__global__ __launch_bounds__(64 * kFoldWaves) void kwfold_kernel(KwFoldParams P) {
+  __shared__ uint8_t s_win[kFoldWaves][kFoldWin];
+  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(P.tabs + P.t_items);
+  const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(P.tabs + P.t_item_ids);
+  const uint8_t* item_cls = P.tabs + P.t_item_cls;
+  const uint32_t* classes = reinterpret_cast<const uint32_t*>(P.tabs + P.t_classes);
+  auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* wb = s_win[wave];
+  const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
+  for (uint32_t si = blockIdx.x * kFoldWaves + wave; si < n_folds; si += gridDim.x * kFoldWaves) {
+    const FoldSite fsite = P.folds[si];
+    const uint64_t fs = P.off[fsite.f], fe = P.off[fsite.f + 1];
+    const uint32_t lead = P.arena[fsite.x];
+    if (lead != 0xC4 && lead != 0xE2) continue;  // U+017F: ToLower keeps it non-ASCII (wave-uniform)
+    const bool kay = lead == 0xE2;
+    const uint64_t w0 = fsite.x > fs + kFoldSpan ? fsite.x - kFoldSpan : fs;
+    const uint64_t w1 = fsite.x + kFoldSpan < fe ? fsite.x + kFoldSpan : fe;
+    wave_sync();
+    for (uint32_t i = lane; i < uint32_t(w1 - w0); i += 64) wb[i] = P.arena[w0 + i];
+    wave_sync();
+    auto kfold = [&](uint64_t p) {
+      return wb[p - w0] == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA;
+    };
+    auto ifold = [&](uint64_t p) { return wb[p - w0] == 0xC4 && p + 1 < w1 && wb[p + 1 - w0] == 0xB0; };
+    if (!(kay ? kfold(fsite.x) : ifold(fsite.x))) continue;  // not the rune itself (wave-uniform)
+    bool other = false;
+    for (uint64_t p = w0 + lane; p < fsite.x; p += 64) other = other || kfold(p) || ifold(p);
+    other = __ballot(other) != 0;
+    const FoldPair* pairs = P.pairs + (other ? (kay ? P.n_rng_i : 0) : P.n_rng_i + P.n_rng_k + (kay ? P.n_cap_i : 0));
+    const uint32_t n_pairs = other ? (kay ? P.n_rng_k : P.n_rng_i) : (kay ? P.n_cap_k : P.n_cap_i);
+    for (uint32_t t = lane; t < n_pairs; t += 64) {
+      const FoldPair fp = pairs[t];
+      const FilterItemGpu it = items[fp.item];
+      for (uint32_t back = fp.lo; back <= fp.hi; back++) {
+        if (fsite.x < w0 + back) break;
+        uint64_t p = fsite.x - back;
+        bool ok = true, covered = false;
+        for (uint32_t q = 0; q < it.n; q++) {
+          if (p >= w1) {
+            ok = false;
+            break;
+          }
+          covered = covered || p == fsite.x;
+          const uint32_t c = item_cls[it.cls_off + q];
+          if (kfold(p) && in_cls(c, 'k')) p += 3;
+          else if (ifold(p) && in_cls(c, 'i')) p += 2;
+          else if (in_cls(c, wb[p - w0])) p += 1;
+          else {
+            ok = false;
+            break;
+          }
+        }
+        if (!ok || !covered) continue;
+        for (uint32_t d = 0; d < it.n_ids; d++) {
+          const uint32_t id = item_ids[it.ids_off + d];
+          uint32_t* w = &P.kwbits[uint64_t(fsite.f) * P.kw_words + (id >> 5)];
+          const uint32_t bit = 1u << (id & 31);
+          if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
+        }
+        break;  // this item is found in the file
+      }
+    }
+  }
+}
+
 // Candidate flags for the host's lazy MatchKeywords (scanner.go:174-186).
 __device__ uint32_t gate_flags(const NfaParams& P, const RuleGpu& rg, uint32_t f) {
   uint32_t fl = kCandGateValid | ((P.flags[f] & 4u) ? kCandFoldFile : 0u);
@@ -1108,7 +1222,8 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
     // A closed ASCII keyword gate in a file without U+0130 / U+212A is exactly
     // MatchKeywords == false (scanner.go:409): the host would drop every match
     // of the rule, so its hits need no verification.
-    if (rg.gate == kGateKeywords && !rg.kw_match_implied && !(ff & 4u) && !(gate_flags(P, rg, f) & kCandGateOpen))
+    if (rg.gate == kGateKeywords && !rg.kw_match_implied && !kw_bits_inexact(P, f) &&
+        !(gate_flags(P, rg, f) & kCandGateOpen))
       continue;
     const int64_t lit_hi = int64_t(end) - int64_t(a.lit_len);
     const int64_t lit_lo = (ff & 1u) ? int64_t(end) - 3 * int64_t(a.lit_len) : lit_hi;
@@ -1235,7 +1350,7 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
       f = uint32_t(t / P.n_fullscan_rules);
       r = P.fullscan_rules[t % P.n_fullscan_rules];
       const RuleGpu rg = P.rules[r];
-      open = rg.gate != kGateKeywords || rg.kw_match_implied || (P.flags[f] & 4u) ||
+      open = rg.gate != kGateKeywords || rg.kw_match_implied || kw_bits_inexact(P, f) ||
              (gate_flags(P, rg, f) & kCandGateOpen);
       open = open && P.off[f + 1] > P.off[f];
     }
@@ -1302,7 +1417,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
     if (lane == 0) {
       const RuleGpu rg = P.rules[c.rule];
       uint32_t fl = gate_flags(P, rg, file);
-      if (rg.gate == kGateKeywords && !rg.kw_match_implied && !(P.flags[file] & 4u) && !(fl & kCandGateOpen))
+      if (rg.gate == kGateKeywords && !rg.kw_match_implied && !kw_bits_inexact(P, file) && !(fl & kCandGateOpen))
         fl |= kCandDrop;
       c.flags = fl;
     }
@@ -1480,8 +1595,53 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       if (!Upload(&err_, &dp, reinterpret_cast<const uint8_t*>(pk.data()), pk.size() * sizeof(FoldPair))) return;
       d_fold_pairs_ = dp;
     }
-    const size_t fixed = 4096 + size_t(kCThreads) * (kCWin + 8 + (kCFse ? 20 : 0)) + size_t(kCThreads / 64) * (kCQ1 + kCQ2) * 4 +
-                         size_t(kCThreads / 64) * kCWaveHits * 12 + size_t(kCThreads / 64) * 16;
+    {  // keyword fold work lists (kwfold_kernel): U+0130 at 'i' positions, U+212A at 'k' positions
+      auto in_cls = [&](uint32_t c, uint32_t b) { return (ft->classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
+      std::vector<FoldPair> ri, rk, ci, ck;
+      kw_fold_ = true;
+      for (uint32_t i = 0; i < uint32_t(ft->items.size()); i++) {
+        const FilterItemGpu& it = ft->items[i];
+        if (it.kind != kItemKeyword) continue;
+        if (it.n > 48) kw_fold_ = false;  // beyond the kernel's window: keep those files' gates open
+        uint32_t before = 0;
+        int64_t ilo = -1, ihi = -1, klo = -1, khi = -1;
+        for (uint32_t q = 0; q < it.n && q <= 0xFFFF; q++) {
+          const uint32_t c = ft->item_cls[it.cls_off + q];
+          const bool hi_ = in_cls(c, 'i'), hk = in_cls(c, 'k');
+          if (hi_) {
+            if (ilo < 0) ilo = q;
+            ihi = before;
+            ci.push_back({i, uint16_t(q), uint16_t(q)});
+          }
+          if (hk) {
+            if (klo < 0) klo = q;
+            khi = before;
+            ck.push_back({i, uint16_t(q), uint16_t(q)});
+          }
+          before += hk ? 3 : hi_ ? 2 : 1;
+        }
+        auto add = [&](std::vector<FoldPair>& v, int64_t lo, int64_t hi) {
+          hi = std::min<int64_t>(hi, 0xFFFF);
+          for (int64_t a = lo; a <= hi; a += kFoldTaskStarts)
+            v.push_back({i, uint16_t(a), uint16_t(std::min<int64_t>(a + kFoldTaskStarts - 1, hi))});
+        };
+        if (ilo >= 0) add(ri, ilo, ihi);
+        if (klo >= 0) add(rk, klo, khi);
+      }
+      n_kwf_ri_ = uint32_t(ri.size());
+      n_kwf_rk_ = uint32_t(rk.size());
+      n_kwf_ci_ = uint32_t(ci.size());
+      n_kwf_ck_ = uint32_t(ck.size());
+      ri.insert(ri.end(), rk.begin(), rk.end());
+      ri.insert(ri.end(), ci.begin(), ci.end());
+      ri.insert(ri.end(), ck.begin(), ck.end());
+      if (ri.empty()) ri.push_back({0, 0, 0});
+      uint8_t* dp = nullptr;
+      if (!Upload(&err_, &dp, reinterpret_cast<const uint8_t*>(ri.data()), ri.size() * sizeof(FoldPair))) return;
+      d_kwfold_pairs_ = dp;
+      if (const char* e = std::getenv("TSG_KWFOLD")) kw_fold_ = kw_fold_ && std::atoi(e) != 0;  // A/B knob
+    }
+    const size_t fixed = ConfirmFixedLds(kCThreads);
     // Tables staged in LDS only while four workgroups still fit a CU (the
     // register-bound maximum); larger ones are read from global memory
     // (L2-resident).  Measured on C2: LDS tables beat global ones by 17% at
@@ -1496,7 +1656,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       err_ = "hipMalloc item diag";
       return;
     }
-    c_lds_bytes_ = fixed + (lds_tabs_ ? ftabs_bytes_ : 0);
+    c_lds_bytes_ = lds_tabs_ ? fixed + ftabs_bytes_ : ConfirmFixedLds(kCThreadsG);
     if (const char* e = std::getenv("TSG_CONFIRM_LDS_PAD")) c_lds_bytes_ += size_t(std::strtoull(e, nullptr, 10));  // occupancy experiments
     hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
@@ -1508,7 +1668,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_item_diag_, d_fold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1],
                 d_kind_[0], d_kind_[1], d_xlen_, d_xoff_, d_xscan_, d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
@@ -1861,7 +2021,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       if (lds_tabs_)
         confirm_kernel<true><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
       else
-        confirm_kernel<false><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
+        confirm_kernel<false><<<2048 * 256 / kCThreadsG, kCThreadsG, c_lds_bytes_, stream_>>>(cp);
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[3], stream_));
@@ -1894,6 +2054,28 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
         fold_kernel<false><<<2048, 64 * kFoldWaves, 0, stream_>>>(fo);
     }
     HIP_OK(hipGetLastError());
+    if (diag_mode_ == 0 && kw_fold_ && n_kwf_ci_ + n_kwf_ck_ > 0) {
+      KwFoldParams kf;
+      kf.arena = d_arena;
+      kf.off = d_offsets;
+      kf.tabs = static_cast<const uint8_t*>(d_ftabs_);
+      kf.t_items = ft_items_;
+      kf.t_item_ids = ft_item_ids_;
+      kf.t_item_cls = ft_item_cls_;
+      kf.t_classes = ft_classes_;
+      kf.pairs = static_cast<const FoldPair*>(d_kwfold_pairs_);
+      kf.n_rng_i = n_kwf_ri_;
+      kf.n_rng_k = n_kwf_rk_;
+      kf.n_cap_i = n_kwf_ci_;
+      kf.n_cap_k = n_kwf_ck_;
+      kf.folds = static_cast<const FoldSite*>(d_folds_);
+      kf.fold_cap = fold_cap_;
+      kf.counters = d_counters_;
+      kf.kwbits = static_cast<uint32_t*>(d_kw_);
+      kf.kw_words = kw_words_;
+      kwfold_kernel<<<1024, 64 * kFoldWaves, 0, stream_>>>(kf);
+      HIP_OK(hipGetLastError());
+    }
     HIP_OK(hipEventRecord(ev_[4], stream_));
     NfaParams np;
     np.arena = d_arena;
@@ -1915,6 +2097,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.fullscan_rules = d_fullscan_rules_;
     np.n_fullscan_rules = n_fullscan_rules_;
     np.fs_chunk = fs_chunk_;
+    np.kw_fold = kw_fold_ ? 1u : 0u;  // no keyword takes 'i' / 'k': the bits are exact without the kernel
 
     if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());

@@ -177,6 +177,7 @@ struct Cand {
   std::vector<std::vector<int>> lit_nodes;  // per literal: the class nodes of its chars
   size_t pre_k = 0;                          // top-level flattened items before the literal(s)
   std::vector<std::pair<std::string, std::vector<int>>> variants;  // every branch literal before dedupe
+  bool class_run = false;  // ExtractClassRun: a run of one-byte classes, not a literal
   size_t minlen() const {
     size_t m = SIZE_MAX;
     for (auto& l : lits) m = std::min(m, l.size());
@@ -300,6 +301,90 @@ bool ExtractAnchor(const Regex& re, Cand* best, bool need_offset = true) {
     }
   }
   return have && best->minlen() >= 2;
+}
+
+bool ExactSet(const Node& n, ByteSet* out);
+
+// Anchor for a rule with no required literal (else it would run in full-scan
+// mode over every file with an open gate): the rarest run of fixed one-byte
+// positions -- classes with an exact byte set (ASCII members, fold-only runes
+// left to the fold kernel) and fixed repeats of them -- at a bounded offset,
+// e.g. [g-z]{3}[0-9]{3}[._-] in `\b[g-z]{3}[0-9]{3}[._-][a-z0-9]{16}\b`.  Every
+// match holds the run at [olo, ohi], exactly as for a literal anchor (the
+// prefilter items are byte sets either way).  Taken only when its least
+// likely 6-position window is below kClassRunMaxProb (printable-uniform prior);
+// a commoner run would cost more than the gated full scans.
+constexpr double kClassRunMaxProb = 1e-5;
+bool ExtractClassRun(const Regex& re, Cand* best) {
+  const std::vector<Node>& nodes = re.nodes();
+  Analyzer an(nodes, false), anf(nodes, true);
+  std::vector<int> items;
+  an.Flatten(re.root(), &items);
+  auto prob = [](const ByteSet& b) {
+    int n = 0;
+    for (int c = 0x20; c < 0x7F; c++) n += b.test(size_t(c));
+    n += b.test('\n') + b.test('\t');
+    return double(n) / 97.0;
+  };
+  int64_t olo = 0, ohi = 0, ohf = 0;
+  double best_p = kClassRunMaxProb;
+  bool have = false;
+  for (size_t k = 0; k < items.size() && ohi < kInf; k++) {
+    std::vector<int> pos;
+    std::vector<double> ps;
+    size_t j = k;
+    while (j < items.size() && pos.size() < kMaxAnchorLit) {
+      const Node& n = nodes[items[j]];
+      ByteSet b;
+      if (n.op == NodeOp::Class && ExactSet(n, &b)) {
+        pos.push_back(items[j]);
+        ps.push_back(prob(b));
+        j++;
+        continue;
+      }
+      if (n.op == NodeOp::Repeat && n.min >= 1 && n.max == n.min) {
+        int sub = n.subs[0];
+        while (nodes[sub].op == NodeOp::Capture) sub = nodes[sub].subs[0];
+        if (nodes[sub].op == NodeOp::Class && ExactSet(nodes[sub], &b) &&
+            pos.size() + size_t(n.min) <= kMaxAnchorLit) {
+          for (int m = 0; m < n.min; m++) {
+            pos.push_back(sub);
+            ps.push_back(prob(b));
+          }
+          j++;
+          continue;
+        }
+      }
+      break;
+    }
+    if (pos.size() >= 3) {
+      double p_run = 1.0;  // the least likely window of <= 6 positions (what the prefilter keeps)
+      const size_t wl = std::min<size_t>(pos.size(), 6);
+      for (size_t a = 0; a + wl <= pos.size(); a++) {
+        double pw = 1.0;
+        for (size_t q = a; q < a + wl; q++) pw *= ps[q];
+        p_run = a == 0 ? pw : std::min(p_run, pw);
+      }
+      if (p_run < best_p) {
+        best_p = p_run;
+        Cand cd{{std::string(pos.size(), '\x01')}, olo, ohi};
+        cd.ohi_fold = ohf;
+        cd.follow.push_back(std::vector<int>(items.begin() + long(j), items.end()));
+        cd.lit_nodes.push_back(pos);
+        cd.pre_k = k;
+        cd.variants.push_back({cd.lits[0], pos});
+        cd.class_run = true;
+        *best = cd;
+        have = true;
+      }
+    }
+    auto b = an.Bytes(items[k]);
+    auto bf = anf.Bytes(items[k]);
+    olo += b.first;
+    ohi = (ohi >= kInf || b.second >= kInf) ? kInf : ohi + b.second;
+    ohf = (ohf >= kInf || bf.second >= kInf) ? kInf : ohf + bf.second;
+  }
+  return have;
 }
 
 // ---------------------------------------------------------------------------
@@ -943,7 +1028,9 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     std::string desc = "-";
     if (re) {
       Cand best{{}, 0, 0};
-      if (ExtractAnchor(*re, &best)) {
+      const char* cr_env = std::getenv("TSG_CLASS_RUNS");  // 0: literal anchors only (full-scan tests)
+      const bool class_runs = !cr_env || std::atoi(cr_env) != 0;
+      if (ExtractAnchor(*re, &best) || (class_runs && ExtractClassRun(*re, &best))) {
         rg.anchored = 1;
         desc = "[" + std::to_string(best.olo) + "," + std::to_string(best.ohi) + "]";
         for (size_t li = 0; li < best.lits.size(); li++) {
@@ -981,7 +1068,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
             fi.sets.insert(fi.sets.end(), after.begin(), after.end());
             out->items.push_back(std::move(fi));
           }
-          desc += " " + l;
+          desc += best.class_run ? " <" + std::to_string(l.size()) + " classes>" : " " + l;
         }
       } else {
         rg.anchored = 0;
@@ -1011,6 +1098,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
   {
     uint32_t nb = 16, nw = 6;
     if (const char* e = std::getenv("TSG_FILTER_BUCKETS")) nb = uint32_t(std::atoi(e));
+    if (const char* e = std::getenv("TSG_FILTER_WINDOW")) nw = uint32_t(std::atoi(e));  // model experiments
     auto ft = std::make_shared<FilterTables>();
     if (!BuildFilter(out->items, nw, nb, ft.get(), err)) return false;
     out->filter = ft;

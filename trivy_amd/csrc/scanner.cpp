@@ -46,6 +46,30 @@ struct Loc {
   int64_t s, e;
 };
 
+bool IsAsciiStr(const std::string& s) {
+  for (unsigned char c : s)
+    if (c >= 0x80) return false;
+  return true;
+}
+
+// Index of kw's least frequent character (English letter order; non-letters
+// rarest): the byte AsciiCaseContains scans for with memchr.
+size_t RarestIndex(const std::string& kw) {
+  static const char* kFreq = "etaoinshrdlcumwfgypbvkjxqz";
+  size_t best = 0;
+  int best_rank = -1;
+  for (size_t i = 0; i < kw.size(); i++) {
+    const char c = kw[i];
+    const char* f = (c >= 'a' && c <= 'z') ? std::strchr(kFreq, c) : nullptr;
+    const int rank = f ? int(f - kFreq) : 100;
+    if (rank > best_rank) {
+      best_rank = rank;
+      best = i;
+    }
+  }
+  return best;
+}
+
 // ---------------------------------------------------------------------------
 // Go sort.Slice = pdqsort_func (sort/zsortfunc.go), restated.
 // ---------------------------------------------------------------------------
@@ -316,6 +340,10 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
         if (names[k] == r.secret_group_name) r.group_idx.push_back(int(k));
     }
     for (auto& kw : r.keywords) r.kw_lower_host.push_back(GoBytesToLower((const uint8_t*)kw.data(), kw.size()));
+    for (auto& kw : r.kw_lower_host) {
+      r.kw_ascii.push_back(IsAsciiStr(kw) ? 1 : 0);
+      r.kw_rare.push_back(uint16_t(RarestIndex(kw)));
+    }
   }
   BuildAllowPathFilter();
   const char* ht = std::getenv("TSG_HOST_THREADS");
@@ -454,22 +482,10 @@ bool FoldCaseContains(const uint8_t* s, size_t n, const std::string& kw) {
 
 // Is the lowercase ASCII string kw a substring of the content with ASCII letters
 // case-folded?  Scans with memchr for kw's least frequent character (both cases).
-bool AsciiCaseContains(const uint8_t* s, size_t n, const std::string& kw) {
+bool AsciiCaseContains(const uint8_t* s, size_t n, const std::string& kw, size_t best) {
   const size_t m = kw.size();
   if (m == 0) return true;
   if (n < m) return false;
-  static const char* kFreq = "etaoinshrdlcumwfgypbvkjxqz";  // English letter order
-  size_t best = 0;
-  int best_rank = -1;
-  for (size_t i = 0; i < m; i++) {
-    const char c = kw[i];
-    const char* f = (c >= 'a' && c <= 'z') ? std::strchr(kFreq, c) : nullptr;
-    const int rank = f ? int(f - kFreq) : 100;  // non-letters are rarest
-    if (rank > best_rank) {
-      best_rank = rank;
-      best = i;
-    }
-  }
   auto eq_at = [&](const uint8_t* p) {  // p = candidate start
     for (size_t i = 0; i < m; i++) {
       uint8_t c = p[i];
@@ -493,11 +509,6 @@ bool AsciiCaseContains(const uint8_t* s, size_t n, const std::string& kw) {
     }
   }
   return false;
-}
-bool IsAsciiStr(const std::string& s) {
-  for (unsigned char c : s)
-    if (c >= 0x80) return false;
-  return true;
 }
 bool AllowRulesAllow(const std::vector<AllowRuleSpec>& rules, const uint8_t* s, size_t n) {
   for (auto& a : rules)
@@ -635,11 +646,13 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
         const size_t mn = size_t(m[k + 1] - m[k]);
         // ASCII keywords in a match without U+0130 / U+212A: the ASCII
         // case-insensitive search is exact (see the whole-content case below)
-        const bool fold = HasSeq(ms, mn, "\xC4\xB0", 2) || HasSeq(ms, mn, "\xE2\x84\xAA", 3);
+        uint8_t high = 0;  // the fold runes are multi-byte: an ASCII match holds none
+        for (size_t q = 0; q < mn; q++) high |= ms[q];
+        const bool fold = (high & 0x80) && (HasSeq(ms, mn, "\xC4\xB0", 2) || HasSeq(ms, mn, "\xE2\x84\xAA", 3));
         bool go = fold;
-        for (auto& kw : R.kw_lower_host) {
-          if (!IsAsciiStr(kw)) go = true;
-          else if (!fold && AsciiCaseContains(ms, mn, kw)) {
+        for (size_t q = 0; q < R.kw_lower_host.size(); q++) {
+          if (!R.kw_ascii[q]) go = true;
+          else if (!fold && AsciiCaseContains(ms, mn, R.kw_lower_host[q], R.kw_rare[q])) {
             hit = true;
             break;
           }
@@ -675,9 +688,13 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
           fold_runes = HasSeq(content, size_t(len), "\xC4\xB0", 2) || HasSeq(content, size_t(len), "\xE2\x84\xAA", 3);
           fold_done = true;
         }
+        if (g_tail_debug && !gpu_bits) {
+          g_wholefile_bytes += len;
+          g_wholefile_calls += 1;
+        }
         if (!gpu_bits)
-          for (auto& kw : R.kw_lower_host)
-            if (IsAsciiStr(kw) && AsciiCaseContains(content, size_t(len), kw)) {
+          for (size_t q = 0; q < R.kw_lower_host.size(); q++)
+            if (R.kw_ascii[q] && AsciiCaseContains(content, size_t(len), R.kw_lower_host[q], R.kw_rare[q])) {
               hit = true;
               break;
             }

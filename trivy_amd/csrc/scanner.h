@@ -45,6 +45,8 @@ struct RuleSpec {
   std::vector<std::unique_ptr<Regex>> exclude;
   std::vector<int> group_idx;  // capture indices named secret_group_name
   std::vector<std::string> kw_lower_host;  // for host-verified gates
+  std::vector<uint8_t> kw_ascii;           // per kw_lower_host entry: all bytes ASCII
+  std::vector<uint16_t> kw_rare;           // per entry: index of its least frequent letter (memchr key)
 };
 
 // Findings of one file, flat: records plus one text pool for every match and
