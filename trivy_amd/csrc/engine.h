@@ -13,7 +13,7 @@ namespace tsg {
 constexpr uint32_t kChunk = 1024;  // bytes per chunk of the per-chunk '\n' counts and chunk -> file map
 
 constexpr uint32_t kCandGateOpen = 1;   // a keyword of the rule occurs in the file (ASCII, GPU bits)
-constexpr uint32_t kCandFoldFile = 2;   // the file holds U+0130 / U+212A (keywords may hide behind them)
+constexpr uint32_t kCandFoldFile = 2;   // keyword bits may miss occurrences through U+0130 / U+212A in this file
 constexpr uint32_t kCandGateValid = 4;  // the two bits above were computed (GPU candidates)
 constexpr uint32_t kCandDrop = 8;       // MatchKeywords is false for the rule in this file (never reaches the host)
 
@@ -114,6 +114,7 @@ class GpuEngine {
   // confirm-only part of the table blob (after the fold kernel's prefix): the
   // core tables over byte classes (filter.h core, columns deduplicated)
   uint32_t ftabs_fold_bytes_ = 0, ft_cmap_ = 0, ft_ccore_ = 0, ft_gitems_ = 0, ft_bgroups_ = 0, n_core_cls_ = 0;
+  uint32_t ft_hkeys_ = 0, ft_hitems_ = 0, hash_bits_ = 0, hash_buckets_ = 0;  // literal-window hash
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;

@@ -554,6 +554,8 @@ struct ConfirmParams {
   // LDS tables only: the core tables over byte classes -- class of byte b at
   // tabs[t_cmap + b], group g's column of class c at u64 [t_ccore/8 + g * n_cls + c]
   uint32_t t_cmap, t_ccore, t_gitems, t_bgroups, n_cls;
+  // literal-window hash (filter.h): keys at u64 [t_hkeys/8], items at u32 [t_hitems/4], 2^hash_bits slots
+  uint32_t t_hkeys, t_hitems, hash_bits, hash_buckets;
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -754,12 +756,14 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     return (pos >= w0 && pos < w0 + kCWin) ? uint32_t(wwin[l * kCWin + (pos - w0)]) : uint32_t(P.arena[pos]);
   };
   // phase C for one queued candidate: item `ix` whose window ends at lane l's block + k
-  auto check_item = [&](uint32_t l, uint32_t k, uint32_t ix) {
+  auto check_item = [&](uint32_t l, uint32_t k, uint32_t ix, uint32_t full) {
     const FilterItemGpu it = items[ix];
     const uint64_t base = wbase[l];
     const int64_t start = int64_t(base + k) + 1 - int64_t(it.back);
     if (start < 0 || uint64_t(start) + it.n > P.n_bytes) return;
-    const uint32_t core_lo = it.back > 8 ? it.back - 8u : 0u;  // [core_lo, back) verified by the core tables
+    // [core_lo, back) verified by the core tables; a hashed candidate (full)
+    // matched its case-folded window only, so every position is checked
+    const uint32_t core_lo = full ? uint32_t(it.back) : (it.back > 8 ? it.back - 8u : 0u);
     // Positions [q0, q1) outside the core range, checked exactly: all of them,
     // before the follow requirements (measured on C2: checking the lookahead
     // sets only after a follow requirement passed, TSG_DIAG_CONFIRM=32, costs
@@ -828,12 +832,8 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
       atomicAdd(&cnt[3], 1u);
       const FollowLut lut = reinterpret_cast<const FollowLut*>(tabs + P.t_luts)[aid];
       if (lut.n[0] && e < P.n_bytes) {
-        if (!have_x) {
-          const uint64_t s = e - w0;
-          if (e >= w0 && (s & ~uint64_t(3)) + 56 <= uint64_t(kCWin))
-            follow_words(reinterpret_cast<const uint32_t*>(wwin + l * kCWin + (s & ~uint64_t(3))), uint32_t(s), X);
-          else
-            follow_words(reinterpret_cast<const uint32_t*>(P.arena + (e & ~uint64_t(3))), uint32_t(e), X);
+        if (!have_x) {  // through the caches: the lane's 48-B window rarely holds the span
+          follow_words(reinterpret_cast<const uint32_t*>(P.arena + (e & ~uint64_t(3))), uint32_t(e), X);
           have_x = true;
         }
         if (!follow_lut_pass(lut, X, int64_t(fe - e))) continue;
@@ -850,7 +850,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     for (uint32_t c2 = 0; c2 < m2; c2 += 64) {
       if (c2 + lane < m2) {
         const uint32_t e = q2[c2 + lane];
-        check_item(e & 63u, (e >> 6) & 15u, e >> 10);
+        check_item(e & 63u, (e >> 6) & 15u, (e >> 10) & 0x1FFFFFu, e >> 31);
       }
       if (__builtin_amdgcn_readfirstlane(cnt[0]) >= 64) flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
     }
@@ -868,6 +868,28 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     for (int q = 0; q < 8; q++) {
       const int64_t pos = int64_t(base + k) - 7 + q;
       cb[q] = pos < 0 ? 0u : win_byte(l, uint64_t(pos));
+    }
+    auto queue_item = [&](uint32_t ix, uint32_t full) {
+      const uint32_t slot = atomicAdd(&cnt[2], 1u);
+      if (slot < kCQ2) q2[slot] = l | (k << 6) | (ix << 10) | (full << 31);
+      else check_item(l, k, ix, full);  // queue full: check in place
+    };
+    if (fm & P.hash_buckets) {  // literal windows: one probe with the lowercased 6 bytes
+      uint64_t key = 0;
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const uint32_t b = cb[2 + q];
+        key |= uint64_t(b - 'A' < 26u ? b + 32 : b) << (8 * q);
+      }
+      const uint64_t* hk = reinterpret_cast<const uint64_t*>(tabs + P.t_hkeys);
+      const uint32_t* hi = reinterpret_cast<const uint32_t*>(tabs + P.t_hitems);
+      const uint32_t mask = (1u << P.hash_bits) - 1;
+      const uint64_t want = key | (uint64_t(1) << 63);
+      for (uint32_t slot = WindowHash(key, P.hash_bits);; slot = (slot + 1) & mask) {
+        const uint64_t kk = hk[slot];
+        if (!kk) break;
+        if (kk == want) queue_item(hi[slot], 1u);
+      }
     }
     // LDS tables: the bytes' classes once per fire, then one ds_read_b64 per
     // byte and group (the global tables cost an L2 round trip per group)
@@ -890,10 +912,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
         while (im) {
           const uint32_t gi = __builtin_ctz(im);
           im &= im - 1;
-          const uint32_t ix = gitems[g * 8 + gi];
-          const uint32_t slot = atomicAdd(&cnt[2], 1u);
-          if (slot < kCQ2) q2[slot] = l | (k << 6) | (ix << 10);
-          else check_item(l, k, ix);  // queue full: check in place
+          queue_item(gitems[g * 8 + gi], 0u);
         }
       }
     }
@@ -1193,7 +1212,9 @@ __global__ __launch_bounds__(64 * kFoldWaves) void kwfold_kernel(KwFoldParams P)
 
 // Candidate flags for the host's lazy MatchKeywords (scanner.go:174-186).
 __device__ uint32_t gate_flags(const NfaParams& P, const RuleGpu& rg, uint32_t f) {
-  uint32_t fl = kCandGateValid | ((P.flags[f] & 4u) ? kCandFoldFile : 0u);
+  // kCandFoldFile: the bits may miss occurrences through U+0130 / U+212A, the
+  // host re-checks the whole content (not after kwfold_kernel covered them)
+  uint32_t fl = kCandGateValid | (kw_bits_inexact(P, f) ? kCandFoldFile : 0u);
   if (rg.gate == kGateKeywords && !rg.kw_match_implied) {
     const uint32_t* kb = P.kwbits + uint64_t(f) * P.kw_words;
     for (uint32_t i = 0; i < rg.kw_cnt; i++) {
@@ -1529,6 +1550,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       ft_ccore_ = put(cc.data(), cc.size() * sizeof(uint64_t));
       ft_gitems_ = put(ft->group_items.data(), ft->group_items.size() * 4);
       ft_bgroups_ = put(ft->bucket_groups.data(), ft->bucket_groups.size() * 4);
+      ft_hkeys_ = put(ft->hash_keys.data(), ft->hash_keys.size() * 8);
+      ft_hitems_ = put(ft->hash_items.data(), ft->hash_items.size() * 4);
+      hash_bits_ = ft->hash_bits;
+      hash_buckets_ = ft->hash_keys.empty() ? 0u : ft->hash_buckets;
     }
     ftabs_bytes_ = uint32_t(tb.size());
     n_fitems_ = uint32_t(ft->items.size());
@@ -2017,6 +2042,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     cp.t_gitems = ft_gitems_;
     cp.t_bgroups = ft_bgroups_;
     cp.n_cls = n_core_cls_;
+    cp.t_hkeys = ft_hkeys_;
+    cp.t_hitems = ft_hitems_;
+    cp.hash_bits = hash_bits_;
+    cp.hash_buckets = hash_buckets_;
     if (diag_mode_ == 0) {
       if (lds_tabs_)
         confirm_kernel<true><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);

@@ -273,11 +273,66 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     }
     out->bucket_off.push_back(uint32_t(out->bucket_items.size()));
   }
-  // core tables (filter.h)
+  // literal windows -> hash table (filter.h); the rest -> core groups
+  std::vector<uint8_t> hashed(n, 0);
+  std::vector<std::pair<uint64_t, uint32_t>> hkeys;
+  const char* hash_env = std::getenv("TSG_WINDOW_HASH");  // 0: core groups only (A/B)
+  // Large rule sets only: builtin-sized buckets hold 1-2 groups, whose LDS core
+  // lookups beat a probe plus the full position check (C2 confirm 5.08 vs 5.35
+  // ms with hashing; C3, 2,108 items: 25.0 -> 4.0 ms, profiles/r02_wl/wl_r02h_*)
+  const bool use_hash = hash_env ? std::atoi(hash_env) != 0 && S == 6 : (S == 6 && n > 256);
+  for (size_t i = 0; i < n && use_hash; i++) {
+    const FilterItemGpu& g = out->items[i];
+    if (g.back < 6) continue;
+    uint64_t key = 0;
+    bool ok = true;
+    for (int q = 0; q < 6 && ok; q++) {
+      const ByteSet& b = uniq[i].sets[size_t(g.back - 6 + q)];
+      const size_t pc = b.count();
+      int c = -1;
+      for (int x = 0; x < 128 && pc <= 2; x++)
+        if (b.test(size_t(x))) {
+          c = x;
+          break;
+        }
+      if (c < 0 || pc > 2) {
+        ok = false;
+        break;
+      }
+      for (int x = 128; x < 256; x++)
+        if (b.test(size_t(x))) ok = false;
+      if (pc == 2) ok = ok && c >= 'A' && c <= 'Z' && b.test(size_t(c + 32));
+      const int lc = (c >= 'A' && c <= 'Z') ? c + 32 : c;
+      key |= uint64_t(lc) << (8 * q);
+    }
+    if (!ok) continue;
+    hashed[i] = 1;
+    hkeys.push_back({key, uint32_t(i)});
+  }
+  if (!hkeys.empty()) {
+    uint32_t bits = 4;
+    while ((size_t(1) << bits) < 2 * hkeys.size()) bits++;
+    out->hash_bits = bits;
+    out->hash_keys.assign(size_t(1) << bits, 0);
+    out->hash_items.assign(size_t(1) << bits, 0);
+    for (auto& kv : hkeys) {
+      uint32_t slot = WindowHash(kv.first, bits);
+      while (out->hash_keys[slot]) slot = (slot + 1) & ((1u << bits) - 1);
+      out->hash_keys[slot] = kv.first | (uint64_t(1) << 63);
+      out->hash_items[slot] = kv.second;
+    }
+    for (uint32_t b = 0; b < n_buckets; b++)
+      for (uint32_t k = out->bucket_off[b]; k < out->bucket_off[b + 1]; k++)
+        if (hashed[out->bucket_items[k]]) out->hash_buckets |= 1u << b;
+  }
+  // core tables (filter.h), over the items not hashed
   out->bucket_groups.push_back(0);
   uint32_t n_groups = 0;
   for (uint32_t b = 0; b < n_buckets; b++) {
-    const uint32_t lo = out->bucket_off[b], hi = out->bucket_off[b + 1];
+    std::vector<uint32_t> grp;
+    for (uint32_t k = out->bucket_off[b]; k < out->bucket_off[b + 1]; k++)
+      if (!hashed[out->bucket_items[k]]) grp.push_back(out->bucket_items[k]);
+    const uint32_t lo = 0, hi = uint32_t(grp.size());
     for (uint32_t g0 = lo; g0 < hi; g0 += 8) {
       std::vector<uint64_t> tab(256, 0);
       for (uint32_t i = 0; i < 8; i++) {
@@ -285,7 +340,7 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
           out->group_items.push_back(0xFFFFFFFFu);
           continue;
         }
-        const uint32_t item = out->bucket_items[g0 + i];
+        const uint32_t item = grp[g0 + i];
         out->group_items.push_back(item);
         const FilterItem& it = uniq[item];
         const int back = out->items[item].back;

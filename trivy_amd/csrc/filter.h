@@ -57,10 +57,31 @@ struct FilterTables {
   std::vector<uint64_t> core;            // n_groups x 256
   std::vector<uint32_t> group_items;     // n_groups x 8 item indices (0xFFFFFFFF: none)
   std::vector<uint32_t> bucket_groups;   // n_buckets + 1 into the groups
+  // Literal windows are confirmed by hashing instead: an item whose 6 window
+  // sets are single ASCII characters (either case) is keyed by its window
+  // lowercased (byte q at bits 8q, the window end in byte 5) in an
+  // open-addressed table of 2^hash_bits slots (key | 1 << 63; 0 = empty); the
+  // core groups hold the other items only.  One probe per fire replaces the
+  // group scans of large literal sets.
+  std::vector<uint64_t> hash_keys;
+  std::vector<uint32_t> hash_items;
+  uint32_t hash_bits = 0;
+  uint32_t hash_buckets = 0;             // buckets holding hashed items
   uint32_t max_after = 0;                // max positions an item extends past its window end
   double est_fp = 0;                     // estimated bucket fires per input byte
 
 };
+
+// Key hash of the literal-window table, shared by the host build (g++) and the
+// confirm kernel (hipcc compiles it for both sides).
+#if defined(__HIPCC__)
+#define TSG_HOST_DEVICE __host__ __device__
+#else
+#define TSG_HOST_DEVICE
+#endif
+TSG_HOST_DEVICE inline uint32_t WindowHash(uint64_t key, uint32_t bits) {
+  return uint32_t((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
 
 // Static byte-frequency prior of source/text bytes (sums to 1).
 const std::vector<double>& BytePrior();

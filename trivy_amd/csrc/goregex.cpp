@@ -915,6 +915,21 @@ std::unique_ptr<Regex> Regex::Compile(const std::string& pattern, std::string* e
     }
   }
   re->ComputeFirstBytes();
+  {  // instructions whose only predecessor is one rune instruction (Backtracker chain skip)
+    std::vector<uint32_t> preds(re->prog_.size(), 0);
+    std::vector<uint8_t> from_rune(re->prog_.size(), 0);
+    for (const Inst& in : re->prog_) {
+      switch (in.op) {
+        case kIAlt: preds[in.out]++; preds[in.arg]++; break;
+        case kICapture: case kIEmpty: case kINop: preds[in.out]++; break;
+        case kIRune: case kIRune1: case kIAny: case kIAnyNotNL: preds[in.out]++; from_rune[in.out] = 1; break;
+        default: break;
+      }
+    }
+    preds[re->start_]++;  // the start state is entered from outside
+    re->single_pred_.assign(re->prog_.size(), 0);
+    for (size_t pc = 0; pc < re->prog_.size(); pc++) re->single_pred_[pc] = preds[pc] == 1 && from_rune[pc];
+  }
   return re;
 }
 
@@ -1326,10 +1341,27 @@ class Backtracker {
         case kIRune1:
         case kIAny:
         case kIAnyNotNL: {
-          const Rune r = DecodeRune(s_, n_, pos);
-          if (!re_->RuneMatch(in, r.r)) continue;
-          pos += r.width;
+          // ASCII bytes inline (the classes' ASCII bitmaps); other runes decoded
+          if (pos < n_ && s_[pos] < 0x80) {
+            const uint32_t c = s_[pos];
+            bool ok;
+            if (in.op == kIRune) {
+              const auto& a = re_->class_ascii_[size_t(in.cls)];
+              ok = ((c < 64 ? a.first : a.second) >> (c & 63)) & 1;
+            } else {
+              ok = in.op == kIRune1 ? c == in.rune : (in.op == kIAny || c != '\n');
+            }
+            if (!ok) continue;
+            pos += 1;
+          } else {
+            const Rune r = DecodeRune(s_, n_, pos);
+            if (!re_->RuneMatch(in, r.r)) continue;
+            pos += r.width;
+          }
           pc = in.out;
+          // a successor reached from this instruction only: (pc, pos) cannot have
+          // been visited, since its one predecessor state is visited once
+          if (re_->single_pred_[pc]) goto skip;
           goto check;
         }
         case kICapture:

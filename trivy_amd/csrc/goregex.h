@@ -103,6 +103,7 @@ class Regex {
   // Bytes that can begin a match (the first byte of its first rune), from the
   // program's start closure; first_all_ when a match can be empty or start
   // with any byte.  Starts at other bytes are skipped (an exact pruning).
+  std::vector<uint8_t> single_pred_;  // pc entered only from one rune instruction (no visited bit needed)
   uint64_t first_[4] = {};
   bool first_all_ = true;
   void ComputeFirstBytes();

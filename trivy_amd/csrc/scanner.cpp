@@ -373,6 +373,7 @@ void SecretScanner::BuildAllowPathFilter() {
   if (allow_.size() > 64) return;
   ap_pair_.assign(65536, 0);
   ap_lits_.clear();
+  for (auto& w : ap_first_) w = 0;
   ap_always_ = 0;
   for (size_t i = 0; i < allow_.size(); i++) {
     const Matcher* m = allow_[i].path.get();
@@ -385,6 +386,7 @@ void SecretScanner::BuildAllowPathFilter() {
       continue;
     }
     for (auto& l : m->lits) {
+      ap_first_[uint8_t(l[0]) >> 6] |= uint64_t(1) << (uint8_t(l[0]) & 63);
       uint16_t& slot = ap_pair_[(uint32_t(uint8_t(l[0])) << 8) | uint8_t(l[1])];
       if (!slot) {
         ap_lits_.emplace_back();
@@ -403,15 +405,16 @@ bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
   // literal present (plus the unfiltered ones) run their regex.
   if (ap_fast_ && n <= 1024) {
     uint8_t low[1024];
-    bool ascii = true;
-    for (size_t i = 0; i < n; i++) {
+    uint8_t high = 0;
+    for (size_t i = 0; i < n; i++) {  // branch-free ASCII lowering (vectorised)
       const uint8_t b = p[i];
-      ascii = ascii && b < 0x80;
-      low[i] = (b >= 'A' && b <= 'Z') ? uint8_t(b + 32) : b;
+      high |= b;
+      low[i] = uint8_t(b + ((uint8_t(b - 'A') < 26) ? 32 : 0));
     }
-    if (ascii) {
+    if (!(high & 0x80)) {
       uint64_t lit_rules = 0;
       for (size_t i = 0; i + 1 < n; i++) {
+        if (!((ap_first_[low[i] >> 6] >> (low[i] & 63)) & 1)) continue;  // L1-resident test first
         const uint16_t slot = ap_pair_[(uint32_t(low[i]) << 8) | low[i + 1]];
         if (!slot) continue;
         for (auto& lr : ap_lits_[slot - 1])
