@@ -250,8 +250,12 @@ def main():
                     help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
                          "the walk's host threads")
     ap.add_argument("--pool-gb", type=float, default=64.0, help="c5: page-locked host pool size")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-file", default=None,
+                    help="PMC traffic summary (default profiles/traffic_r02_<workload>.json, c2: traffic_r02.json)")
     args = ap.parse_args()
+    if args.traffic_file is None:
+        per_wl = os.path.join(ROOT, "profiles", "traffic_r02_%s.json" % args.workload)
+        args.traffic_file = per_wl if os.path.exists(per_wl) else os.path.join(ROOT, "profiles", "traffic_r02.json")
     wl_desc, gb_default, cpu_mb_default, parity_mb_default = WORKLOADS[args.workload]
     if args.parity_mb is None:
         args.parity_mb = parity_mb_default
