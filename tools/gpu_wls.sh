@@ -20,6 +20,7 @@ for w in ${WLS:-c2 c3 c3u c4 c5}; do
     c3u) run c3u 400 --workload c3u --steps 5 --warmup 1 --no-cpu-baseline ;;
     c3u0) TSG_CLASS_RUNS=0 run c3u0 400 --workload c3u --steps 3 --warmup 1 --no-cpu-baseline ;;
     c3h0) TSG_WINDOW_HASH=0 run c3h0 400 --workload c3 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    c3f0) TSG_FOLD_INDEX=0 run c3f0 400 --workload c3 --steps 5 --warmup 1 --no-cpu-baseline ;;
     c2h0) TSG_WINDOW_HASH=0 run c2h0 400 --steps 20 --warmup 5 --no-cpu-baseline --ingest-steps 0 ;;
     c4) run c4 500 --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c5) run c5 500 --workload c5 --steps 2 --warmup 1 --pool-gb 32 --no-cpu-baseline ;;

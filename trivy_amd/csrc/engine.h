@@ -106,6 +106,10 @@ class GpuEngine {
   void* d_fold_pairs_ = nullptr;  // fold kernel work list
   void* d_fold_first_ = nullptr;  // per item: bytes that can start it (fold kernel prefilter)
   uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0, n_fold_cap_k_ = 0, n_fold_cap_s_ = 0;
+  void* d_fold_idx_off_ = nullptr;   // fold kernel: capable tasks by (rune kind, q, key byte)
+  void* d_fold_idx_items_ = nullptr;
+  uint32_t n_fold_cap_k_idx_ = 0, n_fold_cap_s_idx_ = 0;
+  bool fold_idx_ = true;
   void* d_kwfold_pairs_ = nullptr;  // kwfold kernel work list (keyword items through U+0130 / U+212A)
   uint32_t n_kwf_ri_ = 0, n_kwf_rk_ = 0, n_kwf_ci_ = 0, n_kwf_ck_ = 0;
   bool kw_fold_ = false;

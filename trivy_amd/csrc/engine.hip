@@ -1017,6 +1017,14 @@ struct FoldParams {
   const FoldPair* pairs;  // [k ranges | s ranges | k capable | s capable]
   uint32_t n_pairs_k, n_pairs_s, n_cap_k, n_cap_s;
   const uint32_t* first;  // per item 8 x u32: bytes its position 0 accepts (+ E2 / C5 fold leads)
+  // Capable tasks indexed by (rune kind, q, key byte): the byte at x - q (the
+  // item's position 0) for q > 0, the byte after the rune (position 1) for
+  // q = 0.  idx_off[(kind * kFoldIdxQ + q) * 257 + b] .. [+1] -> idx_items;
+  // tasks with q >= kFoldIdxQ or a single position stay in the pair lists.
+  const uint32_t* idx_off;
+  const uint32_t* idx_items;
+  uint32_t use_idx;
+  uint32_t n_cap_k_idx, n_cap_s_idx;  // leading capable pairs covered by the index
   const FoldSite* folds;
   uint32_t fold_cap;
   uint32_t* hits;
@@ -1025,6 +1033,7 @@ struct FoldParams {
 };
 
 constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
+constexpr int kFoldIdxQ = 64;      // capable positions q < kFoldIdxQ go through the byte index (one lane per q)
 constexpr int kFoldWin = 2 * kFoldSpan + 16;
 constexpr int kFoldWaves = 4;
 
@@ -1036,6 +1045,7 @@ template <bool kLdsTabs>  // as confirm_kernel
 __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint8_t s_win[kFoldWaves][kFoldWin];
+  __shared__ uint32_t s_idx[kFoldWaves][2][64];  // per wave: index lists' exclusive prefix and start, per q
   if (kLdsTabs) {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(smem);
@@ -1074,45 +1084,86 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
         other = true;
     }
     other = __ballot(other) != 0;
+    // one start: item `ix` beginning `back` bytes before the rune, matched fold-tolerantly
+    auto try_start = [&](uint32_t ix, uint32_t back) {
+      if (fsite.x < w0 + back) return;
+      const FilterItemGpu it = items[ix];
+      const uint32_t* first = firsts + 8ull * ix;
+      const uint64_t st = fsite.x - back;
+      const uint32_t b0 = wb[st - w0];
+      if (!((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
+      uint64_t p = st, lit_bytes_end = 0;
+      bool ok = true, covered = false;
+      for (uint32_t q = 0; q < it.n && ok; q++) {
+        if (q == it.lit_end) lit_bytes_end = p;
+        if (p >= w1) {
+          ok = false;
+          break;
+        }
+        covered = covered || p == fsite.x;
+        const uint32_t c = item_cls[it.cls_off + q];
+        const uint32_t b = wb[p - w0];
+        if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
+            (in_cls(c, 'k') || in_cls(c, 'K'))) {
+          p += 3;
+        } else if (b == 0xC5 && p + 1 < w1 && wb[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
+          p += 2;
+        } else if (in_cls(c, b)) {
+          p += 1;
+        } else {
+          ok = false;
+        }
+      }
+      if (!ok || !covered) return;
+      if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
+      for (uint32_t d = 0; d < it.n_ids; d++)
+        put_hit(P.hits, P.hit_cap, P.counters, fsite.f, uint32_t(lit_bytes_end - fs), item_ids[it.ids_off + d]);
+    };
     const FoldPair* pairs = P.pairs + (other ? (kay ? 0 : P.n_pairs_k)
                                              : P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k));
     const uint32_t n_pairs = other ? (kay ? P.n_pairs_k : P.n_pairs_s) : (kay ? P.n_cap_k : P.n_cap_s);
-    for (uint32_t t = lane; t < n_pairs; t += 64) {
-      const FoldPair fp = pairs[t];
-      const FilterItemGpu it = items[fp.item];
-      const uint32_t* first = firsts + 8ull * fp.item;
-      for (uint32_t back = fp.lo; back <= fp.hi; back++) {
-        if (fsite.x < w0 + back) break;
-        const uint64_t st = fsite.x - back;
-        const uint32_t b0 = wb[st - w0];
-        if (!((first[b0 >> 5] >> (b0 & 31)) & 1u)) continue;  // position 0 fails (superset test)
-        uint64_t p = st, lit_bytes_end = 0;
-        bool ok = true, covered = false;
-        for (uint32_t q = 0; q < it.n && ok; q++) {
-          if (q == it.lit_end) lit_bytes_end = p;
-          if (p >= w1) {
-            ok = false;
-            break;
-          }
-          covered = covered || p == fsite.x;
-          const uint32_t c = item_cls[it.cls_off + q];
-          const uint32_t b = wb[p - w0];
-          if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
-              (in_cls(c, 'k') || in_cls(c, 'K'))) {
-            p += 3;
-          } else if (b == 0xC5 && p + 1 < w1 && wb[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
-            p += 2;
-          } else if (in_cls(c, b)) {
-            p += 1;
-          } else {
-            ok = false;
-          }
-        }
-        if (!ok || !covered) continue;
-        if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
-        for (uint32_t d = 0; d < it.n_ids; d++)
-          put_hit(P.hits, P.hit_cap, P.counters, fsite.f, uint32_t(lit_bytes_end - fs), item_ids[it.ids_off + d]);
+    if (!other && P.use_idx) {
+      // indexed capable tasks: lane q looks up its list by the key byte, a
+      // wave prefix sum spreads the lists' tasks over the lanes
+      const uint32_t q = lane;
+      const uint32_t rl = kay ? 3u : 2u;
+      uint32_t key = 256;
+      if (q == 0) key = fsite.x + rl < w1 ? wb[fsite.x + rl - w0] : 256u;
+      else if (fsite.x >= w0 + q) key = wb[fsite.x - q - w0];
+      uint32_t lo = 0, cnt = 0;
+      if (key < 256) {
+        const uint32_t* o = P.idx_off + (size_t(kay ? 0 : 1) * kFoldIdxQ + q) * 257 + key;
+        lo = o[0];
+        cnt = o[1] - lo;
       }
+      uint32_t incl = cnt;  // inclusive prefix over the lanes
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(incl, d);
+        if (lane >= uint32_t(d)) incl += v;
+      }
+      const uint32_t total = __shfl(incl, 63);
+      uint32_t* ex = s_idx[wave][0];
+      uint32_t* lw = s_idx[wave][1];
+      wave_sync();
+      ex[lane] = incl - cnt;
+      lw[lane] = lo;
+      wave_sync();
+      for (uint32_t t = lane; t < total; t += 64) {
+        uint32_t a = 0, b = 63;  // the lane (q) whose range holds t: the largest with ex[q] <= t
+        while (a < b) {
+          const uint32_t m = (a + b + 1) >> 1;
+          if (ex[m] <= t) a = m;
+          else b = m - 1;
+        }
+        try_start(P.idx_items[lw[a] + (t - ex[a])], a);
+      }
+      // tasks outside the index (q >= kFoldIdxQ or single-position items) follow in the pair list
+    }
+    const uint32_t t0 = (!other && P.use_idx) ? (kay ? P.n_cap_k_idx : P.n_cap_s_idx) : 0u;
+    for (uint32_t t = t0 + lane; t < n_pairs; t += 64) {
+      const FoldPair fp = pairs[t];
+      for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(fp.item, back);
     }
   }
 }
@@ -1608,6 +1659,57 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       uint8_t* dfm = nullptr;
       if (!Upload(&err_, &dfm, reinterpret_cast<const uint8_t*>(first.data()), first.size() * sizeof(uint32_t))) return;
       d_fold_first_ = dfm;
+      // byte index of the capable tasks (FoldParams idx_*): key = the byte at
+      // x - q (position 0, one byte: no other fold rune precedes x) for q > 0,
+      // the byte after the rune (position 1, or a fold lead when position 1
+      // can be a fold rune) for q = 0.  The capable lists are reordered so the
+      // indexed tasks come first; the rest stay pair-driven.
+      {
+        std::vector<uint32_t> off(size_t(2) * kFoldIdxQ * 257 + 1, 0);
+        std::vector<std::vector<uint32_t>> lists(size_t(2) * kFoldIdxQ * 256);
+        auto index_kind = [&](std::vector<FoldPair>& cap, uint32_t kind, uint32_t* n_idx) {
+          std::vector<FoldPair> idx, rest;
+          for (const FoldPair& fp : cap) {
+            const FilterItemGpu& it = ft->items[fp.item];
+            const uint32_t q = fp.lo;
+            if (q >= uint32_t(kFoldIdxQ) || (q == 0 && it.n < 2)) {
+              rest.push_back(fp);
+              continue;
+            }
+            const uint32_t c = ft->item_cls[it.cls_off + (q == 0 ? 1 : 0)];
+            for (uint32_t b = 0; b < 256; b++) {
+              bool on = in_cls(c, b);
+              if (q == 0 && b == 0xE2) on = on || in_cls(c, 'k') || in_cls(c, 'K');
+              if (q == 0 && b == 0xC5) on = on || in_cls(c, 's') || in_cls(c, 'S');
+              if (on) lists[(size_t(kind) * kFoldIdxQ + q) * 256 + b].push_back(fp.item);
+            }
+            idx.push_back(fp);
+          }
+          *n_idx = uint32_t(idx.size());
+          idx.insert(idx.end(), rest.begin(), rest.end());
+          cap.swap(idx);
+        };
+        index_kind(ck, 0, &n_fold_cap_k_idx_);
+        index_kind(cs, 1, &n_fold_cap_s_idx_);
+        std::vector<uint32_t> items_flat;
+        for (size_t kq = 0; kq < size_t(2) * kFoldIdxQ; kq++)
+          for (uint32_t b = 0; b < 257; b++) {
+            off[kq * 257 + b] = uint32_t(items_flat.size());
+            if (b < 256) {
+              auto& l = lists[kq * 256 + b];
+              items_flat.insert(items_flat.end(), l.begin(), l.end());
+            }
+          }
+        if (items_flat.empty()) items_flat.push_back(0);
+        uint32_t* d_off = nullptr;
+        uint32_t* d_items = nullptr;
+        if (!Upload(&err_, &d_off, off.data(), off.size()) || !Upload(&err_, &d_items, items_flat.data(), items_flat.size()))
+          return;
+        d_fold_idx_off_ = d_off;
+        d_fold_idx_items_ = d_items;
+        const char* fi = std::getenv("TSG_FOLD_INDEX");  // 0: pair lists only (A/B)
+        fold_idx_ = !fi || std::atoi(fi) != 0;
+      }
       n_fold_pairs_k_ = uint32_t(pk.size());
       n_fold_pairs_s_ = uint32_t(ps.size());
       n_fold_cap_k_ = uint32_t(ck.size());
@@ -1693,7 +1795,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 
 GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
-  void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1],
                 d_kind_[0], d_kind_[1], d_xlen_, d_xoff_, d_xscan_, d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
@@ -2073,6 +2175,11 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     fo.n_cap_s = n_fold_cap_s_;
     fo.folds = static_cast<const FoldSite*>(d_folds_);
     fo.fold_cap = fold_cap_;
+    fo.idx_off = static_cast<const uint32_t*>(d_fold_idx_off_);
+    fo.idx_items = static_cast<const uint32_t*>(d_fold_idx_items_);
+    fo.use_idx = fold_idx_ ? 1u : 0u;
+    fo.n_cap_k_idx = n_fold_cap_k_idx_;
+    fo.n_cap_s_idx = n_fold_cap_s_idx_;
     fo.hits = static_cast<uint32_t*>(d_hits_);
     fo.hit_cap = hit_cap_;
     fo.counters = d_counters_;
