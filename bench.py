@@ -480,7 +480,7 @@ def main():
         roofline["frac_h2d"] = ingest["frac_h2d"]
         roofline["h2d_note"] = "per GPU, from the ingest leg (see \"ingest\")"
     if h2d_peak:
-        h2d = world * arena_bytes * args.steps / dt / 1e9 / world  # per GPU
+        h2d = n_bytes * args.steps / dt / 1e9  # per GPU: every byte of the step (all emissions) crossed PCIe
         roofline["achieved_h2d"] = round(h2d, 2)
         roofline["h2d_peak_measured"] = h2d_peak
         roofline["frac_h2d"] = round(h2d / h2d_peak, 4)
