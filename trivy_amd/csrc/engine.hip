@@ -751,10 +751,6 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   uint32_t* q2 = s_q2 + wave * kCQ2;
   uint32_t* hbuf = s_hbuf + wave * kCWaveHits * 3;
   const uint32_t n_recs = P.counters[7] < P.rec_cap ? P.counters[7] : P.rec_cap;
-  auto win_byte = [&](uint32_t l, uint64_t pos) -> uint32_t {  // arena byte via lane l's window
-    const uint64_t b = wbase[l], w0 = b >= 16 ? b - 16 : 0;
-    return (pos >= w0 && pos < w0 + kCWin) ? uint32_t(wwin[l * kCWin + (pos - w0)]) : uint32_t(P.arena[pos]);
-  };
   // phase C for one queued candidate: item `ix` whose window ends at lane l's block + k
   auto check_item = [&](uint32_t l, uint32_t k, uint32_t ix, uint32_t full) {
     const FilterItemGpu it = items[ix];
@@ -768,10 +764,13 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     // before the follow requirements (measured on C2: checking the lookahead
     // sets only after a follow requirement passed, TSG_DIAG_CONFIRM=32, costs
     // 0.35 ms more -- the sets reject half the literal hits at a lower cost).
+    const uint64_t cw0 = base >= 16 ? base - 16 : 0;  // the lane window [cw0, cw0 + kCWin)
+    const uint8_t* cwin = wwin + l * kCWin;
     auto sets_ok = [&](uint32_t q0, uint32_t q1) {
       for (uint32_t q = q0; q < q1; q++) {
         if (q >= core_lo && q < it.back) continue;
-        const uint32_t bt = win_byte(l, uint64_t(start) + q);
+        const uint64_t pos = uint64_t(start) + q;
+        const uint32_t bt = pos - cw0 < uint64_t(kCWin) ? uint32_t(cwin[pos - cw0]) : uint32_t(P.arena[pos]);
         const uint32_t c = item_cls[it.cls_off + q];
         if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return false;
       }
@@ -864,10 +863,12 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     uint32_t fm = e >> 10;
     const uint64_t base = wbase[l];
     uint32_t cb[8];  // the 8 bytes ending at the window end (zero before the arena, as in K1)
+    const uint64_t cw0 = base >= 16 ? base - 16 : 0;  // [base + k - 7, base + k] lies in the lane window
+    const uint8_t* cwin = wwin + l * kCWin;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int64_t pos = int64_t(base + k) - 7 + q;
-      cb[q] = pos < 0 ? 0u : win_byte(l, uint64_t(pos));
+      cb[q] = pos < 0 ? 0u : uint32_t(cwin[uint64_t(pos) - cw0]);
     }
     auto queue_item = [&](uint32_t ix, uint32_t full) {
       const uint32_t slot = atomicAdd(&cnt[2], 1u);
@@ -956,10 +957,13 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
       for (uint32_t k = 0; k < 16; k++) {
         reach_apply(rd1(word_of(v, k >> 2), k & 3), st);
-        uint32_t fm = 0;  // fires at window end base + k: slot 5 = bits 20..23 of each register
+        // any fire at window end base + k (slot 5 = bits 20..23 of each register,
+        // AND-ed over the registers); the per-bucket mask only then (rare)
+        const uint32_t z = st[0] & st[1] & st[2] & st[3];
+        if ((~z & 0x00F00000u) && !(P.diag & 4)) {
+          uint32_t fm = 0;
 #pragma unroll
-        for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
-        if (fm && !(P.diag & 4)) {
+          for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
           const uint32_t e = lane | (k << 6) | (fm << 10);
           const uint32_t slot = atomicAdd(&cnt[1], 1u);
           if (slot < kCQ1) q1[slot] = e;
