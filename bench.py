@@ -386,7 +386,8 @@ def main():
     ingest = None
     unregister_leg = None
     res_timed = last_res[0]  # the timed steps' last result (parity below)
-    if layer is None and args.workload == "c2" and not args.ingest and args.ingest_steps > 0:
+    # (single-process runs only: under torchrun every rank would page-lock its whole corpus)
+    if layer is None and args.workload == "c2" and not args.ingest and args.ingest_steps > 0 and world == 1:
         del d_arena, d_offs
         torch.cuda.empty_cache()
         unregister_leg = secret.HostRegister(C.arena)

@@ -373,6 +373,8 @@ void SecretScanner::BuildAllowPathFilter() {
   if (allow_.size() > 64) return;
   ap_pair_.assign(65536, 0);
   ap_lits_.clear();
+  ap_c0_.clear();
+  ap_c1_.clear();
   for (auto& w : ap_first_) w = 0;
   ap_always_ = 0;
   for (size_t i = 0; i < allow_.size(); i++) {
@@ -389,6 +391,8 @@ void SecretScanner::BuildAllowPathFilter() {
       ap_first_[uint8_t(l[0]) >> 6] |= uint64_t(1) << (uint8_t(l[0]) & 63);
       uint16_t& slot = ap_pair_[(uint32_t(uint8_t(l[0])) << 8) | uint8_t(l[1])];
       if (!slot) {
+        ap_c0_.push_back(uint8_t(l[0]));
+        ap_c1_.push_back(uint8_t(l[1]));
         ap_lits_.emplace_back();
         slot = uint16_t(ap_lits_.size());
       }
@@ -404,23 +408,45 @@ bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
   // path (byte-pair table, then the whole literal), and only the rules with a
   // literal present (plus the unfiltered ones) run their regex.
   if (ap_fast_ && n <= 1024) {
-    uint8_t low[1024];
+    alignas(32) uint8_t low[1024 + 64];
     uint8_t high = 0;
     for (size_t i = 0; i < n; i++) {  // branch-free ASCII lowering (vectorised)
       const uint8_t b = p[i];
       high |= b;
       low[i] = uint8_t(b + ((uint8_t(b - 'A') < 26) ? 32 : 0));
     }
+    std::memset(low + n, 0, 33);  // no literal holds a NUL byte
     if (!(high & 0x80)) {
       uint64_t lit_rules = 0;
-      for (size_t i = 0; i + 1 < n; i++) {
-        if (!((ap_first_[low[i] >> 6] >> (low[i] & 63)) & 1)) continue;  // L1-resident test first
+      auto check_at = [&](size_t i) {
         const uint16_t slot = ap_pair_[(uint32_t(low[i]) << 8) | low[i + 1]];
-        if (!slot) continue;
+        if (!slot) return;
         for (auto& lr : ap_lits_[slot - 1])
           if (!(lit_rules >> lr.second & 1) && lr.first.size() <= n - i &&
               std::memcmp(low + i, lr.first.data(), lr.first.size()) == 0)
             lit_rules |= uint64_t(1) << lr.second;
+      };
+      if (ap_c0_.size() <= 32) {
+        // 32 positions at a time: the pairs (low[i], low[i+1]) that begin some literal
+        typedef char v32 __attribute__((vector_size(32)));
+        const size_t np = ap_c0_.size();
+        for (size_t i = 0; i + 1 < n; i += 32) {
+          v32 a, b;
+          std::memcpy(&a, low + i, 32);
+          std::memcpy(&b, low + i + 1, 32);
+          v32 hit = {};
+          for (size_t k = 0; k < np; k++) hit |= (a == char(ap_c0_[k])) & (b == char(ap_c1_[k]));
+          uint32_t m = uint32_t(__builtin_ia32_pmovmskb256(hit));
+          const size_t lim = n - 1 - i;  // pair starts i .. n - 2
+          if (lim < 32) m &= (1u << lim) - 1;
+          while (m) {
+            check_at(i + size_t(__builtin_ctz(m)));
+            m &= m - 1;
+          }
+        }
+      } else {
+        for (size_t i = 0; i + 1 < n; i++)
+          if ((ap_first_[low[i] >> 6] >> (low[i] & 63)) & 1) check_at(i);  // L1-resident test first
       }
       uint64_t mask = ap_always_ | lit_rules;
       while (mask) {

@@ -189,6 +189,7 @@ class SecretScanner {
   uint64_t ap_always_ = 0;
   std::vector<uint16_t> ap_pair_;  // 65536: 1 + index into ap_lits_, 0 = no literal starts with the pair
   uint64_t ap_first_[4] = {};      // lowercase bytes that begin some literal (checked before ap_pair_)
+  std::vector<uint8_t> ap_c0_, ap_c1_;  // distinct first-two-byte pairs of the literals (SIMD prefilter)
   std::vector<std::vector<std::pair<std::string, uint32_t>>> ap_lits_;  // (literal, allow rule) per pair
 };
 
