@@ -13,7 +13,7 @@ cd "$(dirname "$0")/.."
 ROOT=$(pwd)
 MODE=${1:-all}
 python -c "import __graft_entry__ as g; g.build()" || exit 1
-COMMON="-O1 -g -fPIC -std=c++17 -fno-omit-frame-pointer -I trivy_amd/csrc -I include -I oracle/native -D__HIP_PLATFORM_AMD__ -I /opt/rocm/include"
+COMMON="-O1 -g -march=x86-64-v3 -fPIC -std=c++17 -fno-omit-frame-pointer -I trivy_amd/csrc -I include -I oracle/native -D__HIP_PLATFORM_AMD__ -I /opt/rocm/include"
 TESTS="tests/test_host_concurrency.py tests/test_host_tail.py tests/test_analyzer.py tests/test_allow_path.py tests/test_rules_data.py"
 build() {  # $1 = name, $2 = sanitizer flags
   local out=oracle/build/san_$1
@@ -24,7 +24,7 @@ build() {  # $1 = name, $2 = sanitizer flags
     g++ $COMMON $2 -c $src -o $o || return 1
     objs="$objs $o"
   done
-  g++ -shared $2 -o $out/libtsg_host.so $objs trivy_amd/_obj/engine.hip.o -L/opt/rocm/lib -lamdhip64 -lpthread \
+  g++ -shared $2 -o $out/libtsg_host.so $objs trivy_amd/_obj/engine.hip.o trivy_amd/_obj/xform.hip.o -L/opt/rocm/lib -lamdhip64 -lpthread \
     -Wl,-rpath,/opt/rocm/lib || return 1
   echo $out/libtsg_host.so
 }
