@@ -1045,39 +1045,89 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   for (uint32_t f = 0; f < in.n_files; f++)
     if (allowed[f]) out->kind[f] = uint8_t(kAllowedPath);
   double t2 = NowMs();
-  std::sort(cands.begin(), cands.end(), [](const Candidate& a, const Candidate& b) {
-    if (a.file != b.file) return a.file < b.file;
-    if (a.rule != b.rule) return a.rule < b.rule;
-    return a.wlo < b.wlo;
-  });
+  // Group candidates by file with a stable counting sort over the dense file
+  // ids (O(candidates + files)); each group is put in (rule, wlo) order by the
+  // worker that scans it, so no serial comparison sort runs here.
   std::vector<size_t> starts;
-  for (size_t i = 0; i < cands.size(); i++)
-    if (i == 0 || cands[i].file != cands[i - 1].file) starts.push_back(i);
-  starts.push_back(cands.size());
+  {
+    std::vector<uint32_t> cnt(size_t(in.n_files) + 1, 0);
+    for (const Candidate& c : cands) cnt[c.file + 1]++;
+    starts.reserve(cands.size() + 1);
+    for (uint32_t f = 0; f < in.n_files; f++) {
+      if (cnt[f + 1]) starts.push_back(cnt[f]);
+      cnt[f + 1] += cnt[f];
+    }
+    starts.push_back(cands.size());
+    std::vector<Candidate> sorted(cands.size());
+    for (const Candidate& c : cands) sorted[cnt[c.file]++] = c;
+    cands.swap(sorted);
+  }
   size_t nf = starts.size() - 1;
   std::vector<FileResult> tmp(nf);
   for (auto& g : g_prof) g = 0;
   const double t_sorted = NowMs();
-  // largest work first (candidates x file size) so one big file does not finish last
+  // heaviest groups (candidates x file size) first so one big file does not
+  // finish last; only the top few hundred need ordering, the rest follow in
+  // file order
   std::vector<uint32_t> order(nf);
   for (size_t k = 0; k < nf; k++) order[k] = uint32_t(k);
-  auto work_of = [&](size_t k) {
-    const uint32_t f = cands[starts[k]].file;
-    return double(starts[k + 1] - starts[k]) * double(in.host_offsets[f + 1] - in.host_offsets[f] + 4096);
+  {
+    std::vector<double> w(nf);
+    for (size_t k = 0; k < nf; k++) {
+      const uint32_t f = cands[starts[k]].file;
+      w[k] = double(starts[k + 1] - starts[k]) * double(in.host_offsets[f + 1] - in.host_offsets[f] + 4096);
+    }
+    const size_t top = std::min<size_t>(nf, 1024);  // the LPT head, dispatched one group at a time below
+    auto heavier = [&](uint32_t x, uint32_t y) { return w[x] > w[y] || (w[x] == w[y] && x < y); };
+    if (top < nf) std::nth_element(order.begin(), order.begin() + top, order.end(), heavier);
+    std::sort(order.begin(), order.begin() + top, heavier);
+    if (top < nf) std::sort(order.begin() + top, order.end());
+  }
+  // The tail is bound by cold reads of the arena (the match window, the lines
+  // around it, the path): past the heaviest groups, items go out in runs of
+  // kRun and each one prefetches the next item's windows while it scans.
+  constexpr size_t kRun = 4;
+  const size_t top = std::min<size_t>(nf, 1024);
+  const size_t n_items = top + (nf - top + kRun - 1) / kRun;
+  auto prefetch_group = [&](size_t k) {
+    const size_t a = starts[k], b = starts[k + 1];
+    const uint32_t f = cands[a].file;
+    if (allowed[f]) return;
+    __builtin_prefetch(in.paths[f]);
+    const uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
+    for (size_t q = a; q < b && q < a + 4; q++) {
+      const int64_t lo = std::max<int64_t>(0, cands[q].wlo - 256);
+      const int64_t hi = std::min<int64_t>(int64_t(fe - fs), std::min(cands[q].whi, cands[q].wlo + 2048) + 512);
+      for (int64_t x = lo & ~int64_t(63); x < hi; x += 64) __builtin_prefetch(in.host_arena + fs + uint64_t(x));
+    }
   };
-  std::vector<double> w(nf);
-  for (size_t k = 0; k < nf; k++) w[k] = work_of(k);
-  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return w[x] > w[y]; });
-  ParallelFor(nf, host_threads_, [&](size_t kk) {
-    const size_t k = order[kk];
+  auto scan_group = [&](size_t k) {
     size_t a = starts[k], b = starts[k + 1];
     uint32_t f = cands[a].file;
     if (allowed[f]) return;
+    if (b - a > 1) {
+      auto by_rule = [](const Candidate& x, const Candidate& y) {
+        return x.rule != y.rule ? x.rule < y.rule : x.wlo < y.wlo;
+      };
+      if (!std::is_sorted(&cands[a], &cands[b], by_rule)) std::sort(&cands[a], &cands[b], by_rule);
+    }
     const char* p = in.paths[f];
     size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
     uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
     ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string_view(p, pn), in.binary && in.binary[f], &cands[a],
              b - a, &tmp[k], gpu_windows);
+  };
+  ParallelFor(n_items, host_threads_, [&](size_t it) {
+    if (it < top) {
+      scan_group(order[it]);
+      return;
+    }
+    const size_t kk0 = top + (it - top) * kRun, kk1 = std::min(nf, kk0 + kRun);
+    prefetch_group(order[kk0]);
+    for (size_t kk = kk0; kk < kk1; kk++) {
+      if (kk + 1 < kk1) prefetch_group(order[kk + 1]);
+      scan_group(order[kk]);
+    }
   });
   const double t_par = NowMs();
   if (g_tail_debug)
@@ -1090,6 +1140,8 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   if (g_tail_debug)
     std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB\n", (long long)g_wholefile_calls.load(),
                  g_wholefile_bytes.load() / 1e6);
+  out->found_files.reserve(nf);
+  out->found.reserve(nf);
   for (size_t k = 0; k < nf; k++) {
     if (tmp[k].kind != kHasFindings) continue;
     uint32_t f = cands[starts[k]].file;
