@@ -230,6 +230,29 @@ WORKLOADS = {
 }
 
 
+def _bind_numa(device):
+    """Bind the process to the CPUs of the GPU's NUMA node before the corpus
+    and the host pool exist: the host pass reads the arena with cold misses,
+    and a remote node adds its latency to each (None where sysfs says nothing)."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(device)
+        dev = "/sys/bus/pci/devices/%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        with open(dev + "/numa_node") as f:
+            node = int(f.read())
+        if node < 0:
+            return None
+        with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
+            cpus = set()
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        os.sched_setaffinity(0, cpus & os.sched_getaffinity(0) or cpus)
+        return node
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +264,9 @@ def main():
     ap.add_argument("--parity-mb", type=float, default=None, help="oracle parity sample (first files)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=3, help="scans in flight (pipelined submission)")
+    ap.add_argument("--numa", choices=["gpu", "off"], default="gpu",
+                    help="gpu: bind this rank's threads (and so its first-touch host memory) to the GPU's NUMA "
+                         "node, as numactl --cpunodebind would")
     ap.add_argument("--ingest", action="store_true",
                     help="c2/c3: host-resident corpus (page-locked), H2D inside the timed region")
     ap.add_argument("--ingest-steps", type=int, default=3,
@@ -275,6 +301,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
+    numa_node = _bind_numa(local) if args.numa == "gpu" else None
 
     from trivy_amd import corpus
     import trivy_amd.secret as secret
@@ -519,7 +546,8 @@ def main():
                     % (" and generated-rule samples" if args.workload in ("c3", "c3u") else ""),
             "config": dict({"workload": wl_desc % args.gb, "workload_id": args.workload,
                             "parallelism": "files sharded, dp%d" % world,
-                            "rules_compile_s": round(t_compile, 2)}, **config_extra),
+                            "rules_compile_s": round(t_compile, 2),
+                            "host_numa_node": numa_node}, **config_extra),
             "roofline": roofline,
             "ingest": ingest,
             "cpu_baseline": cpu,

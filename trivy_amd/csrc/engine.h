@@ -154,6 +154,9 @@ class GpuEngine {
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
   uint32_t fs_chunk_ = 65536;         // TSG_FULLSCAN_CHUNK: full-scan bytes per lane (min)
   hipEvent_t ev_fs_ = nullptr;
+  hipEvent_t ev_sync_ = nullptr;  // blocking-sync: the host waits asleep, not spinning
+  bool blocking_sync_ = true;
+  hipError_t WaitStream();
   uint32_t* d_item_diag_ = nullptr;   // TSG_DIAG_ITEMS=<file>: per-item counters dumped after each run
   std::string item_diag_path_;
 };

@@ -1538,6 +1538,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   if (const char* fc = std::getenv("TSG_FULLSCAN_CHUNK")) fs_chunk_ = uint32_t(std::atoi(fc));
   if (fs_chunk_ < 64) fs_chunk_ = 64;
   hipEventCreate(&ev_fs_);
+  // the kernels of one scan run ~10 ms: a thread spinning on the stream for
+  // that long takes a core from the host pool scanning the previous batch
+  hipEventCreateWithFlags(&ev_sync_, hipEventBlockingSync | hipEventDisableTiming);
+  if (const char* bs = std::getenv("TSG_BLOCKING_SYNC")) blocking_sync_ = std::atoi(bs) != 0;
   kw_words_ = std::max<uint32_t>(1, cr.kw_words());
   n_rules_ = uint32_t(cr.rules.size());
   for (uint32_t r = 0; r < n_rules_; r++)
@@ -1810,6 +1814,7 @@ GpuEngine::~GpuEngine() {
   for (auto& e : ev_copied_)
     if (e) hipEventDestroy(e);
   if (ev_fs_) hipEventDestroy(ev_fs_);
+  if (ev_sync_) hipEventDestroy(ev_sync_);
   for (auto& e : ev_h2d_)
     if (e) hipEventDestroy(e);
   for (auto& e : ev_x_)
@@ -2052,6 +2057,12 @@ bool GpuEngine::GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint
   return true;
 }
 
+hipError_t GpuEngine::WaitStream() {
+  if (!blocking_sync_ || !ev_sync_) return hipStreamSynchronize(stream_);
+  hipError_t e = hipEventRecord(ev_sync_, stream_);
+  return e != hipSuccess ? e : hipEventSynchronize(ev_sync_);
+}
+
 bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
                     std::vector<Candidate>* cands, BatchStats* st) {
   HIP_OK(hipSetDevice(device_));
@@ -2252,7 +2263,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     HIP_OK(hipEventRecord(ev_[6], stream_));
     uint32_t cnt[16];
     HIP_OK(hipMemcpyAsync(cnt, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(WaitStream());
     if (std::getenv("TSG_STATS_DEBUG"))
       std::fprintf(stderr, "counters: hits %u cands %u special %u recs %u folds %u\n", cnt[0], cnt[1], cnt[2], cnt[7],
                    cnt[9]);
@@ -2282,7 +2293,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     if (cnt[1]) {
       HIP_OK(hipMemcpyAsync(cands->data(), d_cands_, size_t(cnt[1]) * sizeof(Candidate), hipMemcpyDeviceToHost,
                             stream_));
-      HIP_OK(hipStreamSynchronize(stream_));
+      HIP_OK(WaitStream());
     }
     // closed keyword gates (finalize_kernel) never reach the host
     cands->erase(std::remove_if(cands->begin(), cands->end(), [](const Candidate& c) { return c.flags & kCandDrop; }),
