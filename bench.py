@@ -230,6 +230,19 @@ WORKLOADS = {
 }
 
 
+def _cgroup_cpu():
+    """cgroup v2 cpu.stat counters and cpu.max quota of this container, or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            st = {k: int(v) for k, v in (ln.split() for ln in f if len(ln.split()) == 2)}
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        st["quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+        return st
+    except (OSError, ValueError):
+        return None
+
+
 def _bind_numa(device):
     """Bind the process to the CPUs of the GPU's NUMA node before the corpus
     and the host pool exist: the host pass reads the arena with cold misses,
@@ -393,12 +406,19 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
+    cg0 = _cgroup_cpu()
     t0 = time.time()
     stats = []
     run_steps(args.steps, stats)
     torch.cuda.synchronize()
     barrier()
     dt = time.time() - t0
+    cg1 = _cgroup_cpu()
+    host_cpu = None
+    if cg0 and cg1:  # the container's CPU use over the timed steps (quota throttling shows here)
+        host_cpu = {"cpus_used": round((cg1["usage_usec"] - cg0["usage_usec"]) / (dt * 1e6), 2),
+                    "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3, 1),
+                    "quota_cpus": cg1.get("quota_cpus")}
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -553,6 +573,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "breakdown_ms": breakdown,
+            "host_cpu": host_cpu,
             "counts": counts,
             "gen_s": round(t_gen, 2),
         }

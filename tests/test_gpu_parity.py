@@ -304,3 +304,25 @@ def test_exclude_blocks_on_gpu_windows(secret, tmp_path):
         files.append(("x%d.txt" % i, b"\n".join(parts)))
     n = _compare_corpus(secret, files, str(cfg))
     assert n > 10
+
+
+def test_context_lines_over_long_lines(secret):
+    """Code context around matches behind long lines: the host's walk back over
+    the two previous lines reads the GPU's last-three-newline hints
+    (Candidate::nl_back), including lines longer than the 1-KiB search step,
+    matches on the first lines, adjacent censored secrets and multi-line
+    matches that hide newlines."""
+    rng = random.Random(1729)
+    key = b"AKIA" + b"Q" * 16
+    gh = b"ghp_" + b"a1B2" * 9
+    pk = (b"-----BEGIN RSA PRIVATE KEY-----\n" + b"MIIEow" * 12 + b"\n" + b"abcd" * 16 + b"\n"
+          b"-----END RSA PRIVATE KEY-----")
+    files = []
+    for n, lens in enumerate([[0], [5], [3000], [70000, 3], [1500, 1500, 1500], [1, 2000, 1],
+                              [40000, 0, 0], [5000, 900, 20, 3000]]):
+        body = b"".join(bytes(rng.choice(b"xyz .,=") for _ in range(ln)) + b"\n" for ln in lens)
+        files.append(("long%d.txt" % n, body + b"k = " + key + b"\n" + body + b"t=" + gh + b"\n"))
+        files.append(("first%d.txt" % n, b"k = " + key + b" " + body))
+        files.append(("pk%d.pem" % n, body + pk + b"\n" + b"x" * 2000 + b"\n" + key + b"\n"))
+        files.append(("adj%d.txt" % n, body + key + b"\n" + gh + b"\n" + key + b"\n" + b"y" * 1100 + b"\n" + gh))
+    assert _compare_corpus(secret, files) > 40

@@ -162,3 +162,70 @@ def test_host_tail_c3u_unanchored_rules(tmp_path):
         assert g.to_dict() == want, path
         n += len(want["Findings"] or [])
     assert n > 5
+
+
+CAND = np.dtype([("file", "<u4"), ("rule", "<u4"), ("wlo", "<i8"), ("whi", "<i8"), ("nl_before", "<i8"),
+                 ("flags", "<u4"), ("nl_back", "<u4", (3,))])
+assert CAND.itemsize == 48
+
+
+def _windowed_candidates(files, n_rules, step, hints):
+    """Every rule over every file in windows of `step` bytes, each carrying its
+    '\\n' count and (hints) the last three '\\n' before it, as the GPU's
+    finalize kernel writes them (Candidate::nl_back)."""
+    recs = []
+    for f, (_, b) in enumerate(files):
+        nl = np.flatnonzero(np.frombuffer(b, dtype=np.uint8) == 10)
+        for lo in range(0, max(1, len(b)), step):
+            before = nl[nl < lo]
+            back = [0xFFFFFFFF] * 3
+            if hints:
+                last = before[-3:][::-1]
+                back = [lo - int(x) for x in last] + [0xFFFFFFFE] * (3 - len(last))
+            for r in range(n_rules):
+                recs.append((f, r, lo, min(len(b), lo + step - 1), len(before), 0, back))
+    return np.array(recs, dtype=CAND)
+
+
+@pytest.mark.parametrize("hints", [False, True])
+def test_host_tail_newline_hints(hints):
+    """Code-context lines from the newline hints match the oracle: long lines
+    before a match (farther than one 1-KiB GPU step), matches on the first
+    lines, adjacent censored secrets and a multi-line key hiding newlines."""
+    import random
+    rng = random.Random(99)
+    key, gh = b"AKIA" + b"Q" * 16, b"ghp_" + b"a1B2" * 9
+    pk = (b"-----BEGIN RSA PRIVATE KEY-----\n" + b"MIIEow" * 12 + b"\n" + b"abcd" * 16 + b"\n"
+          b"-----END RSA PRIVATE KEY-----")
+    files = []
+    for n, lens in enumerate([[0], [5], [3000], [9000, 3], [1500, 1500, 1500], [1, 2000, 1], [600, 0, 0]]):
+        body = b"".join(bytes(rng.choice(b"xyz .,=") for _ in range(ln)) + b"\n" for ln in lens)
+        files.append(("long%d.txt" % n, body + b"k = " + key + b"\n" + body + b"t=" + gh + b"\n"))
+        files.append(("first%d.txt" % n, b"k = " + key + b" " + body))
+        files.append(("pk%d.pem" % n, body + pk + b"\n" + b"x" * 2000 + b"\n" + key + b"\n"))
+        files.append(("adj%d.txt" % n, body + key + b"\n" + gh + b"\n" + key + b"\n" + b"y" * 1100 + b"\n" + gh))
+    L = hostlib.lib()
+    _declare(L)
+    rules, allow, exclude = _assemble(None)
+    cg = CGlobal(rules, allow, exclude)
+    contents = [b for _, b in files]
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 16, dtype=np.uint8)
+    pb = [_b(p) for p, _ in files]
+    parr = (c.c_char_p * len(pb))(*pb)
+    plen = np.array([len(p) for p in pb], dtype=np.uint64)
+    batch = _CBatch(len(files), arena.ctypes.data, offs.ctypes.data, None, None,
+                    c.cast(parr, c.c_void_p).value, plen.ctypes.data, None)
+    cands = _windowed_candidates(files, len(rules), 700, hints)
+    h = c.c_void_p()
+    if L.tsg_debug_host_tail_cands(c.byref(cg.g), c.byref(batch), cands.ctypes.data, len(cands), c.byref(h)) != 0:
+        raise RuntimeError(hostlib.last_error())
+    got = ScanResult(_Owner(L), h).secrets([p for p, _ in files])
+    o = osc.new_scanner(None)
+    n = 0
+    for (p, b), g in zip(files, got):
+        want = o.scan(p, b)
+        assert g.to_dict() == want, p
+        n += len(want["Findings"] or [])
+    assert n > 40

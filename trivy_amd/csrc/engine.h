@@ -23,8 +23,14 @@ struct Candidate {      // produced by the verify / full-scan kernels
   int64_t wlo, whi;     // allowed match-start window, file-relative, inclusive
   int64_t nl_before;    // '\n' count in [file start, wlo)
   uint32_t flags;       // kCand*
-  uint32_t pad;
+  // wlo minus the positions of the last three '\n' before wlo, nearest first
+  // (finalize kernel): the host's code-context walk reads these instead of
+  // scanning back over long lines.  kNlNone: fewer newlines precede wlo;
+  // kNlUnknown: not computed (host candidates, or farther than kNlReach).
+  uint32_t nl_back[3];
 };
+constexpr uint32_t kNlNone = 0xFFFFFFFEu, kNlUnknown = 0xFFFFFFFFu;
+constexpr uint64_t kNlReach = uint64_t(1) << 20;
 
 // The transformed bytes of chosen files of a host batch whose transform ran
 // on the GPU (RunHost with kinds): buf holds them in file order, off is a

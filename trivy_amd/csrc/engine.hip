@@ -643,7 +643,7 @@ __device__ __forceinline__ void put_candidate(Candidate* cands, uint32_t cap, ui
     c.whi = whi;
     c.nl_before = -1;
     c.flags = 0;
-    c.pad = 0;
+    c.nl_back[0] = c.nl_back[1] = c.nl_back[2] = kNlUnknown;
     cands[k] = c;
   } else {
     counters[4] = 1;
@@ -1489,6 +1489,47 @@ __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
 #pragma unroll
       for (int x = 1; x < 64; x <<= 1) part += __shfl_xor(part, x);
       if (lane == 0) c.nl_before = part;
+    }
+    // the last three '\n' before wlo: 1 KiB per step, lane 0 on the highest
+    // 16-B block; a lane's newlines take ranks after those of the lanes above
+    {
+      const uint64_t wabs = fs + uint64_t(c.wlo);
+      uint64_t hi = wabs;  // [fs, hi) still unsearched
+      uint32_t found = 0;
+      while (found < 3 && hi > fs && wabs - hi < kNlReach) {
+        const uint64_t blk = (((hi - 1) >> 4) - lane) << 4;  // may wrap below fs: masked out
+        uint32_t mask = 0;
+        if (blk + 16 > fs && blk < hi && int64_t(blk) >= 0) {
+          const uint4 v = load16(P.arena + blk);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++)
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++)
+              if (((w[q] >> (8 * b)) & 0xFFu) == uint32_t('\n')) mask |= 1u << (4 * q + b);
+          const uint32_t lo_cut = fs > blk ? uint32_t(fs - blk) : 0u;
+          const uint32_t hi_cut = hi < blk + 16 ? uint32_t(hi - blk) : 16u;
+          mask &= (hi_cut >= 16 ? 0xFFFFu : ((1u << hi_cut) - 1u)) & ~((1u << lo_cut) - 1u);
+        }
+        const uint32_t cnt = uint32_t(__popc(mask));
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int x = 1; x < 64; x <<= 1) {
+          const uint32_t t = __shfl_up(incl, x);
+          if (lane >= uint32_t(x)) incl += t;
+        }
+        uint32_t rank = found + incl - cnt;
+        for (uint32_t m = mask; m && rank < 3; rank++) {
+          const uint32_t bit = 31u - uint32_t(__clz(m));
+          m &= ~(1u << bit);
+          c.nl_back[rank] = uint32_t(wabs - (blk + bit));
+        }
+        found += __shfl(incl, 63);
+        const uint64_t low = ((hi - 1) >> 4) >= 63 ? ((((hi - 1) >> 4) - 63) << 4) : 0;
+        hi = low;
+      }
+      if (hi <= fs)  // reached the file start: the remaining ranks do not exist
+        for (uint32_t r = found + lane; r < 3; r += 64) c.nl_back[r] = kNlNone;
     }
     if (lane == 0) {
       const RuleGpu rg = P.rules[c.rule];

@@ -574,6 +574,7 @@ struct ScanScratch {
   std::vector<std::pair<uint32_t, Loc>> matched;
   std::vector<Loc> censor, locs, spans, merged;
   std::vector<std::pair<int64_t, int64_t>> nla;
+  std::vector<const Candidate*> hints;
   std::vector<Window> wins;
   std::vector<int64_t> m, span_nl;
 };
@@ -599,6 +600,13 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   nla.clear();
   for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
   std::sort(nla.begin(), nla.end());
+  // the GPU's last-three-newlines before each window (Candidate::nl_back)
+  std::vector<const Candidate*>& hints = S.hints;
+  hints.clear();
+  static const bool use_hints = !std::getenv("TSG_NL_HINTS") || std::atoi(std::getenv("TSG_NL_HINTS")) != 0;
+  for (size_t i = 0; i < nc && use_hints; i++)
+    if (c[i].nl_back[0] != kNlUnknown && c[i].nl_back[0] != 0) hints.push_back(&c[i]);  // 0: never a GPU value
+  std::sort(hints.begin(), hints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
 
   // the candidates are sorted by rule: real rules first, then the exclude-block rules
   const uint32_t n_real = uint32_t(rules_.size());
@@ -859,12 +867,35 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
     --it;
     return p < it->e ? &*it : nullptr;
   };
+  auto last_nl = [&](int64_t pos) -> int64_t {  // the last '\n' in [0, pos), or -1
+    if (pos <= 0) return -1;
+    auto it = std::upper_bound(hints.begin(), hints.end(), pos,
+                               [](int64_t v, const Candidate* h) { return v < h->wlo; });
+    if (it != hints.begin()) {  // a window starting at or below pos: search [wlo, pos), then its list
+      const Candidate& h = **(it - 1);
+      if (pos > h.wlo) {
+        const void* q = memrchr(content + h.wlo, '\n', size_t(pos - h.wlo));
+        if (q) return int64_t(static_cast<const uint8_t*>(q) - content);
+      }
+      return h.nl_back[0] == kNlNone ? -1 : h.wlo - int64_t(h.nl_back[0]);
+    }
+    if (it != hints.end()) {  // the next window above pos: its list may reach below pos
+      const Candidate& h = **it;
+      for (int k = 0; k < 3; k++) {
+        if (h.nl_back[k] == kNlUnknown) break;
+        if (h.nl_back[k] == kNlNone) return -1;  // every '\n' before wlo is listed, all >= pos
+        const int64_t at = h.wlo - int64_t(h.nl_back[k]);
+        if (at < pos) return at;
+      }
+    }
+    const void* q = memrchr(content, '\n', size_t(pos));
+    return q ? int64_t(static_cast<const uint8_t*>(q) - content) : -1;
+  };
   auto line_start_of = [&](int64_t pos) {  // after the last visible '\n' before pos
     int64_t p = pos;  // search [0, p)
     while (p > 0) {
-      const void* q = memrchr(content, '\n', size_t(p));
-      if (!q) return int64_t(0);
-      int64_t at = int64_t(static_cast<const uint8_t*>(q) - content);
+      const int64_t at = last_nl(p);
+      if (at < 0) return int64_t(0);
       const Loc* z = in_span(at);
       if (!z) return at + 1;
       p = z->s;
