@@ -1583,6 +1583,8 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   // that long takes a core from the host pool scanning the previous batch
   hipEventCreateWithFlags(&ev_sync_, hipEventBlockingSync | hipEventDisableTiming);
   if (const char* bs = std::getenv("TSG_BLOCKING_SYNC")) blocking_sync_ = std::atoi(bs) != 0;
+  if (const char* vb = std::getenv("TSG_VERIFY_BLOCKS")) verify_blocks_ = uint32_t(std::max(1, std::atoi(vb)));
+  if (const char* fb = std::getenv("TSG_FINALIZE_BLOCKS")) finalize_blocks_ = uint32_t(std::max(1, std::atoi(fb)));
   kw_words_ = std::max<uint32_t>(1, cr.kw_words());
   n_rules_ = uint32_t(cr.rules.size());
   for (uint32_t r = 0; r < n_rules_; r++)
@@ -2291,7 +2293,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     np.fs_chunk = fs_chunk_;
     np.kw_fold = kw_fold_ ? 1u : 0u;  // no keyword takes 'i' / 'k': the bits are exact without the kernel
 
-    if (diag_mode_ == 0) verify_hits_kernel<<<2048, 256, 0, stream_>>>(np);
+    if (diag_mode_ == 0) verify_hits_kernel<<<verify_blocks_, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     if (np.n_fullscan_rules > 0) {
       HIP_OK(hipEventRecord(ev_fs_, stream_));
@@ -2299,7 +2301,7 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(ev_[5], stream_));
-    if (diag_mode_ == 0) finalize_kernel<<<1024, 256, 0, stream_>>>(np);
+    if (diag_mode_ == 0) finalize_kernel<<<finalize_blocks_, 256, 0, stream_>>>(np);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev_[6], stream_));
     uint32_t cnt[16];
