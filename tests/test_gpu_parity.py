@@ -326,3 +326,33 @@ def test_context_lines_over_long_lines(secret):
         files.append(("pk%d.pem" % n, body + pk + b"\n" + b"x" * 2000 + b"\n" + key + b"\n"))
         files.append(("adj%d.txt" % n, body + key + b"\n" + gh + b"\n" + key + b"\n" + b"y" * 1100 + b"\n" + gh))
     assert _compare_corpus(secret, files) > 40
+
+
+def test_device_batches_pipelined_tickets_and_overflow(secret):
+    """Device-resident scans go through Enqueue/Collect tickets (the lock is
+    released before the read-back): a fresh scanner's first scan overflows the
+    initial candidate buffer (> 65,536 candidates) and is rescanned by Run;
+    then more scans in flight than ticket slots (4) give identical results,
+    and every file's finding is there."""
+    import numpy as np
+    import torch
+    n = 70000
+    contents = [b"k=AKIA%016d\n" % i for i in range(n)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+    paths = ["f%05d.txt" % i for i in range(n)]
+    d_arena = torch.from_numpy(arena.copy()).to("cuda:0")
+    d_offs = torch.from_numpy(offs.view(np.int64)).to("cuda:0")
+    s = secret.NewScanner(None)
+    first = s.scan_arena(arena, offs, paths, dev_arena=d_arena.data_ptr(), dev_offsets=d_offs.data_ptr())
+    want = first.raw()
+    assert first.stats()["findings"] == n
+    pend = [s.scan_arena_async(arena, offs, paths, dev_arena=d_arena.data_ptr(), dev_offsets=d_offs.data_ptr())
+            for _ in range(6)]
+    for p in pend:
+        assert p.wait().raw() == want
+    o = osc.new_scanner(None)
+    got = first.secrets(paths)
+    for i in (0, 1, n // 2, n - 1):
+        assert got[i].to_dict() == o.scan(paths[i], contents[i])

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "rules.h"
@@ -77,12 +78,44 @@ class GpuEngine {
                std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds = nullptr,
                TailOut* tail = nullptr);
 
+  // Split form of Run for pipelined callers: Enqueue (with the engine's lock
+  // held) puts the whole GPU phase and the copies of the counters and of the
+  // full candidate buffer into pinned host memory on the stream and returns;
+  // Collect (no lock) waits for that ticket.  The next scan's kernels queue
+  // right behind the copies, so the GPU does not idle while a caller wakes
+  // up, reads back and releases the lock.  Enqueue returns false when no
+  // ticket is free or a diagnostic mode is on (then call Run); Collect sets
+  // *rerun when a buffer overflowed (then call Run under the lock: it grows
+  // the buffers and rescans).
+  struct Ticket {
+    int slot = -1;
+    uint32_t cand_cap = 0;
+  };
+  bool Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files, Ticket* t);
+  bool Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st, bool* rerun);
+
   // Device buffers of the last run (for tests / bench).
   hipEvent_t ev_scan0() const { return ev_[1]; }
   hipEvent_t ev_scan1() const { return ev_[2]; }
 
  private:
   bool Ensure(void** p, size_t* cap, size_t need);
+  bool EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
+                    uint64_t n_chunks, hipEvent_t* ev, hipEvent_t ev_fs);
+  void InitCaps(uint64_t n_bytes);
+  struct Slot {  // one in-flight Enqueue: its phase events and pinned read-back buffers
+    hipEvent_t ev[7] = {};
+    hipEvent_t ev_fs = nullptr, done = nullptr;
+    uint32_t* h_cnt = nullptr;
+    Candidate* h_cands = nullptr;
+    size_t h_cap = 0;
+    bool busy = false, has_fs = false;
+    uint64_t n_bytes = 0;
+    uint32_t n_files = 0;
+  };
+  static constexpr int kSlots = 4;
+  Slot slots_[kSlots];
+  std::mutex slot_mu_;
   bool Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
                  std::vector<uint64_t>* xoff, float* ms);
   bool GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf, const std::vector<uint64_t>& xoff,

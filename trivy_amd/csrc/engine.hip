@@ -1858,6 +1858,14 @@ GpuEngine::~GpuEngine() {
     if (e) hipEventDestroy(e);
   if (ev_fs_) hipEventDestroy(ev_fs_);
   if (ev_sync_) hipEventDestroy(ev_sync_);
+  for (auto& S : slots_) {
+    for (auto& e : S.ev)
+      if (e) hipEventDestroy(e);
+    if (S.ev_fs) hipEventDestroy(S.ev_fs);
+    if (S.done) hipEventDestroy(S.done);
+    if (S.h_cnt) hipHostFree(S.h_cnt);
+    if (S.h_cands) hipHostFree(S.h_cands);
+  }
   for (auto& e : ev_h2d_)
     if (e) hipEventDestroy(e);
   for (auto& e : ev_x_)
@@ -1870,7 +1878,10 @@ GpuEngine::~GpuEngine() {
 
 bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
   if (*p && *cap >= need) return true;
-  if (*p) hipFree(*p);
+  if (*p) {  // queued work (an Enqueue'd scan) may still read the old buffer
+    HIP_OK(hipStreamSynchronize(stream_));
+    hipFree(*p);
+  }
   *p = nullptr;
   size_t n = std::max<size_t>(need, 64);
   HIP_OK(hipMalloc(p, n));
@@ -2106,6 +2117,310 @@ hipError_t GpuEngine::WaitStream() {
   return e != hipSuccess ? e : hipEventSynchronize(ev_sync_);
 }
 
+void GpuEngine::InitCaps(uint64_t n_bytes) {
+  if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 512, 1 << 16), 1u << 28));
+  if (cand_cap_ == 0) cand_cap_ = 1 << 16;
+  if (rec_cap_ == 0) rec_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 128, 1 << 16), 1u << 30));
+  if (fold_cap_ == 0) fold_cap_ = 1 << 16;
+}
+
+bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
+                        Ticket* t) {
+  t->slot = -1;
+  if (n_files == 0 || n_bytes >= (uint64_t(1) << 36) - 64 || d_item_diag_ || diag_mode_ != 0) return false;
+  int k = -1;
+  {
+    std::lock_guard<std::mutex> g(slot_mu_);
+    for (int i = 0; i < kSlots && k < 0; i++)
+      if (!slots_[i].busy) {
+        slots_[i].busy = true;
+        k = i;
+      }
+  }
+  if (k < 0) return false;
+  Slot& S = slots_[k];
+  auto fail = [&] {
+    std::lock_guard<std::mutex> g(slot_mu_);
+    S.busy = false;
+    return false;
+  };
+  if (hipSetDevice(device_) != hipSuccess) return fail();
+  InitCaps(n_bytes);
+  if (!S.done) {
+    bool ok = hipEventCreateWithFlags(&S.done, hipEventBlockingSync | hipEventDisableTiming) == hipSuccess &&
+              hipEventCreate(&S.ev_fs) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&S.h_cnt), 64, hipHostMallocDefault) == hipSuccess;
+    for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    if (!ok) {
+      err_ = "ticket events / pinned counters";
+      return fail();
+    }
+  }
+  if (S.h_cap < cand_cap_) {
+    if (S.h_cands) hipHostFree(S.h_cands);
+    S.h_cands = nullptr;
+    S.h_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&S.h_cands), size_t(cand_cap_) * sizeof(Candidate),
+                      hipHostMallocDefault) != hipSuccess) {
+      err_ = "hipHostMalloc failed for the candidate read-back";
+      return fail();
+    }
+    S.h_cap = cand_cap_;
+  }
+  uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
+  if (n_chunks == 0) n_chunks = 1;
+  if (!EnqueuePhase(d_arena, n_bytes, d_offsets, n_files, n_chunks, S.ev, S.ev_fs) ||
+      hipMemcpyAsync(S.h_cnt, d_counters_, 64, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
+      hipMemcpyAsync(S.h_cands, d_cands_, size_t(cand_cap_) * sizeof(Candidate), hipMemcpyDeviceToHost, stream_) !=
+          hipSuccess ||
+      hipEventRecord(S.done, stream_) != hipSuccess) {
+    if (err_.empty()) err_ = "Enqueue: HIP call failed";
+    return fail();
+  }
+  S.n_bytes = n_bytes;
+  S.n_files = n_files;
+  S.has_fs = n_fullscan_rules_ > 0;
+  t->slot = k;
+  t->cand_cap = cand_cap_;
+  return true;
+}
+
+bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st, bool* rerun) {
+  *rerun = false;
+  if (t->slot < 0 || t->slot >= kSlots) {
+    err_ = "Collect: no ticket";
+    return false;
+  }
+  Slot& S = slots_[t->slot];
+  auto release = [&] {
+    std::lock_guard<std::mutex> g(slot_mu_);
+    S.busy = false;
+    t->slot = -1;
+  };
+  const hipError_t e = hipEventSynchronize(S.done);
+  if (e != hipSuccess) {
+    err_ = std::string("Collect: ") + hipGetErrorString(e);
+    release();
+    return false;
+  }
+  BatchStats local;
+  if (!st) st = &local;
+  *st = BatchStats();
+  st->bytes = S.n_bytes;
+  st->files = S.n_files;
+  const uint32_t* cnt = S.h_cnt;
+  if (cnt[8] || cnt[10] || cnt[3] || cnt[4] || cnt[1] > t->cand_cap) {  // an overflow: Run grows and rescans
+    *rerun = true;
+    release();
+    return true;
+  }
+  st->hits = cnt[11];
+  st->follow_hits = cnt[0];
+  st->special_files = cnt[2];
+  st->flagged_blocks = cnt[7];
+  st->fullscan_tasks = cnt[13];
+  st->fold_sites = cnt[9];
+  cands->clear();
+  cands->reserve(cnt[1]);
+  for (uint32_t i = 0; i < cnt[1]; i++)  // closed keyword gates (finalize_kernel) never reach the host
+    if (!(S.h_cands[i].flags & kCandDrop)) cands->push_back(S.h_cands[i]);
+  st->candidates = cands->size();
+  hipEventElapsedTime(&st->ms_scan, S.ev[1], S.ev[2]);
+  hipEventElapsedTime(&st->ms_confirm, S.ev[2], S.ev[3]);
+  hipEventElapsedTime(&st->ms_careful, S.ev[3], S.ev[4]);
+  hipEventElapsedTime(&st->ms_verify, S.ev[4], S.ev[5]);
+  hipEventElapsedTime(&st->ms_finalize, S.ev[5], S.ev[6]);
+  if (S.has_fs) hipEventElapsedTime(&st->ms_fullscan, S.ev_fs, S.ev[5]);
+  hipEventElapsedTime(&st->ms_chunkmap, S.ev[0], S.ev[1]);
+  hipEventElapsedTime(&st->ms_total, S.ev[0], S.ev[6]);
+  release();
+  return true;
+}
+
+// The GPU phase of one scan, enqueued on stream_: clears, K0 .. finalize,
+// with the phase events recorded into ev[0..6] (ev_fs before the full scan).
+bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
+                             uint64_t n_chunks, hipEvent_t* ev, hipEvent_t ev_fs) {
+  if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, (n_chunks + 8) * 2) ||
+      !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
+      !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
+      !Ensure(&d_folds_, &cap_folds_, size_t(fold_cap_) * sizeof(FoldSite)) ||
+      !Ensure(&d_recs_, &cap_recs_, size_t(rec_cap_) * 4) ||
+      !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
+      !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
+    return false;
+  HIP_OK(hipEventRecord(ev[0], stream_));  // the GPU phase: clears, K0 .. finalize
+  HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
+  HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
+  HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
+  HIP_OK(hipMemsetAsync(d_chunk_file_, 0, n_chunks * 4, stream_));
+  if (d_item_diag_) HIP_OK(hipMemsetAsync(d_item_diag_, 0, 8 * std::max<size_t>(n_fitems_, 1), stream_));
+  {
+    uint32_t blocks = std::min<uint32_t>((n_files + 255) / 256, 4096);
+    chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, static_cast<uint32_t*>(d_chunk_file_));
+  }
+  // K1: streaming filter -> flagged block records
+  FilterParams fp;
+  fp.arena = d_arena;
+  fp.n_bytes = n_bytes;
+  fp.reach = d_reach_;
+  fp.diag_mode = diag_mode_;
+  fp.nl = static_cast<uint16_t*>(d_nl_);
+  fp.recs = static_cast<uint32_t*>(d_recs_);
+  fp.rec_cap = rec_cap_;
+  fp.counters = d_counters_;
+  const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
+  const uint32_t f_grid =
+      uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves, 256)));
+  HIP_OK(hipEventRecord(ev[1], stream_));
+  filter_kernel<<<f_grid, kScanThreads, 0, stream_>>>(fp);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev[2], stream_));
+  // K2: confirm + verify
+  ConfirmParams cp;
+  cp.arena = d_arena;
+  cp.n_bytes = n_bytes;
+  cp.off = d_offsets;
+  cp.chunk_file = static_cast<const uint32_t*>(d_chunk_file_);
+  cp.nl = static_cast<const uint16_t*>(d_nl_);
+  cp.reach = d_reach_;
+  cp.tabs = d_ftabs_;
+  cp.tabs_bytes = ftabs_bytes_;
+  cp.t_bucket_off = ft_bucket_off_;
+  cp.t_bucket_items = ft_bucket_items_;
+  cp.t_items = ft_items_;
+  cp.t_item_ids = ft_item_ids_;
+  cp.t_item_cls = ft_item_cls_;
+  cp.t_classes = ft_classes_;
+  cp.anchors = d_anchors_;
+  cp.rules = d_rules_;
+  cp.nfa = d_nfa_;
+  cp.recs = static_cast<const uint32_t*>(d_recs_);
+  cp.rec_cap = rec_cap_;
+  cp.flags = static_cast<uint32_t*>(d_flags_);
+  cp.counters = d_counters_;
+  cp.hits = static_cast<uint32_t*>(d_hits_);
+  cp.hit_cap = hit_cap_;
+  cp.folds = static_cast<FoldSite*>(d_folds_);
+  cp.fold_cap = fold_cap_;
+  cp.diag = diag_confirm_;
+  cp.kwbits = static_cast<uint32_t*>(d_kw_);
+  cp.kw_words = kw_words_;
+  cp.core = d_core_;
+  cp.group_items = d_group_items_;
+  cp.bucket_groups = d_bucket_groups_;
+  cp.item_diag = d_item_diag_;
+  cp.t_luts = ft_luts_;
+  cp.t_cmap = ft_cmap_;
+  cp.t_ccore = ft_ccore_;
+  cp.t_gitems = ft_gitems_;
+  cp.t_bgroups = ft_bgroups_;
+  cp.n_cls = n_core_cls_;
+  cp.t_hkeys = ft_hkeys_;
+  cp.t_hitems = ft_hitems_;
+  cp.hash_bits = hash_bits_;
+  cp.hash_buckets = hash_buckets_;
+  if (diag_mode_ == 0) {
+    if (lds_tabs_)
+      confirm_kernel<true><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
+    else
+      confirm_kernel<false><<<2048 * 256 / kCThreadsG, kCThreadsG, c_lds_bytes_, stream_>>>(cp);
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev[3], stream_));
+  // fold runes: fold-tolerant item matching around each one
+  FoldParams fo;
+  fo.arena = d_arena;
+  fo.off = d_offsets;
+  fo.tabs = d_ftabs_;
+  fo.tabs_bytes = ftabs_fold_bytes_;
+  fo.t_items = ft_items_;
+  fo.t_item_ids = ft_item_ids_;
+  fo.t_item_cls = ft_item_cls_;
+  fo.t_classes = ft_classes_;
+  fo.n_items = n_fitems_;
+  fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
+  fo.first = static_cast<const uint32_t*>(d_fold_first_);
+  fo.n_pairs_k = n_fold_pairs_k_;
+  fo.n_pairs_s = n_fold_pairs_s_;
+  fo.n_cap_k = n_fold_cap_k_;
+  fo.n_cap_s = n_fold_cap_s_;
+  fo.folds = static_cast<const FoldSite*>(d_folds_);
+  fo.fold_cap = fold_cap_;
+  fo.idx_off = static_cast<const uint32_t*>(d_fold_idx_off_);
+  fo.idx_items = static_cast<const uint32_t*>(d_fold_idx_items_);
+  fo.use_idx = fold_idx_ ? 1u : 0u;
+  fo.n_cap_k_idx = n_fold_cap_k_idx_;
+  fo.n_cap_s_idx = n_fold_cap_s_idx_;
+  fo.hits = static_cast<uint32_t*>(d_hits_);
+  fo.hit_cap = hit_cap_;
+  fo.counters = d_counters_;
+  if (diag_mode_ == 0) {
+    if (lds_tabs_)
+      fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
+    else
+      fold_kernel<false><<<2048, 64 * kFoldWaves, 0, stream_>>>(fo);
+  }
+  HIP_OK(hipGetLastError());
+  if (diag_mode_ == 0 && kw_fold_ && n_kwf_ci_ + n_kwf_ck_ > 0) {
+    KwFoldParams kf;
+    kf.arena = d_arena;
+    kf.off = d_offsets;
+    kf.tabs = static_cast<const uint8_t*>(d_ftabs_);
+    kf.t_items = ft_items_;
+    kf.t_item_ids = ft_item_ids_;
+    kf.t_item_cls = ft_item_cls_;
+    kf.t_classes = ft_classes_;
+    kf.pairs = static_cast<const FoldPair*>(d_kwfold_pairs_);
+    kf.n_rng_i = n_kwf_ri_;
+    kf.n_rng_k = n_kwf_rk_;
+    kf.n_cap_i = n_kwf_ci_;
+    kf.n_cap_k = n_kwf_ck_;
+    kf.folds = static_cast<const FoldSite*>(d_folds_);
+    kf.fold_cap = fold_cap_;
+    kf.counters = d_counters_;
+    kf.kwbits = static_cast<uint32_t*>(d_kw_);
+    kf.kw_words = kw_words_;
+    kwfold_kernel<<<1024, 64 * kFoldWaves, 0, stream_>>>(kf);
+    HIP_OK(hipGetLastError());
+  }
+  HIP_OK(hipEventRecord(ev[4], stream_));
+  NfaParams np;
+  np.arena = d_arena;
+  np.off = d_offsets;
+  np.n_files = n_files;
+  np.nl = static_cast<const uint16_t*>(d_nl_);
+  np.anchors = d_anchors_;
+  np.rules = d_rules_;
+  np.rule_kw = d_rule_kw_;
+  np.kwbits = static_cast<const uint32_t*>(d_kw_);
+  np.kw_words = kw_words_;
+  np.flags = static_cast<const uint32_t*>(d_flags_);
+  np.nfa = d_nfa_;
+  np.hits = static_cast<const uint32_t*>(d_hits_);
+  np.hit_cap = hit_cap_;
+  np.counters = d_counters_;
+  np.cands = static_cast<Candidate*>(d_cands_);
+  np.cand_cap = cand_cap_;
+  np.fullscan_rules = d_fullscan_rules_;
+  np.n_fullscan_rules = n_fullscan_rules_;
+  np.fs_chunk = fs_chunk_;
+  np.kw_fold = kw_fold_ ? 1u : 0u;  // no keyword takes 'i' / 'k': the bits are exact without the kernel
+
+  if (diag_mode_ == 0) verify_hits_kernel<<<verify_blocks_, 256, 0, stream_>>>(np);
+  HIP_OK(hipGetLastError());
+  if (np.n_fullscan_rules > 0) {
+    HIP_OK(hipEventRecord(ev_fs, stream_));
+    fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
+    HIP_OK(hipGetLastError());
+  }
+  HIP_OK(hipEventRecord(ev[5], stream_));
+  if (diag_mode_ == 0) finalize_kernel<<<finalize_blocks_, 256, 0, stream_>>>(np);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev[6], stream_));
+  return true;
+}
+
 bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
                     std::vector<Candidate>* cands, BatchStats* st) {
   HIP_OK(hipSetDevice(device_));
@@ -2122,188 +2437,9 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
   if (n_chunks == 0) n_chunks = 1;
-  if (hit_cap_ == 0) hit_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 512, 1 << 16), 1u << 28));
-  if (cand_cap_ == 0) cand_cap_ = 1 << 16;
-  if (rec_cap_ == 0) rec_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 128, 1 << 16), 1u << 30));
-  if (fold_cap_ == 0) fold_cap_ = 1 << 16;
+  InitCaps(n_bytes);
   for (int attempt = 0; attempt < 8; attempt++) {
-    if (!Ensure(&d_chunk_file_, &cap_chunk_file_, n_chunks * 4) || !Ensure(&d_nl_, &cap_nl_, (n_chunks + 8) * 2) ||
-        !Ensure(&d_kw_, &cap_kw_, size_t(n_files) * kw_words_ * 4) ||
-        !Ensure(&d_flags_, &cap_flags_, size_t(n_files) * 4) ||
-        !Ensure(&d_folds_, &cap_folds_, size_t(fold_cap_) * sizeof(FoldSite)) ||
-        !Ensure(&d_recs_, &cap_recs_, size_t(rec_cap_) * 4) ||
-        !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
-        !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
-      return false;
-    HIP_OK(hipEventRecord(ev_[0], stream_));  // the GPU phase: clears, K0 .. finalize
-    HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
-    HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
-    HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
-    HIP_OK(hipMemsetAsync(d_chunk_file_, 0, n_chunks * 4, stream_));
-    if (d_item_diag_) HIP_OK(hipMemsetAsync(d_item_diag_, 0, 8 * std::max<size_t>(n_fitems_, 1), stream_));
-    {
-      uint32_t blocks = std::min<uint32_t>((n_files + 255) / 256, 4096);
-      chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, static_cast<uint32_t*>(d_chunk_file_));
-    }
-    // K1: streaming filter -> flagged block records
-    FilterParams fp;
-    fp.arena = d_arena;
-    fp.n_bytes = n_bytes;
-    fp.reach = d_reach_;
-    fp.diag_mode = diag_mode_;
-    fp.nl = static_cast<uint16_t*>(d_nl_);
-    fp.recs = static_cast<uint32_t*>(d_recs_);
-    fp.rec_cap = rec_cap_;
-    fp.counters = d_counters_;
-    const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
-    const uint32_t f_grid =
-        uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves, 256)));
-    HIP_OK(hipEventRecord(ev_[1], stream_));
-    filter_kernel<<<f_grid, kScanThreads, 0, stream_>>>(fp);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[2], stream_));
-    // K2: confirm + verify
-    ConfirmParams cp;
-    cp.arena = d_arena;
-    cp.n_bytes = n_bytes;
-    cp.off = d_offsets;
-    cp.chunk_file = static_cast<const uint32_t*>(d_chunk_file_);
-    cp.nl = static_cast<const uint16_t*>(d_nl_);
-    cp.reach = d_reach_;
-    cp.tabs = d_ftabs_;
-    cp.tabs_bytes = ftabs_bytes_;
-    cp.t_bucket_off = ft_bucket_off_;
-    cp.t_bucket_items = ft_bucket_items_;
-    cp.t_items = ft_items_;
-    cp.t_item_ids = ft_item_ids_;
-    cp.t_item_cls = ft_item_cls_;
-    cp.t_classes = ft_classes_;
-    cp.anchors = d_anchors_;
-    cp.rules = d_rules_;
-    cp.nfa = d_nfa_;
-    cp.recs = static_cast<const uint32_t*>(d_recs_);
-    cp.rec_cap = rec_cap_;
-    cp.flags = static_cast<uint32_t*>(d_flags_);
-    cp.counters = d_counters_;
-    cp.hits = static_cast<uint32_t*>(d_hits_);
-    cp.hit_cap = hit_cap_;
-    cp.folds = static_cast<FoldSite*>(d_folds_);
-    cp.fold_cap = fold_cap_;
-    cp.diag = diag_confirm_;
-    cp.kwbits = static_cast<uint32_t*>(d_kw_);
-    cp.kw_words = kw_words_;
-    cp.core = d_core_;
-    cp.group_items = d_group_items_;
-    cp.bucket_groups = d_bucket_groups_;
-    cp.item_diag = d_item_diag_;
-    cp.t_luts = ft_luts_;
-    cp.t_cmap = ft_cmap_;
-    cp.t_ccore = ft_ccore_;
-    cp.t_gitems = ft_gitems_;
-    cp.t_bgroups = ft_bgroups_;
-    cp.n_cls = n_core_cls_;
-    cp.t_hkeys = ft_hkeys_;
-    cp.t_hitems = ft_hitems_;
-    cp.hash_bits = hash_bits_;
-    cp.hash_buckets = hash_buckets_;
-    if (diag_mode_ == 0) {
-      if (lds_tabs_)
-        confirm_kernel<true><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
-      else
-        confirm_kernel<false><<<2048 * 256 / kCThreadsG, kCThreadsG, c_lds_bytes_, stream_>>>(cp);
-    }
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[3], stream_));
-    // fold runes: fold-tolerant item matching around each one
-    FoldParams fo;
-    fo.arena = d_arena;
-    fo.off = d_offsets;
-    fo.tabs = d_ftabs_;
-    fo.tabs_bytes = ftabs_fold_bytes_;
-    fo.t_items = ft_items_;
-    fo.t_item_ids = ft_item_ids_;
-    fo.t_item_cls = ft_item_cls_;
-    fo.t_classes = ft_classes_;
-    fo.n_items = n_fitems_;
-    fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
-    fo.first = static_cast<const uint32_t*>(d_fold_first_);
-    fo.n_pairs_k = n_fold_pairs_k_;
-    fo.n_pairs_s = n_fold_pairs_s_;
-    fo.n_cap_k = n_fold_cap_k_;
-    fo.n_cap_s = n_fold_cap_s_;
-    fo.folds = static_cast<const FoldSite*>(d_folds_);
-    fo.fold_cap = fold_cap_;
-    fo.idx_off = static_cast<const uint32_t*>(d_fold_idx_off_);
-    fo.idx_items = static_cast<const uint32_t*>(d_fold_idx_items_);
-    fo.use_idx = fold_idx_ ? 1u : 0u;
-    fo.n_cap_k_idx = n_fold_cap_k_idx_;
-    fo.n_cap_s_idx = n_fold_cap_s_idx_;
-    fo.hits = static_cast<uint32_t*>(d_hits_);
-    fo.hit_cap = hit_cap_;
-    fo.counters = d_counters_;
-    if (diag_mode_ == 0) {
-      if (lds_tabs_)
-        fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
-      else
-        fold_kernel<false><<<2048, 64 * kFoldWaves, 0, stream_>>>(fo);
-    }
-    HIP_OK(hipGetLastError());
-    if (diag_mode_ == 0 && kw_fold_ && n_kwf_ci_ + n_kwf_ck_ > 0) {
-      KwFoldParams kf;
-      kf.arena = d_arena;
-      kf.off = d_offsets;
-      kf.tabs = static_cast<const uint8_t*>(d_ftabs_);
-      kf.t_items = ft_items_;
-      kf.t_item_ids = ft_item_ids_;
-      kf.t_item_cls = ft_item_cls_;
-      kf.t_classes = ft_classes_;
-      kf.pairs = static_cast<const FoldPair*>(d_kwfold_pairs_);
-      kf.n_rng_i = n_kwf_ri_;
-      kf.n_rng_k = n_kwf_rk_;
-      kf.n_cap_i = n_kwf_ci_;
-      kf.n_cap_k = n_kwf_ck_;
-      kf.folds = static_cast<const FoldSite*>(d_folds_);
-      kf.fold_cap = fold_cap_;
-      kf.counters = d_counters_;
-      kf.kwbits = static_cast<uint32_t*>(d_kw_);
-      kf.kw_words = kw_words_;
-      kwfold_kernel<<<1024, 64 * kFoldWaves, 0, stream_>>>(kf);
-      HIP_OK(hipGetLastError());
-    }
-    HIP_OK(hipEventRecord(ev_[4], stream_));
-    NfaParams np;
-    np.arena = d_arena;
-    np.off = d_offsets;
-    np.n_files = n_files;
-    np.nl = static_cast<const uint16_t*>(d_nl_);
-    np.anchors = d_anchors_;
-    np.rules = d_rules_;
-    np.rule_kw = d_rule_kw_;
-    np.kwbits = static_cast<const uint32_t*>(d_kw_);
-    np.kw_words = kw_words_;
-    np.flags = static_cast<const uint32_t*>(d_flags_);
-    np.nfa = d_nfa_;
-    np.hits = static_cast<const uint32_t*>(d_hits_);
-    np.hit_cap = hit_cap_;
-    np.counters = d_counters_;
-    np.cands = static_cast<Candidate*>(d_cands_);
-    np.cand_cap = cand_cap_;
-    np.fullscan_rules = d_fullscan_rules_;
-    np.n_fullscan_rules = n_fullscan_rules_;
-    np.fs_chunk = fs_chunk_;
-    np.kw_fold = kw_fold_ ? 1u : 0u;  // no keyword takes 'i' / 'k': the bits are exact without the kernel
-
-    if (diag_mode_ == 0) verify_hits_kernel<<<verify_blocks_, 256, 0, stream_>>>(np);
-    HIP_OK(hipGetLastError());
-    if (np.n_fullscan_rules > 0) {
-      HIP_OK(hipEventRecord(ev_fs_, stream_));
-      fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
-      HIP_OK(hipGetLastError());
-    }
-    HIP_OK(hipEventRecord(ev_[5], stream_));
-    if (diag_mode_ == 0) finalize_kernel<<<finalize_blocks_, 256, 0, stream_>>>(np);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev_[6], stream_));
+    if (!EnqueuePhase(d_arena, n_bytes, d_offsets, n_files, n_chunks, ev_, ev_fs_)) return false;
     uint32_t cnt[16];
     HIP_OK(hipMemcpyAsync(cnt, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
     HIP_OK(WaitStream());

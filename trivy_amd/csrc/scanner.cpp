@@ -1009,13 +1009,26 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     *err = "a pre-transformed batch must be host-resident";
     return false;
   }
+  GpuEngine::Ticket ticket;
   {
     std::lock_guard<std::mutex> g(gpu_mu_[slot]);
-    if (in.dev_arena)
+    static const bool tickets = !std::getenv("TSG_TICKETS") || std::atoi(std::getenv("TSG_TICKETS")) != 0;
+    if (in.dev_arena && tickets && engine->Enqueue(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &ticket))
+      ok = true;  // collected below, after the lock is released
+    else if (in.dev_arena)
       ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
     else
       ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
                            in.transform ? &tail : nullptr);
+    if (!ok) gpu_err = engine->error();
+  }
+  if (ticket.slot >= 0) {
+    bool rerun = false;
+    ok = engine->Collect(&ticket, &cands, gst, &rerun);
+    if (ok && rerun) {  // a buffer overflowed: grow and rescan synchronously
+      std::lock_guard<std::mutex> g(gpu_mu_[slot]);
+      ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
+    }
     if (!ok) gpu_err = engine->error();
   }
   allow_thread.join();
