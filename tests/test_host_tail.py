@@ -229,3 +229,28 @@ def test_host_tail_newline_hints(hints):
         assert g.to_dict() == want, p
         n += len(want["Findings"] or [])
     assert n > 40
+
+
+def test_allow_path_literal_fast_path(tmp_path):
+    """Allow-path regexes that are one literal with optional ^ / $ are matched by
+    a byte compare (Matcher::simple); the result must equal the regex's, including
+    sources that only look literal (escaped anchors, trailing escaped '$', classes)."""
+    pats = [r"\.md$", r"^usr\/share\/", r"\/vendor\/", r"^exact\.txt$", r"a\$", r"b\\$", r"\d\.log$",
+            r"^$x", r"c\.d", r"x.y"]
+    cfg_path = tmp_path / "trivy-secret.yaml"
+    cfg_path.write_text("allow-rules:\n" + "".join(
+        "  - id: p%d\n    path: '%s'\n" % (i, p.replace("'", "''")) for i, p in enumerate(pats)))
+    cfg = ParseConfig(str(cfg_path))
+    body = b"k = AKIA" + b"Q" * 16 + b"\n"
+    paths = ["README.md", "README.mdx", "usr/share/x.txt", "x/usr/share/y", "src/vendor/z.go", "vendor/z.go",
+             "exact.txt", "exact.txt2", "a$", "xa$y", "b\\", "b\\x", "3.log", "x.log", "c.d", "cxd", "xzy",
+             "x.y", "plain.txt", "$x"]
+    files = [(p, body) for p in paths]
+    got = host_tail_scan(cfg, files)
+    o = osc.new_scanner(osc.parse_config(str(cfg_path)))
+    n_allowed = 0
+    for (p, b), g in zip(files, got):
+        want = o.scan(p, b)
+        assert g.to_dict() == want, p
+        n_allowed += not want["Findings"]
+    assert n_allowed >= 8

@@ -4,6 +4,7 @@
 #include "parallel.h"
 
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
@@ -289,8 +290,52 @@ void SortFindings(FileFindings* f, const std::vector<RuleSpec>& rules) {
   Pdqsort(d, 0, n, BitsLen(unsigned(n)));
 }
 
+bool SimpleLiteral(const std::string& src, std::string* lit, bool* begin, bool* end) {
+  static const std::string kMeta = "\\.+*?()|[]{}^$";
+  size_t i = 0, e = src.size();
+  *begin = e > 0 && src[0] == '^';
+  if (*begin) i = 1;
+  // a trailing unescaped '$' (an even run of backslashes before it)
+  *end = false;
+  if (e > i && src[e - 1] == '$') {
+    size_t bs = 0;
+    while (e - 1 - bs > i && src[e - 2 - bs] == '\\') bs++;
+    if (bs % 2 == 0) {
+      *end = true;
+      e--;
+    }
+  }
+  lit->clear();
+  while (i < e) {
+    const unsigned char c = static_cast<unsigned char>(src[i]);
+    if (c == '\\') {
+      if (i + 1 >= e) return false;
+      const unsigned char d = static_cast<unsigned char>(src[i + 1]);
+      if (d >= 0x80 || std::isalnum(d) || d == '_') return false;  // \d, \b, \x.. and the like
+      lit->push_back(char(d));
+      i += 2;
+    } else {
+      if (kMeta.find(char(c)) != std::string::npos) return false;
+      lit->push_back(char(c));
+      i++;
+    }
+  }
+  return !lit->empty();
+}
+
+bool Matcher::MatchSimple(const uint8_t* s, size_t n) const {
+  const size_t k = simple_lit.size();
+  if (k > n) return false;
+  const char* l = simple_lit.data();
+  if (simple_begin && simple_end) return k == n && std::memcmp(s, l, k) == 0;
+  if (simple_begin) return std::memcmp(s, l, k) == 0;
+  if (simple_end) return std::memcmp(s + n - k, l, k) == 0;
+  return memmem(s, n, l, k) != nullptr;
+}
+
 bool Matcher::Match(const uint8_t* s, size_t n) const {
   if (!re) return false;
+  if (simple) return MatchSimple(s, n);
   if (!lits.empty()) {
     bool ascii = true;
     for (size_t i = 0; i < n; i++)
@@ -453,7 +498,8 @@ bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
         const int i = __builtin_ctzll(mask);
         mask &= mask - 1;
         const Matcher& m = *allow_[size_t(i)].path;
-        if ((lit_rules >> i & 1) ? m.re->Match(p, int64_t(n)) : m.Match(p, n)) return true;
+        if (m.simple ? m.MatchSimple(p, n) : (lit_rules >> i & 1) ? m.re->Match(p, int64_t(n)) : m.Match(p, n))
+          return true;
       }
       return false;
     }
