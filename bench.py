@@ -243,6 +243,30 @@ def _cgroup_cpu():
         return None
 
 
+def _thread_cpu():
+    """CPU seconds of this process: per live thread name, and the process total
+    (threads that exited in between, e.g. the per-scan tsg-scan / tsg-allow
+    threads, only show in the total)."""
+    tck = os.sysconf("SC_CLK_TCK")
+    by = {}
+    try:
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                with open("/proc/self/task/%s/stat" % tid) as f:
+                    st = f.read()
+            except OSError:
+                continue
+            name = st[st.index("(") + 1:st.rindex(")")]
+            fl = st[st.rindex(")") + 2:].split()
+            by[name] = by.get(name, 0.0) + (int(fl[11]) + int(fl[12])) / tck
+        with open("/proc/self/stat") as f:
+            st = f.read()
+        fl = st[st.rindex(")") + 2:].split()
+        return by, (int(fl[11]) + int(fl[12])) / tck
+    except (OSError, ValueError, IndexError):
+        return None
+
+
 def _bind_numa(device):
     """Bind the process to the CPUs of the GPU's NUMA node before the corpus
     and the host pool exist: the host pass reads the arena with cold misses,
@@ -407,6 +431,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     cg0 = _cgroup_cpu()
+    tc0 = _thread_cpu()
     t0 = time.time()
     stats = []
     run_steps(args.steps, stats)
@@ -414,11 +439,20 @@ def main():
     barrier()
     dt = time.time() - t0
     cg1 = _cgroup_cpu()
+    tc1 = _thread_cpu()
     host_cpu = None
     if cg0 and cg1:  # the container's CPU use over the timed steps (quota throttling shows here)
         host_cpu = {"cpus_used": round((cg1["usage_usec"] - cg0["usage_usec"]) / (dt * 1e6), 2),
                     "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3, 1),
                     "quota_cpus": cg1.get("quota_cpus")}
+    if tc0 and tc1:  # CPU-ms per step of this process, by thread name (the rest: threads that exited)
+        host_cpu = host_cpu or {}
+        per = {k: round((v - tc0[0].get(k, 0.0)) * 1e3 / args.steps, 2) for k, v in tc1[0].items()}
+        per = {k: v for k, v in sorted(per.items(), key=lambda kv: -kv[1]) if v >= 0.05}
+        total = round((tc1[1] - tc0[1]) * 1e3 / args.steps, 2)
+        per["(exited threads)"] = round(total - sum(per.values()), 2)
+        host_cpu["process_cpu_ms_per_step"] = total
+        host_cpu["by_thread_ms_per_step"] = per
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

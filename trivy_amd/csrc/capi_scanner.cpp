@@ -1,5 +1,6 @@
 // C ABI of the drop-in scanner (include/tsg_scanner.h) and of the rule
 // compiler inspection hooks (include/tsg_debug.h).
+#include <pthread.h>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -48,6 +49,7 @@ class ResultReaper {
  private:
   ResultReaper() : th_([this] { Run(); }) {}
   void Run() {
+    pthread_setname_np(pthread_self(), "tsg-reaper");
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
       cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
@@ -221,6 +223,7 @@ int tsg_scan_submit(tsg_scanner* s, const tsg_batch* b, tsg_pending** out) {
   const tsg_batch bc = *b;
   tsg_pending* pp = p.get();
   pp->th = std::thread([s, bc, pp] {
+    pthread_setname_np(pthread_self(), "tsg-scan");
     pp->rc = tsg_scan(s, &bc, &pp->r);
     if (pp->rc != 0) pp->err = tsg_last_error();
   });

@@ -4,6 +4,7 @@
 // cores instead of each spawning its own threads (oversubscribing a 16-core
 // share measured 1.4x slower).
 #pragma once
+#include <pthread.h>
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -75,7 +76,10 @@ class HostPool {
     int n = e ? std::atoi(e) : DefaultWorkers();
     if (n < 0) n = 0;
     for (int k = 0; k < n; k++) {
-      workers_.emplace_back([this] { Loop(); });
+      workers_.emplace_back([this] {
+        pthread_setname_np(pthread_self(), "tsg-pool");
+        Loop();
+      });
       workers_.back().detach();
     }
   }

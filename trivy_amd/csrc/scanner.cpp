@@ -3,6 +3,7 @@
 
 #include "parallel.h"
 
+#include <pthread.h>
 #include <algorithm>
 #include <cctype>
 #include <cstdio>
@@ -1043,6 +1044,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   std::vector<uint8_t> allowed;
   double ms_allow = 0;
   std::thread allow_thread([&] {
+    pthread_setname_np(pthread_self(), "tsg-allow");
     double a0 = NowMs();
     allowed = AllowedPaths(in);
     ms_allow = NowMs() - a0;
