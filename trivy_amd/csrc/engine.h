@@ -198,6 +198,7 @@ class GpuEngine {
   uint32_t verify_blocks_ = 4096;  // a lane per deferred hit (0.59 -> 0.51 ms vs 2048 on C2)
   uint32_t finalize_blocks_ = 16384;  // a wave per candidate, latency-bound: ~1 candidate per wave (0.42 -> 0.25 ms vs 1024)
   hipError_t WaitStream();
+  hipError_t WaitEvent(hipEvent_t ev);
   uint32_t* d_item_diag_ = nullptr;   // TSG_DIAG_ITEMS=<file>: per-item counters dumped after each run
   std::string item_diag_path_;
 };

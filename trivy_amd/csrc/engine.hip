@@ -17,6 +17,7 @@
 //                   regexp sweeps, scanner.go:102-148).
 //  K4 full-scan   : (file x unanchored rule) tasks: NFA with injection at
 //                   every byte; an accept makes the whole file a candidate.
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2111,10 +2112,22 @@ bool GpuEngine::GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint
   return true;
 }
 
+// Waits for a scan's kernels sleep-poll the event (TSG_WAIT_POLL_US, default
+// 200 us): even a hipEventBlockingSync wait spun in the runtime long enough to
+// cost ~14 CPU-ms per C2 step, and the host side is bound by the
+// box's CPU quota; 200 us of wake-up latency is hidden by the pipeline.
+hipError_t GpuEngine::WaitEvent(hipEvent_t ev) {
+  static const int poll_us = std::getenv("TSG_WAIT_POLL_US") ? std::atoi(std::getenv("TSG_WAIT_POLL_US")) : 200;
+  if (poll_us <= 0) return hipEventSynchronize(ev);
+  hipError_t e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
+  return e;
+}
+
 hipError_t GpuEngine::WaitStream() {
   if (!blocking_sync_ || !ev_sync_) return hipStreamSynchronize(stream_);
   hipError_t e = hipEventRecord(ev_sync_, stream_);
-  return e != hipSuccess ? e : hipEventSynchronize(ev_sync_);
+  return e != hipSuccess ? e : WaitEvent(ev_sync_);
 }
 
 void GpuEngine::InitCaps(uint64_t n_bytes) {
@@ -2197,7 +2210,7 @@ bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st
     S.busy = false;
     t->slot = -1;
   };
-  const hipError_t e = hipEventSynchronize(S.done);
+  const hipError_t e = WaitEvent(S.done);
   if (e != hipSuccess) {
     err_ = std::string("Collect: ") + hipGetErrorString(e);
     release();
