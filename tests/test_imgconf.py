@@ -49,3 +49,52 @@ def test_gpu_imgconf_analyzer_golden(case):
         assert got is None
     else:
         assert got.Secret.to_dict() == case["want"]["Secret"]
+
+
+def test_marshal_history_and_healthcheck():
+    """v1.History and v1.HealthConfig in struct declaration order (go-containerregistry v0.20.2 tags:
+    History{author, created (a v1.Time struct: never omitted), created_by, comment, empty_layer};
+    HealthConfig{Test, Interval, Timeout, StartPeriod, Retries} with Go field names).  Parity
+    unpinned: the reference's tests cover Env only; the expected text follows the struct tags."""
+    cfg = {"architecture": "amd64", "os": "linux",
+           "history": [{"created_by": "RUN echo ghp_" + "a" * 36, "comment": "c", "empty_layer": True,
+                        "author": "me"},
+                       {"created": "2024-01-02T03:04:05Z", "created_by": "CMD sh", "empty_layer": False}],
+           "config": {"Healthcheck": {"Retries": 3, "Test": ["CMD", "true"], "Interval": 1000000000}}}
+    want = "\n".join([
+        '{',
+        '  "architecture": "amd64",',
+        '  "created": "0001-01-01T00:00:00Z",',
+        '  "history": [',
+        '  {',
+        '  "author": "me",',
+        '  "created": "0001-01-01T00:00:00Z",',
+        '  "created_by": "RUN echo ghp_' + "a" * 36 + '",',
+        '  "comment": "c",',
+        '  "empty_layer": true',
+        '  },',
+        '  {',
+        '  "created": "2024-01-02T03:04:05Z",',
+        '  "created_by": "CMD sh"',
+        '  }',
+        '  ],',
+        '  "os": "linux",',
+        '  "rootfs": {',
+        '  "type": "",',
+        '  "diff_ids": null',
+        '  },',
+        '  "config": {',
+        '  "Healthcheck": {',
+        '  "Test": [',
+        '  "CMD",',
+        '  "true"',
+        '  ],',
+        '  "Interval": 1000000000,',
+        '  "Retries": 3',
+        '  }',
+        '  }',
+        '  }'])
+    got = MarshalIndentConfigFile(cfg, "  ", "").decode()
+    assert got == want
+    res = osc.new_scanner(None).scan("config.json", got.encode())
+    assert [(f["RuleID"], f["StartLine"]) for f in res["Findings"]] == [("github-pat", 8)]

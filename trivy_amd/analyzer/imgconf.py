@@ -24,18 +24,25 @@ analyzerVersion = 1                       # secret.go:15
 
 # (json name, Go kind, omitempty) in declaration order
 _CONFIG_FILE = [("architecture", "str", False), ("author", "str", True), ("container", "str", True),
-                ("created", "time", True), ("docker_version", "str", True), ("history", "list", True),
+                ("created", "time", True), ("docker_version", "str", True), ("history", "history", True),
                 ("os", "str", False), ("rootfs", "rootfs", False), ("config", "config", False),
                 ("os.version", "str", True), ("variant", "str", True), ("os.features", "list", True)]
 _ROOTFS = [("type", "str", False), ("diff_ids", "list_null", False)]
 _CONFIG = [("AttachStderr", "bool", True), ("AttachStdin", "bool", True), ("AttachStdout", "bool", True),
-           ("Cmd", "list", True), ("Healthcheck", "obj", True), ("Domainname", "str", True),
+           ("Cmd", "list", True), ("Healthcheck", "health", True), ("Domainname", "str", True),
            ("Entrypoint", "list", True), ("Env", "list", True), ("Hostname", "str", True), ("Image", "str", True),
            ("Labels", "map", True), ("OnBuild", "list", True), ("OpenStdin", "bool", True),
            ("StdinOnce", "bool", True), ("Tty", "bool", True), ("User", "str", True), ("Volumes", "map", True),
            ("WorkingDir", "str", True), ("ExposedPorts", "map", True), ("ArgsEscaped", "bool", True),
            ("NetworkDisabled", "bool", True), ("MacAddress", "str", True), ("StopSignal", "str", True),
            ("Shell", "list", True)]
+# v1.History (struct fields in declaration order; Created is a v1.Time struct, so
+# omitempty never drops it: an unset time marshals as the zero time)
+_HISTORY = [("author", "str", True), ("created", "time", True), ("created_by", "str", True),
+            ("comment", "str", True), ("empty_layer", "bool", True)]
+# v1.HealthConfig (no JSON names: the field names; time.Duration marshals as int64 nanoseconds)
+_HEALTH = [("Test", "list", True), ("Interval", "int", True), ("Timeout", "int", True),
+           ("StartPeriod", "int", True), ("Retries", "int", True)]
 _ZERO_TIME = "0001-01-01T00:00:00Z"
 
 
@@ -76,8 +83,16 @@ def _struct(fields, d: Dict[str, Any]):
         if kind == "time":  # v1.Time wraps time.Time: a struct, never omitted
             items.append((name, _go_string(v or _ZERO_TIME)))
             continue
-        empty = v is None or v == "" or v is False or (isinstance(v, (list, dict)) and len(v) == 0)
+        if kind == "health":  # *HealthConfig: omitted when nil, else the struct (its own omitempty)
+            if v is None:
+                continue
+            items.append((name, _struct(_HEALTH, v)))
+            continue
+        empty = v is None or v == "" or v is False or v == 0 or (isinstance(v, (list, dict)) and len(v) == 0)
         if omit and empty:
+            continue
+        if kind == "history":  # []History: each entry a struct
+            items.append((name, ("arr", [_struct(_HISTORY, h or {}) for h in v])))
             continue
         if kind == "list_null" and v is None:
             items.append((name, "null"))
@@ -86,6 +101,8 @@ def _struct(fields, d: Dict[str, Any]):
             items.append((name, _go_string(v or "")))
         elif kind == "bool":
             items.append((name, "true" if v else "false"))
+        elif kind == "int":
+            items.append((name, str(int(v or 0))))
         else:
             items.append((name, _value(v)))
     return ("obj", items)

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <atomic>
 #include <string>
 #include <mutex>
 #include <vector>
@@ -87,12 +88,19 @@ class GpuEngine {
   // ticket is free or a diagnostic mode is on (then call Run); Collect sets
   // *rerun when a buffer overflowed (then call Run under the lock: it grows
   // the buffers and rescans).
+  // The candidate read-back copies min(cand_cap, 2 x the largest count of
+  // the last collected scans + 64 Ki) records: a one-off spike that grew the
+  // device buffer does not make every later scan copy all of it; a count
+  // above the copied part reruns the scan (as an overflow does).  Errors of
+  // Enqueue / Collect are returned in *err (Collect runs without the engine's
+  // lock, so it must not write err_).
   struct Ticket {
     int slot = -1;
-    uint32_t cand_cap = 0;
+    uint32_t cand_copy = 0;  // candidates copied back
   };
-  bool Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files, Ticket* t);
-  bool Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st, bool* rerun);
+  bool Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files, Ticket* t,
+               std::string* err);
+  bool Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st, bool* rerun, std::string* err);
 
   // Device buffers of the last run (for tests / bench).
   hipEvent_t ev_scan0() const { return ev_[1]; }
@@ -114,6 +122,7 @@ class GpuEngine {
     uint32_t n_files = 0;
   };
   static constexpr int kSlots = 4;
+  std::atomic<uint32_t> cand_recent_{0};  // largest candidate count of the recently collected scans
   Slot slots_[kSlots];
   std::mutex slot_mu_;
   bool Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,

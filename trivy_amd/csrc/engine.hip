@@ -26,6 +26,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <type_traits>
 
 #include "engine.h"
 #include "xform.h"
@@ -68,19 +69,21 @@ __device__ __forceinline__ void wave_sync() {
 // ---------------------------------------------------------------------------
 // K1: streaming bucketed shift-or filter
 // ---------------------------------------------------------------------------
-#ifndef TSG_K1_PINGPONG
-#define TSG_K1_PINGPONG 1
-#endif
-#ifndef TSG_K1_DPP
-#define TSG_K1_DPP 1
-#endif
 constexpr int kFLane = 64;           // bytes per lane per tile (4 blocks of 16 B)
 constexpr int kFBlocks = kFLane / 16;
 constexpr int kFTile = 64 * kFLane;  // 4 KiB per wave tile
-constexpr int kFFlushAt = 256;                      // flush the flagged-block queue at >= this many
-constexpr int kFQueue = kFFlushAt + 64 * kFBlocks;  // per-wave queue entries
+// LDS per 1024-thread workgroup: 64 KiB reach table + 12 KiB queues + 2 KiB
+// newline staging = 78 KiB, so two workgroups share a CU (8 waves per SIMD at
+// <= 64 VGPRs): tools/k1x.hip measured 4.98 vs 5.35 ms for one per CU (C2).
+constexpr int kFFlushAt = 128;                      // flush the flagged-block queue at >= this many
+constexpr int kFQueue = kFFlushAt + 64;             // per-wave queue entries (a block column appends <= 64)
 constexpr int kFChunks = kFTile / 1024;             // newline chunks per tile (kChunk = 1 KiB)
-constexpr int kFNlTiles = 64;                       // tiles whose newline counts a wave stages in LDS
+constexpr int kFNlTiles = 16;                       // tiles whose newline counts a wave stages in LDS
+constexpr int kFWgPerCu = 2;
+#ifndef TSG_K1_READAHEAD
+#define TSG_K1_READAHEAD 4
+#endif
+constexpr uint32_t kFReadAhead = TSG_K1_READAHEAD;  // table rows read ahead of the shift-or chain
 constexpr int kFWindow = 6;          // filter window: a fire stays visible for 9 - 6 = 3 bytes
 constexpr int kFWords = 4;           // 16 buckets = 4 u32 registers of 8 slots x 4 buckets
 constexpr uint32_t kFireBits = 0xFFF00000u;  // slots 5..7 of a register
@@ -144,37 +147,44 @@ __device__ __forceinline__ void load_reach_lds(uint8_t* s_reach, const uint32_t*
 // 4 slots are popcounted.  Flagged blocks go through a ballot/mbcnt-compacted
 // per-wave LDS queue to the global record list (one atomic per 64 records);
 // the confirm kernel (K2) checks them exactly.
-__global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
+__global__ __launch_bounds__(kScanThreads, 4 * kFWgPerCu) void filter_kernel(FilterParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
   __shared__ uint32_t s_queue[kScanWaves * kFQueue];
   __shared__ uint64_t s_nl[kScanWaves * kFNlTiles];  // per wave: the last tiles' 4 chunk counts
   const int tid = threadIdx.x;
   load_reach_lds(s_reach, P.reach, 16, tid, blockDim.x);
   __syncthreads();
-  const uint32_t lane = tid & 63, wave = tid >> 6;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6);
   const uint32_t laneoff = (lane & 15) * 16;
   uint32_t* Q = s_queue + wave * kFQueue;
   uint64_t* NL = s_nl + wave * kFNlTiles;
   uint32_t nl_slots = 0;  // wave-uniform: tiles staged in NL
   uint32_t qn = 0;  // wave-uniform
+  // Each wave streams one contiguous range of tiles, so lane 0's 8-byte
+  // prefix is lane 63's last 8 bytes of the wave's previous tile (carried in
+  // scalar registers) -- only the range's first tile loads it.
   const uint64_t n_tiles = (P.n_bytes + kFTile - 1) / kFTile;
   const uint64_t n_waves = uint64_t(gridDim.x) * kScanWaves;
-  uint64_t t = uint64_t(blockIdx.x) * kScanWaves + wave;
+  const uint64_t wid = uint64_t(blockIdx.x) * kScanWaves + wave;
+  const uint64_t per = n_tiles / n_waves, extra = n_tiles % n_waves;
+  const uint64_t t_begin = wid * per + (wid < extra ? wid : extra);
+  const uint64_t t_end = t_begin + per + (wid < extra ? 1 : 0);
   uint4 bufA[kFBlocks], bufB[kFBlocks];
-  uint2 preA = make_uint2(0, 0), preB = make_uint2(0, 0);
-  auto load_tile = [&](uint4* dst, uint2* pv, uint64_t tt) {
-    const uint64_t t0 = tt * kFTile;
+  uint32_t pre_x = 0, pre_y = 0;  // wave-uniform: the 8 bytes before the current tile
+  if (t_begin < t_end && t_begin > 0) {
+    const uint2 pv = *reinterpret_cast<const uint2*>(P.arena + t_begin * kFTile - 8);
+    pre_x = __builtin_amdgcn_readfirstlane(pv.x);
+    pre_y = __builtin_amdgcn_readfirstlane(pv.y);
+  }
+  auto load_tile = [&](uint4* dst, uint64_t tt) {
     // One clamp per lane, no branch (a wave-uniform full-tile branch around
     // the loads cost 1.4 ms on C2): a lane chunk starting inside the arena is
     // readable whole (64 readable bytes past n_bytes), one past it reloads 0.
-    const uint64_t b0 = t0 + uint64_t(lane) * kFLane;
+    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLane;
     const uint8_t* lp = P.arena + (b0 < P.n_bytes ? b0 : 0);
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) dst[j] = load16(lp + 16 * j);
-    // the 8 bytes before the tile (lane 0's prefix): a uniform address, so one
-    // request; unconditional like the block loads, so the loads in flight stay
-    // a static count and the chain waits only for the current tile's.
-    *pv = *reinterpret_cast<const uint2*>(P.arena + (tt > 0 ? t0 - 8 : 0));
   };
   auto flush = [&]() {  // wave-uniform
     uint32_t base = 0;
@@ -189,18 +199,21 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
   // Global stores are rare on purpose: on gfx9 a store counts in vmcnt like
   // the loads, so a store per tile would make the next tile's wait for its
   // prefetched data also wait for the store's completion.
-  auto flush_nl = [&](uint64_t t_last) {  // wave-uniform; staged tiles are t_last - (nl_slots-1-i) * n_waves
+  auto flush_nl = [&](uint64_t t_last) {  // wave-uniform; staged tiles are t_last - (nl_slots-1) .. t_last
     wave_sync();
     if (lane < nl_slots) {
-      const uint64_t tt = t_last - uint64_t(nl_slots - 1 - lane) * n_waves;
+      const uint64_t tt = t_last - uint64_t(nl_slots - 1 - lane);
       reinterpret_cast<uint64_t*>(P.nl)[tt] = NL[lane];  // chunks 4tt .. 4tt+3 (buffer padded past the end)
     }
     nl_slots = 0;
   };
-  // One tile: `cur` holds its 64 bytes per lane, `pre` lane 0's prefix.
-  auto tile = [&](uint4* cur, uint2 pre, uint64_t tt) {
-    const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLane;
-    if (tt * kFTile + kFTile > P.n_bytes) {  // wave-uniform: bytes past the arena end (last tile only) are zeroed
+  // One tile: `cur` holds its 64 bytes per lane.  kTail: the arena's last,
+  // partial tile (bytes past the end are zeroed); kept out of the main loop's
+  // code so the full tiles carry no masking state.
+  auto tile = [&](uint4* cur, uint64_t tt, auto tail_tag) {
+    constexpr bool kTail = decltype(tail_tag)::value;
+    if (kTail) {
+      const uint64_t b0 = tt * kFTile + uint64_t(lane) * kFLane;
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint64_t p = b0 + 16 * j;
@@ -215,19 +228,13 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
       }
     }
     // the previous 8 bytes: lane l-1's last two words by a DPP wave shift
-    // (lane 0 takes the extra load: the tile before, or zeros at the arena start)
-#if TSG_K1_DPP
-    const uint32_t p0 = uint32_t(__builtin_amdgcn_update_dpp(int(tt > 0 ? pre.x : 0u), int(cur[kFBlocks - 1].z),
-                                                             0x138, 0xF, 0xF, false));
-    const uint32_t p1 = uint32_t(__builtin_amdgcn_update_dpp(int(tt > 0 ? pre.y : 0u), int(cur[kFBlocks - 1].w),
-                                                             0x138, 0xF, 0xF, false));
-#else
-    uint32_t p0 = __shfl(cur[kFBlocks - 1].z, int(lane) - 1), p1 = __shfl(cur[kFBlocks - 1].w, int(lane) - 1);
-    if (lane == 0) {
-      p0 = tt > 0 ? pre.x : 0u;
-      p1 = tt > 0 ? pre.y : 0u;
-    }
-#endif
+    // (lane 0: the carried prefix, zeros at the arena start)
+    const uint32_t p0 = uint32_t(__builtin_amdgcn_update_dpp(int(pre_x), int(cur[kFBlocks - 1].z), 0x138, 0xF, 0xF,
+                                                             false));
+    const uint32_t p1 = uint32_t(__builtin_amdgcn_update_dpp(int(pre_y), int(cur[kFBlocks - 1].w), 0x138, 0xF, 0xF,
+                                                             false));
+    pre_x = __builtin_amdgcn_readlane(cur[kFBlocks - 1].z, 63);
+    pre_y = __builtin_amdgcn_readlane(cur[kFBlocks - 1].w, 63);
     uint32_t flagged = 0, nl = 0;
     if (P.diag_mode < 2) {
       uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
@@ -237,15 +244,22 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
 #pragma unroll
       for (int j = 0; j < kFBlocks; j++) {
         const uint32_t wd[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
-        uint4 m[16];  // a block's table reads first (independent of the state), then the chain
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++) m[k] = reach_read(s_reach, wd[k >> 2], k & 3, laneoff);
         uint32_t acc = ~0u;
+        // table reads in groups of kFReadAhead ahead of the chain (independent of
+        // the state): fewer live VGPRs than a whole block's 16 rows
 #pragma unroll
-        for (uint32_t k = 0; k < 16; k++) {
-          reach_apply(m[k], st);
-          if (k % 3 == 2 || k == 15) acc &= st[0] & st[1] & st[2] & st[3];
-          if (k % 4 == 3) nl += __popc(~st[3] & kNlBits);
+        for (uint32_t g = 0; g < 16; g += kFReadAhead) {
+          uint4 m[kFReadAhead];
+#pragma unroll
+          for (uint32_t q = 0; q < kFReadAhead; q++)
+            m[q] = reach_read(s_reach, wd[(g + q) >> 2], (g + q) & 3, laneoff);
+#pragma unroll
+          for (uint32_t q = 0; q < kFReadAhead; q++) {
+            const uint32_t k = g + q;
+            reach_apply(m[q], st);
+            if (k % 3 == 2 || k == 15) acc &= st[0] & st[1] & st[2] & st[3];
+            if (k % 4 == 3) nl += __popc(~st[3] & kNlBits);
+          }
         }
         flagged |= uint32_t((acc | ~kFireBits) != ~0u) << j;
       }
@@ -254,7 +268,6 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
       for (int j = 0; j < kFBlocks; j++)
         nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
     }
-#if TSG_K1_DPP
     // newlines per 1-KiB chunk = per 16-lane DPP row: a row_shr 1/2/4/8 sum puts it in the row's last lane
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x111, 0xF, 0xF, true));
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x112, 0xF, 0xF, true));
@@ -262,50 +275,45 @@ __global__ __launch_bounds__(kScanThreads) void filter_kernel(FilterParams P) {
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x118, 0xF, 0xF, true));
     static_assert(kChunk / kFLane == 16, "one newline chunk per DPP row");
     if ((lane & 15) == 15) reinterpret_cast<uint16_t*>(NL + nl_slots)[lane >> 4] = uint16_t(nl);
-#else
-#pragma unroll
-    for (int x = 1; x < int(kChunk / kFLane); x <<= 1) nl += __shfl_xor(nl, x);
-    if ((lane & (kChunk / kFLane - 1)) == 0)
-      reinterpret_cast<uint16_t*>(NL + nl_slots)[lane / (kChunk / kFLane)] = uint16_t(nl);
-#endif
     if (++nl_slots == kFNlTiles) flush_nl(tt);
+    // the flagged block columns, compacted (record = arena byte / 16)
+    const uint32_t rec0 = uint32_t(tt * (kFTile / 16)) + lane * kFBlocks;
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) {
       const bool fj = (flagged >> j) & 1u;
       const uint64_t m = __ballot(fj);
       if (m) {
+        if (qn + 64 > kFQueue) flush();  // wave-uniform; rare (> 128 records since the last flush)
         const uint32_t below =
             __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-        if (fj) Q[qn + below] = uint32_t((b0 + 16 * j) >> 4);
+        if (fj) Q[qn + below] = rec0 + uint32_t(j);
         qn += uint32_t(__popcll(m));
       }
     }
     if (qn >= kFFlushAt) flush();
   };
-#if TSG_K1_PINGPONG
-  // two register buffers alternate roles (no copies): tile t in A while t + n_waves loads into B
-  if (t < n_tiles) load_tile(bufA, &preA, t);
-  while (t < n_tiles) {
-    load_tile(bufB, &preB, t + n_waves < n_tiles ? t + n_waves : t);  // past the end: a harmless reload
-    tile(bufA, preA, t);
-    t += n_waves;
-    if (t >= n_tiles) break;
-    load_tile(bufA, &preA, t + n_waves < n_tiles ? t + n_waves : t);
-    tile(bufB, preB, t);
-    t += n_waves;
+  using Full = std::false_type;
+  // whole tiles; the arena's partial last tile (if any) is the last of its wave's range
+  const uint64_t t_full = t_end < P.n_bytes / kFTile ? t_end : P.n_bytes / kFTile;
+  uint64_t t = t_begin;
+  // two register buffers alternate roles (no copies): tile t in A while t + 1 loads into B
+  if (t < t_full) load_tile(bufA, t);
+  while (t < t_full) {
+    load_tile(bufB, t + 1 < t_full ? t + 1 : t);  // past the range: a harmless reload
+    tile(bufA, t, Full());
+    t++;
+    if (t >= t_full) break;
+    load_tile(bufA, t + 1 < t_full ? t + 1 : t);
+    tile(bufB, t, Full());
+    t++;
   }
-#else
-  if (t < n_tiles) load_tile(bufA, &preA, t);
-  for (; t < n_tiles; t += n_waves) {
-    load_tile(bufB, &preB, t + n_waves < n_tiles ? t + n_waves : t);
-    tile(bufA, preA, t);
-#pragma unroll
-    for (int j = 0; j < kFBlocks; j++) bufA[j] = bufB[j];
-    preA = preB;
+  if (t < t_end) {  // the partial last tile
+    load_tile(bufA, t);
+    tile(bufA, t, std::true_type());
+    t++;
   }
-#endif
   if (qn) flush();
-  if (nl_slots) flush_nl(t - n_waves);
+  if (nl_slots) flush_nl(t - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1491,13 +1499,24 @@ __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
       for (int x = 1; x < 64; x <<= 1) part += __shfl_xor(part, x);
       if (lane == 0) c.nl_before = part;
     }
+    // gate flags first: a candidate the host will drop needs no newline hints
+    const RuleGpu rg = P.rules[c.rule];
+    uint32_t fl = gate_flags(P, rg, file);
+    if (rg.gate == kGateKeywords && !rg.kw_match_implied && !kw_bits_inexact(P, file) && !(fl & kCandGateOpen))
+      fl |= kCandDrop;
     // the last three '\n' before wlo: 1 KiB per step, lane 0 on the highest
-    // 16-B block; a lane's newlines take ranks after those of the lanes above
-    {
+    // 16-B block; a lane's newlines take ranks after those of the lanes above.
+    // A 1-KiB chunk whose K1 count is 0 is skipped whole (long single lines).
+    if (!(fl & kCandDrop)) {
       const uint64_t wabs = fs + uint64_t(c.wlo);
       uint64_t hi = wabs;  // [fs, hi) still unsearched
       uint32_t found = 0;
       while (found < 3 && hi > fs && wabs - hi < kNlReach) {
+        const uint64_t ck = (hi - 1) / kChunk;  // wave-uniform
+        if (ck * kChunk >= fs && P.nl[ck] == 0) {  // no '\n' in [ck * kChunk, hi)
+          hi = ck * kChunk;
+          continue;
+        }
         const uint64_t blk = (((hi - 1) >> 4) - lane) << 4;  // may wrap below fs: masked out
         uint32_t mask = 0;
         if (blk + 16 > fs && blk < hi && int64_t(blk) >= 0) {
@@ -1532,13 +1551,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
       if (hi <= fs)  // reached the file start: the remaining ranks do not exist
         for (uint32_t r = found + lane; r < 3; r += 64) c.nl_back[r] = kNlNone;
     }
-    if (lane == 0) {
-      const RuleGpu rg = P.rules[c.rule];
-      uint32_t fl = gate_flags(P, rg, file);
-      if (rg.gate == kGateKeywords && !rg.kw_match_implied && !kw_bits_inexact(P, file) && !(fl & kCandGateOpen))
-        fl |= kCandDrop;
-      c.flags = fl;
-    }
+    if (lane == 0) c.flags = fl;
   }
 }
 
@@ -2138,7 +2151,7 @@ void GpuEngine::InitCaps(uint64_t n_bytes) {
 }
 
 bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
-                        Ticket* t) {
+                        Ticket* t, std::string* err) {
   t->slot = -1;
   if (n_files == 0 || n_bytes >= (uint64_t(1) << 36) - 64 || d_item_diag_ || diag_mode_ != 0) return false;
   int k = -1;
@@ -2153,6 +2166,10 @@ bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t
   if (k < 0) return false;
   Slot& S = slots_[k];
   auto fail = [&] {
+    // copies into the slot's pinned buffers may be queued: let them finish
+    // before the slot (and its buffers) can be reused or freed
+    (void)hipStreamSynchronize(stream_);
+    *err = err_.empty() ? "Enqueue failed" : err_;
     std::lock_guard<std::mutex> g(slot_mu_);
     S.busy = false;
     return false;
@@ -2169,22 +2186,23 @@ bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t
       return fail();
     }
   }
-  if (S.h_cap < cand_cap_) {
+  const uint32_t n_copy = uint32_t(std::min<uint64_t>(cand_cap_, 2 * uint64_t(cand_recent_.load()) + 65536));
+  if (S.h_cap < n_copy) {
     if (S.h_cands) hipHostFree(S.h_cands);
     S.h_cands = nullptr;
     S.h_cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&S.h_cands), size_t(cand_cap_) * sizeof(Candidate),
+    if (hipHostMalloc(reinterpret_cast<void**>(&S.h_cands), size_t(n_copy) * sizeof(Candidate),
                       hipHostMallocDefault) != hipSuccess) {
       err_ = "hipHostMalloc failed for the candidate read-back";
       return fail();
     }
-    S.h_cap = cand_cap_;
+    S.h_cap = n_copy;
   }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
   if (n_chunks == 0) n_chunks = 1;
   if (!EnqueuePhase(d_arena, n_bytes, d_offsets, n_files, n_chunks, S.ev, S.ev_fs) ||
       hipMemcpyAsync(S.h_cnt, d_counters_, 64, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
-      hipMemcpyAsync(S.h_cands, d_cands_, size_t(cand_cap_) * sizeof(Candidate), hipMemcpyDeviceToHost, stream_) !=
+      hipMemcpyAsync(S.h_cands, d_cands_, size_t(n_copy) * sizeof(Candidate), hipMemcpyDeviceToHost, stream_) !=
           hipSuccess ||
       hipEventRecord(S.done, stream_) != hipSuccess) {
     if (err_.empty()) err_ = "Enqueue: HIP call failed";
@@ -2194,14 +2212,14 @@ bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t
   S.n_files = n_files;
   S.has_fs = n_fullscan_rules_ > 0;
   t->slot = k;
-  t->cand_cap = cand_cap_;
+  t->cand_copy = n_copy;
   return true;
 }
 
-bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st, bool* rerun) {
+bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st, bool* rerun, std::string* err) {
   *rerun = false;
   if (t->slot < 0 || t->slot >= kSlots) {
-    err_ = "Collect: no ticket";
+    *err = "Collect: no ticket";
     return false;
   }
   Slot& S = slots_[t->slot];
@@ -2212,7 +2230,7 @@ bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st
   };
   const hipError_t e = WaitEvent(S.done);
   if (e != hipSuccess) {
-    err_ = std::string("Collect: ") + hipGetErrorString(e);
+    *err = std::string("Collect: ") + hipGetErrorString(e);
     release();
     return false;
   }
@@ -2222,7 +2240,9 @@ bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st
   st->bytes = S.n_bytes;
   st->files = S.n_files;
   const uint32_t* cnt = S.h_cnt;
-  if (cnt[8] || cnt[10] || cnt[3] || cnt[4] || cnt[1] > t->cand_cap) {  // an overflow: Run grows and rescans
+  for (uint32_t seen = cand_recent_.load(); cnt[1] > seen && !cand_recent_.compare_exchange_weak(seen, cnt[1]);) {
+  }
+  if (cnt[8] || cnt[10] || cnt[3] || cnt[4] || cnt[1] > t->cand_copy) {  // an overflow: Run grows and rescans
     *rerun = true;
     release();
     return true;
@@ -2284,7 +2304,7 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   fp.counters = d_counters_;
   const uint64_t f_tiles = (n_bytes + kFTile - 1) / kFTile;
   const uint32_t f_grid =
-      uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves, 256)));
+      uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((f_tiles + kScanWaves - 1) / kScanWaves, 256 * kFWgPerCu)));
   HIP_OK(hipEventRecord(ev[1], stream_));
   filter_kernel<<<f_grid, kScanThreads, 0, stream_>>>(fp);
   HIP_OK(hipGetLastError());

@@ -79,11 +79,31 @@ struct Cluster {
   double cost = 0;
 };
 
-double Cost(const B256* u) {
+// Window probability under the prior, with runs of one repeated non-letter
+// byte rated as runs: text repeats punctuation and digits ("-----", "=====",
+// "0000"), so each further copy of the same single byte counts as at least
+// kRepeatProb instead of the independent byte's probability.
+constexpr double kRepeatProb = 0.3;
+bool SameSingleNonLetter(const B256& a, const B256& b) {
+  int n = 0, x = -1;
+  for (int k = 0; k < 4; k++) {
+    if (a.w[k] != b.w[k]) return false;
+    n += __builtin_popcountll(a.w[k]);
+    if (a.w[k]) x = 64 * k + __builtin_ctzll(a.w[k]);
+  }
+  return n == 1 && !((x | 0x20) >= 'a' && (x | 0x20) <= 'z');
+}
+double WindowProb(const B256* u, int n) {
   double c = 1.0;
-  for (int s = 0; s < kFilterSlots; s++) c *= SetProb(u[s]);  // unused slots stay "any" (P = 1)
+  for (int s = 0; s < n; s++) {
+    double p = SetProb(u[s]);
+    if (s > 0 && SameSingleNonLetter(u[s], u[s - 1])) p = std::max(p, kRepeatProb);
+    c *= p;
+  }
   return c;
 }
+
+double Cost(const B256* u) { return WindowProb(u, kFilterSlots); }  // unused slots stay "any" (P = 1)
 
 }  // namespace
 
@@ -135,8 +155,9 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     size_t w = 0, wl = std::min<size_t>(m, S);
     double best = std::numeric_limits<double>::infinity();
     for (size_t s = 0; s + wl <= m; s++) {
-      double c = 1.0;
-      for (size_t q = s; q < s + wl; q++) c *= SetProb(ToB256(it.sets[q]));
+      B256 win[kFilterSlots];
+      for (size_t q = s; q < s + wl; q++) win[q - s] = ToB256(it.sets[q]);
+      const double c = WindowProb(win, int(wl));
       if (c < best) {
         best = c;
         w = s;

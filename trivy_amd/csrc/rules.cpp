@@ -9,6 +9,7 @@
 #include <array>
 #include <bitset>
 #include <deque>
+#include <functional>
 #include <map>
 #include <set>
 
@@ -730,6 +731,134 @@ std::vector<ByteSet> AfterSets(const std::vector<Node>& nodes, const std::vector
   return out;
 }
 
+// Byte sets at the first offsets after a literal, from a Glushkov position
+// automaton of the items after it (Alt branches and optional groups kept
+// apart, repeats unrolled up to the offsets asked for), so offset i's set is
+// the union of the reaches of the positions some path can be in after i bytes
+// -- e.g. after "aws" in aws_?(sec(ret)?)?_?(access)?_?key offset 1 allows
+// _ s a k e c, where the relaxed sequence of AfterSets allows every letter of
+// the optional words at each offset.  Still a superset filter: assertions are
+// ε, positions are exact ASCII sets (fold-only runes left to the fold kernel,
+// as ExactSet) or byte reaches, the sets stop after an offset that admits a
+// byte >= 0x80 (a multi-byte rune's continuation bytes would follow) or once
+// the match may have ended.  Empty when the expansion grows past its budget.
+std::vector<ByteSet> AfterSetsExact(const std::vector<Node>& nodes, const std::vector<int>& fol, size_t cap) {
+  struct Pos {
+    ByteSet reach;
+    std::vector<int> next;
+  };
+  std::vector<Pos> pos;
+  struct Frag {
+    std::vector<int> first, last;
+    bool nullable;
+  };
+  constexpr size_t kBudget = 4096;
+  const int kCopies = int(cap) + 1;  // repeats beyond this many copies only shape offsets >= cap
+  bool over = false;
+  auto link = [&](const std::vector<int>& from, const std::vector<int>& to) {
+    for (int a : from)
+      for (int b : to) pos[size_t(a)].next.push_back(b);
+  };
+  auto cat = [&](Frag a, const Frag& b) {
+    link(a.last, b.first);
+    Frag r;
+    r.first = a.first;
+    if (a.nullable) r.first.insert(r.first.end(), b.first.begin(), b.first.end());
+    r.last = b.last;
+    if (b.nullable) r.last.insert(r.last.end(), a.last.begin(), a.last.end());
+    r.nullable = a.nullable && b.nullable;
+    return r;
+  };
+  std::function<Frag(int)> build = [&](int i) -> Frag {
+    const Node& n = nodes[size_t(i)];
+    if (over) return Frag{{}, {}, true};
+    switch (n.op) {
+      case NodeOp::Empty:
+      case NodeOp::Assert: return Frag{{}, {}, true};
+      case NodeOp::NoMatch: return Frag{{}, {}, false};
+      case NodeOp::Class: {
+        if (pos.size() >= kBudget) {
+          over = true;
+          return Frag{{}, {}, true};
+        }
+        ByteSet b;
+        if (!ExactSet(n, &b)) b = ByteReach(n.ranges);
+        pos.push_back(Pos{b, {}});
+        const int p = int(pos.size()) - 1;
+        return Frag{{p}, {p}, false};
+      }
+      case NodeOp::Capture: return build(n.subs[0]);
+      case NodeOp::Cat: {
+        Frag r{{}, {}, true};
+        for (int s : n.subs) r = cat(r, build(s));
+        return r;
+      }
+      case NodeOp::Alt: {
+        Frag r{{}, {}, false};
+        for (int s : n.subs) {
+          Frag b = build(s);
+          r.first.insert(r.first.end(), b.first.begin(), b.first.end());
+          r.last.insert(r.last.end(), b.last.begin(), b.last.end());
+          r.nullable = r.nullable || b.nullable;
+        }
+        return r;
+      }
+      case NodeOp::Repeat: {
+        const int mn = std::min(n.min, kCopies);
+        const bool star = n.max < 0 || n.max - n.min > kCopies;
+        const int opt = star ? 0 : n.max - n.min;
+        Frag r{{}, {}, true};
+        for (int k = 0; k < mn; k++) r = cat(r, build(n.subs[0]));
+        for (int k = 0; k < opt; k++) {
+          Frag o = build(n.subs[0]);
+          o.nullable = true;
+          r = cat(r, o);
+        }
+        if (star) {
+          Frag o = build(n.subs[0]);
+          link(o.last, o.first);
+          o.nullable = true;
+          r = cat(r, o);
+        }
+        return r;
+      }
+    }
+    return Frag{{}, {}, true};
+  };
+  Frag seq{{}, {}, true};
+  for (int it : fol) seq = cat(seq, build(it));
+  std::vector<ByteSet> out;
+  if (over) return out;
+  std::vector<char> is_last(pos.size(), 0);
+  for (int p : seq.last) is_last[size_t(p)] = 1;
+  std::vector<char> act(pos.size(), 0);
+  for (int p : seq.first) act[size_t(p)] = 1;
+  bool ended = seq.nullable;  // the match may end at this offset
+  while (out.size() < cap && !ended) {
+    ByteSet set;
+    bool any = false;
+    for (size_t p = 0; p < pos.size(); p++)
+      if (act[p]) {
+        set |= pos[p].reach;
+        any = true;
+      }
+    if (!any || set.all() || set.none()) break;
+    out.push_back(set);
+    bool high = false;
+    for (int b = 0x80; b < 0x100 && !high; b++) high = set.test(size_t(b));
+    if (high) break;
+    std::vector<char> nx(pos.size(), 0);
+    for (size_t p = 0; p < pos.size(); p++) {
+      if (!act[p]) continue;
+      if (is_last[p]) ended = true;
+      for (int q : pos[p].next) nx[size_t(q)] = 1;
+    }
+    act.swap(nx);
+  }
+  while (!out.empty() && out.back().all()) out.pop_back();
+  return out;
+}
+
 // Mandatory fixed-width sets right before top-level item `k` (up to `cap`).
 std::vector<ByteSet> BeforeSets(const std::vector<Node>& nodes, const std::vector<int>& items, size_t k, size_t cap) {
   std::vector<ByteSet> out;  // reversed
@@ -1064,7 +1193,15 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
               if (b.none()) b.set();
             fi.sets.insert(fi.sets.end(), lit.begin(), lit.end());
             fi.lit_end = uint32_t(fi.sets.size());
+            // the tighter of the two lookahead computations, position by position
+            // (both are supersets of every match's bytes; the exact one stops
+            // early on non-ASCII sets, the relaxed one on ended fixed items)
             auto after = AfterSets(re->nodes(), best.follow[li], 16);
+            const auto exact = AfterSetsExact(re->nodes(), best.follow[li], 16);
+            for (size_t q = 0; q < exact.size(); q++) {
+              if (q < after.size()) after[q] &= exact[q];
+              else after.push_back(exact[q]);
+            }
             fi.sets.insert(fi.sets.end(), after.begin(), after.end());
             out->items.push_back(std::move(fi));
           }

@@ -309,6 +309,9 @@ bool SimpleLiteral(const std::string& src, std::string* lit, bool* begin, bool* 
   lit->clear();
   while (i < e) {
     const unsigned char c = static_cast<unsigned char>(src[i]);
+    // non-ASCII: Go's regexp matches runes (an invalid byte decodes to
+    // U+FFFD, which a literal EF BF BD matches), so keep the regex for these
+    if (c >= 0x80) return false;
     if (c == '\\') {
       if (i + 1 >= e) return false;
       const unsigned char d = static_cast<unsigned char>(src[i + 1]);
@@ -1061,23 +1064,25 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   {
     std::lock_guard<std::mutex> g(gpu_mu_[slot]);
     static const bool tickets = !std::getenv("TSG_TICKETS") || std::atoi(std::getenv("TSG_TICKETS")) != 0;
-    if (in.dev_arena && tickets && engine->Enqueue(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &ticket))
+    std::string enq_err;  // a failed Enqueue (no free ticket, or a HIP error) falls back to Run
+    if (in.dev_arena && tickets && engine->Enqueue(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &ticket,
+                                                   &enq_err))
       ok = true;  // collected below, after the lock is released
     else if (in.dev_arena)
       ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
     else
       ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
                            in.transform ? &tail : nullptr);
-    if (!ok) gpu_err = engine->error();
+    if (!ok && gpu_err.empty()) gpu_err = engine->error();
   }
   if (ticket.slot >= 0) {
     bool rerun = false;
-    ok = engine->Collect(&ticket, &cands, gst, &rerun);
+    ok = engine->Collect(&ticket, &cands, gst, &rerun, &gpu_err);
     if (ok && rerun) {  // a buffer overflowed: grow and rescan synchronously
       std::lock_guard<std::mutex> g(gpu_mu_[slot]);
       ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
+      if (!ok) gpu_err = engine->error();  // read under the engine's lock
     }
-    if (!ok) gpu_err = engine->error();
   }
   allow_thread.join();
   if (!ok) {
