@@ -124,10 +124,30 @@ def oracle_sample(C, sample_bytes, cores, tmpdir, cfg_path=None):
     return want, dt
 
 
-def cpu_baseline(C, sample_bytes, threads, cfg_path, want):
+def full_diff(gpu_res, cpu_res, n, chunk=4096):
+    """Every file [0, n) of two results compared byte for byte (their JSON text, findings and
+    Code lines included); returns (mismatching files, first mismatching index or None)."""
+    bad, first = 0, None
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        a, b = gpu_res.raw_text(lo, hi), cpu_res.raw_text(lo, hi)
+        if a == b:
+            continue
+        ja, jb = json.loads(a.decode("ascii")), json.loads(b.decode("ascii"))
+        for i, (x, y) in enumerate(zip(ja, jb)):
+            if x != y:
+                bad += 1
+                first = lo + i if first is None else first
+    return bad, first
+
+
+def cpu_baseline(C, sample_bytes, threads, cfg_path, want, gpu_res=None):
     """C++ restatement of the reference CPU algorithm (oracle/native/host_hooks.cpp tsg_cpuref_scan:
     scanner.go:377-463 -- per file and rule bytes.ToLower + Contains, whole-file Go-regexp FindAll,
-    the same tail) on the first files of the corpus, timed on `threads` host threads per entry."""
+    the same tail) on the first files of the corpus, timed on `threads` host threads per entry.
+    The restated reference is itself checked against the Python oracle on the oracle's sample
+    (`want`), and the GPU's findings (`gpu_res`, the timed run) are diffed against it on every
+    file of the sample."""
     import ctypes as c
     import numpy as np
     from oracle import hostlib
@@ -156,6 +176,14 @@ def cpu_baseline(C, sample_bytes, threads, cfg_path, want):
     nw = len(want)
     got = res.secrets([C.path(i) for i in range(nw)], lo=0)
     bad = sum(1 for i in range(nw) if got[i].to_dict() != want[i])
+    full = None
+    if gpu_res is not None:
+        t0 = time.time()
+        nbad, first = full_diff(gpu_res, res, n)
+        full = {"files": n, "bytes": int(offs[-1]), "findings": runs[0]["findings"], "mismatches": nbad,
+                "first_mismatch": C.path(first) if first is not None else None, "s": round(time.time() - t0, 2),
+                "reference": "tsg_cpuref_scan (restated reference CPU algorithm), itself 0-mismatch vs the "
+                             "Python oracle on the first %d files" % nw if bad == 0 else "tsg_cpuref_scan"}
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -171,7 +199,7 @@ def cpu_baseline(C, sample_bytes, threads, cfg_path, want):
                       "Go-regexp FindAll with the product's Go-semantics engine, same tail); %d findings"
                       % (n, int(offs[-1]) / 1e6, runs[0]["findings"]),
             "runs": runs, "cpu_model": cpu_model,
-            "parity_vs_oracle": {"files": nw, "mismatches": bad}}
+            "parity_vs_oracle": {"files": nw, "mismatches": bad}, "gpu_vs_cpuref_all_files": full}
 
 
 def measure_h2d(dev, gb=4.0):
@@ -217,7 +245,7 @@ KERNELS = [("chunk_map_kernel", "ms_chunkmap_kernel"), ("filter_kernel (K1)", "m
 WORKLOADS = {
     # (description, GB per GPU, CPU-baseline sample MB, oracle parity sample MB)
     "c2": ("builtin ruleset (87 rules) over a %g GB synthetic mixed-text corpus per MI355X (BASELINE configs[1])",
-           20.0, 64.0, 24.0),
+           20.0, 1000.0, 24.0),  # CPU baseline: BASELINE configs[0] (C1), 1 GB of the same generator
     "c5": ("%g GB per MI355X per step (1 TB over 8 GPUs) streamed host->HBM from a page-locked pool of "
            "mean-64-KiB files re-emitted with distinct ids, builtin rules (BASELINE configs[4])", 125.0, 64.0, 24.0),
     "c3": ("2,000 generated custom rules (trivy-secret.yaml) + 87 builtins over a %g GB synthetic corpus per "
@@ -225,6 +253,9 @@ WORKLOADS = {
     "c3u": ("C3 variant: 2,000 generated custom rules of which ~10 %% have no literal anchor (keyword-gated "
             "full scan) + 87 builtins over a %g GB synthetic corpus per MI355X (BASELINE configs[2], VERDICT r01 #7)",
             8.0, 2.0, 0.4),
+    "c3f": ("C3 variant: 2,000 generated custom rules of which ~5 %% are bare class runs ((?i)[a-z0-9/+]{32..48}, "
+            "keyword-gated, no literal or rare class run: fullscan_kernel) + 87 builtins over a %g GB synthetic corpus "
+            "per MI355X (BASELINE configs[2], VERDICT r02 #6)", 8.0, 2.0, 0.4),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
            "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0, 0.0),
 }
@@ -340,15 +371,16 @@ def main():
     torch.cuda.set_device(local)
     numa_node = _bind_numa(local) if args.numa == "gpu" else None
 
-    from trivy_amd import corpus
+    from trivy_amd import corpus, shard
     import trivy_amd.secret as secret
 
     tmpdir = os.environ.get("TMPDIR", "/tmp")
     cfg_path = None
     t_gen = time.time()
     C = layer = None
-    if args.workload in ("c3", "c3u"):
-        y, samples = corpus.c3_rules(unanchored_share=0.1 if args.workload == "c3u" else 0.0)
+    if args.workload in ("c3", "c3u", "c3f"):
+        y, samples = corpus.c3_rules(unanchored_share=0.1 if args.workload == "c3u" else 0.0,
+                                     fullscan_share=0.05 if args.workload == "c3f" else 0.0)
         cfg_path = os.path.join(tmpdir, "tsg-bench-c3-%d.yaml" % rank)
         with open(cfg_path, "w") as f:
             f.write(y)
@@ -435,6 +467,19 @@ def main():
     t0 = time.time()
     stats = []
     run_steps(args.steps, stats)
+    gathered = None
+    if dist is not None and layer is None:
+        # host-side findings gather (north_star): the job's result -- every rank's
+        # findings of its shard -- merged on rank 0 in AnalysisResult.Sort order, inside the timed region
+        tg = time.time()
+        rec = last_res[0].records()
+        pth = C.path_buf.reshape(-1, corpus.PATH_STRIDE)[rec["file"] % C.n_files].view("S%d" % corpus.PATH_STRIDE).ravel()
+        merged = shard.gather_records(rec, pth, [r.ID for r in sc.Rules])
+        if merged is not None:
+            gathered = {"findings": int(len(merged["records"])), "ranks": world,
+                        "files": int(len(np.unique(merged["paths"]))), "ms": round((time.time() - tg) * 1e3, 2),
+                        "note": "once per job (the steps re-scan the same shards): tsg_result_records of every rank "
+                                "gathered to rank 0 (gloo) and put in AnalysisResult.Sort order"}
     torch.cuda.synchronize()
     barrier()
     dt = time.time() - t0
@@ -580,7 +625,8 @@ def main():
                 parity = parity_block(C, res_timed, want)
                 if ingest is not None:
                     ingest["parity"] = parity_block(C, last_res[0], want)
-                cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), [cores, 5], cfg_path, want)
+                cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), [cores, 5], cfg_path, want,
+                                   gpu_res=res_timed)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
                 cpu = cpu_baseline_layer(sample, cores, tmpdir)
@@ -597,7 +643,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic generator, seed 0x5EC2E7+rank; planted builtin-rule secrets%s)"
-                    % (" and generated-rule samples" if args.workload in ("c3", "c3u") else ""),
+                    % (" and generated-rule samples" if args.workload in ("c3", "c3u", "c3f") else ""),
             "config": dict({"workload": wl_desc % args.gb, "workload_id": args.workload,
                             "parallelism": "files sharded, dp%d" % world,
                             "rules_compile_s": round(t_compile, 2),
@@ -606,6 +652,7 @@ def main():
             "ingest": ingest,
             "cpu_baseline": cpu,
             "parity": parity,
+            "gather": gathered,
             "breakdown_ms": breakdown,
             "host_cpu": host_cpu,
             "counts": counts,
@@ -615,6 +662,10 @@ def main():
         if ingest is not None and "parity" in ingest and ingest["parity"]["mismatches"]:
             sys.exit("parity (ingest leg): %d of %d sample files differ from the oracle (first: %s)"
                      % (ingest["parity"]["mismatches"], ingest["parity"]["files"], ingest["parity"]["first_mismatch"]))
+        full = (cpu or {}).get("gpu_vs_cpuref_all_files")
+        if full and full["mismatches"]:
+            sys.exit("parity: %d of %d files of the CPU-baseline sample differ from the restated reference "
+                     "(first: %s)" % (full["mismatches"], full["files"], full["first_mismatch"]))
         if parity is not None and parity["mismatches"]:
             sys.exit("parity: %d of %d sample files differ from the oracle (first: %s)"
                      % (parity["mismatches"], parity["files"], parity["first_mismatch"]))

@@ -69,6 +69,11 @@ const char* tsg_debug_rule_anchor(const tsg_compiled* c, uint32_t i);
  * scanners) and the CPU reference scan are NOT in libtsg.so: they live in the
  * oracle's library (oracle/native/tsg_oracle.h, oracle/build/libtsg_host.so). */
 
+/* Host workers the process-wide pool would start now (TSG_POOL_THREADS unset):
+ * the affinity mask, capped by the cgroup quota, shared by LOCAL_WORLD_SIZE
+ * ranks (or TSG_POOL_SHARE processes), minus the per-process reserve. */
+int tsg_debug_pool_budget(void);
+
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);
 

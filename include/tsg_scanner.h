@@ -113,6 +113,20 @@ typedef struct tsg_line {
 } tsg_line;
 int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out);
 
+/* Compact record of every finding, in file then finding order: the unit a
+ * multi-process (one rank per GPU) job gathers to its merging rank, where
+ * the findings are put in AnalysisResult.Sort order (pkg/fanal/analyzer/
+ * analyzer.go:225-234) by the file paths the caller holds.  digest is a
+ * 64-bit FNV-1a over the finding's Match and its Code lines (number, flags,
+ * content), so the merged set can be compared without the text.  Returns the
+ * record count; writes up to cap of them. */
+typedef struct tsg_record {
+  uint32_t file, rule_index;
+  int64_t start_line, end_line;
+  uint64_t digest;
+} tsg_record;
+uint64_t tsg_result_records(const tsg_result* r, tsg_record* out, uint64_t cap);
+
 /* Whole batch as JSON ([{"kind":..,"findings":[..]}...], Go field names). */
 int tsg_result_json(const tsg_result* r, const char** json, uint64_t* len);
 /* Files [lo, hi) only (same format; the text stays valid until the next json call on r). */

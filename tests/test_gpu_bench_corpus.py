@@ -107,3 +107,91 @@ def test_bench_corpus_c3_matches_oracle(tmp_path):
     want = _oracle([(i, C.path(i), C.content(i)) for i in chosen], str(cfg))
     n = _check(C, res, chosen, want)
     assert n > 20
+
+
+def _cpuref(C, n_threads=16, cfg_path=None):
+    """tsg_cpuref_scan (oracle/native/host_hooks.cpp, the restated reference CPU algorithm) over
+    every file of C: the full-size completeness check (the Python oracle checks samples)."""
+    import ctypes as c
+    from oracle import hostlib
+    import trivy_amd.secret as secret
+    from trivy_amd.secret.scanner import ScanResult, _CBatch
+    L = hostlib.lib()
+    sc = secret.NewScanner(secret.ParseConfig(cfg_path) if cfg_path else None, lib=L, host_only=True)
+    offs = np.ascontiguousarray(C.offsets)
+    batch = _CBatch(C.n_files, C.arena.ctypes.data, offs.ctypes.data, None, None, C.path_ptrs.ctypes.data,
+                    None, None)
+    h = c.c_void_p()
+    assert L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), n_threads, c.byref(h)) == 0
+    return ScanResult(sc, h)
+
+
+def test_c5_pool_streamed_twice_matches_oracle(monkeypatch):
+    """BASELINE configs[4] (C5): a page-locked pool of mean-64-KiB files (size_scale 2.6) streamed
+    host->HBM through the double-buffered ingest (RunHost, 16-MiB chunks) twice in flight, as the
+    C5 bench re-emits it.  Both emissions: every file byte-identical to the restated reference
+    CPU scan, and a sample field for field vs the oracle."""
+    from bench import full_diff
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    monkeypatch.setenv("TSG_INGEST_CHUNK_MB", "16")
+    C = corpus.generate(int(72e6), seed=corpus.SEED + 5, size_scale=2.6)
+    assert C.n_bytes / C.n_files > 40e3
+    unreg = secret.HostRegister(C.arena)
+    try:
+        s = secret.NewScanner(None)
+        p1 = s.scan_arena_async(C.arena, C.offsets, C.path_ptrs)
+        p2 = s.scan_arena_async(C.arena, C.offsets, C.path_ptrs)
+        r1, r2 = p1.wait(), p2.wait()
+    finally:
+        unreg()
+    assert r1.stats()["h2d_chunks"] >= 4
+    ref = _cpuref(C)
+    for r in (r1, r2):
+        bad, first = full_diff(r, ref, C.n_files)
+        assert bad == 0, (bad, C.path(first))
+    chosen, big, _, _ = _select(C, random.Random(5), 2e6)
+    want = _oracle([(i, C.path(i), C.content(i)) for i in chosen])
+    assert _check(C, r2, chosen, want) > 5
+
+
+def test_c2_corpus_every_file_matches_cpuref():
+    """Candidate completeness at size: every file of a 256 MB C2 corpus (K1 -> K2 -> verify
+    superset, exact host pass) byte-identical to the restated reference CPU scan."""
+    from bench import full_diff
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    C = corpus.generate(int(256e6), seed=corpus.SEED + 13)
+    res = secret.NewScanner(None).scan_arena(C.arena, C.offsets, C.path_ptrs)
+    ref = _cpuref(C)
+    bad, first = full_diff(res, ref, C.n_files)
+    assert bad == 0, (bad, C.path(first) if first is not None else None)
+    assert res.stats()["findings"] > 500
+
+
+def test_c3f_fullscan_rules_every_file_matches_cpuref(tmp_path):
+    """C3f: 2,000 generated rules of which ~5 % are bare, keyword-gated
+    class runs ((?i)[a-z0-9/+]{32..48}) with neither a literal nor a rare class run, so every file
+    holding a rule's keyword goes through fullscan_kernel.  Every file vs the restated reference
+    CPU scan, a sample vs the oracle; the full-scan path must actually run."""
+    from bench import full_diff
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    y, samples = corpus.c3_rules(fullscan_share=0.05)
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(y)
+    C = corpus.generate_c3(int(48e6), samples, seed=corpus.SEED + 17, secrets_per_byte=1.0 / 16384)
+    s = secret.NewScanner(secret.ParseConfig(str(cfg)))
+    res = s.scan_arena(C.arena, C.offsets, C.path_ptrs)
+    st = res.stats()
+    assert st["fullscan_pairs"] > 0
+    ref = _cpuref(C, cfg_path=str(cfg))
+    bad, first = full_diff(res, ref, C.n_files)
+    assert bad == 0, (bad, C.path(first) if first is not None else None)
+    rng = random.Random(6)
+    sizes = np.diff(C.offsets.astype(np.int64))
+    withkw = [i for i in range(C.n_files) if sizes[i] < 400000 and b"kwf" in C.content(i)]
+    small = [i for i in range(C.n_files) if sizes[i] < 200000]
+    chosen = sorted(set(withkw[:40]) | set(rng.sample(small, 60)))
+    want = _oracle([(i, C.path(i), C.content(i)) for i in chosen], str(cfg))
+    assert _check(C, res, chosen, want) > 10

@@ -84,3 +84,57 @@ def test_submit_without_gpu_reports_error():
             assert "no GPU engine" in str(e)
         else:
             raise AssertionError("scan without a GPU engine succeeded")
+
+
+def _budget_child(q, cpus, env):
+    import os
+    os.environ.pop("TSG_POOL_SHARE", None)
+    os.environ.pop("LOCAL_WORLD_SIZE", None)
+    os.environ.update(env)
+    os.sched_setaffinity(0, cpus)
+    from trivy_amd import _lib
+    q.put(_lib.lib().tsg_debug_pool_budget())
+
+
+def _budget(cpus, **env):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_budget_child, args=(q, cpus, env))
+    p.start()
+    v = q.get(timeout=120)
+    p.join(60)
+    return v
+
+
+def test_pool_budget_follows_affinity_and_ranks():
+    """HostPool's default size (parallel.h PoolBudget): the affinity mask, split over the ranks
+    sharing it (LOCAL_WORLD_SIZE spread over the node, or TSG_POOL_SHARE), minus the reserve --
+    not the whole container per process (8 ranks would otherwise oversubscribe 8x)."""
+    import os
+    online = os.cpu_count()
+    allc = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+
+    def want(aff, share, ranks):
+        c = aff / share
+        if quota:
+            c = min(c, quota / ranks)
+        c = max(1, int(c))
+        return max(1, c - (4 if c >= 16 else max(1, c // 4)))
+
+    four = set(allc[:4])
+    assert _budget(four) == want(4, 1, 1)
+    assert _budget(four, TSG_POOL_SHARE="2") == want(4, 2, 2)
+    if len(allc) == online and online >= 8:
+        # 2 ranks on all CPUs: each gets half
+        assert _budget(set(allc), LOCAL_WORLD_SIZE="2") == want(online, 2, 2)
+        # 8 ranks, this one bound to half the CPUs: ~4 ranks share the half
+        half = set(allc[:online // 2])
+        assert _budget(half, LOCAL_WORLD_SIZE="8") == want(online // 2, max(1, 8 * (online // 2) / online), 8)
+    assert _budget({allc[0]}) == 1

@@ -42,7 +42,7 @@ def _assemble(cfg):
     return rules, allow, cfg.ExcludeBlock.Regexes
 
 
-def host_tail_scan(cfg, files):
+def host_tail_scan(cfg, files, raw=False):
     L = hostlib.lib()
     _declare(L)
     rules, allow, exclude = _assemble(cfg)
@@ -59,7 +59,8 @@ def host_tail_scan(cfg, files):
     h = c.c_void_p()
     if L.tsg_debug_host_tail(c.byref(cg.g), c.byref(batch), c.byref(h)) != 0:
         raise RuntimeError(hostlib.last_error())
-    return ScanResult(_Owner(L), h).secrets([p for p, _ in files])
+    res = ScanResult(_Owner(L), h)
+    return res if raw else res.secrets([p for p, _ in files])
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] + "|" + c["config"] for c in CASES])
@@ -254,3 +255,32 @@ def test_allow_path_literal_fast_path(tmp_path):
         assert g.to_dict() == want, p
         n_allowed += not want["Findings"]
     assert n_allowed >= 8
+
+
+def _fnv(h, b):
+    for x in b:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_result_records_match_findings():
+    """tsg_result_records (the multi-rank gather unit): one record per finding, in file order,
+    with the rule index, lines and the documented FNV-1a digest of Match + Code lines."""
+    import struct
+    from trivy_amd.secret import builtin_rules
+    files = [("d%03d/%s" % (i, p), b.replace(b"\r", b"")) for i, (p, b) in enumerate(make_corpus(23, 120))]
+    res = host_tail_scan(None, files, raw=True)
+    rec = res.records()
+    got = res.secrets([p for p, _ in files])
+    ids = [r.ID for r in builtin_rules()]
+    want = []
+    for i, s in enumerate(got):
+        for f in s.Findings or []:
+            h = _fnv(0xcbf29ce484222325, f.Match.encode("utf-8", "surrogateescape"))
+            for ln in f.Code.Lines or []:
+                h = _fnv(h, struct.pack("<q", ln.Number) + bytes([ln.IsCause, ln.FirstCause, ln.LastCause]))
+                h = _fnv(h, ln.Content.encode("utf-8", "surrogateescape"))
+            want.append((i, f.RuleID, f.StartLine, f.EndLine, h))
+    assert len(want) > 5
+    assert [(int(r["file"]), ids[r["rule"]], int(r["start_line"]), int(r["end_line"]), int(r["digest"]))
+            for r in rec] == want

@@ -153,3 +153,43 @@ def test_two_scanners_one_process_concurrent():
         s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
     assert [s.to_dict() for s in got.Secrets] == want.Secrets
     assert len(got.Secrets) > 5
+
+
+def _rank_main_records(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from trivy_amd.secret.scanner import RECORD_DTYPE
+        from trivy_amd.shard import gather_records
+        rng = np.random.default_rng(100 + rank)
+        n = 50
+        rec = np.zeros(n, dtype=RECORD_DTYPE)
+        rec["file"] = rng.integers(0, 20, n)
+        rec["rule"] = rng.integers(0, 3, n)
+        rec["start_line"] = rng.integers(1, 40, n)
+        rec["end_line"] = rec["start_line"]
+        rec["digest"] = rng.integers(0, 2 ** 62, n)
+        paths = np.array([("r%d/f%02d" % (rank % 2, f)).encode() for f in rec["file"]], dtype="S16")
+        merged = gather_records(rec, paths, ["zeta", "alpha", "mid"])
+        if rank == 0:
+            np.savez(out_path, rec=merged["records"], paths=merged["paths"], ranks=merged["ranks"])
+        else:
+            assert merged is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_records_gather_sorted(tmp_path):
+    """shard.gather_records (bench.py's timed gather at N>1): every rank's records reach rank 0
+    in FilePath, RuleID, StartLine order (analyzer.go:225-234)."""
+    out = tmp_path / "merged.npz"
+    mp.start_processes(_rank_main_records, args=(2, _free_port(), str(out)), nprocs=2, join=True,
+                       start_method="spawn")
+    d = np.load(out)
+    rec, paths = d["rec"], d["paths"]
+    assert len(rec) == 100
+    ids = ["zeta", "alpha", "mid"]
+    keys = [(p, ids[r], int(s)) for p, r, s in zip(paths, rec["rule"], rec["start_line"])]
+    assert keys == sorted(keys)

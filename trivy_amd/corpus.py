@@ -79,7 +79,7 @@ def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=Non
 _C3_OPS = ["=", ">", ":=", "||:", "<=", "=>", ":"]
 
 
-def c3_rules(n_rules=2000, seed=SEED, planted_share=0.10, unanchored_share=0.0):
+def c3_rules(n_rules=2000, seed=SEED, planted_share=0.10, unanchored_share=0.0, fullscan_share=0.0):
     """A trivy-secret.yaml text with n_rules custom rules and planted sample matches.
 
     60 %: generic assignment form (secret group), 40 %: literal-prefix token form;
@@ -88,15 +88,31 @@ def c3_rules(n_rules=2000, seed=SEED, planted_share=0.10, unanchored_share=0.0):
     unanchored_share > 0 (the "C3u" variant) that share of
     the rules has no literal at a bounded offset -- a token of classes only,
     gated by its keyword -- so the engine full-scans the files where the gate is
-    open.  Returns (yaml_text, [sample bytes])."""
+    open.  With fullscan_share > 0 (the "C3f" variant) that
+    share of the rules is a bare class run, (?i)[a-z0-9/+]{L} (L in [32, 48]),
+    gated by its own keyword: neither a literal nor a rare class run anchors it
+    (rules.cpp ExtractClassRun: a 6-window of that class is far above 1e-5),
+    so every file holding the keyword goes through fullscan_kernel.  Returns
+    (yaml_text, [sample bytes])."""
     import random
     rng = random.Random(seed ^ 0xC3)
     alnum = "abcdefghijklmnopqrstuvwxyz0123456789"
     lines = ["rules:"]
     samples = []
     urng = random.Random(seed ^ 0xC3A)
+    frng = random.Random(seed ^ 0xC3F)
     for i in range(n_rules):
         L = rng.randint(16, 64)
+        if fullscan_share and frng.random() < fullscan_share:
+            kw = "kwf%04d" % i
+            n = frng.randint(32, 48)
+            lines += ["  - id: c3-fullscan-%04d" % i, "    category: Generated", "    title: Full-scan rule %d" % i,
+                      "    severity: LOW", "    regex: '(?i)[a-z0-9/+]{%d}'" % n, "    keywords: [%s]" % kw]
+            if frng.random() < 0.5:
+                for _ in range(2):
+                    tok = "".join(frng.choice(alnum + "/+") for _ in range(n))
+                    samples.append(("%s: %s" % (kw, tok)).encode())
+            continue
         if unanchored_share and urng.random() < unanchored_share:
             kw = "kwu%04d" % i
             rx = r"(?i)\b[g-z]{3}[0-9]{3}[._-][a-z0-9]{%d}\b" % (L // 2)

@@ -6,6 +6,7 @@
 #include <string>
 
 #include "goregex.h"
+#include "parallel.h"
 
 namespace tsg {
 extern std::atomic<int> g_regex_engine;
@@ -53,4 +54,6 @@ int64_t tsg_go_bytes_to_lower(const uint8_t* s, uint64_t n, uint8_t* out, uint64
   std::memcpy(out, l.data(), l.size() < out_cap ? l.size() : out_cap);
   return int64_t(l.size());
 }
+
+int tsg_debug_pool_budget(void) { return tsg::PoolBudget(); }
 }

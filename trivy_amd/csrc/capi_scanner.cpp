@@ -316,6 +316,34 @@ int tsg_result_finding(const tsg_result* r, uint32_t file, uint32_t k, tsg_findi
   return 0;
 }
 
+uint64_t tsg_result_records(const tsg_result* r, tsg_record* out, uint64_t cap) {
+  uint64_t n = 0;
+  const auto& fs = r->files;
+  for (size_t i = 0; i < fs.found_files.size(); i++) {
+    const auto& v = fs.found[i];
+    for (const auto& f : v.f) {
+      if (n < cap) {
+        uint64_t h = 0xcbf29ce484222325ull;
+        auto mix = [&h](const void* p, size_t k) {
+          const uint8_t* b = static_cast<const uint8_t*>(p);
+          for (size_t q = 0; q < k; q++) h = (h ^ b[q]) * 0x100000001b3ull;
+        };
+        mix(v.text.data() + f.match_off, f.match_len);
+        for (uint32_t l = f.line_lo; l < f.line_hi; l++) {
+          const auto& ln = v.lines[l];
+          const uint8_t fl[3] = {uint8_t(ln.is_cause), uint8_t(ln.first_cause), uint8_t(ln.last_cause)};
+          mix(&ln.number, sizeof(ln.number));
+          mix(fl, 3);
+          mix(v.text.data() + ln.off, ln.len);
+        }
+        out[n] = tsg_record{fs.found_files[i], f.rule, f.start_line, f.end_line, h};
+      }
+      n++;
+    }
+  }
+  return n;
+}
+
 int tsg_result_line(const tsg_result* r, uint32_t file, uint32_t k, uint32_t line, tsg_line* out) {
   const auto* v = file < r->files.kind.size() ? r->files.Findings(file) : nullptr;
   if (!v || k >= v->size()) return -1;

@@ -5,6 +5,7 @@
 // share measured 1.4x slower).
 #pragma once
 #include <pthread.h>
+#include <sched.h>
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -43,13 +44,43 @@ struct PoolJob {
   }
 };
 
+// Host CPUs this process may use for its pool: its affinity mask (after a
+// NUMA binding, the node's CPUs), capped by the cgroup CPU quota, shared with
+// the other processes of the job on this node -- LOCAL_WORLD_SIZE ranks
+// (torchrun) spread over the node's CPUs, so ~LOCAL_WORLD_SIZE x mask/online
+// of them share this mask, and the container's quota is split LOCAL_WORLD_SIZE
+// ways -- or TSG_POOL_SHARE processes when set.  Minus the per-process
+// reserve (the callers, the GPU-driving thread and the allow-path pass run
+// beside the pool; going over a quota stalls every thread for the rest of the
+// period: on a 16-CPU box 12 workers measured 12% above 15).
+inline int PoolBudget() {
+  int aff = 0, online = int(std::thread::hardware_concurrency());
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) aff = CPU_COUNT(&set);
+  if (online <= 0) online = 16;
+  if (aff <= 0 || aff > online) aff = online;
+  double ranks = 1.0;  // processes of this job on this node
+  if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, std::atoi(e));
+  double sharing = std::max(1.0, ranks * double(aff) / double(online));  // ranks on this mask
+  if (const char* e = std::getenv("TSG_POOL_SHARE")) sharing = ranks = std::max(1.0, std::atof(e));
+  double cpus = double(aff) / sharing;
+  long q = 0, per = 0;
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    if (std::fscanf(f, "%ld %ld", &q, &per) != 2) q = per = 0;  // "max 100000": no quota
+    std::fclose(f);
+  }
+  if (q > 0 && per > 0) cpus = std::min(cpus, double(q) / double(per) / ranks);
+  const int c = std::max(1, int(cpus));
+  const int reserve = c >= 16 ? 4 : std::max(1, c / 4);
+  return std::max(1, c - reserve);
+}
+
 class HostPool {
  public:
-  // TSG_POOL_THREADS workers.  Default: under a cgroup CPU quota of Q CPUs,
-  // Q - 4 (the callers, the GPU-driving thread and the allow-path pass run
-  // beside the pool; going over the quota stalls every thread for the rest
-  // of the period: on a 16-CPU box 12 workers measured 12% above 15);
-  // without a quota 15 (16 cores with the calling thread).
+  // TSG_POOL_THREADS workers; default PoolBudget() (12 on the 16-CPU-quota
+  // one-GPU box; 12 per rank for 8 ranks sharing a 128-CPU quota; 15 with 16
+  // cores and no quota).
   static HostPool& Get() {
     static HostPool* p = new HostPool();  // never destroyed: workers may be parked at exit
     return *p;
@@ -73,7 +104,7 @@ class HostPool {
  private:
   HostPool() {
     const char* e = std::getenv("TSG_POOL_THREADS");
-    int n = e ? std::atoi(e) : DefaultWorkers();
+    int n = e ? std::atoi(e) : PoolBudget();
     if (n < 0) n = 0;
     for (int k = 0; k < n; k++) {
       workers_.emplace_back([this] {
@@ -82,16 +113,6 @@ class HostPool {
       });
       workers_.back().detach();
     }
-  }
-
-  static int DefaultWorkers() {
-    long q = 0, per = 0;
-    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
-      if (std::fscanf(f, "%ld %ld", &q, &per) != 2) q = per = 0;  // "max 100000": no quota
-      std::fclose(f);
-    }
-    if (q > 0 && per > 0) return std::max(1, int(q / per) - 4);
-    return 15;
   }
 
   void Loop() {

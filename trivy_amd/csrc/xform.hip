@@ -7,11 +7,17 @@
 //   kind 2  utils.ExtractPrintableBytes (pkg/fanal/utils/utils.go:128-160):
 //           runs of more than 4 unicode.IsPrint bytes, each followed by '\n'
 //           (.pyc binaries, secret.go:112-117)
-// Three launches per chunk: lengths (one wave per file), an exclusive scan of
-// the lengths into the transformed offsets (hipcub), the compaction (one wave
-// per file, 1-KiB tiles: per-lane kept-byte counts, a wave prefix sum, byte
-// stores at the packed positions).  A gather packs chosen files of the
-// transformed arena for the host's exact pass.
+// Three launches per chunk: lengths (one wave per file: SWAR '\r' counts over
+// 16-B loads, or the printable-run plan), an exclusive scan of the lengths
+// into the transformed offsets (hipcub), the copy (one wave per file).  Files
+// that keep every byte -- all of a layer but its CRLF files and .pyc binaries
+// -- are moved as 16-B-aligned destination blocks, each lane funnel-shifting
+// the two aligned source blocks around its block by the file's (uniform)
+// source/destination misalignment: coalesced 16-B loads and stores, byte
+// stores only in a file's first and last block (shared with the neighbouring
+// files' waves).  CRLF files compact 1 KiB per step (per-lane kept-byte
+// counts, a wave prefix sum).  A gather packs chosen files of the transformed
+// arena for the host's exact pass with the same shifted block copy.
 #include "xform.h"
 
 #include <hipcub/hipcub.hpp>
@@ -26,6 +32,64 @@ __device__ __forceinline__ uint4 xload16(const uint8_t* p) { return *reinterpret
 __device__ __forceinline__ uint32_t xbyte(const uint4& v, uint32_t i) {
   const uint32_t w = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
   return (w >> (8 * (i & 3))) & 0xFFu;
+}
+
+// Bytes of the word at arena position wp that lie in [a, b), as a byte mask.
+__device__ __forceinline__ uint32_t byte_mask(uint64_t wp, uint64_t a, uint64_t b) {
+  const uint32_t lo = a > wp ? uint32_t(a - wp < 4 ? a - wp : 4) : 0u;  // bytes before a
+  const uint32_t hi = b > wp ? uint32_t(b - wp < 4 ? b - wp : 4) : 0u;  // bytes before b
+  const uint32_t mhi = hi >= 4 ? ~0u : (1u << (8 * hi)) - 1u;
+  const uint32_t mlo = lo >= 4 ? 0u : ~((1u << (8 * lo)) - 1u);
+  return mhi & mlo;
+}
+
+// '\r' bytes of w among the bytes of mask m: x = w ^ 0x0D.. is zero exactly
+// in CR bytes (forced non-zero outside m); bit 7 of ((x & 0x7F..) + 0x7F..) | x
+// marks the non-zero bytes.
+__device__ __forceinline__ uint32_t cr_count4(uint32_t w, uint32_t m) {
+  const uint32_t x = (w ^ 0x0D0D0D0Du) | ~m;
+  const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+  return 4u - uint32_t(__popc(nz));
+}
+
+// dst [d, d + n) = src [s, s + n) for one wave (see the file comment).  src
+// has 16 readable bytes past s + n; out is 16-B aligned.
+__device__ void copy_shifted(const uint8_t* __restrict__ src, uint64_t s, uint8_t* __restrict__ out, uint64_t d,
+                             uint64_t n, uint32_t lane) {
+  if (n == 0) return;
+  const uint64_t e = d + n;
+  const uint32_t k = uint32_t((s - d) & 15);  // source byte offset of every aligned destination block (uniform)
+  const uint32_t q = k >> 2, r = k & 3;
+  for (uint64_t y0 = (d & ~uint64_t(15)) + 16 * uint64_t(lane); y0 < e; y0 += 1024) {
+    if (y0 >= d && y0 + 16 <= e) {
+      const uint64_t sa = (s + (y0 - d)) & ~uint64_t(15);
+      const uint4 A = xload16(src + sa), B = xload16(src + sa + 16);
+      const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+      uint32_t o[4];
+      switch (q) {  // wave-uniform
+        case 0:
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], r);
+          break;
+        case 1:
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(w[i + 2], w[i + 1], r);
+          break;
+        case 2:
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(w[i + 3], w[i + 2], r);
+          break;
+        default:
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(w[i + 4], w[i + 3], r);
+          break;
+      }
+      *reinterpret_cast<uint4*>(out + y0) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {  // the file's first / last block: only its own bytes
+      const uint64_t lo = y0 > d ? y0 : d, hi = y0 + 16 < e ? y0 + 16 : e;
+      for (uint64_t y = lo; y < hi; y++) out[y] = src[s + (y - d)];
+    }
+  }
 }
 
 // unicode.IsPrint(rune(b)) of a byte (Latin-1): graphic or ASCII space; not U+00A0, U+00AD
@@ -215,8 +279,9 @@ __global__ __launch_bounds__(kXThreads) void xform_len_kernel(const uint8_t* __r
       uint32_t cr = 0;
       for (uint64_t blk = (a & ~uint64_t(15)) + 16 * lane; blk < b; blk += 1024) {
         const uint4 v = xload16(raw + blk);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (uint32_t i = 0; i < 16; i++) cr += (blk + i >= a && blk + i < b && xbyte(v, i) == '\r') ? 1u : 0u;
+        for (uint32_t q = 0; q < 4; q++) cr += cr_count4(w[q], byte_mask(blk + 4 * q, a, b));
       }
       out -= wave_sum(cr);
     } else if (k == 2) {
@@ -244,6 +309,10 @@ __global__ __launch_bounds__(kXThreads) void xform_copy_kernel(const uint8_t* __
     if (k == 2) {
       pyc_plan(raw + a, b - a, lane, plan);
       pyc_write(raw + a, lane, plan, dst);
+      continue;
+    }
+    if (k != 1 || xoff[f + 1] - xoff[f] == b - a) {  // every byte kept: the shifted block copy
+      copy_shifted(raw, a, out, xoff[f], b - a, lane);
       continue;
     }
     uint64_t written = 0;
@@ -277,8 +346,7 @@ __global__ __launch_bounds__(kXThreads) void gather_kernel(const uint8_t* __rest
   for (uint32_t i = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); i < n; i += waves) {
     const uint32_t f = files[i];
     const uint64_t a = xoff[f], len = xoff[f + 1] - a;
-    uint8_t* d = dst + dst_off[i];
-    for (uint64_t j = lane; j < len; j += 64) d[j] = src[a + j];
+    copy_shifted(src, a, dst, dst_off[i], len, lane);
   }
 }
 

@@ -78,6 +78,9 @@ def _declare(L):
     L.tsg_result_json_range.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.POINTER(c.c_void_p),
                                         c.POINTER(c.c_uint64)]
     L.tsg_result_stats.argtypes = [c.c_void_p, c.POINTER(_CStats)]
+    if hasattr(L, "tsg_result_records"):
+        L.tsg_result_records.argtypes = [c.c_void_p, c.c_void_p, c.c_uint64]
+        L.tsg_result_records.restype = c.c_uint64
     L.tsg_scanner_table_info.argtypes = [c.c_void_p, c.POINTER(_CTableInfo)]
     L.tsg_scanner_rule_anchor.argtypes = [c.c_void_p, c.c_uint32]
     L.tsg_scanner_rule_anchor.restype = c.c_char_p
@@ -332,6 +335,10 @@ class PendingScan:
         return ScanResult(self._sc, r)
 
 
+RECORD_DTYPE = np.dtype([("file", "<u4"), ("rule", "<u4"), ("start_line", "<i8"), ("end_line", "<i8"),
+                         ("digest", "<u8")])  # tsg_record
+
+
 class ScanResult:
     def __init__(self, scanner, h):
         self._sc = scanner
@@ -355,6 +362,24 @@ class ScanResult:
         elif self._sc._L.tsg_result_json_range(self._h, lo, hi, c.byref(p), c.byref(n)) != 0:
             raise IndexError((lo, hi))
         return json.loads(c.string_at(p, n.value).decode("ascii"))
+
+    def raw_text(self, lo, hi) -> bytes:
+        """The JSON text of files [lo, hi) (tsg_result_json_range), unparsed: byte-for-byte
+        comparisons of two results."""
+        p = c.c_void_p()
+        n = c.c_uint64()
+        if self._sc._L.tsg_result_json_range(self._h, lo, hi, c.byref(p), c.byref(n)) != 0:
+            raise IndexError((lo, hi))
+        return c.string_at(p, n.value)
+
+    def records(self) -> np.ndarray:
+        """One compact record per finding (tsg_result_records): file, rule index, lines, digest."""
+        L = self._sc._L
+        n = L.tsg_result_records(self._h, None, 0)
+        out = np.empty(n, dtype=RECORD_DTYPE)
+        if n:
+            L.tsg_result_records(self._h, out.ctypes.data, n)
+        return out
 
     def secrets(self, paths, lo=None) -> List[Secret]:
         """types.Secret per file (files [lo, lo + len(paths)) when lo is given)."""

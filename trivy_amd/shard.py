@@ -106,3 +106,27 @@ def scan_devices(files: Sequence[Tuple[str, bytes]], scanners: Sequence) -> Anal
                 out.Merge(AnalysisResult(Secrets=[s]))
     out.Sort()
     return out
+
+
+def gather_records(records: np.ndarray, paths: np.ndarray, rule_ids: Sequence[str], dst: int = 0,
+                   group=None) -> Optional[dict]:
+    """The compact form of the gather for large scans (bench.py under torchrun): every rank
+    sends its finding records (tsg_result_records: file, rule index, start/end line, a digest of
+    Match + Code lines) with each record's file path; `dst` concatenates them and restores the
+    reference's order -- secrets by FilePath, findings by (RuleID, StartLine)
+    (analyzer.go:225-234) -- with one lexsort.  Returns {"records", "paths", "ranks"} (sorted) on
+    `dst`, None elsewhere."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    parts = [None] * world if rank == dst else None
+    dist.gather_object((records, paths), parts, dst=dst, group=group)
+    if rank != dst:
+        return None
+    recs = np.concatenate([p[0] for p in parts]) if parts else records[:0]
+    pths = np.concatenate([p[1] for p in parts]) if parts else paths[:0]
+    ranks = np.concatenate([np.full(len(p[0]), r, dtype=np.int32) for r, p in enumerate(parts)])
+    order_of_id = np.argsort(np.argsort(np.array(list(rule_ids), dtype=object)))  # RuleID rank per rule index
+    key_rule = order_of_id[recs["rule"]] if len(recs) else np.zeros(0, dtype=np.int64)
+    order = np.lexsort((recs["start_line"], key_rule, pths))
+    return {"records": recs[order], "paths": pths[order], "ranks": ranks[order]}
