@@ -55,6 +55,10 @@ def main():
     cg = CGlobal(builtin_rules(), builtin_allow_rules(), [])
     b = _CBatch(C.n_files, C.arena.ctypes.data, C.offsets.ctypes.data, None, None, C.path_ptrs.ctypes.data,
                 None, None)
+    sp = None
+    if os.environ.get("SPROF"):  # tools/sprof: sample the reps' CPU time
+        sp = c.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "sprof", "sprof.so"))
+        sp.sprof_start(4000)
     for _ in range(args.reps):
         h = c.c_void_p()
         t = time.time()
@@ -68,6 +72,9 @@ def main():
         t2 = time.time()
         print("tail %.1f ms (allow %.1f, exact %.1f) free %.1f ms, findings %d" %
               ((t1 - t) * 1e3, s.ms_host_allow_path, s.ms_host_exact, (t2 - t1) * 1e3, s.findings), flush=True)
+
+    if sp is not None:
+        print("sprof samples", sp.sprof_stop(os.environ["SPROF"].encode()))
 
 
 if __name__ == "__main__":

@@ -2,6 +2,7 @@
 // work pkg/fanal/analyzer/secret/secret.go does before Scanner.Scan, the
 // analyzer group's Required gate, and an uncompressed-tar layer walker
 // (pkg/fanal/walker/tar.go), all packing straight into one batch arena.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include "tsg_analyzer.h"
@@ -530,10 +531,21 @@ void Classify(const uint8_t* tar, TarEntry* e);
 // Everything the walk decides about one entry, on the thread that indexed it
 // (its header and path are still in that core's cache): the name (Classify),
 // AnalyzeFile's Required, Analyze's binary gate and the transformed length.
+std::atomic<int64_t> g_eval_ns[3];
 void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
+  static const bool dbg = std::getenv("TSG_WALK_DEBUG") != nullptr;
+  auto t0 = dbg ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   Classify(tar, e);
   e->state = 0;
-  if (e->what != 3 || !Required(c->a, e->fp.data(), e->fp.size(), int64_t(e->size))) return;
+  if (dbg) {
+    auto t1 = std::chrono::steady_clock::now();
+    g_eval_ns[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    const bool req = e->what == 3 && Required(c->a, e->fp.data(), e->fp.size(), int64_t(e->size));
+    g_eval_ns[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+    if (!req) return;
+  } else if (e->what != 3 || !Required(c->a, e->fp.data(), e->fp.size(), int64_t(e->size))) {
+    return;
+  }
   const uint8_t* d = tar + e->data;
   e->bin = tsg::IsBinaryHead(d, e->size) ? 1 : 0;
   if (e->bin && tsg::GoExt(e->fp) != ".pyc") {
@@ -794,8 +806,9 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       t_phase[1] += t2 - t1;
       t_phase[2] += t3 - t2;
       t_phase[3] += t4 - t3;
-      std::fprintf(stderr, "walk phases (cumulative s): index+evaluate %.3f (classify %.3f) accept %.3f copy %.3f\n", t_phase[0],
-                   t_phase[1], t_phase[2], t_phase[3]);
+      std::fprintf(stderr, "walk phases (cumulative s): index+evaluate %.3f (classify %.3f) accept %.3f copy %.3f"
+                   " | thread-s: classify %.3f required %.3f\n", t_phase[0], t_phase[1], t_phase[2], t_phase[3],
+                   g_eval_ns[0] / 1e9, g_eval_ns[1] / 1e9);
     }
     if (full) {
       *cursor = ents[k].start;
