@@ -256,9 +256,86 @@ WORKLOADS = {
     "c3f": ("C3 variant: 2,000 generated custom rules of which ~5 %% are bare class runs ((?i)[a-z0-9/+]{32..48}, "
             "keyword-gated, no literal or rare class run: fullscan_kernel) + 87 builtins over a %g GB synthetic corpus "
             "per MI355X (BASELINE configs[2], VERDICT r02 #6)", 8.0, 2.0, 0.4),
+    "c1fs": ("`trivy fs` over a %g GB synthetic source tree on tmpfs (the C1/C2 generator's files and paths): "
+             "FS.Walk + Required + reads straight into double-buffered pinned arenas + GPU pre-transform + scan "
+             "(BASELINE configs[0] end to end on the GPU; SURVEY §8(f)1)", 1.0, 1000.0, 0.0),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
            "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0, 0.0),
 }
+
+
+def write_tree(C, root):
+    """The corpus as files under root (tmpfs): its generator paths, contents as generated."""
+    import shutil
+    if os.path.exists(root):
+        shutil.rmtree(root)
+    os.makedirs(root)
+    made = set()
+    for i in range(C.n_files):
+        rel = C.path(i)
+        d = os.path.dirname(rel)
+        if d not in made:
+            os.makedirs(os.path.join(root, d), exist_ok=True)
+            made.add(d)
+        with open(os.path.join(root, rel), "wb") as f:
+            f.write(C.arena[int(C.offsets[i]):int(C.offsets[i + 1])])
+
+
+def cpu_baseline_fs(root, cores, gpu_result=None):
+    """The same tree through the reference's CPU path, restated: FS.Walk + Required in Python
+    (oracle/analyzer.py walk_fs / required, os.scandir order), each file read and CR-stripped,
+    then tsg_cpuref_scan (the restated reference CPU scan, C++) on `cores` threads; end to end
+    GB/s of the files analyzed.  With gpu_result (AnalyzeFS's sorted secrets), every file's
+    findings are compared with it."""
+    import ctypes as c
+    import numpy as np
+    from oracle import analyzer as oan, hostlib
+    import trivy_amd.secret as secret
+    from trivy_amd.secret.scanner import ScanResult, _CBatch
+    t0 = time.time()
+    a = oan.SecretAnalyzer("")
+    rels, datas, nbytes = [], [], 0
+    for rel, size in oan.walk_fs(root):
+        if not a.required(rel, size):
+            continue
+        with open(os.path.join(root, rel), "rb") as f:
+            b = f.read()
+        args = a.prepare(rel, root, b)
+        if args is None:
+            continue
+        rels.append(args[0])
+        datas.append(args[1])
+        nbytes += len(b)
+    offs = np.zeros(len(datas) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in datas])
+    arena = np.frombuffer(b"".join(datas) + b"\0" * 64, dtype=np.uint8)
+    pb = [r.encode("utf-8", "surrogateescape") for r in rels]
+    parr = (c.c_char_p * max(1, len(pb)))(*pb)
+    plen = np.array([len(x) for x in pb], dtype=np.uint64)
+    t_walk = time.time() - t0
+    L = hostlib.lib()
+    sc = secret.NewScanner(None, lib=L, host_only=True)
+    batch = _CBatch(len(datas), arena.ctypes.data, offs.ctypes.data, None, None, c.cast(parr, c.c_void_p).value,
+                    plen.ctypes.data, None)
+    h = c.c_void_p()
+    if L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), int(cores), c.byref(h)) != 0:
+        raise RuntimeError(hostlib.last_error())
+    dt = time.time() - t0
+    res = ScanResult(sc, h)
+    out = {"value": round(nbytes / dt / 1e9, 6), "unit": "GB/s", "cores": cores,
+           "kind": "port (restated reference CPU path: Python FS.Walk + Required + ReadAll/CR strip, "
+                   "C++ tsg_cpuref_scan)",
+           "sample": "the whole %.1f MB tree (%d files analyzed): walk+read %.1f s, scan %.1f s"
+                     % (nbytes / 1e6, len(datas), t_walk, dt - t_walk)}
+    if gpu_result is not None:
+        want = [s for s in res.secrets(rels) if s.Findings]
+        want.sort(key=lambda s: s.FilePath.encode("utf-8", "surrogateescape"))
+        for s_ in want:
+            s_.Findings.sort(key=lambda f: (f.RuleID.encode(), f.StartLine))
+        got = gpu_result.Secrets
+        bad = sum(1 for x, y in zip(got, want) if x.to_dict() != y.to_dict()) + abs(len(got) - len(want))
+        out["gpu_vs_cpuref_all_files"] = {"files": len(datas), "secrets": len(want), "mismatches": bad}
+    return out
 
 
 def _cgroup_cpu():
@@ -387,6 +464,13 @@ def main():
         C = corpus.generate_c3(int(args.gb * 1e9), samples, seed=corpus.SEED + rank)
     elif args.workload == "c4":
         layer = corpus.generate_layer(int(args.gb * 1e9), seed=corpus.SEED + rank)
+    elif args.workload == "c1fs":  # a source tree on tmpfs
+        base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tmpdir
+        fs_root = os.path.join(base, "tsg-c1fs-%d-%d" % (os.getpid(), rank))
+        C0 = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank)
+        write_tree(C0, fs_root)
+        del C0
+        layer = fs_root  # walked below instead of a tar layer
     elif args.workload == "c5":  # the pool, emitted `emissions` times per step through the ingest path
         pool_gb = min(args.pool_gb, args.gb)
         C = corpus.generate(int(pool_gb * 1e9), seed=corpus.SEED + rank, size_scale=2.6)
@@ -449,7 +533,10 @@ def main():
         def run_steps(n, stats):
             for _ in range(n):
                 st = {}
-                an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
+                if args.workload == "c1fs":
+                    an.AnalyzeFS(layer, stats=st, materialize=False, colls=colls)
+                else:
+                    an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
                 stats.append(st)
 
     last_res = [None]  # the last step's ScanResult (findings checked against the oracle below)
@@ -568,16 +655,22 @@ def main():
         n_bytes = int(last["input_bytes"])  # bytes of the files analyzed, as read from the layer
         n_files = int(last["added"])
         arena_bytes = int(last["scan_bytes"])
-        counts = {k: int(last[k]) for k in ("entries", "regular", "required", "added", "skipped_binary",
-                                            "whiteouts")}
+        fs_wl = args.workload == "c1fs"
+        keys = ("walked", "required", "added", "skipped_binary", "files", "dirs", "skipped_dirs", "nonregular") \
+            if fs_wl else ("entries", "regular", "required", "added", "skipped_binary", "whiteouts")
+        counts = {k: int(last[k]) for k in keys}
         counts.update({k: int(last["scan_" + k]) for k in ("candidates", "findings", "anchor_hits",
                                                             "follow_hits")})
         config_extra = {"walk_s_per_step": round(last["walk_s"], 3), "wait_s_per_step": round(last["wait_s"], 3),
-                        "layer_bytes_per_gpu": int(layer.size), "file_bytes_analyzed_per_gpu": n_bytes,
+                        "file_bytes_analyzed_per_gpu": n_bytes,
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
                         "arena_mb": args.arena_mb, "pipeline": "2 collectors (walk k+1 || scan k)",
-                        "pre_transform": args.transform,
-                        "layer_gbps": round(world * int(layer.size) * args.steps / dt / 1e9, 3)}
+                        "pre_transform": args.transform}
+        if fs_wl:
+            config_extra["tree"] = "tmpfs (%s)" % os.path.dirname(layer)
+        else:
+            config_extra["layer_bytes_per_gpu"] = int(layer.size)
+            config_extra["layer_gbps"] = round(world * int(layer.size) * args.steps / dt / 1e9, 3)
     value = world * n_bytes * args.steps / dt / 1e9
     alg_bytes = arena_bytes + 16 * (n_files // emissions)  # 1 B/arena byte + 16 B/file, per scan
     phase = alg_bytes / (gpu_ms * 1e-3) / 1e9  # §8(d): (arena + 16 n_files) / (t_prefilter + t_nfa)
@@ -627,6 +720,10 @@ def main():
                     ingest["parity"] = parity_block(C, last_res[0], want)
                 cpu = cpu_baseline(C, int(args.cpu_sample_mb * 1e6), [cores, 5], cfg_path, want,
                                    gpu_res=res_timed)
+            elif args.workload == "c1fs":
+                from trivy_amd.walker import Option
+                res_fs = an.AnalyzeFS(layer, Option(), colls=colls)  # findings of the same walk, materialized
+                cpu = cpu_baseline_fs(layer, cores, gpu_result=res_fs)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
                 cpu = cpu_baseline_layer(sample, cores, tmpdir)
@@ -669,6 +766,9 @@ def main():
         if parity is not None and parity["mismatches"]:
             sys.exit("parity: %d of %d sample files differ from the oracle (first: %s)"
                      % (parity["mismatches"], parity["files"], parity["first_mismatch"]))
+    if args.workload == "c1fs":
+        import shutil
+        shutil.rmtree(layer, ignore_errors=True)
     if cfg_path:
         os.remove(cfg_path)
     if h2d_peak:

@@ -77,6 +77,30 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
  * (tsg_batch.transform).  The batch limit then counts each file's largest
  * transformed size. */
 int tsg_collector_set_gpu_transform(tsg_collector* c, int on);
+
+/* FS.Walk (pkg/fanal/walker/fs.go:25-78) feeding a collector: the tree under
+ * root in filepath.WalkDir order, skip_dirs / skip_files as utils.SkipPath
+ * doublestar patterns relative to root (the caller applies BuildSkipPaths,
+ * fs.go:102-155; defaultSkipDirs are added here), regular files only,
+ * permission errors ignored; per file AnalyzeFile's Required and Analyze up
+ * to Scan (binary gate, contents read into the batch arena; FilePath = the
+ * path relative to root, Dir = root).  tsg_collector_add_fs returns 1 when the
+ * collector is full (submit, reset, call again), 0 when the walk is done,
+ * <0 on error (tsg_last_error). */
+typedef struct tsg_fs_walk tsg_fs_walk;
+typedef struct tsg_fs_stats {
+  uint64_t files, dirs, skipped_dirs, skipped_files, nonregular, perm_errors;
+} tsg_fs_stats;
+typedef struct tsg_fs_add_stats {
+  uint64_t walked, required, skipped_binary, added, input_bytes;
+} tsg_fs_add_stats;
+int tsg_fs_walk_new(const char* root, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                    const char* const* skip_files, uint32_t n_skip_files, tsg_fs_walk** out);
+int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st);
+int tsg_fs_walk_stats(const tsg_fs_walk* w, tsg_fs_stats* st);
+void tsg_fs_walk_free(tsg_fs_walk* w);
+/* utils.SkipPath's doublestar.Match: 1 match, 0 no match, -1 malformed pattern. */
+int tsg_doublestar_match(const char* pattern, const char* path);
 uint32_t tsg_collector_files(const tsg_collector* c);
 uint64_t tsg_collector_bytes(const tsg_collector* c);       /* arena bytes (transformed; as read in GPU mode) */
 uint64_t tsg_collector_input_bytes(const tsg_collector* c); /* bytes as read, added files only */

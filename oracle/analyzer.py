@@ -171,3 +171,164 @@ def analyze_layer(analyzer: SecretAnalyzer, data: bytes):
         if r is not None:
             out.append(r["Secrets"][0])
     return out
+
+
+# ---- FS.Walk (pkg/fanal/walker/fs.go:25-78), restated with os.scandir ----
+DEFAULT_SKIP_DIRS = ["**/.git", "proc", "sys", "dev"]  # walker/walk.go:11-16
+
+
+def doublestar_regex(pattern: str):
+    """doublestar.Match (github.com/bmatcuk/doublestar/v4) as a Python regex over the whole
+    path, by translation (an independent restatement of the native matcher): '**' as a whole
+    component = zero or more directories ("a/**" also matches "a"), '*' / '?' / '[...]' never
+    cross '/', '{a,b}' alternatives, '\\' escapes.  None for a malformed pattern."""
+    import re
+    out, i, n, depth = [], 0, len(pattern), 0
+    while i < n:
+        ch = pattern[i]
+        comp = i == 0 or pattern[i - 1] == "/"
+        if ch == "*" and comp and pattern[i:i + 2] == "**" and (i + 2 == n or pattern[i + 2] == "/"):
+            if i + 2 == n:
+                out.append(".*")
+                i += 2
+            else:
+                out.append("(?:[^/]*/)*")  # zero or more whole components
+                i += 3
+            continue
+        if ch == "/" and pattern[i:] == "/**":
+            out.append("(?:/.*)?")
+            i = n
+            continue
+        if ch == "*":
+            out.append("[^/]*")
+        elif ch == "?":
+            out.append("[^/]")
+        elif ch == "[":
+            j = i + 1
+            neg = j < n and pattern[j] in "!^"
+            if neg:
+                j += 1
+            items, first = [], True
+            while True:
+                if j >= n:
+                    return None
+                if pattern[j] == "]" and not first:
+                    break
+                first = False
+                if pattern[j] == "\\":
+                    if j + 1 >= n:
+                        return None
+                    lo = pattern[j + 1]
+                    j += 2
+                else:
+                    lo = pattern[j]
+                    j += 1
+                hi = lo
+                if j + 1 < n and pattern[j] == "-" and pattern[j + 1] != "]":
+                    if pattern[j + 1] == "\\":
+                        if j + 2 >= n:
+                            return None
+                        hi = pattern[j + 2]
+                        j += 3
+                    else:
+                        hi = pattern[j + 1]
+                        j += 2
+                items.append(re.escape(lo) + ("-" + re.escape(hi) if hi != lo else ""))
+            cls = "".join(items)
+            out.append("(?!/)[^%s]" % cls if neg else "(?=[^/])[%s]" % cls)
+            i = j + 1
+            continue
+        elif ch == "{":
+            out.append("(?:")
+            depth += 1
+        elif ch == "}" and depth:
+            out.append(")")
+            depth -= 1
+        elif ch == "," and depth:
+            out.append("|")
+        elif ch == "\\":
+            if i + 1 >= n:
+                return None
+            out.append(re.escape(pattern[i + 1]))
+            i += 2
+            continue
+        else:
+            out.append(re.escape(ch))
+        i += 1
+    if depth:
+        return None
+    return re.compile("(?s)" + "".join(out) + r"\Z")
+
+
+def skip_path(path: str, patterns) -> bool:  # utils.SkipPath, utils.go:112-126
+    path = path.lstrip("/")
+    for p in patterns:
+        rx = doublestar_regex(p)
+        if rx is None:
+            return False
+        if rx.match(path):
+            return True
+    return False
+
+
+def walk_fs(root: str, skip_dirs=(), skip_files=()):
+    """FS.Walk + WalkDirFunc (fs.go:25-78): [(relPath, size)] of the regular files in
+    filepath.WalkDir order (entries by name, directories not followed through symlinks),
+    skip patterns already relative to root (BuildSkipPaths applied), defaultSkipDirs added,
+    permission errors ignored."""
+    import os
+    import stat as st_
+    skip_dirs = list(skip_dirs) + DEFAULT_SKIP_DIRS
+    out = []
+    rs = os.lstat(root)
+    if not st_.S_ISDIR(rs.st_mode):
+        if st_.S_ISREG(rs.st_mode) and not skip_path(".", skip_files):
+            out.append((os.path.basename(root), rs.st_size))
+        return out
+
+    def walk(abs_dir, rel):
+        try:
+            names = sorted(os.listdir(abs_dir), key=lambda x: x.encode("utf-8", "surrogateescape"))
+        except PermissionError:
+            return
+        for name in names:
+            p = os.path.join(abs_dir, name)
+            r = name if rel == "." else rel + "/" + name
+            try:
+                s = os.lstat(p)
+            except FileNotFoundError:
+                continue
+            if st_.S_ISDIR(s.st_mode):
+                if skip_path(r, skip_dirs):
+                    continue
+                walk(p, r)
+            elif not st_.S_ISREG(s.st_mode):
+                continue
+            elif skip_path(r, skip_files):
+                continue
+            else:
+                out.append((r, s.st_size))
+    walk(root, ".")
+    return out
+
+
+def analyze_fs(analyzer: SecretAnalyzer, root: str, skip_dirs=(), skip_files=()):
+    """`trivy fs` for the secret analyzer (artifact/local/fs.go:87-100 -> AnalyzeFile(dir=root)):
+    [secret dict] of the files with findings, sorted as AnalysisResult.Sort."""
+    import os
+    out = []
+    files = walk_fs(root, skip_dirs, skip_files)
+    is_file = not os.path.isdir(root)
+    for rel, size in files:
+        if not analyzer.required(rel, size):
+            continue
+        with open(root if is_file else os.path.join(root, rel), "rb") as f:
+            content = f.read()
+        r = analyzer.analyze(rel, root, content)
+        if r is not None:
+            out.append(r["Secrets"][0])
+    out.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape")
+             if isinstance(s["FilePath"], str) else s["FilePath"])
+    for s in out:
+        s["Findings"].sort(key=lambda f: (f["RuleID"], f["StartLine"]))
+    return out

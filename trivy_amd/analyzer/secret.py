@@ -337,6 +337,60 @@ class SecretAnalyzer:
         flush()
         return out
 
+    def AnalyzeFS(self, root: str, opt=None, arena_bytes: int = 256 << 20, stats: Optional[dict] = None,
+                  materialize: bool = True, colls: Optional[List["Collector"]] = None,
+                  gpu_transform: bool = False) -> AnalysisResult:
+        """`trivy fs` for this analyzer: FS.Walk (walker/fs.go:25-78) + AnalyzeFile's Required +
+        Analyze for every regular file under root, read natively into double-buffered pinned
+        arenas (tsg_collector_add_fs); one collector fills while the other's batch scans.
+        FilePath is the path relative to root (Dir = root, no '/' prefix: secret.go:130-135)."""
+        from ..walker import FS, Option, _CFsAddStats
+        w = FS().Walk(root, opt or Option(), lib=self._L)
+        result = AnalysisResult()
+        scan_tot: dict = {}
+        st = _CFsAddStats()
+
+        def take(p):
+            out = p.wait(materialize)
+            if materialize:
+                result.Secrets.extend(sec for sec in out if sec is not None)
+            else:
+                for k2, v in out.items():
+                    scan_tot[k2] = scan_tot.get(k2, 0) + v
+        colls = colls or [Collector(self, arena_bytes, gpu_transform), Collector(self, arena_bytes, gpu_transform)]
+        pending, k, done = None, 0, False
+        t_walk = t_wait = 0.0
+        try:
+            while not done:
+                coll = colls[k]
+                t0 = time.perf_counter()
+                rc = self._L.tsg_collector_add_fs(coll._h, w._h, c.byref(st))
+                t_walk += time.perf_counter() - t0
+                if rc < 0:
+                    raise RuntimeError("fs walk: %s" % _lib.last_error(self._L))
+                done = rc == 0
+                nxt = coll.submit() if coll.files() else None
+                t0 = time.perf_counter()
+                if pending is not None:
+                    p, pending = pending, None
+                    take(p)
+                t_wait += time.perf_counter() - t0
+                pending = nxt
+                k ^= 1
+            if pending is not None:
+                p, pending = pending, None
+                take(p)
+        finally:
+            if pending is not None:
+                pending.__del__()
+        if stats is not None:
+            stats.update({n: getattr(st, n) for n, _ in st._fields_})
+            stats.update(w.stats())
+            stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})
+            stats.update({"walk_s": t_walk, "wait_s": t_wait})
+        result.Sort()
+        return result
+
     def AnalyzeLayer(self, layer, arena_bytes: int = 256 << 20, stats: Optional[dict] = None,
                      materialize: bool = True, colls: Optional[List[Collector]] = None,
                      gpu_transform: bool = False) -> AnalysisResult:
