@@ -489,10 +489,14 @@ def main():
             # step streams it through the engine's double-buffered H2D (RunHost)
             unregister = secret.HostRegister(C.arena)
             h2d_peak = measure_h2d(dev)
-            d_arena = d_offs = None
+            d_arena = d_offs = d_paths = d_poffs = None
         else:
             d_arena = torch.from_numpy(C.arena).to(dev)
             d_offs = torch.from_numpy(C.offsets.view(np.int64)).to(dev)
+            # the paths are input too: packed in HBM beside the contents (GPU allow-path prefilter)
+            pp, poffs = C.packed_paths()
+            d_paths = torch.from_numpy(pp).to(dev)
+            d_poffs = torch.from_numpy(poffs.view(np.int64)).to(dev)
         torch.cuda.synchronize()
         t_c = time.time()
         sc = secret.NewScanner(secret.ParseConfig(cfg_path) if cfg_path else None, device=local)
@@ -502,7 +506,8 @@ def main():
             if args.ingest or host_leg[0]:
                 return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs)
             return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(),
-                                       dev_offsets=d_offs.data_ptr())
+                                       dev_offsets=d_offs.data_ptr(), dev_paths=d_paths.data_ptr(),
+                                       dev_path_offsets=d_poffs.data_ptr())
 
         emissions = max(1, int(round(args.gb * 1e9 / C.n_bytes))) if args.workload == "c5" else 1
 

@@ -25,6 +25,13 @@ int tsg_regex_find_all(const char* pattern, const uint8_t* text, uint64_t n, int
  * 0 auto (bit-state backtracker, Pike VM past its row budget), 1 Pike VM only,
  * 2 backtracker with an 8-position budget (exercises the fallback). */
 void tsg_debug_regex_engine(int mode);
+/* The GPU pre-transform (trivy_amd/csrc/xform.hip) on a host batch, on HIP
+ * device `device`: out receives the transformed arena (up to out_cap bytes),
+ * xoff the n_files + 1 transformed offsets.  kinds per file: 0 as is, 1 CR
+ * strip (secret.go:121), 2 ExtractPrintableBytes (utils.go:128-160).  Tests
+ * compare it with the oracle's transforms byte for byte. */
+int tsg_debug_xform(int device, const uint8_t* raw, uint64_t n_bytes, const uint64_t* offsets, uint32_t n_files,
+                    const uint8_t* kinds, uint8_t* out, uint64_t out_cap, uint64_t* xoff);
 /* regexp.MatchString: 1 = match, 0 = no match, <0 = compile error. */
 int tsg_regex_match(const char* pattern, const uint8_t* text, uint64_t n);
 

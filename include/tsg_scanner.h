@@ -81,6 +81,13 @@ typedef struct tsg_batch {
    * must be NULL): 0 as is, 1 every '\r' removed (secret.go:121), 2
    * utils.ExtractPrintableBytes (.pyc, secret.go:112-117, utils.go:128-160) */
   const uint8_t* transform;
+  /* optional: the FilePath bytes packed in HBM (dev_path_offsets: n_files + 1
+   * u64, device) -- the global allow-path rules (scanner.go:381-386) are then
+   * prefiltered on the GPU and the host runs them only on the paths that hold
+   * one of their literals (trivy_amd/csrc/pathfilter.h).  `paths` is still
+   * required (the exact rule and the results use it). */
+  const void* dev_paths;
+  const void* dev_path_offsets;
 } tsg_batch;
 
 int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);

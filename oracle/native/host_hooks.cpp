@@ -102,7 +102,7 @@ int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_result** ou
     const uint64_t fs = b->host_offsets[f], fe = b->host_offsets[f + 1];
     for (uint32_t r = 0; r < sc->rules().size(); r++)
       if (sc->compiled().regex[r])
-        cands.push_back({f, r, 0, int64_t(fe - fs), 0, 0, {tsg::kNlUnknown, tsg::kNlUnknown, tsg::kNlUnknown}});
+        cands.push_back(tsg::HostCandidate(f, r, 0, int64_t(fe - fs), 0, 0));
   }
   return Tail(std::move(sc), b, &cands, out);
 }
@@ -161,8 +161,8 @@ int tsg_cpuref_scan(const tsg_global* g, const tsg_batch* b, int threads, tsg_re
         if (!hit) continue;
       }
       if (!sc->compiled().regex[r]) continue;  // FindLocations: r.Regex == nil -> nil (:103)
-      per_file[f].push_back({uint32_t(f), r, 0, int64_t(len), 0, tsg::kCandGateValid | tsg::kCandGateOpen,
-                             {tsg::kNlUnknown, tsg::kNlUnknown, tsg::kNlUnknown}});
+      per_file[f].push_back(
+          tsg::HostCandidate(uint32_t(f), r, 0, int64_t(len), 0, tsg::kCandGateValid | tsg::kCandGateOpen));
     }
   });
   std::vector<tsg::Candidate> cands;

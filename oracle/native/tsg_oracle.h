@@ -27,7 +27,7 @@ extern "C" {
 #endif
 
 int tsg_debug_host_tail(const tsg_global* g, const tsg_batch* b, tsg_result** out);
-/* candidates: 40-B records (trivy_amd/csrc/engine.h Candidate), e.g. dumped by TSG_DUMP_CANDS */
+/* candidates: 64-B records (trivy_amd/csrc/engine.h Candidate), e.g. dumped by TSG_DUMP_CANDS */
 int tsg_debug_host_tail_cands(const tsg_global* g, const tsg_batch* b, const void* cands, uint64_t n_cands,
                               tsg_result** out);
 int tsg_debug_scanner_host_only(const tsg_global* g, tsg_scanner** out);

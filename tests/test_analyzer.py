@@ -333,3 +333,49 @@ def test_gpu_transform_edges_vs_oracle():
             n += 1
             assert [_norm_secret(s) for s in g.Secrets] == w["Secrets"], inp.FilePath
     assert n > 40
+
+
+@pytest.mark.gpu
+def test_gpu_xform_bytes_vs_oracle():
+    """The flat GPU pre-transform (xform.hip) byte for byte against the oracle's
+    CR strip and ExtractPrintableBytes (utils.go:128-160): tiny and empty files
+    packed into one 16-B block, printable runs of 3..7 bytes around 16-B / 1-KiB
+    edges and file ends, CRs at block edges, Latin-1 bytes (0xA0, 0xAD are not
+    printable), files spanning many tiles."""
+    import ctypes as c
+    import random
+    import numpy as np
+    from trivy_amd import _lib
+    L = _lib.lib()
+    L.tsg_debug_xform.argtypes = [c.c_int, c.c_void_p, c.c_uint64, c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p,
+                                  c.c_uint64, c.c_void_p]
+    rng = random.Random(5)
+    alpha = [b"a", b"Z", b" ", b"~", b"\x00", b"\x07", b"\r", b"\n", b"\xa0", b"\xa1", b"\xad", b"\xff", b"\x7f",
+             b"\x1f"]
+    files, kinds = [], []
+    for i in range(4000):
+        n = rng.choice([0, 0, 1, 3, 4, 5, 6, 9, 15, 16, 17, 31, 63, 100, 1000, 1023, 1024, 1025, 3000, 9000])
+        if rng.random() < 0.5:  # runs of printable bytes of chosen lengths between separators
+            parts = []
+            while sum(map(len, parts)) < n:
+                parts.append(b"p" * rng.choice([1, 3, 4, 5, 6, 7, 20]) + rng.choice(alpha))
+            b = b"".join(parts)[:n]
+        else:
+            b = b"".join(rng.choice(alpha) for _ in range(n))
+        files.append(b)
+        kinds.append(rng.choice([0, 1, 1, 2, 2]))
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in files])
+    raw = np.frombuffer(b"".join(files) + b"\0" * 64, dtype=np.uint8)
+    kd = np.array(kinds, dtype=np.uint8)
+    out = np.zeros(int(offs[-1]) * 2 + 64, dtype=np.uint8)
+    xoff = np.zeros(len(files) + 1, dtype=np.uint64)
+    rc = L.tsg_debug_xform(0, raw.ctypes.data, int(offs[-1]), offs.ctypes.data, len(files), kd.ctypes.data,
+                           out.ctypes.data, len(out), xoff.ctypes.data)
+    assert rc == 0, _lib.last_error(L)
+    for i, (b, k) in enumerate(zip(files, kinds)):
+        want = b if k == 0 else b.replace(b"\r", b"") if k == 1 else oan.extract_printable_bytes(b)
+        got = out[int(xoff[i]):int(xoff[i + 1])].tobytes()
+        assert got == want, (i, k, b[:80])
+    assert int(xoff[-1]) == sum(len(b if k == 0 else b.replace(b"\r", b"") if k == 1 else
+                                    oan.extract_printable_bytes(b)) for b, k in zip(files, kinds))

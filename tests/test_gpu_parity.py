@@ -356,3 +356,65 @@ def test_device_batches_pipelined_tickets_and_overflow(secret):
     got = first.secrets(paths)
     for i in (0, 1, n // 2, n - 1):
         assert got[i].to_dict() == o.scan(paths[i], contents[i])
+
+
+def _allow_paths_batch(rng):
+    """Paths around the builtin allow rules' literals (scanner builtin-allow-rules.go):
+    every case mix, literals at the start / end / middle, near misses, non-ASCII
+    paths, paths longer than one shift-and word and than 1 KiB."""
+    words = ["test", "TEST", "Test", "tests", "example", "EXAMPLE", "vendor", "Vendor", "usr", "USR", "locale",
+             "locales", "share", "include", "lib", "go", "python3.11", "gems", "wordpress", "anaconda", "yarn-v1.22",
+             "src", "md", "MD", "log", "var", "opt", "local", "pkg", "a", "tést", "vеndor", "ſrc", "K"]
+    seps = ["/", "-", "_", ".", "", " "]
+    paths = ["test", "Test/x", "xtest", "a/test", "a-test", "a_TEST", "a.test", "README.md", "README.MD", "x.md.txt",
+             "usr/share/doc/x", "usr/include/y.h", "usr/lib/z", "usr/libx/z", "/usr/share/x", "opt/yarn-v1.2.3/a",
+             "opt/yarn-v/a", "usr/local/go/src/x.go", "usr/local/lib/python3.11/site.py", "usr/local/lib/python/x",
+             "usr/lib/gems/x", "usr/src/wordpress/wp.php", "var/log/anaconda/x.log", "a/vendor/b", "a/vendor",
+             "a/locale/b", "a/locales/b", "a/localesx/b", "examples/x", "x/exAmple", "", "/", "ü/test", "tést",
+             "x" * 70 + "/vendor/" + "y" * 70, "z" * 1500 + ".md", "z" * 1500 + "/test", "K" * 2000]
+    for _ in range(3000):
+        k = rng.randint(1, 6)
+        paths.append("".join(rng.choice(words) + rng.choice(seps) for _ in range(k)).strip("/") or "p")
+    return paths
+
+
+@pytest.mark.parametrize("custom", [False, True])
+def test_allow_paths_gpu_prefilter_vs_oracle(secret, tmp_path, custom):
+    """Global allow-path results with the paths in HBM (the GPU prefilter of
+    pathfilter.hip reports candidate paths, the host confirms) equal the
+    oracle's AllowPath for every path; the custom config adds allow rules with
+    and without usable literals (the latter turn the GPU prefilter off)."""
+    import numpy as np
+    import torch
+    rng = random.Random(7)
+    paths = _allow_paths_batch(rng)
+    cfg = None
+    if custom:
+        p = tmp_path / "trivy-secret.yaml"
+        extra = "  - id: digits\n    path: '[0-9]{5}'\n" if custom else ""
+        p.write_text("allow-rules:\n  - id: lockfiles\n    path: '(?i)\\.lock$'\n  - id: internal\n"
+                     "    path: '^internal/|/Internal/'\n" + extra)
+        cfg = str(p)
+    for cfg_i in ([cfg] if not custom else [cfg, None]):
+        s = secret.NewScanner(secret.ParseConfig(cfg_i) if cfg_i else None)
+        o = osc.new_scanner(osc.parse_config(cfg_i) if cfg_i else None)
+        contents = [b"AKIA" + b"Q" * 16 + b"\n" if i % 3 == 0 else b"nothing here\n" for i in range(len(paths))]
+        offs = np.zeros(len(paths) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(x) for x in contents])
+        arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+        pb = [x.encode() for x in paths]
+        poffs = np.zeros(len(pb) + 1, dtype=np.uint64)
+        poffs[1:] = np.cumsum([len(x) for x in pb])
+        d_arena = torch.from_numpy(arena.copy()).to("cuda:0")
+        d_offs = torch.from_numpy(offs.view(np.int64)).to("cuda:0")
+        d_paths = torch.from_numpy(np.frombuffer(b"".join(pb) + b"\0" * 16, dtype=np.uint8).copy()).to("cuda:0")
+        d_poffs = torch.from_numpy(poffs.view(np.int64)).to("cuda:0")
+        r = s.scan_arena(arena, offs, paths, dev_arena=d_arena.data_ptr(), dev_offsets=d_offs.data_ptr(),
+                         dev_paths=d_paths.data_ptr(), dev_path_offsets=d_poffs.data_ptr())
+        got = r.secrets(paths)
+        n_allowed = 0
+        for path, b, g in zip(paths, contents, got):
+            want = o.scan(path, b)
+            assert g.to_dict() == want, path
+            n_allowed += int(bool(want.get("FilePath")) and not want.get("Findings"))
+        assert n_allowed > 100

@@ -166,25 +166,29 @@ def test_host_tail_c3u_unanchored_rules(tmp_path):
 
 
 CAND = np.dtype([("file", "<u4"), ("rule", "<u4"), ("wlo", "<i8"), ("whi", "<i8"), ("nl_before", "<i8"),
-                 ("flags", "<u4"), ("nl_back", "<u4", (3,))])
-assert CAND.itemsize == 48
+                 ("flags", "<u4"), ("nl_back", "<u4", (3,)), ("nl_fwd", "<u4", (3,)), ("pad", "<u4")])
+assert CAND.itemsize == 64
 
 
 def _windowed_candidates(files, n_rules, step, hints):
     """Every rule over every file in windows of `step` bytes, each carrying its
-    '\\n' count and (hints) the last three '\\n' before it, as the GPU's
-    finalize kernel writes them (Candidate::nl_back)."""
+    '\\n' count and (hints) the last three '\\n' before it and the first three
+    at or after it, as the GPU's finalize kernel writes them
+    (Candidate::nl_back / nl_fwd)."""
     recs = []
     for f, (_, b) in enumerate(files):
         nl = np.flatnonzero(np.frombuffer(b, dtype=np.uint8) == 10)
         for lo in range(0, max(1, len(b)), step):
             before = nl[nl < lo]
             back = [0xFFFFFFFF] * 3
+            fwd = [0xFFFFFFFF] * 3
             if hints:
                 last = before[-3:][::-1]
                 back = [lo - int(x) for x in last] + [0xFFFFFFFE] * (3 - len(last))
+                nxt = nl[nl >= lo][:3]
+                fwd = [int(x) - lo for x in nxt] + [0xFFFFFFFE] * (3 - len(nxt))
             for r in range(n_rules):
-                recs.append((f, r, lo, min(len(b), lo + step - 1), len(before), 0, back))
+                recs.append((f, r, lo, min(len(b), lo + step - 1), len(before), 0, back, fwd, 0))
     return np.array(recs, dtype=CAND)
 
 

@@ -23,33 +23,46 @@ def main():
     ap.add_argument("cands")
     ap.add_argument("--gb", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--rec", type=int, default=64, help="record size of the dump (40 / 48: older builds)")
     ap.add_argument("--hints", action="store_true", help="fill Candidate::nl_back on the host first")
     args = ap.parse_args()
     from oracle import hostlib
     L = hostlib.lib()
     cand = np.fromfile(args.cands, dtype=np.uint8)
-    if len(cand) % 48 and not len(cand) % 40:  # a dump from before Candidate::nl_back: hints unknown
-        old = cand.reshape(-1, 40)
-        cand = np.full((len(old), 48), 0xFF, dtype=np.uint8)
-        cand[:, :36] = old[:, :36]
-        cand = cand.reshape(-1)
-    n_c = len(cand) // 48
+    if args.rec != 64:  # dumps from before Candidate::nl_back (40 B) / nl_fwd (48 B): those hints unknown
+        rec = args.rec
+        if True:
+            old = cand.reshape(-1, rec)
+            cand = np.full((len(old), 64), 0xFF, dtype=np.uint8)
+            cand[:, :rec] = old
+            cand[:, 60:64] = 0
+            cand = cand.reshape(-1)
+    n_c = len(cand) // 64
     t = time.time()
     C = corpus.generate(int(args.gb * 1e9))
     if args.hints:  # fill nl_back as the finalize kernel does (last three '\n' before wlo)
-        rec = cand.reshape(-1, 48)
+        rec = cand.reshape(-1, 64)
         file = rec[:, 0:4].copy().view(np.uint32).ravel()
         wlo = rec[:, 8:16].copy().view(np.int64).ravel()
         back = np.full((n_c, 3), 0xFFFFFFFF, dtype=np.uint32)
+        fwd = np.full((n_c, 3), 0xFFFFFFFF, dtype=np.uint32)
         for i in range(n_c):
-            fs = int(C.offsets[file[i]])
-            lo = max(fs, fs + int(wlo[i]) - (1 << 20))
-            nl = np.flatnonzero(C.arena[lo:fs + int(wlo[i])] == 10)[-3:][::-1]
+            fs, fe = int(C.offsets[file[i]]), int(C.offsets[file[i] + 1])
+            w = fs + int(wlo[i])
+            lo = max(fs, w - (1 << 20))
+            nl = np.flatnonzero(C.arena[lo:w] == 10)[-3:][::-1]
             for k, x in enumerate(nl):
-                back[i, k] = fs + int(wlo[i]) - (lo + int(x))
+                back[i, k] = w - (lo + int(x))
             if lo == fs:
                 back[i, len(nl):] = 0xFFFFFFFE
+            hi = min(fe, w + (1 << 20))
+            nl = np.flatnonzero(C.arena[w:hi] == 10)[:3]
+            for k, x in enumerate(nl):
+                fwd[i, k] = int(x)
+            if hi == fe:
+                fwd[i, len(nl):] = 0xFFFFFFFE
         rec[:, 36:48] = back.view(np.uint8).reshape(-1, 12)
+        rec[:, 48:60] = fwd.view(np.uint8).reshape(-1, 12)
         print("hints filled %.1f s" % (time.time() - t), flush=True)
     print("corpus %.1f s, %d files, %d candidates" % (time.time() - t, C.n_files, n_c), flush=True)
     cg = CGlobal(builtin_rules(), builtin_allow_rules(), [])

@@ -17,7 +17,7 @@ def main():
             continue
         a, b = (int(x, 16) for x in parts[0].split("-"))
         maps.append((a, b, int(parts[2], 16), parts[5]))
-    pcs = [int(x, 16) for x in open(path)]
+    pcs = [int(x.split()[0], 16) for x in open(path)]
     libs = collections.Counter()
     per = collections.defaultdict(list)
     for pc in pcs:
@@ -68,12 +68,21 @@ def lines(path, want):
             maps.append((a, b, int(parts[2], 16), parts[5]))
     offs, lib = [], None
     tot = 0
+    tags = []
     for x in open(path):
-        pc = int(x, 16)
+        parts = x.split()
+        pc = int(parts[0], 16)
+        ra = int(parts[1], 16) if len(parts) > 1 else 0
         tot += 1
+        tag = ""
+        for a, b, off, name in maps:
+            if a <= pc < b and "libc.so" in name:  # a leaf in libc: charge the line that called it
+                pc, tag = ra, "libc<- "
+                break
         for a, b, off, name in maps:
             if a <= pc < b and want in name:
                 offs.append(pc - a + off)
+                tags.append(tag)
                 lib = name
     # file offset -> vaddr: for a PIC .so the text segment's vaddr == file offset in practice
     uniq = sorted(set(offs))
@@ -83,7 +92,7 @@ def lines(path, want):
     for i, o in enumerate(uniq):
         fn, fl = out[2 * i], out[2 * i + 1]
         where[o] = "%s  %s" % (fl.split("/")[-1], fn[:70])
-    cnt = collections.Counter(where[o] for o in offs)
+    cnt = collections.Counter(t + where[o] for o, t in zip(offs, tags))
     for s, n in cnt.most_common(40):
         print("%6.1f%%  %s" % (100.0 * n / tot, s))
 

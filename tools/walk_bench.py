@@ -27,6 +27,11 @@ def main():
     an = SecretAnalyzer(lib=hostlib.lib(), host_only=True)
     an.Init(AnalyzerOptions(SecretScannerOption("")))
     col = Collector(an, a.arena_mb << 20)
+    sp = None
+    if os.environ.get("SPROF"):  # tools/sprof: sample the walks' CPU time
+        import ctypes
+        sp = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "sprof", "sprof.so"))
+        sp.sprof_start(4000)
     for rep in range(a.reps):
         t0 = time.time()
         cur, files, st = 0, 0, _CTarStats()
@@ -38,6 +43,8 @@ def main():
                 break
         dt = time.time() - t0
         print("walk %.3f s  %.2f GB/s layer  files %d" % (dt, layer.size / dt / 1e9, files))
+    if sp is not None:
+        print("sprof samples", sp.sprof_stop(os.environ["SPROF"].encode()))
 
 
 if __name__ == "__main__":

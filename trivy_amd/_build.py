@@ -16,7 +16,7 @@ BUILD = PKG / "_obj"
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
-CXXFLAGS = ["-O3", "-march=x86-64-v3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-I", str(CSRC),
+CXXFLAGS = ["-O3", "-g1", "-fno-omit-frame-pointer", "-march=x86-64-v3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-I", str(CSRC),
             "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROCM, "include"),
             "-I", str(PKG.parent / "include")]
 HIPFLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I", str(CSRC),

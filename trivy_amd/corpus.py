@@ -42,6 +42,16 @@ class Corpus:
         raw = self.path_buf[i * PATH_STRIDE:(i + 1) * PATH_STRIDE].tobytes()
         return raw.split(b"\0", 1)[0].decode()
 
+    def packed_paths(self):
+        """The paths packed back to back (uint8, +16 B pad) and their n+1 offsets (uint64)."""
+        rows = self.path_buf[:self.n_files * PATH_STRIDE].reshape(self.n_files, PATH_STRIDE)
+        z = rows == 0
+        lens = np.where(z.any(axis=1), z.argmax(axis=1), PATH_STRIDE).astype(np.uint64)
+        offs = np.zeros(self.n_files + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens)
+        keep = np.arange(PATH_STRIDE)[None, :] < lens[:, None].astype(np.int64)
+        return np.concatenate([rows[keep], np.zeros(16, np.uint8)]), offs
+
     def content(self, i):
         return self.arena[int(self.offsets[i]):int(self.offsets[i + 1])].tobytes()
 

@@ -515,6 +515,9 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
   const uint64_t seg = std::max<uint64_t>(((end - p) / n_seg + 511) & ~uint64_t(511), 1 << 16);
   const size_t segs = size_t(std::max<uint64_t>(1, (end - p + seg - 1) / seg));
   std::vector<std::vector<TarEntry>> spec(segs);
+  static const bool dbg = std::getenv("TSG_WALK_DEBUG") != nullptr;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = dbg ? now() : 0;
   tsg::ParallelFor(segs, threads, [&](size_t s) {
     const uint64_t a = p + s * seg, b = std::min(end, a + seg);
     spec[s].reserve(size_t(seg / 2048) + 8);
@@ -537,6 +540,8 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
     std::vector<TarEntry>* v;
     size_t lo, hi;
   };
+  const double t1 = dbg ? now() : 0;
+  size_t n_fallback = 0;
   std::vector<Range> plan;
   std::vector<std::vector<TarEntry>> fallback;
   fallback.reserve(segs);
@@ -574,6 +579,7 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
         Evaluate(c, tar, &e);
         if (e.what == 3) regular += e.size + 512;
         fb.push_back(std::move(e));
+        n_fallback++;
       }
       plan.push_back({&fb, 0, fb.size()});
     }
@@ -586,6 +592,12 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
     tsg::ParallelFor(plan.size(), threads, [&](size_t k) {
       for (size_t i = plan[k].lo; i < plan[k].hi; i++) (*out)[at[k] + (i - plan[k].lo)] = std::move((*plan[k].v)[i]);
     });
+  }
+  if (dbg) {
+    size_t n_spec = 0;
+    for (auto& v : spec) n_spec += v.size();
+    std::fprintf(stderr, "index: segs %zu spec %.3f s (%zu entries) merge+move %.3f s (kept %zu, fallback %zu)\n", segs,
+                 t1 - t0, n_spec, now() - t1, out->size(), n_fallback);
   }
   if (ended) {
     *next = cur;

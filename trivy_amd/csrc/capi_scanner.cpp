@@ -252,6 +252,8 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   in.path_lens = b->path_lens;
   in.binary = b->binary;
   in.transform = b->transform;
+  in.dev_paths = static_cast<const uint8_t*>(b->dev_paths);
+  in.dev_path_off = static_cast<const uint64_t*>(b->dev_path_offsets);
   std::unique_ptr<tsg_result> r(new tsg_result());
   r->owner = s->s.get();
   tsg::BatchStats gs;

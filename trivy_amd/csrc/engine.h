@@ -30,8 +30,22 @@ struct Candidate {      // produced by the verify / full-scan kernels
   // scanning back over long lines.  kNlNone: fewer newlines precede wlo;
   // kNlUnknown: not computed (host candidates, or farther than kNlReach).
   uint32_t nl_back[3];
+  // The first three '\n' at or after wlo, as distances from wlo, nearest
+  // first (finalize kernel): the line ends of the match line and the code
+  // lines after it, which the host otherwise finds by memchr over long lines.
+  // kNlNone: fewer newlines follow before the file end; kNlUnknown: not
+  // computed (host candidates, or farther than kNlReach).
+  uint32_t nl_fwd[3];
+  uint32_t pad_;
 };
+static_assert(sizeof(Candidate) == 64, "Candidate is a 64-B record (tsg_oracle.h, tests/test_host_tail.py)");
 constexpr uint32_t kNlNone = 0xFFFFFFFEu, kNlUnknown = 0xFFFFFFFFu;
+// A candidate made on the host (no newline hints).
+inline Candidate HostCandidate(uint32_t file, uint32_t rule, int64_t wlo, int64_t whi, int64_t nl_before,
+                               uint32_t flags) {
+  return Candidate{file, rule, wlo, whi, nl_before, flags, {kNlUnknown, kNlUnknown, kNlUnknown},
+                   {kNlUnknown, kNlUnknown, kNlUnknown}, 0};
+}
 constexpr uint64_t kNlReach = uint64_t(1) << 20;
 
 // The transformed bytes of chosen files of a host batch whose transform ran

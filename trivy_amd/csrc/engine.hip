@@ -653,6 +653,8 @@ __device__ __forceinline__ void put_candidate(Candidate* cands, uint32_t cap, ui
     c.nl_before = -1;
     c.flags = 0;
     c.nl_back[0] = c.nl_back[1] = c.nl_back[2] = kNlUnknown;
+    c.nl_fwd[0] = c.nl_fwd[1] = c.nl_fwd[2] = kNlUnknown;
+    c.pad_ = 0;
     cands[k] = c;
   } else {
     counters[4] = 1;
@@ -1550,6 +1552,49 @@ __global__ __launch_bounds__(256) void finalize_kernel(NfaParams P) {
       }
       if (hi <= fs)  // reached the file start: the remaining ranks do not exist
         for (uint32_t r = found + lane; r < 3; r += 64) c.nl_back[r] = kNlNone;
+      // the first three '\n' at or after wlo, the same way forwards: lane 0 on
+      // the lowest 16-B block, ranks in lane order
+      const uint64_t fe = P.off[file + 1];
+      uint64_t lo = wabs;  // [lo, fe) still unsearched
+      found = 0;
+      while (found < 3 && lo < fe && lo - wabs < kNlReach) {
+        const uint64_t ck = lo / kChunk;  // wave-uniform
+        if (P.nl[ck] == 0) {              // no '\n' in [lo, (ck + 1) * kChunk)
+          lo = (ck + 1) * kChunk;
+          continue;
+        }
+        const uint64_t blk = ((lo >> 4) + lane) << 4;
+        uint32_t mask = 0;
+        if (blk < fe) {
+          const uint4 v = load16(P.arena + blk);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++)
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++)
+              if (((w[q] >> (8 * b)) & 0xFFu) == uint32_t('\n')) mask |= 1u << (4 * q + b);
+          const uint32_t lo_cut = lo > blk ? uint32_t(lo - blk) : 0u;
+          const uint32_t hi_cut = fe < blk + 16 ? uint32_t(fe - blk) : 16u;
+          mask &= (hi_cut >= 16 ? 0xFFFFu : ((1u << hi_cut) - 1u)) & ~((1u << lo_cut) - 1u);
+        }
+        const uint32_t cnt = uint32_t(__popc(mask));
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int x = 1; x < 64; x <<= 1) {
+          const uint32_t t = __shfl_up(incl, x);
+          if (lane >= uint32_t(x)) incl += t;
+        }
+        uint32_t rank = found + incl - cnt;
+        for (uint32_t m = mask; m && rank < 3; rank++) {
+          const uint32_t bit = uint32_t(__ffs(m)) - 1u;
+          m &= m - 1u;
+          c.nl_fwd[rank] = uint32_t(blk + bit - wabs);
+        }
+        found += __shfl(incl, 63);
+        lo = ((lo >> 4) + 64) << 4;
+      }
+      if (lo >= fe)  // reached the file end: the remaining ranks do not exist
+        for (uint32_t r = found + lane; r < 3; r += 64) c.nl_fwd[r] = kNlNone;
     }
     if (lane == 0) c.flags = fl;
   }
@@ -2059,25 +2104,23 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
 // compaction into d_xf_.  Points the scan at the transformed arena.
 bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
                           std::vector<uint64_t>* xoff, float* ms) {
-  size_t scan_bytes = 0;
-  HIP_OK(XformScanBytes(nf, &scan_bytes));
-  if (!Ensure(&d_xlen_, &cap_xlen_, (size_t(nf) + 1) * 8) || !Ensure(&d_xoff_, &cap_xoff_, (size_t(nf) + 1) * 8) ||
-      !Ensure(&d_xscan_, &cap_xscan_, scan_bytes + 16))
+  const uint64_t raw_bytes = *n_bytes;
+  if (!Ensure(&d_xoff_, &cap_xoff_, (size_t(nf) + 1) * 8) ||
+      !Ensure(&d_xscan_, &cap_xscan_, XformScratchBytes(raw_bytes, nf)))
     return false;
   const uint8_t* raw = static_cast<const uint8_t*>(d_stage_[b]);
   const uint64_t* off = static_cast<const uint64_t*>(d_stage_off_[b]);
   const uint8_t* kd = static_cast<const uint8_t*>(d_kind_[b]);
   uint64_t* xo = static_cast<uint64_t*>(d_xoff_);
   HIP_OK(hipEventRecord(ev_x_[0], stream_));
-  HIP_OK(XformLengths(raw, off, kd, nf, static_cast<uint64_t*>(d_xlen_), stream_));
-  HIP_OK(XformScan(d_xscan_, scan_bytes, static_cast<const uint64_t*>(d_xlen_), xo, nf, stream_));
+  HIP_OK(XformPlan(raw, raw_bytes, off, kd, nf, d_xscan_, xo, stream_));
   xoff->resize(size_t(nf) + 1);
   HIP_OK(hipMemcpyAsync(xoff->data(), xo, (size_t(nf) + 1) * 8, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   const uint64_t total = (*xoff)[nf];
   if (!Ensure(&d_xf_, &cap_xf_, total + 64)) return false;
   uint8_t* out = static_cast<uint8_t*>(d_xf_);
-  HIP_OK(XformCopy(raw, off, kd, nf, xo, out, stream_));
+  HIP_OK(XformWrite(raw, raw_bytes, off, kd, nf, d_xscan_, out, stream_));
   HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));
   HIP_OK(hipEventRecord(ev_x_[1], stream_));
   HIP_OK(hipEventSynchronize(ev_x_[1]));

@@ -1,0 +1,67 @@
+// Global allow-path prefilter on the GPU (scanner.go:57-59, 381-386).
+//
+// Scan returns Secret{FilePath} for every file whose path an allow rule
+// matches, so the allow-path rules run over every path of a batch -- on the
+// host that was ~31 ns per path, a sixth of the host CPU of a C2 scan.  Here
+// one lane per path runs a shift-and over the allow rules' required literals
+// (Matcher::lits: an ASCII path holding none of a rule's lowercased literals
+// cannot match it) and reports the paths that hold one, with the rules whose
+// literal they hold, plus every non-ASCII path.  The host runs the exact rule
+// only on those (about 10 % of C2's paths); every other path is not allowed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace tsg {
+
+struct PathHit {        // one reported path
+  uint32_t file;        // | kPathNonAscii: the host runs every rule on it
+  uint32_t pad;
+  uint64_t rules;       // allow rules (bit i = rule i) with a literal in the lowered path
+};
+constexpr uint32_t kPathNonAscii = 0x80000000u;
+
+// Literals packed into up to four 64-bit shift-and words (a literal never
+// crosses a word); the byte table is indexed by the ASCII-lowered byte.
+struct PathTable {
+  uint64_t B[256][4];   // positions that accept the byte
+  uint64_t S[4], E[4];  // first / last position of each literal
+  uint8_t rule_of[256]; // word * 64 + bit of a literal's last position -> its rule
+  uint32_t words;
+};
+
+// Builds the table; false when the literals do not fit (more than 64 rules,
+// a literal shorter than 2 or longer than 64 bytes, over 256 positions).
+bool BuildPathTable(const std::vector<std::pair<std::string, uint32_t>>& lits, PathTable* t);
+
+class PathFilter {
+ public:
+  PathFilter(int device, const PathTable& t);
+  ~PathFilter();
+  bool ok() const { return err_.empty(); }
+  const std::string& error() const { return err_; }
+  // Paths [off[i], off[i+1]) of d_paths (device), i < n: the reported ones
+  // (any order).  Thread-safe (one call at a time per filter).  Runs on a
+  // high-priority stream of its own: a few microseconds of GPU time that
+  // should not queue behind a scan's kernels.
+  bool Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out, std::string* err);
+
+ private:
+  std::mutex mu_;
+  int device_ = 0;
+  std::string err_;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t done_ = nullptr;
+  PathTable* d_table_ = nullptr;
+  uint32_t* d_cnt_ = nullptr;
+  uint32_t* h_cnt_ = nullptr;
+  PathHit* d_out_ = nullptr;
+  PathHit* h_out_ = nullptr;  // pinned: a pageable read-back stalled the engine's stream (5 ms per C2 scan)
+  size_t cap_ = 0;
+};
+
+}  // namespace tsg

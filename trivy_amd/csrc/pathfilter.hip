@@ -1,0 +1,181 @@
+// GPU allow-path prefilter (pathfilter.h).
+#include "pathfilter.h"
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+namespace tsg {
+
+bool BuildPathTable(const std::vector<std::pair<std::string, uint32_t>>& lits, PathTable* t) {
+  std::memset(t, 0, sizeof(*t));
+  uint32_t w = 0, bit = 0;
+  for (auto& [lit, rule] : lits) {
+    const size_t k = lit.size();
+    if (k < 2 || k > 64 || rule >= 64) return false;
+    if (bit + k > 64) {  // a literal never crosses a word
+      w++;
+      bit = 0;
+    }
+    if (w >= 4) return false;
+    t->S[w] |= uint64_t(1) << bit;
+    for (size_t j = 0; j < k; j++) {
+      const uint8_t c = uint8_t(lit[j]);
+      if (c >= 'A' && c <= 'Z') return false;  // the literals are lowercased (Matcher::lits)
+      t->B[c][w] |= uint64_t(1) << (bit + j);
+    }
+    t->E[w] |= uint64_t(1) << (bit + k - 1);
+    t->rule_of[w * 64 + bit + k - 1] = uint8_t(rule);
+    bit += uint32_t(k);
+  }
+  t->words = w + 1;
+  return !lits.empty();
+}
+
+namespace {
+
+constexpr int kPathThreads = 256;
+
+__global__ __launch_bounds__(kPathThreads) void path_filter_kernel(const uint8_t* __restrict__ paths,
+                                                                   const uint64_t* __restrict__ off, uint32_t n,
+                                                                   const PathTable* __restrict__ T,
+                                                                   uint32_t* __restrict__ cnt,
+                                                                   PathHit* __restrict__ out) {
+  __shared__ uint64_t sB[256][4];
+  __shared__ uint8_t s_rule[256];
+  for (uint32_t i = threadIdx.x; i < 256 * 4; i += kPathThreads) (&sB[0][0])[i] = (&T->B[0][0])[i];
+  for (uint32_t i = threadIdx.x; i < 256; i += kPathThreads) s_rule[i] = T->rule_of[i];
+  __syncthreads();
+  uint64_t S[4], E[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    S[w] = T->S[w];
+    E[w] = T->E[w];
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t stride = gridDim.x * kPathThreads;
+  // whole waves iterate together (the ballot below needs every lane)
+  for (uint32_t base = blockIdx.x * kPathThreads + (threadIdx.x & ~63u); base < n; base += stride) {
+    const uint32_t i = base + lane;
+    uint32_t rec = 0;
+    uint64_t rules = 0;
+    bool emit = false;
+    if (i < n) {
+      uint64_t D[4] = {0, 0, 0, 0}, H[4] = {0, 0, 0, 0};
+      uint32_t high = 0;
+      const uint64_t e = off[i + 1];
+      for (uint64_t p = off[i]; p < e; p++) {
+        const uint32_t b = paths[p];
+        high |= b;
+        const uint32_t c = b + ((b - 'A') < 26u ? 32u : 0u);
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          D[w] = ((D[w] << 1) | S[w]) & sB[c][w];
+          H[w] |= D[w] & E[w];
+        }
+      }
+      if (high & 0x80u) {
+        rec = i | kPathNonAscii;
+        emit = true;
+      } else {
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+          for (uint64_t h = H[w]; h; h &= h - 1) rules |= uint64_t(1) << s_rule[w * 64 + __builtin_ctzll(h)];
+        rec = i;
+        emit = rules != 0;
+      }
+    }
+    const uint64_t m = __ballot(emit);
+    if (m) {
+      uint32_t at = 0;
+      if (lane == 0) at = atomicAdd(cnt, uint32_t(__popcll(m)));
+      at = __shfl(at, 0);
+      if (emit) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        PathHit h;
+        h.file = rec;
+        h.pad = 0;
+        h.rules = rules;
+        out[at + below] = h;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+PathFilter::PathFilter(int device, const PathTable& t) : device_(device) {
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi) != hipSuccess ||
+      hipEventCreateWithFlags(&done_, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&d_table_), sizeof(PathTable)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&d_cnt_), 64) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&h_cnt_), 64, hipHostMallocDefault) != hipSuccess ||
+      hipMemcpy(d_table_, &t, sizeof(PathTable), hipMemcpyHostToDevice) != hipSuccess)
+    err_ = "PathFilter: HIP setup failed";
+}
+
+PathFilter::~PathFilter() {
+  (void)hipSetDevice(device_);
+  if (d_out_) (void)hipFree(d_out_);
+  if (h_out_) (void)hipHostFree(h_out_);
+  if (d_table_) (void)hipFree(d_table_);
+  if (d_cnt_) (void)hipFree(d_cnt_);
+  if (h_cnt_) (void)hipHostFree(h_cnt_);
+  if (done_) (void)hipEventDestroy(done_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+bool PathFilter::Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out,
+                     std::string* err) {
+  std::lock_guard<std::mutex> g(mu_);
+  out->clear();
+  if (n == 0) return true;
+  auto fail = [&](const char* what, hipError_t e) {
+    *err = std::string("PathFilter: ") + what + ": " + hipGetErrorString(e);
+    return false;
+  };
+  // sleep-poll (as GpuEngine::WaitEvent): a spinning wait takes a core from the host pool
+  auto wait = [&]() {
+    hipError_t e = hipEventRecord(done_, stream_);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(done_)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    return e;
+  };
+  hipError_t e = hipSetDevice(device_);
+  if (e != hipSuccess) return fail("hipSetDevice", e);
+  if (cap_ < n) {
+    if (d_out_) (void)hipFree(d_out_);
+    if (h_out_) (void)hipHostFree(h_out_);
+    d_out_ = nullptr;
+    h_out_ = nullptr;
+    cap_ = 0;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&d_out_), size_t(n) * sizeof(PathHit))) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&h_out_), size_t(n) * sizeof(PathHit), hipHostMallocDefault)) !=
+            hipSuccess)
+      return fail("hipMalloc", e);
+    cap_ = n;
+  }
+  if ((e = hipMemsetAsync(d_cnt_, 0, 4, stream_)) != hipSuccess) return fail("hipMemsetAsync", e);
+  const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n) + kPathThreads - 1) / kPathThreads, 4096));
+  path_filter_kernel<<<grid, kPathThreads, 0, stream_>>>(d_paths, d_off, n, d_table_, d_cnt_, d_out_);
+  if ((e = hipGetLastError()) != hipSuccess) return fail("path_filter_kernel", e);
+  if ((e = hipMemcpyAsync(h_cnt_, d_cnt_, 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+      (e = wait()) != hipSuccess)
+    return fail("count read-back", e);
+  const uint32_t k = *h_cnt_;
+  if (k > n) {
+    *err = "PathFilter: record count out of range";
+    return false;
+  }
+  if (k && ((e = hipMemcpyAsync(h_out_, d_out_, size_t(k) * sizeof(PathHit), hipMemcpyDeviceToHost, stream_)) !=
+                hipSuccess ||
+            (e = wait()) != hipSuccess))
+    return fail("record read-back", e);
+  out->assign(h_out_, h_out_ + k);
+  return true;
+}
+
+}  // namespace tsg

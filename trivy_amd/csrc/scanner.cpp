@@ -395,6 +395,7 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
     }
   }
   BuildAllowPathFilter();
+  BuildPathFilter(device);
   const char* ht = std::getenv("TSG_HOST_THREADS");
   host_threads_ = ht ? std::atoi(ht) : 16;
   if (host_threads_ <= 0) host_threads_ = 1;
@@ -451,6 +452,20 @@ void SecretScanner::BuildAllowPathFilter() {
   ap_fast_ = ap_lits_.size() < 65535;
 }
 
+void SecretScanner::BuildPathFilter(int device) {
+  // the GPU prefilter reports every path holding one of a rule's literals
+  // (and every non-ASCII path): usable when no path rule goes unfiltered
+  if (!ap_fast_ || ap_always_ || device < 0 || std::getenv("TSG_GPU_ALLOW_PATH") &&
+                                                    std::atoi(std::getenv("TSG_GPU_ALLOW_PATH")) == 0)
+    return;
+  std::vector<std::pair<std::string, uint32_t>> lits;
+  for (auto& v : ap_lits_) lits.insert(lits.end(), v.begin(), v.end());
+  PathTable t;
+  if (!BuildPathTable(lits, &t)) return;
+  std::unique_ptr<PathFilter> pf(new PathFilter(device, t));
+  if (pf->ok()) path_filter_ = std::move(pf);
+}
+
 bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
   // Matcher::Match rejects an ASCII path holding none of a rule's (lowercase)
   // literals; here the literals are located in one pass over the lowered
@@ -497,19 +512,23 @@ bool SecretScanner::AllowPath(const uint8_t* p, size_t n) const {
         for (size_t i = 0; i + 1 < n; i++)
           if ((ap_first_[low[i] >> 6] >> (low[i] & 63)) & 1) check_at(i);  // L1-resident test first
       }
-      uint64_t mask = ap_always_ | lit_rules;
-      while (mask) {
-        const int i = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const Matcher& m = *allow_[size_t(i)].path;
-        if (m.simple ? m.MatchSimple(p, n) : (lit_rules >> i & 1) ? m.re->Match(p, int64_t(n)) : m.Match(p, n))
-          return true;
-      }
-      return false;
+      return AllowPathRules(p, n, lit_rules);
     }
   }
   for (auto& a : allow_)
     if (a.path && a.path->Match(p, n)) return true;
+  return false;
+}
+
+bool SecretScanner::AllowPathRules(const uint8_t* p, size_t n, uint64_t lit_rules) const {
+  uint64_t mask = ap_always_ | lit_rules;
+  while (mask) {
+    const int i = __builtin_ctzll(mask);
+    mask &= mask - 1;
+    const Matcher& m = *allow_[size_t(i)].path;
+    if (m.simple ? m.MatchSimple(p, n) : (lit_rules >> i & 1) ? m.re->Match(p, int64_t(n)) : m.Match(p, n))
+      return true;
+  }
   return false;
 }
 
@@ -603,7 +622,7 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 
 // Host-tail phase profile (TSG_TAIL_DEBUG=1 only; otherwise the timers are inert).
 const bool g_tail_debug = std::getenv("TSG_TAIL_DEBUG") != nullptr;
-std::atomic<int64_t> g_prof[8];
+std::atomic<int64_t> g_prof[10];  // [8] [9]: bytes memchr'd forward / backward by the line walks
 std::atomic<int64_t> g_wholefile_bytes{0}, g_wholefile_calls{0};  // TSG_TAIL_DEBUG: whole-content gate scans
 struct PhaseTimer {
   int k;
@@ -624,7 +643,7 @@ struct ScanScratch {
   std::vector<std::pair<uint32_t, Loc>> matched;
   std::vector<Loc> censor, locs, spans, merged;
   std::vector<std::pair<int64_t, int64_t>> nla;
-  std::vector<const Candidate*> hints;
+  std::vector<const Candidate*> hints, fhints;
   std::vector<Window> wins;
   std::vector<int64_t> m, span_nl;
 };
@@ -657,6 +676,12 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   for (size_t i = 0; i < nc && use_hints; i++)
     if (c[i].nl_back[0] != kNlUnknown && c[i].nl_back[0] != 0) hints.push_back(&c[i]);  // 0: never a GPU value
   std::sort(hints.begin(), hints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
+  // and the first three at or after it (Candidate::nl_fwd)
+  std::vector<const Candidate*>& fhints = S.fhints;
+  fhints.clear();
+  for (size_t i = 0; i < nc && use_hints; i++)
+    if (c[i].nl_fwd[0] != kNlUnknown) fhints.push_back(&c[i]);
+  std::sort(fhints.begin(), fhints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
 
   // the candidates are sorted by rule: real rules first, then the exclude-block rules
   const uint32_t n_real = uint32_t(rules_.size());
@@ -939,6 +964,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
       }
     }
     const void* q = memrchr(content, '\n', size_t(pos));
+    if (g_tail_debug) g_prof[9] += q ? pos - (static_cast<const uint8_t*>(q) - content) : pos;
     return q ? int64_t(static_cast<const uint8_t*>(q) - content) : -1;
   };
   auto line_start_of = [&](int64_t pos) {  // after the last visible '\n' before pos
@@ -952,12 +978,53 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
     }
     return int64_t(0);
   };
+  auto next_nl = [&](int64_t pos) -> int64_t {  // the first '\n' in [pos, len), or -1
+    auto it = std::upper_bound(fhints.begin(), fhints.end(), pos,
+                               [](int64_t v, const Candidate* h) { return v < h->wlo; });
+    if (it != fhints.begin()) {  // a window starting at or below pos: its list covers [wlo, third '\n']
+      const Candidate& h = **(it - 1);
+      for (int k = 0; k < 3; k++) {
+        if (h.nl_fwd[k] == kNlUnknown) break;
+        if (h.nl_fwd[k] == kNlNone) return -1;  // every '\n' after wlo is listed, all < pos
+        const int64_t at = h.wlo + int64_t(h.nl_fwd[k]);
+        if (at >= pos) return at;
+      }
+    }
+    int64_t lim = len;  // no '\n' in [pos, lim) is known; `known` is the first one at or after lim
+    int64_t known = -1;
+    if (it != fhints.end()) {  // the next window above pos: the '\n' around its wlo are listed
+      const Candidate& h = **it;
+      lim = h.wlo;
+      known = h.nl_fwd[0] == kNlNone ? -1 : h.wlo + int64_t(h.nl_fwd[0]);
+      if (h.nl_back[0] != kNlUnknown && h.nl_back[0] != 0) {  // the last three before wlo, nearest first
+        for (int k = 0; k < 3; k++) {
+          if (h.nl_back[k] == kNlUnknown) break;
+          if (h.nl_back[k] == kNlNone) {  // every '\n' before wlo is listed
+            lim = pos;
+            break;
+          }
+          const int64_t at = h.wlo - int64_t(h.nl_back[k]);
+          if (at < pos) {  // the listed ones at or after pos are all there are in [pos, wlo)
+            lim = pos;
+            break;
+          }
+          lim = at;  // no other '\n' in [at, wlo)
+          known = at;
+        }
+      }
+    }
+    if (lim > pos) {
+      const void* q = std::memchr(content + pos, '\n', size_t(lim - pos));
+      if (g_tail_debug) g_prof[8] += q ? static_cast<const uint8_t*>(q) - (content + pos) : lim - pos;
+      if (q) return int64_t(static_cast<const uint8_t*>(q) - content);
+    }
+    return known;
+  };
   auto line_end_of = [&](int64_t pos) {  // first visible '\n' at or after pos, or len
     int64_t p = pos;
     while (p < len) {
-      const void* q = std::memchr(content + p, '\n', size_t(len - p));
-      if (!q) return len;
-      int64_t at = int64_t(static_cast<const uint8_t*>(q) - content);
+      const int64_t at = next_nl(p);
+      if (at < 0) return len;
       const Loc* z = in_span(at);
       if (!z) return at;
       p = z->e;
@@ -1115,6 +1182,28 @@ std::vector<uint8_t> SecretScanner::AllowedPaths(const BatchInput& in) const {
   bool any_path_rule = false;
   for (auto& a : allow_)
     if (a.path) any_path_rule = true;
+  if (any_path_rule && path_filter_ && in.dev_paths && in.dev_path_off) {
+    // the GPU reports the paths that can match; every other path is not allowed
+    std::vector<PathHit> hits;
+    std::string perr;
+    if (path_filter_->Run(in.dev_paths, in.dev_path_off, in.n_files, &hits, &perr)) {
+      const size_t blocks = (hits.size() + 1023) / 1024;
+      ParallelFor(blocks, host_threads_, [&](size_t b) {
+        const size_t lo = b * 1024, hi = std::min<size_t>(lo + 1024, hits.size());
+        for (size_t k = lo; k < hi; k++) {
+          const uint32_t f = hits[k].file & ~kPathNonAscii;
+          if (f >= in.n_files) continue;
+          const char* p = in.paths[f];
+          const size_t n = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
+          const uint8_t* P = reinterpret_cast<const uint8_t*>(p);
+          const bool a = (hits[k].file & kPathNonAscii) ? AllowPath(P, n) : AllowPathRules(P, n, hits[k].rules);
+          allowed[f] = a ? 1 : 0;
+        }
+      });
+      return allowed;
+    }
+    // a HIP error: fall through to the host pass (the scan itself reports GPU failures)
+  }
   if (any_path_rule) {
     size_t blocks = (in.n_files + 4095) / 4096;
     ParallelFor(blocks, host_threads_, [&](size_t b) {
@@ -1235,8 +1324,8 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
                  g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
   if (g_tail_debug)
-    std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB\n", (long long)g_wholefile_calls.load(),
-                 g_wholefile_bytes.load() / 1e6);
+    std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB; line walks: %.1f MB forward, %.1f MB back\n",
+                 (long long)g_wholefile_calls.load(), g_wholefile_bytes.load() / 1e6, g_prof[8] / 1e6, g_prof[9] / 1e6);
   out->found_files.reserve(nf);
   out->found.reserve(nf);
   for (size_t k = 0; k < nf; k++) {

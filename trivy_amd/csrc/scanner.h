@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "pathfilter.h"
 #include "goregex.h"
 #include "rules.h"
 
@@ -123,6 +124,8 @@ struct BatchInput {
   const uint8_t* binary = nullptr;      // optional per-file Binary flag
   const uint8_t* transform = nullptr;   // optional per-file pre-transform (xform.h) run on the GPU: then
                                         // host_arena holds the bytes as read (host-resident batches only)
+  const uint8_t* dev_paths = nullptr;   // optional: the paths packed in HBM (the allow-path prefilter runs
+  const uint64_t* dev_path_off = nullptr;  // on the GPU, pathfilter.h); n_files + 1 offsets, device
 };
 
 struct HostStats {
@@ -194,12 +197,17 @@ class SecretScanner {
   // rules that have a required literal starting with that pair; rules without
   // a literal prefilter (or with a 1-byte literal) are always evaluated.
   void BuildAllowPathFilter();
+  void BuildPathFilter(int device);
   bool ap_fast_ = false;
   uint64_t ap_always_ = 0;
   std::vector<uint16_t> ap_pair_;  // 65536: 1 + index into ap_lits_, 0 = no literal starts with the pair
   uint64_t ap_first_[4] = {};      // lowercase bytes that begin some literal (checked before ap_pair_)
   std::vector<uint8_t> ap_c0_, ap_c1_;  // distinct first-two-byte pairs of the literals (SIMD prefilter)
   std::vector<std::vector<std::pair<std::string, uint32_t>>> ap_lits_;  // (literal, allow rule) per pair
+  // the rules of `lit_rules` (their literal is in the ASCII path) plus the unfiltered ones, exactly
+  bool AllowPathRules(const uint8_t* p, size_t n, uint64_t lit_rules) const;
+  // GPU allow-path prefilter (pathfilter.h): built when every path rule has usable literals
+  std::unique_ptr<PathFilter> path_filter_;
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.

@@ -10,16 +10,15 @@ namespace tsg {
 
 constexpr uint8_t kXformNone = 0, kXformStripCR = 1, kXformPrintable = 2;
 
-// len[f] = transformed length of file f (len[n_files] = 0); raw has 16 readable bytes past off[n_files].
-hipError_t XformLengths(const uint8_t* raw, const uint64_t* off, const uint8_t* kind, uint32_t n_files, uint64_t* len,
-                        hipStream_t s);
-// xoff = exclusive prefix sums of len (n_files + 1 entries)
-hipError_t XformScanBytes(uint32_t n_files, size_t* bytes);
-hipError_t XformScan(void* temp, size_t temp_bytes, const uint64_t* len, uint64_t* xoff, uint32_t n_files,
-                     hipStream_t s);
-// out[xoff[f] ..) = transform(kind[f], raw[off[f] .. off[f+1]))
-hipError_t XformCopy(const uint8_t* raw, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
-                     const uint64_t* xoff, uint8_t* out, hipStream_t s);
+// Flat transform of a batch (n_files + 1 offsets into raw; raw has 64
+// readable bytes past n_bytes).  XformPlan writes xoff (n_files + 1 entries:
+// the transformed offsets) using `scratch` (XformScratchBytes); XformWrite,
+// with the same scratch, writes out[xoff[f] ..) = transform(kind[f], file f).
+size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files);
+hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
+                     void* scratch, uint64_t* xoff, hipStream_t s);
+hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
+                      const void* scratch, uint8_t* out, hipStream_t s);
 // dst[dst_off[i] ..) = src[xoff[files[i]] .. xoff[files[i] + 1])
 hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t* files, const uint64_t* dst_off,
                        uint32_t n, uint8_t* dst, hipStream_t s);

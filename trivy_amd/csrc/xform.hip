@@ -7,17 +7,12 @@
 //   kind 2  utils.ExtractPrintableBytes (pkg/fanal/utils/utils.go:128-160):
 //           runs of more than 4 unicode.IsPrint bytes, each followed by '\n'
 //           (.pyc binaries, secret.go:112-117)
-// Three launches per chunk: lengths (one wave per file: SWAR '\r' counts over
-// 16-B loads, or the printable-run plan), an exclusive scan of the lengths
-// into the transformed offsets (hipcub), the copy (one wave per file).  Files
-// that keep every byte -- all of a layer but its CRLF files and .pyc binaries
-// -- are moved as 16-B-aligned destination blocks, each lane funnel-shifting
-// the two aligned source blocks around its block by the file's (uniform)
-// source/destination misalignment: coalesced 16-B loads and stores, byte
-// stores only in a file's first and last block (shared with the neighbouring
-// files' waves).  CRLF files compact 1 KiB per step (per-lane kept-byte
-// counts, a wave prefix sum).  A gather packs chosen files of the transformed
-// arena for the host's exact pass with the same shifted block copy.
+// Byte-parallel (see the kernels' comment below): every output byte depends
+// on at most 5 input bytes before it and 4 after it, so a lane per 16-B block
+// computes its block's output with no per-file serial pass; two passes
+// (count, write) around an exclusive scan of the per-KiB output counts.  A
+// gather packs chosen files of the transformed arena for the host's exact
+// pass (shifted 16-B block copies).
 #include "xform.h"
 
 #include <hipcub/hipcub.hpp>
@@ -28,29 +23,6 @@ namespace {
 constexpr int kXThreads = 256;
 
 __device__ __forceinline__ uint4 xload16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
-
-__device__ __forceinline__ uint32_t xbyte(const uint4& v, uint32_t i) {
-  const uint32_t w = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
-  return (w >> (8 * (i & 3))) & 0xFFu;
-}
-
-// Bytes of the word at arena position wp that lie in [a, b), as a byte mask.
-__device__ __forceinline__ uint32_t byte_mask(uint64_t wp, uint64_t a, uint64_t b) {
-  const uint32_t lo = a > wp ? uint32_t(a - wp < 4 ? a - wp : 4) : 0u;  // bytes before a
-  const uint32_t hi = b > wp ? uint32_t(b - wp < 4 ? b - wp : 4) : 0u;  // bytes before b
-  const uint32_t mhi = hi >= 4 ? ~0u : (1u << (8 * hi)) - 1u;
-  const uint32_t mlo = lo >= 4 ? 0u : ~((1u << (8 * lo)) - 1u);
-  return mhi & mlo;
-}
-
-// '\r' bytes of w among the bytes of mask m: x = w ^ 0x0D.. is zero exactly
-// in CR bytes (forced non-zero outside m); bit 7 of ((x & 0x7F..) + 0x7F..) | x
-// marks the non-zero bytes.
-__device__ __forceinline__ uint32_t cr_count4(uint32_t w, uint32_t m) {
-  const uint32_t x = (w ^ 0x0D0D0D0Du) | ~m;
-  const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-  return 4u - uint32_t(__popc(nz));
-}
 
 // dst [d, d + n) = src [s, s + n) for one wave (see the file comment).  src
 // has 16 readable bytes past s + n; out is 16-B aligned.
@@ -95,12 +67,6 @@ __device__ void copy_shifted(const uint8_t* __restrict__ src, uint64_t s, uint8_
 // unicode.IsPrint(rune(b)) of a byte (Latin-1): graphic or ASCII space; not U+00A0, U+00AD
 __device__ __forceinline__ bool xprint(uint32_t b) { return (b >= 0x20 && b <= 0x7E) || (b >= 0xA1 && b != 0xAD); }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-  return v;
-}
-
 __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t lane) {  // exclusive prefix over lanes
   uint32_t x = v;
 #pragma unroll
@@ -111,228 +77,214 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t lane) {  // e
   return x - v;
 }
 
-// ExtractPrintableBytes on one wave (kind 2).  The file is cut into 64 lane
-// chunks.  Pass 1: each lane scans its chunk -- leading printable run (pre),
-// trailing run (suf), the output of the runs strictly inside (inner), whether
-// the chunk is all printable.  Lane 0 then walks the 64 chunks in order,
-// joining the runs that cross chunk boundaries: it places every run's output
-// and decides it kept (> 4 bytes) or not, and leaves each lane its positions.
-// Pass 2 (copy kernel): each lane writes its chunk's share -- the head of a
-// run that began in earlier chunks, its inner runs (the first 4 bytes of a run
-// wait in registers until the run is long enough), the tail of a run that
-// continues into later chunks.
-struct PycPlan {
-  uint64_t c0[64], c1[64];           // chunk [c0, c1) (file-relative)
-  uint64_t pre[64], suf[64], inner[64];
-  uint8_t full[64];
-  uint64_t pos_pre[64], pos_inner[64], pos_suf[64];  // output positions (file-relative)
-  uint8_t keep_pre[64], end_pre[64], keep_suf[64];   // end_pre: the run through the chunk head ends in it
-  uint64_t total;
-  uint64_t final_pos;  // the '\n' after a kept run that reaches the file end
-  uint8_t final_keep;
+// ---------------------------------------------------------------------------
+// Byte-parallel transform.  Every output byte is a function of a few input
+// bytes around it, so the transform is a stream compaction with local rules:
+//   kind 0: every byte is kept;
+//   kind 1: every byte but '\r' is kept;
+//   kind 2: ExtractPrintableBytes keeps a printable byte iff its run of
+//     printable bytes is longer than 4, i.e. some 5 consecutive printable
+//     bytes of the file cover it; a non-printable byte emits the '\n' that
+//     closes the run before it iff the 5 bytes before it are printable; the
+//     file's last byte emits the closing '\n' of a run reaching the file end
+//     iff the last 5 bytes are printable (utils.go:128-160).
+// A lane owns one 16-B block, a wave one 1-KiB tile.  Pass 1 counts each
+// tile's output bytes and records where each file starts inside its tile;
+// an exclusive scan over the tiles and a per-file fix-up give the
+// transformed offsets; pass 2 recomputes the bytes, packs the wave's output
+// in LDS at its global 16-B phase and writes aligned 16-B stores (byte stores
+// only at the tile's two ragged ends, which the neighbouring tiles share).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kXTile = 1024;
+
+__global__ __launch_bounds__(kXThreads) void xf_chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
+                                                                 uint32_t* __restrict__ chunk_file) {
+  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < n_files; f += gridDim.x * blockDim.x) {
+    const uint64_t s = off[f], e = off[f + 1];
+    for (uint64_t c = (s + kXTile - 1) / kXTile; c * kXTile < e; c++) chunk_file[c] = f;
+  }
+}
+
+// The 32 bytes around a lane's block: [blk - 8, blk + 24) as 8 words (the
+// neighbours' words by wave shuffles; the wave's edge lanes load theirs).
+struct XWindow {
+  uint32_t w[8];
+  __device__ __forceinline__ uint32_t byte(int i) const { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
 };
 
-__device__ void pyc_plan(const uint8_t* in, uint64_t n, uint32_t lane, PycPlan* P) {
-  const uint64_t cs = (n + 63) / 64;
-  const uint64_t c0 = lane * cs < n ? lane * cs : n, c1 = c0 + cs < n ? c0 + cs : n;
-  uint64_t cur = 0, pre = 0, inner = 0;
-  bool seen = false;  // a non-printable byte in the chunk
-  for (uint64_t i = c0; i < c1; i++) {
-    if (xprint(in[i])) {
-      cur++;
-      continue;
-    }
-    if (!seen) pre = cur;
-    else if (cur > 4) inner += cur + 1;
-    cur = 0;
-    seen = true;
-  }
-  P->c0[lane] = c0;
-  P->c1[lane] = c1;
-  P->full[lane] = seen ? 0 : 1;
-  P->pre[lane] = seen ? pre : c1 - c0;
-  P->suf[lane] = seen ? cur : 0;
-  P->inner[lane] = inner;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+__device__ __forceinline__ XWindow x_window(const uint8_t* raw, uint64_t n_bytes, uint64_t blk, uint32_t lane,
+                                            const uint4& v) {
+  XWindow W;
+  W.w[2] = v.x;
+  W.w[3] = v.y;
+  W.w[4] = v.z;
+  W.w[5] = v.w;
+  W.w[0] = __shfl_up(v.z, 1);
+  W.w[1] = __shfl_up(v.w, 1);
+  W.w[6] = __shfl_down(v.x, 1);
+  W.w[7] = __shfl_down(v.y, 1);
   if (lane == 0) {
-    uint64_t emitted = 0, open = 0, start_pos = 0;
-    int first = -1;  // first lane of the open run (-1: none); first_suf: it starts in that lane's tail
-    bool first_suf = false;
-    auto close = [&](int last) {  // the open run ends in lane `last` (or at the file end: last = -1)
-      const bool keep = open > 4;
-      for (int j = first < 0 ? 64 : first; j < 64 && (last < 0 || j <= last); j++) {
-        if (j == first && first_suf) P->keep_suf[j] = keep;
-        else P->keep_pre[j] = keep;
-      }
-      if (keep) emitted = start_pos + open + 1;
-      if (last < 0) {
-        P->final_keep = keep;
-        P->final_pos = start_pos + open;
-      }
-      open = 0;
-      first = -1;
-    };
-    P->final_keep = 0;
-    for (int i = 0; i < 64; i++) {
-      P->keep_pre[i] = 0;
-      P->end_pre[i] = 0;
-      P->keep_suf[i] = 0;
-      P->pos_suf[i] = 0;
-    }
-    for (int i = 0; i < 64; i++) {
-      const uint64_t len = P->c1[i] - P->c0[i];
-      if (len == 0) continue;
-      if (P->full[i]) {
-        if (first < 0) {
-          first = i;
-          first_suf = false;
-          start_pos = emitted;
-        }
-        P->pos_pre[i] = start_pos + open;
-        open += len;
-        continue;
-      }
-      // the run through the chunk head (possibly empty) ends here
-      if (first < 0) {
-        first = i;
-        first_suf = false;
-        start_pos = emitted;
-      }
-      P->pos_pre[i] = start_pos + open;
-      open += P->pre[i];
-      P->end_pre[i] = 1;
-      close(i);
-      P->pos_inner[i] = emitted;
-      emitted += P->inner[i];
-      if (P->suf[i] > 0) {
-        first = i;
-        first_suf = true;
-        start_pos = emitted;
-        P->pos_suf[i] = emitted;
-        open = P->suf[i];
-      }
-    }
-    if (first >= 0) close(-1);
-    P->total = emitted;
+    const uint2 p = blk >= 8 ? *reinterpret_cast<const uint2*>(raw + blk - 8) : make_uint2(0, 0);
+    W.w[0] = p.x;
+    W.w[1] = p.y;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane == 63) {
+    const uint2 p = blk + 16 < n_bytes ? *reinterpret_cast<const uint2*>(raw + blk + 16) : make_uint2(0, 0);
+    W.w[6] = p.x;
+    W.w[7] = p.y;
+  }
+  return W;
 }
 
-// Pass 2 for lane `lane` (plan from pyc_plan).
-__device__ void pyc_write(const uint8_t* in, uint32_t lane, const PycPlan* P, uint8_t* out) {
-  const uint64_t c0 = P->c0[lane], c1 = P->c1[lane];
-  if (lane == 0 && P->final_keep) out[P->final_pos] = '\n';
-  if (c1 <= c0) return;
-  uint64_t i = c0;
-  // head: the bytes of the run through the chunk head
-  const uint64_t pre = P->pre[lane];
-  if (P->keep_pre[lane])
-    for (uint64_t k = 0; k < pre; k++) out[P->pos_pre[lane] + k] = in[c0 + k];
-  if (P->full[lane]) return;
-  if (P->end_pre[lane] && P->keep_pre[lane]) out[P->pos_pre[lane] + pre] = '\n';
-  i = c0 + pre + 1;  // past the first non-printable byte
-  // inner runs up to the chunk's last non-printable byte
-  const uint64_t tail0 = c1 - P->suf[lane];  // the suffix run starts here
-  uint64_t w = P->pos_inner[lane], run = 0;
-  uint8_t held[4];
-  for (; i < tail0; i++) {
-    const uint8_t b = in[i];
-    if (xprint(b)) {
-      if (run < 4) {
-        held[run] = b;
-      } else {
-        if (run == 4)
-          for (int k = 0; k < 4; k++) out[w + k] = held[k];
-        out[w + run] = b;
-      }
-      run++;
-      continue;
-    }
-    if (run > 4) {
-      out[w + run] = '\n';
-      w += run + 1;
-    }
-    run = 0;
+// Kind-2 masks over the window for the file [fs, fe): bit i of K = window
+// byte i is a kept printable byte, bit i of C = window byte i closes a kept
+// run (non-printable, the 5 bytes before it printable), bit i of Z = the file's
+// last byte is window byte i and closes a run reaching the file end.
+struct XMasks {
+  uint32_t K, C, Z;
+};
+__device__ __forceinline__ XMasks x_masks(const XWindow& W, uint64_t blk, uint64_t fs, uint64_t fe) {
+  uint32_t P = 0, in = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    const int64_t pos = int64_t(blk) - 8 + i;
+    const bool inside = pos >= int64_t(fs) && pos < int64_t(fe);
+    in |= uint32_t(inside) << i;
+    P |= uint32_t(inside && xprint(W.byte(i))) << i;
   }
-  // the suffix run (its '\n' is written where it ends)
-  if (P->keep_suf[lane])
-    for (uint64_t k = 0; k < P->suf[lane]; k++) out[P->pos_suf[lane] + k] = in[tail0 + k];
+  const uint32_t Q = P & (P >> 1) & (P >> 2) & (P >> 3) & (P >> 4);  // bit k: bytes k .. k+4 printable
+  XMasks m;
+  m.K = (Q | (Q << 1) | (Q << 2) | (Q << 3) | (Q << 4)) & P;
+  m.C = ~P & in & (Q << 5);
+  const int64_t last = int64_t(fe) - 1 - (int64_t(blk) - 8);  // window index of the file's last byte
+  m.Z = (last >= 4 && last < 32 && ((Q >> (last - 4)) & 1u)) ? (1u << last) : 0u;
+  return m;
 }
 
-__global__ __launch_bounds__(kXThreads) void xform_len_kernel(const uint8_t* __restrict__ raw,
-                                                              const uint64_t* __restrict__ off,
-                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
-                                                              uint64_t* __restrict__ len) {
-  __shared__ PycPlan s_plan[kXThreads / 64];
-  PycPlan* plan = &s_plan[threadIdx.x >> 6];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t waves = gridDim.x * (kXThreads / 64);
-  for (uint32_t f = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); f < n_files; f += waves) {
-    const uint64_t a = off[f], b = off[f + 1];
-    const uint32_t k = kind[f];
-    uint64_t out = b - a;
-    if (k == 1) {
-      uint32_t cr = 0;
-      for (uint64_t blk = (a & ~uint64_t(15)) + 16 * lane; blk < b; blk += 1024) {
-        const uint4 v = xload16(raw + blk);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) cr += cr_count4(w[q], byte_mask(blk + 4 * q, a, b));
-      }
-      out -= wave_sum(cr);
-    } else if (k == 2) {
-      pyc_plan(raw + a, b - a, lane, plan);
-      out = plan->total;
-    }
-    if (lane == 0) len[f] = out;
+// Walks a lane's 16 bytes in file order.  emit(byte) is called per output
+// byte, start(f) at each file start inside the block (before its bytes).
+template <typename Emit, typename Start>
+__device__ __forceinline__ void x_lane(const uint8_t* raw, uint64_t n_bytes, const uint64_t* __restrict__ off,
+                                       const uint8_t* __restrict__ kind, uint32_t n_files,
+                                       const uint32_t* __restrict__ chunk_file, uint64_t blk, const XWindow& W,
+                                       Emit emit, Start start) {
+  if (blk >= n_bytes) return;
+  uint32_t f = chunk_file[blk / kXTile];
+  uint64_t fs = off[f], fe = off[f + 1];
+  while (fe <= blk && f + 1 < n_files) {  // files ending before the block (the chunk map names the chunk's first)
+    f++;
+    fs = fe;
+    fe = off[f + 1];
+    if (fs >= blk) start(f);  // empty files at the block start
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) len[n_files] = 0;
+  if (fs == blk) start(f);
+  uint32_t k = kind[f];
+  XMasks m = {0, 0, 0};
+  if (k == 2) m = x_masks(W, blk, fs, fe);
+  const uint64_t end = blk + 16 < n_bytes ? blk + 16 : n_bytes;
+  for (uint64_t p = blk; p < end; p++) {
+    while (p >= fe && f + 1 < n_files) {
+      f++;
+      fs = fe;
+      fe = off[f + 1];
+      start(f);
+      k = kind[f];
+      if (k == 2) m = x_masks(W, blk, fs, fe);
+    }
+    const int i = int(p - blk) + 8;
+    const uint32_t b = W.byte(i);
+    if (k == 0) {
+      emit(b);
+    } else if (k == 1) {
+      if (b != '\r') emit(b);
+    } else {
+      if ((m.C >> i) & 1u) emit('\n');
+      if ((m.K >> i) & 1u) emit(b);
+      if ((m.Z >> i) & 1u) emit('\n');
+    }
+  }
 }
 
-__global__ __launch_bounds__(kXThreads) void xform_copy_kernel(const uint8_t* __restrict__ raw,
-                                                               const uint64_t* __restrict__ off,
-                                                               const uint8_t* __restrict__ kind, uint32_t n_files,
-                                                               const uint64_t* __restrict__ xoff,
-                                                               uint8_t* __restrict__ out) {
-  __shared__ PycPlan s_plan[kXThreads / 64];
-  PycPlan* plan = &s_plan[threadIdx.x >> 6];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t waves = gridDim.x * (kXThreads / 64);
-  for (uint32_t f = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); f < n_files; f += waves) {
-    const uint64_t a = off[f], b = off[f + 1];
-    const uint32_t k = kind[f];
-    uint8_t* dst = out + xoff[f];
-    if (k == 2) {
-      pyc_plan(raw + a, b - a, lane, plan);
-      pyc_write(raw + a, lane, plan, dst);
-      continue;
+__global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __restrict__ raw, uint64_t n_bytes,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint8_t* __restrict__ kind, uint32_t n_files,
+                                                             const uint32_t* __restrict__ chunk_file,
+                                                             uint32_t* __restrict__ tile_cnt,
+                                                             uint32_t* __restrict__ fstart) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint64_t waves = uint64_t(gridDim.x) * (kXThreads / 64);
+  for (uint64_t t = uint64_t(blockIdx.x) * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
+    const uint64_t blk = t * kXTile + 16 * uint64_t(lane);
+    const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
+    const XWindow W = x_window(raw, n_bytes, blk, lane, v);
+    uint32_t c = 0;
+    bool starts = false;
+    x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t) { c++; },
+           [&](uint32_t) { starts = true; });
+    const uint32_t ex = wave_excl(c, lane);
+    if (lane == 63) tile_cnt[t] = ex + c;
+    if (starts) {  // the files starting in this block: their tile-relative output offsets
+      uint32_t c2 = ex;
+      x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t) { c2++; },
+             [&](uint32_t f) { fstart[f] = c2; });
     }
-    if (k != 1 || xoff[f + 1] - xoff[f] == b - a) {  // every byte kept: the shifted block copy
-      copy_shifted(raw, a, out, xoff[f], b - a, lane);
-      continue;
-    }
-    uint64_t written = 0;
-    for (uint64_t t0 = a & ~uint64_t(15); t0 < b; t0 += 1024) {
-      const uint64_t blk = t0 + 16 * lane;
-      const uint4 v = blk < b ? xload16(raw + blk) : make_uint4(0, 0, 0, 0);
-      uint32_t keep = 0;  // bit i: byte blk + i is kept
-#pragma unroll
-      for (uint32_t i = 0; i < 16; i++) {
-        const bool in = blk + i >= a && blk + i < b;
-        keep |= uint32_t(in && !(k == 1 && xbyte(v, i) == '\r')) << i;
+  }
+}
+
+__global__ __launch_bounds__(kXThreads) void xf_fixup_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
+                                                             uint64_t n_bytes, const uint64_t* __restrict__ tile_pre,
+                                                             const uint32_t* __restrict__ fstart,
+                                                             uint64_t* __restrict__ xoff) {
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_files; f += gridDim.x * blockDim.x) {
+    const uint64_t s = f < n_files ? off[f] : n_bytes;
+    xoff[f] = s < n_bytes ? tile_pre[s / kXTile] + fstart[f] : tile_pre[n_tiles];
+  }
+}
+
+__global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __restrict__ raw, uint64_t n_bytes,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint8_t* __restrict__ kind, uint32_t n_files,
+                                                             const uint32_t* __restrict__ chunk_file,
+                                                             const uint64_t* __restrict__ tile_pre,
+                                                             uint8_t* __restrict__ out) {
+  // a tile emits at most 1024 + 1024 / 5 + 16 bytes (a '\n' per closed run of >= 5 bytes)
+  constexpr uint32_t kStage = 1280 + 32;
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kXThreads / 64][kStage];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint8_t* S = s_out[threadIdx.x >> 6];
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint64_t waves = uint64_t(gridDim.x) * (kXThreads / 64);
+  for (uint64_t t = uint64_t(blockIdx.x) * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
+    const uint64_t blk = t * kXTile + 16 * uint64_t(lane);
+    const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
+    const XWindow W = x_window(raw, n_bytes, blk, lane, v);
+    uint32_t c = 0;
+    x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t) { c++; }, [&](uint32_t) {});
+    const uint32_t ex = wave_excl(c, lane);
+    const uint32_t total = __shfl(ex + c, 63);
+    const uint64_t start = tile_pre[t];
+    const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
+    uint32_t at = phase + ex;
+    x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t b) { S[at++] = uint8_t(b); },
+           [&](uint32_t) {});
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t base = start - phase, end = start + total;
+    for (uint32_t q = 16 * lane; base + q < end; q += 1024) {
+      const uint64_t g = base + q;
+      if (g >= start && g + 16 <= end) {
+        *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(S + q);
+      } else {  // the ragged ends: only this tile's bytes
+        for (uint32_t j = 0; j < 16; j++)
+          if (g + j >= start && g + j < end) out[g + j] = S[q + j];
       }
-      const uint32_t c = __popc(keep);
-      const uint64_t at = written + wave_excl(c, lane);
-      uint32_t j = 0;
-#pragma unroll
-      for (uint32_t i = 0; i < 16; i++)
-        if ((keep >> i) & 1u) dst[at + j++] = uint8_t(xbyte(v, i));
-      written += wave_sum(c);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -357,26 +309,67 @@ uint32_t grid_for(uint32_t n_waves) {
 
 }  // namespace
 
-hipError_t XformLengths(const uint8_t* raw, const uint64_t* off, const uint8_t* kind, uint32_t n_files, uint64_t* len,
-                        hipStream_t s) {
-  xform_len_kernel<<<grid_for(n_files), kXThreads, 0, s>>>(raw, off, kind, n_files, len);
+// Scratch of the flat transform: chunk map | tile counts | tile prefix | file starts | scan temp.
+struct XformScratch {
+  size_t chunk_file, tile_cnt, tile_pre, fstart, scan, scan_bytes, total;
+};
+
+static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  XformScratch L;
+  size_t scan = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, static_cast<const uint32_t*>(nullptr),
+                                         static_cast<uint64_t*>(nullptr), int(n_tiles) + 1);
+  auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+  L.chunk_file = 0;
+  L.tile_cnt = up(L.chunk_file + (n_tiles + 1) * 4);
+  L.tile_pre = up(L.tile_cnt + (n_tiles + 1) * 4);
+  L.fstart = up(L.tile_pre + (n_tiles + 1) * 8);
+  L.scan = up(L.fstart + (size_t(n_files) + 1) * 4);
+  L.scan_bytes = scan;
+  L.total = up(L.scan + scan + 16);
+  return L;
+}
+
+size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files) { return ScratchLayout(n_bytes, n_files).total; }
+
+hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
+                     void* scratch, uint64_t* xoff, hipStream_t s) {
+  const XformScratch L = ScratchLayout(n_bytes, n_files);
+  uint8_t* sc = static_cast<uint8_t*>(scratch);
+  uint32_t* chunk_file = reinterpret_cast<uint32_t*>(sc + L.chunk_file);
+  uint32_t* tile_cnt = reinterpret_cast<uint32_t*>(sc + L.tile_cnt);
+  uint64_t* tile_pre = reinterpret_cast<uint64_t*>(sc + L.tile_pre);
+  uint32_t* fstart = reinterpret_cast<uint32_t*>(sc + L.fstart);
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  hipError_t e;
+  if ((e = hipMemsetAsync(tile_cnt, 0, (n_tiles + 1) * 4, s)) != hipSuccess) return e;
+  if (n_files) {
+    xf_chunk_map_kernel<<<grid_for((n_files + 63) / 64), kXThreads, 0, s>>>(off, n_files, chunk_file);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (n_tiles) {
+    const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
+    xf_count_kernel<<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  size_t sb = L.scan_bytes;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(sc + L.scan, sb, tile_cnt, tile_pre, int(n_tiles) + 1, s)) != hipSuccess)
+    return e;
+  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, n_bytes, tile_pre, fstart, xoff);
   return hipGetLastError();
 }
 
-hipError_t XformScanBytes(uint32_t n_files, size_t* bytes) {
-  *bytes = 0;
-  return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, static_cast<const uint64_t*>(nullptr),
-                                          static_cast<uint64_t*>(nullptr), int(n_files) + 1);
-}
-
-hipError_t XformScan(void* temp, size_t temp_bytes, const uint64_t* len, uint64_t* xoff, uint32_t n_files,
-                     hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, len, xoff, int(n_files) + 1, s);
-}
-
-hipError_t XformCopy(const uint8_t* raw, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
-                     const uint64_t* xoff, uint8_t* out, hipStream_t s) {
-  xform_copy_kernel<<<grid_for(n_files), kXThreads, 0, s>>>(raw, off, kind, n_files, xoff, out);
+hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
+                      const void* scratch, uint8_t* out, hipStream_t s) {
+  const XformScratch L = ScratchLayout(n_bytes, n_files);
+  const uint8_t* sc = static_cast<const uint8_t*>(scratch);
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  if (!n_tiles) return hipSuccess;
+  const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
+  xf_write_kernel<<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files,
+                                          reinterpret_cast<const uint32_t*>(sc + L.chunk_file),
+                                          reinterpret_cast<const uint64_t*>(sc + L.tile_pre), out);
   return hipGetLastError();
 }
 

@@ -40,7 +40,8 @@ class _CGlobal(c.Structure):
 class _CBatch(c.Structure):
     _fields_ = [("n_files", c.c_uint32), ("host_arena", c.c_void_p), ("host_offsets", c.c_void_p),
                 ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.c_void_p),
-                ("path_lens", c.c_void_p), ("binary", c.c_void_p), ("transform", c.c_void_p)]
+                ("path_lens", c.c_void_p), ("binary", c.c_void_p), ("transform", c.c_void_p),
+                ("dev_paths", c.c_void_p), ("dev_path_offsets", c.c_void_p)]
 
 
 class _CStats(c.Structure):
@@ -246,17 +247,19 @@ class Scanner:
         return res.secrets([a.FilePath for a in args])
 
     # --- batched arena API (analyzer / bench) -------------------------------
-    def scan_arena_async(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None):
+    def scan_arena_async(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None,
+                         dev_paths=None, dev_path_offsets=None):
         """Pipelined scan (tsg_scan_submit): returns a PendingScan; .wait() gives the ScanResult.
         The arrays passed must stay alive until then (the PendingScan keeps references)."""
-        keep, batch = self._batch(arena, offsets, paths, binary, dev_arena, dev_offsets)
+        keep, batch = self._batch(arena, offsets, paths, binary, dev_arena, dev_offsets, dev_paths,
+                                  dev_path_offsets)
         h = c.c_void_p()
         rc = self._L.tsg_scan_submit(self._h, c.byref(batch), c.byref(h))
         if rc != 0:
             raise RuntimeError("tsg_scan_submit failed: %s" % _lib.last_error(self._L))
         return PendingScan(self, h, (keep, batch))
 
-    def _batch(self, arena, offsets, paths, binary, dev_arena, dev_offsets):
+    def _batch(self, arena, offsets, paths, binary, dev_arena, dev_offsets, dev_paths=None, dev_path_offsets=None):
         n = len(offsets) - 1
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -273,10 +276,14 @@ class Scanner:
         bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
         batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
                         dev_arena, dev_offsets, paths_addr, plen_ptr,
-                        bin_arr.ctypes.data if bin_arr is not None else None)
+                        bin_arr.ctypes.data if bin_arr is not None else None, None,
+                        dev_paths, dev_path_offsets)
         return (arena_buf, offs, parr, plen, bin_arr), batch
 
-    def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None):
+    def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None, dev_paths=None,
+                   dev_path_offsets=None):
+        """One batch (tsg_scan).  dev_arena / dev_offsets: the contents already in HBM;
+        dev_paths / dev_path_offsets: the paths packed in HBM (GPU allow-path prefilter)."""
         n = len(offsets) - 1
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -292,7 +299,8 @@ class Scanner:
         bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
         batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
                         dev_arena, dev_offsets, paths_addr, plen_ptr,
-                        bin_arr.ctypes.data if bin_arr is not None else None)
+                        bin_arr.ctypes.data if bin_arr is not None else None, None,
+                        dev_paths, dev_path_offsets)
         h = c.c_void_p()
         rc = self._L.tsg_scan(self._h, c.byref(batch), c.byref(h))
         if rc != 0:
