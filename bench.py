@@ -409,6 +409,8 @@ def main():
     ap.add_argument("--parity-mb", type=float, default=None, help="oracle parity sample (first files)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=3, help="scans in flight (pipelined submission)")
+    ap.add_argument("--crlf", type=float, default=0.05,
+                    help="c2: share of CRLF files (SURVEY §8(d)); stripped while packing the HBM arena")
     ap.add_argument("--numa", choices=["gpu", "off"], default="gpu",
                     help="gpu: bind this rank's threads (and so its first-touch host memory) to the GPU's NUMA "
                          "node, as numactl --cpunodebind would")
@@ -454,7 +456,7 @@ def main():
     tmpdir = os.environ.get("TMPDIR", "/tmp")
     cfg_path = None
     t_gen = time.time()
-    C = layer = None
+    C = layer = R = None
     if args.workload in ("c3", "c3u", "c3f"):
         y, samples = corpus.c3_rules(unanchored_share=0.1 if args.workload == "c3u" else 0.0,
                                      fullscan_share=0.05 if args.workload == "c3f" else 0.0)
@@ -467,7 +469,7 @@ def main():
     elif args.workload == "c1fs":  # a source tree on tmpfs
         base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tmpdir
         fs_root = os.path.join(base, "tsg-c1fs-%d-%d" % (os.getpid(), rank))
-        C0 = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank)
+        C0 = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank, crlf_share=args.crlf)  # C1: 5 % CRLF
         write_tree(C0, fs_root)
         del C0
         layer = fs_root  # walked below instead of a tar layer
@@ -476,8 +478,16 @@ def main():
         C = corpus.generate(int(pool_gb * 1e9), seed=corpus.SEED + rank, size_scale=2.6)
         args.ingest = True
     else:
-        C = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank)
+        # C2: 5 % of the files CRLF.  The files as read (R) are CR-stripped while
+        # packed into the arena (secret.go:121; the analyzer's packing step, before timing) and the
+        # HBM-resident steps scan the stripped arena C; the value's numerator is R's bytes (pre-strip,
+        # §8(d)).  The ingest leg streams R itself and strips it on the GPU inside its timed region.
+        R = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank, crlf_share=args.crlf)
+        C = R.stripped() if args.crlf > 0 else R
+        if args.crlf <= 0:
+            R = None
     t_gen = time.time() - t_gen
+    kinds_raw = np.ones(R.n_files, dtype=np.uint8) if R is not None else None  # every text file: CR strip
 
     h2d_peak = None
     host_leg = [False]  # the ingest leg of a resident run: submit() streams the host arena
@@ -503,6 +513,8 @@ def main():
         t_compile = time.time() - t_c
 
         def submit():
+            if host_leg[0] and R is not None:  # the files as read; the GPU strips the CRs
+                return sc.scan_arena_async(R.arena, R.offsets, R.path_ptrs, transform=kinds_raw)
             if args.ingest or host_leg[0]:
                 return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs)
             return sc.scan_arena_async(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(),
@@ -608,7 +620,7 @@ def main():
     if layer is None and args.workload == "c2" and not args.ingest and args.ingest_steps > 0 and world == 1:
         del d_arena, d_offs
         torch.cuda.empty_cache()
-        unregister_leg = secret.HostRegister(C.arena)
+        unregister_leg = secret.HostRegister(C.arena if R is None else R.arena)
         peak = measure_h2d(dev)
         host_leg[0] = True
         ist = []
@@ -625,13 +637,16 @@ def main():
             t = torch.tensor([dti], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dti = float(t.item())
-        h2d = C.n_bytes * args.ingest_steps / dti / 1e9  # per GPU
-        ingest = {"value": round(world * C.n_bytes * args.ingest_steps / dti / 1e9, 3), "unit": "GB/s",
+        leg_bytes = C.n_bytes if R is None else R.n_bytes
+        h2d = leg_bytes * args.ingest_steps / dti / 1e9  # per GPU
+        ingest = {"value": round(world * leg_bytes * args.ingest_steps / dti / 1e9, 3), "unit": "GB/s",
                   "steps": args.ingest_steps, "ms_per_step": round(dti / args.ingest_steps * 1e3, 3),
                   "achieved_h2d": round(h2d, 2), "h2d_peak_measured": peak, "frac_h2d": round(h2d / peak, 4),
                   "h2d_chunks_per_scan": int(ist[-1].get("h2d_chunks", 0)),
                   "note": "same corpus and scanner, host-resident (page-locked) arena: H2D of every byte inside "
-                          "the timed region, overlapped with the kernels (two staging buffers, copy stream)"}
+                          "the timed region, overlapped with the kernels (two staging buffers, copy stream)"
+                          + ("; the files as read (%d CRLF), CR-stripped on the GPU (xform.hip) inside the timed "
+                             "region" % int(R.crlf.sum()) if R is not None else "")}
     pre = "" if layer is None else "scan_"
 
     def avg(k):  # per-scan mean over the timed steps (c4 sums its batches per step)
@@ -644,6 +659,8 @@ def main():
                                                      "ms_host_exact")})
     if layer is None:
         n_bytes, n_files = C.n_bytes * emissions, C.n_files * emissions  # per step
+        if R is not None:  # the files' bytes as read (pre-strip numerator)
+            n_bytes = R.n_bytes
         arena_bytes = C.n_bytes  # per scan
         counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs", "fold_sites",
                                             "candidates", "special_files", "findings")}
@@ -653,6 +670,8 @@ def main():
         counts["hits_to_verify"] = counts["follow_hits"]
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
+                        "crlf_files": int(R.crlf.sum()) if R is not None else 0,
+                        "arena_bytes_after_cr_strip": C.n_bytes,
                         "emissions_per_step": emissions, "pool_bytes": C.n_bytes,
                         "resident": "host (page-locked), H2D in the timed region" if args.ingest
                         else "HBM (copied once before timing)"}

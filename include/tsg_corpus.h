@@ -15,6 +15,16 @@ int64_t tsg_corpus_plan(uint64_t seed, uint64_t target_bytes, uint64_t* offsets,
 int tsg_corpus_fill(uint64_t seed, const uint64_t* offsets, uint64_t n_files, const char* pool,
                     const uint64_t* pool_off, uint32_t n_pool, double secrets_per_byte, uint8_t* arena,
                     char* paths, uint32_t path_stride, int threads);
+/* Turns a deterministic `share` of the files CRLF in place ('\n' -> "\r\n",
+ * cut at each file's size); is_crlf (optional, n_files) marks them.  Returns
+ * the number of CRLF files. */
+int64_t tsg_corpus_crlf(uint64_t seed, const uint64_t* offsets, uint64_t n_files, uint8_t* arena, double share,
+                        uint8_t* is_crlf, int threads);
+/* bytes.ReplaceAll(content, "\r", "") per file (secret.go:121), the packing
+ * step of the HBM-resident C2 bench: out gets the stripped files back to back,
+ * out_offsets their n_files + 1 offsets. */
+int tsg_corpus_strip(const uint64_t* offsets, uint64_t n_files, const uint8_t* in, uint8_t* out, uint64_t* out_offsets,
+                     int threads);
 /* BASELINE configs[3] (C4): an uncompressed ustar image layer of many small
  * files (log-normal sizes, median 1.5 KiB, sigma 1.2) with distro-like paths
  * (allow-listed system dirs, executables, .pyc files, skipped extensions, app

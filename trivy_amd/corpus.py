@@ -16,6 +16,9 @@ PATH_STRIDE = 64
 def _declare(L):
     L.tsg_corpus_plan.restype = c.c_int64
     L.tsg_corpus_plan.argtypes = [c.c_uint64, c.c_uint64, c.c_void_p, c.c_uint64]
+    L.tsg_corpus_crlf.restype = c.c_int64
+    L.tsg_corpus_crlf.argtypes = [c.c_uint64, c.c_void_p, c.c_uint64, c.c_void_p, c.c_double, c.c_void_p, c.c_int]
+    L.tsg_corpus_strip.argtypes = [c.c_void_p, c.c_uint64, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int]
     L.tsg_corpus_fill.argtypes = [c.c_uint64, c.c_void_p, c.c_uint64, c.c_char_p, c.c_void_p, c.c_uint32,
                                   c.c_double, c.c_void_p, c.c_void_p, c.c_uint32, c.c_int]
 
@@ -42,6 +45,23 @@ class Corpus:
         raw = self.path_buf[i * PATH_STRIDE:(i + 1) * PATH_STRIDE].tobytes()
         return raw.split(b"\0", 1)[0].decode()
 
+    crlf = None  # per file: 1 = CRLF text (generate(crlf_share=...))
+
+    def stripped(self, threads=None):
+        """The analyzer's CR strip (secret.go:121) of every file: a Corpus over the
+        stripped contents with the same paths (the arena the HBM-resident bench scans)."""
+        L = _lib.lib()
+        _declare(L)
+        n = self.n_files
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        out = np.zeros(self.n_bytes + 64, dtype=np.uint8)
+        threads = threads or int(os.environ.get("TSG_HOST_THREADS", "16"))
+        L.tsg_corpus_strip(self.offsets.ctypes.data, n, self.arena.ctypes.data, out.ctypes.data, offs.ctypes.data,
+                           threads)
+        S = Corpus(out[:int(offs[-1]) + 64], offs, self.path_buf)
+        S.crlf = self.crlf
+        return S
+
     def packed_paths(self):
         """The paths packed back to back (uint8, +16 B pad) and their n+1 offsets (uint64)."""
         rows = self.path_buf[:self.n_files * PATH_STRIDE].reshape(self.n_files, PATH_STRIDE)
@@ -56,9 +76,11 @@ class Corpus:
         return self.arena[int(self.offsets[i]):int(self.offsets[i + 1])].tobytes()
 
 
-def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=None, size_scale=1.0):
+def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=None, size_scale=1.0, crlf_share=0.0):
     """The C1/C2 generator; size_scale multiplies every planned file size (clipped at
-    10 MiB, the total cut at target_bytes): C5's mean-64-KiB files use 2.6."""
+    10 MiB, the total cut at target_bytes): C5's mean-64-KiB files use 2.6.
+    crlf_share: that share of the files is CRLF text (SURVEY §8(d): 5 % for C1/C2;
+    Corpus.crlf marks them, Corpus.stripped() is the analyzer's CR strip)."""
     L = _lib.lib()
     _declare(L)
     n = L.tsg_corpus_plan(seed, int(target_bytes), None, 0)
@@ -82,7 +104,11 @@ def generate(target_bytes, seed=SEED, secrets_per_byte=1.0 / 262144, threads=Non
     threads = threads or int(os.environ.get("TSG_HOST_THREADS", "16"))
     L.tsg_corpus_fill(seed, offs.ctypes.data, n, blob, poff.ctypes.data, len(samples), float(secrets_per_byte),
                       arena.ctypes.data, paths.ctypes.data, PATH_STRIDE, threads)
-    return Corpus(arena, offs, paths)
+    C = Corpus(arena, offs, paths)
+    if crlf_share > 0:
+        C.crlf = np.zeros(n, dtype=np.uint8)
+        L.tsg_corpus_crlf(seed, offs.ctypes.data, n, arena.ctypes.data, float(crlf_share), C.crlf.ctypes.data, threads)
+    return C
 
 
 # ---- BASELINE configs[2] (C3): 2,000 generated custom rules ----

@@ -158,13 +158,7 @@ std::string GoBase(std::string p) {
   return k == std::string::npos ? p : p.substr(k + 1);
 }
 
-// secret.go:28-62
-const char* const kSkipFiles[] = {"go.mod", "go.sum", "package-lock.json", "yarn.lock",
-                                  "pnpm-lock.yaml", "Pipfile.lock", "Gemfile.lock"};
-const char* const kSkipDirs[] = {".git", "node_modules"};
-const char* const kSkipExts[] = {".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg",
-                                 ".socket", ".deb", ".rpm", ".zip", ".gz", ".gzip", ".tar"};
-
+// secret.go:28-62 (skipFiles, skipDirs, skipExts): inlined in Required below
 }  // namespace tsg
 
 #include "collector.h"
@@ -179,26 +173,25 @@ bool Required(const tsg_analyzer* a, const char* path, uint64_t len, int64_t siz
   const size_t slash = fp.rfind('/');
   const std::string_view dir = slash == std::string_view::npos ? std::string_view() : fp.substr(0, slash + 1);
   const std::string_view name = slash == std::string_view::npos ? fp : fp.substr(slash + 1);
-  // strings.Split(dir, "/") contains a skip dir
-  for (size_t b = 0;;) {
-    const size_t e = dir.find('/', b);
-    const std::string_view part = dir.substr(b, e == std::string_view::npos ? std::string_view::npos : e - b);
-    for (const char* d : tsg::kSkipDirs)
-      if (part == d) return false;
-    if (e == std::string_view::npos) break;
-    b = e + 1;
+  // strings.Split(dir, "/") holds a skip dir: dir (which ends in '/') starts
+  // with "<skip>/" or contains "/<skip>/"
+  for (const std::string_view d : {std::string_view("/.git/"), std::string_view("/node_modules/")}) {
+    if (dir.substr(0, d.size() - 1) == d.substr(1)) return false;
+    if (dir.size() >= d.size() && memmem(dir.data(), dir.size(), d.data(), d.size())) return false;
   }
-  for (const char* f : tsg::kSkipFiles)
+  static constexpr std::string_view kFiles[] = {"go.mod", "go.sum", "package-lock.json", "yarn.lock",
+                                                "pnpm-lock.yaml", "Pipfile.lock", "Gemfile.lock"};
+  for (const std::string_view f : kFiles)
     if (name == f) return false;
   if (a->config_base == fp) return false;
-  std::string_view ext;  // filepath.Ext
-  for (size_t i = name.size(); i-- > 0;)
-    if (name[i] == '.') {
-      ext = name.substr(i);
-      break;
-    }
-  for (const char* x : tsg::kSkipExts)
-    if (ext == x) return false;
+  const size_t dot = name.rfind('.');  // filepath.Ext
+  if (dot != std::string_view::npos && name.size() - dot <= 7) {
+    static constexpr std::string_view kExts[] = {".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg",
+                                                 ".socket", ".deb", ".rpm", ".zip", ".gz", ".gzip", ".tar"};
+    const std::string_view ext = name.substr(dot);
+    for (const std::string_view x : kExts)
+      if (ext == x) return false;
+  }
   if (a->s->s->AllowPath(reinterpret_cast<const uint8_t*>(path), size_t(len))) return false;
   return true;
 }
@@ -376,7 +369,7 @@ int64_t tsg_collector_add(tsg_collector* c, const char* path, uint64_t path_len,
 
 }  // extern "C"
 
-namespace {
+namespace tsg {
 // One archive entry as the walk sees it (header chain resolved).
 struct TarEntry {
   uint64_t start, next;  // header chain start, next entry
@@ -392,6 +385,11 @@ struct TarEntry {
   uint8_t bin;
   uint64_t out_len, out_off;
 };
+
+}  // namespace tsg
+
+namespace {
+using tsg::TarEntry;
 
 // Sequential step of the walk: hop over the header chain starting at p using
 // only what decides the next entry's position (zero block, typeflag, size,
@@ -629,6 +627,23 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
   return 0;
 }
 
+}  // namespace
+
+namespace tsg {
+// Entries indexed and evaluated ahead of the walk's cursor (see tsg_collector_add_tar).
+struct TarWalkCache {
+  const uint8_t* tar = nullptr;
+  uint64_t n = 0;
+  bool gpu_xform = false;
+  std::vector<TarEntry> ents;
+  size_t pos = 0;        // the next entry to accept
+  uint64_t next = 0;     // the position after the last indexed entry
+  bool at_end = false;   // the archive ends at `next`
+};
+void FreeTarWalkCache(TarWalkCache* w) { delete w; }
+}  // namespace tsg
+
+namespace {
 // The entry's name (ustar prefix, GNU long name, PAX path) and header checksum.
 void Resolve(const uint8_t* tar, TarEntry* e) {
   const uint8_t* h = tar + e->hdr;
@@ -673,36 +688,56 @@ void Classify(const uint8_t* tar, TarEntry* e) {
 
 extern "C" {
 
-// The walk runs in rounds: index the entries ahead (~1.5x the room left in
-// the batch) and evaluate each on the thread that found it (name, Required,
-// binary gate, transformed length), accept the longest prefix that fits, copy
-// and transform the accepted contents on the threads.  Entries past the
-// accepted prefix are re-read from *cursor by the next call.
+// The walk runs in rounds: index a window of entries ahead of the cursor in
+// parallel (each evaluated on the thread that found it: name, Required,
+// binary gate, transformed length), accept the longest prefix that fits the
+// batch, copy the accepted contents on the threads.  The window is several
+// batches long and its entries past this batch stay in the analyzer's walk
+// cache, so the next call (on this or the other collector of a pipeline)
+// starts accepting at once: one parallel index pass per window instead of a
+// shrinking series of them per batch.
 int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st) {
   tsg_tar_stats local{};
   if (!st) st = &local;
+  std::lock_guard<std::mutex> walk_lock(c->a->walk_mu);
+  if (!c->a->walk) c->a->walk = new tsg::TarWalkCache();
+  tsg::TarWalkCache& W = *c->a->walk;
   uint64_t p = *cursor;
-  std::vector<TarEntry> ents;
   static const bool dbg = std::getenv("TSG_WALK_DEBUG") != nullptr;
+  static const uint64_t ahead = std::getenv("TSG_WALK_AHEAD") ? uint64_t(std::atoi(std::getenv("TSG_WALK_AHEAD"))) : 8;
   static double t_phase[4];
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   for (;;) {
-    // 1. index
+    // 1. the cached entries from p on, else index a window starting at p
     double t0 = dbg ? now() : 0;
-    const uint64_t room = c->limit > c->used ? c->limit - c->used : 0;
-    bool at_end = false;
-    if (IndexEntries(c, tar, n, p, 2 * room + (1 << 20), room + room / 2, c->threads, &ents, &p, &at_end) < 0)
-      return -1;
+    const bool hit = W.tar == tar && W.n == n && W.gpu_xform == c->gpu_xform &&
+                     ((W.pos < W.ents.size() && W.ents[W.pos].start == p) || (W.pos == W.ents.size() && W.next == p &&
+                                                                               W.at_end));
+    if (!hit) {
+      const uint64_t room = std::max<uint64_t>(c->limit, 1 << 20);
+      W.tar = tar;
+      W.n = n;
+      W.gpu_xform = c->gpu_xform;
+      W.pos = 0;
+      W.at_end = false;
+      if (IndexEntries(c, tar, n, p, ahead * room + (1 << 20), (ahead * room * 3) / 4, c->threads, &W.ents, &W.next,
+                       &W.at_end) < 0) {
+        W.tar = nullptr;
+        return -1;
+      }
+    }
     double t1 = dbg ? now() : 0;
     double t2 = dbg ? now() : 0;
     const size_t kBlock = 64;
-    // 3. accept in order
-    size_t k = 0;
+    // 2. accept in order
+    const size_t k0 = W.pos;
+    size_t k = k0;
     bool full = false;
-    for (; k < ents.size(); k++) {
-      TarEntry& e = ents[k];
+    for (; k < W.ents.size(); k++) {
+      TarEntry& e = W.ents[k];
       if (e.bad) {
         tsg::SetError("tar: invalid header checksum at offset " + std::to_string(e.hdr));
+        W.tar = nullptr;
         return -1;
       }
       if (e.state == 2) {
@@ -735,11 +770,12 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       st->required += e.state != 0;
       st->skipped_binary += e.state == 1;
     }
+    W.pos = k;
     double t3 = dbg ? now() : 0;
-    // 4. copy / transform the accepted contents
-    tsg::ParallelFor((k + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
-      for (size_t i = b * kBlock; i < std::min(k, (b + 1) * kBlock); i++) {
-        const TarEntry& e = ents[i];
+    // 3. copy / transform the accepted contents
+    tsg::ParallelFor((k - k0 + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
+      for (size_t i = k0 + b * kBlock; i < std::min(k, k0 + (b + 1) * kBlock); i++) {
+        const TarEntry& e = W.ents[i];
         if (e.state != 2) continue;
         uint8_t* dst = c->arena + e.out_off;
         if (c->gpu_xform) std::memcpy(dst, tar + e.data, e.size);
@@ -759,11 +795,12 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
                    g_eval_ns[0] / 1e9, g_eval_ns[1] / 1e9);
     }
     if (full) {
-      *cursor = ents[k].start;
+      *cursor = W.ents[k].start;
       return 1;
     }
+    p = W.next;
     *cursor = p;
-    if (at_end) return 0;
+    if (W.at_end) return 0;
   }
 }
 

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -14,9 +15,20 @@ namespace tsg {
 void SetError(const std::string& e);
 }
 
+namespace tsg {
+struct TarWalkCache;  // analyzer.cpp: evaluated tar entries indexed ahead of the cursor
+void FreeTarWalkCache(TarWalkCache* w);
+}
+
 struct tsg_analyzer {
   const tsg_scanner* s = nullptr;
   std::string config_base;  // filepath.Base(configPath)
+  // One tar walk at a time over this analyzer's collectors: the entries
+  // indexed past one batch's end are the next batch's (the collectors of a
+  // two-collector pipeline alternate on one layer).
+  std::mutex walk_mu;
+  tsg::TarWalkCache* walk = nullptr;
+  ~tsg_analyzer() { tsg::FreeTarWalkCache(walk); }
 };
 
 struct tsg_collector {

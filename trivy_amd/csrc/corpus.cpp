@@ -7,7 +7,9 @@
 // blobs, 2 % UTF-8 (incl. U+0130, U+212A, U+017F and invalid bytes).  Lines
 // are geometric (mean ~40 B) with 1 % > 100 B and 0.1 % > 10 KiB.  Secrets
 // from a sampled pool are planted at 1 per 256 KiB (Poisson).  Contents are
-// generated CR-free (the analyzer strips CR before Scan).
+// generated CR-free; tsg_corpus_crlf turns a share of the files into CRLF
+// text afterwards (5 % of C1/C2 files; the analyzer strips the
+// CRs before Scan).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -367,6 +369,93 @@ int tsg_corpus_fill(uint64_t seed, const uint64_t* offsets, uint64_t n_files, co
   for (int t = 1; t < threads; t++) pool_t.emplace_back(work);
   work();
   for (auto& th : pool_t) th.join();
+  return 0;
+}
+
+int64_t tsg_corpus_crlf(uint64_t seed, const uint64_t* offsets, uint64_t n_files, uint8_t* arena, double share,
+                        uint8_t* is_crlf, int threads) {
+  if (threads <= 0) threads = 1;
+  std::atomic<uint64_t> next{0}, count{0};
+  auto work = [&]() {
+    std::vector<uint8_t> tmp;
+    for (;;) {
+      const uint64_t lo = next.fetch_add(256);
+      if (lo >= n_files) break;
+      const uint64_t hi = std::min<uint64_t>(lo + 256, n_files);
+      for (uint64_t i = lo; i < hi; i++) {
+        Rng r(seed ^ (i * 0xD1B54A32D192ED03ull) ^ 0xC3C3C3C3ull);
+        const bool on = double(r.Below(1u << 20)) < share * double(1u << 20);
+        if (is_crlf) is_crlf[i] = on ? 1 : 0;
+        if (!on) continue;
+        count++;
+        // LF -> CR LF, cut at the file's size (the lines past it are dropped)
+        uint8_t* d = arena + offsets[i];
+        const uint64_t n = offsets[i + 1] - offsets[i];
+        tmp.assign(d, d + n);
+        uint64_t w = 0;
+        for (uint64_t k = 0; k < n && w < n; k++) {
+          if (tmp[k] == '\n') {
+            d[w++] = '\r';
+            if (w >= n) break;
+          }
+          d[w++] = tmp[k];
+        }
+      }
+    }
+  };
+  std::vector<std::thread> pool_t;
+  for (int t = 1; t < threads; t++) pool_t.emplace_back(work);
+  work();
+  for (auto& th : pool_t) th.join();
+  return int64_t(count.load());
+}
+
+int tsg_corpus_strip(const uint64_t* offsets, uint64_t n_files, const uint8_t* in, uint8_t* out, uint64_t* out_offsets,
+                     int threads) {
+  if (threads <= 0) threads = 1;
+  std::vector<uint64_t> cr(n_files + 1, 0);
+  auto par = [&](auto fn) {
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+      for (;;) {
+        const uint64_t lo = next.fetch_add(512);
+        if (lo >= n_files) break;
+        for (uint64_t i = lo; i < std::min<uint64_t>(lo + 512, n_files); i++) fn(i);
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int t = 1; t < threads; t++) ts.emplace_back(work);
+    work();
+    for (auto& th : ts) th.join();
+  };
+  par([&](uint64_t i) {
+    const uint8_t* p = in + offsets[i];
+    const uint8_t* e = in + offsets[i + 1];
+    uint64_t c = 0;
+    while (p < e && (p = static_cast<const uint8_t*>(std::memchr(p, '\r', size_t(e - p))))) {
+      c++;
+      p++;
+    }
+    cr[i] = c;
+  });
+  out_offsets[0] = 0;
+  for (uint64_t i = 0; i < n_files; i++) out_offsets[i + 1] = out_offsets[i] + (offsets[i + 1] - offsets[i]) - cr[i];
+  par([&](uint64_t i) {
+    const uint8_t* p = in + offsets[i];
+    const uint8_t* e = in + offsets[i + 1];
+    uint8_t* d = out + out_offsets[i];
+    if (!cr[i]) {
+      std::memcpy(d, p, size_t(e - p));
+      return;
+    }
+    while (p < e) {
+      const uint8_t* q = static_cast<const uint8_t*>(std::memchr(p, '\r', size_t(e - p)));
+      const uint8_t* stop = q ? q : e;
+      std::memcpy(d, p, size_t(stop - p));
+      d += stop - p;
+      p = q ? q + 1 : e;
+    }
+  });
   return 0;
 }
 

@@ -51,9 +51,13 @@ constexpr uint64_t kNlReach = uint64_t(1) << 20;
 // The transformed bytes of chosen files of a host batch whose transform ran
 // on the GPU (RunHost with kinds): buf holds them in file order, off is a
 // full n_files+1 offset table into buf (files not chosen are empty).
+// Files whose transform is the identity (kind 0, or kind 1 without a '\r')
+// are not gathered: raw[f] = 1 and the exact pass reads them in the host
+// batch as given.
 struct TailOut {
   std::vector<uint8_t> buf;
   std::vector<uint64_t> off;
+  std::vector<uint8_t> raw;
   uint64_t xform_bytes = 0;  // transformed arena bytes of the whole batch
 };
 
@@ -142,7 +146,7 @@ class GpuEngine {
   bool Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
                  std::vector<uint64_t>* xoff, float* ms);
   bool GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf, const std::vector<uint64_t>& xoff,
-                  std::vector<uint64_t>* tail_len, TailOut* tail);
+                  const uint64_t* raw_off, const uint8_t* kinds, std::vector<uint64_t>* tail_len, TailOut* tail);
   void DumpItemDiag();
   std::vector<uint8_t> h_items_kind_;
   std::vector<uint32_t> h_items_id_;

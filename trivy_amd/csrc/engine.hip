@@ -1972,6 +1972,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
   if (tail) {
     tail->buf.clear();
     tail->off.assign(size_t(n_files) + 1, 0);
+    tail->raw.assign(n_files, 1);
     tail->xform_bytes = 0;
   }
   if (kinds && !tail) {
@@ -2063,7 +2064,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
       st->ms_xform += ms_x;
       cs.ms_total += ms_x;
       tail->xform_bytes += scan_bytes;
-      if (!GatherTail(part, f0, f1 - f0, xoff, &tail_len, tail)) {
+      if (!GatherTail(part, f0, f1 - f0, xoff, h_offsets + f0, kinds + f0, &tail_len, tail)) {
         if (copier.joinable()) copier.join();
         return false;
       }
@@ -2134,12 +2135,18 @@ bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint6
 // The transformed bytes of the chunk's files with candidates -> tail->buf
 // (appended in file order); their lengths -> (*tail_len)[f0 + f].
 bool GpuEngine::GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf,
-                           const std::vector<uint64_t>& xoff, std::vector<uint64_t>* tail_len, TailOut* tail) {
+                           const std::vector<uint64_t>& xoff, const uint64_t* raw_off, const uint8_t* kinds,
+                           std::vector<uint64_t>* tail_len, TailOut* tail) {
+  // only the files the transform changed (a CRLF file, .pyc printable runs):
+  // the others are read where they are in the host batch (TailOut::raw)
   std::vector<uint32_t> files;
   files.reserve(part.size());
-  for (const auto& c : part) files.push_back(c.file);
+  for (const auto& c : part)
+    if (c.file < nf && (kinds[c.file] == 2 || xoff[c.file + 1] - xoff[c.file] != raw_off[c.file + 1] - raw_off[c.file]))
+      files.push_back(c.file);
   std::sort(files.begin(), files.end());
   files.erase(std::unique(files.begin(), files.end()), files.end());
+  for (uint32_t f : files) tail->raw[f0 + f] = 0;
   if (files.empty()) return true;
   std::vector<uint64_t> dst(files.size());
   uint64_t total = 0;

@@ -1037,7 +1037,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   PhaseTimer pt3(3);
   ff.f.reserve(matched.size());
   ff.lines.reserve(matched.size() * 5);
-  ff.text.reserve(matched.size() * 512);  // match line + 4 lines of <= 100 B, typically
+  ff.text.reserve(matched.size() * 320);  // match line + 4 lines of <= 100 B, typically
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
@@ -1157,9 +1157,24 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     return false;
   }
   BatchInput tin = in;  // the exact pass reads the transformed bytes
-  if (in.transform) {
-    tin.host_arena = tail.buf.data();
-    tin.host_offsets = tail.off.data();
+  std::vector<const uint8_t*> fdata;
+  std::vector<uint64_t> flen;
+  if (in.transform) {  // gathered files from tail.buf, identity-transformed ones in place
+    fdata.assign(in.n_files, nullptr);
+    flen.assign(in.n_files, 0);
+    for (const Candidate& c : cands) {
+      const uint32_t f = c.file;
+      if (f >= in.n_files || fdata[f]) continue;
+      if (tail.raw[f]) {
+        fdata[f] = in.host_arena + in.host_offsets[f];
+        flen[f] = in.host_offsets[f + 1] - in.host_offsets[f];
+      } else {
+        fdata[f] = tail.buf.data() + tail.off[f];
+        flen[f] = tail.off[f + 1] - tail.off[f];
+      }
+    }
+    tin.file_data = fdata.data();
+    tin.file_len = flen.data();
   }
   double t1 = NowMs();
   if (const char* dump = std::getenv("TSG_DUMP_CANDS")) {  // profiling aid (tools/host_tail_bench.py)
@@ -1224,6 +1239,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   out->kind.assign(in.n_files, uint8_t(kNoFindings));
   out->found_files.clear();
   out->found.clear();
+  out->arenas.clear();
   double t1 = NowMs();
   std::vector<uint8_t> allowed_local;
   if (!allowed_pre) allowed_local = AllowedPaths(in);
@@ -1261,7 +1277,8 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     std::vector<double> w(nf);
     for (size_t k = 0; k < nf; k++) {
       const uint32_t f = cands[starts[k]].file;
-      w[k] = double(starts[k + 1] - starts[k]) * double(in.host_offsets[f + 1] - in.host_offsets[f] + 4096);
+      const uint64_t flen = in.file_data ? in.file_len[f] : in.host_offsets[f + 1] - in.host_offsets[f];
+      w[k] = double(starts[k + 1] - starts[k]) * double(flen + 4096);
     }
     const size_t top = std::min<size_t>(nf, 1024);  // the LPT head, dispatched one group at a time below
     auto heavier = [&](uint32_t x, uint32_t y) { return w[x] > w[y] || (w[x] == w[y] && x < y); };
@@ -1280,17 +1297,35 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     const uint32_t f = cands[a].file;
     if (allowed[f]) return;
     __builtin_prefetch(in.paths[f]);
-    const uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
+    const uint8_t* data = in.file_data ? in.file_data[f] : in.host_arena + in.host_offsets[f];
+    const int64_t len = int64_t(in.file_data ? in.file_len[f] : in.host_offsets[f + 1] - in.host_offsets[f]);
     for (size_t q = a; q < b && q < a + 4; q++) {
       const int64_t lo = std::max<int64_t>(0, cands[q].wlo - 256);
-      const int64_t hi = std::min<int64_t>(int64_t(fe - fs), std::min(cands[q].whi, cands[q].wlo + 2048) + 512);
-      for (int64_t x = lo & ~int64_t(63); x < hi; x += 64) __builtin_prefetch(in.host_arena + fs + uint64_t(x));
+      const int64_t hi = std::min<int64_t>(len, std::min(cands[q].whi, cands[q].wlo + 2048) + 512);
+      for (int64_t x = lo & ~int64_t(63); x < hi; x += 64) __builtin_prefetch(data + x);
     }
+  };
+  // one findings arena per host thread of this pass (handed to the result)
+  std::mutex arena_mu;
+  static std::atomic<uint64_t> pass_serial{0};
+  const uint64_t serial = ++pass_serial;
+  auto thread_arena = [&]() -> ResultArena* {
+    thread_local uint64_t t_serial = 0;
+    thread_local ResultArena* t_arena = nullptr;
+    if (t_serial != serial) {
+      std::unique_ptr<ResultArena> a(new ResultArena());
+      t_arena = a.get();
+      t_serial = serial;
+      std::lock_guard<std::mutex> g(arena_mu);
+      out->arenas.push_back(std::move(a));
+    }
+    return t_arena;
   };
   auto scan_group = [&](size_t k) {
     size_t a = starts[k], b = starts[k + 1];
     uint32_t f = cands[a].file;
     if (allowed[f]) return;
+    tmp[k].findings = FileFindings(thread_arena());
     if (b - a > 1) {
       auto by_rule = [](const Candidate& x, const Candidate& y) {
         return x.rule != y.rule ? x.rule < y.rule : x.wlo < y.wlo;
@@ -1299,9 +1334,9 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     }
     const char* p = in.paths[f];
     size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
-    uint64_t fs = in.host_offsets[f], fe = in.host_offsets[f + 1];
-    ScanFile(in.host_arena + fs, int64_t(fe - fs), std::string_view(p, pn), in.binary && in.binary[f], &cands[a],
-             b - a, &tmp[k], gpu_windows);
+    const uint8_t* data = in.file_data ? in.file_data[f] : in.host_arena + in.host_offsets[f];
+    const int64_t len = int64_t(in.file_data ? in.file_len[f] : in.host_offsets[f + 1] - in.host_offsets[f]);
+    ScanFile(data, len, std::string_view(p, pn), in.binary && in.binary[f], &cands[a], b - a, &tmp[k], gpu_windows);
   };
   ParallelFor(n_items, host_threads_, [&](size_t it) {
     if (it < top) {

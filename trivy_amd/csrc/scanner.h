@@ -74,10 +74,65 @@ struct FindingOut {
   uint32_t line_lo, line_hi;      // into FileFindings::lines
 };
 
+// Bump allocator for one batch's findings: each host thread of the exact
+// pass fills its own, and the batch result frees them whole -- per file the
+// findings, lines and text were three heap allocations made on the pool
+// threads and freed on the reaper thread (malloc arena lock traffic).
+class ResultArena {
+ public:
+  void* Alloc(size_t n, size_t align) {
+    size_t pad = (align - (reinterpret_cast<uintptr_t>(cur_) & (align - 1))) & (align - 1);
+    if (n + pad > left_) {
+      const size_t sz = std::max<size_t>(kBlock, n + align);
+      blocks_.emplace_back(new uint8_t[sz]);
+      cur_ = blocks_.back().get();
+      left_ = sz;
+      pad = (align - (reinterpret_cast<uintptr_t>(cur_) & (align - 1))) & (align - 1);
+    }
+    void* p = cur_ + pad;
+    cur_ += pad + n;
+    left_ -= pad + n;
+    return p;
+  }
+
+ private:
+  static constexpr size_t kBlock = size_t(1) << 20;
+  std::vector<std::unique_ptr<uint8_t[]>> blocks_;
+  uint8_t* cur_ = nullptr;
+  size_t left_ = 0;
+};
+
+// Allocator over a ResultArena (deallocate is a no-op); without an arena it
+// is std::allocator.
+template <class T>
+struct ArenaAlloc {
+  using value_type = T;
+  using propagate_on_container_move_assignment = std::true_type;
+  using propagate_on_container_copy_assignment = std::true_type;
+  using propagate_on_container_swap = std::true_type;
+  ResultArena* a = nullptr;
+  ArenaAlloc() = default;
+  explicit ArenaAlloc(ResultArena* x) : a(x) {}
+  template <class U>
+  ArenaAlloc(const ArenaAlloc<U>& o) : a(o.a) {}
+  T* allocate(size_t n) {
+    return a ? static_cast<T*>(a->Alloc(n * sizeof(T), alignof(T))) : std::allocator<T>().allocate(n);
+  }
+  void deallocate(T* p, size_t n) {
+    if (!a) std::allocator<T>().deallocate(p, n);
+  }
+  template <class U>
+  bool operator==(const ArenaAlloc<U>& o) const { return a == o.a; }
+  template <class U>
+  bool operator!=(const ArenaAlloc<U>& o) const { return a != o.a; }
+};
+
 struct FileFindings {
-  std::vector<FindingOut> f;
-  std::vector<LineOut> lines;
-  std::string text;
+  explicit FileFindings(ResultArena* a = nullptr)
+      : f(ArenaAlloc<FindingOut>(a)), lines(ArenaAlloc<LineOut>(a)), text(ArenaAlloc<char>(a)) {}
+  std::vector<FindingOut, ArenaAlloc<FindingOut>> f;
+  std::vector<LineOut, ArenaAlloc<LineOut>> lines;
+  std::basic_string<char, std::char_traits<char>, ArenaAlloc<char>> text;
   bool binary = false;  // ScanArgs.Binary: findings carry Code{} (Lines nil, scanner.go:441-444)
   size_t size() const { return f.size(); }
   std::string_view Str(uint32_t off, uint32_t len) const { return std::string_view(text).substr(off, len); }
@@ -98,6 +153,7 @@ struct FileResult {
 
 // Per-batch result, sparse: a kind byte per file, findings only where present.
 struct BatchResult {
+  std::vector<std::unique_ptr<ResultArena>> arenas;  // the findings' storage (declared first: freed last)
   std::vector<uint8_t> kind;              // FileKind per file
   std::vector<uint32_t> found_files;      // ascending
   std::vector<FileFindings> found;
@@ -124,6 +180,10 @@ struct BatchInput {
   const uint8_t* binary = nullptr;      // optional per-file Binary flag
   const uint8_t* transform = nullptr;   // optional per-file pre-transform (xform.h) run on the GPU: then
                                         // host_arena holds the bytes as read (host-resident batches only)
+  // optional, per file: where the exact pass reads file f (file_data[f], file_len[f] bytes) instead of
+  // host_arena + host_offsets[f] (a GPU pre-transformed batch: the gathered transformed files)
+  const uint8_t* const* file_data = nullptr;
+  const uint64_t* file_len = nullptr;
   const uint8_t* dev_paths = nullptr;   // optional: the paths packed in HBM (the allow-path prefilter runs
   const uint64_t* dev_path_off = nullptr;  // on the GPU, pathfilter.h); n_files + 1 offsets, device
 };

@@ -88,12 +88,14 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t lane) {  // e
 //     closes the run before it iff the 5 bytes before it are printable; the
 //     file's last byte emits the closing '\n' of a run reaching the file end
 //     iff the last 5 bytes are printable (utils.go:128-160).
-// A lane owns one 16-B block, a wave one 1-KiB tile.  Pass 1 counts each
-// tile's output bytes and records where each file starts inside its tile;
-// an exclusive scan over the tiles and a per-file fix-up give the
-// transformed offsets; pass 2 recomputes the bytes, packs the wave's output
-// in LDS at its global 16-B phase and writes aligned 16-B stores (byte stores
-// only at the tile's two ragged ends, which the neighbouring tiles share).
+// A lane owns one 16-B block, a wave one 1-KiB tile.  Per file segment of the
+// block the rule is evaluated as 16-bit masks (keep, '\n' before, '\n' after);
+// pass 1 counts each tile's output bytes and records where each file starts
+// inside its tile; an exclusive scan over the tiles and a per-file fix-up give
+// the transformed offsets; pass 2 recomputes the masks, packs the wave's
+// output in LDS at its global 16-B phase and writes aligned 16-B stores (byte
+// stores only at the tile's two ragged ends, which the neighbouring tiles
+// share).  Positions are 32-bit (a call covers < 4 GiB).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kXTile = 1024;
 
@@ -109,10 +111,12 @@ __global__ __launch_bounds__(kXThreads) void xf_chunk_map_kernel(const uint64_t*
 // neighbours' words by wave shuffles; the wave's edge lanes load theirs).
 struct XWindow {
   uint32_t w[8];
-  __device__ __forceinline__ uint32_t byte(int i) const { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const {
+    return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+  }
 };
 
-__device__ __forceinline__ XWindow x_window(const uint8_t* raw, uint64_t n_bytes, uint64_t blk, uint32_t lane,
+__device__ __forceinline__ XWindow x_window(const uint8_t* raw, uint32_t n_bytes, uint32_t blk, uint32_t lane,
                                             const uint4& v) {
   XWindow W;
   W.w[2] = v.x;
@@ -136,114 +140,139 @@ __device__ __forceinline__ XWindow x_window(const uint8_t* raw, uint64_t n_bytes
   return W;
 }
 
-// Kind-2 masks over the window for the file [fs, fe): bit i of K = window
-// byte i is a kept printable byte, bit i of C = window byte i closes a kept
-// run (non-printable, the 5 bytes before it printable), bit i of Z = the file's
-// last byte is window byte i and closes a run reaching the file end.
+// 4-bit mask of the bytes of w equal to c (exact per byte: no carries between bytes).
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t c4) {
+  const uint32_t x = w ^ c4;
+  const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of each zero byte
+  return ((t >> 7) * 0x204081u >> 21) & 0xFu;  // gather bits 0, 8, 16, 24 into bits 0..3
+}
+
+// Kind-2 masks for the file window bits [lo, hi) of the 32-byte window
+// (window bit i = byte blk - 8 + i): K kept printable bytes, C bytes that emit
+// the '\n' closing the run before them, Z the file's last byte when it closes
+// a run reaching the file end (hi <= 24: the file ends in or before the block).
 struct XMasks {
   uint32_t K, C, Z;
 };
-__device__ __forceinline__ XMasks x_masks(const XWindow& W, uint64_t blk, uint64_t fs, uint64_t fe) {
-  uint32_t P = 0, in = 0;
-#pragma unroll
-  for (int i = 0; i < 32; i++) {
-    const int64_t pos = int64_t(blk) - 8 + i;
-    const bool inside = pos >= int64_t(fs) && pos < int64_t(fe);
-    in |= uint32_t(inside) << i;
-    P |= uint32_t(inside && xprint(W.byte(i))) << i;
+__device__ XMasks x_masks(const XWindow& W, uint32_t lo, uint32_t hi) {
+  const uint32_t in = (hi >= 32 ? ~0u : (1u << hi) - 1u) & ~((1u << lo) - 1u);
+  uint32_t P = 0;
+#pragma unroll 4
+  for (uint32_t i = 0; i < 32; i++) {
+    const uint32_t b = W.byte(i);
+    P |= uint32_t((b >= 0x20u && b <= 0x7Eu) || (b >= 0xA1u && b != 0xADu)) << i;
   }
+  P &= in;
   const uint32_t Q = P & (P >> 1) & (P >> 2) & (P >> 3) & (P >> 4);  // bit k: bytes k .. k+4 printable
   XMasks m;
   m.K = (Q | (Q << 1) | (Q << 2) | (Q << 3) | (Q << 4)) & P;
   m.C = ~P & in & (Q << 5);
-  const int64_t last = int64_t(fe) - 1 - (int64_t(blk) - 8);  // window index of the file's last byte
-  m.Z = (last >= 4 && last < 32 && ((Q >> (last - 4)) & 1u)) ? (1u << last) : 0u;
+  m.Z = (hi <= 32 && hi >= 5 && ((Q >> (hi - 5)) & 1u)) ? (1u << (hi - 1)) : 0u;
   return m;
 }
 
-// Walks a lane's 16 bytes in file order.  emit(byte) is called per output
-// byte, start(f) at each file start inside the block (before its bytes).
-template <typename Emit, typename Start>
-__device__ __forceinline__ void x_lane(const uint8_t* raw, uint64_t n_bytes, const uint64_t* __restrict__ off,
-                                       const uint8_t* __restrict__ kind, uint32_t n_files,
-                                       const uint32_t* __restrict__ chunk_file, uint64_t blk, const XWindow& W,
-                                       Emit emit, Start start) {
-  if (blk >= n_bytes) return;
+// A lane's block in file order.  For each file segment [s, e) of the block:
+// start(f, count so far) at a file starting inside the block (empty files
+// too), then out(emit mask, nl-before mask, nl-after mask) over the block's
+// 16 bytes (bit i = byte blk + i): the output is, in byte order, a '\n' for a
+// bit of the second mask, the byte for a bit of the first, a '\n' for a bit of
+// the third.  Returns the lane's output byte count.
+template <typename Start, typename Out>
+__device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const uint64_t* __restrict__ off,
+                                           const uint8_t* __restrict__ kind, uint32_t n_files,
+                                           const uint32_t* __restrict__ chunk_file, uint32_t blk, const XWindow& W,
+                                           Start start, Out out) {
+  if (blk >= n_bytes) return 0;
+  const uint32_t bend = blk + 16 < n_bytes ? blk + 16 : n_bytes;
   uint32_t f = chunk_file[blk / kXTile];
-  uint64_t fs = off[f], fe = off[f + 1];
-  while (fe <= blk && f + 1 < n_files) {  // files ending before the block (the chunk map names the chunk's first)
+  uint32_t fs = uint32_t(off[f]), fe = uint32_t(off[f + 1]);
+  while (fe <= blk && f + 1 < n_files) {  // the file holding blk (the chunk map names the tile's first)
     f++;
     fs = fe;
-    fe = off[f + 1];
-    if (fs >= blk) start(f);  // empty files at the block start
+    fe = uint32_t(off[f + 1]);
+    if (fs >= blk) start(f, 0u);  // an empty file at the block start
   }
-  if (fs == blk) start(f);
-  uint32_t k = kind[f];
-  XMasks m = {0, 0, 0};
-  if (k == 2) m = x_masks(W, blk, fs, fe);
-  const uint64_t end = blk + 16 < n_bytes ? blk + 16 : n_bytes;
-  for (uint64_t p = blk; p < end; p++) {
-    while (p >= fe && f + 1 < n_files) {
-      f++;
-      fs = fe;
-      fe = off[f + 1];
-      start(f);
-      k = kind[f];
-      if (k == 2) m = x_masks(W, blk, fs, fe);
+  // the block's CR bytes (kinds 1)
+  const uint32_t cr = eq_bytes(W.w[2], 0x0D0D0D0Du) | (eq_bytes(W.w[3], 0x0D0D0D0Du) << 4) |
+                      (eq_bytes(W.w[4], 0x0D0D0D0Du) << 8) | (eq_bytes(W.w[5], 0x0D0D0D0Du) << 12);
+  uint32_t cnt = 0;
+  for (;;) {
+    if (fs >= blk && fs < bend) start(f, cnt);
+    const uint32_t s = fs > blk ? fs - blk : 0u, e = (fe < bend ? fe : bend) - blk;  // the segment, block bits
+    if (s < e) {
+      const uint32_t seg = ((1u << e) - 1u) & ~((1u << s) - 1u);
+      const uint32_t k = kind[f];
+      if (k == 0) {
+        out(seg, 0u, 0u);
+        cnt += uint32_t(__popc(seg));
+      } else if (k == 1) {
+        out(seg & ~cr, 0u, 0u);
+        cnt += uint32_t(__popc(seg & ~cr));
+      } else {
+        const uint32_t lo = fs + 8 > blk ? fs + 8 - blk : 0u;  // window bits of the file
+        const uint32_t hi = fe - blk + 8 < 32 ? fe - blk + 8 : 32u;
+        const XMasks m = x_masks(W, fs + 8 >= blk ? lo : 0u, fe + 8 >= blk ? hi : 0u);
+        const uint32_t K = (m.K >> 8) & seg, C = (m.C >> 8) & seg, Z = (m.Z >> 8) & seg;
+        out(K, C, Z);
+        cnt += uint32_t(__popc(K) + __popc(C) + __popc(Z));
+      }
     }
-    const int i = int(p - blk) + 8;
-    const uint32_t b = W.byte(i);
-    if (k == 0) {
-      emit(b);
-    } else if (k == 1) {
-      if (b != '\r') emit(b);
-    } else {
-      if ((m.C >> i) & 1u) emit('\n');
-      if ((m.K >> i) & 1u) emit(b);
-      if ((m.Z >> i) & 1u) emit('\n');
-    }
+    if (fe >= bend || f + 1 >= n_files) break;
+    f++;
+    fs = fe;
+    fe = uint32_t(off[f + 1]);
   }
+  return cnt;
 }
 
-__global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __restrict__ raw, uint64_t n_bytes,
+__global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __restrict__ raw, uint32_t n_bytes,
                                                              const uint64_t* __restrict__ off,
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
                                                              uint32_t* __restrict__ tile_cnt,
                                                              uint32_t* __restrict__ fstart) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
-  const uint64_t waves = uint64_t(gridDim.x) * (kXThreads / 64);
-  for (uint64_t t = uint64_t(blockIdx.x) * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
-    const uint64_t blk = t * kXTile + 16 * uint64_t(lane);
+  const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint32_t waves = gridDim.x * (kXThreads / 64);
+  for (uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
+    const uint32_t blk = t * kXTile + 16 * lane;
     const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
-    uint32_t c = 0;
-    bool starts = false;
-    x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t) { c++; },
-           [&](uint32_t) { starts = true; });
+    // file starts: tile-relative output offsets once the lane's prefix is known
+    uint32_t sf[4], sc[4], ns = 0;
+    const uint32_t c = x_lane(
+        n_bytes, off, kind, n_files, chunk_file, blk, W,
+        [&](uint32_t f, uint32_t at) {
+          if (ns < 4) {
+            sf[ns] = f;
+            sc[ns] = at;
+          }
+          ns++;
+        },
+        [&](uint32_t, uint32_t, uint32_t) {});
     const uint32_t ex = wave_excl(c, lane);
     if (lane == 63) tile_cnt[t] = ex + c;
-    if (starts) {  // the files starting in this block: their tile-relative output offsets
-      uint32_t c2 = ex;
-      x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t) { c2++; },
-             [&](uint32_t f) { fstart[f] = c2; });
+    if (ns > 4) {  // many tiny files in one block: walk it again, recording all
+      x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t f, uint32_t at) { fstart[f] = ex + at; },
+             [&](uint32_t, uint32_t, uint32_t) {});
+    } else {
+      for (uint32_t i = 0; i < ns; i++) fstart[sf[i]] = ex + sc[i];
     }
   }
 }
 
 __global__ __launch_bounds__(kXThreads) void xf_fixup_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
-                                                             uint64_t n_bytes, const uint64_t* __restrict__ tile_pre,
+                                                             uint32_t n_bytes, const uint64_t* __restrict__ tile_pre,
                                                              const uint32_t* __restrict__ fstart,
                                                              uint64_t* __restrict__ xoff) {
-  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_files; f += gridDim.x * blockDim.x) {
     const uint64_t s = f < n_files ? off[f] : n_bytes;
     xoff[f] = s < n_bytes ? tile_pre[s / kXTile] + fstart[f] : tile_pre[n_tiles];
   }
 }
 
-__global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __restrict__ raw, uint64_t n_bytes,
+__global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __restrict__ raw, uint32_t n_bytes,
                                                              const uint64_t* __restrict__ off,
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
@@ -254,21 +283,41 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kXThreads / 64][kStage];
   const uint32_t lane = threadIdx.x & 63u;
   uint8_t* S = s_out[threadIdx.x >> 6];
-  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
-  const uint64_t waves = uint64_t(gridDim.x) * (kXThreads / 64);
-  for (uint64_t t = uint64_t(blockIdx.x) * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
-    const uint64_t blk = t * kXTile + 16 * uint64_t(lane);
+  const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint32_t waves = gridDim.x * (kXThreads / 64);
+  for (uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
+    const uint32_t blk = t * kXTile + 16 * lane;
     const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
-    uint32_t c = 0;
-    x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t) { c++; }, [&](uint32_t) {});
+    // the lane's masks per segment, kept for the write below (at most a few segments per block)
+    uint32_t segK[4], segC[4], segZ[4], nseg = 0;
+    const uint32_t c = x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t, uint32_t) {},
+                              [&](uint32_t K, uint32_t C, uint32_t Z) {
+                                if (nseg < 4) {
+                                  segK[nseg] = K;
+                                  segC[nseg] = C;
+                                  segZ[nseg] = Z;
+                                }
+                                nseg++;
+                              });
     const uint32_t ex = wave_excl(c, lane);
     const uint32_t total = __shfl(ex + c, 63);
     const uint64_t start = tile_pre[t];
     const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
     uint32_t at = phase + ex;
-    x_lane(raw, n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t b) { S[at++] = uint8_t(b); },
-           [&](uint32_t) {});
+    auto put = [&](uint32_t K, uint32_t C, uint32_t Z) {
+      for (uint32_t m = K | C | Z; m; m &= m - 1) {
+        const uint32_t i = uint32_t(__ffs(m)) - 1u;
+        if ((C >> i) & 1u) S[at++] = '\n';
+        if ((K >> i) & 1u) S[at++] = uint8_t(W.byte(8 + i));
+        if ((Z >> i) & 1u) S[at++] = '\n';
+      }
+    };
+    if (nseg <= 4) {
+      for (uint32_t i = 0; i < nseg; i++) put(segK[i], segC[i], segZ[i]);
+    } else {
+      x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t, uint32_t) {}, put);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -335,6 +384,7 @@ size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files) { return ScratchLay
 
 hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                      void* scratch, uint64_t* xoff, hipStream_t s) {
+  if (n_bytes >= (uint64_t(1) << 32) - 64) return hipErrorInvalidValue;  // 32-bit positions
   const XformScratch L = ScratchLayout(n_bytes, n_files);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* chunk_file = reinterpret_cast<uint32_t*>(sc + L.chunk_file);
@@ -350,13 +400,14 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   }
   if (n_tiles) {
     const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
-    xf_count_kernel<<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart);
+    xf_count_kernel<<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file, tile_cnt, fstart);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   size_t sb = L.scan_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(sc + L.scan, sb, tile_cnt, tile_pre, int(n_tiles) + 1, s)) != hipSuccess)
     return e;
-  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, n_bytes, tile_pre, fstart, xoff);
+  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, uint32_t(n_bytes), tile_pre, fstart,
+                                                                       xoff);
   return hipGetLastError();
 }
 
@@ -367,7 +418,7 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   if (!n_tiles) return hipSuccess;
   const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
-  xf_write_kernel<<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files,
+  xf_write_kernel<<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files,
                                           reinterpret_cast<const uint32_t*>(sc + L.chunk_file),
                                           reinterpret_cast<const uint64_t*>(sc + L.tile_pre), out);
   return hipGetLastError();

@@ -248,18 +248,21 @@ class Scanner:
 
     # --- batched arena API (analyzer / bench) -------------------------------
     def scan_arena_async(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None,
-                         dev_paths=None, dev_path_offsets=None):
+                         dev_paths=None, dev_path_offsets=None, transform=None):
         """Pipelined scan (tsg_scan_submit): returns a PendingScan; .wait() gives the ScanResult.
         The arrays passed must stay alive until then (the PendingScan keeps references)."""
         keep, batch = self._batch(arena, offsets, paths, binary, dev_arena, dev_offsets, dev_paths,
-                                  dev_path_offsets)
+                                  dev_path_offsets, transform)
         h = c.c_void_p()
         rc = self._L.tsg_scan_submit(self._h, c.byref(batch), c.byref(h))
         if rc != 0:
             raise RuntimeError("tsg_scan_submit failed: %s" % _lib.last_error(self._L))
         return PendingScan(self, h, (keep, batch))
 
-    def _batch(self, arena, offsets, paths, binary, dev_arena, dev_offsets, dev_paths=None, dev_path_offsets=None):
+    def _batch(self, arena, offsets, paths, binary, dev_arena, dev_offsets, dev_paths=None, dev_path_offsets=None,
+               transform=None):
+        """transform: per-file pre-transform kinds (uint8; 1 = CR strip, 2 = printable runs) run on the
+        GPU over the host arena (the bytes as read)."""
         n = len(offsets) - 1
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -276,9 +279,10 @@ class Scanner:
         bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
         batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
                         dev_arena, dev_offsets, paths_addr, plen_ptr,
-                        bin_arr.ctypes.data if bin_arr is not None else None, None,
+                        bin_arr.ctypes.data if bin_arr is not None else None,
+                        transform.ctypes.data if transform is not None else None,
                         dev_paths, dev_path_offsets)
-        return (arena_buf, offs, parr, plen, bin_arr), batch
+        return (arena_buf, offs, parr, plen, bin_arr, transform), batch
 
     def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None, dev_paths=None,
                    dev_path_offsets=None):
