@@ -28,7 +28,15 @@ def main():
         if len(parts) >= 6 and "x" in parts[1] and want in parts[5]:
             a, b = (int(x, 16) for x in parts[0].split("-"))
             maps.append((a, b, int(parts[2], 16), parts[5]))
+    import os
     lib = maps[0][3]
+    if not os.path.exists(lib):  # a profile taken on another machine: the same library in this tree
+        here = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        for cand in ("trivy_amd", "oracle/build"):
+            q = os.path.join(here, cand, os.path.basename(lib))
+            if os.path.exists(q):
+                lib = q
+                break
     out = subprocess.run(["nm", "-C", "--defined-only", "-S", lib], capture_output=True, text=True).stdout
     ranges = []
     for ln in out.splitlines():

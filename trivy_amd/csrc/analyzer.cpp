@@ -506,6 +506,13 @@ void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
 // of the archive (*at_end) or on a malformed header (-1).
 int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
                  uint64_t max_regular, int threads, std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
+  // the previous window's entries own ~10^6 heap path strings: free them on
+  // the pool threads (a plain clear() freed them one by one on this thread)
+  static const bool pfree = !getenv("TSG_WALK_PFREE") || atoi(getenv("TSG_WALK_PFREE")) != 0;
+  if (pfree)
+    tsg::ParallelFor((out->size() + 4095) / 4096, threads, [&](size_t b) {
+      for (size_t i = b * 4096; i < std::min(out->size(), (b + 1) * 4096); i++) std::string().swap((*out)[i].fp);
+    });
   out->clear();
   *at_end = false;
   const uint64_t end = std::min<uint64_t>(n, p + window);

@@ -762,6 +762,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   uint32_t* q2 = s_q2 + wave * kCQ2;
   uint32_t* hbuf = s_hbuf + wave * kCWaveHits * 3;
   const uint32_t n_recs = P.counters[7] < P.rec_cap ? P.counters[7] : P.rec_cap;
+  uint32_t n_anchor = 0;  // anchor-item matches of this lane (stats; summed once per wave at the end)
   // phase C for one queued candidate: item `ix` whose window ends at lane l's block + k
   auto check_item = [&](uint32_t l, uint32_t k, uint32_t ix, uint32_t full) {
     const FilterItemGpu it = items[ix];
@@ -839,7 +840,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     int after = check_to < it.n ? -1 : 1;  // lookahead sets: -1 unchecked, 0 fail, 1 pass
     for (uint32_t d = 0; d < it.n_ids; d++) {
       const uint32_t aid = item_ids[it.ids_off + d];
-      atomicAdd(&cnt[3], 1u);
+      n_anchor++;
       const FollowLut lut = reinterpret_cast<const FollowLut*>(tabs + P.t_luts)[aid];
       if (lut.n[0] && e < P.n_bytes) {
         if (!have_x) {  // through the caches: the lane's 48-B window rarely holds the span
@@ -933,6 +934,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave * 64; r0 < n_recs; r0 += stride) {
     // ---- A: one block per lane
     const uint32_t r = r0 + lane;
+    uint32_t fire_e[4], n_fire = 0;
     if (r < n_recs) {
       const uint64_t base = uint64_t(P.recs[r]) * 16;
       const uint64_t w0 = base >= 16 ? base - 16 : 0;
@@ -975,12 +977,29 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
           uint32_t fm = 0;
 #pragma unroll
           for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
-          const uint32_t e = lane | (k << 6) | (fm << 10);
-          const uint32_t slot = atomicAdd(&cnt[1], 1u);
-          if (slot < kCQ1) q1[slot] = e;
-          else do_fire(e);  // queue full: handle in place
+          fire_e[n_fire < 4 ? n_fire : 3] = lane | (k << 6) | (fm << 10);
+          if (n_fire >= 4) do_fire(fire_e[3]);  // more than 4 fires in one block: handle in place
+          n_fire++;
         }
       }
+    }
+    // the fires into the wave's queue: a prefix sum over the lanes' counts
+    // instead of an LDS atomic per fire
+    {
+      const uint32_t mine = n_fire < 4 ? n_fire : 4u;
+      uint32_t incl = mine;
+#pragma unroll
+      for (int x = 1; x < 64; x <<= 1) {
+        const uint32_t t = __shfl_up(incl, x);
+        if (lane >= uint32_t(x)) incl += t;
+      }
+      const uint32_t at = __builtin_amdgcn_readfirstlane(cnt[1]) + incl - mine;
+      for (uint32_t i = 0; i < mine; i++) {
+        if (at + i < kCQ1) q1[at + i] = fire_e[i];
+        else do_fire(fire_e[i]);  // queue full: handle in place
+      }
+      wave_sync();
+      if (lane == 63) cnt[1] = at + mine < kCQ1 ? at + mine : kCQ1;
     }
     wave_sync();
     // ---- B: one fire per lane
@@ -998,8 +1017,9 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     wave_sync();
   }
   flush_staged(hbuf, &cnt[0], P.hits, P.hit_cap, P.counters, lane);
-  wave_sync();
-  if (lane == 0 && cnt[3]) atomicAdd(&P.counters[11], cnt[3]);  // anchor-item matches (stats)
+#pragma unroll
+  for (int x = 32; x >= 1; x >>= 1) n_anchor += __shfl_xor(n_anchor, x);
+  if (lane == 0 && n_anchor) atomicAdd(&P.counters[11], n_anchor);  // anchor-item matches (stats)
 }
 
 // Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
@@ -1342,9 +1362,12 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
 // emitted unverified (a candidate is always safe -- the host pass is exact).
 constexpr int kFsMaxRounds = 6;
 
-template <int W>
+template <int W, typename Acc>
 __device__ bool nfa_chunk(const uint8_t* __restrict arena, uint64_t a, uint64_t b, uint64_t* D,
-                          const uint64_t* __restrict tab) {  // arena [a, b), injection everywhere
+                          const uint64_t* __restrict tab, Acc on_acc, bool inject = true) {
+  // arena [a, b) from state D, a start injected at every byte (inject) or
+  // none (D's paths only); on_acc(abs): an accept after byte abs, false stops
+  // the chunk there
   uint64_t O[W], Lp[W], F[W];
 #pragma unroll
   for (int w = 0; w < W; w++) {
@@ -1355,13 +1378,14 @@ __device__ bool nfa_chunk(const uint8_t* __restrict arena, uint64_t a, uint64_t 
   const uint64_t* B = tab + 3 * W;
   uint4 buf = make_uint4(0, 0, 0, 0);
   uint64_t buf_at = ~uint64_t(0);
+  bool any = false;
   for (uint64_t abs = a; abs < b; abs++) {
     if ((abs & ~uint64_t(15)) != buf_at) {
       buf_at = abs & ~uint64_t(15);
       buf = load16(arena + buf_at);
     }
     const uint32_t byte = (word_of(buf, uint32_t(abs >> 2) & 3) >> ((abs & 3) * 8)) & 0xFFu;
-    uint64_t carry = 1, T[W];
+    uint64_t carry = inject ? 1 : 0, T[W];
 #pragma unroll
     for (int w = 0; w < W; w++) {
       T[w] = (D[w] << 1) | carry | (D[w] & Lp[w]);
@@ -1382,20 +1406,81 @@ __device__ bool nfa_chunk(const uint8_t* __restrict arena, uint64_t a, uint64_t 
       D[w] = (T[w] & Bb[w]) | (keep ? D[w] : 0);
       acc |= D[w] & F[w];
     }
-    if (acc) return true;
+    if (acc) {
+      any = true;
+      if (!on_acc(abs)) return true;
+    }
   }
-  return false;
+  return any;
 }
 
+// Full scan of one (file, rule) pair by a wave: 64 lane
+// chunks, exit states passed on until no chunk's entry state grows.  A rule
+// with bounded match length emits candidate windows of match starts around
+// its accepts (a merged run per lane, at most kFsLaneWins per lane per pass,
+// then the rest of the file); unbounded rules, or a pass that does not
+// settle, make the whole file the candidate (returns true).
+constexpr uint32_t kFsLaneWins = 32;
+
 template <int W>
-__device__ bool fullscan_pair(const NfaParams& P, const uint8_t* arena, uint64_t fs, uint64_t len,
-                              const uint64_t* tab, uint32_t lane) {
+__device__ bool fullscan_pair(const NfaParams& P, const uint8_t* arena, uint32_t f, uint32_t r, uint64_t fs,
+                              uint64_t len, const uint64_t* tab, const RuleGpu& rg, uint32_t lane) {
   const uint64_t cs = (len + 63) / 64 > P.fs_chunk ? (len + 63) / 64 : uint64_t(P.fs_chunk);
   const uint64_t a = fs + uint64_t(lane) * cs, b = a + cs < fs + len ? a + cs : fs + len;
   const bool mine = a < fs + len;
+  const bool win = rg.max_len != kNoMaxLen;
+  int64_t wlo = 0, whi = -1;  // the lane's open window of match starts (file-relative, inclusive)
+  uint32_t n_win = 0;
+  auto flush = [&]() {
+    if (whi >= wlo) put_candidate(P.cands, P.cand_cap, P.counters, f, r, wlo, whi);
+    whi = -1;
+  };
+  auto on_acc = [&](uint64_t abs) -> bool {
+    if (!win) return false;  // the first accept decides: the whole file
+    const int64_t e = int64_t(abs + 1 - fs);  // the match ends before e
+    const int64_t lo = e - int64_t(rg.max_len) > 0 ? e - int64_t(rg.max_len) : 0;
+    const int64_t hi = e - int64_t(rg.min_len) < int64_t(len) ? e - int64_t(rg.min_len) : int64_t(len);
+    if (whi >= wlo && lo <= whi + 1 && hi + 1 >= wlo) {  // overlaps or touches the open window
+      whi = hi > whi ? hi : whi;
+      wlo = lo < wlo ? lo : wlo;
+      return true;
+    }
+    flush();
+    wlo = lo;
+    if (++n_win > kFsLaneWins) {  // many windows: the rest of the file from here
+      whi = int64_t(len);
+      return false;
+    }
+    whi = hi;
+    return true;
+  };
   uint64_t D[W] = {}, E[W] = {};  // exit state, the entry it came from
-  bool acc = mine && nfa_chunk<W>(arena, a, b, D, tab);
-  if (__ballot(acc)) return true;
+  bool acc = mine && nfa_chunk<W>(arena, a, b, D, tab, on_acc);
+  if (!win && __ballot(acc)) return true;
+  if (win && cs >= uint64_t(rg.max_len) + 4) {
+    // Bounded matches: a match crossing into chunk c starts in the max_len
+    // bytes before it, all inside chunk c-1, so lane c-1's exit state already
+    // holds every such path and none of chunk c's exits depends on its entry;
+    // the paths from lane c-1 only need the first max_len bytes of chunk c
+    // (no start injected), and no fixpoint rounds are needed.
+    uint64_t S[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint32_t lo = __shfl_up(uint32_t(D[w]), 1), hi = __shfl_up(uint32_t(D[w] >> 32), 1);
+      S[w] = lane == 0 ? 0 : (uint64_t(hi) << 32) | lo;
+    }
+    bool any_in = false;
+#pragma unroll
+    for (int w = 0; w < W; w++) any_in = any_in || S[w] != 0;
+    if (mine && any_in) {
+      flush();
+      n_win = 0;
+      const uint64_t e = a + uint64_t(rg.max_len) + 4 < b ? a + uint64_t(rg.max_len) + 4 : b;
+      nfa_chunk<W>(arena, a, e, S, tab, on_acc, false);
+    }
+    flush();
+    return false;
+  }
   for (int round = 0; round < kFsMaxRounds; round++) {
     uint64_t in[W];
     bool grow = false;
@@ -1406,7 +1491,10 @@ __device__ bool fullscan_pair(const NfaParams& P, const uint8_t* arena, uint64_t
       if (lane == 0) in[w] = 0;
       grow = grow || (in[w] & ~E[w]) != 0;
     }
-    if (!__ballot(grow && mine)) return false;  // fixpoint: no chunk's entry state changed
+    if (!__ballot(grow && mine)) {  // fixpoint: no chunk's entry state changed
+      flush();
+      return false;
+    }
     if (grow && mine) {
       uint64_t S[W];
 #pragma unroll
@@ -1414,13 +1502,16 @@ __device__ bool fullscan_pair(const NfaParams& P, const uint8_t* arena, uint64_t
         E[w] |= in[w];
         S[w] = E[w];
       }
-      acc = nfa_chunk<W>(arena, a, b, S, tab);
+      flush();  // a re-run finds the chunk's accepts again from its start
+      n_win = 0;
+      acc = nfa_chunk<W>(arena, a, b, S, tab, on_acc);
 #pragma unroll
       for (int w = 0; w < W; w++) D[w] = S[w];
     }
-    if (__ballot(acc)) return true;
+    if (!win && __ballot(acc)) return true;
   }
-  return true;  // not settled: emit (always safe)
+  flush();
+  return true;  // not settled: the whole file (always safe)
 }
 
 __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
@@ -1452,10 +1543,10 @@ __global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
       if (rg.nfa_words != 0) {
         const uint64_t* tab = P.nfa + rg.nfa_off;
         switch (rg.nfa_words) {
-          case 1: acc = fullscan_pair<1>(P, P.arena, fs, len, tab, lane); break;
-          case 2: acc = fullscan_pair<2>(P, P.arena, fs, len, tab, lane); break;
-          case 3: acc = fullscan_pair<3>(P, P.arena, fs, len, tab, lane); break;
-          default: acc = fullscan_pair<4>(P, P.arena, fs, len, tab, lane); break;
+          case 1: acc = fullscan_pair<1>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
+          case 2: acc = fullscan_pair<2>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
+          case 3: acc = fullscan_pair<3>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
+          default: acc = fullscan_pair<4>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
         }
       }
       if (acc && lane == 0) put_candidate(P.cands, P.cand_cap, P.counters, pf, pr, 0, int64_t(len));

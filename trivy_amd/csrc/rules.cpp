@@ -1082,6 +1082,7 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
   for (size_t ri = 0; ri < src.size(); ri++) {
     const RuleSrc& r = src[ri];
     RuleGpu rg{};
+    rg.max_len = kNoMaxLen;
     std::unique_ptr<Regex> re;
     if (r.has_regex) {
       re = Regex::Compile(r.regex, err);
@@ -1210,6 +1211,12 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
       } else {
         rg.anchored = 0;
         out->n_fullscan_rules++;
+      }
+      {  // match length bounds: the fold runes widen the max, the min ignores them
+        const int64_t mx = Analyzer(re->nodes(), true).Bytes(re->root()).second;
+        const int64_t mn = Analyzer(re->nodes(), false).Bytes(re->root()).first;
+        rg.min_len = uint32_t(std::min<int64_t>(std::max<int64_t>(mn, 0), 1 << 30));
+        rg.max_len = mx >= (int64_t(1) << 20) ? kNoMaxLen : uint32_t(mx);
       }
       BuildNfa(Relax(re->nodes(), re->root()), &out->nfa, &rg);
     }

@@ -78,7 +78,11 @@ struct RuleGpu {  // mirrored on the device
   uint8_t has_regex;
   uint32_t kw_off, kw_cnt;  // into rule_kw
   uint32_t kw_match_implied;  // every match holds a keyword unless the file has U+017F (no GPU bits)
+  // bounds of a match's length in bytes (max_len = kNoMaxLen: unbounded): a
+  // full-scan accept after byte p puts the match start in [p+1-max, p+1-min]
+  uint32_t min_len, max_len;
 };
+constexpr uint32_t kNoMaxLen = 0xFFFFFFFFu;
 
 // Prefilter item: a fixed-width sequence of byte sets that
 // every occurrence of a keyword (ASCII case-insensitive), an anchor literal
