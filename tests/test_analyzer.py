@@ -259,6 +259,38 @@ def test_native_walk_generated_layer_vs_oracle(host_analyzer, gpu_transform):
     assert any(b"\r" in f[2] for f in files)  # CRLF files present (stripped in want)
 
 
+@pytest.fixture(scope="module")
+def layer_30mb():
+    from trivy_amd import corpus
+    layer = corpus.generate_layer(30_000_000, seed=corpus.SEED + 11)
+    files, wh, opq = oan.walk_layer_tar(layer.tobytes())
+    return layer, files, wh
+
+
+@pytest.mark.parametrize("arena_mb", [2, 12, 64])
+@pytest.mark.parametrize("gpu_transform", [False, True])
+def test_native_walk_bulk_accept_vs_oracle(host_analyzer, layer_30mb, arena_mb, gpu_transform):
+    """~20 k entries: the accept step takes whole 4,096-entry blocks in bulk (batches
+    of 12 and 64 MiB), cuts inside a block (12 MiB) and entry by entry (2 MiB)."""
+    from trivy_amd.analyzer.secret import Collector, _CTarStats
+    layer, files, wh = layer_30mb
+    o = oan.SecretAnalyzer("")
+    want = [a for a in (o.prepare(fp, "", b) for fp, sz, b in files if o.required(fp, sz)) if a is not None]
+    st = _CTarStats()
+    coll = Collector(host_analyzer, arena_mb << 20, gpu_transform)
+    got, cursor, batches = [], 0, 0
+    while True:
+        rc, cursor = coll.add_tar(layer, cursor, st)
+        got += [coll.file(i) for i in range(coll.files())]
+        coll.reset()
+        batches += 1
+        if rc == 0:
+            break
+    assert got == want
+    assert st.whiteouts == wh and st.added == len(want) and st.regular == len(files)
+    assert batches == (1 if arena_mb == 64 else batches) and (arena_mb == 64 or batches > 1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("gpu_transform", [False, True])
 def test_gpu_analyze_generated_layer_vs_oracle(gpu_transform):

@@ -237,11 +237,13 @@ def test_host_tail_newline_hints(hints):
 
 
 def test_allow_path_literal_fast_path(tmp_path):
-    """Allow-path regexes that are one literal with optional ^ / $ are matched by
-    a byte compare (Matcher::simple); the result must equal the regex's, including
-    sources that only look literal (escaped anchors, trailing escaped '$', classes)."""
+    """Allow-path regexes that are one literal (or one group of literal alternatives)
+    with optional ^ / $ are matched by byte compares (Matcher::simple); the result must
+    equal the regex's, including sources that only look literal (escaped anchors,
+    trailing escaped '$', classes, an empty alternative, two groups)."""
     pats = [r"\.md$", r"^usr\/share\/", r"\/vendor\/", r"^exact\.txt$", r"a\$", r"b\\$", r"\d\.log$",
-            r"^$x", r"c\.d", r"x.y"]
+            r"^$x", r"c\.d", r"x.y", r"^opt\/(?:alpha|be|)\/", r"(?:gam|delt)a\.cfg$", r"^(?:one|two)$",
+            r"q(?:r|s)(?:t|u)"]
     cfg_path = tmp_path / "trivy-secret.yaml"
     cfg_path.write_text("allow-rules:\n" + "".join(
         "  - id: p%d\n    path: '%s'\n" % (i, p.replace("'", "''")) for i, p in enumerate(pats)))
@@ -249,7 +251,8 @@ def test_allow_path_literal_fast_path(tmp_path):
     body = b"k = AKIA" + b"Q" * 16 + b"\n"
     paths = ["README.md", "README.mdx", "usr/share/x.txt", "x/usr/share/y", "src/vendor/z.go", "vendor/z.go",
              "exact.txt", "exact.txt2", "a$", "xa$y", "b\\", "b\\x", "3.log", "x.log", "c.d", "cxd", "xzy",
-             "x.y", "plain.txt", "$x"]
+             "x.y", "plain.txt", "$x", "opt/alpha/k", "opt/be/k", "opt//k", "opt/beta/k", "x/opt/be/k",
+             "gamma.cfg", "a/delta.cfg", "delt.cfg", "one", "two", "one2", "qrt", "qsu", "qrx", "x|y"]
     files = [(p, body) for p in paths]
     got = host_tail_scan(cfg, files)
     o = osc.new_scanner(osc.parse_config(str(cfg_path)))

@@ -9,7 +9,7 @@ rc=$?; tail -3 gpurun_out/gpu_tests_$T.log; [ $rc -eq 0 ] || exit $rc
 for s in 1 2 1 2; do
   TSG_GPU_SLOTS=$s timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ingest-steps 0 > gpurun_out/bench_${T}_s$s.json 2> gpurun_out/bench_${T}_s$s.err
   rc=$?; echo "slots=$s"; python tools/bench_brief.py gpurun_out/bench_${T}_s$s.json; [ $rc -eq 0 ] || exit $rc
-  python -c "import json;d=json.load(open('gpurun_out/bench_${T}_s$s.json'));print(d['ms_per_step'],d['host_cpu']['process_cpu_ms_per_step'],d['host_cpu']['cpus_used'],d['parity']['mismatches'])"
+  python -c "import json;d=json.load(open('gpurun_out/bench_${T}_s$s.json'));print(d['ms_per_step'],d['host_cpu']['process_cpu_ms_per_step'],d['host_cpu']['cpus_used'],(d.get("parity") or {}).get("mismatches"))"
 done
 timeout -k 10 400 python bench.py --workload c3f --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/wl_${T}_c3f.json 2> gpurun_out/wl_${T}_c3f.err
 rc=$?; python tools/bench_brief.py gpurun_out/wl_${T}_c3f.json; tail -2 gpurun_out/wl_${T}_c3f.err; [ $rc -eq 0 ] || exit $rc

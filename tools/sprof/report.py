@@ -7,6 +7,22 @@ import subprocess
 import sys
 
 
+def to_vaddr(lib):
+    """File offset -> link-time address for a library's executable LOAD segments."""
+    segs = []
+    out = subprocess.run(["readelf", "-lW", lib], capture_output=True, text=True).stdout
+    for ln in out.splitlines():
+        p = ln.split()
+        if p and p[0] == "LOAD" and "E" in "".join(p[6:-1]):
+            segs.append((int(p[1], 16), int(p[2], 16), int(p[4], 16)))  # offset, vaddr, filesz
+    def f(off):
+        for o, v, n in segs:
+            if o <= off < o + n:
+                return off - o + v
+        return off
+    return f
+
+
 def main():
     path = sys.argv[1]
     want = sys.argv[2] if len(sys.argv) > 2 else "libtsg"
@@ -46,8 +62,9 @@ def main():
         syms.sort()
         addrs = [s[0] for s in syms]
         cnt = collections.Counter()
+        va = to_vaddr(name)
         for off in per[name]:
-            i = bisect.bisect_right(addrs, off) - 1
+            i = bisect.bisect_right(addrs, va(off)) - 1
             cnt[syms[i][1][:110] if i >= 0 else "?"] += 1
         print("--", name)
         for s, n in cnt.most_common(30):
@@ -84,7 +101,8 @@ def lines(path, want):
                 offs.append(pc - a + off)
                 tags.append(tag)
                 lib = name
-    # file offset -> vaddr: for a PIC .so the text segment's vaddr == file offset in practice
+    va = to_vaddr(lib)
+    offs = [va(o) for o in offs]
     uniq = sorted(set(offs))
     out = subprocess.run(["addr2line", "-f", "-C", "-e", lib] + ["%x" % o for o in uniq], capture_output=True,
                          text=True).stdout.splitlines()

@@ -280,16 +280,16 @@ bool ParseNumeric(const uint8_t* b, size_t n, int64_t* out) {  // parseNumeric
 bool ChecksumOK(const uint8_t* b) {
   int64_t want = 0;
   if (!ParseNumeric(b + 148, 8, &want)) return false;
-  // unsigned and signed byte sums with the checksum field read as spaces
-  // (two plain loops: the compiler vectorises them)
-  int32_t u = 0, s = 0;
+  // the unsigned byte sum with the checksum field read as spaces, else the
+  // signed one (old writers); plain loops, vectorised by the compiler
+  int32_t u = 0;
   for (int i = 0; i < 512; i++) u += b[i];
+  for (int i = 148; i < 156; i++) u += ' ' - b[i];
+  if (want == u) return true;
+  int32_t s = 0;
   for (int i = 0; i < 512; i++) s += int8_t(b[i]);
-  for (int i = 148; i < 156; i++) {
-    u += ' ' - b[i];
-    s += ' ' - int8_t(b[i]);
-  }
-  return want == u || want == s;
+  for (int i = 148; i < 156; i++) s += ' ' - int8_t(b[i]);
+  return want == s;
 }
 // PAX records "%d %s=%s\n" (parsePAX): path, size and linkpath matter here.
 bool ParsePax(const uint8_t* d, uint64_t n, std::string* path, int64_t* size, bool* has_path, bool* has_size) {
@@ -379,7 +379,17 @@ struct TarEntry {
   uint8_t what;          // 0 other, 1 whiteout, 2 opaque dir, 3 regular file
   uint8_t has_pax_path;
   uint8_t bad;           // the entry header's checksum is wrong (checked on the threads)
-  std::string fp;        // PAX path, then the cleaned path (walker/tar.go:46-48)
+  // The cleaned path (walker/tar.go:46-48): a view of the header's name field
+  // in the archive itself when that is already the answer (a ustar name with
+  // no prefix, clean), else an owned string (PAX / GNU long names, prefixes,
+  // names that Clean changes) -- no allocation per entry on the common path.
+  std::string fp_own;
+  uint64_t fp_off = 0;
+  uint32_t fp_len = 0;
+  uint8_t fp_owned = 0;
+  std::string_view path(const uint8_t* tar) const {
+    return fp_owned ? std::string_view(fp_own) : std::string_view(reinterpret_cast<const char*>(tar + fp_off), fp_len);
+  }
   // filled by the parallel pass
   uint8_t state;         // 0 not required, 1 binary skipped, 2 add
   uint8_t bin;
@@ -454,7 +464,8 @@ int ChainEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
   e->next = e->data + ((dsz + 511) & ~uint64_t(511));
   e->what = type == '0' ? 3 : 0;
   if (has_pax_path) {
-    e->fp = std::move(pax_path);
+    e->fp_own = std::move(pax_path);
+    e->fp_owned = 1;
     e->has_pax_path = 1;
   }
   return 0;
@@ -474,15 +485,16 @@ void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
   if (dbg) {
     auto t1 = std::chrono::steady_clock::now();
     g_eval_ns[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-    const bool req = e->what == 3 && Required(c->a, e->fp.data(), e->fp.size(), int64_t(e->size));
+    const std::string_view fp = e->path(tar);
+    const bool req = e->what == 3 && Required(c->a, fp.data(), fp.size(), int64_t(e->size));
     g_eval_ns[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     if (!req) return;
-  } else if (e->what != 3 || !Required(c->a, e->fp.data(), e->fp.size(), int64_t(e->size))) {
+  } else if (e->what != 3 || !Required(c->a, e->path(tar).data(), e->path(tar).size(), int64_t(e->size))) {
     return;
   }
   const uint8_t* d = tar + e->data;
   e->bin = tsg::IsBinaryHead(d, e->size) ? 1 : 0;
-  if (e->bin && tsg::GoExt(e->fp) != ".pyc") {
+  if (e->bin && tsg::GoExt(std::string(e->path(tar))) != ".pyc") {
     e->state = 1;
     return;
   }
@@ -506,13 +518,6 @@ void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
 // of the archive (*at_end) or on a malformed header (-1).
 int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
                  uint64_t max_regular, int threads, std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
-  // the previous window's entries own ~10^6 heap path strings: free them on
-  // the pool threads (a plain clear() freed them one by one on this thread)
-  static const bool pfree = !getenv("TSG_WALK_PFREE") || atoi(getenv("TSG_WALK_PFREE")) != 0;
-  if (pfree)
-    tsg::ParallelFor((out->size() + 4095) / 4096, threads, [&](size_t b) {
-      for (size_t i = b * 4096; i < std::min(out->size(), (b + 1) * 4096); i++) std::string().swap((*out)[i].fp);
-    });
   out->clear();
   *at_end = false;
   const uint64_t end = std::min<uint64_t>(n, p + window);
@@ -657,7 +662,8 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
   e->bad = ChecksumOK(h) ? 0 : 1;
   if (e->has_pax_path) return;
   if (e->long_len != ~uint64_t(0)) {
-    e->fp = CStr(tar + e->long_off, size_t(e->long_len));
+    e->fp_own = CStr(tar + e->long_off, size_t(e->long_len));
+    e->fp_owned = 1;
   } else {
     auto clen = [](const uint8_t* b, size_t n) {
       size_t k = 0;
@@ -667,13 +673,17 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
     const size_t nl = clen(h, 100);
     size_t pl = 0;
     if (std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0) pl = clen(h + 345, 155);
-    e->fp.clear();
-    e->fp.reserve(pl + 1 + nl);
     if (pl) {
-      e->fp.append(reinterpret_cast<const char*>(h + 345), pl);
-      e->fp.push_back('/');
+      e->fp_own.reserve(pl + 1 + nl);
+      e->fp_own.append(reinterpret_cast<const char*>(h + 345), pl);
+      e->fp_own.push_back('/');
+      e->fp_own.append(reinterpret_cast<const char*>(h), nl);
+      e->fp_owned = 1;
+    } else {
+      e->fp_off = e->hdr;
+      e->fp_len = uint32_t(nl);
+      e->fp_owned = 0;
     }
-    e->fp.append(reinterpret_cast<const char*>(h), nl);
   }
 }
 
@@ -681,16 +691,127 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
 // classify whiteout / opaque markers.
 void Classify(const uint8_t* tar, TarEntry* e) {
   Resolve(tar, e);
-  if (tar[e->hdr + 156] == '\0' && !e->fp.empty() && e->fp.back() == '/') e->what = 0;  // TypeRegA dir
-  if (!tsg::GoPathIsClean(e->fp.data(), e->fp.size())) e->fp = tsg::GoPathClean(e->fp);
+  std::string_view fp = e->path(tar);
+  if (tar[e->hdr + 156] == '\0' && !fp.empty() && fp.back() == '/') e->what = 0;  // TypeRegA dir
+  if (!tsg::GoPathIsClean(fp.data(), fp.size())) {
+    e->fp_own = tsg::GoPathClean(std::string(fp));
+    e->fp_owned = 1;
+    fp = e->fp_own;
+  }
   size_t t = 0;
-  while (t < e->fp.size() && e->fp[t] == '/') t++;
-  if (t) e->fp.erase(0, t);
-  const size_t slash = e->fp.rfind('/');
-  const char* file_name = e->fp.c_str() + (slash == std::string::npos ? 0 : slash + 1);
-  if (std::strcmp(file_name, ".wh..wh..opq") == 0) e->what = 2;
-  else if (std::strncmp(file_name, ".wh.", 4) == 0) e->what = 1;
+  while (t < fp.size() && fp[t] == '/') t++;
+  if (t) {
+    if (e->fp_owned) {
+      e->fp_own.erase(0, t);
+    } else {
+      e->fp_off += t;
+      e->fp_len -= uint32_t(t);
+    }
+    fp = e->path(tar);
+  }
+  const size_t slash = fp.rfind('/');
+  const std::string_view file_name = fp.substr(slash == std::string_view::npos ? 0 : slash + 1);
+  if (file_name == ".wh..wh..opq") e->what = 2;
+  else if (file_name.substr(0, 4) == ".wh.") e->what = 1;
 }
+}  // namespace
+
+namespace {
+// The bulk part of the walk's accept step: the longest run of whole
+// kAcceptBlock-entry blocks from k0 that fits the batch (limit and arena) and
+// holds no bad header, appended to the collector exactly as the entry-by-entry
+// loop would (same offsets, paths, kinds, flags, stats).  Returns the number
+// of entries taken.
+constexpr size_t kAcceptBlock = 4096;
+size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry>& ents, size_t k0, tsg_tar_stats* st) {
+  const size_t nb = (ents.size() - k0) / kAcceptBlock;
+  if (nb == 0) return 0;
+  struct Sum {
+    uint64_t files = 0, used = 0, acct = 0, pbytes = 0, input = 0;
+    uint64_t entries = 0, whiteouts = 0, opaque = 0, regular = 0, required = 0, skipped = 0;
+    bool bad = false;
+  };
+  std::vector<Sum> sum(nb);
+  tsg::ParallelFor(nb, c->threads, [&](size_t b) {
+    Sum& q = sum[b];
+    for (size_t i = k0 + b * kAcceptBlock; i < k0 + (b + 1) * kAcceptBlock; i++) {
+      const TarEntry& e = ents[i];
+      q.bad = q.bad || e.bad;
+      if (e.state == 2) {
+        q.files++;
+        q.used += c->gpu_xform ? e.size : e.out_len;
+        q.acct += e.out_len;
+        q.pbytes += 1 + e.path(tar).size();
+        q.input += e.size;
+      }
+      q.whiteouts += e.what == 1;
+      q.opaque += e.what == 2;
+      q.regular += e.what == 3;
+      q.required += e.state != 0;
+      q.skipped += e.state == 1;
+    }
+    q.entries = kAcceptBlock;
+  });
+  // the blocks that fit, and each one's starting row
+  std::vector<Sum> at(1);
+  uint64_t acct = c->acct(), used = c->used;
+  size_t m = 0;
+  for (; m < nb; m++) {
+    const Sum& q = sum[m];
+    if (q.bad || acct + q.acct > c->limit || used + q.used + 64 > c->cap) break;
+    acct += q.acct;
+    used += q.used;
+    Sum n = at.back();
+    n.files += q.files;
+    n.used += q.used;
+    n.pbytes += q.pbytes;
+    at.push_back(n);
+  }
+  if (m == 0) return 0;
+  const size_t f0 = c->files(), p0 = c->path_pool.size();
+  const uint64_t u0 = c->used;
+  const Sum& tot = at[m];
+  c->offs.resize(f0 + 1 + tot.files);
+  c->path_off.resize(f0 + 1 + tot.files);
+  c->path_pool.resize(p0 + tot.pbytes);
+  c->binary.resize(f0 + tot.files);
+  if (c->gpu_xform) c->kinds.resize(f0 + tot.files);
+  tsg::ParallelFor(m, c->threads, [&](size_t b) {
+    size_t f = f0 + at[b].files, pp = p0 + at[b].pbytes;
+    uint64_t u = u0 + at[b].used;
+    for (size_t i = k0 + b * kAcceptBlock; i < k0 + (b + 1) * kAcceptBlock; i++) {
+      TarEntry& e = ents[i];
+      if (e.state != 2) continue;
+      e.out_off = u;
+      u += c->gpu_xform ? e.size : e.out_len;
+      if (c->gpu_xform) c->kinds[f] = e.bin ? 2 : 1;
+      c->binary[f] = e.bin;
+      c->offs[f + 1] = u;
+      const std::string_view fp = e.path(tar);
+      c->path_pool[pp] = '/';  // Dir "" (image files, secret.go:130-135)
+      std::memcpy(&c->path_pool[pp + 1], fp.data(), fp.size());
+      pp += 1 + fp.size();
+      c->path_off[f + 1] = pp;
+      f++;
+    }
+  });
+  for (size_t b = 0; b < m; b++) {
+    const Sum& q = sum[b];
+    c->used += q.used;
+    if (c->gpu_xform) c->bound += q.acct;
+    c->input_bytes += q.input;
+    st->added += q.files;
+    st->input_bytes += q.input;
+    st->entries += q.entries;
+    st->whiteouts += q.whiteouts;
+    st->opaque_dirs += q.opaque;
+    st->regular += q.regular;
+    st->required += q.required;
+    st->skipped_binary += q.skipped;
+  }
+  return m * kAcceptBlock;
+}
+
 }  // namespace
 
 extern "C" {
@@ -736,9 +857,11 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     double t1 = dbg ? now() : 0;
     double t2 = dbg ? now() : 0;
     const size_t kBlock = 64;
-    // 2. accept in order
+    // 2. accept in order: whole blocks of entries that fit the batch in bulk
+    // (per-block sums, then the blocks' rows written in parallel), the block
+    // where the batch fills entry by entry
     const size_t k0 = W.pos;
-    size_t k = k0;
+    size_t k = k0 + AcceptBlocks(c, tar, W.ents, k0, st);
     bool full = false;
     for (; k < W.ents.size(); k++) {
       TarEntry& e = W.ents[k];
@@ -763,7 +886,8 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         }
         c->offs.push_back(c->used);
         c->path_pool.push_back('/');  // Dir "" (image files, secret.go:130-135)
-        c->path_pool.append(e.fp);
+        const std::string_view fp = e.path(tar);
+      c->path_pool.append(fp.data(), fp.size());
         c->path_off.push_back(c->path_pool.size());
         c->binary.push_back(e.bin);
         c->input_bytes += e.size;

@@ -87,7 +87,7 @@ bool MakeMatcher(const char* src, std::unique_ptr<tsg::Matcher>* out, std::strin
   (*out)->lits = tsg::RequiredLiterals(*re);
   (*out)->re = std::move(re);
   tsg::Matcher& m = **out;
-  m.simple = tsg::SimpleLiteral(src, &m.simple_lit, &m.simple_begin, &m.simple_end);
+  m.simple = tsg::SimpleLiteral(src, &m.simple_lits, &m.simple_begin, &m.simple_end);
   return true;
 }
 

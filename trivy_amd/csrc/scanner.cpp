@@ -291,7 +291,7 @@ void SortFindings(FileFindings* f, const std::vector<RuleSpec>& rules) {
   Pdqsort(d, 0, n, BitsLen(unsigned(n)));
 }
 
-bool SimpleLiteral(const std::string& src, std::string* lit, bool* begin, bool* end) {
+bool SimpleLiteral(const std::string& src, std::vector<std::string>* lits, bool* begin, bool* end) {
   static const std::string kMeta = "\\.+*?()|[]{}^$";
   size_t i = 0, e = src.size();
   *begin = e > 0 && src[0] == '^';
@@ -306,9 +306,13 @@ bool SimpleLiteral(const std::string& src, std::string* lit, bool* begin, bool* 
       e--;
     }
   }
-  lit->clear();
+  // prefix, at most one (?:alt|alt...) group of plain literals, suffix
+  std::string pre, post;
+  std::vector<std::string> alts;
+  int part = 0;  // 0 prefix, 1 inside the group, 2 suffix
   while (i < e) {
     const unsigned char c = static_cast<unsigned char>(src[i]);
+    std::string* out = part == 0 ? &pre : part == 2 ? &post : &alts.back();
     // non-ASCII: Go's regexp matches runes (an invalid byte decodes to
     // U+FFFD, which a literal EF BF BD matches), so keep the regex for these
     if (c >= 0x80) return false;
@@ -316,25 +320,46 @@ bool SimpleLiteral(const std::string& src, std::string* lit, bool* begin, bool* 
       if (i + 1 >= e) return false;
       const unsigned char d = static_cast<unsigned char>(src[i + 1]);
       if (d >= 0x80 || std::isalnum(d) || d == '_') return false;  // \d, \b, \x.. and the like
-      lit->push_back(char(d));
+      out->push_back(char(d));
       i += 2;
+    } else if (part == 0 && src.compare(i, 3, "(?:") == 0) {
+      part = 1;
+      alts.emplace_back();
+      i += 3;
+    } else if (part == 1 && c == '|') {
+      alts.emplace_back();
+      i++;
+    } else if (part == 1 && c == ')') {
+      part = 2;
+      i++;
     } else {
       if (kMeta.find(char(c)) != std::string::npos) return false;
-      lit->push_back(char(c));
+      out->push_back(char(c));
       i++;
     }
   }
-  return !lit->empty();
+  if (part == 1) return false;
+  lits->clear();
+  if (alts.empty()) alts.emplace_back();
+  for (auto& x : alts) {
+    lits->push_back(pre + x + post);
+    if (lits->back().empty()) return false;  // matches everywhere: keep the regex
+  }
+  return true;
 }
 
 bool Matcher::MatchSimple(const uint8_t* s, size_t n) const {
-  const size_t k = simple_lit.size();
-  if (k > n) return false;
-  const char* l = simple_lit.data();
-  if (simple_begin && simple_end) return k == n && std::memcmp(s, l, k) == 0;
-  if (simple_begin) return std::memcmp(s, l, k) == 0;
-  if (simple_end) return std::memcmp(s + n - k, l, k) == 0;
-  return memmem(s, n, l, k) != nullptr;
+  for (const std::string& lit : simple_lits) {
+    const size_t k = lit.size();
+    if (k > n) continue;
+    const char* l = lit.data();
+    if (simple_begin && simple_end ? k == n && std::memcmp(s, l, k) == 0
+        : simple_begin             ? std::memcmp(s, l, k) == 0
+        : simple_end               ? std::memcmp(s + n - k, l, k) == 0
+                                   : memmem(s, n, l, k) != nullptr)
+      return true;
+  }
+  return false;
 }
 
 bool Matcher::Match(const uint8_t* s, size_t n) const {

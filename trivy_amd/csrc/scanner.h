@@ -28,17 +28,20 @@ namespace tsg {
 struct Matcher {
   std::unique_ptr<Regex> re;
   std::vector<std::string> lits;  // lowercased; empty = no prefilter
-  // A source that is one literal with optional ^ / $ (`\/vendor\/`, `\.md$`):
-  // matched by a byte compare, with the regex's exact result (see SimpleLiteral).
+  // A source that is a literal, or a few (one group of literal alternatives),
+  // with optional ^ / $ (`\/vendor\/`, `\.md$`, `^usr\/(?:share|include|lib)\/`):
+  // matched by byte compares, with the regex's exact result (see SimpleLiteral).
   bool simple = false, simple_begin = false, simple_end = false;
-  std::string simple_lit;
+  std::vector<std::string> simple_lits;
   bool Match(const uint8_t* s, size_t n) const;
   bool MatchSimple(const uint8_t* s, size_t n) const;
 };
 
-// `src` is [^]literal[$] with plain bytes and backslash-escaped punctuation only
-// (no flags, classes, repeats, groups or alternation): *lit gets the bytes.
-bool SimpleLiteral(const std::string& src, std::string* lit, bool* begin, bool* end);
+// `src` is [^]prefix[(?:alt|alt...)]suffix[$] with plain bytes and
+// backslash-escaped punctuation only (no flags, classes, repeats, other groups
+// or alternation): *lits gets prefix + alt + suffix per alternative, and a
+// MatchString of the regex is true iff one of them occurs (anchored as given).
+bool SimpleLiteral(const std::string& src, std::vector<std::string>* lits, bool* begin, bool* end);
 
 struct AllowRuleSpec {
   std::string id;
