@@ -3,7 +3,8 @@
 
 Generates a C4-style layer (--gb of file data), walks it into 256-MiB batches
 with a host-only scanner from the oracle library (no GPU needed) and prints
-seconds per full walk.  TSG_WALK_DEBUG=1 adds the per-phase split.
+seconds per full walk.  By default the arena gets the bytes as read (the bench's
+C4 GPU pre-transform mode); --host-transform packs them transformed.  TSG_WALK_DEBUG=1 adds the per-phase split.
 """
 import argparse
 import os
@@ -20,13 +21,15 @@ def main():
     ap.add_argument("--gb", type=float, default=1.0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--arena-mb", type=int, default=256)
+    ap.add_argument("--host-transform", action="store_true",
+                    help="CR strip / printable extraction while packing (default: bytes as read, as C4's GPU mode)")
     a = ap.parse_args()
     layer = corpus.generate_layer(int(a.gb * 1e9))
     from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer, SecretScannerOption
     from trivy_amd.analyzer.secret import Collector, _CTarStats
     an = SecretAnalyzer(lib=hostlib.lib(), host_only=True)
     an.Init(AnalyzerOptions(SecretScannerOption("")))
-    col = Collector(an, a.arena_mb << 20)
+    col = Collector(an, a.arena_mb << 20, not a.host_transform)
     sp = None
     if os.environ.get("SPROF"):  # tools/sprof: sample the walks' CPU time
         import ctypes

@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <immintrin.h>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -25,11 +27,57 @@ void SetError(const std::string& e);
 // utils.IsBinary (utils.go:85-103): the head is min(size, 300) bytes.
 bool IsBinaryHead(const uint8_t* p, uint64_t size) {
   const uint64_t n = size < 300 ? size : 300;
-  for (uint64_t i = 0; i < n; i++) {
+  uint64_t i = 0;
+  // 32 bytes at a time: a byte below 0x20 is looked up by its low nibble in
+  // the table of its half (0x00-0x0F / 0x10-0x1F); 0x7F compared directly
+  const __m256i lo_tab = _mm256_setr_epi8(1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 1, 0, 0, 1, 1,  //
+                                          1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 1, 0, 0, 1, 1);
+  const __m256i hi_tab = _mm256_setr_epi8(1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1,  //
+                                          1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1);
+  for (; i + 32 <= n; i += 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + i));
+    const __m256i nib = _mm256_and_si256(v, _mm256_set1_epi8(0x0F));
+    const __m256i lt16 = _mm256_cmpeq_epi8(_mm256_min_epu8(v, _mm256_set1_epi8(0x0F)), v);
+    const __m256i lt32 = _mm256_cmpeq_epi8(_mm256_min_epu8(v, _mm256_set1_epi8(0x1F)), v);
+    const __m256i t = _mm256_blendv_epi8(_mm256_shuffle_epi8(hi_tab, nib), _mm256_shuffle_epi8(lo_tab, nib), lt16);
+    const __m256i bad = _mm256_or_si256(_mm256_and_si256(lt32, _mm256_cmpgt_epi8(t, _mm256_setzero_si256())),
+                                        _mm256_cmpeq_epi8(v, _mm256_set1_epi8(0x7F)));
+    if (_mm256_movemask_epi8(bad)) return true;
+  }
+  for (; i < n; i++) {
     const uint8_t b = p[i];
     if (b < 7 || b == 11 || (13 < b && b < 27) || (27 < b && b < 0x20) || b == 0x7f) return true;
   }
   return false;
+}
+
+// memcpy into a batch arena with non-temporal stores for the 32-B aligned
+// middle: the arena is only read again by the DMA engine, so its lines need
+// not be fetched for ownership (a plain copy of small files reads them) nor
+// kept in the caches.  The caller fences (_mm_sfence) before the arena is
+// handed on.
+void CopyToArena(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  if (n < 256) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const uint64_t head = (32 - (reinterpret_cast<uintptr_t>(dst) & 31)) & 31;
+  std::memcpy(dst, src, head);
+  uint64_t i = head;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+    const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+  }
+  for (; i + 32 <= n; i += 32)
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i),
+                        _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i)));
+  std::memcpy(dst + i, src + i, n - i);
 }
 
 // unicode.IsPrint(rune(b)) for a byte (Latin-1 code points): graphic
@@ -236,7 +284,9 @@ int64_t Add(tsg_collector* c, const char* path, uint64_t plen, bool image, const
 
 // ---- archive/tar header reading (Go 1.22 archive/tar/reader.go semantics) ----
 bool AllZero(const uint8_t* b) {
-  uint64_t acc = 0;
+  uint64_t acc;
+  std::memcpy(&acc, b, 8);  // a header starts with its name: almost always decided here
+  if (acc) return false;
   for (int i = 0; i < 64; i++) {
     uint64_t w;
     std::memcpy(&w, b + 8 * i, 8);
@@ -282,8 +332,12 @@ bool ChecksumOK(const uint8_t* b) {
   if (!ParseNumeric(b + 148, 8, &want)) return false;
   // the unsigned byte sum with the checksum field read as spaces, else the
   // signed one (old writers); plain loops, vectorised by the compiler
-  int32_t u = 0;
-  for (int i = 0; i < 512; i++) u += b[i];
+  __m256i acc = _mm256_setzero_si256();  // unsigned sum: psadbw against zero, 32 B a step
+  for (int i = 0; i < 512; i += 32)
+    acc = _mm256_add_epi64(acc, _mm256_sad_epu8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(b + i)),
+                                                 _mm256_setzero_si256()));
+  int32_t u = int32_t(_mm256_extract_epi64(acc, 0) + _mm256_extract_epi64(acc, 1) + _mm256_extract_epi64(acc, 2) +
+                      _mm256_extract_epi64(acc, 3));
   for (int i = 148; i < 156; i++) u += ' ' - b[i];
   if (want == u) return true;
   int32_t s = 0;
@@ -383,13 +437,13 @@ struct TarEntry {
   // in the archive itself when that is already the answer (a ustar name with
   // no prefix, clean), else an owned string (PAX / GNU long names, prefixes,
   // names that Clean changes) -- no allocation per entry on the common path.
-  std::string fp_own;
+  std::unique_ptr<std::string> fp_own;  // set: the path is *fp_own
   uint64_t fp_off = 0;
   uint32_t fp_len = 0;
-  uint8_t fp_owned = 0;
   std::string_view path(const uint8_t* tar) const {
-    return fp_owned ? std::string_view(fp_own) : std::string_view(reinterpret_cast<const char*>(tar + fp_off), fp_len);
+    return fp_own ? std::string_view(*fp_own) : std::string_view(reinterpret_cast<const char*>(tar + fp_off), fp_len);
   }
+  void own(std::string v) { fp_own.reset(new std::string(std::move(v))); }
   // filled by the parallel pass
   uint8_t state;         // 0 not required, 1 binary skipped, 2 add
   uint8_t bin;
@@ -464,8 +518,7 @@ int ChainEntry(const uint8_t* tar, uint64_t n, uint64_t p, TarEntry* e) {
   e->next = e->data + ((dsz + 511) & ~uint64_t(511));
   e->what = type == '0' ? 3 : 0;
   if (has_pax_path) {
-    e->fp_own = std::move(pax_path);
-    e->fp_owned = 1;
+    e->own(std::move(pax_path));
     e->has_pax_path = 1;
   }
   return 0;
@@ -517,14 +570,17 @@ void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
 // after `max_regular` bytes of regular files (at least one entry), at the end
 // of the archive (*at_end) or on a malformed header (-1).
 int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
-                 uint64_t max_regular, int threads, std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
+                 uint64_t max_regular, int threads, std::vector<std::vector<TarEntry>>& spec,
+                 std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
   out->clear();
   *at_end = false;
   const uint64_t end = std::min<uint64_t>(n, p + window);
   const size_t n_seg = size_t(std::max(1, threads) * 4);
   const uint64_t seg = std::max<uint64_t>(((end - p) / n_seg + 511) & ~uint64_t(511), 1 << 16);
   const size_t segs = size_t(std::max<uint64_t>(1, (end - p + seg - 1) / seg));
-  std::vector<std::vector<TarEntry>> spec(segs);
+  // per-segment vectors kept across windows (their pages stay mapped)
+  if (spec.size() < segs) spec.resize(segs);
+  for (auto& v : spec) v.clear();
   static const bool dbg = std::getenv("TSG_WALK_DEBUG") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = dbg ? now() : 0;
@@ -539,6 +595,15 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
       TarEntry e;
       if (ChainEntry(tar, n, q, &e) != 0) break;  // end marker or garbage: the merge decides
       q = e.next;
+      // the next header (all 8 lines: its checksum reads them) and this
+      // entry's content head (IsBinaryHead) are on their way while this
+      // entry is evaluated: the chain is a walk through cold memory
+      if (q + 512 <= n)
+        for (int l = 0; l < 512; l += 64) __builtin_prefetch(tar + q + l);
+      if (e.size) {
+        __builtin_prefetch(tar + e.data);
+        __builtin_prefetch(tar + e.data + 64);
+      }
       Evaluate(c, tar, &e);
       spec[s].push_back(std::move(e));
     }
@@ -648,6 +713,7 @@ struct TarWalkCache {
   uint64_t n = 0;
   bool gpu_xform = false;
   std::vector<TarEntry> ents;
+  std::vector<std::vector<TarEntry>> spec;  // IndexEntries' per-segment scratch
   size_t pos = 0;        // the next entry to accept
   uint64_t next = 0;     // the position after the last indexed entry
   bool at_end = false;   // the archive ends at `next`
@@ -662,8 +728,7 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
   e->bad = ChecksumOK(h) ? 0 : 1;
   if (e->has_pax_path) return;
   if (e->long_len != ~uint64_t(0)) {
-    e->fp_own = CStr(tar + e->long_off, size_t(e->long_len));
-    e->fp_owned = 1;
+    e->own(CStr(tar + e->long_off, size_t(e->long_len)));
   } else {
     auto clen = [](const uint8_t* b, size_t n) {
       size_t k = 0;
@@ -674,15 +739,16 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
     size_t pl = 0;
     if (std::memcmp(h + 257, "ustar\0", 6) == 0 && std::memcmp(h + 263, "00", 2) == 0) pl = clen(h + 345, 155);
     if (pl) {
-      e->fp_own.reserve(pl + 1 + nl);
-      e->fp_own.append(reinterpret_cast<const char*>(h + 345), pl);
-      e->fp_own.push_back('/');
-      e->fp_own.append(reinterpret_cast<const char*>(h), nl);
-      e->fp_owned = 1;
+      std::string v;
+      v.reserve(pl + 1 + nl);
+      v.append(reinterpret_cast<const char*>(h + 345), pl);
+      v.push_back('/');
+      v.append(reinterpret_cast<const char*>(h), nl);
+      e->own(std::move(v));
     } else {
+      e->fp_own.reset();
       e->fp_off = e->hdr;
       e->fp_len = uint32_t(nl);
-      e->fp_owned = 0;
     }
   }
 }
@@ -694,15 +760,14 @@ void Classify(const uint8_t* tar, TarEntry* e) {
   std::string_view fp = e->path(tar);
   if (tar[e->hdr + 156] == '\0' && !fp.empty() && fp.back() == '/') e->what = 0;  // TypeRegA dir
   if (!tsg::GoPathIsClean(fp.data(), fp.size())) {
-    e->fp_own = tsg::GoPathClean(std::string(fp));
-    e->fp_owned = 1;
-    fp = e->fp_own;
+    e->own(tsg::GoPathClean(std::string(fp)));
+    fp = *e->fp_own;
   }
   size_t t = 0;
   while (t < fp.size() && fp[t] == '/') t++;
   if (t) {
-    if (e->fp_owned) {
-      e->fp_own.erase(0, t);
+    if (e->fp_own) {
+      e->fp_own->erase(0, t);
     } else {
       e->fp_off += t;
       e->fp_len -= uint32_t(t);
@@ -848,7 +913,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       W.gpu_xform = c->gpu_xform;
       W.pos = 0;
       W.at_end = false;
-      if (IndexEntries(c, tar, n, p, ahead * room + (1 << 20), (ahead * room * 3) / 4, c->threads, &W.ents, &W.next,
+      if (IndexEntries(c, tar, n, p, ahead * room + (1 << 20), (ahead * room * 3) / 4, c->threads, W.spec, &W.ents, &W.next,
                        &W.at_end) < 0) {
         W.tar = nullptr;
         return -1;
@@ -909,10 +974,11 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         const TarEntry& e = W.ents[i];
         if (e.state != 2) continue;
         uint8_t* dst = c->arena + e.out_off;
-        if (c->gpu_xform) std::memcpy(dst, tar + e.data, e.size);
+        if (c->gpu_xform) tsg::CopyToArena(dst, tar + e.data, e.size);
         else if (e.bin) tsg::ExtractPrintable(tar + e.data, e.size, dst);
         else tsg::StripCR(tar + e.data, e.size, dst);
       }
+      _mm_sfence();
     });
     std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
     if (dbg) {
