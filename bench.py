@@ -419,6 +419,8 @@ def main():
     ap.add_argument("--ingest-steps", type=int, default=3,
                     help="c2 resident runs: steps of the extra ingest-inclusive leg (0: skip)")
     ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
+    ap.add_argument("--collectors", type=int, default=3,
+                    help="c4/c1fs: collectors filled in turn (collectors - 1 scans in flight during a walk)")
     ap.add_argument("--transform", choices=["gpu", "host"], default="gpu",
                     help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
                          "the walk's host threads")
@@ -545,7 +547,7 @@ def main():
         an.Init(AnalyzerOptions())
         t_compile = time.time() - t_c
         gx = args.transform == "gpu"
-        colls = [Collector(an, args.arena_mb << 20, gx), Collector(an, args.arena_mb << 20, gx)]
+        colls = [Collector(an, args.arena_mb << 20, gx) for _ in range(args.collectors)]
 
         def run_steps(n, stats):
             for _ in range(n):
@@ -688,7 +690,7 @@ def main():
         config_extra = {"walk_s_per_step": round(last["walk_s"], 3), "wait_s_per_step": round(last["wait_s"], 3),
                         "file_bytes_analyzed_per_gpu": n_bytes,
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
-                        "arena_mb": args.arena_mb, "pipeline": "2 collectors (walk k+1 || scan k)",
+                        "arena_mb": args.arena_mb, "pipeline": "%d collectors (walk k+1 || scans k-%d..k)" % (args.collectors, args.collectors - 2),
                         "pre_transform": args.transform}
         if fs_wl:
             config_extra["tree"] = "tmpfs (%s)" % os.path.dirname(layer)

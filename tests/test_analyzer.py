@@ -292,14 +292,17 @@ def test_native_walk_bulk_accept_vs_oracle(host_analyzer, layer_30mb, arena_mb, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_colls", [2, 3])
 @pytest.mark.parametrize("gpu_transform", [False, True])
-def test_gpu_analyze_generated_layer_vs_oracle(gpu_transform):
+def test_gpu_analyze_generated_layer_vs_oracle(gpu_transform, n_colls):
     from trivy_amd import corpus
     from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
+    from trivy_amd.analyzer.secret import Collector
     layer = corpus.generate_layer(1_500_000, seed=corpus.SEED + 4, secrets_per_byte=1.0 / 8192)
     a = SecretAnalyzer()
     a.Init(AnalyzerOptions())
-    got = a.AnalyzeLayer(layer, arena_bytes=256 << 10, gpu_transform=gpu_transform)
+    colls = [Collector(a, 256 << 10, gpu_transform) for _ in range(n_colls)]  # n - 1 scans in flight
+    got = a.AnalyzeLayer(layer, colls=colls)
     got.Sort()
     want = oan.analyze_layer(oan.SecretAnalyzer(""), layer.tobytes())
     want.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))

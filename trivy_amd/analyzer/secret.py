@@ -20,6 +20,7 @@ Every transform runs in libtsg.so (include/tsg_analyzer.h); there is no CPU
 fallback for the scan itself.
 """
 import ctypes
+import collections
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -251,6 +252,37 @@ class _ScannerRef:  # what ScanResult needs of its scanner
         self._L = L
 
 
+def _pipeline(colls, fill, take):
+    """Fill the collectors in turn (fill(coll) -> True at the end of the input) and submit
+    each batch; with n collectors, n - 1 scans stay in flight while the next batch is
+    filled (a collector is refilled only after its scan was taken).  Returns the seconds
+    spent filling and waiting."""
+    inflight = collections.deque()
+    k, done = 0, False
+    t_walk = t_wait = 0.0
+    try:
+        while not done:
+            coll = colls[k]
+            t0 = time.perf_counter()
+            done = fill(coll)
+            t_walk += time.perf_counter() - t0
+            if coll.files():
+                inflight.append(coll.submit())
+            t0 = time.perf_counter()
+            while len(inflight) > len(colls) - 1:
+                take(inflight.popleft())
+            t_wait += time.perf_counter() - t0
+            k = (k + 1) % len(colls)
+        t0 = time.perf_counter()
+        while inflight:
+            take(inflight.popleft())
+        t_wait += time.perf_counter() - t0
+    finally:
+        while inflight:  # an error left batches in flight: join them before the arenas go
+            inflight.popleft().__del__()
+    return t_walk, t_wait
+
+
 class SecretAnalyzer:
     """analyzer/secret.SecretAnalyzer bound to the MI355X engine."""
 
@@ -342,7 +374,7 @@ class SecretAnalyzer:
                   gpu_transform: bool = False) -> AnalysisResult:
         """`trivy fs` for this analyzer: FS.Walk (walker/fs.go:25-78) + AnalyzeFile's Required +
         Analyze for every regular file under root, read natively into double-buffered pinned
-        arenas (tsg_collector_add_fs); one collector fills while the other's batch scans.
+        arenas (tsg_collector_add_fs); one collector fills while the others' batches scan.
         FilePath is the path relative to root (Dir = root, no '/' prefix: secret.go:130-135)."""
         from ..walker import FS, Option, _CFsAddStats
         w = FS().Walk(root, opt or Option(), lib=self._L)
@@ -358,31 +390,12 @@ class SecretAnalyzer:
                 for k2, v in out.items():
                     scan_tot[k2] = scan_tot.get(k2, 0) + v
         colls = colls or [Collector(self, arena_bytes, gpu_transform), Collector(self, arena_bytes, gpu_transform)]
-        pending, k, done = None, 0, False
-        t_walk = t_wait = 0.0
-        try:
-            while not done:
-                coll = colls[k]
-                t0 = time.perf_counter()
-                rc = self._L.tsg_collector_add_fs(coll._h, w._h, c.byref(st))
-                t_walk += time.perf_counter() - t0
-                if rc < 0:
-                    raise RuntimeError("fs walk: %s" % _lib.last_error(self._L))
-                done = rc == 0
-                nxt = coll.submit() if coll.files() else None
-                t0 = time.perf_counter()
-                if pending is not None:
-                    p, pending = pending, None
-                    take(p)
-                t_wait += time.perf_counter() - t0
-                pending = nxt
-                k ^= 1
-            if pending is not None:
-                p, pending = pending, None
-                take(p)
-        finally:
-            if pending is not None:
-                pending.__del__()
+        def fill(coll):
+            rc = self._L.tsg_collector_add_fs(coll._h, w._h, c.byref(st))
+            if rc < 0:
+                raise RuntimeError("fs walk: %s" % _lib.last_error(self._L))
+            return rc == 0
+        t_walk, t_wait = _pipeline(colls, fill, take)
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update(w.stats())
@@ -395,8 +408,8 @@ class SecretAnalyzer:
                      materialize: bool = True, colls: Optional[List[Collector]] = None,
                      gpu_transform: bool = False) -> AnalysisResult:
         """Every regular file of an uncompressed tar layer (bytes or a uint8 numpy array),
-        as the image artifact's AnalyzeFile(dir="") would run it.  Two collectors alternate:
-        one is being filled while the other's batch is on the GPU.  materialize=False
+        as the image artifact's AnalyzeFile(dir="") would run it.  The collectors (two by
+        default) are filled in turn while the others' batches are on the GPU.  materialize=False
         (bench): findings stay in the engine; stats gets the summed scan counters."""
         result = AnalysisResult()
         scan_tot: dict = {}
@@ -410,34 +423,15 @@ class SecretAnalyzer:
                     scan_tot[k2] = scan_tot.get(k2, 0) + v
         st = _CTarStats()
         colls = colls or [Collector(self, arena_bytes, gpu_transform), Collector(self, arena_bytes, gpu_transform)]
-        pending = None
-        cursor, k, done = 0, 0, False
-        t_walk = t_wait = 0.0
-        try:
-            while not done:
-                coll = colls[k]
-                t0 = time.perf_counter()
-                rc, cursor = coll.add_tar(layer, cursor, st)
-                t_walk += time.perf_counter() - t0
-                done = rc == 0
-                if rc == 1 and coll.files() == 0:
-                    raise RuntimeError("tar layer: an entry does not fit an empty collector")
-                nxt = coll.submit() if coll.files() else None
-                t0 = time.perf_counter()
-                if pending is not None:
-                    p, pending = pending, None
-                    take(p)
-                t_wait += time.perf_counter() - t0
-                pending = nxt
-                k ^= 1
-            t0 = time.perf_counter()
-            if pending is not None:
-                p, pending = pending, None
-                take(p)
-            t_wait += time.perf_counter() - t0
-        finally:
-            if pending is not None:  # an error left a batch in flight: join it before the arenas go
-                pending.__del__()
+        cursor = 0
+
+        def fill(coll):
+            nonlocal cursor
+            rc, cursor = coll.add_tar(layer, cursor, st)
+            if rc == 1 and coll.files() == 0:
+                raise RuntimeError("tar layer: an entry does not fit an empty collector")
+            return rc == 0
+        t_walk, t_wait = _pipeline(colls, fill, take)
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})

@@ -223,9 +223,12 @@ bool Required(const tsg_analyzer* a, const char* path, uint64_t len, int64_t siz
   const std::string_view name = slash == std::string_view::npos ? fp : fp.substr(slash + 1);
   // strings.Split(dir, "/") holds a skip dir: dir (which ends in '/') starts
   // with "<skip>/" or contains "/<skip>/"
-  for (const std::string_view d : {std::string_view("/.git/"), std::string_view("/node_modules/")}) {
-    if (dir.substr(0, d.size() - 1) == d.substr(1)) return false;
-    if (dir.size() >= d.size() && memmem(dir.data(), dir.size(), d.data(), d.size())) return false;
+  constexpr std::string_view kGit = "/.git/", kNode = "/node_modules/";
+  if (dir.substr(0, kGit.size() - 1) == kGit.substr(1) || dir.substr(0, kNode.size() - 1) == kNode.substr(1))
+    return false;
+  for (size_t q = dir.find('/'); q != std::string_view::npos; q = dir.find('/', q + 1)) {
+    const std::string_view rest = dir.substr(q);
+    if (rest.substr(0, kGit.size()) == kGit || rest.substr(0, kNode.size()) == kNode) return false;
   }
   static constexpr std::string_view kFiles[] = {"go.mod", "go.sum", "package-lock.json", "yarn.lock",
                                                 "pnpm-lock.yaml", "Pipfile.lock", "Gemfile.lock"};
@@ -531,7 +534,7 @@ void Classify(const uint8_t* tar, TarEntry* e);
 // AnalyzeFile's Required, Analyze's binary gate and the transformed length.
 std::atomic<int64_t> g_eval_ns[3];
 void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
-  static const bool dbg = std::getenv("TSG_WALK_DEBUG") != nullptr;
+  static const bool dbg = std::getenv("TSG_WALK_DEBUG") && std::atoi(std::getenv("TSG_WALK_DEBUG")) >= 2;  // per-entry timers: level 2
   auto t0 = dbg ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   Classify(tar, e);
   e->state = 0;
@@ -731,9 +734,8 @@ void Resolve(const uint8_t* tar, TarEntry* e) {
     e->own(CStr(tar + e->long_off, size_t(e->long_len)));
   } else {
     auto clen = [](const uint8_t* b, size_t n) {
-      size_t k = 0;
-      while (k < n && b[k]) k++;
-      return k;
+      const void* z = std::memchr(b, 0, n);
+      return z ? size_t(static_cast<const uint8_t*>(z) - b) : n;
     };
     const size_t nl = clen(h, 100);
     size_t pl = 0;
