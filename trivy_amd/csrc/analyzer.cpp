@@ -574,8 +574,12 @@ void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
 // of the archive (*at_end) or on a malformed header (-1).
 int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
                  uint64_t max_regular, int threads, std::vector<std::vector<TarEntry>>& spec,
-                 std::vector<TarEntry>* out, uint64_t* next, bool* at_end) {
+                 std::vector<std::vector<TarEntry>>& fallback, std::vector<TarEntry*>* out, uint64_t* next,
+                 bool* at_end) {
+  // *out points into spec / fallback, which hold the entries until the next call
   out->clear();
+  fallback.clear();
+  fallback.reserve(size_t(std::max(1, threads) * 4) + 8);
   *at_end = false;
   const uint64_t end = std::min<uint64_t>(n, p + window);
   const size_t n_seg = size_t(std::max(1, threads) * 4);
@@ -612,8 +616,8 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
     }
   });
   // The merge plans ranges of the speculative vectors (and of the rare
-  // sequential fallbacks) first, reading only positions and sizes; the
-  // entries are then moved into *out in parallel.
+  // sequential fallbacks) first, reading only positions and sizes; *out then
+  // gets pointers to the entries, filled in parallel.
   struct Range {
     std::vector<TarEntry>* v;
     size_t lo, hi;
@@ -621,8 +625,6 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
   const double t1 = dbg ? now() : 0;
   size_t n_fallback = 0;
   std::vector<Range> plan;
-  std::vector<std::vector<TarEntry>> fallback;
-  fallback.reserve(segs);
   uint64_t cur = p, regular = 0;
   bool ended = false;
   for (size_t s = 0; s < segs && !ended; s++) {
@@ -668,7 +670,7 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
     for (size_t k = 0; k < plan.size(); k++) at[k + 1] = at[k] + (plan[k].hi - plan[k].lo);
     out->resize(at.back());
     tsg::ParallelFor(plan.size(), threads, [&](size_t k) {
-      for (size_t i = plan[k].lo; i < plan[k].hi; i++) (*out)[at[k] + (i - plan[k].lo)] = std::move((*plan[k].v)[i]);
+      for (size_t i = plan[k].lo; i < plan[k].hi; i++) (*out)[at[k] + (i - plan[k].lo)] = &(*plan[k].v)[i];
     });
   }
   if (dbg) {
@@ -682,7 +684,9 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
     return 0;
   }
   if (out->empty() || (cur >= n && !*at_end)) {  // nothing in the window (a huge entry) or the tail
-    while (out->empty() || (cur < n && regular <= max_regular && out->size() < 1)) {
+    fallback.emplace_back();
+    auto& fb = fallback.back();
+    while (out->empty() && fb.empty()) {
       TarEntry e;
       const int r = ChainEntry(tar, n, cur, &e);
       if (r < 0) return -1;
@@ -692,8 +696,9 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
       }
       cur = e.next;
       Evaluate(c, tar, &e);
-      out->push_back(std::move(e));
+      fb.push_back(std::move(e));
     }
+    for (auto& e : fb) out->push_back(&e);
   }
   if (!*at_end && cur >= n) *at_end = true;  // io.EOF without the zero blocks
   if (!*at_end && regular <= max_regular && cur < n && end >= n) {
@@ -715,8 +720,9 @@ struct TarWalkCache {
   const uint8_t* tar = nullptr;
   uint64_t n = 0;
   bool gpu_xform = false;
-  std::vector<TarEntry> ents;
-  std::vector<std::vector<TarEntry>> spec;  // IndexEntries' per-segment scratch
+  std::vector<TarEntry*> ents;              // the window's entries in archive order
+  std::vector<std::vector<TarEntry>> spec;  // their storage: IndexEntries' per-segment vectors
+  std::vector<std::vector<TarEntry>> fallback;  // and its sequential fallbacks
   size_t pos = 0;        // the next entry to accept
   uint64_t next = 0;     // the position after the last indexed entry
   bool at_end = false;   // the archive ends at `next`
@@ -790,7 +796,7 @@ namespace {
 // loop would (same offsets, paths, kinds, flags, stats).  Returns the number
 // of entries taken.
 constexpr size_t kAcceptBlock = 4096;
-size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry>& ents, size_t k0, tsg_tar_stats* st) {
+size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry*>& ents, size_t k0, tsg_tar_stats* st) {
   const size_t nb = (ents.size() - k0) / kAcceptBlock;
   if (nb == 0) return 0;
   struct Sum {
@@ -802,7 +808,7 @@ size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry>&
   tsg::ParallelFor(nb, c->threads, [&](size_t b) {
     Sum& q = sum[b];
     for (size_t i = k0 + b * kAcceptBlock; i < k0 + (b + 1) * kAcceptBlock; i++) {
-      const TarEntry& e = ents[i];
+      const TarEntry& e = *ents[i];
       q.bad = q.bad || e.bad;
       if (e.state == 2) {
         q.files++;
@@ -847,7 +853,7 @@ size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry>&
     size_t f = f0 + at[b].files, pp = p0 + at[b].pbytes;
     uint64_t u = u0 + at[b].used;
     for (size_t i = k0 + b * kAcceptBlock; i < k0 + (b + 1) * kAcceptBlock; i++) {
-      TarEntry& e = ents[i];
+      TarEntry& e = *ents[i];
       if (e.state != 2) continue;
       e.out_off = u;
       u += c->gpu_xform ? e.size : e.out_len;
@@ -906,7 +912,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     // 1. the cached entries from p on, else index a window starting at p
     double t0 = dbg ? now() : 0;
     const bool hit = W.tar == tar && W.n == n && W.gpu_xform == c->gpu_xform &&
-                     ((W.pos < W.ents.size() && W.ents[W.pos].start == p) || (W.pos == W.ents.size() && W.next == p &&
+                     ((W.pos < W.ents.size() && W.ents[W.pos]->start == p) || (W.pos == W.ents.size() && W.next == p &&
                                                                                W.at_end));
     if (!hit) {
       const uint64_t room = std::max<uint64_t>(c->limit, 1 << 20);
@@ -915,7 +921,8 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       W.gpu_xform = c->gpu_xform;
       W.pos = 0;
       W.at_end = false;
-      if (IndexEntries(c, tar, n, p, ahead * room + (1 << 20), (ahead * room * 3) / 4, c->threads, W.spec, &W.ents, &W.next,
+      // every entry indexed in the window is kept (no re-indexing past a cut)
+      if (IndexEntries(c, tar, n, p, ahead * room + (1 << 20), ~uint64_t(0) >> 1, c->threads, W.spec, W.fallback, &W.ents, &W.next,
                        &W.at_end) < 0) {
         W.tar = nullptr;
         return -1;
@@ -931,7 +938,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     size_t k = k0 + AcceptBlocks(c, tar, W.ents, k0, st);
     bool full = false;
     for (; k < W.ents.size(); k++) {
-      TarEntry& e = W.ents[k];
+      TarEntry& e = *W.ents[k];
       if (e.bad) {
         tsg::SetError("tar: invalid header checksum at offset " + std::to_string(e.hdr));
         W.tar = nullptr;
@@ -973,7 +980,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     // 3. copy / transform the accepted contents
     tsg::ParallelFor((k - k0 + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
       for (size_t i = k0 + b * kBlock; i < std::min(k, k0 + (b + 1) * kBlock); i++) {
-        const TarEntry& e = W.ents[i];
+        const TarEntry& e = *W.ents[i];
         if (e.state != 2) continue;
         uint8_t* dst = c->arena + e.out_off;
         if (c->gpu_xform) tsg::CopyToArena(dst, tar + e.data, e.size);
@@ -994,7 +1001,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
                    g_eval_ns[0] / 1e9, g_eval_ns[1] / 1e9);
     }
     if (full) {
-      *cursor = W.ents[k].start;
+      *cursor = W.ents[k]->start;
       return 1;
     }
     p = W.next;
