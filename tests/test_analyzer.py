@@ -370,6 +370,74 @@ def test_gpu_transform_edges_vs_oracle():
     assert n > 40
 
 
+def _xform_check(files, kinds):
+    import ctypes as c
+    import numpy as np
+    from trivy_amd import _lib
+    L = _lib.lib()
+    L.tsg_debug_xform.argtypes = [c.c_int, c.c_void_p, c.c_uint64, c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p,
+                                  c.c_uint64, c.c_void_p]
+    offs = np.zeros(len(files) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in files])
+    raw = np.frombuffer(b"".join(files) + b"\0" * 64, dtype=np.uint8)
+    kd = np.array(kinds, dtype=np.uint8)
+    out = np.zeros(int(offs[-1]) * 2 + 64, dtype=np.uint8)
+    xoff = np.zeros(len(files) + 1, dtype=np.uint64)
+    rc = L.tsg_debug_xform(0, raw.ctypes.data, int(offs[-1]), offs.ctypes.data, len(files), kd.ctypes.data,
+                           out.ctypes.data, len(out), xoff.ctypes.data)
+    assert rc == 0, _lib.last_error(L)
+    want_all = [b if k == 0 else b.replace(b"\r", b"") if k == 1 else oan.extract_printable_bytes(b)
+                for b, k in zip(files, kinds)]
+    for i, want in enumerate(want_all):
+        got = out[int(xoff[i]):int(xoff[i + 1])].tobytes()
+        assert got == want, (i, kinds[i], files[i][:80])
+    assert int(xoff[-1]) == sum(map(len, want_all))
+    assert out[int(xoff[-1]):].tobytes() == b"\0" * (len(out) - int(xoff[-1]))  # nothing written past the end
+
+
+@pytest.mark.gpu
+def test_gpu_xform_identity_tiles_vs_oracle():
+    """Mostly text that the transform leaves as is (whole KiB tiles copied by the
+    write kernel's identity path at every output phase 0..15), with CRLF files,
+    all-printable and mixed .pyc-like files shifting the phase between them."""
+    import random
+    rng = random.Random(11)
+    files, kinds = [], []
+    for i in range(3000):
+        r = rng.random()
+        n = rng.choice([0, 7, 100, 700, 1024, 1500, 2600, 5000, 12000])
+        text = bytes(rng.choice(b"abcdefghij =:/\n") for _ in range(n))
+        if r < 0.6:
+            files.append(text)
+            kinds.append(rng.choice([0, 1]))
+        elif r < 0.8:  # a few CRs: shifts every later tile's output phase
+            b = bytearray(text)
+            for _ in range(rng.randint(1, 15)):
+                b.insert(rng.randint(0, len(b)), 13)
+            files.append(bytes(b))
+            kinds.append(1)
+        elif r < 0.9:  # printable only: identity inside, a '\n' after a final run of >= 5
+            files.append(bytes(rng.choice(b"abcdef") for _ in range(n)))
+            kinds.append(2)
+        else:
+            files.append(bytes(rng.choice(b"ab\x00\x01 z") for _ in range(n)))
+            kinds.append(2)
+    _xform_check(files, kinds)
+
+
+@pytest.mark.gpu
+def test_gpu_xform_empty_files_at_tile_starts():
+    """Empty files exactly at a 1-KiB tile's first byte (before the file the chunk map
+    names): their transformed offsets come from the count kernel, not from whatever the
+    scratch held (a call on other data runs first so reused device memory is dirty)."""
+    _xform_check([b"\x01q" * 3000] * 8, [2] * 8)
+    files, kinds = [], []
+    for i in range(300):
+        files += [b"x" * (1024 - (i % 3)), b"", b"", b"\r\nab" * (i % 7)]
+        kinds += [1, 1, 2, 1]
+    _xform_check(files, kinds)
+
+
 @pytest.mark.gpu
 def test_gpu_xform_bytes_vs_oracle():
     """The flat GPU pre-transform (xform.hip) byte for byte against the oracle's

@@ -186,6 +186,8 @@ __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const uint64_t* __r
   const uint32_t bend = blk + 16 < n_bytes ? blk + 16 : n_bytes;
   uint32_t f = chunk_file[blk / kXTile];
   uint32_t fs = uint32_t(off[f]), fe = uint32_t(off[f + 1]);
+  if (fs == blk)  // empty files at a tile's first byte come before the file the chunk map names
+    for (uint32_t g = f; g > 0 && uint32_t(off[g - 1]) == blk;) start(--g, 0u);
   while (fe <= blk && f + 1 < n_files) {  // the file holding blk (the chunk map names the tile's first)
     f++;
     fs = fe;
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
     const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
-    uint32_t segK[4], segC[4], segZ[4], nseg = 0;
+    uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0, added = 0;
     const uint32_t c = x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t, uint32_t) {},
                               [&](uint32_t K, uint32_t C, uint32_t Z) {
                                 if (nseg < 4) {
@@ -299,11 +301,48 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
                                   segZ[nseg] = Z;
                                 }
                                 nseg++;
+                                kept |= K;
+                                added |= C | Z;
                               });
-    const uint32_t ex = wave_excl(c, lane);
-    const uint32_t total = __shfl(ex + c, 63);
     const uint64_t start = tile_pre[t];
     const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
+    if (__all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
+      // An identity tile (no CR dropped, no printable-run edits, a whole KiB):
+      // its output is its input moved to `start`, so each lane writes one
+      // aligned 16-B block composed from its own and the previous lane's bytes
+      // (a byte shift by the tile's output phase), no staging.
+      uint32_t P[4] = {__shfl_up(v.x, 1), __shfl_up(v.y, 1), __shfl_up(v.z, 1), __shfl_up(v.w, 1)};
+      const uint32_t X[8] = {P[0], P[1], P[2], P[3], v.x, v.y, v.z, v.w};  // prev ++ own
+      const uint32_t sh = 16u - phase;  // output block = X[sh .. sh + 16)
+      const uint32_t q = sh >> 2, r = 8u * (sh & 3u);
+      uint32_t o[4];
+#pragma unroll
+      for (uint32_t i = 0; i < 4; i++) {
+        // X[q + i], X[q + i + 1] with q wave-uniform (0..4)
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 5; k++)
+          if (q == k) {
+            lo = X[k + i];
+            hi = k + i + 1 < 8 ? X[k + i + 1] : 0u;
+          }
+        o[i] = r ? (lo >> r) | (hi << (32u - r)) : lo;
+      }
+      const uint64_t base = start - phase;
+      const uint64_t g = base + 16u * lane;
+      if (lane > 0 || phase == 0) {
+        *reinterpret_cast<uint4*>(out + g) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {  // block 0: the previous tile owns out[base, start)
+        for (uint32_t j = phase; j < 16; j++) out[g + j] = uint8_t(o[j >> 2] >> (8 * (j & 3)));
+      }
+      if (lane == 0 && phase) {  // the last `phase` bytes spill into block 64
+        const uint8_t* src = raw + t * kXTile + kXTile - phase;
+        for (uint32_t j = 0; j < phase; j++) out[base + kXTile + j] = src[j];
+      }
+      continue;
+    }
+    const uint32_t ex = wave_excl(c, lane);
+    const uint32_t total = __shfl(ex + c, 63);
     uint32_t at = phase + ex;
     auto put = [&](uint32_t K, uint32_t C, uint32_t Z) {
       for (uint32_t m = K | C | Z; m; m &= m - 1) {
