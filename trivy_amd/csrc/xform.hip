@@ -107,6 +107,13 @@ __global__ __launch_bounds__(kXThreads) void xf_chunk_map_kernel(const uint64_t*
   }
 }
 
+// A lane's 16-B block of tile t (zeros past the end).
+__device__ __forceinline__ uint4 x_block(const uint8_t* raw, uint32_t n_bytes, uint32_t t, uint32_t lane,
+                                         uint32_t n_tiles) {
+  const uint32_t blk = t * kXTile + 16 * lane;
+  return t < n_tiles && blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
+}
+
 // The 32 bytes around a lane's block: [blk - 8, blk + 24) as 8 words (the
 // neighbours' words by wave shuffles; the wave's edge lanes load theirs).
 struct XWindow {
@@ -180,11 +187,12 @@ __device__ XMasks x_masks(const XWindow& W, uint32_t lo, uint32_t hi) {
 template <typename Start, typename Out>
 __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const uint64_t* __restrict__ off,
                                            const uint8_t* __restrict__ kind, uint32_t n_files,
-                                           const uint32_t* __restrict__ chunk_file, uint32_t blk, const XWindow& W,
+                                           uint32_t tile_file, uint32_t blk, const XWindow& W,
                                            Start start, Out out) {
+  // tile_file: chunk_file[] of the lane's tile (loaded by the caller a tile ahead)
   if (blk >= n_bytes) return 0;
   const uint32_t bend = blk + 16 < n_bytes ? blk + 16 : n_bytes;
-  uint32_t f = chunk_file[blk / kXTile];
+  uint32_t f = tile_file;
   uint32_t fs = uint32_t(off[f]), fe = uint32_t(off[f + 1]);
   if (fs == blk)  // empty files at a tile's first byte come before the file the chunk map names
     for (uint32_t g = f; g > 0 && uint32_t(off[g - 1]) == blk;) start(--g, 0u);
@@ -236,14 +244,21 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   const uint32_t waves = gridDim.x * (kXThreads / 64);
-  for (uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
+  // a wave walks tiles t, t + waves, ...: the next tile's block and chunk-map
+  // entry are loaded while this one is processed (the per-tile chain of
+  // dependent loads, not bytes, bounds these kernels)
+  uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
+  uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
+  uint32_t tf = t < n_tiles ? chunk_file[t] : 0u;
+  for (; t < n_tiles; t += waves) {
     const uint32_t blk = t * kXTile + 16 * lane;
-    const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
+    const uint4 vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
+    const uint32_t tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // file starts: tile-relative output offsets once the lane's prefix is known
     uint32_t sf[4], sc[4], ns = 0;
     const uint32_t c = x_lane(
-        n_bytes, off, kind, n_files, chunk_file, blk, W,
+        n_bytes, off, kind, n_files, tf, blk, W,
         [&](uint32_t f, uint32_t at) {
           if (ns < 4) {
             sf[ns] = f;
@@ -255,11 +270,13 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
     const uint32_t ex = wave_excl(c, lane);
     if (lane == 63) tile_cnt[t] = ex + c;
     if (ns > 4) {  // many tiny files in one block: walk it again, recording all
-      x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t f, uint32_t at) { fstart[f] = ex + at; },
+      x_lane(n_bytes, off, kind, n_files, tf, blk, W, [&](uint32_t f, uint32_t at) { fstart[f] = ex + at; },
              [&](uint32_t, uint32_t, uint32_t) {});
     } else {
       for (uint32_t i = 0; i < ns; i++) fstart[sf[i]] = ex + sc[i];
     }
+    v = vn;
+    tf = tfn;
   }
 }
 
@@ -287,13 +304,22 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
   uint8_t* S = s_out[threadIdx.x >> 6];
   const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   const uint32_t waves = gridDim.x * (kXThreads / 64);
-  for (uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); t < n_tiles; t += waves) {
+  uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
+  uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);  // the next tile's inputs, a tile ahead
+  uint32_t tfn = t < n_tiles ? chunk_file[t] : 0u;
+  uint64_t pren = t < n_tiles ? tile_pre[t] : 0u;
+  for (; t < n_tiles; t += waves) {
     const uint32_t blk = t * kXTile + 16 * lane;
-    const uint4 v = blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
+    const uint4 v = vn;
+    const uint32_t tf = tfn;
+    const uint64_t start = pren;
+    vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
+    tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
+    pren = t + waves < n_tiles ? tile_pre[t + waves] : 0u;
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
     uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0, added = 0;
-    const uint32_t c = x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t, uint32_t) {},
+    const uint32_t c = x_lane(n_bytes, off, kind, n_files, tf, blk, W, [&](uint32_t, uint32_t) {},
                               [&](uint32_t K, uint32_t C, uint32_t Z) {
                                 if (nseg < 4) {
                                   segK[nseg] = K;
@@ -304,7 +330,6 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
                                 kept |= K;
                                 added |= C | Z;
                               });
-    const uint64_t start = tile_pre[t];
     const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
     if (__all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
       // An identity tile (no CR dropped, no printable-run edits, a whole KiB):
@@ -355,7 +380,7 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
     if (nseg <= 4) {
       for (uint32_t i = 0; i < nseg; i++) put(segK[i], segC[i], segZ[i]);
     } else {
-      x_lane(n_bytes, off, kind, n_files, chunk_file, blk, W, [&](uint32_t, uint32_t) {}, put);
+      x_lane(n_bytes, off, kind, n_files, tf, blk, W, [&](uint32_t, uint32_t) {}, put);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
