@@ -401,8 +401,10 @@ def _bind_numa(device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 50 for c2: a depth-3 pipeline's fill and drain are then a few %% of the "
+                         "timed region, as in a long scan job; 10 for the other workloads)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3 for c2, 2 otherwise)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--gb", type=float, default=None, help="corpus size per GPU (GB = 1e9 B)")
     ap.add_argument("--cpu-sample-mb", type=float, default=None, help="CPU-baseline sample (first files)")
@@ -426,11 +428,16 @@ def main():
                          "the walk's host threads")
     ap.add_argument("--pool-gb", type=float, default=64.0, help="c5: page-locked host pool size")
     ap.add_argument("--traffic-file", default=None,
-                    help="PMC traffic summary (default profiles/traffic_r02_<workload>.json, c2: traffic_r02.json)")
+                    help="PMC traffic summary (default: the newest profiles/traffic_rNN_<workload>.json, c2: traffic_rNN.json)")
     args = ap.parse_args()
-    if args.traffic_file is None:
-        per_wl = os.path.join(ROOT, "profiles", "traffic_r02_%s.json" % args.workload)
-        args.traffic_file = per_wl if os.path.exists(per_wl) else os.path.join(ROOT, "profiles", "traffic_r02.json")
+    if args.steps is None:
+        args.steps = 50 if args.workload == "c2" else 10
+    if args.warmup is None:
+        args.warmup = 3 if args.workload == "c2" else 2
+    if args.traffic_file is None:  # the newest PMC pass of this workload (c2: traffic_rNN.json)
+        cands = [os.path.join(ROOT, "profiles", "traffic_r%02d%s.json" % (r, "" if args.workload == "c2" else
+                                                                            "_" + args.workload)) for r in (3, 2)]
+        args.traffic_file = next((c for c in cands if os.path.exists(c)), cands[-1])
     wl_desc, gb_default, cpu_mb_default, parity_mb_default = WORKLOADS[args.workload]
     if args.parity_mb is None:
         args.parity_mb = parity_mb_default
