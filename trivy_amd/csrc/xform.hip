@@ -178,6 +178,52 @@ __device__ XMasks x_masks(const XWindow& W, uint32_t lo, uint32_t hi) {
   return m;
 }
 
+// The file table around a tile: offsets of files tf .. tf + 64 and kinds of
+// tf .. tf + 63 staged in the wave's LDS (one coalesced load per tile, a tile
+// ahead), so a lane finds the file holding its block and the files after it
+// without a chain of dependent global loads; files further on (a tile of more
+// than 64 tiny files) are read from global memory.
+struct XFiles {
+  uint32_t tf;
+  const uint32_t* so;
+  const uint8_t* sk;
+  const uint64_t* off;
+  const uint8_t* kind;
+  __device__ __forceinline__ uint32_t O(uint32_t g) const {
+    const uint32_t d = g - tf;
+    return d < 65u ? so[d] : uint32_t(off[g]);
+  }
+  __device__ __forceinline__ uint32_t K(uint32_t g) const {
+    const uint32_t d = g - tf;
+    return d < 64u ? uint32_t(sk[d]) : uint32_t(kind[g]);
+  }
+};
+
+// Per lane: its slice of the file table of tile tf (loaded a tile ahead).
+struct XFileRegs {
+  uint32_t o, o64, k;
+};
+__device__ __forceinline__ XFileRegs x_file_regs(const uint64_t* off, const uint8_t* kind, uint32_t n_files,
+                                                 uint32_t tf, uint32_t lane) {
+  XFileRegs r;
+  const uint32_t g = tf + lane < n_files ? tf + lane : n_files;
+  r.o = uint32_t(off[g]);
+  r.o64 = uint32_t(off[tf + 64u < n_files ? tf + 64u : n_files]);
+  r.k = tf + lane < n_files ? uint32_t(kind[tf + lane]) : 0u;
+  return r;
+}
+__device__ __forceinline__ void x_stage_files(uint32_t* so, uint8_t* sk, const XFileRegs& r, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous tile's reads are done
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  so[lane] = r.o;
+  if (lane == 0) so[64] = r.o64;
+  sk[lane] = uint8_t(r.k);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // A lane's block in file order.  For each file segment [s, e) of the block:
 // start(f, count so far) at a file starting inside the block (empty files
 // too), then out(emit mask, nl-before mask, nl-after mask) over the block's
@@ -185,21 +231,19 @@ __device__ XMasks x_masks(const XWindow& W, uint32_t lo, uint32_t hi) {
 // bit of the second mask, the byte for a bit of the first, a '\n' for a bit of
 // the third.  Returns the lane's output byte count.
 template <typename Start, typename Out>
-__device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const uint64_t* __restrict__ off,
-                                           const uint8_t* __restrict__ kind, uint32_t n_files,
-                                           uint32_t tile_file, uint32_t blk, const XWindow& W,
-                                           Start start, Out out) {
-  // tile_file: chunk_file[] of the lane's tile (loaded by the caller a tile ahead)
+__device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const XFiles& T, uint32_t n_files, uint32_t blk,
+                                           const XWindow& W, Start start, Out out) {
+  // T.tf: chunk_file[] of the lane's tile, the file holding its first byte
   if (blk >= n_bytes) return 0;
   const uint32_t bend = blk + 16 < n_bytes ? blk + 16 : n_bytes;
-  uint32_t f = tile_file;
-  uint32_t fs = uint32_t(off[f]), fe = uint32_t(off[f + 1]);
+  uint32_t f = T.tf;
+  uint32_t fs = T.O(f), fe = T.O(f + 1);
   if (fs == blk)  // empty files at a tile's first byte come before the file the chunk map names
-    for (uint32_t g = f; g > 0 && uint32_t(off[g - 1]) == blk;) start(--g, 0u);
+    for (uint32_t g = f; g > 0 && uint32_t(T.off[g - 1]) == blk;) start(--g, 0u);
   while (fe <= blk && f + 1 < n_files) {  // the file holding blk (the chunk map names the tile's first)
     f++;
     fs = fe;
-    fe = uint32_t(off[f + 1]);
+    fe = T.O(f + 1);
     if (fs >= blk) start(f, 0u);  // an empty file at the block start
   }
   // the block's CR bytes (kinds 1)
@@ -211,7 +255,7 @@ __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const uint64_t* __r
     const uint32_t s = fs > blk ? fs - blk : 0u, e = (fe < bend ? fe : bend) - blk;  // the segment, block bits
     if (s < e) {
       const uint32_t seg = ((1u << e) - 1u) & ~((1u << s) - 1u);
-      const uint32_t k = kind[f];
+      const uint32_t k = T.K(f);
       if (k == 0) {
         out(seg, 0u, 0u);
         cnt += uint32_t(__popc(seg));
@@ -230,7 +274,7 @@ __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const uint64_t* __r
     if (fe >= bend || f + 1 >= n_files) break;
     f++;
     fs = fe;
-    fe = uint32_t(off[f + 1]);
+    fe = T.O(f + 1);
   }
   return cnt;
 }
@@ -247,18 +291,26 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
   // a wave walks tiles t, t + waves, ...: the next tile's block and chunk-map
   // entry are loaded while this one is processed (the per-tile chain of
   // dependent loads, not bytes, bounds these kernels)
+  __shared__ uint32_t s_fo[kXThreads / 64][65];
+  __shared__ uint8_t s_fk[kXThreads / 64][64];
+  uint32_t* so = s_fo[threadIdx.x >> 6];
+  uint8_t* sk = s_fk[threadIdx.x >> 6];
   uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
   uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
   uint32_t tf = t < n_tiles ? chunk_file[t] : 0u;
+  XFileRegs fr = x_file_regs(off, kind, n_files, tf, lane);
   for (; t < n_tiles; t += waves) {
     const uint32_t blk = t * kXTile + 16 * lane;
+    x_stage_files(so, sk, fr, lane);
+    const XFiles T{tf, so, sk, off, kind};
     const uint4 vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
     const uint32_t tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
+    const XFileRegs frn = t + waves < n_tiles ? x_file_regs(off, kind, n_files, tfn, lane) : fr;
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // file starts: tile-relative output offsets once the lane's prefix is known
     uint32_t sf[4], sc[4], ns = 0;
     const uint32_t c = x_lane(
-        n_bytes, off, kind, n_files, tf, blk, W,
+        n_bytes, T, n_files, blk, W,
         [&](uint32_t f, uint32_t at) {
           if (ns < 4) {
             sf[ns] = f;
@@ -270,13 +322,14 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
     const uint32_t ex = wave_excl(c, lane);
     if (lane == 63) tile_cnt[t] = ex + c;
     if (ns > 4) {  // many tiny files in one block: walk it again, recording all
-      x_lane(n_bytes, off, kind, n_files, tf, blk, W, [&](uint32_t f, uint32_t at) { fstart[f] = ex + at; },
+      x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t f, uint32_t at) { fstart[f] = ex + at; },
              [&](uint32_t, uint32_t, uint32_t) {});
     } else {
       for (uint32_t i = 0; i < ns; i++) fstart[sf[i]] = ex + sc[i];
     }
     v = vn;
     tf = tfn;
+    fr = frn;
   }
 }
 
@@ -304,22 +357,30 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
   uint8_t* S = s_out[threadIdx.x >> 6];
   const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   const uint32_t waves = gridDim.x * (kXThreads / 64);
+  __shared__ uint32_t s_fo[kXThreads / 64][65];
+  __shared__ uint8_t s_fk[kXThreads / 64][64];
+  uint32_t* so = s_fo[threadIdx.x >> 6];
+  uint8_t* sk = s_fk[threadIdx.x >> 6];
   uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
   uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);  // the next tile's inputs, a tile ahead
   uint32_t tfn = t < n_tiles ? chunk_file[t] : 0u;
   uint64_t pren = t < n_tiles ? tile_pre[t] : 0u;
+  XFileRegs frn = x_file_regs(off, kind, n_files, tfn, lane);
   for (; t < n_tiles; t += waves) {
     const uint32_t blk = t * kXTile + 16 * lane;
     const uint4 v = vn;
     const uint32_t tf = tfn;
     const uint64_t start = pren;
+    x_stage_files(so, sk, frn, lane);
+    const XFiles T{tf, so, sk, off, kind};
     vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
     tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
     pren = t + waves < n_tiles ? tile_pre[t + waves] : 0u;
+    if (t + waves < n_tiles) frn = x_file_regs(off, kind, n_files, tfn, lane);
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
     uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0, added = 0;
-    const uint32_t c = x_lane(n_bytes, off, kind, n_files, tf, blk, W, [&](uint32_t, uint32_t) {},
+    const uint32_t c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
                               [&](uint32_t K, uint32_t C, uint32_t Z) {
                                 if (nseg < 4) {
                                   segK[nseg] = K;
@@ -380,7 +441,7 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
     if (nseg <= 4) {
       for (uint32_t i = 0; i < nseg; i++) put(segK[i], segC[i], segZ[i]);
     } else {
-      x_lane(n_bytes, off, kind, n_files, tf, blk, W, [&](uint32_t, uint32_t) {}, put);
+      x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {}, put);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
