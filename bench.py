@@ -410,7 +410,7 @@ def main():
     ap.add_argument("--cpu-sample-mb", type=float, default=None, help="CPU-baseline sample (first files)")
     ap.add_argument("--parity-mb", type=float, default=None, help="oracle parity sample (first files)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=3, help="scans in flight (pipelined submission)")
+    ap.add_argument("--depth", type=int, default=4, help="scans in flight (pipelined submission)")
     ap.add_argument("--crlf", type=float, default=0.05,
                     help="c2: share of CRLF files (SURVEY §8(d)); stripped while packing the HBM arena")
     ap.add_argument("--numa", choices=["gpu", "off"], default="gpu",
