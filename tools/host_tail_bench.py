@@ -71,7 +71,7 @@ def main():
     sp = None
     if os.environ.get("SPROF"):  # tools/sprof: sample the reps' CPU time
         sp = c.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "sprof", "sprof.so"))
-        sp.sprof_start(4000)
+        sp.sprof_start(int(os.environ.get("SPROF_US", "4000")))
     for _ in range(args.reps):
         h = c.c_void_p()
         t = time.time()

@@ -14,7 +14,7 @@ ROOT=$(pwd)
 MODE=${1:-all}
 python -c "import __graft_entry__ as g; g.build()" || exit 1
 COMMON="-O1 -g -march=x86-64-v3 -fPIC -std=c++17 -fno-omit-frame-pointer -I trivy_amd/csrc -I include -I oracle/native -D__HIP_PLATFORM_AMD__ -I /opt/rocm/include"
-TESTS="tests/test_host_concurrency.py tests/test_host_tail.py tests/test_analyzer.py tests/test_allow_path.py tests/test_rules_data.py"
+TESTS="tests/test_host_concurrency.py tests/test_host_tail.py tests/test_analyzer.py tests/test_allow_path.py tests/test_rules_data.py tests/test_fs_walk.py"
 build() {  # $1 = name, $2 = sanitizer flags
   local out=oracle/build/san_$1
   mkdir -p $out
@@ -24,7 +24,7 @@ build() {  # $1 = name, $2 = sanitizer flags
     g++ $COMMON $2 -c $src -o $o || return 1
     objs="$objs $o"
   done
-  g++ -shared $2 -o $out/libtsg_host.so $objs trivy_amd/_obj/engine.hip.o trivy_amd/_obj/xform.hip.o -L/opt/rocm/lib -lamdhip64 -lpthread \
+  g++ -shared $2 -o $out/libtsg_host.so $objs trivy_amd/_obj/*.hip.o -L/opt/rocm/lib -lamdhip64 -lpthread \
     -Wl,-rpath,/opt/rocm/lib || return 1
   echo $out/libtsg_host.so
 }
@@ -38,9 +38,10 @@ if [ "$MODE" = asan ] || [ "$MODE" = all ]; then
 fi
 if [ "$MODE" = tsan ] || [ "$MODE" = all ]; then
   lib=$(build tsan "-fsanitize=thread") || exit 1
-  LD_PRELOAD=$(g++ -print-file-name=libtsan.so) TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
-  TSG_HOSTLIB=$ROOT/$lib python -m pytest tests/test_host_concurrency.py tests/test_host_tail.py -q -m "not gpu" \
-    -p no:cacheprovider > profiles/sanitize_tsan.log 2>&1
+  LD_PRELOAD=$(readlink -f $(g++ -print-file-name=libtsan.so)) TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
+  # (the pool-budget test spawns interpreters that inherit the TSan preload and stall in it: not a race test)
+  TSG_HOSTLIB=$ROOT/$lib python -m pytest tests/test_host_concurrency.py tests/test_host_tail.py \
+    -q -m "not gpu" -k "not pool_budget" -p no:cacheprovider > profiles/sanitize_tsan.log 2>&1
   r=$?; tail -3 profiles/sanitize_tsan.log; [ $r -eq 0 ] || rc=$r
 fi
 exit $rc

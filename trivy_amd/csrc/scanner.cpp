@@ -647,7 +647,7 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 
 // Host-tail phase profile (TSG_TAIL_DEBUG=1 only; otherwise the timers are inert).
 const bool g_tail_debug = std::getenv("TSG_TAIL_DEBUG") != nullptr;
-std::atomic<int64_t> g_prof[10];  // [8] [9]: bytes memchr'd forward / backward by the line walks
+std::atomic<int64_t> g_prof[11];  // [8] [9] [10]: bytes memchr'd forward / backward (no hint, in a window) by the line walks
 std::atomic<int64_t> g_wholefile_bytes{0}, g_wholefile_calls{0};  // TSG_TAIL_DEBUG: whole-content gate scans
 struct PhaseTimer {
   int k;
@@ -971,11 +971,35 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
     if (pos <= 0) return -1;
     auto it = std::upper_bound(hints.begin(), hints.end(), pos,
                                [](int64_t v, const Candidate* h) { return v < h->wlo; });
-    if (it != hints.begin()) {  // a window starting at or below pos: search [wlo, pos), then its list
+    if (it != hints.begin()) {  // a window starting at or below pos: [wlo, pos), then its list
       const Candidate& h = **(it - 1);
       if (pos > h.wlo) {
-        const void* q = memrchr(content + h.wlo, '\n', size_t(pos - h.wlo));
-        if (q) return int64_t(static_cast<const uint8_t*>(q) - content);
+        // the forward list names the first '\n' at or after wlo: when it ends
+        // below pos, only (its last, pos) is searched, when it reaches pos or
+        // the file end nothing is (a match deep in a long line: no scan back
+        // over the line)
+        int64_t known = -1, from = h.wlo;
+        bool complete = false;
+        for (int k = 0; k < 3; k++) {
+          if (h.nl_fwd[k] == kNlUnknown) break;
+          if (h.nl_fwd[k] == kNlNone) {
+            complete = true;
+            break;
+          }
+          const int64_t at = h.wlo + int64_t(h.nl_fwd[k]);
+          if (at >= pos) {
+            complete = true;
+            break;
+          }
+          known = at;
+          from = at + 1;
+        }
+        if (!complete && from < pos) {
+          const void* q = memrchr(content + from, '\n', size_t(pos - from));
+          if (g_tail_debug) g_prof[10] += q ? pos - (static_cast<const uint8_t*>(q) - content) : pos - from;
+          if (q) return int64_t(static_cast<const uint8_t*>(q) - content);
+        }
+        if (known >= 0) return known;
       }
       return h.nl_back[0] == kNlNone ? -1 : h.wlo - int64_t(h.nl_back[0]);
     }
@@ -1384,8 +1408,9 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
                  g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
   if (g_tail_debug)
-    std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB; line walks: %.1f MB forward, %.1f MB back\n",
-                 (long long)g_wholefile_calls.load(), g_wholefile_bytes.load() / 1e6, g_prof[8] / 1e6, g_prof[9] / 1e6);
+    std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB; line walks: %.1f MB forward, %.1f MB back"
+                 " (%.1f MB inside windows)\n", (long long)g_wholefile_calls.load(), g_wholefile_bytes.load() / 1e6,
+                 g_prof[8] / 1e6, (g_prof[9] + g_prof[10]) / 1e6, g_prof[10] / 1e6);
   out->found_files.reserve(nf);
   out->found.reserve(nf);
   for (size_t k = 0; k < nf; k++) {
