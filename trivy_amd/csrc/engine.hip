@@ -931,12 +931,18 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     }
   };
   const uint32_t stride = gridDim.x * blockDim.x;
+  // the next iteration's record is loaded a batch ahead: one dependent global
+  // round trip (record -> window bytes -> file offsets) less per batch
+  uint32_t rec_next = blockIdx.x * blockDim.x + wave * 64 + lane < n_recs ? P.recs[blockIdx.x * blockDim.x + wave * 64 + lane]
+                                                                          : 0u;
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave * 64; r0 < n_recs; r0 += stride) {
     // ---- A: one block per lane
     const uint32_t r = r0 + lane;
+    const uint32_t rec = rec_next;
+    rec_next = r + stride < n_recs ? P.recs[r + stride] : 0u;
     uint32_t fire_e[4], n_fire = 0;
     if (r < n_recs) {
-      const uint64_t base = uint64_t(P.recs[r]) * 16;
+      const uint64_t base = uint64_t(rec) * 16;
       const uint64_t w0 = base >= 16 ? base - 16 : 0;
       uint4 dw[kCWin / 16];
 #pragma unroll
