@@ -291,6 +291,31 @@ def test_native_walk_bulk_accept_vs_oracle(host_analyzer, layer_30mb, arena_mb, 
     assert batches == (1 if arena_mb == 64 else batches) and (arena_mb == 64 or batches > 1)
 
 
+@pytest.mark.parametrize("arena_mb", [2, 64])
+def test_native_walk_bad_header_in_bulk_block(host_analyzer, layer_30mb, arena_mb):
+    """A corrupted header checksum two thirds into the layer -- inside a block the accept
+    step takes in bulk (64 MiB batches) or entry by entry (2 MiB) -- fails the walk with
+    archive/tar's error; with small batches the ones before it are returned first."""
+    import tarfile
+    from trivy_amd.analyzer.secret import Collector, _CTarStats
+    layer, files, wh = layer_30mb
+    raw = bytearray(layer.tobytes())
+    with tarfile.open(fileobj=io.BytesIO(bytes(raw))) as tf:
+        members = tf.getmembers()
+    m = members[len(members) * 2 // 3]
+    raw[m.offset + 148] ^= 0x01  # a digit of the checksum field
+    coll = Collector(host_analyzer, arena_mb << 20, True)
+    cursor, batches = 0, 0
+    with pytest.raises(ValueError, match="checksum"):
+        while True:
+            rc, cursor = coll.add_tar(bytes(raw), cursor, _CTarStats())
+            coll.reset()
+            batches += 1
+            if rc == 0:
+                break
+    assert (batches > 3) if arena_mb == 2 else batches == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_colls", [2, 3])
 @pytest.mark.parametrize("gpu_transform", [False, True])
