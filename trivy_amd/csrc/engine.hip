@@ -201,9 +201,14 @@ __global__ __launch_bounds__(kScanThreads, 4 * kFWgPerCu) void filter_kernel(Fil
   // prefetched data also wait for the store's completion.
   auto flush_nl = [&](uint64_t t_last) {  // wave-uniform; staged tiles are t_last - (nl_slots-1) .. t_last
     wave_sync();
-    if (lane < nl_slots) {
-      const uint64_t tt = t_last - uint64_t(nl_slots - 1 - lane);
-      reinterpret_cast<uint64_t*>(P.nl)[tt] = NL[lane];  // chunks 4tt .. 4tt+3 (buffer padded past the end)
+    // the lane index through an empty asm: the compiler otherwise hoists &NL[lane]
+    // out of the tile loop and, at 64 VGPRs, spills it -- and the scratch reload's
+    // s_waitcnt vmcnt(0) also waited for the next tile's loads in flight
+    uint32_t l = lane;
+    asm volatile("" : "+v"(l));
+    if (l < nl_slots) {
+      const uint64_t tt = t_last - uint64_t(nl_slots - 1 - l);
+      reinterpret_cast<uint64_t*>(P.nl)[tt] = NL[l];  // chunks 4tt .. 4tt+3 (buffer padded past the end)
     }
     nl_slots = 0;
   };
