@@ -295,6 +295,11 @@ __global__ __launch_bounds__(kScanThreads, 4 * kFWgPerCu) void filter_kernel(Fil
         qn += uint32_t(__popcll(m));
       }
     }
+  };
+  // A flush's atomicAdd returns the records' base: waiting for it waits for every
+  // older vector-memory op too, so it goes before the next tile's loads are issued
+  // (then it only waits for the loads the coming tile needs at once anyway).
+  auto flush_due = [&]() {
     if (qn >= kFFlushAt) flush();
   };
   using Full = std::false_type;
@@ -304,15 +309,18 @@ __global__ __launch_bounds__(kScanThreads, 4 * kFWgPerCu) void filter_kernel(Fil
   // two register buffers alternate roles (no copies): tile t in A while t + 1 loads into B
   if (t < t_full) load_tile(bufA, t);
   while (t < t_full) {
+    flush_due();
     load_tile(bufB, t + 1 < t_full ? t + 1 : t);  // past the range: a harmless reload
     tile(bufA, t, Full());
     t++;
     if (t >= t_full) break;
+    flush_due();
     load_tile(bufA, t + 1 < t_full ? t + 1 : t);
     tile(bufB, t, Full());
     t++;
   }
   if (t < t_end) {  // the partial last tile
+    flush_due();
     load_tile(bufA, t);
     tile(bufA, t, std::true_type());
     t++;
