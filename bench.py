@@ -405,6 +405,10 @@ def main():
                     help="timed steps (default 50 for c2: a depth-3 pipeline's fill and drain are then a few %% of the "
                          "timed region, as in a long scan job; 10 for the other workloads)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3 for c2, 2 otherwise)")
+    ap.add_argument("--warmup-s", type=float, default=None,
+                    help="then more untimed steps until this many seconds have passed (default 10 for c2, 0 "
+                         "otherwise): on some boxes the kernels ran 5-7 %% slower for the first minute or two "
+                         "of GPU load; the JSON's warmup is the number of warm-up steps actually run")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--gb", type=float, default=None, help="corpus size per GPU (GB = 1e9 B)")
     ap.add_argument("--cpu-sample-mb", type=float, default=None, help="CPU-baseline sample (first files)")
@@ -434,6 +438,8 @@ def main():
         args.steps = 50 if args.workload == "c2" else 10
     if args.warmup is None:
         args.warmup = 3 if args.workload == "c2" else 2
+    if args.warmup_s is None:
+        args.warmup_s = 10.0 if args.workload == "c2" else 0.0
     if args.traffic_file is None:  # the newest PMC pass of this workload (c2: traffic_rNN.json)
         cands = [os.path.join(ROOT, "profiles", "traffic_r%02d%s.json" % (r, "" if args.workload == "c2" else
                                                                             "_" + args.workload)) for r in (3, 2)]
@@ -567,7 +573,11 @@ def main():
 
     last_res = [None]  # the last step's ScanResult (findings checked against the oracle below)
     warm = []
+    tw0 = time.time()
     run_steps(args.warmup, warm)
+    while time.time() - tw0 < args.warmup_s:  # keep the GPU loaded until its clocks have settled
+        run_steps(10, warm)
+        args.warmup += 10
 
     def barrier():
         if dist is not None:
