@@ -406,9 +406,10 @@ def main():
                          "timed region, as in a long scan job; 10 for the other workloads)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3 for c2, 2 otherwise)")
     ap.add_argument("--warmup-s", type=float, default=None,
-                    help="then more untimed steps until this many seconds have passed (default 10 for c2, 0 "
-                         "otherwise): on some boxes the kernels ran 5-7 %% slower for the first minute or two "
-                         "of GPU load; the JSON's warmup is the number of warm-up steps actually run")
+                    help="then more untimed steps until this many seconds have passed (default: 10 for c2 when "
+                         "--warmup is not given, else 0 -- an explicit --warmup is honoured as given): on some "
+                         "boxes the kernels ran 5-7 %% slower for the first minute or two of GPU load; the JSON "
+                         "reports the warm-up steps actually run and warmup_s")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--gb", type=float, default=None, help="corpus size per GPU (GB = 1e9 B)")
     ap.add_argument("--cpu-sample-mb", type=float, default=None, help="CPU-baseline sample (first files)")
@@ -436,10 +437,10 @@ def main():
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 50 if args.workload == "c2" else 10
+    if args.warmup_s is None:  # only when the warm-up steps are not given explicitly
+        args.warmup_s = 10.0 if args.workload == "c2" and args.warmup is None else 0.0
     if args.warmup is None:
         args.warmup = 3 if args.workload == "c2" else 2
-    if args.warmup_s is None:
-        args.warmup_s = 10.0 if args.workload == "c2" else 0.0
     if args.traffic_file is None:  # the newest PMC pass of this workload (c2: traffic_rNN.json)
         cands = [os.path.join(ROOT, "profiles", "traffic_r%02d%s.json" % (r, "" if args.workload == "c2" else
                                                                             "_" + args.workload)) for r in (3, 2)]
@@ -578,6 +579,7 @@ def main():
     while time.time() - tw0 < args.warmup_s:  # keep the GPU loaded until its clocks have settled
         run_steps(10, warm)
         args.warmup += 10
+    warm_s = time.time() - tw0
 
     def barrier():
         if dist is not None:
@@ -777,6 +779,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_s": round(warm_s, 2),
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "weak",

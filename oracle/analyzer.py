@@ -285,6 +285,8 @@ def walk_fs(root: str, skip_dirs=(), skip_files=()):
         if st_.S_ISREG(rs.st_mode) and not skip_path(".", skip_files):
             out.append((os.path.basename(root), rs.st_size))
         return out
+    if skip_path(".", skip_dirs):  # WalkDir's first call is the root itself, relPath "." (fs.go:51-55)
+        return out
 
     def walk(abs_dir, rel):
         try:
@@ -319,12 +321,14 @@ def analyze_fs(analyzer: SecretAnalyzer, root: str, skip_dirs=(), skip_files=())
     out = []
     files = walk_fs(root, skip_dirs, skip_files)
     is_file = not os.path.isdir(root)
+    # a file root: dir, filePath = path.Split(rootPath) (artifact/local/fs.go:90-93)
+    dir_ = root[:root.rfind("/") + 1] if is_file else root
     for rel, size in files:
         if not analyzer.required(rel, size):
             continue
         with open(root if is_file else os.path.join(root, rel), "rb") as f:
             content = f.read()
-        r = analyzer.analyze(rel, root, content)
+        r = analyzer.analyze(rel, dir_, content)
         if r is not None:
             out.append(r["Secrets"][0])
     out.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape")

@@ -106,8 +106,9 @@ def _collect_oracle(root, skip_dirs=(), skip_files=()):
     for rel, size in oan.walk_fs(root, skip_dirs, skip_files):
         if not a.required(rel, size):
             continue
-        with open(os.path.join(root, rel) if os.path.isdir(root) else root, "rb") as f:
-            args = a.prepare(rel, root, f.read())
+        is_dir = os.path.isdir(root)
+        with open(os.path.join(root, rel) if is_dir else root, "rb") as f:
+            args = a.prepare(rel, root if is_dir else root[:root.rfind("/") + 1], f.read())
         if args is not None:
             out.append(args)
     return out
@@ -128,6 +129,32 @@ def test_native_walk_file_root(tmp_path):
     p.write_bytes(b"GITHUB=ghp_" + b"z" * 36 + b"\n")
     got, _, _, _ = _collect_native(str(p), Option())
     assert [(x[0], x[1]) for x in got] == [(x[0], x[1]) for x in _collect_oracle(str(p))] == [("one.env", p.read_bytes())]
+
+
+def test_native_walk_bare_file_root(tmp_path):
+    """A root given as a bare file name: path.Split gives Dir "", so Analyze reports "/name"
+    (artifact/local/fs.go:90-93, analyzer/secret/secret.go:130-135); Required still sees "name"."""
+    p = tmp_path / "two.env"
+    p.write_bytes(b"GITHUB=ghp_" + b"y" * 36 + b"\n")
+    cwd = os.getcwd()
+    try:
+        os.chdir(tmp_path)
+        got, _, _, _ = _collect_native("two.env", Option())
+        want = _collect_oracle("two.env")
+    finally:
+        os.chdir(cwd)
+    assert [(x[0], x[1]) for x in got] == [(x[0], x[1]) for x in want] == [("/two.env", p.read_bytes())]
+
+
+@pytest.mark.parametrize("pat", ["*", ".", "**"])
+def test_native_walk_root_skipped(tmp_path, pat):
+    """filepath.WalkDir calls the WalkDirFunc on the root first with relPath ".": a SkipDirs
+    pattern matching "." skips the whole tree (walker/fs.go:51-55)."""
+    root = _tree(str(tmp_path / "t"), random.Random(13), n_files=20)
+    got, _, _, _ = _collect_native(root, Option(SkipDirs=[pat]))
+    want = _collect_oracle(root, (pat,))
+    assert [(p, d, b) for p, d, b in got] == [(p, d, b) for p, d, b in want]
+    assert (len(got) == 0) == bool(oan.skip_path(".", [pat]))
 
 
 @pytest.mark.gpu

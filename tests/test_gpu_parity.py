@@ -165,6 +165,36 @@ def test_c3_generated_rules_corpus(secret, tmp_path):
     assert n > 50
 
 
+def test_blocks_with_many_fires(secret):
+    """Anchor literals packed back to back, so single 16-B blocks hold five or more
+    filter-window ends: the confirm kernel keeps four fires per lane in registers and
+    handles the rest in place (the 4th fire of such a block was dropped).
+    Real tokens follow the dense runs, vs the oracle; the CPU filter model shows the
+    content really has such blocks."""
+    import numpy as np
+    from tests.filter_model import FilterModel
+    from trivy_amd.secret.config import builtin_rules
+    lits = [b"ghp_", b"gho_", b"AKIA", b"xoxb-", b"glpat-", b"sk_live_", b"linear", b"-----", b"eyJ", b"hf_",
+            b"aws", b"twitter", b"heroku", b"asana", b"pk.", b"SG.", b"dapi", b"shpat_", b"npm_", b"pypi-"]
+    toks = [b"ghp_" + b"a1B2" * 9, b"AKIA" + b"Q" * 16, b"glpat-" + b"d" * 20, b"sk_live_" + b"e" * 24,
+            b"xoxb-" + b"1" * 10 + b"-" + b"2" * 12 + b"-" + b"c" * 24, b'linear_secret = "' + b"ab12" * 8 + b'"',
+            b"npm_" + b"Z" * 36, b"shpat_" + b"0123456789abcdef" * 2]
+    rng = random.Random(55)
+    files = []
+    for i in range(160):
+        parts = []
+        for _ in range(rng.randint(1, 6)):
+            run = b"".join(rng.choice(lits) for _ in range(rng.randint(4, 24)))
+            parts.append(run + rng.choice(toks) + rng.choice([b"", b" ", b"\n", b'"']))
+        files.append(("dense%03d.txt" % i, rng.choice([b"", b"x = ", b"\n"]).join(parts)))
+    fm = FilterModel(builtin_rules())
+    blob = b"".join(c for _, c in files)
+    fr = fm.fires(np.frombuffer(blob, dtype=np.uint8))[:fm.n_buckets - 1].any(axis=0)
+    per_block = np.bincount(np.nonzero(fr)[0] >> 4)
+    assert per_block.max() >= 5 and (per_block >= 5).sum() > 50, per_block.max()
+    assert _compare_corpus(secret, files) > 200
+
+
 def test_empty_batch(secret):
     s = secret.NewScanner(None)
     assert s.ScanBatch([]) == []

@@ -1,0 +1,46 @@
+# Round-4 GPU iteration: stages chosen by STAGES (space-separated), each under its own time limit,
+# stopping at the first failure.  Usage: gpurun -- 'TAG=r04a STAGES="tests bench diag prof" bash tools/gpu_r04.sh'
+#   tests  : the -m gpu suite (PYTEST_ARGS narrows it)
+#   smoke  : __graft_entry__.smoke()
+#   bench  : the driver-style default line (20 steps, 5 warm-up, CPU baseline, parity, ingest leg)
+#   quick  : C2 without the CPU baseline (BENCH_ARGS adds flags)
+#   diag   : C2 confirm-kernel split (TSG_DIAG_CONFIRM 4 / 8 / 16), 5 steps each
+#   prof   : rocprofv3 --kernel-trace --stats of a short C2 run
+#   wl     : the workloads in WLS (default c3 c3f c4 c1fs c5), with CPU baselines unless WL_ARGS says otherwise
+set -o pipefail
+TAG=${TAG:-r04}
+STAGES=${STAGES:-tests bench}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+for st in $STAGES; do
+  case $st in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests_$TAG.log 2>&1
+      rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
+      rc=$?; tail -2 gpurun_out/smoke_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+      rc=$?; python tools/bench_brief.py gpurun_out/bench_$TAG.json; tail -2 gpurun_out/bench_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
+    quick)
+      timeout -k 10 400 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/quick_$TAG.json 2> gpurun_out/quick_$TAG.err
+      rc=$?; python tools/bench_brief.py gpurun_out/quick_$TAG.json; tail -2 gpurun_out/quick_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
+    diag)
+      for d in 0 4 8 16; do
+        TSG_DIAG_CONFIRM=$d timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --ingest-steps 0 > gpurun_out/diag${d}_$TAG.json 2> gpurun_out/diag${d}_$TAG.err
+        rc=$?; echo "== diag $d"; python tools/bench_brief.py gpurun_out/diag${d}_$TAG.json; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    prof)
+      cd /tmp
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --ingest-steps 0 > $R/gpurun_out/prof_bench_$TAG.json 2> $R/gpurun_out/prof_$TAG.err
+      rc=$?; cd $R; tail -2 gpurun_out/prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
+      find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
+    wl)
+      for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
+        timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
+        rc=$?; echo "== $wl"; python tools/bench_brief.py gpurun_out/wl_${TAG}_$wl.json; tail -2 gpurun_out/wl_${TAG}_$wl.err; [ $rc -eq 0 ] || exit $rc
+      done ;;
+  esac
+done

@@ -996,8 +996,9 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
           uint32_t fm = 0;
 #pragma unroll
           for (int w = 0; w < kFWords; w++) fm |= ((~st[w] >> 20) & 0xFu) << (4 * w);
-          fire_e[n_fire < 4 ? n_fire : 3] = lane | (k << 6) | (fm << 10);
-          if (n_fire >= 4) do_fire(fire_e[3]);  // more than 4 fires in one block: handle in place
+          const uint32_t fe = lane | (k << 6) | (fm << 10);
+          if (n_fire < 4) fire_e[n_fire] = fe;
+          else do_fire(fe);  // more than 4 fires in one block: the 5th and later in place
           n_fire++;
         }
       }

@@ -257,6 +257,9 @@ struct tsg_fs_walk {
   size_t next = 0;
   bool listed = false;
   bool root_is_file = false;
+  // a bare file name as the root: path.Split gives Dir "" and Analyze reports
+  // "/" + name (artifact/local/fs.go:90-93, analyzer/secret/secret.go:130-135)
+  bool slash_prefix = false;
   uint64_t dirs = 0, skipped_dirs = 0, nonregular = 0, skipped_files = 0, perm_errors = 0;
 };
 
@@ -291,7 +294,14 @@ bool ListTree(tsg_fs_walk* w, int threads) {
       const size_t sl = w->root.find_last_of('/');
       w->files.push_back({sl == std::string::npos ? w->root : w->root.substr(sl + 1), uint64_t(rs.st_size)});
       w->root_is_file = true;
+      w->slash_prefix = sl == std::string::npos;
     }
+    return true;
+  }
+  // WalkDir visits the root first with relPath ".": a SkipDirs pattern
+  // matching "." skips the whole tree (walker/fs.go:51-55)
+  if (tsg::SkipPath(".", w->skip_dirs)) {
+    w->skipped_dirs++;
     return true;
   }
   std::vector<DirNode> nodes(1);
@@ -526,6 +536,7 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
         c->used += need;  // final length fixed after the read (host mode)
         added.push_back(k);
         c->offs.push_back(c->used);
+        if (w->slash_prefix) c->path_pool.push_back('/');
         c->path_pool.append(f.rel);  // Dir = root: FilePath as walked (secret.go:130-135 adds no '/')
         c->path_off.push_back(c->path_pool.size());
         c->binary.push_back(x.bin);
