@@ -62,12 +62,16 @@ def _compare(secret, files, cfg):
     return n
 
 
-@pytest.mark.parametrize("chunk,class_runs", [("4096", "0"), ("65536", "0"), ("4096", "1")])
-def test_fullscan_chunks_vs_oracle(tmp_path, monkeypatch, chunk, class_runs):
+@pytest.mark.parametrize("chunk,class_runs,task", [("4096", "0", "4096"), ("65536", "0", "4096"),
+                                                   ("4096", "0", "16"), ("4096", "1", "4096")])
+def test_fullscan_chunks_vs_oracle(tmp_path, monkeypatch, chunk, class_runs, task):
     """class_runs 0: no literal anchors, the rules run in full-scan mode; 1: they are
-    anchored on their runs of one-byte classes (rules.cpp ExtractClassRun)."""
+    anchored on their runs of one-byte classes (rules.cpp ExtractClassRun).  Bounded rules
+    run as lane tasks (task: TSG_FS_TASK_BYTES, 16 = the 8 x max_len minimum: many task
+    edges inside tokens), the unbounded one wave-wide in chunks (TSG_FULLSCAN_CHUNK)."""
     import trivy_amd.secret as secret
     monkeypatch.setenv("TSG_FULLSCAN_CHUNK", chunk)
+    monkeypatch.setenv("TSG_FS_TASK_BYTES", task)
     monkeypatch.setenv("TSG_CLASS_RUNS", class_runs)
     cfg = tmp_path / "trivy-secret.yaml"
     cfg.write_text(RULES)
@@ -127,3 +131,49 @@ def test_keyword_gate_through_fold_runes_vs_oracle(tmp_path, monkeypatch, class_
     cfg.write_text(FOLD_RULES)
     n = _compare(secret, files, str(cfg))
     assert n >= 8
+
+
+def test_fullscan_lists_overflow_and_grow(tmp_path, monkeypatch):
+    """More open pairs (20,000 files, a keyword-less bounded rule) than the initial pair list
+    (16,384) and more lane tasks (a 6 MB file cut into ~80-B tasks) than the initial task list
+    (65,536): the scan sees the overflow, grows the lists to the counts and rescans.  Every file
+    vs the restated reference CPU scan (tsg_cpuref_scan), a sample vs the oracle."""
+    import numpy as np
+    from bench import full_diff
+    from tests.test_gpu_bench_corpus import _cpuref
+    import trivy_amd.secret as secret
+    monkeypatch.setenv("TSG_FS_TASK_BYTES", "16")
+    monkeypatch.setenv("TSG_CLASS_RUNS", "0")
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text("rules:\n  - id: digits\n    category: Custom\n    title: Digits\n    severity: LOW\n"
+                   "    regex: '[0-9]{3}-[0-9]{4}-[0-9]{3}'\n")
+    rng = random.Random(3)
+    contents = [b"x %03d-%04d-%03d y" % (i % 1000, i, i % 997) if i % 3 == 0 else b"nothing %d" % i
+                for i in range(20000)]
+    big = bytearray(b"ab 12-3456-789 " * (6_000_000 // 15))
+    for k in range(300):
+        at = rng.randrange(len(big) - 20)
+        big[at:at + 14] = b" 123-4567-890 "
+    contents.insert(7000, bytes(big))
+    paths = ["f%05d.txt" % i for i in range(len(contents))]
+    offs = np.zeros(len(contents) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+
+    class C:  # the shape _cpuref / full_diff read
+        pass
+    C.arena, C.offsets, C.n_files = arena, offs, len(contents)
+    keep = [np.frombuffer(p.encode() + b"\0", dtype=np.uint8) for p in paths]  # alive while C is
+    C.path_ptrs = np.array([k.ctypes.data for k in keep], dtype=np.uint64)
+    res = secret.NewScanner(secret.ParseConfig(str(cfg))).scan_arena(arena, offs, paths)
+    st = res.stats()
+    assert st["fullscan_pairs"] > 16384
+    ref = _cpuref(C, cfg_path=str(cfg))
+    bad, first = full_diff(res, ref, C.n_files)
+    assert bad == 0, (bad, paths[first] if first is not None else None)
+    assert st["findings"] > 6000
+    o = osc.new_scanner(osc.parse_config(str(cfg)))
+    got = res.secrets(paths)
+    for i in list(range(0, 20001, 997)):
+        if i != 7000:
+            assert got[i].to_dict() == o.scan(paths[i], contents[i]), paths[i]

@@ -37,6 +37,11 @@ for st in $STAGES; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --ingest-steps 0 > $R/gpurun_out/prof_bench_$TAG.json 2> $R/gpurun_out/prof_$TAG.err
       rc=$?; cd $R; tail -2 gpurun_out/prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
       find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
+    ingprof)  # the C2 ingest leg under a kernel + memory-copy trace (copy / kernel timeline)
+      cd /tmp
+      timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace -d $R/gpurun_out/ingprof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --warmup-s 0 --no-cpu-baseline --ingest-steps 3 > $R/gpurun_out/ingprof_bench_$TAG.json 2> $R/gpurun_out/ingprof_$TAG.err
+      rc=$?; cd $R; tail -2 gpurun_out/ingprof_$TAG.err; [ $rc -eq 0 ] || exit $rc
+      python tools/bench_brief.py gpurun_out/ingprof_bench_$TAG.json ;;
     wl)
       for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
         timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err

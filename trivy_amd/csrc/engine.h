@@ -200,6 +200,7 @@ class GpuEngine {
   uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
                                     // [7] flagged-block records [8] record overflow
                                     // [9] fold sites [10] fold-site overflow
+                                    // [6] full-scan list overflow [11] anchor-item matches [13] open pairs
   // host-batch streaming (RunHost): two staging buffers, a copy stream
   hipStream_t copy_stream_ = nullptr;
   hipEvent_t ev_copied_[2] = {}, ev_h2d_[2] = {};
@@ -218,7 +219,13 @@ class GpuEngine {
   hipEvent_t ev_x_[2] = {};
   uint64_t chunk_bytes_ = uint64_t(1) << 30;             // TSG_INGEST_CHUNK_MB
   uint32_t hit_cap_ = 0, cand_cap_ = 0;
-  uint32_t fs_chunk_ = 65536;         // TSG_FULLSCAN_CHUNK: full-scan bytes per lane (min)
+  uint32_t fs_chunk_ = 65536;         // TSG_FULLSCAN_CHUNK: full-scan bytes per lane (min, wave-wide pairs)
+  uint32_t fs_task_bytes_ = 4096;     // TSG_FS_TASK_BYTES: full-scan lane task size (min; >= 8 x max_len)
+  uint32_t fs_pair_cap_ = 0, fs_task_cap_ = 0;
+  void* d_fs_pairs_ = nullptr; size_t cap_fs_pairs_ = 0;  // FsPair list
+  void* d_fs_tasks_ = nullptr; size_t cap_fs_tasks_ = 0;  // 4 x FsTask lists (by NFA width)
+  void* d_fs_wave_ = nullptr; size_t cap_fs_wave_ = 0;    // pairs run wave-wide
+  uint32_t* d_fs_ctr_ = nullptr;                          // [0] pairs [1..4] tasks [5] wave pairs
   hipEvent_t ev_fs_ = nullptr;
   hipEvent_t ev_sync_ = nullptr;  // blocking-sync: the host waits asleep, not spinning
   bool blocking_sync_ = true;

@@ -414,22 +414,35 @@ __device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
 #endif
 constexpr uint32_t kCWaveHits = TSG_C_HITS;
 
+// A hit record is 3 u32: file, the literal end in the file (low 32 bits),
+// the anchor id with the end's bits 32..39 in its top byte (files of 4 GiB
+// and more; anchor ids < 2^24, checked when the engine is built).
+constexpr uint32_t kHitAidBits = 24;
+__device__ __forceinline__ uint32_t hit_aid_word(uint32_t aid, uint64_t end) {
+  return aid | (uint32_t(end >> 32) << kHitAidBits);
+}
+__device__ __forceinline__ void hit_unpack(const uint32_t* h, uint32_t* f, uint64_t* end, uint32_t* aid) {
+  *f = h[0];
+  *end = uint64_t(h[1]) | (uint64_t(h[2] >> kHitAidBits) << 32);
+  *aid = h[2] & ((1u << kHitAidBits) - 1u);
+}
+
 // Appends a hit to the wave's LDS buffer (LDS atomic); a full buffer spills to
 // the global list directly.
 __device__ __forceinline__ void stage_hit(uint32_t* hbuf, uint32_t* hcnt, uint32_t* hits, uint32_t cap,
-                                          uint32_t* counters, uint32_t f, uint32_t end, uint32_t aid) {
+                                          uint32_t* counters, uint32_t f, uint64_t end, uint32_t aid) {
   const uint32_t k = atomicAdd(hcnt, 1u);
   if (k < kCWaveHits) {
     hbuf[3 * k + 0] = f;
-    hbuf[3 * k + 1] = end;
-    hbuf[3 * k + 2] = aid;
+    hbuf[3 * k + 1] = uint32_t(end);
+    hbuf[3 * k + 2] = hit_aid_word(aid, end);
     return;
   }
   const uint32_t g = atomicAdd(&counters[0], 1u);
   if (g < cap) {
     hits[3ull * g + 0] = f;
-    hits[3ull * g + 1] = end;
-    hits[3ull * g + 2] = aid;
+    hits[3ull * g + 1] = uint32_t(end);
+    hits[3ull * g + 2] = hit_aid_word(aid, end);
   } else {
     counters[3] = 1;
   }
@@ -460,13 +473,13 @@ __device__ __forceinline__ void flush_staged(uint32_t* hbuf, uint32_t* hcnt, uin
   wave_sync();
 }
 
-__device__ __forceinline__ void put_hit(uint32_t* hits, uint32_t cap, uint32_t* counters, uint32_t f, uint32_t end,
+__device__ __forceinline__ void put_hit(uint32_t* hits, uint32_t cap, uint32_t* counters, uint32_t f, uint64_t end,
                                         uint32_t aid) {
   const uint32_t g = wave_slot(&counters[0]);
   if (g < cap) {
     hits[3ull * g + 0] = f;
-    hits[3ull * g + 1] = end;
-    hits[3ull * g + 2] = aid;
+    hits[3ull * g + 1] = uint32_t(end);
+    hits[3ull * g + 2] = hit_aid_word(aid, end);
   } else {
     counters[3] = 1;
   }
@@ -841,7 +854,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
       return;
     }
     if (P.item_diag) atomicAdd(&P.item_diag[2 * ix], 1u);
-    const uint32_t lit_end = uint32_t(s0 - fs) + it.lit_end;
+    const uint64_t lit_end = (s0 - fs) + it.lit_end;
     // The anchor's follow requirements over the 52 bytes after the literal,
     // read from the lane's LDS window when it holds them (else through the
     // caches): most hits of frequent anchor words ("aws_region", prose
@@ -1172,7 +1185,7 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
       if (!ok || !covered) return;
       if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
       for (uint32_t d = 0; d < it.n_ids; d++)
-        put_hit(P.hits, P.hit_cap, P.counters, fsite.f, uint32_t(lit_bytes_end - fs), item_ids[it.ids_off + d]);
+        put_hit(P.hits, P.hit_cap, P.counters, fsite.f, lit_bytes_end - fs, item_ids[it.ids_off + d]);
     };
     const FoldPair* pairs = P.pairs + (other ? (kay ? 0 : P.n_pairs_k)
                                              : P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k));
@@ -1342,7 +1355,9 @@ __device__ uint32_t gate_flags(const NfaParams& P, const RuleGpu& rg, uint32_t f
 __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
   const uint32_t n = P.counters[0] < P.hit_cap ? P.counters[0] : P.hit_cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t f = P.hits[3ull * i], end = P.hits[3ull * i + 1], aid = P.hits[3ull * i + 2];
+    uint32_t f, aid;
+    uint64_t end;
+    hit_unpack(P.hits + 3ull * i, &f, &end, &aid);
     const AnchorInfo a = P.anchors[aid];
     const RuleGpu rg = P.rules[a.rule];  // keyword gates are evaluated lazily by the host tail
     const uint32_t ff = P.flags[f];
@@ -1534,44 +1549,228 @@ __device__ bool fullscan_pair(const NfaParams& P, const uint8_t* arena, uint32_t
   return true;  // not settled: the whole file (always safe)
 }
 
-__global__ __launch_bounds__(256) void fullscan_kernel(NfaParams P) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t n_waves = uint64_t(gridDim.x) * (blockDim.x / 64);
+// Full-scan work lists (round 4).  The old shape gave each wave a slab of 64
+// (file, rule) slots and ran its open pairs one after another: the pairs of a
+// multi-MiB file are adjacent, so a few waves did all the work (C3f: 97 ms,
+// 1,091 pairs).  Now fs_pairs_kernel compacts the open pairs into a global
+// list and cuts each pair whose rule has a bounded match length into lane
+// tasks of task_bytes (>= 8 x max_len): a match ending in a task's range
+// [a, b) starts at or after a + 1 - max_len, so each task runs the relaxed NFA
+// on its own from there (injection everywhere, accepts before a ignored) and
+// needs no state from its neighbours.  fs_task_kernel spreads the tasks over
+// every lane of the GPU (one list per NFA width, so the lanes of a wave run
+// the same code); unbounded rules keep the wave-wide chunk fixpoint
+// (fullscan_pair), one wave per pair from fs_wave_kernel.
+struct FsPair {
+  uint32_t f, r, task_bytes, pad;
+};
+struct FsTask {
+  uint32_t pair, chunk;
+};
+struct FsLists {
+  FsPair* pairs;
+  uint32_t pair_cap;
+  FsTask* tasks;  // list w (NFA words w + 1) at tasks + w * task_cap
+  uint32_t task_cap;
+  uint32_t* wave_pairs;  // pair indices run wave-wide (pair_cap entries)
+  uint32_t* ctr;         // [0] pairs [1..4] tasks per NFA width [5] wave pairs
+  uint32_t task_min;     // TSG_FS_TASK_BYTES
+};
+constexpr uint32_t kFsLaneMaxLen = 8192;  // longer bounded matches: the wave path (a lane would own >= 64 KiB)
+
+__global__ __launch_bounds__(256) void fs_pairs_kernel(NfaParams P, FsLists Q) {
   const uint64_t total = uint64_t(P.n_files) * P.n_fullscan_rules;
-  for (uint64_t t0 = (uint64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; t0 < total;
-       t0 += n_waves * 64) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += stride) {
     // one (file, rule) pair per lane: can its keyword gate be open?
-    const uint64_t t = t0 + lane;
-    bool open = false;
-    uint32_t f = 0, r = 0;
-    if (t < total) {
-      f = uint32_t(t / P.n_fullscan_rules);
-      r = P.fullscan_rules[t % P.n_fullscan_rules];
-      const RuleGpu rg = P.rules[r];
-      open = rg.gate != kGateKeywords || rg.kw_match_implied || kw_bits_inexact(P, f) ||
-             (gate_flags(P, rg, f) & kCandGateOpen);
-      open = open && P.off[f + 1] > P.off[f];
+    const uint32_t f = uint32_t(t / P.n_fullscan_rules);
+    const uint32_t r = P.fullscan_rules[t % P.n_fullscan_rules];
+    const RuleGpu rg = P.rules[r];
+    bool open = rg.gate != kGateKeywords || rg.kw_match_implied || kw_bits_inexact(P, f) ||
+                (gate_flags(P, rg, f) & kCandGateOpen);
+    const uint64_t len = P.off[f + 1] - P.off[f];
+    if (!open || len == 0) continue;
+    atomicAdd(&P.counters[13], 1u);  // open pairs (stats)
+    if (rg.nfa_words == 0) {  // the relaxed NFA accepts at once: the whole file
+      put_candidate(P.cands, P.cand_cap, P.counters, f, r, 0, int64_t(len));
+      continue;
     }
-    uint64_t m = __ballot(open);
-    while (m) {  // the open pairs, one at a time, wave-wide
-      const int src = __ffsll(static_cast<unsigned long long>(m)) - 1;
-      m &= m - 1;
-      const uint32_t pf = __shfl(f, src), pr = __shfl(r, src);
-      const RuleGpu rg = P.rules[pr];
-      const uint64_t fs = P.off[pf], len = P.off[pf + 1] - fs;
-      bool acc = true;
-      if (rg.nfa_words != 0) {
-        const uint64_t* tab = P.nfa + rg.nfa_off;
-        switch (rg.nfa_words) {
-          case 1: acc = fullscan_pair<1>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
-          case 2: acc = fullscan_pair<2>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
-          case 3: acc = fullscan_pair<3>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
-          default: acc = fullscan_pair<4>(P, P.arena, pf, pr, fs, len, tab, rg, lane); break;
+    const uint32_t p = atomicAdd(&Q.ctr[0], 1u);
+    if (p >= Q.pair_cap) {
+      P.counters[6] = 1;  // grow and rescan (GpuEngine::Run)
+      continue;
+    }
+    uint32_t tb = 0;
+    if (rg.max_len != kNoMaxLen && rg.max_len <= kFsLaneMaxLen) {
+      tb = Q.task_min > 8 * rg.max_len ? Q.task_min : 8 * rg.max_len;
+      tb = (tb + 15u) & ~15u;
+      const uint32_t n = uint32_t((len + tb - 1) / tb);
+      const uint32_t w = rg.nfa_words - 1u;
+      const uint32_t base = atomicAdd(&Q.ctr[1 + w], n);
+      for (uint32_t i = 0; i < n; i++) {
+        if (base + i < Q.task_cap) Q.tasks[uint64_t(w) * Q.task_cap + base + i] = FsTask{p, i};
+        else P.counters[6] = 1;
+      }
+    } else {
+      Q.wave_pairs[atomicAdd(&Q.ctr[5], 1u)] = p;  // <= pairs <= pair_cap
+    }
+    Q.pairs[p] = FsPair{f, r, tb, 0};
+  }
+}
+
+// The relaxed NFA of one lane over arena [s0, e) with a start injected at
+// every byte; on_acc(abs) for each accept after byte abs (false stops).  The
+// byte-table rows of a group of bytes are loaded before the group's chain of
+// steps (they depend on the bytes only), so the chain does not wait for a
+// global load per byte.
+template <int W, typename Acc>
+__device__ void nfa_lane(const uint8_t* __restrict arena, uint64_t s0, uint64_t e, const uint64_t* __restrict tab,
+                         Acc on_acc) {
+  constexpr int G = W == 1 ? 16 : (W == 2 ? 8 : 4);  // bytes per prefetched group
+  uint64_t O[W], Lp[W], F[W], D[W];
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    O[w] = tab[w];
+    Lp[w] = tab[W + w];
+    F[w] = tab[2 * W + w];
+    D[w] = 0;
+  }
+  const uint64_t* B = tab + 3 * W;
+  for (uint64_t g0 = s0 & ~uint64_t(15); g0 < e; g0 += 16) {
+    const uint4 v = load16(arena + g0);
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int h = 0; h < 16; h += G) {
+      uint64_t M[G][W];
+      uint32_t by[G];
+#pragma unroll
+      for (int q = 0; q < G; q++) {
+        by[q] = (wd[(h + q) >> 2] >> (8 * ((h + q) & 3))) & 0xFFu;
+#pragma unroll
+        for (int w = 0; w < W; w++) M[q][w] = B[by[q] * W + w];
+      }
+#pragma unroll
+      for (int q = 0; q < G; q++) {
+        const uint64_t abs = g0 + uint64_t(h + q);
+        if (abs < s0 || abs >= e) continue;
+        uint64_t carry = 1, T[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          T[w] = (D[w] << 1) | carry | (D[w] & Lp[w]);
+          carry = D[w] >> 63;
+        }
+        uint64_t c = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          const uint64_t x = T[w] & O[w], s1 = O[w] + x, c1 = s1 < O[w], s2 = s1 + c, c2 = s2 < s1;
+          T[w] |= s2 ^ O[w];
+          c = c1 | c2;
+        }
+        const bool keep = (by[q] & 0xC0u) == 0x80u;  // UTF-8 continuation: also stay
+        uint64_t acc = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          D[w] = (T[w] & M[q][w]) | (keep ? D[w] : 0);
+          acc |= D[w] & F[w];
+        }
+        if (acc && !on_acc(abs)) return;
+      }
+    }
+  }
+}
+
+// One lane task: the accepts after bytes [a, b) of the pair's file, as merged
+// windows of match starts (scanner.go:409-414 candidates for the host's exact
+// FindAll); more than kFsLaneWins windows: one window to the task's end.
+template <int W>
+__device__ void fs_lane_task(const NfaParams& P, const FsPair& pr, uint32_t chunk) {
+  const RuleGpu rg = P.rules[pr.r];
+  const uint64_t fs = P.off[pr.f], fe = P.off[pr.f + 1];
+  const int64_t len = int64_t(fe - fs);
+  const uint64_t a = fs + uint64_t(chunk) * pr.task_bytes;
+  if (a >= fe) return;
+  const uint64_t b = a + pr.task_bytes < fe ? a + pr.task_bytes : fe;
+  const uint64_t back = rg.max_len > 0 ? rg.max_len - 1 : 0;
+  const uint64_t s0 = a - fs > back ? a - back : fs;
+  int64_t wlo = 0, whi = -1;
+  uint32_t n_win = 0;
+  auto flush = [&]() {
+    if (whi >= wlo) put_candidate(P.cands, P.cand_cap, P.counters, pr.f, pr.r, wlo, whi);
+    whi = -1;
+  };
+  nfa_lane<W>(P.arena, s0, b, P.nfa + rg.nfa_off, [&](uint64_t abs) -> bool {
+    if (abs < a) return true;  // the previous task's accept
+    const int64_t e = int64_t(abs + 1 - fs);  // the match ends before e
+    const int64_t lo = e - int64_t(rg.max_len) > 0 ? e - int64_t(rg.max_len) : 0;
+    const int64_t hi = e - int64_t(rg.min_len) < len ? e - int64_t(rg.min_len) : len;
+    if (whi >= wlo && lo <= whi + 1 && hi + 1 >= wlo) {
+      whi = hi > whi ? hi : whi;
+      wlo = lo < wlo ? lo : wlo;
+      return true;
+    }
+    flush();
+    wlo = lo;
+    if (++n_win > kFsLaneWins) {  // many windows: every start up to the task's end
+      whi = int64_t(b - fs);
+      return false;
+    }
+    whi = hi;
+    return true;
+  });
+  flush();
+}
+
+__global__ __launch_bounds__(256) void fs_task_kernel(NfaParams P, FsLists Q) {
+  uint32_t n[4], total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    n[w] = Q.ctr[1 + w] < Q.task_cap ? Q.ctr[1 + w] : Q.task_cap;
+    total += n[w];
+  }
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    uint32_t w = 0, i = t;  // list w holds task t (t < total)
+    if (i >= n[0]) {
+      i -= n[0];
+      w = 1;
+      if (i >= n[1]) {
+        i -= n[1];
+        w = 2;
+        if (i >= n[2]) {
+          i -= n[2];
+          w = 3;
         }
       }
-      if (acc && lane == 0) put_candidate(P.cands, P.cand_cap, P.counters, pf, pr, 0, int64_t(len));
-      if (lane == 0) atomicAdd(&P.counters[13], 1u);  // pairs scanned (stats)
     }
+    const FsTask tk = Q.tasks[uint64_t(w) * Q.task_cap + i];
+    const FsPair pr = Q.pairs[tk.pair];
+    switch (w) {  // uniform except where a wave straddles two lists
+      case 0: fs_lane_task<1>(P, pr, tk.chunk); break;
+      case 1: fs_lane_task<2>(P, pr, tk.chunk); break;
+      case 2: fs_lane_task<3>(P, pr, tk.chunk); break;
+      default: fs_lane_task<4>(P, pr, tk.chunk); break;
+    }
+  }
+}
+
+// Unbounded rules (and bounds too long for a lane): one wave per pair.
+__global__ __launch_bounds__(256) void fs_wave_kernel(NfaParams P, FsLists Q) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n_waves = gridDim.x * (blockDim.x / 64);
+  const uint32_t n = Q.ctr[5] < Q.pair_cap ? Q.ctr[5] : Q.pair_cap;
+  for (uint32_t k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < n; k += n_waves) {
+    const FsPair pr = Q.pairs[Q.wave_pairs[k]];
+    const RuleGpu rg = P.rules[pr.r];
+    const uint64_t fs = P.off[pr.f], len = P.off[pr.f + 1] - fs;
+    const uint64_t* tab = P.nfa + rg.nfa_off;
+    bool acc;
+    switch (rg.nfa_words) {
+      case 1: acc = fullscan_pair<1>(P, P.arena, pr.f, pr.r, fs, len, tab, rg, lane); break;
+      case 2: acc = fullscan_pair<2>(P, P.arena, pr.f, pr.r, fs, len, tab, rg, lane); break;
+      case 3: acc = fullscan_pair<3>(P, P.arena, pr.f, pr.r, fs, len, tab, rg, lane); break;
+      default: acc = fullscan_pair<4>(P, P.arena, pr.f, pr.r, fs, len, tab, rg, lane); break;
+    }
+    if (acc && lane == 0) put_candidate(P.cands, P.cand_cap, P.counters, pr.f, pr.r, 0, int64_t(len));
   }
 }
 
@@ -1748,6 +1947,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   if (const char* di = std::getenv("TSG_DIAG_ITEMS")) item_diag_path_ = di;
   if (const char* fc = std::getenv("TSG_FULLSCAN_CHUNK")) fs_chunk_ = uint32_t(std::atoi(fc));
   if (fs_chunk_ < 64) fs_chunk_ = 64;
+  if (const char* tb = std::getenv("TSG_FS_TASK_BYTES")) fs_task_bytes_ = uint32_t(std::max(16, std::atoi(tb)));
   hipEventCreate(&ev_fs_);
   // the kernels of one scan run ~10 ms: a thread spinning on the stream for
   // that long takes a core from the host pool scanning the previous batch
@@ -1760,13 +1960,17 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
   for (uint32_t r = 0; r < n_rules_; r++)
     if (cr.rules[r].has_regex && !cr.rules[r].anchored) fullscan_rules_.push_back(r);
   n_fullscan_rules_ = uint32_t(fullscan_rules_.size());
+  if (cr.anchors.size() >= (size_t(1) << kHitAidBits)) {  // hit records keep the anchor id in 24 bits
+    err_ = "too many anchors for the hit records (>= 2^24)";
+    return;
+  }
   if (!Upload(&err_, &d_anchors_, cr.anchors.data(), cr.anchors.size()) ||
       !Upload(&err_, &d_rules_, cr.rules.data(), cr.rules.size()) ||
       !Upload(&err_, &d_rule_kw_, cr.rule_kw.data(), cr.rule_kw.size()) ||
       !Upload(&err_, &d_nfa_, cr.nfa.data(), cr.nfa.size()) ||
       !Upload(&err_, &d_fullscan_rules_, fullscan_rules_.data(), fullscan_rules_.size()))
     return;
-  if (hipMalloc(&d_counters_, 64) != hipSuccess) {
+  if (hipMalloc(&d_counters_, 64) != hipSuccess || hipMalloc(&d_fs_ctr_, 64) != hipSuccess) {
     err_ = "hipMalloc counters";
     return;
   }
@@ -2018,7 +2222,7 @@ GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
   void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
-                d_flags_, d_hits_, d_cands_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1],
+                d_flags_, d_hits_, d_cands_, d_fs_pairs_, d_fs_tasks_, d_fs_wave_, d_fs_ctr_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1],
                 d_kind_[0], d_kind_[1], d_xlen_, d_xoff_, d_xscan_, d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
   for (void* p : ps)
     if (p) hipFree(p);
@@ -2309,6 +2513,8 @@ void GpuEngine::InitCaps(uint64_t n_bytes) {
   if (cand_cap_ == 0) cand_cap_ = 1 << 16;
   if (rec_cap_ == 0) rec_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(n_bytes / 128, 1 << 16), 1u << 30));
   if (fold_cap_ == 0) fold_cap_ = 1 << 16;
+  if (fs_pair_cap_ == 0) fs_pair_cap_ = 1 << 14;
+  if (fs_task_cap_ == 0) fs_task_cap_ = 1 << 16;
 }
 
 bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
@@ -2403,7 +2609,7 @@ bool GpuEngine::Collect(Ticket* t, std::vector<Candidate>* cands, BatchStats* st
   const uint32_t* cnt = S.h_cnt;
   for (uint32_t seen = cand_recent_.load(); cnt[1] > seen && !cand_recent_.compare_exchange_weak(seen, cnt[1]);) {
   }
-  if (cnt[8] || cnt[10] || cnt[3] || cnt[4] || cnt[1] > t->cand_copy) {  // an overflow: Run grows and rescans
+  if (cnt[8] || cnt[10] || cnt[3] || cnt[4] || cnt[6] || cnt[1] > t->cand_copy) {  // an overflow: Run grows and rescans
     *rerun = true;
     release();
     return true;
@@ -2442,6 +2648,11 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
       !Ensure(&d_recs_, &cap_recs_, size_t(rec_cap_) * 4) ||
       !Ensure(&d_hits_, &cap_hits_, size_t(hit_cap_) * 12) ||
       !Ensure(&d_cands_, &cap_cands_, size_t(cand_cap_) * sizeof(Candidate)))
+    return false;
+  if (n_fullscan_rules_ > 0 &&
+      (!Ensure(&d_fs_pairs_, &cap_fs_pairs_, size_t(fs_pair_cap_) * sizeof(FsPair)) ||
+       !Ensure(&d_fs_wave_, &cap_fs_wave_, size_t(fs_pair_cap_) * 4) ||
+       !Ensure(&d_fs_tasks_, &cap_fs_tasks_, size_t(fs_task_cap_) * 4 * sizeof(FsTask))))
     return false;
   HIP_OK(hipEventRecord(ev[0], stream_));  // the GPU phase: clears, K0 .. finalize
   HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
@@ -2605,7 +2816,22 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   HIP_OK(hipGetLastError());
   if (np.n_fullscan_rules > 0) {
     HIP_OK(hipEventRecord(ev_fs, stream_));
-    fullscan_kernel<<<1024, 256, 0, stream_>>>(np);
+    FsLists fq;
+    fq.pairs = static_cast<FsPair*>(d_fs_pairs_);
+    fq.pair_cap = fs_pair_cap_;
+    fq.tasks = static_cast<FsTask*>(d_fs_tasks_);
+    fq.task_cap = fs_task_cap_;
+    fq.wave_pairs = static_cast<uint32_t*>(d_fs_wave_);
+    fq.ctr = d_fs_ctr_;
+    fq.task_min = fs_task_bytes_;
+    HIP_OK(hipMemsetAsync(d_fs_ctr_, 0, 64, stream_));
+    const uint64_t pairs = uint64_t(n_files) * n_fullscan_rules_;
+    const uint32_t pb = uint32_t(std::min<uint64_t>(std::max<uint64_t>((pairs + 255) / 256, 1), 4096));
+    fs_pairs_kernel<<<pb, 256, 0, stream_>>>(np, fq);
+    HIP_OK(hipGetLastError());
+    fs_task_kernel<<<2048, 256, 0, stream_>>>(np, fq);
+    HIP_OK(hipGetLastError());
+    fs_wave_kernel<<<1024, 256, 0, stream_>>>(np, fq);
     HIP_OK(hipGetLastError());
   }
   HIP_OK(hipEventRecord(ev[5], stream_));
@@ -2650,6 +2876,15 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     }
     st->hit_overflow = cnt[3] != 0;
     st->cand_overflow = cnt[4] != 0;
+    if (cnt[6]) {  // full-scan pair / task list overflow: grow to the counts seen
+      uint32_t fc[16];
+      HIP_OK(hipMemcpy(fc, d_fs_ctr_, sizeof(fc), hipMemcpyDeviceToHost));
+      fs_pair_cap_ = std::max<uint32_t>(fs_pair_cap_, fc[0] + fc[0] / 4 + 1024);
+      const uint32_t mt = std::max(std::max(fc[1], fc[2]), std::max(fc[3], fc[4]));
+      fs_task_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(fs_task_cap_, uint64_t(mt) + mt / 4 + 1024),
+                                                 0x7FFFFFFFu / sizeof(FsTask) / 4));
+      continue;
+    }
     if (cnt[10]) {  // fold site list overflow
       fold_cap_ = uint32_t(std::min<uint64_t>(uint64_t(cnt[9]) + cnt[9] / 4 + 1024, 0xFFFFFFF0u / 16));
       continue;

@@ -95,7 +95,7 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t lane) {  // e
 // the transformed offsets; pass 2 recomputes the masks, packs the wave's
 // output in LDS at its global 16-B phase and writes aligned 16-B stores (byte
 // stores only at the tile's two ragged ends, which the neighbouring tiles
-// share).  Positions are 32-bit (a call covers < 4 GiB).
+// share).  Positions are 32-bit below 4 GiB per call, 64-bit above (Pos).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kXTile = 1024;
 
@@ -107,10 +107,15 @@ __global__ __launch_bounds__(kXThreads) void xf_chunk_map_kernel(const uint64_t*
   }
 }
 
+// Positions are Pos: uint32_t for calls under 4 GiB (the common case: fewer
+// registers), uint64_t for a lone file of 4 GiB or more (the reference reads
+// files of any size, analyzer/secret/secret.go:110-121).
+//
 // A lane's 16-B block of tile t (zeros past the end).
-__device__ __forceinline__ uint4 x_block(const uint8_t* raw, uint32_t n_bytes, uint32_t t, uint32_t lane,
+template <typename Pos>
+__device__ __forceinline__ uint4 x_block(const uint8_t* raw, Pos n_bytes, uint32_t t, uint32_t lane,
                                          uint32_t n_tiles) {
-  const uint32_t blk = t * kXTile + 16 * lane;
+  const Pos blk = Pos(t) * kXTile + 16 * lane;
   return t < n_tiles && blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
 }
 
@@ -123,7 +128,8 @@ struct XWindow {
   }
 };
 
-__device__ __forceinline__ XWindow x_window(const uint8_t* raw, uint32_t n_bytes, uint32_t blk, uint32_t lane,
+template <typename Pos>
+__device__ __forceinline__ XWindow x_window(const uint8_t* raw, Pos n_bytes, Pos blk, uint32_t lane,
                                             const uint4& v) {
   XWindow W;
   W.w[2] = v.x;
@@ -183,15 +189,16 @@ __device__ XMasks x_masks(const XWindow& W, uint32_t lo, uint32_t hi) {
 // ahead), so a lane finds the file holding its block and the files after it
 // without a chain of dependent global loads; files further on (a tile of more
 // than 64 tiny files) are read from global memory.
+template <typename Pos>
 struct XFiles {
   uint32_t tf;
-  const uint32_t* so;
+  const Pos* so;
   const uint8_t* sk;
   const uint64_t* off;
   const uint8_t* kind;
-  __device__ __forceinline__ uint32_t O(uint32_t g) const {
+  __device__ __forceinline__ Pos O(uint32_t g) const {
     const uint32_t d = g - tf;
-    return d < 65u ? so[d] : uint32_t(off[g]);
+    return d < 65u ? so[d] : Pos(off[g]);
   }
   __device__ __forceinline__ uint32_t K(uint32_t g) const {
     const uint32_t d = g - tf;
@@ -200,19 +207,23 @@ struct XFiles {
 };
 
 // Per lane: its slice of the file table of tile tf (loaded a tile ahead).
+template <typename Pos>
 struct XFileRegs {
-  uint32_t o, o64, k;
+  Pos o, o64;
+  uint32_t k;
 };
-__device__ __forceinline__ XFileRegs x_file_regs(const uint64_t* off, const uint8_t* kind, uint32_t n_files,
-                                                 uint32_t tf, uint32_t lane) {
-  XFileRegs r;
+template <typename Pos>
+__device__ __forceinline__ XFileRegs<Pos> x_file_regs(const uint64_t* off, const uint8_t* kind, uint32_t n_files,
+                                                      uint32_t tf, uint32_t lane) {
+  XFileRegs<Pos> r;
   const uint32_t g = tf + lane < n_files ? tf + lane : n_files;
-  r.o = uint32_t(off[g]);
-  r.o64 = uint32_t(off[tf + 64u < n_files ? tf + 64u : n_files]);
+  r.o = Pos(off[g]);
+  r.o64 = Pos(off[tf + 64u < n_files ? tf + 64u : n_files]);
   r.k = tf + lane < n_files ? uint32_t(kind[tf + lane]) : 0u;
   return r;
 }
-__device__ __forceinline__ void x_stage_files(uint32_t* so, uint8_t* sk, const XFileRegs& r, uint32_t lane) {
+template <typename Pos>
+__device__ __forceinline__ void x_stage_files(Pos* so, uint8_t* sk, const XFileRegs<Pos>& r, uint32_t lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous tile's reads are done
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -230,16 +241,16 @@ __device__ __forceinline__ void x_stage_files(uint32_t* so, uint8_t* sk, const X
 // 16 bytes (bit i = byte blk + i): the output is, in byte order, a '\n' for a
 // bit of the second mask, the byte for a bit of the first, a '\n' for a bit of
 // the third.  Returns the lane's output byte count.
-template <typename Start, typename Out>
-__device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const XFiles& T, uint32_t n_files, uint32_t blk,
+template <typename Pos, typename Start, typename Out>
+__device__ __forceinline__ uint32_t x_lane(Pos n_bytes, const XFiles<Pos>& T, uint32_t n_files, Pos blk,
                                            const XWindow& W, Start start, Out out) {
   // T.tf: chunk_file[] of the lane's tile, the file holding its first byte
   if (blk >= n_bytes) return 0;
-  const uint32_t bend = blk + 16 < n_bytes ? blk + 16 : n_bytes;
+  const Pos bend = blk + 16 < n_bytes ? blk + 16 : n_bytes;
   uint32_t f = T.tf;
-  uint32_t fs = T.O(f), fe = T.O(f + 1);
+  Pos fs = T.O(f), fe = T.O(f + 1);
   if (fs == blk)  // empty files at a tile's first byte come before the file the chunk map names
-    for (uint32_t g = f; g > 0 && uint32_t(T.off[g - 1]) == blk;) start(--g, 0u);
+    for (uint32_t g = f; g > 0 && Pos(T.off[g - 1]) == blk;) start(--g, 0u);
   while (fe <= blk && f + 1 < n_files) {  // the file holding blk (the chunk map names the tile's first)
     f++;
     fs = fe;
@@ -252,7 +263,7 @@ __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const XFiles& T, ui
   uint32_t cnt = 0;
   for (;;) {
     if (fs >= blk && fs < bend) start(f, cnt);
-    const uint32_t s = fs > blk ? fs - blk : 0u, e = (fe < bend ? fe : bend) - blk;  // the segment, block bits
+    const uint32_t s = fs > blk ? uint32_t(fs - blk) : 0u, e = uint32_t((fe < bend ? fe : bend) - blk);  // the segment, block bits
     if (s < e) {
       const uint32_t seg = ((1u << e) - 1u) & ~((1u << s) - 1u);
       const uint32_t k = T.K(f);
@@ -263,8 +274,8 @@ __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const XFiles& T, ui
         out(seg & ~cr, 0u, 0u);
         cnt += uint32_t(__popc(seg & ~cr));
       } else {
-        const uint32_t lo = fs + 8 > blk ? fs + 8 - blk : 0u;  // window bits of the file
-        const uint32_t hi = fe - blk + 8 < 32 ? fe - blk + 8 : 32u;
+        const uint32_t lo = fs + 8 > blk ? uint32_t(fs + 8 - blk) : 0u;  // window bits of the file
+        const uint32_t hi = fe - blk + 8 < 32 ? uint32_t(fe - blk + 8) : 32u;
         const XMasks m = x_masks(W, fs + 8 >= blk ? lo : 0u, fe + 8 >= blk ? hi : 0u);
         const uint32_t K = (m.K >> 8) & seg, C = (m.C >> 8) & seg, Z = (m.Z >> 8) & seg;
         out(K, C, Z);
@@ -279,33 +290,34 @@ __device__ __forceinline__ uint32_t x_lane(uint32_t n_bytes, const XFiles& T, ui
   return cnt;
 }
 
-__global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __restrict__ raw, uint32_t n_bytes,
+template <typename Pos>
+__global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __restrict__ raw, Pos n_bytes,
                                                              const uint64_t* __restrict__ off,
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
                                                              uint32_t* __restrict__ tile_cnt,
                                                              uint32_t* __restrict__ fstart) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
   const uint32_t waves = gridDim.x * (kXThreads / 64);
   // a wave walks tiles t, t + waves, ...: the next tile's block and chunk-map
   // entry are loaded while this one is processed (the per-tile chain of
   // dependent loads, not bytes, bounds these kernels)
-  __shared__ uint32_t s_fo[kXThreads / 64][65];
+  __shared__ Pos s_fo[kXThreads / 64][65];
   __shared__ uint8_t s_fk[kXThreads / 64][64];
-  uint32_t* so = s_fo[threadIdx.x >> 6];
+  Pos* so = s_fo[threadIdx.x >> 6];
   uint8_t* sk = s_fk[threadIdx.x >> 6];
   uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
   uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
   uint32_t tf = t < n_tiles ? chunk_file[t] : 0u;
-  XFileRegs fr = x_file_regs(off, kind, n_files, tf, lane);
+  XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
   for (; t < n_tiles; t += waves) {
-    const uint32_t blk = t * kXTile + 16 * lane;
+    const Pos blk = Pos(t) * kXTile + 16 * lane;
     x_stage_files(so, sk, fr, lane);
-    const XFiles T{tf, so, sk, off, kind};
+    const XFiles<Pos> T{tf, so, sk, off, kind};
     const uint4 vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
     const uint32_t tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
-    const XFileRegs frn = t + waves < n_tiles ? x_file_regs(off, kind, n_files, tfn, lane) : fr;
+    const XFileRegs<Pos> frn = t + waves < n_tiles ? x_file_regs<Pos>(off, kind, n_files, tfn, lane) : fr;
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // file starts: tile-relative output offsets once the lane's prefix is known
     uint32_t sf[4], sc[4], ns = 0;
@@ -334,17 +346,18 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
 }
 
 __global__ __launch_bounds__(kXThreads) void xf_fixup_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
-                                                             uint32_t n_bytes, const uint64_t* __restrict__ tile_pre,
+                                                             uint64_t n_bytes, const uint64_t* __restrict__ tile_pre,
                                                              const uint32_t* __restrict__ fstart,
                                                              uint64_t* __restrict__ xoff) {
-  const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_files; f += gridDim.x * blockDim.x) {
     const uint64_t s = f < n_files ? off[f] : n_bytes;
     xoff[f] = s < n_bytes ? tile_pre[s / kXTile] + fstart[f] : tile_pre[n_tiles];
   }
 }
 
-__global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __restrict__ raw, uint32_t n_bytes,
+template <typename Pos>
+__global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __restrict__ raw, Pos n_bytes,
                                                              const uint64_t* __restrict__ off,
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
@@ -355,28 +368,28 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kXThreads / 64][kStage];
   const uint32_t lane = threadIdx.x & 63u;
   uint8_t* S = s_out[threadIdx.x >> 6];
-  const uint32_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
   const uint32_t waves = gridDim.x * (kXThreads / 64);
-  __shared__ uint32_t s_fo[kXThreads / 64][65];
+  __shared__ Pos s_fo[kXThreads / 64][65];
   __shared__ uint8_t s_fk[kXThreads / 64][64];
-  uint32_t* so = s_fo[threadIdx.x >> 6];
+  Pos* so = s_fo[threadIdx.x >> 6];
   uint8_t* sk = s_fk[threadIdx.x >> 6];
   uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
   uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);  // the next tile's inputs, a tile ahead
   uint32_t tfn = t < n_tiles ? chunk_file[t] : 0u;
   uint64_t pren = t < n_tiles ? tile_pre[t] : 0u;
-  XFileRegs frn = x_file_regs(off, kind, n_files, tfn, lane);
+  XFileRegs<Pos> frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
   for (; t < n_tiles; t += waves) {
-    const uint32_t blk = t * kXTile + 16 * lane;
+    const Pos blk = Pos(t) * kXTile + 16 * lane;
     const uint4 v = vn;
     const uint32_t tf = tfn;
     const uint64_t start = pren;
     x_stage_files(so, sk, frn, lane);
-    const XFiles T{tf, so, sk, off, kind};
+    const XFiles<Pos> T{tf, so, sk, off, kind};
     vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
     tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
     pren = t + waves < n_tiles ? tile_pre[t + waves] : 0u;
-    if (t + waves < n_tiles) frn = x_file_regs(off, kind, n_files, tfn, lane);
+    if (t + waves < n_tiles) frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
     uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0, added = 0;
@@ -422,7 +435,7 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
         for (uint32_t j = phase; j < 16; j++) out[g + j] = uint8_t(o[j >> 2] >> (8 * (j & 3)));
       }
       if (lane == 0 && phase) {  // the last `phase` bytes spill into block 64
-        const uint8_t* src = raw + t * kXTile + kXTile - phase;
+        const uint8_t* src = raw + uint64_t(t) * kXTile + kXTile - phase;
         for (uint32_t j = 0; j < phase; j++) out[base + kXTile + j] = src[j];
       }
       continue;
@@ -509,7 +522,7 @@ size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files) { return ScratchLay
 
 hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                      void* scratch, uint64_t* xoff, hipStream_t s) {
-  if (n_bytes >= (uint64_t(1) << 32) - 64) return hipErrorInvalidValue;  // 32-bit positions
+  const bool wide = n_bytes >= (uint64_t(1) << 32) - 64;  // 64-bit positions (a lone file of >= 4 GiB)
   const XformScratch L = ScratchLayout(n_bytes, n_files);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* chunk_file = reinterpret_cast<uint32_t*>(sc + L.chunk_file);
@@ -525,14 +538,17 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   }
   if (n_tiles) {
     const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
-    xf_count_kernel<<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file, tile_cnt, fstart);
+    if (wide)
+      xf_count_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart);
+    else
+      xf_count_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file, tile_cnt,
+                                                        fstart);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   size_t sb = L.scan_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(sc + L.scan, sb, tile_cnt, tile_pre, int(n_tiles) + 1, s)) != hipSuccess)
     return e;
-  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, uint32_t(n_bytes), tile_pre, fstart,
-                                                                       xoff);
+  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, n_bytes, tile_pre, fstart, xoff);
   return hipGetLastError();
 }
 
@@ -543,9 +559,12 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   if (!n_tiles) return hipSuccess;
   const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
-  xf_write_kernel<<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files,
-                                          reinterpret_cast<const uint32_t*>(sc + L.chunk_file),
-                                          reinterpret_cast<const uint64_t*>(sc + L.tile_pre), out);
+  const uint32_t* cf = reinterpret_cast<const uint32_t*>(sc + L.chunk_file);
+  const uint64_t* tp = reinterpret_cast<const uint64_t*>(sc + L.tile_pre);
+  if (n_bytes >= (uint64_t(1) << 32) - 64)
+    xf_write_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, cf, tp, out);
+  else
+    xf_write_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, cf, tp, out);
   return hipGetLastError();
 }
 
