@@ -55,42 +55,6 @@ def _cpu_sample_worker(args):
     return nb, nf, res
 
 
-def _cpu_layer_worker(args):
-    k, cores, layer_path = args
-    from oracle import analyzer as oan
-    data = open(layer_path, "rb").read()
-    a = oan.SecretAnalyzer("")
-    files, _, _ = oan.walk_layer_tar(data)
-    nb = nf = 0
-    for i, (fp, size, content) in enumerate(files):
-        if i % cores != k or not a.required(fp, size):
-            continue
-        r = a.analyze(fp, "", content)
-        if a.prepare(fp, "", content) is not None:
-            nb += size
-        nf += len(r["Secrets"][0]["Findings"]) if r else 0
-    return nb, nf
-
-
-def cpu_baseline_layer(layer, cores, tmpdir):
-    """Oracle analyzer (walk + Required + Analyze, 'port' of the reference CPU path) on a layer sample."""
-    import multiprocessing as mp
-    lp = os.path.join(tmpdir, "cpu_layer.tar")
-    layer.tofile(lp)
-    ctx = mp.get_context("spawn")
-    t0 = time.time()
-    with ctx.Pool(cores) as pool:
-        res = pool.map(_cpu_layer_worker, [(k, cores, lp) for k in range(cores)])
-    dt = time.time() - t0
-    os.remove(lp)
-    nb = sum(r[0] for r in res)
-    nf = sum(r[1] for r in res)
-    return {"value": round(nb / dt / 1e9, 6), "unit": "GB/s", "cores": cores, "kind": "port",
-            "sample": "a %.1f MB layer of the same generator (its first files), oracle/analyzer.py (tarfile walk + "
-                      "Required + Analyze restated) in %d processes; %.1f MB of files analyzed; %d findings; "
-                      "%.1f s wall" % (layer.size / 1e6, cores, nb / 1e6, nf, dt)}
-
-
 def _first_files(C, sample_bytes):
     n = 0
     while n < C.n_files and int(C.offsets[n + 1]) <= sample_bytes:
@@ -260,7 +224,7 @@ WORKLOADS = {
              "FS.Walk + Required + reads straight into double-buffered pinned arenas + GPU pre-transform + scan "
              "(BASELINE configs[0] end to end on the GPU; SURVEY §8(f)1)", 1.0, 1000.0, 0.0),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
-           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 24.0, 0.0),
+           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 120.0, 0.0),
 }
 
 
@@ -281,20 +245,77 @@ def write_tree(C, root):
             f.write(C.arena[int(C.offsets[i]):int(C.offsets[i + 1])])
 
 
+def _cpuref_prepared(rels, datas, bins, threads):
+    """tsg_cpuref_scan (the restated reference CPU scan, C++) over prepared ScanArgs -- paths,
+    transformed contents, Binary flags -- once per entry of `threads`; returns (runs, the first
+    run's ScanResult)."""
+    import ctypes as c
+    import numpy as np
+    from oracle import hostlib
+    import trivy_amd.secret as secret
+    from trivy_amd.secret.scanner import ScanResult, _CBatch, _CStats
+    offs = np.zeros(len(datas) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in datas])
+    arena = np.frombuffer(b"".join(datas) + b"\0" * 64, dtype=np.uint8)
+    pb = [r.encode("utf-8", "surrogateescape") for r in rels]
+    parr = (c.c_char_p * max(1, len(pb)))(*pb)
+    plen = np.array([len(x) for x in pb], dtype=np.uint64)
+    barr = np.array(bins, dtype=np.uint8) if bins is not None else None
+    L = hostlib.lib()
+    sc = secret.NewScanner(None, lib=L, host_only=True)
+    batch = _CBatch(len(datas), arena.ctypes.data, offs.ctypes.data, None, None, c.cast(parr, c.c_void_p).value,
+                    plen.ctypes.data, barr.ctypes.data if barr is not None else None)
+    runs, res = [], None
+    for T in threads:
+        h = c.c_void_p()
+        t0 = time.time()
+        if L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), int(T), c.byref(h)) != 0:
+            raise RuntimeError(hostlib.last_error())
+        dt = time.time() - t0
+        st = _CStats()
+        L.tsg_result_stats(h, c.byref(st))
+        runs.append({"threads": int(T), "scan_s": round(dt, 3), "findings": int(st.findings)})
+        if res is None:
+            res = ScanResult(sc, h)
+        else:
+            L.tsg_result_free(h)
+    return runs, res
+
+
+def _diff_secrets(got, res, rels):
+    """GPU AnalysisResult secrets vs the restated reference's, in AnalysisResult.Sort order."""
+    want = [s for s in res.secrets(rels) if s.Findings]
+    want.sort(key=lambda s: s.FilePath.encode("utf-8", "surrogateescape"))
+    for s_ in want:
+        s_.Findings.sort(key=lambda f: (f.RuleID.encode(), f.StartLine))
+    got = sorted(got, key=lambda s: s.FilePath.encode("utf-8", "surrogateescape"))
+    for s_ in got:
+        s_.Findings.sort(key=lambda f: (f.RuleID.encode(), f.StartLine))
+    bad = sum(1 for x, y in zip(got, want) if x.to_dict() != y.to_dict()) + abs(len(got) - len(want))
+    return {"files": len(rels), "secrets": len(want), "findings": sum(len(s.Findings) for s in want),
+            "mismatches": bad}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
 def cpu_baseline_fs(root, cores, gpu_result=None):
     """The same tree through the reference's CPU path, restated: FS.Walk + Required in Python
     (oracle/analyzer.py walk_fs / required, os.scandir order), each file read and CR-stripped,
-    then tsg_cpuref_scan (the restated reference CPU scan, C++) on `cores` threads; end to end
-    GB/s of the files analyzed.  With gpu_result (AnalyzeFS's sorted secrets), every file's
-    findings are compared with it."""
-    import ctypes as c
-    import numpy as np
-    from oracle import analyzer as oan, hostlib
-    import trivy_amd.secret as secret
-    from trivy_amd.secret.scanner import ScanResult, _CBatch
+    then tsg_cpuref_scan (the restated reference CPU scan, C++) on `cores` threads and on 5
+    (--parallel's default); end to end GB/s of the files analyzed.  With gpu_result
+    (AnalyzeFS's secrets), every file's findings are compared with it."""
+    from oracle import analyzer as oan
     t0 = time.time()
     a = oan.SecretAnalyzer("")
-    rels, datas, nbytes = [], [], 0
+    rels, datas, bins, nbytes = [], [], [], 0
     for rel, size in oan.walk_fs(root):
         if not a.required(rel, size):
             continue
@@ -305,36 +326,56 @@ def cpu_baseline_fs(root, cores, gpu_result=None):
             continue
         rels.append(args[0])
         datas.append(args[1])
+        bins.append(args[2])
         nbytes += len(b)
-    offs = np.zeros(len(datas) + 1, dtype=np.uint64)
-    offs[1:] = np.cumsum([len(x) for x in datas])
-    arena = np.frombuffer(b"".join(datas) + b"\0" * 64, dtype=np.uint8)
-    pb = [r.encode("utf-8", "surrogateescape") for r in rels]
-    parr = (c.c_char_p * max(1, len(pb)))(*pb)
-    plen = np.array([len(x) for x in pb], dtype=np.uint64)
     t_walk = time.time() - t0
-    L = hostlib.lib()
-    sc = secret.NewScanner(None, lib=L, host_only=True)
-    batch = _CBatch(len(datas), arena.ctypes.data, offs.ctypes.data, None, None, c.cast(parr, c.c_void_p).value,
-                    plen.ctypes.data, None)
-    h = c.c_void_p()
-    if L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), int(cores), c.byref(h)) != 0:
-        raise RuntimeError(hostlib.last_error())
-    dt = time.time() - t0
-    res = ScanResult(sc, h)
-    out = {"value": round(nbytes / dt / 1e9, 6), "unit": "GB/s", "cores": cores,
+    runs, res = _cpuref_prepared(rels, datas, bins, [cores, 5])
+    for r in runs:
+        r["value"] = round(nbytes / (t_walk + r["scan_s"]) / 1e9, 6)
+    out = {"value": runs[0]["value"], "unit": "GB/s", "cores": cores,
            "kind": "port (restated reference CPU path: Python FS.Walk + Required + ReadAll/CR strip, "
                    "C++ tsg_cpuref_scan)",
-           "sample": "the whole %.1f MB tree (%d files analyzed): walk+read %.1f s, scan %.1f s"
-                     % (nbytes / 1e6, len(datas), t_walk, dt - t_walk)}
+           "sample": "the whole %.1f MB tree (%d files analyzed): walk+read %.1f s, scan %.1f s on %d threads"
+                     % (nbytes / 1e6, len(datas), t_walk, runs[0]["scan_s"], cores),
+           "runs": runs, "cpu_model": _cpu_model()}
     if gpu_result is not None:
-        want = [s for s in res.secrets(rels) if s.Findings]
-        want.sort(key=lambda s: s.FilePath.encode("utf-8", "surrogateescape"))
-        for s_ in want:
-            s_.Findings.sort(key=lambda f: (f.RuleID.encode(), f.StartLine))
-        got = gpu_result.Secrets
-        bad = sum(1 for x, y in zip(got, want) if x.to_dict() != y.to_dict()) + abs(len(got) - len(want))
-        out["gpu_vs_cpuref_all_files"] = {"files": len(datas), "secrets": len(want), "mismatches": bad}
+        out["gpu_vs_cpuref_all_files"] = _diff_secrets(gpu_result.Secrets, res, rels)
+    return out
+
+
+def cpu_baseline_layer_cpp(layer, cores, gpu_result=None):
+    """A layer sample through the reference's CPU path, restated: LayerTar.Walk + Required +
+    ReadAll / CR strip / ExtractPrintableBytes in Python (oracle/analyzer.py walk_layer_tar,
+    tarfile), then tsg_cpuref_scan (C++) on `cores` threads and on 5; GB/s of the files
+    analyzed.  With gpu_result (AnalyzeLayer over the same sample), every file compared."""
+    from oracle import analyzer as oan
+    t0 = time.time()
+    files, _, _ = oan.walk_layer_tar(layer.tobytes())
+    a = oan.SecretAnalyzer("")
+    rels, datas, bins, nbytes = [], [], [], 0
+    for fp, size, content in files:
+        if not a.required(fp, size):
+            continue
+        args = a.prepare(fp, "", content)
+        if args is None:
+            continue
+        rels.append(args[0])
+        datas.append(args[1])
+        bins.append(args[2])
+        nbytes += size
+    t_walk = time.time() - t0
+    runs, res = _cpuref_prepared(rels, datas, bins, [cores, 5])
+    for r in runs:
+        r["value"] = round(nbytes / (t_walk + r["scan_s"]) / 1e9, 6)
+    out = {"value": runs[0]["value"], "unit": "GB/s", "cores": cores,
+           "kind": "port (restated reference CPU path: Python LayerTar.Walk + Required + transforms, "
+                   "C++ tsg_cpuref_scan)",
+           "sample": "a %.1f MB layer of the same generator (%d files analyzed, %.1f MB): walk+read %.1f s, "
+                     "scan %.1f s on %d threads" % (layer.size / 1e6, len(datas), nbytes / 1e6, t_walk,
+                                                    runs[0]["scan_s"], cores),
+           "runs": runs, "cpu_model": _cpu_model()}
+    if gpu_result is not None:
+        out["gpu_vs_cpuref_all_files"] = _diff_secrets(gpu_result.Secrets, res, rels)
     return out
 
 
@@ -771,7 +812,9 @@ def main():
                 cpu = cpu_baseline_fs(layer, cores, gpu_result=res_fs)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
-                cpu = cpu_baseline_layer(sample, cores, tmpdir)
+                res_l = an.AnalyzeLayer(sample, colls=[Collector(an, args.arena_mb << 20, gx)
+                                                       for _ in range(args.collectors)])
+                cpu = cpu_baseline_layer_cpp(sample, cores, gpu_result=res_l)
         out = {
             "metric": "GB/s secret-scanned (whole node) at 1/2/4/8 MI355X; findings bit-exact vs CPU",
             "value": round(value, 3),
@@ -808,7 +851,7 @@ def main():
         full = (cpu or {}).get("gpu_vs_cpuref_all_files")
         if full and full["mismatches"]:
             sys.exit("parity: %d of %d files of the CPU-baseline sample differ from the restated reference "
-                     "(first: %s)" % (full["mismatches"], full["files"], full["first_mismatch"]))
+                     "(first: %s)" % (full["mismatches"], full["files"], full.get("first_mismatch")))
         if parity is not None and parity["mismatches"]:
             sys.exit("parity: %d of %d sample files differ from the oracle (first: %s)"
                      % (parity["mismatches"], parity["files"], parity["first_mismatch"]))

@@ -136,7 +136,8 @@ uint64_t tsg_result_records(const tsg_result* r, tsg_record* out, uint64_t cap);
 
 /* Whole batch as JSON ([{"kind":..,"findings":[..]}...], Go field names). */
 int tsg_result_json(const tsg_result* r, const char** json, uint64_t* len);
-/* Files [lo, hi) only (same format; the text stays valid until the next json call on r). */
+/* Files [lo, hi) only (same format; the text stays valid until the next range call on r; the
+   whole-result text of tsg_result_json is kept apart). */
 int tsg_result_json_range(const tsg_result* r, uint32_t lo, uint32_t hi, const char** json, uint64_t* len);
 
 /* Timings / counters of the batch (GPU ms from HIP events on the engine stream). */

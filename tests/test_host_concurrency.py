@@ -138,3 +138,19 @@ def test_pool_budget_follows_affinity_and_ranks():
         half = set(allc[:online // 2])
         assert _budget(half, LOCAL_WORLD_SIZE="8") == want(online // 2, max(1, 8 * (online // 2) / online), 8)
     assert _budget({allc[0]}) == 1
+
+
+def test_result_json_range_then_whole():
+    """tsg_result_json_range keeps its own buffer: a range read first must not become what
+    tsg_result_json returns for the whole batch (a bench/test full_diff followed by secrets())."""
+    L = hostlib.lib()
+    sc = NewScanner(None, lib=L, host_only=True)
+    files = [(p, b.replace(b"\r", b"")) for p, b in make_corpus(61, 200)]
+    keep, batch = _batch(files)
+    h = c.c_void_p()
+    assert L.tsg_cpuref_scan(c.byref(sc._cg.g), c.byref(batch), 4, c.byref(h)) == 0
+    r = ScanResult(sc, h)
+    tail = r.raw(150, 200)
+    whole = r.raw()
+    assert len(whole) == len(files) and whole[150:200] == tail
+    assert r.raw(0, 10) == whole[:10] and r.raw() == whole

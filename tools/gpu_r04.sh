@@ -42,6 +42,17 @@ for st in $STAGES; do
       timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace -d $R/gpurun_out/ingprof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --warmup-s 0 --no-cpu-baseline --ingest-steps 3 > $R/gpurun_out/ingprof_bench_$TAG.json 2> $R/gpurun_out/ingprof_$TAG.err
       rc=$?; cd $R; tail -2 gpurun_out/ingprof_$TAG.err; [ $rc -eq 0 ] || exit $rc
       python tools/bench_brief.py gpurun_out/ingprof_bench_$TAG.json ;;
+    ab)  # C2 A/B of library variants (VARIANTS="base pf ..."; base = the in-tree build), twice interleaved
+      for rep in 1 2; do
+        for v in ${VARIANTS:-base}; do
+          if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
+          TSG_LIB=$L timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > gpurun_out/ab_${TAG}_${v}_$rep.json 2> gpurun_out/ab_${TAG}_${v}_$rep.err
+          rc=$?; echo "== $v $rep"; python tools/bench_brief.py gpurun_out/ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
+    dump)  # candidates of one C3f scan for tools/host_tail_bench.py (CPU profiling of the exact pass)
+      TSG_TAIL_DEBUG=1 TSG_DUMP_CANDS=$R/gpurun_out/cands_${DUMP_WL:-c3f}.bin timeout -k 10 600 python bench.py --workload ${DUMP_WL:-c3f} --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dump_$TAG.json 2> gpurun_out/dump_$TAG.err
+      rc=$?; ls -la gpurun_out/cands_${DUMP_WL:-c3f}.bin; grep -a "tail" gpurun_out/dump_$TAG.err | tail -4; [ $rc -eq 0 ] || exit $rc ;;
     wl)
       for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
         timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err

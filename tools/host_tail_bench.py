@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rec", type=int, default=64, help="record size of the dump (40 / 48: older builds)")
     ap.add_argument("--hints", action="store_true", help="fill Candidate::nl_back on the host first")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3f"],
+                    help="corpus / rules of the dump (bench.py --workload; rank 0 seed)")
     args = ap.parse_args()
     from oracle import hostlib
     L = hostlib.lib()
@@ -39,7 +41,18 @@ def main():
             cand = cand.reshape(-1)
     n_c = len(cand) // 64
     t = time.time()
-    C = corpus.generate(int(args.gb * 1e9))
+    rules = builtin_rules()
+    if args.workload == "c2":
+        C = corpus.generate(int(args.gb * 1e9))
+    else:
+        import tempfile
+        from trivy_amd.secret import ParseConfig
+        y, samples = corpus.c3_rules(fullscan_share=0.05 if args.workload == "c3f" else 0.0)
+        with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
+            f.write(y)
+        rules = rules + list(ParseConfig(f.name).CustomRules)
+        os.remove(f.name)
+        C = corpus.generate_c3(int(args.gb * 1e9), samples, seed=corpus.SEED)
     if args.hints:  # fill nl_back as the finalize kernel does (last three '\n' before wlo)
         rec = cand.reshape(-1, 64)
         file = rec[:, 0:4].copy().view(np.uint32).ravel()
@@ -65,7 +78,7 @@ def main():
         rec[:, 48:60] = fwd.view(np.uint8).reshape(-1, 12)
         print("hints filled %.1f s" % (time.time() - t), flush=True)
     print("corpus %.1f s, %d files, %d candidates" % (time.time() - t, C.n_files, n_c), flush=True)
-    cg = CGlobal(builtin_rules(), builtin_allow_rules(), [])
+    cg = CGlobal(rules, builtin_allow_rules(), [])
     b = _CBatch(C.n_files, C.arena.ctypes.data, C.offsets.ctypes.data, None, None, C.path_ptrs.ctypes.data,
                 None, None)
     sp = None

@@ -14,7 +14,8 @@ struct tsg_scanner {
 struct tsg_result {
   tsg::BatchResult files;
   tsg_stats stats;
-  std::string json;
+  std::string json;        // tsg_result_json: every file (built once)
+  std::string json_range;  // tsg_result_json_range: the last range asked for
   const tsg::SecretScanner* owner;
   std::unique_ptr<tsg::SecretScanner> owned;  // results of scanners made for one call (oracle hooks)
 };

@@ -427,10 +427,12 @@ int tsg_result_json(const tsg_result* rc, const char** json, uint64_t* len) {
 int tsg_result_json_range(const tsg_result* rc, uint32_t lo, uint32_t hi, const char** json, uint64_t* len) {
   tsg_result* r = const_cast<tsg_result*>(rc);
   if (lo > hi || hi > r->files.kind.size()) return -1;
-  r->json.clear();
-  ResultJson(r, lo, hi, &r->json);
-  *json = r->json.data();
-  *len = r->json.size();
+  // its own buffer: a range must not replace the whole-result JSON that
+  // tsg_result_json builds once and returns from then on
+  r->json_range.clear();
+  ResultJson(r, lo, hi, &r->json_range);
+  *json = r->json_range.data();
+  *len = r->json_range.size();
   return 0;
 }
 

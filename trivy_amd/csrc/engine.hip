@@ -735,6 +735,9 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
 #ifndef TSG_C_FSE
 #define TSG_C_FSE 0
 #endif
+#ifndef TSG_C_PREFETCH
+#define TSG_C_PREFETCH 0
+#endif
 constexpr bool kCFse = TSG_C_FSE;     // cache each block's file in LDS in phase A (-0.2 ms at equal occupancy; costs 20 B/lane)
 constexpr uint32_t kCQ1 = TSG_C_Q1;  // fires (overflow: handled in place)
 constexpr uint32_t kCQ2 = TSG_C_Q2;  // candidate items (overflow: checked in place)
@@ -957,23 +960,42 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     }
   };
   const uint32_t stride = gridDim.x * blockDim.x;
-  // the next iteration's record is loaded a batch ahead: one dependent global
-  // round trip (record -> window bytes -> file offsets) less per batch
-  uint32_t rec_next = blockIdx.x * blockDim.x + wave * 64 + lane < n_recs ? P.recs[blockIdx.x * blockDim.x + wave * 64 + lane]
-                                                                          : 0u;
+  // The records are loaded two batches ahead and their window bytes one batch
+  // ahead (TSG_C_PREFETCH): the gather of the next blocks' bytes is in flight
+  // while this batch's phases run, instead of one dependent global round trip
+  // (record -> window bytes) at the top of every batch.
+  auto load_win = [&](uint32_t rec, bool valid, uint4* dst) {
+    const uint64_t base = uint64_t(rec) * 16;
+    const uint64_t w0 = base >= 16 ? base - 16 : 0;
+#pragma unroll
+    for (int q = 0; q < kCWin / 16; q++)  // the arena holds 64 readable bytes past n_bytes
+      dst[q] = valid && w0 + 16 * q + 16 <= P.n_bytes + 64 ? load16(P.arena + w0 + 16 * q) : make_uint4(0, 0, 0, 0);
+  };
+  const uint32_t r_first = blockIdx.x * blockDim.x + wave * 64 + lane;
+  uint32_t rec_next = r_first < n_recs ? P.recs[r_first] : 0u;
+#if TSG_C_PREFETCH
+  uint4 dwn[kCWin / 16];
+  load_win(rec_next, r_first < n_recs, dwn);
+  uint32_t rec_nn = r_first + stride < n_recs ? P.recs[r_first + stride] : 0u;
+#endif
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave * 64; r0 < n_recs; r0 += stride) {
     // ---- A: one block per lane
     const uint32_t r = r0 + lane;
     const uint32_t rec = rec_next;
+    uint4 dw[kCWin / 16];
+#if TSG_C_PREFETCH
+#pragma unroll
+    for (int q = 0; q < kCWin / 16; q++) dw[q] = dwn[q];
+    rec_next = rec_nn;
+    load_win(rec_next, r + stride < n_recs, dwn);
+    rec_nn = r + 2 * stride < n_recs ? P.recs[r + 2 * stride] : 0u;
+#else
     rec_next = r + stride < n_recs ? P.recs[r + stride] : 0u;
+    load_win(rec, r < n_recs, dw);
+#endif
     uint32_t fire_e[4], n_fire = 0;
     if (r < n_recs) {
       const uint64_t base = uint64_t(rec) * 16;
-      const uint64_t w0 = base >= 16 ? base - 16 : 0;
-      uint4 dw[kCWin / 16];
-#pragma unroll
-      for (int q = 0; q < kCWin / 16; q++)  // the arena holds 64 readable bytes past n_bytes
-        dw[q] = w0 + 16 * q + 16 <= P.n_bytes + 64 ? load16(P.arena + w0 + 16 * q) : make_uint4(0, 0, 0, 0);
       const uint4 d0 = dw[0], d1 = dw[1];
       uint4* wl = reinterpret_cast<uint4*>(wwin + lane * kCWin);
 #pragma unroll
