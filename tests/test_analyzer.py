@@ -507,3 +507,14 @@ def test_gpu_xform_bytes_vs_oracle():
         assert got == want, (i, k, b[:80])
     assert int(xoff[-1]) == sum(len(b if k == 0 else b.replace(b"\r", b"") if k == 1 else
                                     oan.extract_printable_bytes(b)) for b, k in zip(files, kinds))
+
+
+@pytest.mark.gpu
+def test_gpu_xform_wide_positions_vs_oracle(monkeypatch):
+    """The 64-bit-position instantiation of the pre-transform kernels (used for a lone file of
+    4 GiB or more, test_gpu_large_file.py) forced on the small edge-case batches above
+    (TSG_XFORM_WIDE=1): byte for byte the same transforms."""
+    monkeypatch.setenv("TSG_XFORM_WIDE", "1")
+    test_gpu_xform_bytes_vs_oracle()
+    test_gpu_xform_identity_tiles_vs_oracle()
+    test_gpu_xform_empty_files_at_tile_starts()

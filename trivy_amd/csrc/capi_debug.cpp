@@ -66,8 +66,10 @@ int tsg_debug_xform(int device, const uint8_t* raw, uint64_t n_bytes, const uint
       ok(hipMemcpyAsync(xoff, d_xoff, (size_t(n_files) + 1) * 8, hipMemcpyDeviceToHost, s)) &&
       ok(hipStreamSynchronize(s)) && ok(hipMalloc(&d_out, xoff[n_files] + 64)) &&
       ok(tsg::XformWrite(static_cast<const uint8_t*>(d_raw), n_bytes, static_cast<const uint64_t*>(d_off),
-                         static_cast<const uint8_t*>(d_kind), n_files, d_sc, static_cast<uint8_t*>(d_out), s)) &&
-      ok(hipStreamSynchronize(s)))
+                         static_cast<const uint8_t*>(d_kind), n_files, d_sc, static_cast<uint8_t*>(d_out),
+                         xoff[n_files] + 64, s)) &&
+      ok(hipStreamSynchronize(s)) &&
+      ok(tsg::XformErrorWord(n_bytes, n_files, d_sc, s) == 0 ? hipSuccess : hipErrorIllegalAddress))
     ok(hipMemcpy(out, d_out, std::min<uint64_t>(out_cap, xoff[n_files]), hipMemcpyDeviceToHost));
   for (void* p : {d_raw, d_off, d_kind, d_xoff, d_out, d_sc})
     if (p) (void)hipFree(p);

@@ -203,12 +203,13 @@ class GpuEngine {
                                     // [6] full-scan list overflow [11] anchor-item matches [13] open pairs
   // host-batch streaming (RunHost): two staging buffers, a copy stream
   hipStream_t copy_stream_ = nullptr;
-  hipEvent_t ev_copied_[2] = {}, ev_h2d_[2] = {};
-  void* d_stage_[2] = {}; size_t cap_stage_[2] = {};
-  void* d_stage_off_[2] = {}; size_t cap_stage_off_[2] = {};
-  uint64_t* h_off_[2] = {}; size_t cap_h_off_[2] = {};  // pinned, rebased chunk offsets
+  static constexpr int kNStage = 3;  // staging buffers: the copier runs up to two chunks ahead
+  hipEvent_t ev_copied_[kNStage] = {}, ev_h2d_[2] = {};
+  void* d_stage_[kNStage] = {}; size_t cap_stage_[kNStage] = {};
+  void* d_stage_off_[kNStage] = {}; size_t cap_stage_off_[kNStage] = {};
+  uint64_t* h_off_[kNStage] = {}; size_t cap_h_off_[kNStage] = {};  // pinned, rebased chunk offsets
   // GPU pre-transform (xform.h): per-chunk kinds, lengths, transformed offsets and bytes, the gather
-  void* d_kind_[2] = {}; size_t cap_kind_[2] = {};
+  void* d_kind_[kNStage] = {}; size_t cap_kind_[kNStage] = {};
   void* d_xlen_ = nullptr; size_t cap_xlen_ = 0;
   void* d_xoff_ = nullptr; size_t cap_xoff_ = 0;
   void* d_xscan_ = nullptr; size_t cap_xscan_ = 0;

@@ -18,6 +18,8 @@
 //  K4 full-scan   : (file x unanchored rule) tasks: NFA with injection at
 //                   every byte; an accept makes the whole file a candidate.
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2244,10 +2246,13 @@ GpuEngine::~GpuEngine() {
   hipSetDevice(device_);
   void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
-                d_flags_, d_hits_, d_cands_, d_fs_pairs_, d_fs_tasks_, d_fs_wave_, d_fs_ctr_, d_stage_[0], d_stage_[1], d_stage_off_[0], d_stage_off_[1],
-                d_kind_[0], d_kind_[1], d_xlen_, d_xoff_, d_xscan_, d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
+                d_flags_, d_hits_, d_cands_, d_fs_pairs_, d_fs_tasks_, d_fs_wave_, d_fs_ctr_, d_xlen_, d_xoff_, d_xscan_,
+                d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
   for (void* p : ps)
     if (p) hipFree(p);
+  for (int b = 0; b < kNStage; b++)
+    for (void* p : {d_stage_[b], d_stage_off_[b], d_kind_[b]})
+      if (p) hipFree(p);
   for (auto& e : ev_)
     if (e) hipEventDestroy(e);
   for (auto& e : ev_copied_)
@@ -2332,7 +2337,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     max_bytes = std::max<uint64_t>(max_bytes, h_offsets[cut[k + 1]] - h_offsets[cut[k]]);
     max_files = std::max<uint64_t>(max_files, cut[k + 1] - cut[k]);
   }
-  for (int b = 0; b < 2 && b < int(n_chunks); b++) {
+  for (int b = 0; b < kNStage && b < int(n_chunks); b++) {
     if (!Ensure(&d_stage_[b], &cap_stage_[b], max_bytes + 64) ||
         !Ensure(&d_stage_off_[b], &cap_stage_off_[b], (max_files + 1) * 8) ||
         (kinds && !Ensure(&d_kind_[b], &cap_kind_[b], max_files + 1)))
@@ -2345,14 +2350,17 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
       cap_h_off_[b] = max_files + 1;
     }
   }
-  auto copy = [&](size_t k) -> bool {  // chunk k -> staging buffer k % 2, on the copy stream
+  auto copy = [&](size_t k) -> bool {  // chunk k -> staging buffer k % kNStage, on the copy stream
     if (hipSetDevice(device_) != hipSuccess) return false;
-    const int b = int(k % 2);
+    const int b = int(k % kNStage);
     const uint32_t f0 = cut[k], f1 = cut[k + 1];
     const uint64_t a = h_offsets[f0], e = h_offsets[f1];
     for (uint32_t f = f0; f <= f1; f++) h_off_[b][f - f0] = h_offsets[f] - a;
     uint8_t* d = static_cast<uint8_t*>(d_stage_[b]);
-    if (e > a) HIP_OK(hipMemcpyAsync(d, h_arena + a, e - a, hipMemcpyHostToDevice, copy_stream_));
+    // in pieces of at most 1 GiB (a lone file can make a chunk of many GiB)
+    for (uint64_t x = a; x < e; x += uint64_t(1) << 30)
+      HIP_OK(hipMemcpyAsync(d + (x - a), h_arena + x, std::min<uint64_t>(e - x, uint64_t(1) << 30),
+                            hipMemcpyHostToDevice, copy_stream_));
     HIP_OK(hipMemsetAsync(d + (e - a), 0, 64, copy_stream_));
     HIP_OK(hipMemcpyAsync(d_stage_off_[b], h_off_[b], (size_t(f1 - f0) + 1) * 8, hipMemcpyHostToDevice,
                           copy_stream_));
@@ -2362,25 +2370,68 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     return true;
   };
   HIP_OK(hipEventRecord(ev_h2d_[0], copy_stream_));
-  // copy(k) on the helper thread; joined before chunk k's kernels are queued
+  // One copier thread issues the chunk copies in order, each into the staging
+  // buffer chunk k - kNStage freed (this thread has scanned it: Run returns
+  // after the chunk's kernels).  It runs up to kNStage - 1 chunks ahead, so the
+  // copy engine keeps streaming while this thread transforms, scans and reads
+  // back a chunk -- and while it waits for CPU time behind other scans' host
+  // work.  (A 1-GiB hipMemcpyAsync from registered memory returns only at
+  // completion on this runtime, profiles/r02_ingest_trace_*: the copies are
+  // issued off this thread.)
+  std::mutex cm;
+  std::condition_variable cv;
+  size_t issued = 0, scanned = 0;  // chunks copied (issued + event recorded) / scanned (buffer free)
+  bool stop = false;
   std::string copy_err;
-  auto start_copy = [&](size_t k) {
-    return std::thread([&, k] {
-      if (!copy(k) && copy_err.empty()) copy_err = err_.empty() ? "chunk copy failed" : err_;
-    });
+  std::thread copier([&] {
+    for (size_t k = 0; k < n_chunks; k++) {
+      {
+        std::unique_lock<std::mutex> lk(cm);
+        cv.wait(lk, [&] { return stop || k < scanned + kNStage; });
+        if (stop) return;
+      }
+      // the previous use of h_off_[b] (chunk k - kNStage) is transferred: its event completed
+      if (k >= size_t(kNStage) && hipEventSynchronize(ev_copied_[k % kNStage]) != hipSuccess) {
+        std::lock_guard<std::mutex> g(cm);
+        copy_err = "staging event";
+        issued = n_chunks;
+        cv.notify_all();
+        return;
+      }
+      const bool ok = copy(k);
+      std::lock_guard<std::mutex> g(cm);
+      if (!ok) {
+        copy_err = err_.empty() ? "chunk copy failed" : err_;
+        issued = n_chunks;
+        cv.notify_all();
+        return;
+      }
+      issued = k + 1;
+      cv.notify_all();
+    }
+  });
+  auto finish = [&](bool ok) {
+    {
+      std::lock_guard<std::mutex> g(cm);
+      stop = true;
+    }
+    cv.notify_all();
+    copier.join();
+    if (!ok) (void)hipStreamSynchronize(copy_stream_);  // no copy into a staging buffer may outlive the call
+    return ok;
   };
-  std::thread copier = start_copy(0);
   std::vector<Candidate> part;
   for (size_t k = 0; k < n_chunks; k++) {
-    const int b = int(k % 2);
-    copier.join();  // chunk k's copy is queued (and its event recorded)
-    if (!copy_err.empty()) {
-      err_ = copy_err;
-      return false;
+    const int b = int(k % kNStage);
+    {
+      std::unique_lock<std::mutex> lk(cm);
+      cv.wait(lk, [&] { return issued > k; });
+      if (!copy_err.empty()) {
+        err_ = copy_err;
+        lk.unlock();
+        return finish(false);
+      }
     }
-    // chunk k+1 goes to the other buffer, last used by chunk k-1 (whose
-    // kernels are done: Run returned); its offsets staging too
-    if (k + 1 < n_chunks) copier = start_copy(k + 1);
     HIP_OK(hipStreamWaitEvent(stream_, ev_copied_[b], 0));
     const uint32_t f0 = cut[k], f1 = cut[k + 1];
     BatchStats cs;
@@ -2389,22 +2440,18 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     uint64_t scan_bytes = h_offsets[f1] - h_offsets[f0];
     std::vector<uint64_t> xoff;
     float ms_x = 0;
-    if (kinds && !Transform(b, f1 - f0, &scan_arena, &scan_off, &scan_bytes, &xoff, &ms_x)) {
-      if (copier.joinable()) copier.join();
-      return false;
+    if (kinds && !Transform(b, f1 - f0, &scan_arena, &scan_off, &scan_bytes, &xoff, &ms_x)) return finish(false);
+    if (!Run(scan_arena, scan_bytes, scan_off, f1 - f0, &part, &cs)) return finish(false);
+    {  // the chunk's kernels are done with staging buffer b
+      std::lock_guard<std::mutex> g(cm);
+      scanned = k + 1;
     }
-    if (!Run(scan_arena, scan_bytes, scan_off, f1 - f0, &part, &cs)) {
-      if (copier.joinable()) copier.join();
-      return false;
-    }
+    cv.notify_all();
     if (kinds) {
       st->ms_xform += ms_x;
       cs.ms_total += ms_x;
       tail->xform_bytes += scan_bytes;
-      if (!GatherTail(part, f0, f1 - f0, xoff, h_offsets + f0, kinds + f0, &tail_len, tail)) {
-        if (copier.joinable()) copier.join();
-        return false;
-      }
+      if (!GatherTail(part, f0, f1 - f0, xoff, h_offsets + f0, kinds + f0, &tail_len, tail)) return finish(false);
     }
     for (auto c : part) {
       c.file += f0;
@@ -2428,6 +2475,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     st->ms_chunkmap += cs.ms_chunkmap;
     st->ms_total += cs.ms_total;
   }
+  finish(true);
   HIP_OK(hipEventRecord(ev_h2d_[1], copy_stream_));
   HIP_OK(hipEventSynchronize(ev_h2d_[1]));
   hipEventElapsedTime(&st->ms_h2d_span, ev_h2d_[0], ev_h2d_[1]);
@@ -2458,10 +2506,14 @@ bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint6
   const uint64_t total = (*xoff)[nf];
   if (!Ensure(&d_xf_, &cap_xf_, total + 64)) return false;
   uint8_t* out = static_cast<uint8_t*>(d_xf_);
-  HIP_OK(XformWrite(raw, raw_bytes, off, kd, nf, d_xscan_, out, stream_));
+  HIP_OK(XformWrite(raw, raw_bytes, off, kd, nf, d_xscan_, out, cap_xf_, stream_));
   HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));
   HIP_OK(hipEventRecord(ev_x_[1], stream_));
   HIP_OK(hipEventSynchronize(ev_x_[1]));
+  if (const uint32_t xe = XformErrorWord(raw_bytes, nf, d_xscan_, stream_)) {
+    err_ = "GPU pre-transform: output past its buffer (error word " + std::to_string(xe) + ")";
+    return false;
+  }
   hipEventElapsedTime(ms, ev_x_[0], ev_x_[1]);
   *arena = out;
   *offsets = xo;

@@ -13,12 +13,16 @@ constexpr uint8_t kXformNone = 0, kXformStripCR = 1, kXformPrintable = 2;
 // Flat transform of a batch (n_files + 1 offsets into raw; raw has 64
 // readable bytes past n_bytes).  XformPlan writes xoff (n_files + 1 entries:
 // the transformed offsets) using `scratch` (XformScratchBytes); XformWrite,
-// with the same scratch, writes out[xoff[f] ..) = transform(kind[f], file f).
+// with the same scratch, writes out[xoff[f] ..) = transform(kind[f], file f)
+// and never at or past out_cap (out holds out_cap bytes): a tile whose output
+// would is skipped and flagged in the scratch's error word (XformErrorWord,
+// nonzero = the call failed; read after the stream's work).
 size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files);
 hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                      void* scratch, uint64_t* xoff, hipStream_t s);
 hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
-                      const void* scratch, uint8_t* out, hipStream_t s);
+                      const void* scratch, uint8_t* out, uint64_t out_cap, hipStream_t s);
+uint32_t XformErrorWord(uint64_t n_bytes, uint32_t n_files, const void* scratch, hipStream_t s);
 // dst[dst_off[i] ..) = src[xoff[files[i]] .. xoff[files[i] + 1])
 hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t* files, const uint64_t* dst_off,
                        uint32_t n, uint8_t* dst, hipStream_t s);

@@ -17,6 +17,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 namespace tsg {
 namespace {
 
@@ -362,7 +364,8 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
                                                              const uint64_t* __restrict__ tile_pre,
-                                                             uint8_t* __restrict__ out) {
+                                                             uint8_t* __restrict__ out, uint64_t out_cap,
+                                                             uint32_t* __restrict__ err) {
   // a tile emits at most 1024 + 1024 / 5 + 16 bytes (a '\n' per closed run of >= 5 bytes)
   constexpr uint32_t kStage = 1280 + 32;
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kXThreads / 64][kStage];
@@ -429,6 +432,10 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
       }
       const uint64_t base = start - phase;
       const uint64_t g = base + 16u * lane;
+      if (__any(base + kXTile + 16 > out_cap)) {  // a tile offset past the output: plan and write disagree
+        if (lane == 0) atomicOr(err, 1u);
+        continue;
+      }
       if (lane > 0 || phase == 0) {
         *reinterpret_cast<uint4*>(out + g) = make_uint4(o[0], o[1], o[2], o[3]);
       } else {  // block 0: the previous tile owns out[base, start)
@@ -460,6 +467,10 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t base = start - phase, end = start + total;
+    if (end > out_cap) {  // wave-uniform: never write past the output (the error fails the call)
+      if (lane == 0) atomicOr(err, 2u);
+      continue;
+    }
     for (uint32_t q = 16 * lane; base + q < end; q += 1024) {
       const uint64_t g = base + q;
       if (g >= start && g + 16 <= end) {
@@ -498,8 +509,15 @@ uint32_t grid_for(uint32_t n_waves) {
 
 // Scratch of the flat transform: chunk map | tile counts | tile prefix | file starts | scan temp.
 struct XformScratch {
-  size_t chunk_file, tile_cnt, tile_pre, fstart, scan, scan_bytes, total;
+  size_t chunk_file, tile_cnt, tile_pre, fstart, err, scan, scan_bytes, total;
 };
+
+// 64-bit positions for calls of 4 GiB or more; TSG_XFORM_WIDE=1 forces them
+// (tests run the wide kernels on small batches).
+static bool XformWide(uint64_t n_bytes) {
+  const char* e = std::getenv("TSG_XFORM_WIDE");  // read per call: tests switch it within one process
+  return (e && std::atoi(e) != 0) || n_bytes >= (uint64_t(1) << 32) - 64;
+}
 
 static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
@@ -512,7 +530,8 @@ static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
   L.tile_cnt = up(L.chunk_file + (n_tiles + 1) * 4);
   L.tile_pre = up(L.tile_cnt + (n_tiles + 1) * 4);
   L.fstart = up(L.tile_pre + (n_tiles + 1) * 8);
-  L.scan = up(L.fstart + (size_t(n_files) + 1) * 4);
+  L.err = up(L.fstart + (size_t(n_files) + 1) * 4);
+  L.scan = up(L.err + 16);
   L.scan_bytes = scan;
   L.total = up(L.scan + scan + 16);
   return L;
@@ -522,7 +541,7 @@ size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files) { return ScratchLay
 
 hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                      void* scratch, uint64_t* xoff, hipStream_t s) {
-  const bool wide = n_bytes >= (uint64_t(1) << 32) - 64;  // 64-bit positions (a lone file of >= 4 GiB)
+  const bool wide = XformWide(n_bytes);
   const XformScratch L = ScratchLayout(n_bytes, n_files);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* chunk_file = reinterpret_cast<uint32_t*>(sc + L.chunk_file);
@@ -532,6 +551,7 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   hipError_t e;
   if ((e = hipMemsetAsync(tile_cnt, 0, (n_tiles + 1) * 4, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess) return e;
   if (n_files) {
     xf_chunk_map_kernel<<<grid_for((n_files + 63) / 64), kXThreads, 0, s>>>(off, n_files, chunk_file);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -553,7 +573,7 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
 }
 
 hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
-                      const void* scratch, uint8_t* out, hipStream_t s) {
+                      const void* scratch, uint8_t* out, uint64_t out_cap, hipStream_t s) {
   const XformScratch L = ScratchLayout(n_bytes, n_files);
   const uint8_t* sc = static_cast<const uint8_t*>(scratch);
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
@@ -561,11 +581,22 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
   const uint32_t* cf = reinterpret_cast<const uint32_t*>(sc + L.chunk_file);
   const uint64_t* tp = reinterpret_cast<const uint64_t*>(sc + L.tile_pre);
-  if (n_bytes >= (uint64_t(1) << 32) - 64)
-    xf_write_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, cf, tp, out);
+  uint32_t* err = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(sc) + L.err);
+  if (XformWide(n_bytes))
+    xf_write_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, cf, tp, out, out_cap, err);
   else
-    xf_write_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, cf, tp, out);
+    xf_write_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, cf, tp, out, out_cap,
+                                                      err);
   return hipGetLastError();
+}
+
+uint32_t XformErrorWord(uint64_t n_bytes, uint32_t n_files, const void* scratch, hipStream_t s) {
+  const XformScratch L = ScratchLayout(n_bytes, n_files);
+  uint32_t w = 0;
+  if (hipMemcpyAsync(&w, static_cast<const uint8_t*>(scratch) + L.err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return ~0u;
+  return w;
 }
 
 hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t* files, const uint64_t* dst_off,
