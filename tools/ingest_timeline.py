@@ -9,6 +9,7 @@ Usage: tools/ingest_timeline.py <trace dir> [--min-mb 64] [--last-s 3.0]
 """
 import argparse
 import csv
+import re
 import glob
 import os
 from collections import defaultdict
@@ -61,13 +62,14 @@ def main():
     for (s0, e0, _), (s1, e1, _) in zip(big, big[1:]):
         if s1 > e0:
             gaps.append((e0, s1))
-    gaps.sort(key=lambda g: -(g[1] - g[0]))
     print("gaps between chunk copies: %d, total %.1f ms" % (len(gaps), sum(b - a for a, b in gaps) / 1e6))
-    for ga, gb in gaps[:12]:
+    show = sorted(sorted(gaps, key=lambda g: -(g[1] - g[0]))[:16])  # the largest, in time order
+    for ga, gb in show:
         by = defaultdict(float)
         for s, e, n in ks:
             if e > ga and s < gb:
-                by[n.split("(")[0][-60:]] += (min(e, gb) - max(s, ga)) / 1e6
+                m = re.findall(r"(\w+)(?:<[^()]*>)?\(", n)
+                by[m[0] if m else n[:40]] += (min(e, gb) - max(s, ga)) / 1e6
         top = sorted(by.items(), key=lambda kv: -kv[1])[:4]
         print("  gap %.3f ms at +%.1f ms: %s" % ((gb - ga) / 1e6, (ga - big[0][0]) / 1e6,
                                                ", ".join("%s %.3f" % kv for kv in top) or "(no kernels)"))

@@ -14,6 +14,8 @@
 #include <cstring>
 #include <immintrin.h>
 #include <memory>
+#include <pthread.h>
+#include <thread>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -533,7 +535,11 @@ void Classify(const uint8_t* tar, TarEntry* e);
 // (its header and path are still in that core's cache): the name (Classify),
 // AnalyzeFile's Required, Analyze's binary gate and the transformed length.
 std::atomic<int64_t> g_eval_ns[3];
-void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
+struct EvalCtx {  // what Evaluate needs of the collector (copied: a background index outlives the call)
+  const tsg_analyzer* a;
+  bool gpu_xform;
+};
+void Evaluate(const EvalCtx* c, const uint8_t* tar, TarEntry* e) {
   static const bool dbg = std::getenv("TSG_WALK_DEBUG") && std::atoi(std::getenv("TSG_WALK_DEBUG")) >= 2;  // per-entry timers: level 2
   auto t0 = dbg ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   Classify(tar, e);
@@ -572,7 +578,7 @@ void Evaluate(const tsg_collector* c, const uint8_t* tar, TarEntry* e) {
 // two) that segment is walked sequentially from the true position.  Stops
 // after `max_regular` bytes of regular files (at least one entry), at the end
 // of the archive (*at_end) or on a malformed header (-1).
-int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
+int IndexEntries(const EvalCtx* c, const uint8_t* tar, uint64_t n, uint64_t p, uint64_t window,
                  uint64_t max_regular, int threads, std::vector<std::vector<TarEntry>>& spec,
                  std::vector<std::vector<TarEntry>>& fallback, std::vector<TarEntry*>* out, uint64_t* next,
                  bool* at_end) {
@@ -716,18 +722,40 @@ int IndexEntries(const tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_
 
 namespace tsg {
 // Entries indexed and evaluated ahead of the walk's cursor (see tsg_collector_add_tar).
+struct TarWindow {  // a window of entries indexed from `start`
+  std::vector<TarEntry*> ents;              // the window's entries in archive order
+  std::vector<std::vector<TarEntry>> spec;  // their storage: IndexEntries' per-segment vectors
+  std::vector<std::vector<TarEntry>> fallback;  // and its sequential fallbacks
+  uint64_t start = 0;
+  uint64_t next = 0;     // the position after the last indexed entry
+  bool at_end = false;   // the archive ends at `next`
+};
 struct TarWalkCache {
   const uint8_t* tar = nullptr;
   uint64_t n = 0;
   bool gpu_xform = false;
-  std::vector<TarEntry*> ents;              // the window's entries in archive order
-  std::vector<std::vector<TarEntry>> spec;  // their storage: IndexEntries' per-segment vectors
-  std::vector<std::vector<TarEntry>> fallback;  // and its sequential fallbacks
-  size_t pos = 0;        // the next entry to accept
-  uint64_t next = 0;     // the position after the last indexed entry
-  bool at_end = false;   // the archive ends at `next`
+  TarWindow w;
+  size_t pos = 0;        // the next entry of w to accept
+  // The window after w, indexed on a background thread while the batches of w
+  // are accepted and scanned (tsg_collector_add_tar); it reads the archive
+  // after the call that started it returned -- the buffer-lifetime rule of
+  // tsg_analyzer.h.
+  TarWindow ahead;
+  const uint8_t* ahead_tar = nullptr;
+  uint64_t ahead_n = 0;
+  bool ahead_xform = false, ahead_ok = false;
+  std::thread bg;
+  void Join() {
+    if (bg.joinable()) bg.join();
+  }
+  ~TarWalkCache() { Join(); }
 };
 void FreeTarWalkCache(TarWalkCache* w) { delete w; }
+void EndTarWalk(TarWalkCache* w) {
+  if (!w) return;
+  w->Join();
+  w->ahead_ok = false;
+}
 }  // namespace tsg
 
 namespace {
@@ -908,24 +936,52 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
   static const uint64_t ahead = std::getenv("TSG_WALK_AHEAD") ? uint64_t(std::atoi(std::getenv("TSG_WALK_AHEAD"))) : 8;
   static double t_phase[4];
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const EvalCtx ectx{c->a, c->gpu_xform};
+  static const bool bg_index = !std::getenv("TSG_WALK_BG") || std::atoi(std::getenv("TSG_WALK_BG")) != 0;
   for (;;) {
-    // 1. the cached entries from p on, else index a window starting at p
+    // 1. the cached entries from p on, else the window indexed ahead in the
+    // background (when it starts at p), else index a window starting at p
     double t0 = dbg ? now() : 0;
     const bool hit = W.tar == tar && W.n == n && W.gpu_xform == c->gpu_xform &&
-                     ((W.pos < W.ents.size() && W.ents[W.pos]->start == p) || (W.pos == W.ents.size() && W.next == p &&
-                                                                               W.at_end));
+                     ((W.pos < W.w.ents.size() && W.w.ents[W.pos]->start == p) ||
+                      (W.pos == W.w.ents.size() && W.w.next == p && W.w.at_end));
     if (!hit) {
       const uint64_t room = std::max<uint64_t>(c->limit, 1 << 20);
+      const uint64_t window = ahead * room + (1 << 20);
+      W.Join();  // the background window (if any) is complete, or this walk moved elsewhere
+      const bool take = W.ahead_ok && W.ahead_tar == tar && W.ahead_n == n && W.ahead_xform == c->gpu_xform &&
+                        W.ahead.start == p;
+      W.ahead_ok = false;
       W.tar = tar;
       W.n = n;
       W.gpu_xform = c->gpu_xform;
       W.pos = 0;
-      W.at_end = false;
-      // every entry indexed in the window is kept (no re-indexing past a cut)
-      if (IndexEntries(c, tar, n, p, ahead * room + (1 << 20), ~uint64_t(0) >> 1, c->threads, W.spec, W.fallback, &W.ents, &W.next,
-                       &W.at_end) < 0) {
-        W.tar = nullptr;
-        return -1;
+      if (take) {
+        std::swap(W.w, W.ahead);
+      } else {
+        W.w.start = p;
+        W.w.at_end = false;
+        // every entry indexed in the window is kept (no re-indexing past a cut)
+        if (IndexEntries(&ectx, tar, n, p, window, ~uint64_t(0) >> 1, c->threads, W.w.spec, W.w.fallback, &W.w.ents,
+                         &W.w.next, &W.w.at_end) < 0) {
+          W.tar = nullptr;
+          return -1;
+        }
+      }
+      if (bg_index && !W.w.at_end && W.w.next < n) {
+        // the next window on a background thread (a malformed header there
+        // is found again, with its error, when the walk gets to it)
+        W.ahead_tar = tar;
+        W.ahead_n = n;
+        W.ahead_xform = c->gpu_xform;
+        W.ahead.start = W.w.next;
+        W.ahead.at_end = false;
+        const int threads = c->threads;
+        W.bg = std::thread([&W, ectx, tar, n, window, threads] {
+          pthread_setname_np(pthread_self(), "tsg-walk-bg");
+          W.ahead_ok = IndexEntries(&ectx, tar, n, W.ahead.start, window, ~uint64_t(0) >> 1, threads, W.ahead.spec,
+                                    W.ahead.fallback, &W.ahead.ents, &W.ahead.next, &W.ahead.at_end) == 0;
+        });
       }
     }
     double t1 = dbg ? now() : 0;
@@ -935,10 +991,10 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     // (per-block sums, then the blocks' rows written in parallel), the block
     // where the batch fills entry by entry
     const size_t k0 = W.pos;
-    size_t k = k0 + AcceptBlocks(c, tar, W.ents, k0, st);
+    size_t k = k0 + AcceptBlocks(c, tar, W.w.ents, k0, st);
     bool full = false;
-    for (; k < W.ents.size(); k++) {
-      TarEntry& e = *W.ents[k];
+    for (; k < W.w.ents.size(); k++) {
+      TarEntry& e = *W.w.ents[k];
       if (e.bad) {
         tsg::SetError("tar: invalid header checksum at offset " + std::to_string(e.hdr));
         W.tar = nullptr;
@@ -980,7 +1036,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     // 3. copy / transform the accepted contents
     tsg::ParallelFor((k - k0 + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
       for (size_t i = k0 + b * kBlock; i < std::min(k, k0 + (b + 1) * kBlock); i++) {
-        const TarEntry& e = *W.ents[i];
+        const TarEntry& e = *W.w.ents[i];
         if (e.state != 2) continue;
         uint8_t* dst = c->arena + e.out_off;
         if (c->gpu_xform) tsg::CopyToArena(dst, tar + e.data, e.size);
@@ -1001,13 +1057,19 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
                    g_eval_ns[0] / 1e9, g_eval_ns[1] / 1e9);
     }
     if (full) {
-      *cursor = W.ents[k]->start;
+      *cursor = W.w.ents[k]->start;
       return 1;
     }
-    p = W.next;
+    p = W.w.next;
     *cursor = p;
-    if (W.at_end) return 0;
+    if (W.w.at_end) return 0;
   }
+}
+
+int tsg_analyzer_walk_end(tsg_analyzer* a) {
+  std::lock_guard<std::mutex> g(a->walk_mu);
+  tsg::EndTarWalk(a->walk);
+  return 0;
 }
 
 uint32_t tsg_collector_files(const tsg_collector* c) { return c->files(); }

@@ -18,6 +18,7 @@ void SetError(const std::string& e);
 namespace tsg {
 struct TarWalkCache;  // analyzer.cpp: evaluated tar entries indexed ahead of the cursor
 void FreeTarWalkCache(TarWalkCache* w);
+void EndTarWalk(TarWalkCache* w);  // joins the background index of the next window
 }
 
 struct tsg_analyzer {

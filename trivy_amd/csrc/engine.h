@@ -203,7 +203,7 @@ class GpuEngine {
                                     // [6] full-scan list overflow [11] anchor-item matches [13] open pairs
   // host-batch streaming (RunHost): two staging buffers, a copy stream
   hipStream_t copy_stream_ = nullptr;
-  static constexpr int kNStage = 3;  // staging buffers: the copier runs up to two chunks ahead
+  static constexpr int kNStage = 4;  // staging buffers: the copier runs up to three chunks ahead
   hipEvent_t ev_copied_[kNStage] = {}, ev_h2d_[2] = {};
   void* d_stage_[kNStage] = {}; size_t cap_stage_[kNStage] = {};
   void* d_stage_off_[kNStage] = {}; size_t cap_stage_off_[kNStage] = {};

@@ -738,7 +738,7 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
 #define TSG_C_FSE 0
 #endif
 #ifndef TSG_C_PREFETCH
-#define TSG_C_PREFETCH 0
+#define TSG_C_PREFETCH 1
 #endif
 constexpr bool kCFse = TSG_C_FSE;     // cache each block's file in LDS in phase A (-0.2 ms at equal occupancy; costs 20 B/lane)
 constexpr uint32_t kCQ1 = TSG_C_Q1;  // fires (overflow: handled in place)

@@ -297,7 +297,7 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
                                                              const uint64_t* __restrict__ off,
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
-                                                             uint32_t* __restrict__ tile_cnt,
+                                                             uint64_t* __restrict__ tile_cnt,
                                                              uint32_t* __restrict__ fstart) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
@@ -523,12 +523,12 @@ static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   XformScratch L;
   size_t scan = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, static_cast<const uint32_t*>(nullptr),
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, static_cast<const uint64_t*>(nullptr),
                                          static_cast<uint64_t*>(nullptr), int(n_tiles) + 1);
   auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
   L.chunk_file = 0;
   L.tile_cnt = up(L.chunk_file + (n_tiles + 1) * 4);
-  L.tile_pre = up(L.tile_cnt + (n_tiles + 1) * 4);
+  L.tile_pre = up(L.tile_cnt + (n_tiles + 1) * 8);
   L.fstart = up(L.tile_pre + (n_tiles + 1) * 8);
   L.err = up(L.fstart + (size_t(n_files) + 1) * 4);
   L.scan = up(L.err + 16);
@@ -545,12 +545,14 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   const XformScratch L = ScratchLayout(n_bytes, n_files);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* chunk_file = reinterpret_cast<uint32_t*>(sc + L.chunk_file);
-  uint32_t* tile_cnt = reinterpret_cast<uint32_t*>(sc + L.tile_cnt);
+  // 64-bit counts: the scan's accumulator is the input type, and the sum of a
+  // batch of 4 GiB or more does not fit 32 bits
+  uint64_t* tile_cnt = reinterpret_cast<uint64_t*>(sc + L.tile_cnt);
   uint64_t* tile_pre = reinterpret_cast<uint64_t*>(sc + L.tile_pre);
   uint32_t* fstart = reinterpret_cast<uint32_t*>(sc + L.fstart);
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   hipError_t e;
-  if ((e = hipMemsetAsync(tile_cnt, 0, (n_tiles + 1) * 4, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(tile_cnt, 0, (n_tiles + 1) * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess) return e;
   if (n_files) {
     xf_chunk_map_kernel<<<grid_for((n_files + 63) / 64), kXThreads, 0, s>>>(off, n_files, chunk_file);
