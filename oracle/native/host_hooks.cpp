@@ -57,6 +57,13 @@ int Tail(std::unique_ptr<tsg::SecretScanner> sc, const tsg_batch* b, std::vector
   const tsg::BatchInput in = Input(b);
   std::unique_ptr<tsg_result> r(new tsg_result());
   tsg::HostStats hs;
+  // TSG_TAIL_REPS=n: the tail n times on copies of the candidates (profiling:
+  // the samples then come from the tail, not from compiling the rules)
+  for (int rep = std::getenv("TSG_TAIL_REPS") ? std::atoi(std::getenv("TSG_TAIL_REPS")) : 1; rep > 1; rep--) {
+    std::vector<tsg::Candidate> cc(*cands);
+    tsg::BatchResult tmp;
+    sc->HostTail(in, &cc, &tmp, &hs);
+  }
   sc->HostTail(in, cands, &r->files, &hs);
   std::memset(&r->stats, 0, sizeof(r->stats));
   r->stats.bytes = in.n_files ? in.host_offsets[in.n_files] : 0;

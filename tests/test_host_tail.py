@@ -291,3 +291,46 @@ def test_result_records_match_findings():
     assert len(want) > 5
     assert [(int(r["file"]), ids[r["rule"]], int(r["start_line"]), int(r["end_line"]), int(r["digest"]))
             for r in rec] == want
+
+
+def test_host_tail_dense_findings_line_index(tmp_path):
+    """Files with many findings for their size take the per-file index of the newlines the
+    censored content keeps (scanner.cpp ScanFile): line numbers, match lines over 100 B,
+    code windows at the file's first and last lines, multi-line private keys whose newlines
+    are censored, adjacent matches on one line and on consecutive lines -- vs the oracle."""
+    import random
+    cfg_path = tmp_path / "trivy-secret.yaml"
+    cfg_path.write_text(
+        "rules:\n  - id: b64run\n    category: Custom\n    title: Base64 run\n    severity: LOW\n"
+        "    regex: '(?i)[a-z0-9/+]{32,48}'\n    keywords: [blobkw]\n")
+    cfg = ParseConfig(str(cfg_path))
+    rng = random.Random(77)
+    alpha = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
+    pk = (b"-----BEGIN RSA PRIVATE KEY-----\n" + b"MIIEow" * 11 + b"\n" + b"abcd" * 16 + b"\n"
+          b"-----END RSA PRIVATE KEY-----")
+    files = []
+    for i in range(60):
+        parts = [b"blobkw"] if i % 5 else []
+        for _ in range(rng.randint(6, 40)):
+            r = rng.random()
+            if r < 0.5:
+                parts.append(bytes(rng.choice(alpha) for _ in range(rng.randint(20, 400))))
+            elif r < 0.6:
+                parts.append(pk)
+            elif r < 0.75:
+                parts.append(b"k = AKIA" + bytes(rng.choice(b"ABCDEFGHIJKLMNOPQRSTUVWXYZ234567") for _ in range(16)))
+            elif r < 0.85:
+                parts.append(b"x" * rng.randint(0, 300))
+            else:
+                parts.append(b"")
+        sep = [b"\n", b" ", b"\n\n", b"="]
+        body = b"".join(p + rng.choice(sep) for p in parts)
+        files.append(("dense%02d.txt" % i, body))
+    got = host_tail_scan(cfg, files)
+    o = osc.new_scanner(osc.parse_config(str(cfg_path)))
+    n = 0
+    for (p, b), g in zip(files, got):
+        want = o.scan(p, b)
+        assert g.to_dict() == want, p
+        n += len(want["Findings"] or [])
+    assert n > 600

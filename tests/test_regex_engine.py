@@ -48,7 +48,10 @@ PATTERNS = ([r["regex"] for r in BUILTIN["rules"]]
             + [a[k] for a in BUILTIN["allow_rules"] for k in ("regex", "path") if a[k]]
             + _golden_custom_regexes()
             + [r"a*", r"x{2,5}?y", r"(?m)^ab$", r"\bfoo\b", r"(?i)straße", r"(?s).{0,3}z",
-               r"[^\x00-\x7f]+", r"\x{FFFD}", r"(?U)a+b", r"(?i)k+s", r"^", r"$", r"(?i)[^k]"])
+               r"[^\x00-\x7f]+", r"\x{FFFD}", r"(?U)a+b", r"(?i)k+s", r"^", r"$", r"(?i)[^k]",
+               # one greedy class repeat (FindAll's class-run path, goregex.cpp FindAllRun)
+               r"(?i)[a-z0-9/+]{32,48}", r"[0-9]{3}", r"(?P<secret>[a-f0-9]{8,})", r"(?i)[ks]{2,4}",
+               r"[^\s]{3,5}", r"((?:[a-c]){2,3})", r"(?i)(?P<x>[k-s]+)", r"\S{4}", r"[^a]{1,2}", r"[\x{FFFD}a]{2}"])
 
 NOISE = ["the quick brown fox ", "key=", "secret: ", "\n", "  ", "'", '"', "AKIA", "ghp_",
          "sk_live_", "K", "ſ", "İ", "é", "日本", "\udcff", "-----BEGIN ", "=>",

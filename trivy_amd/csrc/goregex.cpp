@@ -915,6 +915,7 @@ std::unique_ptr<Regex> Regex::Compile(const std::string& pattern, std::string* e
     }
   }
   re->ComputeFirstBytes();
+  re->DetectRun();
   {  // instructions whose only predecessor is one rune instruction (Backtracker chain skip)
     std::vector<uint32_t> preds(re->prog_.size(), 0);
     std::vector<uint8_t> from_rune(re->prog_.size(), 0);
@@ -1413,11 +1414,104 @@ bool Regex::Match(const uint8_t* s, int64_t n) const {
   return m.Search(s, n, 0, nullptr);
 }
 
+void Regex::DetectRun() {
+  int x = root_, caps = 0;
+  for (;;) {  // through capture groups and single-element concatenations
+    const Node& nd = nodes_[size_t(x)];
+    if (nd.op == NodeOp::Capture) {
+      caps++;
+      x = nd.subs[0];
+      continue;
+    }
+    if (nd.op == NodeOp::Cat) {
+      int only = -1, cnt = 0;
+      for (int sub : nd.subs)
+        if (nodes_[size_t(sub)].op != NodeOp::Empty) {
+          only = sub;
+          cnt++;
+        }
+      if (cnt != 1) return;
+      x = only;
+      continue;
+    }
+    break;
+  }
+  const Node& r = nodes_[size_t(x)];
+  if (r.op != NodeOp::Repeat || !r.greedy || r.min < 1 || caps != num_cap_) return;
+  const Node& c = nodes_[size_t(r.subs[0])];
+  if (c.op != NodeOp::Class) return;
+  run_cls_ = c.ranges;
+  run_ascii_[0] = run_ascii_[1] = 0;
+  for (uint32_t b = 0; b < 128; b++)
+    if (InRanges(run_cls_, b)) run_ascii_[b >> 6] |= uint64_t(1) << (b & 63);
+  run_min_ = r.min;
+  run_max_ = r.max;
+  run_ok_ = true;
+}
+
+// FindAll of C{m,n} (greedy, m >= 1), leftmost-first as the backtracker finds
+// it: at a start, the match is the longest run of class runes there, cut at n;
+// with fewer than m class runes at a start, no start up to the rune that ended
+// the run can match either (their runs are shorter), so the search resumes
+// after it.  Windows restrict the starts as in Backtracker::Search.
+void Regex::FindAllRun(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
+                       std::vector<int64_t>* out) const {
+  const int groups = submatch ? num_cap_ + 1 : 1;
+  const int64_t lim = run_max_ < 0 ? INT64_MAX : int64_t(run_max_);
+  int64_t pos = 0;
+  size_t wi = 0;
+  while (pos < n) {
+    if (wins) {
+      while (wi < wins->size() && (*wins)[wi].hi < pos) wi++;
+      if (wi >= wins->size()) break;
+      if ((*wins)[wi].lo > pos) {
+        const int64_t t = Machine::Align(s, n, (*wins)[wi].lo);
+        if (t > pos) pos = t;
+      }
+      if (pos >= n) break;
+      if ((*wins)[wi].lo > pos) {  // not a start the windows allow: the next rune
+        pos += DecodeRune(s, n, pos).width;
+        continue;
+      }
+    }
+    int64_t q = pos, k = 0;
+    int w = 1;
+    while (q < n && k < lim) {
+      const uint8_t b = s[q];
+      bool in;
+      if (b < 0x80) {
+        w = 1;
+        in = (run_ascii_[b >> 6] >> (b & 63)) & 1;
+      } else {
+        const Rune r = DecodeRune(s, n, q);
+        w = r.width;
+        in = InRanges(run_cls_, uint32_t(r.r));
+      }
+      if (!in) break;
+      q += w;
+      k++;
+    }
+    if (k >= run_min_) {
+      for (int g = 0; g < groups; g++) {
+        out->push_back(pos);
+        out->push_back(q);
+      }
+      pos = q;
+      continue;
+    }
+    pos = q < n ? q + w : n;  // q: the rune that ended the run (w: its width)
+  }
+}
+
 void Regex::FindAll(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
                     std::vector<int64_t>* out) const {
   int ncap = submatch ? 2 * (num_cap_ + 1) : 2;
   Backtracker& bt = t_bt;
   const int mode = g_regex_engine.load(std::memory_order_relaxed);
+  if (run_ok_ && mode == 0) {  // modes 1-3: the general engines (tests compare them)
+    FindAllRun(s, n, submatch, wins, out);
+    return;
+  }
   bt.max_rows_ = mode == 2 ? 8 : Backtracker::kMaxRows;
   std::unique_ptr<Machine> m;  // only when the backtracker's row budget runs out
   if (mode == 1) m.reset(new Machine(this, ncap));

@@ -106,6 +106,16 @@ class Regex {
   std::vector<uint8_t> single_pred_;  // pc entered only from one rune instruction (no visited bit needed)
   uint64_t first_[4] = {};
   bool first_all_ = true;
+  // A regex that is one greedy repeat of one single-rune class, C{m,n} / C{m,}
+  // with m >= 1, possibly inside capture groups (custom rules such as
+  // (?i)[a-z0-9/+]{32,48}): FindAll is then a scan over class runs (FindAllRun).
+  bool run_ok_ = false;
+  int run_min_ = 0, run_max_ = 0;  // run_max_ < 0: unbounded
+  RuneRanges run_cls_;
+  uint64_t run_ascii_[2] = {};
+  void DetectRun();
+  void FindAllRun(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
+                  std::vector<int64_t>* out) const;
   void ComputeFirstBytes();
   bool FirstOk(const uint8_t* s, int64_t n, int64_t pos) const {
     return first_all_ || (pos < n && ((first_[s[pos] >> 6] >> (s[pos] & 63)) & 1));
