@@ -306,9 +306,10 @@ def test_native_walk_bad_header_in_bulk_block(host_analyzer, layer_30mb, arena_m
     raw[m.offset + 148] ^= 0x01  # a digit of the checksum field
     coll = Collector(host_analyzer, arena_mb << 20, True)
     cursor, batches = 0, 0
+    buf = bytes(raw)  # one buffer for the whole walk (tsg_analyzer.h buffer lifetime)
     with pytest.raises(ValueError, match="checksum"):
         while True:
-            rc, cursor = coll.add_tar(bytes(raw), cursor, _CTarStats())
+            rc, cursor = coll.add_tar(buf, cursor, _CTarStats())
             coll.reset()
             batches += 1
             if rc == 0:

@@ -965,6 +965,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         if (IndexEntries(&ectx, tar, n, p, window, ~uint64_t(0) >> 1, c->threads, W.w.spec, W.w.fallback, &W.w.ents,
                          &W.w.next, &W.w.at_end) < 0) {
           W.tar = nullptr;
+          W.Join();
           return -1;
         }
       }
@@ -998,6 +999,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       if (e.bad) {
         tsg::SetError("tar: invalid header checksum at offset " + std::to_string(e.hdr));
         W.tar = nullptr;
+        W.Join();  // a walk that fails ends here: the background index must not outlive it
         return -1;
       }
       if (e.state == 2) {
@@ -1005,7 +1007,10 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
           full = true;
           break;
         }
-        if (c->used + e.out_len + 64 > c->cap && !c->Reserve(e.out_len + 64)) return -1;  // a lone large file
+        if (c->used + e.out_len + 64 > c->cap && !c->Reserve(e.out_len + 64)) {  // a lone large file
+          W.Join();
+          return -1;
+        }
         e.out_off = c->used;
         if (c->gpu_xform) {
           c->used += e.size;
