@@ -56,6 +56,14 @@ for st in $STAGES; do
     large)  # the > 4 GiB transformed-file test alone (last: it moves ~9 GB through the box)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_large_file.py -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_large_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_large_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    c4ab)  # C4 with the default ingest chunking and with C4_ENV (e.g. TSG_INGEST_CHUNK_MB=64), interleaved
+      for rep in 1 2; do
+        for v in base alt; do
+          if [ "$v" = base ]; then E=""; else E="${C4_ENV:-TSG_INGEST_CHUNK_MB=64}"; fi
+          env $E timeout -k 10 600 python bench.py --workload c4 --steps 5 --warmup 2 --no-cpu-baseline ${C4_ARGS:-} > gpurun_out/c4ab_${TAG}_${v}_$rep.json 2> gpurun_out/c4ab_${TAG}_${v}_$rep.err
+          rc=$?; echo "== c4 $v $rep ($E)"; python tools/bench_brief.py gpurun_out/c4ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
     wl)
       for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
         timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err

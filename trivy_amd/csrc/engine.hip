@@ -51,12 +51,23 @@ constexpr int kScanWaves = kScanThreads / 64;
   } while (0)
 
 
-__global__ void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
-                                 uint32_t* __restrict__ chunk_file) {
-  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < n_files; f += gridDim.x * blockDim.x) {
-    uint64_t s = off[f], e = off[f + 1];
-    if (s >= e) continue;
-    for (uint64_t c = (s + kChunk - 1) / kChunk; c * kChunk < e; c++) chunk_file[c] = f;
+// K0: chunk c -> the file holding byte c * kChunk (off[f] <= c * kChunk <
+// off[f + 1], so never an empty file), one thread per chunk by a binary
+// search over the offsets (L2-resident).  A thread per file looping over its
+// chunks left a multi-MiB file's thousands of stores to one thread (0.19 ms
+// on C2 for 80 MB of map).
+__global__ __launch_bounds__(256) void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
+                                                        uint64_t n_chunks, uint32_t* __restrict__ chunk_file) {
+  for (uint64_t c = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; c < n_chunks;
+       c += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t x = c * kChunk;
+    uint32_t lo = 0, hi = n_files;  // the last f with off[f] <= x: off[lo] <= x < off[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    chunk_file[c] = lo;
   }
 }
 
@@ -2732,11 +2743,11 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
   HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
   HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
-  HIP_OK(hipMemsetAsync(d_chunk_file_, 0, n_chunks * 4, stream_));
   if (d_item_diag_) HIP_OK(hipMemsetAsync(d_item_diag_, 0, 8 * std::max<size_t>(n_fitems_, 1), stream_));
-  {
-    uint32_t blocks = std::min<uint32_t>((n_files + 255) / 256, 4096);
-    chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, static_cast<uint32_t*>(d_chunk_file_));
+  {  // every chunk below n_bytes gets its file (no clear needed)
+    const uint64_t used = (n_bytes + kChunk - 1) / kChunk;
+    const uint32_t blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((used + 255) / 256, 8192)));
+    chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, used, static_cast<uint32_t*>(d_chunk_file_));
   }
   // K1: streaming filter -> flagged block records
   FilterParams fp;

@@ -101,11 +101,20 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t lane) {  // e
 // ---------------------------------------------------------------------------
 constexpr uint32_t kXTile = 1024;
 
+// tile t -> the file holding byte t * kXTile: one thread per tile, binary
+// search over the offsets (as engine.hip chunk_map_kernel)
 __global__ __launch_bounds__(kXThreads) void xf_chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
-                                                                 uint32_t* __restrict__ chunk_file) {
-  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < n_files; f += gridDim.x * blockDim.x) {
-    const uint64_t s = off[f], e = off[f + 1];
-    for (uint64_t c = (s + kXTile - 1) / kXTile; c * kXTile < e; c++) chunk_file[c] = f;
+                                                                 uint64_t n_tiles, uint32_t* __restrict__ chunk_file) {
+  for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < n_tiles;
+       t += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t x = t * kXTile;
+    uint32_t lo = 0, hi = n_files;  // off[lo] <= x < off[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    chunk_file[t] = lo;
   }
 }
 
@@ -554,8 +563,9 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   hipError_t e;
   if ((e = hipMemsetAsync(tile_cnt, 0, (n_tiles + 1) * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess) return e;
-  if (n_files) {
-    xf_chunk_map_kernel<<<grid_for((n_files + 63) / 64), kXThreads, 0, s>>>(off, n_files, chunk_file);
+  if (n_files && n_tiles) {
+    const uint32_t gm = uint32_t(std::min<uint64_t>((n_tiles + kXThreads - 1) / kXThreads, 8192));
+    xf_chunk_map_kernel<<<gm, kXThreads, 0, s>>>(off, n_files, n_tiles, chunk_file);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (n_tiles) {
