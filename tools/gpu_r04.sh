@@ -64,6 +64,18 @@ for st in $STAGES; do
           rc=$?; echo "== c4 $v $rep ($E)"; python tools/bench_brief.py gpurun_out/c4ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
         done
       done ;;
+    pmc)  # SQ counters per kernel, two passes (tools/gpu_pmc.sh groups 1-2) over a 1-step C2 run
+      cd /tmp
+      i=0
+      for g in "GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAIT_INST_LDS SQ_CYCLES" \
+               "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD"; do
+        i=$((i+1))
+        timeout -s KILL 150 rocprofv3 --pmc $g --kernel-trace -d $R/gpurun_out/pmc_${TAG}_$i -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --warmup-s 0 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > $R/gpurun_out/pmc_${TAG}_$i.json 2> $R/gpurun_out/pmc_${TAG}_$i.err
+        rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        python3 $R/tools/pmc_summary.py $(find $R/gpurun_out/pmc_${TAG}_$i -name '*counter_collection.csv') > $R/gpurun_out/pmc_${TAG}_$i.txt
+        cat $R/gpurun_out/pmc_${TAG}_$i.txt
+      done
+      cd $R ;;
     wl)
       for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
         timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
