@@ -71,6 +71,12 @@ typedef struct tsg_tar_stats {
  * batch filled up (*cursor = the entry to resume from), <0 on a malformed
  * archive.  Whiteout (.wh.) and opaque-dir entries are counted, not added. */
 int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st);
+/* Buffer lifetime: the analyzer indexes the next window of entries on a
+ * background thread after tsg_collector_add_tar returns 1, so `tar` must stay
+ * valid and unchanged until that walk ends -- add_tar returned 0 (end of the
+ * archive) or < 0 -- or until tsg_analyzer_walk_end / tsg_analyzer_free
+ * returns (call it before freeing the buffer of a walk abandoned midway). */
+int tsg_analyzer_walk_end(tsg_analyzer* a);
 
 /* GPU pre-transform mode (empty collector only): files go into the arena as
  * read, and the CR strip / printable extraction runs on the GPU at scan time

@@ -50,6 +50,7 @@ def _declare(L):
     L.tsg_strip_cr.restype = c.c_uint64
     L.tsg_analyzer_new.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_void_p)]
     L.tsg_analyzer_free.argtypes = [c.c_void_p]
+    L.tsg_analyzer_walk_end.argtypes = [c.c_void_p]
     L.tsg_analyzer_required.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64, c.c_int64]
     L.tsg_collector_new.argtypes = [c.c_void_p, c.c_uint64, c.POINTER(c.c_void_p)]
     L.tsg_collector_free.argtypes = [c.c_void_p]
@@ -431,7 +432,10 @@ class SecretAnalyzer:
             if rc == 1 and coll.files() == 0:
                 raise RuntimeError("tar layer: an entry does not fit an empty collector")
             return rc == 0
-        t_walk, t_wait = _pipeline(colls, fill, take)
+        try:
+            t_walk, t_wait = _pipeline(colls, fill, take)
+        finally:  # the layer buffer may go away after this call (tsg_analyzer.h buffer lifetime)
+            self._L.tsg_analyzer_walk_end(self._h)
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})
