@@ -37,6 +37,11 @@ for st in $STAGES; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --ingest-steps 0 > $R/gpurun_out/prof_bench_$TAG.json 2> $R/gpurun_out/prof_$TAG.err
       rc=$?; cd $R; tail -2 gpurun_out/prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
       find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
+    c4prof)  # rocprofv3 kernel stats of a short C4 run (the pre-transform kernels per batch)
+      cd /tmp
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/c4prof_$TAG -o run --output-format csv -- python3 $R/bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/c4prof_bench_$TAG.json 2> $R/gpurun_out/c4prof_$TAG.err
+      rc=$?; cd $R; tail -2 gpurun_out/c4prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
+      find gpurun_out/c4prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
     ingprof)  # the C2 ingest leg under a kernel + memory-copy trace (copy / kernel timeline)
       cd /tmp
       timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace -d $R/gpurun_out/ingprof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --warmup-s 0 --no-cpu-baseline --ingest-steps 3 > $R/gpurun_out/ingprof_bench_$TAG.json 2> $R/gpurun_out/ingprof_$TAG.err
@@ -56,10 +61,11 @@ for st in $STAGES; do
     large)  # the > 4 GiB transformed-file test alone (last: it moves ~9 GB through the box)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_large_file.py -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_large_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_large_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
-    c4ab)  # C4 with the default ingest chunking and with C4_ENV (e.g. TSG_INGEST_CHUNK_MB=64), interleaved
+    c4ab)  # C4 with the defaults and with each env of C4_ENVS ('|'-separated, e.g. "TSG_INGEST_CHUNK_MB=64|TSG_GPU_SLOTS=2"), interleaved
+      IFS='|' read -r -a envs <<< "${C4_ENVS:-TSG_INGEST_CHUNK_MB=64}"
       for rep in 1 2; do
-        for v in base alt; do
-          if [ "$v" = base ]; then E=""; else E="${C4_ENV:-TSG_INGEST_CHUNK_MB=64}"; fi
+        for i in base "${!envs[@]}"; do
+          if [ "$i" = base ]; then E=""; v=base; else E="${envs[$i]}"; v=alt$i; fi
           env $E timeout -k 10 600 python bench.py --workload c4 --steps 5 --warmup 2 --no-cpu-baseline ${C4_ARGS:-} > gpurun_out/c4ab_${TAG}_${v}_$rep.json 2> gpurun_out/c4ab_${TAG}_${v}_$rep.err
           rc=$?; echo "== c4 $v $rep ($E)"; python tools/bench_brief.py gpurun_out/c4ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
         done

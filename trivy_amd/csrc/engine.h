@@ -208,6 +208,7 @@ class GpuEngine {
   void* d_stage_[kNStage] = {}; size_t cap_stage_[kNStage] = {};
   void* d_stage_off_[kNStage] = {}; size_t cap_stage_off_[kNStage] = {};
   uint64_t* h_off_[kNStage] = {}; size_t cap_h_off_[kNStage] = {};  // pinned, rebased chunk offsets
+  uint64_t* h_xoff_ = nullptr; size_t cap_h_xoff_ = 0;  // pinned: transformed offsets + the error word
   // GPU pre-transform (xform.h): per-chunk kinds, lengths, transformed offsets and bytes, the gather
   void* d_kind_[kNStage] = {}; size_t cap_kind_[kNStage] = {};
   void* d_xlen_ = nullptr; size_t cap_xlen_ = 0;

@@ -2284,6 +2284,7 @@ GpuEngine::~GpuEngine() {
     if (e) hipEventDestroy(e);
   for (auto* h : h_off_)
     if (h) hipHostFree(h);
+  if (h_xoff_) hipHostFree(h_xoff_);
   if (copy_stream_) hipStreamDestroy(copy_stream_);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -2498,33 +2499,44 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
 
 // Pre-transform of the chunk in staging buffer b (xform.h): lengths, their
 // prefix sums (the transformed offsets, also copied back to *xoff), the
-// compaction into d_xf_.  Points the scan at the transformed arena.
+// compaction into d_xf_.  Points the scan at the transformed arena.  The
+// output buffer is sized by the bound XformMaxOut, so plan and write run back
+// to back and the host waits once, for the offsets and the error word together.
 bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
                           std::vector<uint64_t>* xoff, float* ms) {
   const uint64_t raw_bytes = *n_bytes;
   if (!Ensure(&d_xoff_, &cap_xoff_, (size_t(nf) + 1) * 8) ||
-      !Ensure(&d_xscan_, &cap_xscan_, XformScratchBytes(raw_bytes, nf)))
+      !Ensure(&d_xscan_, &cap_xscan_, XformScratchBytes(raw_bytes, nf)) ||
+      !Ensure(&d_xf_, &cap_xf_, XformMaxOut(raw_bytes, nf) + 64))
     return false;
+  if (cap_h_xoff_ < size_t(nf) + 2) {  // nf + 1 offsets, then the error word
+    if (h_xoff_) hipHostFree(h_xoff_);
+    h_xoff_ = nullptr;
+    cap_h_xoff_ = 0;
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&h_xoff_), (size_t(nf) + 2) * 8, hipHostMallocDefault));
+    cap_h_xoff_ = size_t(nf) + 2;
+  }
   const uint8_t* raw = static_cast<const uint8_t*>(d_stage_[b]);
   const uint64_t* off = static_cast<const uint64_t*>(d_stage_off_[b]);
   const uint8_t* kd = static_cast<const uint8_t*>(d_kind_[b]);
   uint64_t* xo = static_cast<uint64_t*>(d_xoff_);
+  uint8_t* out = static_cast<uint8_t*>(d_xf_);
+  h_xoff_[nf + 1] = 0;
   HIP_OK(hipEventRecord(ev_x_[0], stream_));
   HIP_OK(XformPlan(raw, raw_bytes, off, kd, nf, d_xscan_, xo, stream_));
-  xoff->resize(size_t(nf) + 1);
-  HIP_OK(hipMemcpyAsync(xoff->data(), xo, (size_t(nf) + 1) * 8, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
-  const uint64_t total = (*xoff)[nf];
-  if (!Ensure(&d_xf_, &cap_xf_, total + 64)) return false;
-  uint8_t* out = static_cast<uint8_t*>(d_xf_);
   HIP_OK(XformWrite(raw, raw_bytes, off, kd, nf, d_xscan_, out, cap_xf_, stream_));
-  HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));
+  HIP_OK(hipMemcpyAsync(h_xoff_, xo, (size_t(nf) + 1) * 8, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_xoff_ + nf + 1, XformErrorPtr(raw_bytes, nf, d_xscan_), 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipEventRecord(ev_x_[1], stream_));
   HIP_OK(hipEventSynchronize(ev_x_[1]));
-  if (const uint32_t xe = XformErrorWord(raw_bytes, nf, d_xscan_, stream_)) {
-    err_ = "GPU pre-transform: output past its buffer (error word " + std::to_string(xe) + ")";
+  const uint64_t total = h_xoff_[nf];
+  if (const uint32_t xe = uint32_t(h_xoff_[nf + 1]); xe != 0 || total + 64 > cap_xf_) {
+    err_ = "GPU pre-transform: output past its buffer (error word " + std::to_string(xe) + ", " +
+           std::to_string(total) + " bytes)";
     return false;
   }
+  HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));
+  xoff->assign(h_xoff_, h_xoff_ + nf + 1);
   hipEventElapsedTime(ms, ev_x_[0], ev_x_[1]);
   *arena = out;
   *offsets = xo;

@@ -23,6 +23,12 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
 hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                       const void* scratch, uint8_t* out, uint64_t out_cap, hipStream_t s);
 uint32_t XformErrorWord(uint64_t n_bytes, uint32_t n_files, const void* scratch, hipStream_t s);
+// The error word's device address (read it with the stream's other results).
+const uint32_t* XformErrorPtr(uint64_t n_bytes, uint32_t n_files, const void* scratch);
+// Upper bound of a batch's transformed size: the strip only drops bytes, the
+// printable extraction replaces a byte by '\n' where it closes a run and adds one
+// '\n' per file at most (a run reaching the file's end).
+inline uint64_t XformMaxOut(uint64_t n_bytes, uint32_t n_files) { return n_bytes + n_files; }
 // dst[dst_off[i] ..) = src[xoff[files[i]] .. xoff[files[i] + 1])
 hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t* files, const uint64_t* dst_off,
                        uint32_t n, uint8_t* dst, hipStream_t s);

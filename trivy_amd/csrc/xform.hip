@@ -611,6 +611,10 @@ uint32_t XformErrorWord(uint64_t n_bytes, uint32_t n_files, const void* scratch,
   return w;
 }
 
+const uint32_t* XformErrorPtr(uint64_t n_bytes, uint32_t n_files, const void* scratch) {
+  return reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(scratch) + ScratchLayout(n_bytes, n_files).err);
+}
+
 hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t* files, const uint64_t* dst_off,
                        uint32_t n, uint8_t* dst, hipStream_t s) {
   if (n == 0) return hipSuccess;
