@@ -61,6 +61,20 @@ for st in $STAGES; do
     large)  # the > 4 GiB transformed-file test alone (last: it moves ~9 GB through the box)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_large_file.py -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_large_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_large_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    ingab)  # ingest leg A/B of library variants (VARIANTS; base = the in-tree build), twice interleaved
+      for rep in 1 2; do
+        for v in ${VARIANTS:-base}; do
+          if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
+          TSG_LIB=$L timeout -k 10 400 python bench.py --steps 5 --warmup 2 --warmup-s 0 --no-cpu-baseline --ingest-steps 6 ${BENCH_ARGS:-} > gpurun_out/ingab_${TAG}_${v}_$rep.json 2> gpurun_out/ingab_${TAG}_${v}_$rep.err
+          rc=$?; echo "== $v $rep"; python - gpurun_out/ingab_${TAG}_${v}_$rep.json <<'PYEOF'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+i = d.get("ingest") or {}
+print("value=%s ingest=%s frac_h2d=%s ms=%s" % (d["value"], i.get("value"), i.get("frac_h2d"), i.get("ms_per_step")))
+PYEOF
+          [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
     c4ab)  # C4 with the defaults and with each env of C4_ENVS ('|'-separated, e.g. "TSG_INGEST_CHUNK_MB=64|TSG_GPU_SLOTS=2"), interleaved
       IFS='|' read -r -a envs <<< "${C4_ENVS:-TSG_INGEST_CHUNK_MB=64}"
       for rep in 1 2; do
@@ -80,6 +94,15 @@ for st in $STAGES; do
         rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
         python3 $R/tools/pmc_summary.py $(find $R/gpurun_out/pmc_${TAG}_$i -name '*counter_collection.csv') > $R/gpurun_out/pmc_${TAG}_$i.txt
         cat $R/gpurun_out/pmc_${TAG}_$i.txt
+      done
+      cd $R ;;
+    fetch)  # HBM traffic: FETCH_SIZE and WRITE_SIZE, one pass each, over a 1-step run (BENCH_ARGS picks the workload)
+      cd /tmp
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace -d $R/gpurun_out/fetch_${TAG}_$c -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --warmup-s 0 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > $R/gpurun_out/fetch_${TAG}_$c.json 2> $R/gpurun_out/fetch_${TAG}_$c.err
+        rc=$?; echo "pass $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        python3 $R/tools/pmc_summary.py $(find $R/gpurun_out/fetch_${TAG}_$c -name '*counter_collection.csv') > $R/gpurun_out/fetch_${TAG}_$c.txt
+        cat $R/gpurun_out/fetch_${TAG}_$c.txt
       done
       cd $R ;;
     wl)

@@ -4,8 +4,11 @@
 
 #include <cstdint>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <string>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "rules.h"
@@ -88,14 +91,17 @@ class GpuEngine {
   bool Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_offsets, uint32_t n_files,
            std::vector<Candidate>* cands, BatchStats* st);
 
-  // Host-resident batch (PCIe-inclusive path): streamed in chunks through two
-  // device staging buffers, copies overlapping the previous chunk's kernels.
-  // With kinds (per file, xform.h), h_arena holds the bytes as read: each
-  // chunk is transformed on the GPU before the scan, and the transformed
-  // bytes of the files that got candidates come back in *tail.
+  // Host-resident batch (PCIe-inclusive path): streamed in chunks through the
+  // engine's staging ring (below), copies overlapping the kernels of earlier
+  // chunks -- of this call and of the calls before it.  With kinds (per file,
+  // xform.h), h_arena holds the bytes as read: each chunk is transformed on the
+  // GPU before the scan, and the transformed bytes of the files that got
+  // candidates come back in *tail.  Concurrent calls are allowed; the caller
+  // must NOT hold the engine's device lock: RunHost takes `dev_mu` (the lock
+  // the caller's other scans on this engine use) around each chunk's GPU work.
   bool RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds = nullptr,
-               TailOut* tail = nullptr);
+               TailOut* tail = nullptr, std::mutex* dev_mu = nullptr);
 
   // Split form of Run for pipelined callers: Enqueue (with the engine's lock
   // held) puts the whole GPU phase and the copies of the counters and of the
@@ -201,9 +207,33 @@ class GpuEngine {
                                     // [7] flagged-block records [8] record overflow
                                     // [9] fold sites [10] fold-site overflow
                                     // [6] full-scan list overflow [11] anchor-item matches [13] open pairs
-  // host-batch streaming (RunHost): two staging buffers, a copy stream
+  // host-batch streaming (RunHost): a ring of staging buffers, a copy stream
   hipStream_t copy_stream_ = nullptr;
   static constexpr int kNStage = 4;  // staging buffers: the copier runs up to three chunks ahead
+  // The staging ring.  RunHost reserves one slot per chunk, numbered in call
+  // arrival order across calls; slot s uses staging buffer s % kNStage.  One
+  // copier thread (CopierLoop) copies the slots in order, slot s as soon as
+  // slot s - kNStage has been scanned; chunks are scanned in slot order
+  // (ring_turn_).  So the copy engine moves the next call's first chunks while
+  // this call's last chunk is transformed, scanned and read back, and several
+  // small host batches in flight (the analyzer's collectors) overlap their
+  // copies with each other's kernels.
+  struct HostCall;
+  struct StageJob {
+    uint64_t slot;
+    HostCall* call;
+    uint32_t f0, f1;  // the chunk's files
+  };
+  bool CopyChunk(const StageJob& j, std::string* err);
+  void CopierLoop();
+  std::mutex ring_mu_;
+  std::condition_variable ring_cv_;
+  std::deque<StageJob> ring_jobs_;                     // reserved, not yet copied (slot order)
+  uint64_t ring_next_ = 0, ring_turn_ = 0, ring_copied_ = 0;  // next slot to reserve / to scan / copied below
+  bool stage_ok_[kNStage] = {};                        // the copy of the buffer's current slot was issued
+  std::string stage_err_[kNStage];
+  bool ring_stop_ = false;
+  std::thread copier_;
   hipEvent_t ev_copied_[kNStage] = {}, ev_h2d_[2] = {};
   void* d_stage_[kNStage] = {}; size_t cap_stage_[kNStage] = {};
   void* d_stage_off_[kNStage] = {}; size_t cap_stage_off_[kNStage] = {};

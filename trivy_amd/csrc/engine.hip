@@ -27,6 +27,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <pthread.h>
+
 #include <thread>
 #include <type_traits>
 
@@ -52,22 +54,40 @@ constexpr int kScanWaves = kScanThreads / 64;
 
 
 // K0: chunk c -> the file holding byte c * kChunk (off[f] <= c * kChunk <
-// off[f + 1], so never an empty file), one thread per chunk by a binary
-// search over the offsets (L2-resident).  A thread per file looping over its
-// chunks left a multi-MiB file's thousands of stores to one thread (0.19 ms
-// on C2 for 80 MB of map).
+// off[f + 1], so never an empty file).  A thread per run of 16 chunks: a
+// binary search over the offsets (L2-resident) for the first, a forward walk
+// for the rest, one 64-B store.  (A thread per file left a multi-MiB file's
+// thousands of stores to one thread; a search per chunk cost 20 dependent
+// loads per chunk, 0.32 ms on C2.)
+constexpr uint32_t kK0Run = 16;
 __global__ __launch_bounds__(256) void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
                                                         uint64_t n_chunks, uint32_t* __restrict__ chunk_file) {
-  for (uint64_t c = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; c < n_chunks;
-       c += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t x = c * kChunk;
+  const uint64_t n_runs = (n_chunks + kK0Run - 1) / kK0Run;
+  for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n_runs;
+       r += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t c0 = r * kK0Run;
+    uint64_t x = c0 * kChunk;
     uint32_t lo = 0, hi = n_files;  // the last f with off[f] <= x: off[lo] <= x < off[hi]
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
       if (off[mid] <= x) lo = mid;
       else hi = mid;
     }
-    chunk_file[c] = lo;
+    uint32_t v[kK0Run];
+    uint64_t fe = off[lo + 1];
+#pragma unroll
+    for (uint32_t i = 0; i < kK0Run; i++) {
+      x = (c0 + i) * kChunk;
+      while (x >= fe && lo + 1 < n_files) fe = off[++lo + 1];
+      v[i] = lo;
+    }
+    if (c0 + kK0Run <= n_chunks) {  // (the map is 64-B aligned: hipMalloc)
+      uint4* d = reinterpret_cast<uint4*>(chunk_file + c0);
+#pragma unroll
+      for (uint32_t q = 0; q < kK0Run / 4; q++) d[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+      for (uint32_t i = 0; c0 + i < n_chunks; i++) chunk_file[c0 + i] = v[i];
+    }
   }
 }
 
@@ -2254,6 +2274,12 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
 }
 
 GpuEngine::~GpuEngine() {
+  {
+    std::lock_guard<std::mutex> g(ring_mu_);
+    ring_stop_ = true;
+  }
+  ring_cv_.notify_all();
+  if (copier_.joinable()) copier_.join();
   hipSetDevice(device_);
   void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
@@ -2304,19 +2330,106 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
 
 // Host-resident batches (the analyzer's pinned arenas, a caller's registered
 // pool): the files are cut into chunks of at most chunk_bytes_ at file
-// boundaries and streamed through two device staging buffers.  The copy
-// stream moves chunk k+1 (arena + rebased offsets) while the kernels of chunk
-// k run on the scan stream (which waits on the chunk's copy event); Run()
-// returns only after chunk k's kernels finished, so the buffer it used is
-// free when chunk k+2's copy is issued.  Pinned host memory is required for
-// the copies to be asynchronous (hipHostMalloc / tsg_host_register).  The
-// copies are issued from a helper thread: on this runtime a 1-GiB
-// hipMemcpyAsync from registered memory returns only once the transfer is
-// done (measured, profiles/r02_ingest_trace_*), which would otherwise keep the
-// scan thread from launching chunk k's kernels during chunk k+1's copy.
+// boundaries and streamed through the staging ring (engine.h): the copier
+// thread moves chunk slots into the staging buffers on copy_stream_ while the
+// kernels of earlier slots run on the scan stream (which waits on the slot's
+// copy event).  Pinned host memory is required for the copies to be
+// asynchronous (hipHostMalloc / tsg_host_register).  The copies are issued off
+// the scanning threads: on this runtime a 1-GiB hipMemcpyAsync from registered
+// memory returns only once the transfer is done (profiles/r02_ingest_trace_*).
+struct GpuEngine::HostCall {
+  const uint8_t* h_arena;
+  const uint64_t* h_offsets;
+  const uint8_t* kinds;
+  bool cancelled = false;  // ring_mu_: a chunk failed; the call's later slots are not copied
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // first copy issued / last chunk scanned
+  bool ev0_recorded = false;
+};
+
+// One chunk slot into staging buffer slot % kNStage (copier thread).  The
+// buffer is free: slot - kNStage was scanned (its kernels and copy are done).
+// Errors go to *err (err_ belongs to the scanning threads).
+bool GpuEngine::CopyChunk(const StageJob& j, std::string* err) {
+  const int b = int(j.slot % kNStage);
+  const HostCall& c = *j.call;
+  const uint64_t a = c.h_offsets[j.f0], e = c.h_offsets[j.f1];
+  const uint32_t nf = j.f1 - j.f0;
+  auto fail = [&](const char* what, hipError_t x) {
+    *err = std::string(what) + ": " + hipGetErrorString(x);
+    return false;
+  };
+  auto grow = [&](void** p, size_t* cap, size_t need) -> hipError_t {
+    if (*p && *cap >= need) return hipSuccess;
+    if (*p) hipFree(*p);  // (implicitly synchronising; rare: a larger chunk than before)
+    *p = nullptr;
+    *cap = 0;
+    const hipError_t x = hipMalloc(p, need);
+    if (x == hipSuccess) *cap = need;
+    return x;
+  };
+  hipError_t x;
+  if ((x = hipEventSynchronize(ev_copied_[b])) != hipSuccess) return fail("staging event", x);  // h_off_[b] reusable
+  if ((x = grow(&d_stage_[b], &cap_stage_[b], (e - a) + 64)) != hipSuccess ||
+      (x = grow(&d_stage_off_[b], &cap_stage_off_[b], (size_t(nf) + 1) * 8)) != hipSuccess ||
+      (c.kinds && (x = grow(&d_kind_[b], &cap_kind_[b], size_t(nf) + 1)) != hipSuccess))
+    return fail("staging hipMalloc", x);
+  if (cap_h_off_[b] < size_t(nf) + 1) {
+    if (h_off_[b]) hipHostFree(h_off_[b]);
+    h_off_[b] = nullptr;
+    cap_h_off_[b] = 0;
+    if ((x = hipHostMalloc(reinterpret_cast<void**>(&h_off_[b]), (size_t(nf) + 1) * 8, hipHostMallocDefault)) !=
+        hipSuccess)
+      return fail("staging hipHostMalloc", x);
+    cap_h_off_[b] = size_t(nf) + 1;
+  }
+  for (uint32_t f = j.f0; f <= j.f1; f++) h_off_[b][f - j.f0] = c.h_offsets[f] - a;
+  if (!c.ev0_recorded) {
+    if ((x = hipEventRecord(c.ev0, copy_stream_)) != hipSuccess) return fail("hipEventRecord", x);
+    j.call->ev0_recorded = true;
+  }
+  uint8_t* d = static_cast<uint8_t*>(d_stage_[b]);
+  // in pieces of at most 1 GiB (a lone file can make a chunk of many GiB)
+  for (uint64_t p = a; p < e; p += uint64_t(1) << 30)
+    if ((x = hipMemcpyAsync(d + (p - a), c.h_arena + p, std::min<uint64_t>(e - p, uint64_t(1) << 30),
+                            hipMemcpyHostToDevice, copy_stream_)) != hipSuccess)
+      return fail("chunk copy", x);
+  if ((x = hipMemsetAsync(d + (e - a), 0, 64, copy_stream_)) != hipSuccess ||
+      (x = hipMemcpyAsync(d_stage_off_[b], h_off_[b], (size_t(nf) + 1) * 8, hipMemcpyHostToDevice, copy_stream_)) !=
+          hipSuccess ||
+      (c.kinds && (x = hipMemcpyAsync(d_kind_[b], c.kinds + j.f0, nf, hipMemcpyHostToDevice, copy_stream_)) !=
+                      hipSuccess) ||
+      (x = hipEventRecord(ev_copied_[b], copy_stream_)) != hipSuccess)
+    return fail("chunk copy", x);
+  return true;
+}
+
+void GpuEngine::CopierLoop() {
+  pthread_setname_np(pthread_self(), "tsg-copier");
+  (void)hipSetDevice(device_);
+  std::unique_lock<std::mutex> lk(ring_mu_);
+  for (;;) {
+    ring_cv_.wait(lk, [&] {
+      return ring_stop_ || (!ring_jobs_.empty() && ring_jobs_.front().slot < ring_turn_ + kNStage);
+    });
+    if (ring_stop_) return;  // (no call in flight: the engine is being destroyed)
+    const StageJob j = ring_jobs_.front();
+    ring_jobs_.pop_front();
+    const bool skip = j.call->cancelled;
+    lk.unlock();
+    std::string e;
+    const bool ok = !skip && CopyChunk(j, &e);
+    lk.lock();
+    const int b = int(j.slot % kNStage);
+    stage_ok_[b] = ok;
+    stage_err_[b] = skip ? std::string("cancelled") : e;
+    ring_copied_ = j.slot + 1;
+    ring_cv_.notify_all();
+  }
+}
+
 bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
-                        std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail) {
-  HIP_OK(hipSetDevice(device_));
+                        std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail,
+                        std::mutex* dev_mu) {
   cands->clear();
   BatchStats local;
   if (!st) st = &local;
@@ -2329,10 +2442,14 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     tail->raw.assign(n_files, 1);
     tail->xform_bytes = 0;
   }
-  if (kinds && !tail) {
-    err_ = "RunHost: a transformed batch needs a tail output";
+  std::string fail;  // (err_ is written only under dev_mu)
+  auto set_err = [&](const std::string& m) {
+    std::unique_lock<std::mutex> g;
+    if (dev_mu) g = std::unique_lock<std::mutex>(*dev_mu);
+    err_ = m;
     return false;
-  }
+  };
+  if (kinds && !tail) return set_err("RunHost: a transformed batch needs a tail output");
   if (n_files == 0) return true;
   std::vector<uint64_t> tail_len;  // per file: transformed bytes kept for the host (0: not a candidate file)
   if (kinds) tail_len.assign(n_files, 0);
@@ -2344,156 +2461,104 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
   }
   cut.push_back(n_files);
   const size_t n_chunks = cut.size() - 1;
-  uint64_t max_bytes = 0, max_files = 0;
-  for (size_t k = 0; k < n_chunks; k++) {
-    max_bytes = std::max<uint64_t>(max_bytes, h_offsets[cut[k + 1]] - h_offsets[cut[k]]);
-    max_files = std::max<uint64_t>(max_files, cut[k + 1] - cut[k]);
+  HostCall call{h_arena, h_offsets, kinds};
+  if (hipSetDevice(device_) != hipSuccess || hipEventCreate(&call.ev0) != hipSuccess ||
+      hipEventCreate(&call.ev1) != hipSuccess) {
+    if (call.ev0) hipEventDestroy(call.ev0);
+    return set_err("RunHost: hipEventCreate failed");
   }
-  for (int b = 0; b < kNStage && b < int(n_chunks); b++) {
-    if (!Ensure(&d_stage_[b], &cap_stage_[b], max_bytes + 64) ||
-        !Ensure(&d_stage_off_[b], &cap_stage_off_[b], (max_files + 1) * 8) ||
-        (kinds && !Ensure(&d_kind_[b], &cap_kind_[b], max_files + 1)))
-      return false;
-    if (cap_h_off_[b] < max_files + 1) {
-      if (h_off_[b]) hipHostFree(h_off_[b]);
-      h_off_[b] = nullptr;
-      cap_h_off_[b] = 0;
-      HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&h_off_[b]), (max_files + 1) * 8, hipHostMallocDefault));
-      cap_h_off_[b] = max_files + 1;
-    }
+  uint64_t s0;
+  {
+    std::lock_guard<std::mutex> g(ring_mu_);
+    if (!copier_.joinable()) copier_ = std::thread(&GpuEngine::CopierLoop, this);
+    s0 = ring_next_;
+    ring_next_ += n_chunks;
+    for (size_t k = 0; k < n_chunks; k++) ring_jobs_.push_back(StageJob{s0 + k, &call, cut[k], cut[k + 1]});
   }
-  auto copy = [&](size_t k) -> bool {  // chunk k -> staging buffer k % kNStage, on the copy stream
-    if (hipSetDevice(device_) != hipSuccess) return false;
-    const int b = int(k % kNStage);
-    const uint32_t f0 = cut[k], f1 = cut[k + 1];
-    const uint64_t a = h_offsets[f0], e = h_offsets[f1];
-    for (uint32_t f = f0; f <= f1; f++) h_off_[b][f - f0] = h_offsets[f] - a;
-    uint8_t* d = static_cast<uint8_t*>(d_stage_[b]);
-    // in pieces of at most 1 GiB (a lone file can make a chunk of many GiB)
-    for (uint64_t x = a; x < e; x += uint64_t(1) << 30)
-      HIP_OK(hipMemcpyAsync(d + (x - a), h_arena + x, std::min<uint64_t>(e - x, uint64_t(1) << 30),
-                            hipMemcpyHostToDevice, copy_stream_));
-    HIP_OK(hipMemsetAsync(d + (e - a), 0, 64, copy_stream_));
-    HIP_OK(hipMemcpyAsync(d_stage_off_[b], h_off_[b], (size_t(f1 - f0) + 1) * 8, hipMemcpyHostToDevice,
-                          copy_stream_));
-    if (kinds)
-      HIP_OK(hipMemcpyAsync(d_kind_[b], kinds + f0, size_t(f1 - f0), hipMemcpyHostToDevice, copy_stream_));
-    HIP_OK(hipEventRecord(ev_copied_[b], copy_stream_));
-    return true;
-  };
-  HIP_OK(hipEventRecord(ev_h2d_[0], copy_stream_));
-  // One copier thread issues the chunk copies in order, each into the staging
-  // buffer chunk k - kNStage freed (this thread has scanned it: Run returns
-  // after the chunk's kernels).  It runs up to kNStage - 1 chunks ahead, so the
-  // copy engine keeps streaming while this thread transforms, scans and reads
-  // back a chunk -- and while it waits for CPU time behind other scans' host
-  // work.  (A 1-GiB hipMemcpyAsync from registered memory returns only at
-  // completion on this runtime, profiles/r02_ingest_trace_*: the copies are
-  // issued off this thread.)
-  std::mutex cm;
-  std::condition_variable cv;
-  size_t issued = 0, scanned = 0;  // chunks copied (issued + event recorded) / scanned (buffer free)
-  bool stop = false;
-  std::string copy_err;
-  std::thread copier([&] {
-    for (size_t k = 0; k < n_chunks; k++) {
-      {
-        std::unique_lock<std::mutex> lk(cm);
-        cv.wait(lk, [&] { return stop || k < scanned + kNStage; });
-        if (stop) return;
-      }
-      // the previous use of h_off_[b] (chunk k - kNStage) is transferred: its event completed
-      if (k >= size_t(kNStage) && hipEventSynchronize(ev_copied_[k % kNStage]) != hipSuccess) {
-        std::lock_guard<std::mutex> g(cm);
-        copy_err = "staging event";
-        issued = n_chunks;
-        cv.notify_all();
-        return;
-      }
-      const bool ok = copy(k);
-      std::lock_guard<std::mutex> g(cm);
-      if (!ok) {
-        copy_err = err_.empty() ? "chunk copy failed" : err_;
-        issued = n_chunks;
-        cv.notify_all();
-        return;
-      }
-      issued = k + 1;
-      cv.notify_all();
-    }
-  });
-  auto finish = [&](bool ok) {
-    {
-      std::lock_guard<std::mutex> g(cm);
-      stop = true;
-    }
-    cv.notify_all();
-    copier.join();
-    if (!ok) (void)hipStreamSynchronize(copy_stream_);  // no copy into a staging buffer may outlive the call
-    return ok;
-  };
+  ring_cv_.notify_all();
+  bool ok = true;
   std::vector<Candidate> part;
   for (size_t k = 0; k < n_chunks; k++) {
-    const int b = int(k % kNStage);
-    {
-      std::unique_lock<std::mutex> lk(cm);
-      cv.wait(lk, [&] { return issued > k; });
-      if (!copy_err.empty()) {
-        err_ = copy_err;
-        lk.unlock();
-        return finish(false);
+    const uint64_t slot = s0 + k;
+    const int b = int(slot % kNStage);
+    bool copied;
+    {  // this slot's turn (slot order across calls) and its copy issued
+      std::unique_lock<std::mutex> lk(ring_mu_);
+      ring_cv_.wait(lk, [&] { return ring_turn_ == slot && ring_copied_ > slot; });
+      copied = stage_ok_[b];
+      if (ok && !copied) {
+        ok = false;
+        fail = "staging: " + stage_err_[b];
+      }
+      if (!ok) call.cancelled = true;
+    }
+    if (ok) {
+      std::unique_lock<std::mutex> g;
+      if (dev_mu) g = std::unique_lock<std::mutex>(*dev_mu);
+      const uint32_t f0 = cut[k], f1 = cut[k + 1];
+      BatchStats cs;
+      const uint8_t* scan_arena = static_cast<const uint8_t*>(d_stage_[b]);
+      const uint64_t* scan_off = static_cast<const uint64_t*>(d_stage_off_[b]);
+      uint64_t scan_bytes = h_offsets[f1] - h_offsets[f0];
+      std::vector<uint64_t> xoff;
+      float ms_x = 0;
+      ok = hipSetDevice(device_) == hipSuccess && hipStreamWaitEvent(stream_, ev_copied_[b], 0) == hipSuccess &&
+           (!kinds || Transform(b, f1 - f0, &scan_arena, &scan_off, &scan_bytes, &xoff, &ms_x)) &&
+           Run(scan_arena, scan_bytes, scan_off, f1 - f0, &part, &cs);
+      if (ok && kinds) {
+        st->ms_xform += ms_x;
+        cs.ms_total += ms_x;
+        tail->xform_bytes += scan_bytes;
+        ok = GatherTail(part, f0, f1 - f0, xoff, h_offsets + f0, kinds + f0, &tail_len, tail);
+      }
+      if (ok && k + 1 == n_chunks) ok = hipEventRecord(call.ev1, stream_) == hipSuccess;
+      if (!ok) fail = err_.empty() ? std::string("RunHost: chunk scan failed") : err_;
+      if (ok) {
+        for (auto c : part) {
+          c.file += f0;
+          cands->push_back(c);
+        }
+        st->hits += cs.hits;
+        st->follow_hits += cs.follow_hits;
+        st->candidates += cs.candidates;
+        st->special_files += cs.special_files;
+        st->flagged_blocks += cs.flagged_blocks;
+        st->hit_overflow = st->hit_overflow || cs.hit_overflow;
+        st->cand_overflow = st->cand_overflow || cs.cand_overflow;
+        st->ms_scan += cs.ms_scan;
+        st->ms_confirm += cs.ms_confirm;
+        st->ms_careful += cs.ms_careful;
+        st->ms_verify += cs.ms_verify;
+        st->ms_fullscan += cs.ms_fullscan;
+        st->fullscan_tasks += cs.fullscan_tasks;
+        st->fold_sites += cs.fold_sites;
+        st->ms_finalize += cs.ms_finalize;
+        st->ms_chunkmap += cs.ms_chunkmap;
+        st->ms_total += cs.ms_total;
       }
     }
-    HIP_OK(hipStreamWaitEvent(stream_, ev_copied_[b], 0));
-    const uint32_t f0 = cut[k], f1 = cut[k + 1];
-    BatchStats cs;
-    const uint8_t* scan_arena = static_cast<const uint8_t*>(d_stage_[b]);
-    const uint64_t* scan_off = static_cast<const uint64_t*>(d_stage_off_[b]);
-    uint64_t scan_bytes = h_offsets[f1] - h_offsets[f0];
-    std::vector<uint64_t> xoff;
-    float ms_x = 0;
-    if (kinds && !Transform(b, f1 - f0, &scan_arena, &scan_off, &scan_bytes, &xoff, &ms_x)) return finish(false);
-    if (!Run(scan_arena, scan_bytes, scan_off, f1 - f0, &part, &cs)) return finish(false);
-    {  // the chunk's kernels are done with staging buffer b
-      std::lock_guard<std::mutex> g(cm);
-      scanned = k + 1;
+    // the staging buffer goes to slot + kNStage only once nothing reads it
+    // (a scanned slot's copy and kernels are done: Run waited for them)
+    if (!ok) {
+      if (copied) (void)hipStreamSynchronize(copy_stream_);
+      (void)hipStreamSynchronize(stream_);  // a failed chunk's kernels may still be queued
     }
-    cv.notify_all();
-    if (kinds) {
-      st->ms_xform += ms_x;
-      cs.ms_total += ms_x;
-      tail->xform_bytes += scan_bytes;
-      if (!GatherTail(part, f0, f1 - f0, xoff, h_offsets + f0, kinds + f0, &tail_len, tail)) return finish(false);
+    {
+      std::lock_guard<std::mutex> g(ring_mu_);
+      ring_turn_ = slot + 1;
     }
-    for (auto c : part) {
-      c.file += f0;
-      cands->push_back(c);
-    }
-    st->hits += cs.hits;
-    st->follow_hits += cs.follow_hits;
-    st->candidates += cs.candidates;
-    st->special_files += cs.special_files;
-    st->flagged_blocks += cs.flagged_blocks;
-    st->hit_overflow = st->hit_overflow || cs.hit_overflow;
-    st->cand_overflow = st->cand_overflow || cs.cand_overflow;
-    st->ms_scan += cs.ms_scan;
-    st->ms_confirm += cs.ms_confirm;
-    st->ms_careful += cs.ms_careful;
-    st->ms_verify += cs.ms_verify;
-    st->ms_fullscan += cs.ms_fullscan;
-    st->fullscan_tasks += cs.fullscan_tasks;
-    st->fold_sites += cs.fold_sites;
-    st->ms_finalize += cs.ms_finalize;
-    st->ms_chunkmap += cs.ms_chunkmap;
-    st->ms_total += cs.ms_total;
+    ring_cv_.notify_all();
   }
-  finish(true);
-  HIP_OK(hipEventRecord(ev_h2d_[1], copy_stream_));
-  HIP_OK(hipEventSynchronize(ev_h2d_[1]));
-  hipEventElapsedTime(&st->ms_h2d_span, ev_h2d_[0], ev_h2d_[1]);
-  st->h2d_chunks = n_chunks;
-  if (kinds)
-    for (uint32_t f = 0; f < n_files; f++) tail->off[f + 1] = tail->off[f] + tail_len[f];
+  if (ok) {
+    ok = hipEventSynchronize(call.ev1) == hipSuccess;
+    hipEventElapsedTime(&st->ms_h2d_span, call.ev0, call.ev1);
+    st->h2d_chunks = n_chunks;
+    if (kinds)
+      for (uint32_t f = 0; f < n_files; f++) tail->off[f + 1] = tail->off[f] + tail_len[f];
+  }
+  hipEventDestroy(call.ev0);
+  hipEventDestroy(call.ev1);
+  if (!ok) return set_err(fail.empty() ? std::string("RunHost failed") : fail);
   return true;
 }
 
@@ -2758,7 +2823,8 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   if (d_item_diag_) HIP_OK(hipMemsetAsync(d_item_diag_, 0, 8 * std::max<size_t>(n_fitems_, 1), stream_));
   {  // every chunk below n_bytes gets its file (no clear needed)
     const uint64_t used = (n_bytes + kChunk - 1) / kChunk;
-    const uint32_t blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((used + 255) / 256, 8192)));
+    const uint64_t runs = (used + kK0Run - 1) / kK0Run;
+    const uint32_t blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((runs + 255) / 256, 8192)));
     chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, used, static_cast<uint32_t*>(d_chunk_file_));
   }
   // K1: streaming filter -> flagged block records

@@ -1213,18 +1213,21 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     return false;
   }
   GpuEngine::Ticket ticket;
-  {
+  if (!in.dev_arena) {  // the staging ring orders concurrent host batches; it takes the lock per chunk
+    ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
+                         in.transform ? &tail : nullptr, &gpu_mu_[slot]);
+    if (!ok) {
+      std::lock_guard<std::mutex> g(gpu_mu_[slot]);
+      gpu_err = engine->error();
+    }
+  } else {
     std::lock_guard<std::mutex> g(gpu_mu_[slot]);
     static const bool tickets = !std::getenv("TSG_TICKETS") || std::atoi(std::getenv("TSG_TICKETS")) != 0;
     std::string enq_err;  // a failed Enqueue (no free ticket, or a HIP error) falls back to Run
-    if (in.dev_arena && tickets && engine->Enqueue(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &ticket,
-                                                   &enq_err))
+    if (tickets && engine->Enqueue(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &ticket, &enq_err))
       ok = true;  // collected below, after the lock is released
-    else if (in.dev_arena)
-      ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
     else
-      ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
-                           in.transform ? &tail : nullptr);
+      ok = engine->Run(in.dev_arena, n_bytes, in.dev_offsets, in.n_files, &cands, gst);
     if (!ok && gpu_err.empty()) gpu_err = engine->error();
   }
   if (ticket.slot >= 0) {
