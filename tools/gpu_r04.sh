@@ -61,6 +61,16 @@ for st in $STAGES; do
     large)  # the > 4 GiB transformed-file test alone (last: it moves ~9 GB through the box)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_large_file.py -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_large_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_large_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    abenv)  # C2 A/B over "variant[:ENV=V ...]" specs ('|'-separated AB_SPECS; variant base = the in-tree build), twice interleaved
+      IFS='|' read -r -a specs <<< "${AB_SPECS:-base}"
+      for rep in 1 2; do
+        for i in "${!specs[@]}"; do
+          sp="${specs[$i]}"; v="${sp%%:*}"; E=""; [ "$sp" != "$v" ] && E="${sp#*:}"
+          if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
+          env TSG_LIB=$L $E timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > gpurun_out/abenv_${TAG}_${i}_$rep.json 2> gpurun_out/abenv_${TAG}_${i}_$rep.err
+          rc=$?; echo "== [$i] $sp $rep"; python tools/bench_brief.py gpurun_out/abenv_${TAG}_${i}_$rep.json; [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
     ingab)  # ingest leg A/B of library variants (VARIANTS; base = the in-tree build), twice interleaved
       for rep in 1 2; do
         for v in ${VARIANTS:-base}; do

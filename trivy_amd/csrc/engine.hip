@@ -112,7 +112,10 @@ constexpr int kFFlushAt = 128;                      // flush the flagged-block q
 constexpr int kFQueue = kFFlushAt + 64;             // per-wave queue entries (a block column appends <= 64)
 constexpr int kFChunks = kFTile / 1024;             // newline chunks per tile (kChunk = 1 KiB)
 constexpr int kFNlTiles = 16;                       // tiles whose newline counts a wave stages in LDS
-constexpr int kFWgPerCu = 2;
+#ifndef TSG_K1_WGS
+#define TSG_K1_WGS 2
+#endif
+constexpr int kFWgPerCu = TSG_K1_WGS;  // 1: leaves ~80 KiB of LDS per CU to a concurrent scan's confirm kernel
 #ifndef TSG_K1_READAHEAD
 #define TSG_K1_READAHEAD 4
 #endif
@@ -180,7 +183,9 @@ __device__ __forceinline__ void load_reach_lds(uint8_t* s_reach, const uint32_t*
 // 4 slots are popcounted.  Flagged blocks go through a ballot/mbcnt-compacted
 // per-wave LDS queue to the global record list (one atomic per 64 records);
 // the confirm kernel (K2) checks them exactly.
-__global__ __launch_bounds__(kScanThreads, 4 * kFWgPerCu) void filter_kernel(FilterParams P) {
+// (<= 64 VGPRs in both shapes: with one workgroup per CU the other half of the
+// VGPRs and LDS go to a concurrent scan's confirm kernel)
+__global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
   __shared__ uint32_t s_queue[kScanWaves * kFQueue];
   __shared__ uint64_t s_nl[kScanWaves * kFNlTiles];  // per wave: the last tiles' 4 chunk counts
