@@ -90,7 +90,7 @@ PYEOF
       for rep in 1 2; do
         for i in base "${!envs[@]}"; do
           if [ "$i" = base ]; then E=""; v=base; else E="${envs[$i]}"; v=alt$i; fi
-          env $E timeout -k 10 600 python bench.py --workload c4 --steps 5 --warmup 2 --no-cpu-baseline ${C4_ARGS:-} > gpurun_out/c4ab_${TAG}_${v}_$rep.json 2> gpurun_out/c4ab_${TAG}_${v}_$rep.err
+          env $E timeout -k 10 600 python bench.py --workload c4 --steps ${C4_STEPS:-5} --warmup 2 --no-cpu-baseline ${C4_ARGS:-} > gpurun_out/c4ab_${TAG}_${v}_$rep.json 2> gpurun_out/c4ab_${TAG}_${v}_$rep.err
           rc=$?; echo "== c4 $v $rep ($E)"; python tools/bench_brief.py gpurun_out/c4ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
         done
       done ;;

@@ -246,6 +246,24 @@ __device__ __forceinline__ void x_stage_files(Pos* so, uint8_t* sk, const XFileR
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// An identity tile, decided from the tile's bytes and its staged file table
+// alone (no per-block segment walk): no '\r' in the tile, no kind-2 file
+// starting in it or holding its first byte, at most 64 files starting in it,
+// and no file starting exactly at its first byte (empty files before that one
+// are named by no staged entry).  Its output is its input: the count is its
+// length and a file starting in it starts at the same tile offset.
+// Conservative: a tile failing the test takes the exact per-block path.
+template <typename Pos>
+__device__ __forceinline__ bool x_fast_identity(const uint4& v, const Pos* so, const uint8_t* sk, uint32_t tf,
+                                                Pos t0, Pos tend, uint32_t lane) {
+  const uint32_t cr = eq_bytes(v.x, 0x0D0D0D0Du) | eq_bytes(v.y, 0x0D0D0D0Du) | eq_bytes(v.z, 0x0D0D0D0Du) |
+                      eq_bytes(v.w, 0x0D0D0D0Du);
+  const bool k2 = so[lane] < tend && sk[lane] == kXformPrintable;  // file tf + lane holds bytes of the tile
+  const bool many = so[64] < tend;                                  // file tf + 64 starts in the tile
+  const bool edge = so[0] == t0 && tf > 0;
+  return !__any(cr != 0u || k2) && !many && !edge;
+}
+
 // A lane's block in file order.  For each file segment [s, e) of the block:
 // start(f, count so far) at a file starting inside the block (empty files
 // too), then out(emit mask, nl-before mask, nl-after mask) over the block's
@@ -329,6 +347,15 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
     const uint4 vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
     const uint32_t tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
     const XFileRegs<Pos> frn = t + waves < n_tiles ? x_file_regs<Pos>(off, kind, n_files, tfn, lane) : fr;
+    const Pos t0 = Pos(t) * kXTile, tend = t0 + kXTile < n_bytes ? t0 + kXTile : n_bytes;
+    if (x_fast_identity(v, so, sk, tf, t0, tend, lane)) {
+      if (lane == 0) tile_cnt[t] = uint64_t(tend - t0);
+      if (so[lane] >= t0 && so[lane] < tend) fstart[tf + lane] = uint32_t(so[lane] - t0);
+      v = vn;
+      tf = tfn;
+      fr = frn;
+      continue;
+    }
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // file starts: tile-relative output offsets once the lane's prefix is known
     uint32_t sf[4], sc[4], ns = 0;
@@ -402,42 +429,49 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
     tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
     pren = t + waves < n_tiles ? tile_pre[t + waves] : 0u;
     if (t + waves < n_tiles) frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
-    const XWindow W = x_window(raw, n_bytes, blk, lane, v);
+    const Pos t0 = Pos(t) * kXTile;
+    const bool fast = t0 + kXTile <= n_bytes && x_fast_identity(v, so, sk, tf, t0, t0 + Pos(kXTile), lane);
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
-    uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0, added = 0;
-    const uint32_t c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
-                              [&](uint32_t K, uint32_t C, uint32_t Z) {
-                                if (nseg < 4) {
-                                  segK[nseg] = K;
-                                  segC[nseg] = C;
-                                  segZ[nseg] = Z;
-                                }
-                                nseg++;
-                                kept |= K;
-                                added |= C | Z;
-                              });
+    uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0xFFFFu, added = 0, c = 16;
+    XWindow W;
+    if (!fast) {
+      W = x_window(raw, n_bytes, blk, lane, v);
+      kept = 0;
+      c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
+                 [&](uint32_t K, uint32_t C, uint32_t Z) {
+                   if (nseg < 4) {
+                     segK[nseg] = K;
+                     segC[nseg] = C;
+                     segZ[nseg] = Z;
+                   }
+                   nseg++;
+                   kept |= K;
+                   added |= C | Z;
+                 });
+    }
     const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
-    if (__all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
+    if (fast || __all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
       // An identity tile (no CR dropped, no printable-run edits, a whole KiB):
       // its output is its input moved to `start`, so each lane writes one
       // aligned 16-B block composed from its own and the previous lane's bytes
       // (a byte shift by the tile's output phase), no staging.
-      uint32_t P[4] = {__shfl_up(v.x, 1), __shfl_up(v.y, 1), __shfl_up(v.z, 1), __shfl_up(v.w, 1)};
-      const uint32_t X[8] = {P[0], P[1], P[2], P[3], v.x, v.y, v.z, v.w};  // prev ++ own
-      const uint32_t sh = 16u - phase;  // output block = X[sh .. sh + 16)
-      const uint32_t q = sh >> 2, r = 8u * (sh & 3u);
+      const uint32_t X[9] = {__shfl_up(v.x, 1), __shfl_up(v.y, 1), __shfl_up(v.z, 1), __shfl_up(v.w, 1),
+                             v.x, v.y, v.z, v.w, 0u};  // prev ++ own
+      const uint32_t sh = 16u - phase;  // output block = X bytes [sh, sh + 16)
+      const uint32_t rb = sh & 3u;
       uint32_t o[4];
-#pragma unroll
-      for (uint32_t i = 0; i < 4; i++) {
-        // X[q + i], X[q + i + 1] with q wave-uniform (0..4)
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 5; k++)
-          if (q == k) {
-            lo = X[k + i];
-            hi = k + i + 1 < 8 ? X[k + i + 1] : 0u;
-          }
-        o[i] = r ? (lo >> r) | (hi << (32u - r)) : lo;
+      switch (sh >> 2) {  // wave-uniform
+#define TSG_XO(k)                                                                  \
+  case k:                                                                          \
+    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(X[k + i + 1], X[k + i], rb); \
+    break;
+        TSG_XO(0)
+        TSG_XO(1)
+        TSG_XO(2)
+        TSG_XO(3)
+        default:
+          for (int i = 0; i < 4; i++) o[i] = X[4 + i];  // phase 0
+#undef TSG_XO
       }
       const uint64_t base = start - phase;
       const uint64_t g = base + 16u * lane;
@@ -445,14 +479,20 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
         if (lane == 0) atomicOr(err, 1u);
         continue;
       }
-      if (lane > 0 || phase == 0) {
-        *reinterpret_cast<uint4*>(out + g) = make_uint4(o[0], o[1], o[2], o[3]);
-      } else {  // block 0: the previous tile owns out[base, start)
-        for (uint32_t j = phase; j < 16; j++) out[g + j] = uint8_t(o[j >> 2] >> (8 * (j & 3)));
-      }
-      if (lane == 0 && phase) {  // the last `phase` bytes spill into block 64
-        const uint8_t* src = raw + uint64_t(t) * kXTile + kXTile - phase;
-        for (uint32_t j = 0; j < phase; j++) out[base + kXTile + j] = src[j];
+      if (lane > 0 || phase == 0) *reinterpret_cast<uint4*>(out + g) = make_uint4(o[0], o[1], o[2], o[3]);
+      if (phase) {  // the ragged ends, a byte per lane: the previous tile owns out[base, start)
+        const uint32_t jb = lane & 15u;
+        // lanes 0-15: lane 0's block, bytes [phase, 16); lanes 16-31: the tile's last
+        // `phase` bytes, which spill into block 64 (lane 63's bytes [16 - phase, 16))
+        const bool head = lane < 16;
+        const uint32_t src = head ? 0u : 63u, b = head ? jb : 16u - phase + jb;
+        const uint32_t a0 = __builtin_amdgcn_readlane(o[0], 0), a1 = __builtin_amdgcn_readlane(o[1], 0),
+                       a2 = __builtin_amdgcn_readlane(o[2], 0), a3 = __builtin_amdgcn_readlane(o[3], 0);
+        const uint32_t c0 = __builtin_amdgcn_readlane(v.x, 63), c1 = __builtin_amdgcn_readlane(v.y, 63),
+                       c2 = __builtin_amdgcn_readlane(v.z, 63), c3 = __builtin_amdgcn_readlane(v.w, 63);
+        const uint32_t w = b < 8 ? (b < 4 ? (src ? c0 : a0) : (src ? c1 : a1)) : (b < 12 ? (src ? c2 : a2) : (src ? c3 : a3));
+        if (head ? jb >= phase : (lane < 32 && jb < phase))
+          out[head ? base + jb : base + kXTile + jb] = uint8_t(w >> (8 * (b & 3)));
       }
       continue;
     }
@@ -528,6 +568,17 @@ static bool XformWide(uint64_t n_bytes) {
   return (e && std::atoi(e) != 0) || n_bytes >= (uint64_t(1) << 32) - 64;
 }
 
+// Workgroups of the count / write kernels (TSG_XFORM_GRID; tuning): each wave
+// walks tiles grid-strided with the next tile's loads in flight.
+static uint32_t XformGrid() {
+  static const uint32_t g = [] {
+    const char* e = std::getenv("TSG_XFORM_GRID");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? uint32_t(v) : 8192u;
+  }();
+  return g;
+}
+
 static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   XformScratch L;
@@ -569,7 +620,7 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (n_tiles) {
-    const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
+    const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), XformGrid()));
     if (wide)
       xf_count_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart);
     else
@@ -590,7 +641,7 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   const uint8_t* sc = static_cast<const uint8_t*>(scratch);
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   if (!n_tiles) return hipSuccess;
-  const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), 8192));
+  const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), XformGrid()));
   const uint32_t* cf = reinterpret_cast<const uint32_t*>(sc + L.chunk_file);
   const uint64_t* tp = reinterpret_cast<const uint64_t*>(sc + L.tile_pre);
   uint32_t* err = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(sc) + L.err);
