@@ -222,9 +222,9 @@ WORKLOADS = {
             "per MI355X (BASELINE configs[2], VERDICT r02 #6)", 8.0, 2.0, 0.4),
     "c1fs": ("`trivy fs` over a %g GB synthetic source tree on tmpfs (the C1/C2 generator's files and paths): "
              "FS.Walk + Required + reads straight into double-buffered pinned arenas + GPU pre-transform + scan "
-             "(BASELINE configs[0] end to end on the GPU; SURVEY §8(f)1)", 1.0, 1000.0, 0.0),
+             "(BASELINE configs[0] end to end on the GPU; SURVEY §8(f)1)", 1.0, 1000.0, 2.0),
     "c4": ("image layer scan: %g GB of small files (median 1.5 KiB) in a synthetic uncompressed tar layer per "
-           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 120.0, 0.0),
+           "MI355X, native walk + arena packing + scan (BASELINE configs[3])", 12.0, 120.0, 2.0),
 }
 
 
@@ -306,7 +306,37 @@ def _cpu_model():
     return ""
 
 
-def cpu_baseline_fs(root, cores, gpu_result=None):
+def oracle_vs_gpu(a, rels, datas, bins, gpu_result, max_bytes):
+    """The Python oracle (oracle/secret_scanner.py, pinned by the reference's golden tests) on the
+    first files of a prepared analyzer sample vs the GPU's findings for the same files (the
+    AnalysisResult of the timed path's analyzer): the line's parity block.  Findings compare as
+    their JSON dicts, each file's in (RuleID, StartLine) order (AnalysisResult.Sort)."""
+    gpu = {}
+    for s_ in gpu_result.Secrets:
+        gpu[s_.FilePath] = s_.to_dict()
+
+    def key(f):
+        return (f["RuleID"], f["StartLine"])
+    n = bad = nf = used = 0
+    first = None
+    for rel, data, b in zip(rels, datas, bins):
+        if n and used + len(data) > max_bytes:
+            break
+        want = sorted(a.scanner.scan(rel, data, b)["Findings"] or [], key=key)
+        got = sorted((gpu.get(rel) or {}).get("Findings") or [], key=key)
+        n += 1
+        used += len(data)
+        nf += len(want)
+        if want != got:
+            bad += 1
+            first = rel if first is None else first
+    return {"files": n, "bytes": used, "findings": nf, "mismatches": bad, "first_mismatch": first,
+            "reference": "oracle/secret_scanner.py (scanner.go:377-463 restated, pinned by the reference's "
+                         "golden tests) on the first files of the CPU-baseline sample, after the restated "
+                         "analyzer steps (oracle/analyzer.py)"}
+
+
+def cpu_baseline_fs(root, cores, gpu_result=None, parity_bytes=0):
     """The same tree through the reference's CPU path, restated: FS.Walk + Required in Python
     (oracle/analyzer.py walk_fs / required, os.scandir order), each file read and CR-stripped,
     then tsg_cpuref_scan (the restated reference CPU scan, C++) on `cores` threads and on 5
@@ -340,10 +370,12 @@ def cpu_baseline_fs(root, cores, gpu_result=None):
            "runs": runs, "cpu_model": _cpu_model()}
     if gpu_result is not None:
         out["gpu_vs_cpuref_all_files"] = _diff_secrets(gpu_result.Secrets, res, rels)
+        if parity_bytes:
+            out["parity"] = oracle_vs_gpu(a, rels, datas, bins, gpu_result, parity_bytes)
     return out
 
 
-def cpu_baseline_layer_cpp(layer, cores, gpu_result=None):
+def cpu_baseline_layer_cpp(layer, cores, gpu_result=None, parity_bytes=0):
     """A layer sample through the reference's CPU path, restated: LayerTar.Walk + Required +
     ReadAll / CR strip / ExtractPrintableBytes in Python (oracle/analyzer.py walk_layer_tar,
     tarfile), then tsg_cpuref_scan (C++) on `cores` threads and on 5; GB/s of the files
@@ -376,6 +408,8 @@ def cpu_baseline_layer_cpp(layer, cores, gpu_result=None):
            "runs": runs, "cpu_model": _cpu_model()}
     if gpu_result is not None:
         out["gpu_vs_cpuref_all_files"] = _diff_secrets(gpu_result.Secrets, res, rels)
+        if parity_bytes:
+            out["parity"] = oracle_vs_gpu(a, rels, datas, bins, gpu_result, parity_bytes)
     return out
 
 
@@ -674,7 +708,7 @@ def main():
 
     # Ingest-inclusive leg of a resident c2 run (value stays the HBM-resident rate): the same corpus
     # page-locked on the host, every byte copied host->HBM inside the timed region through the
-    # engine's two staging buffers and copy stream (tsg_scan_submit without a device arena).
+    # engine's staging ring and copy stream (tsg_scan_submit without a device arena).
     ingest = None
     unregister_leg = None
     res_timed = last_res[0]  # the timed steps' last result (parity below)
@@ -706,7 +740,8 @@ def main():
                   "achieved_h2d": round(h2d, 2), "h2d_peak_measured": peak, "frac_h2d": round(h2d / peak, 4),
                   "h2d_chunks_per_scan": int(ist[-1].get("h2d_chunks", 0)),
                   "note": "same corpus and scanner, host-resident (page-locked) arena: H2D of every byte inside "
-                          "the timed region, overlapped with the kernels (two staging buffers, copy stream)"
+                          "the timed region, overlapped with the kernels (the engine's staging ring: one copier thread, "
+                          "four staging buffers, copy stream)"
                           + ("; the files as read (%d CRLF), CR-stripped on the GPU (xform.hip) inside the timed "
                              "region" % int(R.crlf.sum()) if R is not None else "")}
     pre = "" if layer is None else "scan_"
@@ -791,7 +826,7 @@ def main():
         roofline["h2d_peak_measured"] = h2d_peak
         roofline["frac_h2d"] = round(h2d / h2d_peak, 4)
         roofline["h2d_note"] = ("per GPU: arena bytes / step time with every byte copied host->HBM in the timed region "
-                                "(%d chunks per scan, two staging buffers); peak = pinned hipMemcpyAsync on this box"
+                                "(%d chunks per scan through the staging ring); peak = pinned hipMemcpyAsync on this box"
                                 % int(last.get("h2d_chunks", 0)))
 
     if rank == 0:
@@ -809,12 +844,14 @@ def main():
             elif args.workload == "c1fs":
                 from trivy_amd.walker import Option
                 res_fs = an.AnalyzeFS(layer, Option(), colls=colls)  # findings of the same walk, materialized
-                cpu = cpu_baseline_fs(layer, cores, gpu_result=res_fs)
+                cpu = cpu_baseline_fs(layer, cores, gpu_result=res_fs, parity_bytes=int(args.parity_mb * 1e6))
+                parity = cpu.pop("parity", None)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
                 res_l = an.AnalyzeLayer(sample, colls=[Collector(an, args.arena_mb << 20, gx)
                                                        for _ in range(args.collectors)])
-                cpu = cpu_baseline_layer_cpp(sample, cores, gpu_result=res_l)
+                cpu = cpu_baseline_layer_cpp(sample, cores, gpu_result=res_l, parity_bytes=int(args.parity_mb * 1e6))
+                parity = cpu.pop("parity", None)
         out = {
             "metric": "GB/s secret-scanned (whole node) at 1/2/4/8 MI355X; findings bit-exact vs CPU",
             "value": round(value, 3),
