@@ -519,3 +519,14 @@ def test_gpu_xform_wide_positions_vs_oracle(monkeypatch):
     test_gpu_xform_bytes_vs_oracle()
     test_gpu_xform_identity_tiles_vs_oracle()
     test_gpu_xform_empty_files_at_tile_starts()
+
+
+@pytest.mark.gpu
+def test_gpu_xform_one_pass_vs_oracle(monkeypatch):
+    """The one-pass pre-transform (decoupled look-back over the tiles' output lengths,
+    TSG_XFORM_ONEPASS=1; off by default) on the same edge-case batches as the default
+    two passes, byte for byte."""
+    monkeypatch.setenv("TSG_XFORM_ONEPASS", "1")
+    test_gpu_xform_bytes_vs_oracle()
+    test_gpu_xform_identity_tiles_vs_oracle()
+    test_gpu_xform_empty_files_at_tile_starts()

@@ -60,7 +60,17 @@ int tsg_debug_xform(int device, const uint8_t* raw, uint64_t n_bytes, const uint
       ok(hipMalloc(&d_xoff, (size_t(n_files) + 1) * 8)) && ok(hipMalloc(&d_sc, sc_bytes)) &&
       ok(hipMemset(d_raw, 0, n_bytes + 64)) && ok(hipMemcpy(d_raw, raw, n_bytes, hipMemcpyHostToDevice)) &&
       ok(hipMemcpy(d_off, offsets, (size_t(n_files) + 1) * 8, hipMemcpyHostToDevice)) &&
-      ok(hipMemcpy(d_kind, kinds, n_files, hipMemcpyHostToDevice)) &&
+      ok(hipMemcpy(d_kind, kinds, n_files, hipMemcpyHostToDevice)) && tsg::XformOnePassOn()) {
+    const uint64_t cap = tsg::XformMaxOut(n_bytes, n_files) + 64;  // (the engine's bound)
+    if (ok(hipMalloc(&d_out, cap)) &&
+        ok(tsg::XformOnePass(static_cast<const uint8_t*>(d_raw), n_bytes, static_cast<const uint64_t*>(d_off),
+                             static_cast<const uint8_t*>(d_kind), n_files, d_sc, static_cast<uint64_t*>(d_xoff),
+                             static_cast<uint8_t*>(d_out), cap, s)) &&
+        ok(hipMemcpyAsync(xoff, d_xoff, (size_t(n_files) + 1) * 8, hipMemcpyDeviceToHost, s)) &&
+        ok(hipStreamSynchronize(s)) &&
+        ok(tsg::XformErrorWord(n_bytes, n_files, d_sc, s) == 0 ? hipSuccess : hipErrorIllegalAddress))
+      ok(hipMemcpy(out, d_out, std::min<uint64_t>(out_cap, xoff[n_files]), hipMemcpyDeviceToHost));
+  } else if (ok(e) &&
       ok(tsg::XformPlan(static_cast<const uint8_t*>(d_raw), n_bytes, static_cast<const uint64_t*>(d_off),
                         static_cast<const uint8_t*>(d_kind), n_files, d_sc, static_cast<uint64_t*>(d_xoff), s)) &&
       ok(hipMemcpyAsync(xoff, d_xoff, (size_t(n_files) + 1) * 8, hipMemcpyDeviceToHost, s)) &&

@@ -2593,8 +2593,12 @@ bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint6
   uint8_t* out = static_cast<uint8_t*>(d_xf_);
   h_xoff_[nf + 1] = 0;
   HIP_OK(hipEventRecord(ev_x_[0], stream_));
-  HIP_OK(XformPlan(raw, raw_bytes, off, kd, nf, d_xscan_, xo, stream_));
-  HIP_OK(XformWrite(raw, raw_bytes, off, kd, nf, d_xscan_, out, cap_xf_, stream_));
+  if (XformOnePassOn()) {
+    HIP_OK(XformOnePass(raw, raw_bytes, off, kd, nf, d_xscan_, xo, out, cap_xf_, stream_));
+  } else {
+    HIP_OK(XformPlan(raw, raw_bytes, off, kd, nf, d_xscan_, xo, stream_));
+    HIP_OK(XformWrite(raw, raw_bytes, off, kd, nf, d_xscan_, out, cap_xf_, stream_));
+  }
   HIP_OK(hipMemcpyAsync(h_xoff_, xo, (size_t(nf) + 1) * 8, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipMemcpyAsync(h_xoff_ + nf + 1, XformErrorPtr(raw_bytes, nf, d_xscan_), 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipEventRecord(ev_x_[1], stream_));

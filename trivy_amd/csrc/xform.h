@@ -22,6 +22,14 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
                      void* scratch, uint64_t* xoff, hipStream_t s);
 hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                       const void* scratch, uint8_t* out, uint64_t out_cap, hipStream_t s);
+// One pass (TSG_XFORM_ONEPASS=1; off by default, slower: xform.hip): XformOnePass
+// writes xoff and out together (a decoupled look-back over the tiles' output
+// lengths).  out_cap must hold the bound XformMaxOut -- the offsets are known
+// only when the call's work is done.
+bool XformOnePassOn();
+hipError_t XformOnePass(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind,
+                        uint32_t n_files, void* scratch, uint64_t* xoff, uint8_t* out, uint64_t out_cap,
+                        hipStream_t s);
 uint32_t XformErrorWord(uint64_t n_bytes, uint32_t n_files, const void* scratch, hipStream_t s);
 // The error word's device address (read it with the stream's other results).
 const uint32_t* XformErrorPtr(uint64_t n_bytes, uint32_t n_files, const void* scratch);

@@ -127,7 +127,10 @@ template <typename Pos>
 __device__ __forceinline__ uint4 x_block(const uint8_t* raw, Pos n_bytes, uint32_t t, uint32_t lane,
                                          uint32_t n_tiles) {
   const Pos blk = Pos(t) * kXTile + 16 * lane;
-  return t < n_tiles && blk < n_bytes ? *reinterpret_cast<const uint4*>(raw + blk) : make_uint4(0, 0, 0, 0);
+  // branch-free (a load under a branch makes the compiler's vmcnt waits after it conservative)
+  const bool in = t < n_tiles && blk < n_bytes;
+  const uint4 x = *reinterpret_cast<const uint4*>(raw + (in ? blk : Pos(0)));
+  return in ? x : make_uint4(0, 0, 0, 0);
 }
 
 // The 32 bytes around a lane's block: [blk - 8, blk + 24) as 8 words (the
@@ -230,7 +233,8 @@ __device__ __forceinline__ XFileRegs<Pos> x_file_regs(const uint64_t* off, const
   const uint32_t g = tf + lane < n_files ? tf + lane : n_files;
   r.o = Pos(off[g]);
   r.o64 = Pos(off[tf + 64u < n_files ? tf + 64u : n_files]);
-  r.k = tf + lane < n_files ? uint32_t(kind[tf + lane]) : 0u;
+  const uint32_t k = kind[g < n_files ? g : 0u];  // branch-free (n_files >= 1 here)
+  r.k = g < n_files ? k : 0u;
   return r;
 }
 template <typename Pos>
@@ -254,13 +258,23 @@ __device__ __forceinline__ void x_stage_files(Pos* so, uint8_t* sk, const XFileR
 // length and a file starting in it starts at the same tile offset.
 // Conservative: a tile failing the test takes the exact per-block path.
 template <typename Pos>
-__device__ __forceinline__ bool x_fast_identity(const uint4& v, const Pos* so, const uint8_t* sk, uint32_t tf,
-                                                Pos t0, Pos tend, uint32_t lane) {
+__device__ __forceinline__ Pos x_lane0(Pos x) {  // lane 0's value (all lanes active)
+  if constexpr (sizeof(Pos) == 4) {
+    return Pos(__builtin_amdgcn_readfirstlane(uint32_t(x)));
+  } else {
+    return (Pos(__builtin_amdgcn_readfirstlane(uint32_t(uint64_t(x) >> 32))) << 32) |
+           Pos(__builtin_amdgcn_readfirstlane(uint32_t(x)));
+  }
+}
+
+template <typename Pos>
+__device__ __forceinline__ bool x_fast_identity(const uint4& v, const XFileRegs<Pos>& fr, uint32_t tf, Pos t0,
+                                                Pos tend) {
   const uint32_t cr = eq_bytes(v.x, 0x0D0D0D0Du) | eq_bytes(v.y, 0x0D0D0D0Du) | eq_bytes(v.z, 0x0D0D0D0Du) |
                       eq_bytes(v.w, 0x0D0D0D0Du);
-  const bool k2 = so[lane] < tend && sk[lane] == kXformPrintable;  // file tf + lane holds bytes of the tile
-  const bool many = so[64] < tend;                                  // file tf + 64 starts in the tile
-  const bool edge = so[0] == t0 && tf > 0;
+  const bool k2 = fr.o < tend && fr.k == kXformPrintable;  // file tf + lane holds bytes of the tile
+  const bool many = fr.o64 < tend;                          // file tf + 64 starts in the tile
+  const bool edge = x_lane0(fr.o) == t0 && tf > 0;         // lane 0's file: the one holding byte t0
   return !__any(cr != 0u || k2) && !many && !edge;
 }
 
@@ -338,24 +352,33 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
   uint8_t* sk = s_fk[threadIdx.x >> 6];
   uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
   uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
-  uint32_t tf = t < n_tiles ? chunk_file[t] : 0u;
+  if (t >= n_tiles) return;
+  uint32_t tf = chunk_file[t];
+  uint32_t tfn = chunk_file[t + waves < n_tiles ? t + waves : t];  // chunk map entries two tiles ahead
   XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
   for (; t < n_tiles; t += waves) {
     const Pos blk = Pos(t) * kXTile + 16 * lane;
-    x_stage_files(so, sk, fr, lane);
-    const XFiles<Pos> T{tf, so, sk, off, kind};
-    const uint4 vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
-    const uint32_t tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
-    const XFileRegs<Pos> frn = t + waves < n_tiles ? x_file_regs<Pos>(off, kind, n_files, tfn, lane) : fr;
+    // The next tile's inputs.  Its chunk map entry was loaded an iteration ago,
+    // before that iteration's stores: on gfx9 a store counts in vmcnt like a
+    // load, so waiting for a load issued after a store waits for the store too
+    // (with the entry loaded here, every tile waited for the last tile's stores).
+    // (unconditional, clamped indices: a load under a branch makes every later vmcnt wait a full drain)
+    const uint32_t t1 = t + waves < n_tiles ? t + waves : t, t2 = t + 2 * waves < n_tiles ? t + 2 * waves : t1;
+    const XFileRegs<Pos> frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
+    const uint4 vn = x_block(raw, n_bytes, t1, lane, n_tiles);
+    const uint32_t tfnn = chunk_file[t2];
     const Pos t0 = Pos(t) * kXTile, tend = t0 + kXTile < n_bytes ? t0 + kXTile : n_bytes;
-    if (x_fast_identity(v, so, sk, tf, t0, tend, lane)) {
+    if (x_fast_identity(v, fr, tf, t0, tend)) {
       if (lane == 0) tile_cnt[t] = uint64_t(tend - t0);
-      if (so[lane] >= t0 && so[lane] < tend) fstart[tf + lane] = uint32_t(so[lane] - t0);
+      if (fr.o >= t0 && fr.o < tend) fstart[tf + lane] = uint32_t(fr.o - t0);
       v = vn;
       tf = tfn;
+      tfn = tfnn;
       fr = frn;
       continue;
     }
+    x_stage_files(so, sk, fr, lane);
+    const XFiles<Pos> T{tf, so, sk, off, kind};
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
     // file starts: tile-relative output offsets once the lane's prefix is known
     uint32_t sf[4], sc[4], ns = 0;
@@ -379,6 +402,7 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
     }
     v = vn;
     tf = tfn;
+    tfn = tfnn;
     fr = frn;
   }
 }
@@ -392,6 +416,94 @@ __global__ __launch_bounds__(kXThreads) void xf_fixup_kernel(const uint64_t* __r
     const uint64_t s = f < n_files ? off[f] : n_bytes;
     xoff[f] = s < n_bytes ? tile_pre[s / kXTile] + fstart[f] : tile_pre[n_tiles];
   }
+}
+
+// An identity tile's output: its input moved to `start`, so each lane writes one
+// aligned 16-B block composed from its own and the previous lane's bytes (a
+// byte shift by the tile's output phase), no staging; the two ragged 16-B
+// blocks, shared with the neighbouring tiles, a byte per lane.
+__device__ __forceinline__ void x_store_identity(const uint4& v, uint64_t start, uint32_t lane, uint8_t* out,
+                                                 uint64_t out_cap, uint32_t* err) {
+  const uint32_t phase = uint32_t(start & 15);
+  const uint32_t X[9] = {__shfl_up(v.x, 1), __shfl_up(v.y, 1), __shfl_up(v.z, 1), __shfl_up(v.w, 1),
+                         v.x, v.y, v.z, v.w, 0u};  // prev ++ own
+  const uint32_t sh = 16u - phase;  // output block = X bytes [sh, sh + 16)
+  const uint32_t rb = sh & 3u;
+  uint32_t o[4];
+  switch (sh >> 2) {  // wave-uniform
+#define TSG_XO(k)                                                                                \
+  case k:                                                                                        \
+    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(X[k + i + 1], X[k + i], rb); \
+    break;
+    TSG_XO(0)
+    TSG_XO(1)
+    TSG_XO(2)
+    TSG_XO(3)
+    default:
+      for (int i = 0; i < 4; i++) o[i] = X[4 + i];  // phase 0
+#undef TSG_XO
+  }
+  const uint64_t base = start - phase;
+  const uint64_t g = base + 16u * lane;
+  if (__any(base + kXTile + 16 > out_cap)) {  // a tile offset past the output: plan and write disagree
+    if (lane == 0) atomicOr(err, 1u);
+    return;
+  }
+  if (lane > 0 || phase == 0) *reinterpret_cast<uint4*>(out + g) = make_uint4(o[0], o[1], o[2], o[3]);
+  if (phase) {  // the ragged ends, a byte per lane: the previous tile owns out[base, start)
+    const uint32_t jb = lane & 15u;
+    // lanes 0-15: lane 0's block, bytes [phase, 16); lanes 16-31: the tile's last
+    // `phase` bytes, which spill into block 64 (lane 63's bytes [16 - phase, 16))
+    const bool head = lane < 16;
+    const uint32_t src = head ? 0u : 63u, b = head ? jb : 16u - phase + jb;
+    const uint32_t a0 = __builtin_amdgcn_readlane(o[0], 0), a1 = __builtin_amdgcn_readlane(o[1], 0),
+                   a2 = __builtin_amdgcn_readlane(o[2], 0), a3 = __builtin_amdgcn_readlane(o[3], 0);
+    const uint32_t c0 = __builtin_amdgcn_readlane(v.x, 63), c1 = __builtin_amdgcn_readlane(v.y, 63),
+                   c2 = __builtin_amdgcn_readlane(v.z, 63), c3 = __builtin_amdgcn_readlane(v.w, 63);
+    const uint32_t w =
+        b < 8 ? (b < 4 ? (src ? c0 : a0) : (src ? c1 : a1)) : (b < 12 ? (src ? c2 : a2) : (src ? c3 : a3));
+    if (head ? jb >= phase : (lane < 32 && jb < phase))
+      out[head ? base + jb : base + kXTile + jb] = uint8_t(w >> (8 * (b & 3)));
+  }
+}
+
+// A tile with edits: the lanes' output packed in the wave's LDS stage S at its
+// global 16-B phase (emit(put) replays the lanes' masks into put), then
+// aligned 16-B stores, byte stores at the two ragged ends.
+template <typename Emit>
+__device__ __forceinline__ void x_store_staged(uint8_t* S, uint64_t start, uint32_t ex, uint32_t total,
+                                               uint32_t lane, uint8_t* out, uint64_t out_cap, uint32_t* err,
+                                               Emit emit, const XWindow& W) {
+  const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
+  uint32_t at = phase + ex;
+  emit([&](uint32_t K, uint32_t C, uint32_t Z) {
+    for (uint32_t m = K | C | Z; m; m &= m - 1) {
+      const uint32_t i = uint32_t(__ffs(m)) - 1u;
+      if ((C >> i) & 1u) S[at++] = '\n';
+      if ((K >> i) & 1u) S[at++] = uint8_t(W.byte(8 + i));
+      if ((Z >> i) & 1u) S[at++] = '\n';
+    }
+  });
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t base = start - phase, end = start + total;
+  if (end > out_cap) {  // wave-uniform: never write past the output (the error fails the call)
+    if (lane == 0) atomicOr(err, 2u);
+  } else {
+    for (uint32_t q = 16 * lane; base + q < end; q += 1024) {
+      const uint64_t g = base + q;
+      if (g >= start && g + 16 <= end) {
+        *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(S + q);
+      } else {  // the ragged ends: only this tile's bytes
+        for (uint32_t j = 0; j < 16; j++)
+          if (g + j >= start && g + j < end) out[g + j] = S[q + j];
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <typename Pos>
@@ -414,27 +526,34 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
   Pos* so = s_fo[threadIdx.x >> 6];
   uint8_t* sk = s_fk[threadIdx.x >> 6];
   uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
+  if (t >= n_tiles) return;
   uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);  // the next tile's inputs, a tile ahead
-  uint32_t tfn = t < n_tiles ? chunk_file[t] : 0u;
-  uint64_t pren = t < n_tiles ? tile_pre[t] : 0u;
+  uint32_t tfn = chunk_file[t];
+  uint32_t tfnn = chunk_file[t + waves < n_tiles ? t + waves : t];  // chunk map entries two tiles ahead
+  uint64_t pren = tile_pre[t];
   XFileRegs<Pos> frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
   for (; t < n_tiles; t += waves) {
     const Pos blk = Pos(t) * kXTile + 16 * lane;
     const uint4 v = vn;
     const uint32_t tf = tfn;
     const uint64_t start = pren;
-    x_stage_files(so, sk, frn, lane);
-    const XFiles<Pos> T{tf, so, sk, off, kind};
-    vn = x_block(raw, n_bytes, t + waves, lane, n_tiles);
-    tfn = t + waves < n_tiles ? chunk_file[t + waves] : 0u;
-    pren = t + waves < n_tiles ? tile_pre[t + waves] : 0u;
-    if (t + waves < n_tiles) frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
+    const XFileRegs<Pos> fr = frn;
+    // the next tile's inputs, none of them behind this tile's stores (xf_count_kernel)
+    // (unconditional, clamped indices: see xf_count_kernel)
+    const uint32_t t1 = t + waves < n_tiles ? t + waves : t, t2 = t + 2 * waves < n_tiles ? t + 2 * waves : t1;
+    frn = x_file_regs<Pos>(off, kind, n_files, tfnn, lane);
+    vn = x_block(raw, n_bytes, t1, lane, n_tiles);
+    pren = tile_pre[t1];
+    tfn = tfnn;
+    tfnn = chunk_file[t2];
     const Pos t0 = Pos(t) * kXTile;
-    const bool fast = t0 + kXTile <= n_bytes && x_fast_identity(v, so, sk, tf, t0, t0 + Pos(kXTile), lane);
+    const bool fast = t0 + kXTile <= n_bytes && x_fast_identity(v, fr, tf, t0, t0 + Pos(kXTile));
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
     uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0xFFFFu, added = 0, c = 16;
     XWindow W;
+    const XFiles<Pos> T{tf, so, sk, off, kind};
     if (!fast) {
+      x_stage_files(so, sk, fr, lane);
       W = x_window(raw, n_bytes, blk, lane, v);
       kept = 0;
       c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
@@ -449,89 +568,174 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
                    added |= C | Z;
                  });
     }
-    const uint32_t phase = uint32_t(start & 15);  // the stage holds out[start - phase ..) at offset 0
     if (fast || __all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
-      // An identity tile (no CR dropped, no printable-run edits, a whole KiB):
-      // its output is its input moved to `start`, so each lane writes one
-      // aligned 16-B block composed from its own and the previous lane's bytes
-      // (a byte shift by the tile's output phase), no staging.
-      const uint32_t X[9] = {__shfl_up(v.x, 1), __shfl_up(v.y, 1), __shfl_up(v.z, 1), __shfl_up(v.w, 1),
-                             v.x, v.y, v.z, v.w, 0u};  // prev ++ own
-      const uint32_t sh = 16u - phase;  // output block = X bytes [sh, sh + 16)
-      const uint32_t rb = sh & 3u;
-      uint32_t o[4];
-      switch (sh >> 2) {  // wave-uniform
-#define TSG_XO(k)                                                                  \
-  case k:                                                                          \
-    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(X[k + i + 1], X[k + i], rb); \
-    break;
-        TSG_XO(0)
-        TSG_XO(1)
-        TSG_XO(2)
-        TSG_XO(3)
-        default:
-          for (int i = 0; i < 4; i++) o[i] = X[4 + i];  // phase 0
-#undef TSG_XO
-      }
-      const uint64_t base = start - phase;
-      const uint64_t g = base + 16u * lane;
-      if (__any(base + kXTile + 16 > out_cap)) {  // a tile offset past the output: plan and write disagree
-        if (lane == 0) atomicOr(err, 1u);
-        continue;
-      }
-      if (lane > 0 || phase == 0) *reinterpret_cast<uint4*>(out + g) = make_uint4(o[0], o[1], o[2], o[3]);
-      if (phase) {  // the ragged ends, a byte per lane: the previous tile owns out[base, start)
-        const uint32_t jb = lane & 15u;
-        // lanes 0-15: lane 0's block, bytes [phase, 16); lanes 16-31: the tile's last
-        // `phase` bytes, which spill into block 64 (lane 63's bytes [16 - phase, 16))
-        const bool head = lane < 16;
-        const uint32_t src = head ? 0u : 63u, b = head ? jb : 16u - phase + jb;
-        const uint32_t a0 = __builtin_amdgcn_readlane(o[0], 0), a1 = __builtin_amdgcn_readlane(o[1], 0),
-                       a2 = __builtin_amdgcn_readlane(o[2], 0), a3 = __builtin_amdgcn_readlane(o[3], 0);
-        const uint32_t c0 = __builtin_amdgcn_readlane(v.x, 63), c1 = __builtin_amdgcn_readlane(v.y, 63),
-                       c2 = __builtin_amdgcn_readlane(v.z, 63), c3 = __builtin_amdgcn_readlane(v.w, 63);
-        const uint32_t w = b < 8 ? (b < 4 ? (src ? c0 : a0) : (src ? c1 : a1)) : (b < 12 ? (src ? c2 : a2) : (src ? c3 : a3));
-        if (head ? jb >= phase : (lane < 32 && jb < phase))
-          out[head ? base + jb : base + kXTile + jb] = uint8_t(w >> (8 * (b & 3)));
-      }
+      // an identity tile (no CR dropped, no printable-run edits, a whole KiB)
+      x_store_identity(v, start, lane, out, out_cap, err);
       continue;
     }
     const uint32_t ex = wave_excl(c, lane);
-    const uint32_t total = __shfl(ex + c, 63);
-    uint32_t at = phase + ex;
-    auto put = [&](uint32_t K, uint32_t C, uint32_t Z) {
-      for (uint32_t m = K | C | Z; m; m &= m - 1) {
-        const uint32_t i = uint32_t(__ffs(m)) - 1u;
-        if ((C >> i) & 1u) S[at++] = '\n';
-        if ((K >> i) & 1u) S[at++] = uint8_t(W.byte(8 + i));
-        if ((Z >> i) & 1u) S[at++] = '\n';
+    x_store_staged(S, start, ex, __shfl(ex + c, 63), lane, out, out_cap, err, [&](auto put) {
+      if (nseg <= 4) {
+        for (uint32_t i = 0; i < nseg; i++) put(segK[i], segC[i], segZ[i]);
+      } else {
+        x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {}, put);
       }
-    };
-    if (nseg <= 4) {
-      for (uint32_t i = 0; i < nseg; i++) put(segK[i], segC[i], segZ[i]);
+    }, W);
+  }
+}
+
+// One pass (TSG_XFORM_ONEPASS=1; the default is count, scan, fix-up, write): waves
+// take tiles in ticket order, compute a tile's output length, publish it
+// (status[t] = kXAgg | length), find the tile's output offset by a decoupled
+// look-back over the predecessors' published lengths and prefixes (a wave
+// reads 64 predecessors at a time; tile 0 and every tile done publish
+// kXIncl | inclusive prefix), publish their inclusive prefix and write the
+// tile and the transformed offsets of the files starting in it.  Tiles are
+// claimed in order by resident waves, and a wave publishes its length before
+// it waits, so every wait is for a tile that is being processed; a wait that
+// still exceeds kXSpinMax rounds gives up and flags the error word (the call
+// fails instead of hanging the GPU).
+constexpr uint64_t kXAgg = uint64_t(1) << 62, kXIncl = uint64_t(1) << 63, kXVal = kXAgg - 1;
+constexpr uint32_t kXSpinMax = 1u << 22;
+#ifndef TSG_XFORM_SLEEP
+#define TSG_XFORM_SLEEP 8
+#endif
+
+template <typename Pos>
+__global__ __launch_bounds__(kXThreads) void xf_onepass_kernel(const uint8_t* __restrict__ raw, Pos n_bytes,
+                                                               const uint64_t* __restrict__ off,
+                                                               const uint8_t* __restrict__ kind, uint32_t n_files,
+                                                               const uint32_t* __restrict__ chunk_file,
+                                                               uint64_t* status, uint32_t* ticket,
+                                                               uint64_t* __restrict__ xoff, uint8_t* __restrict__ out,
+                                                               uint64_t out_cap, uint32_t* __restrict__ err) {
+  constexpr uint32_t kStage = 1280 + 32;  // as xf_write_kernel
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kXThreads / 64][kStage];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint8_t* S = s_out[threadIdx.x >> 6];
+  const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
+  __shared__ Pos s_fo[kXThreads / 64][65];
+  __shared__ uint8_t s_fk[kXThreads / 64][64];
+  Pos* so = s_fo[threadIdx.x >> 6];
+  uint8_t* sk = s_fk[threadIdx.x >> 6];
+  for (;;) {
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(ticket, 1u);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(tk);
+    if (t >= n_tiles) break;
+    const Pos t0 = Pos(t) * kXTile, tend = t0 + kXTile < n_bytes ? t0 + kXTile : n_bytes;
+    const Pos blk = t0 + 16 * lane;
+    const uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
+    const uint32_t tf = chunk_file[t];
+    const XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
+    const bool fast = x_fast_identity(v, fr, tf, t0, tend);
+    // the tile's length and, on the exact path, the lanes' masks and file starts
+    uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0xFFFFu, added = 0, c = 0, ex = 0;
+    uint32_t sf[4], sc[4], ns = 0;
+    XWindow W;
+    const XFiles<Pos> T{tf, so, sk, off, kind};
+    uint64_t len;
+    if (fast) {
+      len = uint64_t(tend - t0);
     } else {
-      x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {}, put);
+      x_stage_files(so, sk, fr, lane);
+      W = x_window(raw, n_bytes, blk, lane, v);
+      kept = 0;
+      c = x_lane(
+          n_bytes, T, n_files, blk, W,
+          [&](uint32_t f, uint32_t at) {
+            if (ns < 4) {
+              sf[ns] = f;
+              sc[ns] = at;
+            }
+            ns++;
+          },
+          [&](uint32_t K, uint32_t C, uint32_t Z) {
+            if (nseg < 4) {
+              segK[nseg] = K;
+              segC[nseg] = C;
+              segZ[nseg] = Z;
+            }
+            nseg++;
+            kept |= K;
+            added |= C | Z;
+          });
+      ex = wave_excl(c, lane);
+      len = __shfl(ex + c, 63);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t base = start - phase, end = start + total;
-    if (end > out_cap) {  // wave-uniform: never write past the output (the error fails the call)
-      if (lane == 0) atomicOr(err, 2u);
+    // publish the length, then look back for the tile's output offset
+    uint64_t excl = 0;
+    if (t == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], kXIncl | len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[t], kXAgg | len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t hi = t;  // predecessors [0, hi) not yet summed
+      for (uint32_t spin = 0;;) {
+        const int64_t p = int64_t(hi) - 1 - int64_t(lane);  // lane l reads tile hi - 1 - l
+        const uint64_t st =
+            p >= 0 ? __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kXIncl;
+        const uint64_t incl = __ballot((st & kXIncl) != 0);
+        const uint64_t ready = __ballot((st & (kXIncl | kXAgg)) != 0);
+        // the nearest inclusive prefix (always within reach: tile 0 publishes one)
+        const uint32_t k = incl ? uint32_t(__ffsll(static_cast<unsigned long long>(incl)) - 1) : 64u;
+        const uint64_t need = k >= 63 ? ~uint64_t(0) : ((uint64_t(1) << (k + 1)) - 1);  // lanes 0..k
+        if ((ready & need) == need) {
+          uint64_t x = (lane <= k && p >= 0) ? (st & kXVal) : 0;
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+          excl += x;
+          if (k < 64) break;
+          hi -= 64;
+          continue;
+        }
+        if (++spin > kXSpinMax) {  // never expected: fail the call rather than spin forever
+          if (lane == 0) atomicOr(err, 4u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(TSG_XFORM_SLEEP);  // (the waiting waves share the memory path with the working ones)
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[t], kXIncl | (excl + len), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the transformed offsets of the files starting in the tile (xf_fixup_kernel's job)
+    if (fast) {
+      if (fr.o >= t0 && fr.o < tend) xoff[tf + lane] = excl + uint64_t(fr.o - t0);
+    } else if (ns > 4) {  // many tiny files in one block: walk it again, recording all
+      x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t f, uint32_t at) { xoff[f] = excl + ex + at; },
+             [&](uint32_t, uint32_t, uint32_t) {});
+    } else {
+      for (uint32_t i = 0; i < ns; i++) xoff[sf[i]] = excl + ex + sc[i];
+    }
+    if (t + 1 == n_tiles && lane == 0) {  // the end: files starting at n_bytes (empty) and the total
+      for (uint32_t f = n_files; f > 0 && Pos(off[f - 1]) == n_bytes; f--) xoff[f - 1] = excl + len;
+      xoff[n_files] = excl + len;
+    }
+    const bool whole = t0 + kXTile <= n_bytes;
+    if (whole && (fast || __all(kept == 0xFFFFu && added == 0u))) {
+      x_store_identity(v, excl, lane, out, out_cap, err);
       continue;
     }
-    for (uint32_t q = 16 * lane; base + q < end; q += 1024) {
-      const uint64_t g = base + q;
-      if (g >= start && g + 16 <= end) {
-        *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(S + q);
-      } else {  // the ragged ends: only this tile's bytes
-        for (uint32_t j = 0; j < 16; j++)
-          if (g + j >= start && g + j < end) out[g + j] = S[q + j];
-      }
+    if (fast) {  // the arena's partial last tile, identity: its masks for the staged write
+      x_stage_files(so, sk, fr, lane);
+      W = x_window(raw, n_bytes, blk, lane, v);
+      c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
+                 [&](uint32_t K, uint32_t C, uint32_t Z) {
+                   if (nseg < 4) {
+                     segK[nseg] = K;
+                     segC[nseg] = C;
+                     segZ[nseg] = Z;
+                   }
+                   nseg++;
+                 });
+      ex = wave_excl(c, lane);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    x_store_staged(S, excl, ex, uint32_t(len), lane, out, out_cap, err, [&](auto put) {
+      if (nseg <= 4) {
+        for (uint32_t i = 0; i < nseg; i++) put(segK[i], segC[i], segZ[i]);
+      } else {
+        x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {}, put);
+      }
+    }, W);
   }
 }
 
@@ -558,7 +762,7 @@ uint32_t grid_for(uint32_t n_waves) {
 
 // Scratch of the flat transform: chunk map | tile counts | tile prefix | file starts | scan temp.
 struct XformScratch {
-  size_t chunk_file, tile_cnt, tile_pre, fstart, err, scan, scan_bytes, total;
+  size_t chunk_file, tile_cnt, tile_pre, fstart, err, scan, scan_bytes, status, total;
 };
 
 // 64-bit positions for calls of 4 GiB or more; TSG_XFORM_WIDE=1 forces them
@@ -591,9 +795,10 @@ static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
   L.tile_pre = up(L.tile_cnt + (n_tiles + 1) * 8);
   L.fstart = up(L.tile_pre + (n_tiles + 1) * 8);
   L.err = up(L.fstart + (size_t(n_files) + 1) * 4);
-  L.scan = up(L.err + 16);
+  L.scan = up(L.err + 16);  // (the one-pass ticket lives in the error block: err[1])
   L.scan_bytes = scan;
-  L.total = up(L.scan + scan + 16);
+  L.status = up(L.scan + scan + 16);
+  L.total = up(L.status + (n_tiles + 1) * 8);
   return L;
 }
 
@@ -650,6 +855,42 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   else
     xf_write_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, cf, tp, out, out_cap,
                                                       err);
+  return hipGetLastError();
+}
+
+// One pass (xf_onepass_kernel): xoff and out together, TSG_XFORM_ONEPASS=1 only
+// (read per call: tests run both paths in one process).  Measured 3.3 ms per
+// 256-MB C4 batch against 0.3 ms for the two passes, whatever the spin's sleep:
+// a ticket per 1-KiB tile is 256 Ki atomics on one address, which serialise at
+// ~12 ns each -- the ticket, not the look-back, sets the time.
+bool XformOnePassOn() {
+  const char* e = std::getenv("TSG_XFORM_ONEPASS");
+  return e && std::atoi(e) != 0;
+}
+
+hipError_t XformOnePass(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind,
+                        uint32_t n_files, void* scratch, uint64_t* xoff, uint8_t* out, uint64_t out_cap,
+                        hipStream_t s) {
+  const XformScratch L = ScratchLayout(n_bytes, n_files);
+  uint8_t* sc = static_cast<uint8_t*>(scratch);
+  uint32_t* chunk_file = reinterpret_cast<uint32_t*>(sc + L.chunk_file);
+  uint32_t* err = reinterpret_cast<uint32_t*>(sc + L.err);
+  uint64_t* status = reinterpret_cast<uint64_t*>(sc + L.status);
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  hipError_t e;
+  if ((e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess) return e;  // error word, ticket
+  if (n_tiles == 0 || n_files == 0) return hipMemsetAsync(xoff, 0, (size_t(n_files) + 1) * 8, s);
+  if ((e = hipMemsetAsync(status, 0, n_tiles * 8, s)) != hipSuccess) return e;
+  const uint32_t gm = uint32_t(std::min<uint64_t>((n_tiles + kXThreads - 1) / kXThreads, 8192));
+  xf_chunk_map_kernel<<<gm, kXThreads, 0, s>>>(off, n_files, n_tiles, chunk_file);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), XformGrid()));
+  if (XformWide(n_bytes))
+    xf_onepass_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, status,
+                                                        err + 1, xoff, out, out_cap, err);
+  else
+    xf_onepass_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file,
+                                                        status, err + 1, xoff, out, out_cap, err);
   return hipGetLastError();
 }
 
