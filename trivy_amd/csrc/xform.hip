@@ -129,8 +129,13 @@ __device__ __forceinline__ uint4 x_block(const uint8_t* raw, Pos n_bytes, uint32
   const Pos blk = Pos(t) * kXTile + 16 * lane;
   // branch-free (a load under a branch makes the compiler's vmcnt waits after it conservative)
   const bool in = t < n_tiles && blk < n_bytes;
+  // An opaque mask instead of a select on the loaded value: with the select the
+  // compiler moves the load under a branch, and a memory operation under a branch
+  // makes its vmcnt waits in the loop drain everything (xf_count_fast_kernel).
+  uint32_t m = in ? ~0u : 0u;
+  asm volatile("" : "+v"(m));
   const uint4 x = *reinterpret_cast<const uint4*>(raw + (in ? blk : Pos(0)));
-  return in ? x : make_uint4(0, 0, 0, 0);
+  return make_uint4(x.x & m, x.y & m, x.z & m, x.w & m);
 }
 
 // The 32 bytes around a lane's block: [blk - 8, blk + 24) as 8 words (the
@@ -339,44 +344,30 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
                                                              const uint8_t* __restrict__ kind, uint32_t n_files,
                                                              const uint32_t* __restrict__ chunk_file,
                                                              uint64_t* __restrict__ tile_cnt,
-                                                             uint32_t* __restrict__ fstart) {
+                                                             uint32_t* __restrict__ fstart,
+                                                             const uint32_t* __restrict__ tile_fast) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
   const uint32_t waves = gridDim.x * (kXThreads / 64);
-  // a wave walks tiles t, t + waves, ...: the next tile's block and chunk-map
-  // entry are loaded while this one is processed (the per-tile chain of
-  // dependent loads, not bytes, bounds these kernels)
+  // The tiles xf_count_fast_kernel left (tile_fast[t] == 0: a '\r', a kind-2
+  // file, an empty file at the tile start, > 64 file starts, the arena's partial
+  // last tile).
   __shared__ Pos s_fo[kXThreads / 64][65];
   __shared__ uint8_t s_fk[kXThreads / 64][64];
   Pos* so = s_fo[threadIdx.x >> 6];
   uint8_t* sk = s_fk[threadIdx.x >> 6];
-  uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
-  uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
-  if (t >= n_tiles) return;
-  uint32_t tf = chunk_file[t];
-  uint32_t tfn = chunk_file[t + waves < n_tiles ? t + waves : t];  // chunk map entries two tiles ahead
-  XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
-  for (; t < n_tiles; t += waves) {
+  // a wave's tiles are t, t + waves, ... (balanced: a CRLF file's run of tiles
+  // spreads over the waves); their flags are read 64 at a time
+  for (uint32_t base = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); base < n_tiles; base += 64 * waves) {
+    const uint32_t tl = base + lane * waves;
+    uint64_t left = __ballot(tl < n_tiles && tile_fast[tl] == 0u);
+    while (left) {
+    const uint32_t t = base + uint32_t(__builtin_ctzll(left)) * waves;
+    left &= left - 1;
     const Pos blk = Pos(t) * kXTile + 16 * lane;
-    // The next tile's inputs.  Its chunk map entry was loaded an iteration ago,
-    // before that iteration's stores: on gfx9 a store counts in vmcnt like a
-    // load, so waiting for a load issued after a store waits for the store too
-    // (with the entry loaded here, every tile waited for the last tile's stores).
-    // (unconditional, clamped indices: a load under a branch makes every later vmcnt wait a full drain)
-    const uint32_t t1 = t + waves < n_tiles ? t + waves : t, t2 = t + 2 * waves < n_tiles ? t + 2 * waves : t1;
-    const XFileRegs<Pos> frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
-    const uint4 vn = x_block(raw, n_bytes, t1, lane, n_tiles);
-    const uint32_t tfnn = chunk_file[t2];
-    const Pos t0 = Pos(t) * kXTile, tend = t0 + kXTile < n_bytes ? t0 + kXTile : n_bytes;
-    if (x_fast_identity(v, fr, tf, t0, tend)) {
-      if (lane == 0) tile_cnt[t] = uint64_t(tend - t0);
-      if (fr.o >= t0 && fr.o < tend) fstart[tf + lane] = uint32_t(fr.o - t0);
-      v = vn;
-      tf = tfn;
-      tfn = tfnn;
-      fr = frn;
-      continue;
-    }
+    const uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
+    const uint32_t tf = chunk_file[t];
+    const XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
     x_stage_files(so, sk, fr, lane);
     const XFiles<Pos> T{tf, so, sk, off, kind};
     const XWindow W = x_window(raw, n_bytes, blk, lane, v);
@@ -400,6 +391,56 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
     } else {
       for (uint32_t i = 0; i < ns; i++) fstart[sf[i]] = ex + sc[i];
     }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kXThreads) void xf_fixup_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
+                                                             uint64_t n_bytes, const uint64_t* __restrict__ tile_pre,
+                                                             const uint32_t* __restrict__ fstart,
+                                                             const uint32_t* __restrict__ tile_fast,
+                                                             uint64_t* __restrict__ xoff) {
+  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
+  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_files; f += gridDim.x * blockDim.x) {
+    const uint64_t s = f < n_files ? off[f] : n_bytes;
+    const uint64_t t = s / kXTile;
+    // an identity tile's output offsets are its input offsets (no fstart entry)
+    xoff[f] = s < n_bytes ? tile_pre[t] + (tile_fast[t] ? s - t * kXTile : uint64_t(fstart[f])) : tile_pre[n_tiles];
+  }
+}
+
+// The identity tiles, counted (a pass the exact count kernel then skips).  Each
+// iteration issues the same loads and the same two stores whatever the tile is
+// (every lane stores the tile's count and flag; no branch around a memory
+// operation), so the compiler's vmcnt waits for the next tile's loads -- issued
+// before this tile's stores -- need not drain the stores: on gfx9 a store counts
+// in vmcnt like a load, and one branch around a load or store in the loop made
+// every tile wait for all of the previous tile's memory traffic.
+template <typename Pos>
+__global__ __launch_bounds__(kXThreads) void xf_count_fast_kernel(const uint8_t* __restrict__ raw, Pos n_bytes,
+                                                                  const uint64_t* __restrict__ off,
+                                                                  const uint8_t* __restrict__ kind, uint32_t n_files,
+                                                                  const uint32_t* __restrict__ chunk_file,
+                                                                  uint64_t* __restrict__ tile_cnt,
+                                                                  uint32_t* __restrict__ tile_fast) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
+  const uint32_t waves = gridDim.x * (kXThreads / 64);
+  uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6));
+  if (t >= n_tiles) return;
+  uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
+  uint32_t tf = chunk_file[t];
+  uint32_t tfn = chunk_file[t + waves < n_tiles ? t + waves : t];  // chunk map entries two tiles ahead
+  XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
+  for (; t < n_tiles; t += waves) {
+    const uint32_t t1 = t + waves < n_tiles ? t + waves : t, t2 = t + 2 * waves < n_tiles ? t + 2 * waves : t1;
+    const XFileRegs<Pos> frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
+    const uint4 vn = x_block(raw, n_bytes, t1, lane, n_tiles);
+    const uint32_t tfnn = chunk_file[t2];
+    const Pos t0 = Pos(t) * kXTile;
+    const bool fast = t0 + kXTile <= n_bytes && x_fast_identity(v, fr, tf, t0, t0 + Pos(kXTile));
+    tile_cnt[t] = fast ? uint64_t(kXTile) : 0u;  // (the exact kernel counts the others)
+    tile_fast[t] = fast ? 1u : 0u;
     v = vn;
     tf = tfn;
     tfn = tfnn;
@@ -407,15 +448,78 @@ __global__ __launch_bounds__(kXThreads) void xf_count_kernel(const uint8_t* __re
   }
 }
 
-__global__ __launch_bounds__(kXThreads) void xf_fixup_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
-                                                             uint64_t n_bytes, const uint64_t* __restrict__ tile_pre,
-                                                             const uint32_t* __restrict__ fstart,
-                                                             uint64_t* __restrict__ xoff) {
-  const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
-  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f <= n_files; f += gridDim.x * blockDim.x) {
-    const uint64_t s = f < n_files ? off[f] : n_bytes;
-    xoff[f] = s < n_bytes ? tile_pre[s / kXTile] + fstart[f] : tile_pre[n_tiles];
+// The identity tiles, written: out[tile_pre[t] ..) = the tile's KiB (the exact
+// write kernel skips them).  The same loads and stores every iteration, as
+// xf_count_fast_kernel: a lane's store that must not land (a tile with edits,
+// lane 0's shared first block, the ragged bytes no lane owns) goes to the
+// wave's slot of `trash`; the capacity check is folded the same way.
+constexpr uint32_t kXTrashWaves = 1024;  // trash: kXTrashWaves x (1 KiB + 64 B)
+template <typename Pos>
+__global__ __launch_bounds__(kXThreads) void xf_write_fast_kernel(const uint8_t* __restrict__ raw, Pos n_bytes,
+                                                                  const uint32_t* __restrict__ tile_fast,
+                                                                  const uint64_t* __restrict__ tile_pre,
+                                                                  uint8_t* __restrict__ out, uint64_t out_cap,
+                                                                  uint8_t* __restrict__ trash,
+                                                                  uint32_t* __restrict__ err) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
+  const uint32_t waves = gridDim.x * (kXThreads / 64);
+  uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6));
+  if (t >= n_tiles) return;
+  uint8_t* tw = trash + size_t(t % kXTrashWaves) * (kXTile + 64);
+  uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);
+  uint64_t pren = tile_pre[t];
+  uint32_t fn = tile_fast[t];
+  bool over = false;
+  for (; t < n_tiles; t += waves) {
+    const uint4 v = vn;
+    const uint64_t start = pren;
+    const bool fast = fn != 0;
+    const uint32_t t1 = t + waves < n_tiles ? t + waves : t;
+    vn = x_block(raw, n_bytes, t1, lane, n_tiles);
+    pren = tile_pre[t1];
+    fn = tile_fast[t1];
+    const uint32_t phase = uint32_t(start & 15);
+    const uint32_t X[9] = {__shfl_up(v.x, 1), __shfl_up(v.y, 1), __shfl_up(v.z, 1), __shfl_up(v.w, 1),
+                           v.x, v.y, v.z, v.w, 0u};  // prev ++ own
+    const uint32_t sh = 16u - phase;  // output block = X bytes [sh, sh + 16)
+    const uint32_t rb = sh & 3u;
+    uint32_t o[4];
+    switch (sh >> 2) {  // wave-uniform
+#define TSG_XO(k)                                                                                \
+  case k:                                                                                        \
+    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(X[k + i + 1], X[k + i], rb); \
+    break;
+      TSG_XO(0)
+      TSG_XO(1)
+      TSG_XO(2)
+      TSG_XO(3)
+      default:
+        for (int i = 0; i < 4; i++) o[i] = X[4 + i];  // phase 0
+#undef TSG_XO
+    }
+    const uint64_t base = start - phase;
+    const bool fits = base + kXTile + 16 <= out_cap;
+    over = over || (fast && !fits);
+    const bool live = fast && fits;
+    uint8_t* blk = (live && (lane > 0 || phase == 0)) ? out + base + 16u * lane : tw + 16u * lane;
+    *reinterpret_cast<uint4*>(blk) = make_uint4(o[0], o[1], o[2], o[3]);
+    // the ragged ends, a byte per lane: lanes 0-15 lane 0's block, bytes [phase, 16);
+    // lanes 16-31 the tile's last `phase` bytes, which spill into block 64
+    const uint32_t jb = lane & 15u;
+    const bool head = lane < 16;
+    const uint32_t src = head ? 0u : 63u, b = head ? jb : 16u - phase + jb;
+    const uint32_t a0 = __builtin_amdgcn_readlane(o[0], 0), a1 = __builtin_amdgcn_readlane(o[1], 0),
+                   a2 = __builtin_amdgcn_readlane(o[2], 0), a3 = __builtin_amdgcn_readlane(o[3], 0);
+    const uint32_t c0 = __builtin_amdgcn_readlane(v.x, 63), c1 = __builtin_amdgcn_readlane(v.y, 63),
+                   c2 = __builtin_amdgcn_readlane(v.z, 63), c3 = __builtin_amdgcn_readlane(v.w, 63);
+    const uint32_t w =
+        b < 8 ? (b < 4 ? (src ? c0 : a0) : (src ? c1 : a1)) : (b < 12 ? (src ? c2 : a2) : (src ? c3 : a3));
+    const bool own = live && phase != 0 && (head ? jb >= phase : (lane < 32 && jb < phase));
+    uint8_t* pb = own ? out + (head ? base + jb : base + kXTile + jb) : tw + kXTile + lane;
+    *pb = uint8_t(w >> (8 * (b & 3)));
   }
+  if (__any(over) && lane == 0) atomicOr(err, 1u);
 }
 
 // An identity tile's output: its input moved to `start`, so each lane writes one
@@ -513,8 +617,10 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
                                                              const uint32_t* __restrict__ chunk_file,
                                                              const uint64_t* __restrict__ tile_pre,
                                                              uint8_t* __restrict__ out, uint64_t out_cap,
-                                                             uint32_t* __restrict__ err) {
-  // a tile emits at most 1024 + 1024 / 5 + 16 bytes (a '\n' per closed run of >= 5 bytes)
+                                                             uint32_t* __restrict__ err,
+                                                             const uint32_t* __restrict__ tile_fast) {
+  // the tiles xf_write_fast_kernel left; a tile emits at most 1024 + 1024 / 5 + 16
+  // bytes (a '\n' per closed run of >= 5 bytes)
   constexpr uint32_t kStage = 1280 + 32;
   __shared__ __attribute__((aligned(16))) uint8_t s_out[kXThreads / 64][kStage];
   const uint32_t lane = threadIdx.x & 63u;
@@ -525,51 +631,37 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
   __shared__ uint8_t s_fk[kXThreads / 64][64];
   Pos* so = s_fo[threadIdx.x >> 6];
   uint8_t* sk = s_fk[threadIdx.x >> 6];
-  uint32_t t = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6);
-  if (t >= n_tiles) return;
-  uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);  // the next tile's inputs, a tile ahead
-  uint32_t tfn = chunk_file[t];
-  uint32_t tfnn = chunk_file[t + waves < n_tiles ? t + waves : t];  // chunk map entries two tiles ahead
-  uint64_t pren = tile_pre[t];
-  XFileRegs<Pos> frn = x_file_regs<Pos>(off, kind, n_files, tfn, lane);
-  for (; t < n_tiles; t += waves) {
+  // a wave's tiles are t, t + waves, ... (balanced: a CRLF file's run of tiles
+  // spreads over the waves); their flags are read 64 at a time
+  for (uint32_t base = blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6); base < n_tiles; base += 64 * waves) {
+    const uint32_t tl = base + lane * waves;
+    uint64_t left = __ballot(tl < n_tiles && tile_fast[tl] == 0u);
+    while (left) {
+    const uint32_t t = base + uint32_t(__builtin_ctzll(left)) * waves;
+    left &= left - 1;
     const Pos blk = Pos(t) * kXTile + 16 * lane;
-    const uint4 v = vn;
-    const uint32_t tf = tfn;
-    const uint64_t start = pren;
-    const XFileRegs<Pos> fr = frn;
-    // the next tile's inputs, none of them behind this tile's stores (xf_count_kernel)
-    // (unconditional, clamped indices: see xf_count_kernel)
-    const uint32_t t1 = t + waves < n_tiles ? t + waves : t, t2 = t + 2 * waves < n_tiles ? t + 2 * waves : t1;
-    frn = x_file_regs<Pos>(off, kind, n_files, tfnn, lane);
-    vn = x_block(raw, n_bytes, t1, lane, n_tiles);
-    pren = tile_pre[t1];
-    tfn = tfnn;
-    tfnn = chunk_file[t2];
-    const Pos t0 = Pos(t) * kXTile;
-    const bool fast = t0 + kXTile <= n_bytes && x_fast_identity(v, fr, tf, t0, t0 + Pos(kXTile));
+    const uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
+    const uint32_t tf = chunk_file[t];
+    const uint64_t start = tile_pre[t];
+    const XFileRegs<Pos> fr = x_file_regs<Pos>(off, kind, n_files, tf, lane);
     // the lane's masks per segment, kept for the write below (at most a few segments per block)
-    uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0xFFFFu, added = 0, c = 16;
-    XWindow W;
+    uint32_t segK[4], segC[4], segZ[4], nseg = 0, kept = 0, added = 0;
     const XFiles<Pos> T{tf, so, sk, off, kind};
-    if (!fast) {
-      x_stage_files(so, sk, fr, lane);
-      W = x_window(raw, n_bytes, blk, lane, v);
-      kept = 0;
-      c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
-                 [&](uint32_t K, uint32_t C, uint32_t Z) {
-                   if (nseg < 4) {
-                     segK[nseg] = K;
-                     segC[nseg] = C;
-                     segZ[nseg] = Z;
-                   }
-                   nseg++;
-                   kept |= K;
-                   added |= C | Z;
-                 });
-    }
-    if (fast || __all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
-      // an identity tile (no CR dropped, no printable-run edits, a whole KiB)
+    x_stage_files(so, sk, fr, lane);
+    const XWindow W = x_window(raw, n_bytes, blk, lane, v);
+    const uint32_t c = x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {},
+                              [&](uint32_t K, uint32_t C, uint32_t Z) {
+                                if (nseg < 4) {
+                                  segK[nseg] = K;
+                                  segC[nseg] = C;
+                                  segZ[nseg] = Z;
+                                }
+                                nseg++;
+                                kept |= K;
+                                added |= C | Z;
+                              });
+    if (__all(kept == 0xFFFFu && added == 0u && blk + 16 <= n_bytes)) {
+      // an identity tile the fast test left (e.g. an empty file at its start)
       x_store_identity(v, start, lane, out, out_cap, err);
       continue;
     }
@@ -581,6 +673,7 @@ __global__ __launch_bounds__(kXThreads) void xf_write_kernel(const uint8_t* __re
         x_lane(n_bytes, T, n_files, blk, W, [&](uint32_t, uint32_t) {}, put);
       }
     }, W);
+    }
   }
 }
 
@@ -762,7 +855,7 @@ uint32_t grid_for(uint32_t n_waves) {
 
 // Scratch of the flat transform: chunk map | tile counts | tile prefix | file starts | scan temp.
 struct XformScratch {
-  size_t chunk_file, tile_cnt, tile_pre, fstart, err, scan, scan_bytes, status, total;
+  size_t chunk_file, tile_cnt, tile_pre, fstart, err, scan, scan_bytes, status, tile_fast, trash, total;
 };
 
 // 64-bit positions for calls of 4 GiB or more; TSG_XFORM_WIDE=1 forces them
@@ -798,7 +891,9 @@ static XformScratch ScratchLayout(uint64_t n_bytes, uint32_t n_files) {
   L.scan = up(L.err + 16);  // (the one-pass ticket lives in the error block: err[1])
   L.scan_bytes = scan;
   L.status = up(L.scan + scan + 16);
-  L.total = up(L.status + (n_tiles + 1) * 8);
+  L.tile_fast = up(L.status + (n_tiles + 1) * 8);
+  L.trash = up(L.tile_fast + (n_tiles + 1) * 4);  // (u32: scalar loads by the write kernel)
+  L.total = up(L.trash + size_t(kXTrashWaves) * (kXTile + 64));
   return L;
 }
 
@@ -815,9 +910,11 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   uint64_t* tile_cnt = reinterpret_cast<uint64_t*>(sc + L.tile_cnt);
   uint64_t* tile_pre = reinterpret_cast<uint64_t*>(sc + L.tile_pre);
   uint32_t* fstart = reinterpret_cast<uint32_t*>(sc + L.fstart);
+  uint32_t* tile_fast = reinterpret_cast<uint32_t*>(sc + L.tile_fast);
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   hipError_t e;
-  if ((e = hipMemsetAsync(tile_cnt, 0, (n_tiles + 1) * 8, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(tile_cnt + n_tiles, 0, 8, s)) != hipSuccess) return e;  // (the fast pass writes the rest)
+  if ((e = hipMemsetAsync(tile_fast + n_tiles, 0, 4, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess) return e;
   if (n_files && n_tiles) {
     const uint32_t gm = uint32_t(std::min<uint64_t>((n_tiles + kXThreads - 1) / kXThreads, 8192));
@@ -826,17 +923,25 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   }
   if (n_tiles) {
     const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), XformGrid()));
-    if (wide)
-      xf_count_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart);
-    else
-      xf_count_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file, tile_cnt,
-                                                        fstart);
+    // identity tiles first (counted, flagged), then the exact count of the rest
+    if (wide) {
+      xf_count_fast_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt,
+                                                             tile_fast);
+      xf_count_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart,
+                                                         tile_fast);
+    } else {
+      xf_count_fast_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file,
+                                                             tile_cnt, tile_fast);
+      xf_count_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file,
+                                                         tile_cnt, fstart, tile_fast);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   size_t sb = L.scan_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(sc + L.scan, sb, tile_cnt, tile_pre, int(n_tiles) + 1, s)) != hipSuccess)
     return e;
-  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, n_bytes, tile_pre, fstart, xoff);
+  xf_fixup_kernel<<<grid_for((n_files + 64) / 64), kXThreads, 0, s>>>(off, n_files, n_bytes, tile_pre, fstart,
+                                                                      tile_fast, xoff);
   return hipGetLastError();
 }
 
@@ -850,11 +955,18 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   const uint32_t* cf = reinterpret_cast<const uint32_t*>(sc + L.chunk_file);
   const uint64_t* tp = reinterpret_cast<const uint64_t*>(sc + L.tile_pre);
   uint32_t* err = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(sc) + L.err);
-  if (XformWide(n_bytes))
-    xf_write_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, cf, tp, out, out_cap, err);
-  else
-    xf_write_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, cf, tp, out, out_cap,
-                                                      err);
+  const uint32_t* tfast = reinterpret_cast<const uint32_t*>(sc + L.tile_fast);
+  uint8_t* trash = const_cast<uint8_t*>(sc) + L.trash;
+  if (XformWide(n_bytes)) {
+    xf_write_fast_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, tfast, tp, out, out_cap, trash, err);
+    xf_write_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, cf, tp, out, out_cap, err,
+                                                       tfast);
+  } else {
+    xf_write_fast_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), tfast, tp, out, out_cap, trash,
+                                                           err);
+    xf_write_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, cf, tp, out,
+                                                       out_cap, err, tfast);
+  }
   return hipGetLastError();
 }
 
