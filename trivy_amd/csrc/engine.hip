@@ -2609,7 +2609,7 @@ bool GpuEngine::Transform(int b, uint32_t nf, const uint8_t** arena, const uint6
            std::to_string(total) + " bytes)";
     return false;
   }
-  HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));
+  if (XformOnePassOn()) HIP_OK(hipMemsetAsync(out + total, 0, 64, stream_));  // (XformWrite zeroes them)
   xoff->assign(h_xoff_, h_xoff_ + nf + 1);
   hipEventElapsedTime(ms, ev_x_[0], ev_x_[1]);
   *arena = out;

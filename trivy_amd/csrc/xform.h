@@ -16,7 +16,8 @@ constexpr uint8_t kXformNone = 0, kXformStripCR = 1, kXformPrintable = 2;
 // with the same scratch, writes out[xoff[f] ..) = transform(kind[f], file f)
 // and never at or past out_cap (out holds out_cap bytes): a tile whose output
 // would is skipped and flagged in the scratch's error word (XformErrorWord,
-// nonzero = the call failed; read after the stream's work).
+// nonzero = the call failed; read after the stream's work).  XformWrite also
+// zeroes the 64 bytes after the output (out_cap >= xoff[n_files] + 64).
 size_t XformScratchBytes(uint64_t n_bytes, uint32_t n_files);
 hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, const uint8_t* kind, uint32_t n_files,
                      void* scratch, uint64_t* xoff, hipStream_t s);

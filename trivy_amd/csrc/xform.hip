@@ -422,10 +422,16 @@ __global__ __launch_bounds__(kXThreads) void xf_count_fast_kernel(const uint8_t*
                                                                   const uint8_t* __restrict__ kind, uint32_t n_files,
                                                                   const uint32_t* __restrict__ chunk_file,
                                                                   uint64_t* __restrict__ tile_cnt,
-                                                                  uint32_t* __restrict__ tile_fast) {
+                                                                  uint32_t* __restrict__ tile_fast,
+                                                                  uint32_t* __restrict__ err) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_tiles = uint32_t((n_bytes + kXTile - 1) / kXTile);
   const uint32_t waves = gridDim.x * (kXThreads / 64);
+  if (blockIdx.x == 0 && threadIdx.x < 4) {  // (instead of three memsets: each a launch)
+    err[threadIdx.x] = 0;
+    if (threadIdx.x == 0) tile_cnt[n_tiles] = 0;  // the exclusive scan's last input
+    if (threadIdx.x == 1) tile_fast[n_tiles] = 0;
+  }
   uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6));
   if (t >= n_tiles) return;
   uint4 v = x_block(raw, n_bytes, t, lane, n_tiles);
@@ -466,6 +472,10 @@ __global__ __launch_bounds__(kXThreads) void xf_write_fast_kernel(const uint8_t*
   const uint32_t waves = gridDim.x * (kXThreads / 64);
   uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * (kXThreads / 64) + (threadIdx.x >> 6));
   if (t >= n_tiles) return;
+  if (t == 0) {  // the 64 zero bytes after the output the scan reads past its end (no tile writes there)
+    const uint64_t total = tile_pre[n_tiles];
+    if (total + 64 <= out_cap) out[total + lane] = 0;
+  }
   uint8_t* tw = trash + size_t(t % kXTrashWaves) * (kXTile + 64);
   uint4 vn = x_block(raw, n_bytes, t, lane, n_tiles);
   uint64_t pren = tile_pre[t];
@@ -913,9 +923,9 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
   uint32_t* tile_fast = reinterpret_cast<uint32_t*>(sc + L.tile_fast);
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
   hipError_t e;
-  if ((e = hipMemsetAsync(tile_cnt + n_tiles, 0, 8, s)) != hipSuccess) return e;  // (the fast pass writes the rest)
-  if ((e = hipMemsetAsync(tile_fast + n_tiles, 0, 4, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess) return e;
+  if (n_tiles == 0 && ((e = hipMemsetAsync(tile_cnt, 0, 8, s)) != hipSuccess ||
+                       (e = hipMemsetAsync(sc + L.err, 0, 16, s)) != hipSuccess))  // (else xf_count_fast_kernel)
+    return e;
   if (n_files && n_tiles) {
     const uint32_t gm = uint32_t(std::min<uint64_t>((n_tiles + kXThreads - 1) / kXThreads, 8192));
     xf_chunk_map_kernel<<<gm, kXThreads, 0, s>>>(off, n_files, n_tiles, chunk_file);
@@ -926,12 +936,13 @@ hipError_t XformPlan(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off, 
     // identity tiles first (counted, flagged), then the exact count of the rest
     if (wide) {
       xf_count_fast_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt,
-                                                             tile_fast);
+                                                             tile_fast, reinterpret_cast<uint32_t*>(sc + L.err));
       xf_count_kernel<uint64_t><<<g, kXThreads, 0, s>>>(raw, n_bytes, off, kind, n_files, chunk_file, tile_cnt, fstart,
                                                          tile_fast);
     } else {
       xf_count_fast_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file,
-                                                             tile_cnt, tile_fast);
+                                                             tile_cnt, tile_fast,
+                                                             reinterpret_cast<uint32_t*>(sc + L.err));
       xf_count_kernel<uint32_t><<<g, kXThreads, 0, s>>>(raw, uint32_t(n_bytes), off, kind, n_files, chunk_file,
                                                          tile_cnt, fstart, tile_fast);
     }
@@ -950,7 +961,7 @@ hipError_t XformWrite(const uint8_t* raw, uint64_t n_bytes, const uint64_t* off,
   const XformScratch L = ScratchLayout(n_bytes, n_files);
   const uint8_t* sc = static_cast<const uint8_t*>(scratch);
   const uint64_t n_tiles = (n_bytes + kXTile - 1) / kXTile;
-  if (!n_tiles) return hipSuccess;
+  if (!n_tiles) return out_cap >= 64 ? hipMemsetAsync(out, 0, 64, s) : hipSuccess;  // (else xf_write_fast_kernel)
   const uint32_t g = uint32_t(std::min<uint64_t>((n_tiles + kXThreads / 64 - 1) / (kXThreads / 64), XformGrid()));
   const uint32_t* cf = reinterpret_cast<const uint32_t*>(sc + L.chunk_file);
   const uint64_t* tp = reinterpret_cast<const uint64_t*>(sc + L.tile_pre);
