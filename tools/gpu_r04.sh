@@ -24,6 +24,11 @@ for st in $STAGES; do
     bench)
       timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
       rc=$?; python tools/bench_brief.py gpurun_out/bench_$TAG.json; tail -2 gpurun_out/bench_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
+    dflt)  # the default bench (no flags), DFLT_N times
+      for i in $(seq 1 ${DFLT_N:-2}); do
+        timeout -k 10 600 python bench.py > gpurun_out/dflt_${TAG}_$i.json 2> gpurun_out/dflt_${TAG}_$i.err
+        rc=$?; echo "== default $i"; python tools/bench_brief.py gpurun_out/dflt_${TAG}_$i.json; tail -1 gpurun_out/dflt_${TAG}_$i.err; [ $rc -eq 0 ] || exit $rc
+      done ;;
     quick)
       timeout -k 10 400 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/quick_$TAG.json 2> gpurun_out/quick_$TAG.err
       rc=$?; python tools/bench_brief.py gpurun_out/quick_$TAG.json; tail -2 gpurun_out/quick_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
