@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -45,23 +47,32 @@ class PathFilter {
   bool ok() const { return err_.empty(); }
   const std::string& error() const { return err_; }
   // Paths [off[i], off[i+1]) of d_paths (device), i < n: the reported ones
-  // (any order).  Thread-safe (one call at a time per filter).  Runs on a
-  // high-priority stream of its own: a few microseconds of GPU time that
-  // should not queue behind a scan's kernels.
+  // (any order).  Thread-safe: up to kSlots calls run at once, each on a
+  // high-priority stream and buffers of its own (a few microseconds of GPU time
+  // that should not queue behind a scan's kernels, nor behind another scan's
+  // filter: one shared stream and lock serialised the first scans of a
+  // pipeline, each waiting out a filter kernel queued behind a K1).
   bool Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out, std::string* err);
 
  private:
+  struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint32_t* d_cnt = nullptr;
+    uint32_t* h_cnt = nullptr;
+    PathHit* d_out = nullptr;
+    PathHit* h_out = nullptr;  // pinned: a pageable read-back stalled the engine's stream (5 ms per C2 scan)
+    size_t cap = 0;
+    bool busy = false;
+  };
+  static constexpr int kSlots = 4;
   std::mutex mu_;
+  std::condition_variable cv_;
+  Slot slots_[kSlots];
+  std::atomic<uint32_t> last_k_{0};  // records of the last call: one read-back when the count repeats
   int device_ = 0;
   std::string err_;
-  hipStream_t stream_ = nullptr;
-  hipEvent_t done_ = nullptr;
   PathTable* d_table_ = nullptr;
-  uint32_t* d_cnt_ = nullptr;
-  uint32_t* h_cnt_ = nullptr;
-  PathHit* d_out_ = nullptr;
-  PathHit* h_out_ = nullptr;  // pinned: a pageable read-back stalled the engine's stream (5 ms per C2 scan)
-  size_t cap_ = 0;
 };
 
 }  // namespace tsg

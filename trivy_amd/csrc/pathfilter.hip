@@ -107,75 +107,105 @@ __global__ __launch_bounds__(kPathThreads) void path_filter_kernel(const uint8_t
 PathFilter::PathFilter(int device, const PathTable& t) : device_(device) {
   int lo = 0, hi = 0;
   if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi) != hipSuccess ||
-      hipEventCreateWithFlags(&done_, hipEventDisableTiming) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&d_table_), sizeof(PathTable)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&d_cnt_), 64) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&h_cnt_), 64, hipHostMallocDefault) != hipSuccess ||
-      hipMemcpy(d_table_, &t, sizeof(PathTable), hipMemcpyHostToDevice) != hipSuccess)
-    err_ = "PathFilter: HIP setup failed";
+  bool ok = hipSetDevice(device) == hipSuccess &&
+            hipMalloc(reinterpret_cast<void**>(&d_table_), sizeof(PathTable)) == hipSuccess &&
+            hipMemcpy(d_table_, &t, sizeof(PathTable), hipMemcpyHostToDevice) == hipSuccess;
+  for (Slot& S : slots_)
+    ok = ok && hipStreamCreateWithPriority(&S.stream, hipStreamNonBlocking, hi) == hipSuccess &&
+         hipEventCreateWithFlags(&S.done, hipEventDisableTiming) == hipSuccess &&
+         hipMalloc(reinterpret_cast<void**>(&S.d_cnt), 64) == hipSuccess &&
+         hipHostMalloc(reinterpret_cast<void**>(&S.h_cnt), 64, hipHostMallocDefault) == hipSuccess;
+  if (!ok) err_ = "PathFilter: HIP setup failed";
 }
 
 PathFilter::~PathFilter() {
   (void)hipSetDevice(device_);
-  if (d_out_) (void)hipFree(d_out_);
-  if (h_out_) (void)hipHostFree(h_out_);
+  for (Slot& S : slots_) {
+    if (S.d_out) (void)hipFree(S.d_out);
+    if (S.h_out) (void)hipHostFree(S.h_out);
+    if (S.d_cnt) (void)hipFree(S.d_cnt);
+    if (S.h_cnt) (void)hipHostFree(S.h_cnt);
+    if (S.done) (void)hipEventDestroy(S.done);
+    if (S.stream) (void)hipStreamDestroy(S.stream);
+  }
   if (d_table_) (void)hipFree(d_table_);
-  if (d_cnt_) (void)hipFree(d_cnt_);
-  if (h_cnt_) (void)hipHostFree(h_cnt_);
-  if (done_) (void)hipEventDestroy(done_);
-  if (stream_) (void)hipStreamDestroy(stream_);
 }
 
 bool PathFilter::Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out,
                      std::string* err) {
-  std::lock_guard<std::mutex> g(mu_);
   out->clear();
   if (n == 0) return true;
+  Slot* S = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] {
+      for (Slot& x : slots_)
+        if (!x.busy) return true;
+      return false;
+    });
+    for (Slot& x : slots_)
+      if (!x.busy) {
+        S = &x;
+        break;
+      }
+    S->busy = true;
+  }
+  auto release = [&](bool ok) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      S->busy = false;
+    }
+    cv_.notify_one();
+    return ok;
+  };
   auto fail = [&](const char* what, hipError_t e) {
     *err = std::string("PathFilter: ") + what + ": " + hipGetErrorString(e);
-    return false;
+    return release(false);
   };
   // sleep-poll (as GpuEngine::WaitEvent): a spinning wait takes a core from the host pool
   auto wait = [&]() {
-    hipError_t e = hipEventRecord(done_, stream_);
+    hipError_t e = hipEventRecord(S->done, S->stream);
     if (e != hipSuccess) return e;
-    while ((e = hipEventQuery(done_)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    while ((e = hipEventQuery(S->done)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(100));
     return e;
   };
   hipError_t e = hipSetDevice(device_);
   if (e != hipSuccess) return fail("hipSetDevice", e);
-  if (cap_ < n) {
-    if (d_out_) (void)hipFree(d_out_);
-    if (h_out_) (void)hipHostFree(h_out_);
-    d_out_ = nullptr;
-    h_out_ = nullptr;
-    cap_ = 0;
-    if ((e = hipMalloc(reinterpret_cast<void**>(&d_out_), size_t(n) * sizeof(PathHit))) != hipSuccess ||
-        (e = hipHostMalloc(reinterpret_cast<void**>(&h_out_), size_t(n) * sizeof(PathHit), hipHostMallocDefault)) !=
+  if (S->cap < n) {
+    if (S->d_out) (void)hipFree(S->d_out);
+    if (S->h_out) (void)hipHostFree(S->h_out);
+    S->d_out = nullptr;
+    S->h_out = nullptr;
+    S->cap = 0;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&S->d_out), size_t(n) * sizeof(PathHit))) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&S->h_out), size_t(n) * sizeof(PathHit), hipHostMallocDefault)) !=
             hipSuccess)
       return fail("hipMalloc", e);
-    cap_ = n;
+    S->cap = n;
   }
-  if ((e = hipMemsetAsync(d_cnt_, 0, 4, stream_)) != hipSuccess) return fail("hipMemsetAsync", e);
+  if ((e = hipMemsetAsync(S->d_cnt, 0, 4, S->stream)) != hipSuccess) return fail("hipMemsetAsync", e);
   const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n) + kPathThreads - 1) / kPathThreads, 4096));
-  path_filter_kernel<<<grid, kPathThreads, 0, stream_>>>(d_paths, d_off, n, d_table_, d_cnt_, d_out_);
+  path_filter_kernel<<<grid, kPathThreads, 0, S->stream>>>(d_paths, d_off, n, d_table_, S->d_cnt, S->d_out);
   if ((e = hipGetLastError()) != hipSuccess) return fail("path_filter_kernel", e);
-  if ((e = hipMemcpyAsync(h_cnt_, d_cnt_, 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+  // the count and as many records as the last call had (+1/8): one round trip when the paths repeat
+  const uint32_t guess = std::min<uint32_t>(n, last_k_.load() + last_k_.load() / 8 + 1024);
+  if ((e = hipMemcpyAsync(S->h_cnt, S->d_cnt, 4, hipMemcpyDeviceToHost, S->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(S->h_out, S->d_out, size_t(guess) * sizeof(PathHit), hipMemcpyDeviceToHost, S->stream)) !=
+          hipSuccess ||
       (e = wait()) != hipSuccess)
-    return fail("count read-back", e);
-  const uint32_t k = *h_cnt_;
+    return fail("read-back", e);
+  const uint32_t k = *S->h_cnt;
   if (k > n) {
     *err = "PathFilter: record count out of range";
-    return false;
+    return release(false);
   }
-  if (k && ((e = hipMemcpyAsync(h_out_, d_out_, size_t(k) * sizeof(PathHit), hipMemcpyDeviceToHost, stream_)) !=
-                hipSuccess ||
-            (e = wait()) != hipSuccess))
+  if (k > guess && ((e = hipMemcpyAsync(S->h_out + guess, S->d_out + guess, size_t(k - guess) * sizeof(PathHit),
+                                        hipMemcpyDeviceToHost, S->stream)) != hipSuccess ||
+                    (e = wait()) != hipSuccess))
     return fail("record read-back", e);
-  out->assign(h_out_, h_out_ + k);
-  return true;
+  last_k_.store(k);
+  out->assign(S->h_out, S->h_out + k);
+  return release(true);
 }
 
 }  // namespace tsg
