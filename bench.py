@@ -518,7 +518,7 @@ def main():
         args.warmup = 3 if args.workload == "c2" else 2
     if args.traffic_file is None:  # the newest PMC pass of this workload (c2: traffic_rNN.json)
         cands = [os.path.join(ROOT, "profiles", "traffic_r%02d%s.json" % (r, "" if args.workload == "c2" else
-                                                                            "_" + args.workload)) for r in (3, 2)]
+                                                                            "_" + args.workload)) for r in range(9, 1, -1)]
         args.traffic_file = next((c for c in cands if os.path.exists(c)), cands[-1])
     wl_desc, gb_default, cpu_mb_default, parity_mb_default = WORKLOADS[args.workload]
     if args.parity_mb is None:
