@@ -776,11 +776,20 @@ __device__ int64_t count_nl_abs(const uint8_t* arena, const uint16_t* nl, uint64
 #ifndef TSG_C_PREFETCH
 #define TSG_C_PREFETCH 1
 #endif
+#ifndef TSG_C_REACH_COPIES
+#define TSG_C_REACH_COPIES 1
+#endif
 constexpr bool kCFse = TSG_C_FSE;     // cache each block's file in LDS in phase A (-0.2 ms at equal occupancy; costs 20 B/lane)
+// Copies of the 4-KiB reach table in the confirm kernel's LDS, the copy chosen
+// by lane & (copies - 1).  Phase A's row reads conflict (SQ_LDS_BANK_CONFLICT is
+// 29 % of K2's LDS cycles, profiles/r04f), but four copies (+12 KiB per
+// workgroup) measured K2 2.42 -> 3.42 ms (profiles/r04y): one copy stays.
+constexpr uint32_t kCReachCopies = TSG_C_REACH_COPIES;
+static_assert((kCReachCopies & (kCReachCopies - 1)) == 0, "a power of two");
 constexpr uint32_t kCQ1 = TSG_C_Q1;  // fires (overflow: handled in place)
 constexpr uint32_t kCQ2 = TSG_C_Q2;  // candidate items (overflow: checked in place)
 constexpr size_t ConfirmFixedLds(int t) {  // LDS of a t-thread workgroup besides the staged tables
-  return 4096 + size_t(t) * (kCWin + 8 + (kCFse ? 20 : 0)) + size_t(t / 64) * (kCQ1 + kCQ2) * 4 +
+  return 4096 * kCReachCopies + size_t(t) * (kCWin + 8 + (kCFse ? 20 : 0)) + size_t(t / 64) * (kCQ1 + kCQ2) * 4 +
          size_t(t / 64) * kCWaveHits * 12 + size_t(t / 64) * 16;
 }
 
@@ -795,8 +804,8 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int kCThreads = ConfirmThreads<kLdsTabs>();  // shadows the file-scope constant
   constexpr uint32_t kWaves = kCThreads / 64;
-  uint8_t* s_reach = smem;                                                      // 4 KiB, one copy per byte
-  uint8_t* s_win = smem + 4096;                                                 // kCThreads x 64 B
+  uint8_t* s_reach = smem;                                        // 4 KiB x kCReachCopies (row b: copies x 16 B)
+  uint8_t* s_win = smem + 4096 * kCReachCopies;                   // kCThreads x 64 B
   uint64_t* s_base = reinterpret_cast<uint64_t*>(s_win + kCThreads * kCWin);    // kCThreads
   uint64_t* s_fse = s_base + kCThreads;                                         // kCThreads x 2: block's file [fs, fe)
   uint32_t* s_file = reinterpret_cast<uint32_t*>(s_fse + (kCFse ? 2 * kCThreads : 0));  // kCThreads: block's file
@@ -806,7 +815,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   uint32_t* s_cnt = s_hbuf + kWaves * kCWaveHits * 3;                           // kWaves x 4
   uint8_t* s_tabs = reinterpret_cast<uint8_t*>(s_cnt + kWaves * 4);
   const int tid = threadIdx.x;
-  load_reach_lds(s_reach, P.reach, 1, tid, blockDim.x);
+  load_reach_lds(s_reach, P.reach, kCReachCopies, tid, blockDim.x);
   if (kLdsTabs) {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(s_tabs);
@@ -1054,8 +1063,9 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
       const uint4 pv = base >= 16 ? d0 : make_uint4(0, 0, 0, 0);
       const uint4 v = base >= 16 ? d1 : d0;
       uint32_t st[kFWords] = {~0u, ~0u, ~0u, ~0u};
-      auto rd1 = [&](uint32_t w, uint32_t k) {  // single-copy table: entry b at 16 * b
-        return *reinterpret_cast<const uint4*>(s_reach + (((w >> (8 * k)) & 0xFFu) << 4));
+      const uint32_t rcopy = lane & (kCReachCopies - 1);
+      auto rd1 = [&](uint32_t w, uint32_t k) {  // entry b, copy c at 16 * (b * copies + c)
+        return *reinterpret_cast<const uint4*>(s_reach + ((((w >> (8 * k)) & 0xFFu) * kCReachCopies + rcopy) << 4));
       };
 #pragma unroll
       for (uint32_t k = 11; k < 16; k++) reach_apply(rd1(word_of(pv, k >> 2), k & 3), st);
