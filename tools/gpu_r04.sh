@@ -78,9 +78,11 @@ for st in $STAGES; do
       done ;;
     ingab)  # ingest leg A/B of library variants (VARIANTS; base = the in-tree build), twice interleaved
       for rep in 1 2; do
-        for v in ${VARIANTS:-base}; do
+        for sp in ${VARIANTS:-base}; do  # variant[:ENV=V] (one env assignment)
+          v="${sp%%:*}"; E=""; [ "$sp" != "$v" ] && E="${sp#*:}"
           if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
-          TSG_LIB=$L timeout -k 10 400 python bench.py --steps 5 --warmup 2 --warmup-s 0 --no-cpu-baseline --ingest-steps 6 ${BENCH_ARGS:-} > gpurun_out/ingab_${TAG}_${v}_$rep.json 2> gpurun_out/ingab_${TAG}_${v}_$rep.err
+          v="$v${E:+_${E//=/}}"
+          env TSG_LIB=$L $E timeout -k 10 400 python bench.py --steps 5 --warmup 2 --warmup-s 0 --no-cpu-baseline --ingest-steps ${INGEST_STEPS:-6} ${BENCH_ARGS:-} > gpurun_out/ingab_${TAG}_${v}_$rep.json 2> gpurun_out/ingab_${TAG}_${v}_$rep.err
           rc=$?; echo "== $v $rep"; python - gpurun_out/ingab_${TAG}_${v}_$rep.json <<'PYEOF'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
