@@ -615,7 +615,7 @@ def main():
         dev = torch.device("cuda", local)
         if args.ingest:
             # host-resident corpus in a page-locked pool (the caller's pinned arena pool): every
-            # step streams it through the engine's double-buffered H2D (RunHost)
+            # step streams it through the engine's staging ring (RunHost)
             unregister = secret.HostRegister(C.arena)
             h2d_peak = measure_h2d(dev)
             d_arena = d_offs = d_paths = d_poffs = None

@@ -160,8 +160,9 @@ typedef struct tsg_stats {
 int tsg_result_stats(const tsg_result* r, tsg_stats* out);
 
 /* Page-lock a caller's host buffer (hipHostRegister) so batches in it stream
- * to the GPU asynchronously (two staging buffers, copies overlapping kernels):
- * the Go caller's pinned arena pool.  Unregister before freeing it. */
+ * to the GPU asynchronously (the engine's staging ring: copies of this and of
+ * the next submitted batches overlap the kernels): the Go caller's pinned arena
+ * pool.  Unregister before freeing it. */
 int tsg_host_register(void* p, uint64_t bytes);
 int tsg_host_unregister(void* p);
 

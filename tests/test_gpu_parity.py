@@ -274,7 +274,7 @@ def test_fold_runes_in_custom_rule_items(secret, tmp_path):
 
 
 def test_host_batches_stream_in_chunks(secret, monkeypatch):
-    """Host-resident batches (RunHost) streamed through two staging buffers in many chunks
+    """Host-resident batches (RunHost) streamed through the staging ring in many chunks
     (TSG_INGEST_CHUNK_MB), pipelined submissions included, give the device-resident
     results; the chunks really are many (h2d_chunks)."""
     import numpy as np

@@ -239,6 +239,15 @@ class GpuEngine {
   void* d_stage_off_[kNStage] = {}; size_t cap_stage_off_[kNStage] = {};
   uint64_t* h_off_[kNStage] = {}; size_t cap_h_off_[kNStage] = {};  // pinned, rebased chunk offsets
   uint64_t* h_xoff_ = nullptr; size_t cap_h_xoff_ = 0;  // pinned: transformed offsets + the error word
+  // Pinned staging of Run's counter / candidate read-back and GatherTail's
+  // uploads and read-back: a pageable hipMemcpy goes through the runtime's own
+  // staging and held up the copier's H2D of later chunks (blocking 20-80 ms
+  // copies at fixed chunks of the C2 ingest leg, TSG_RING_DEBUG).
+  uint32_t* h_run_cnt_ = nullptr;
+  void* h_run_cands_ = nullptr; size_t cap_h_run_cands_ = 0;
+  void* h_gup_ = nullptr; size_t cap_h_gup_ = 0;
+  void* h_gbuf_ = nullptr; size_t cap_h_gbuf_ = 0;
+  bool EnsureHost(void** p, size_t* cap, size_t need);
   // GPU pre-transform (xform.h): per-chunk kinds, lengths, transformed offsets and bytes, the gather
   void* d_kind_[kNStage] = {}; size_t cap_kind_[kNStage] = {};
   void* d_xlen_ = nullptr; size_t cap_xlen_ = 0;

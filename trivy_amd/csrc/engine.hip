@@ -2326,6 +2326,8 @@ GpuEngine::~GpuEngine() {
   for (auto* h : h_off_)
     if (h) hipHostFree(h);
   if (h_xoff_) hipHostFree(h_xoff_);
+  for (void* h : {static_cast<void*>(h_run_cnt_), h_run_cands_, h_gup_, h_gbuf_})
+    if (h) hipHostFree(h);
   if (copy_stream_) hipStreamDestroy(copy_stream_);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -2337,8 +2339,21 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
     hipFree(*p);
   }
   *p = nullptr;
-  size_t n = std::max<size_t>(need, 64);
+  // (+1/8: a batch slightly larger than the last does not free and reallocate again --
+  // hipFree synchronises the device, stalling the staging ring's copies)
+  size_t n = std::max<size_t>(need + need / 8, 64);
   HIP_OK(hipMalloc(p, n));
+  *cap = n;
+  return true;
+}
+
+bool GpuEngine::EnsureHost(void** p, size_t* cap, size_t need) {
+  if (*p && *cap >= need) return true;
+  if (*p) hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const size_t n = std::max<size_t>(need + need / 4, 4096);
+  HIP_OK(hipHostMalloc(p, n, hipHostMallocDefault));
   *cap = n;
   return true;
 }
@@ -2352,6 +2367,16 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
 // asynchronous (hipHostMalloc / tsg_host_register).  The copies are issued off
 // the scanning threads: on this runtime a 1-GiB hipMemcpyAsync from registered
 // memory returns only once the transfer is done (profiles/r02_ingest_trace_*).
+// TSG_RING_DEBUG=1: one stderr line per ring event (reserve / copy / scan), ms since the first
+static void RingLog(const char* what, uint64_t slot, uint64_t extra) {
+  static const bool on = std::getenv("TSG_RING_DEBUG") && std::atoi(std::getenv("TSG_RING_DEBUG")) != 0;
+  if (!on) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::fprintf(stderr, "ring %10.3f %-12s slot %llu %llu\n", ms, what, (unsigned long long)slot,
+               (unsigned long long)extra);
+}
+
 struct GpuEngine::HostCall {
   const uint8_t* h_arena;
   const uint64_t* h_offsets;
@@ -2373,29 +2398,36 @@ bool GpuEngine::CopyChunk(const StageJob& j, std::string* err) {
     *err = std::string(what) + ": " + hipGetErrorString(x);
     return false;
   };
-  auto grow = [&](void** p, size_t* cap, size_t need) -> hipError_t {
+  // Growth is rare and generous: hipFree / hipHostFree synchronise the device, so
+  // a buffer grown by a few bytes for each slightly larger chunk stalled the copier
+  // behind every kernel in flight (20-50 ms, TSG_RING_DEBUG): the arena buffers
+  // start at a whole chunk, the per-file arrays grow by half again.
+  auto grow = [&](void** p, size_t* cap, size_t need, size_t floor) -> hipError_t {
     if (*p && *cap >= need) return hipSuccess;
-    if (*p) hipFree(*p);  // (implicitly synchronising; rare: a larger chunk than before)
+    if (*p) hipFree(*p);
     *p = nullptr;
     *cap = 0;
-    const hipError_t x = hipMalloc(p, need);
-    if (x == hipSuccess) *cap = need;
+    const size_t n = std::max(need + need / 2, floor);
+    const hipError_t x = hipMalloc(p, n);
+    if (x == hipSuccess) *cap = n;
     return x;
   };
   hipError_t x;
   if ((x = hipEventSynchronize(ev_copied_[b])) != hipSuccess) return fail("staging event", x);  // h_off_[b] reusable
-  if ((x = grow(&d_stage_[b], &cap_stage_[b], (e - a) + 64)) != hipSuccess ||
-      (x = grow(&d_stage_off_[b], &cap_stage_off_[b], (size_t(nf) + 1) * 8)) != hipSuccess ||
-      (c.kinds && (x = grow(&d_kind_[b], &cap_kind_[b], size_t(nf) + 1)) != hipSuccess))
+  const size_t arena_need = (e - a) + 64;
+  if ((x = grow(&d_stage_[b], &cap_stage_[b], arena_need,
+                std::min<size_t>(chunk_bytes_, 4 * (e - a)) + 64)) != hipSuccess ||
+      (x = grow(&d_stage_off_[b], &cap_stage_off_[b], (size_t(nf) + 1) * 8, 0)) != hipSuccess ||
+      (c.kinds && (x = grow(&d_kind_[b], &cap_kind_[b], size_t(nf) + 1, 0)) != hipSuccess))
     return fail("staging hipMalloc", x);
   if (cap_h_off_[b] < size_t(nf) + 1) {
     if (h_off_[b]) hipHostFree(h_off_[b]);
     h_off_[b] = nullptr;
     cap_h_off_[b] = 0;
-    if ((x = hipHostMalloc(reinterpret_cast<void**>(&h_off_[b]), (size_t(nf) + 1) * 8, hipHostMallocDefault)) !=
-        hipSuccess)
+    const size_t n = size_t(nf) + 1 + (size_t(nf) + 1) / 2;
+    if ((x = hipHostMalloc(reinterpret_cast<void**>(&h_off_[b]), n * 8, hipHostMallocDefault)) != hipSuccess)
       return fail("staging hipHostMalloc", x);
-    cap_h_off_[b] = size_t(nf) + 1;
+    cap_h_off_[b] = n;
   }
   for (uint32_t f = j.f0; f <= j.f1; f++) h_off_[b][f - j.f0] = c.h_offsets[f] - a;
   if (!c.ev0_recorded) {
@@ -2432,7 +2464,11 @@ void GpuEngine::CopierLoop() {
     const bool skip = j.call->cancelled;
     lk.unlock();
     std::string e;
+    RingLog("copy-issue", j.slot, ring_turn_);
+    RingLog("copy-src", j.slot, (reinterpret_cast<uintptr_t>(j.call->h_arena + j.call->h_offsets[j.f0]) & 0xFFFFF) |
+                                    (uint64_t(j.call->h_offsets[j.f1] - j.call->h_offsets[j.f0]) << 20));
     const bool ok = !skip && CopyChunk(j, &e);
+    RingLog("copy-issued", j.slot, 0);
     lk.lock();
     const int b = int(j.slot % kNStage);
     stage_ok_[b] = ok;
@@ -2490,6 +2526,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     ring_next_ += n_chunks;
     for (size_t k = 0; k < n_chunks; k++) ring_jobs_.push_back(StageJob{s0 + k, &call, cut[k], cut[k + 1]});
   }
+  RingLog("reserve", s0, n_chunks);
   ring_cv_.notify_all();
   bool ok = true;
   std::vector<Candidate> part;
@@ -2507,9 +2544,11 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
       }
       if (!ok) call.cancelled = true;
     }
+    RingLog("turn", slot, 0);
     if (ok) {
       std::unique_lock<std::mutex> g;
       if (dev_mu) g = std::unique_lock<std::mutex>(*dev_mu);
+      RingLog("scan-start", slot, 0);
       const uint32_t f0 = cut[k], f1 = cut[k + 1];
       BatchStats cs;
       const uint8_t* scan_arena = static_cast<const uint8_t*>(d_stage_[b]);
@@ -2558,6 +2597,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
       if (copied) (void)hipStreamSynchronize(copy_stream_);
       (void)hipStreamSynchronize(stream_);  // a failed chunk's kernels may still be queued
     }
+    RingLog("scan-end", slot, 0);
     {
       std::lock_guard<std::mutex> g(ring_mu_);
       ring_turn_ = slot + 1;
@@ -2659,15 +2699,22 @@ bool GpuEngine::GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint
   if (!Ensure(&d_gfiles_, &cap_gfiles_, files.size() * 4) || !Ensure(&d_gdst_, &cap_gdst_, files.size() * 8) ||
       !Ensure(&d_gbuf_, &cap_gbuf_, total + 64))
     return false;
-  HIP_OK(hipMemcpyAsync(d_gfiles_, files.data(), files.size() * 4, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_gdst_, dst.data(), dst.size() * 8, hipMemcpyHostToDevice, stream_));
+  // uploads and read-back through pinned staging (engine.h)
+  const size_t up = files.size() * 12;
+  if (!EnsureHost(&h_gup_, &cap_h_gup_, up) || !EnsureHost(&h_gbuf_, &cap_h_gbuf_, total + 1)) return false;
+  uint8_t* hu = static_cast<uint8_t*>(h_gup_);
+  std::memcpy(hu, dst.data(), dst.size() * 8);
+  std::memcpy(hu + dst.size() * 8, files.data(), files.size() * 4);
+  HIP_OK(hipMemcpyAsync(d_gdst_, hu, dst.size() * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_gfiles_, hu + dst.size() * 8, files.size() * 4, hipMemcpyHostToDevice, stream_));
   HIP_OK(GatherFiles(static_cast<const uint8_t*>(d_xf_), static_cast<const uint64_t*>(d_xoff_),
                      static_cast<const uint32_t*>(d_gfiles_), static_cast<const uint64_t*>(d_gdst_),
                      uint32_t(files.size()), static_cast<uint8_t*>(d_gbuf_), stream_));
+  HIP_OK(hipMemcpyAsync(h_gbuf_, d_gbuf_, total, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(WaitStream());
   const size_t at = tail->buf.size();
   tail->buf.resize(at + total);
-  HIP_OK(hipMemcpyAsync(tail->buf.data() + at, d_gbuf_, total, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
+  std::memcpy(tail->buf.data() + at, h_gbuf_, total);
   return true;
 }
 
@@ -3043,8 +3090,10 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
   for (int attempt = 0; attempt < 8; attempt++) {
     if (!EnqueuePhase(d_arena, n_bytes, d_offsets, n_files, n_chunks, ev_, ev_fs_)) return false;
     uint32_t cnt[16];
-    HIP_OK(hipMemcpyAsync(cnt, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
+    if (!h_run_cnt_) HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&h_run_cnt_), 64, hipHostMallocDefault));
+    HIP_OK(hipMemcpyAsync(h_run_cnt_, d_counters_, sizeof(cnt), hipMemcpyDeviceToHost, stream_));
     HIP_OK(WaitStream());
+    std::memcpy(cnt, h_run_cnt_, sizeof(cnt));
     if (std::getenv("TSG_STATS_DEBUG"))
       std::fprintf(stderr, "counters: hits %u cands %u special %u recs %u folds %u\n", cnt[0], cnt[1], cnt[2], cnt[7],
                    cnt[9]);
@@ -3081,9 +3130,11 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
     }
     cands->resize(cnt[1]);
     if (cnt[1]) {
-      HIP_OK(hipMemcpyAsync(cands->data(), d_cands_, size_t(cnt[1]) * sizeof(Candidate), hipMemcpyDeviceToHost,
-                            stream_));
+      const size_t nb = size_t(cnt[1]) * sizeof(Candidate);
+      if (!EnsureHost(&h_run_cands_, &cap_h_run_cands_, nb)) return false;
+      HIP_OK(hipMemcpyAsync(h_run_cands_, d_cands_, nb, hipMemcpyDeviceToHost, stream_));
       HIP_OK(WaitStream());
+      std::memcpy(cands->data(), h_run_cands_, nb);
     }
     // closed keyword gates (finalize_kernel) never reach the host
     cands->erase(std::remove_if(cands->begin(), cands->end(), [](const Candidate& c) { return c.flags & kCandDrop; }),
