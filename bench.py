@@ -797,6 +797,10 @@ def main():
         counts["anchor_item_matches"] = counts["anchor_hits"]
         counts["hits_to_verify"] = counts["follow_hits"]
         breakdown.update({k: round(avg(k), 3) for k in ("ms_host_allow_path", "ms_host_total")})
+        # the pipeline's drain: the last scan's host work after its GPU phase (nothing overlaps it),
+        # and the timed region beyond the steps' GPU time (fill, drain, gaps between scans)
+        breakdown["ms_last_scan_after_gpu"] = round(last["ms_host_total"] - last["ms_host_gpu_phase"], 3)
+        breakdown["ms_timed_minus_gpu"] = round(dt * 1e3 - args.steps * emissions * gpu_ms, 3)
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
                         "crlf_files": int(R.crlf.sum()) if R is not None else 0,
                         "arena_bytes_after_cr_strip": C.n_bytes,
