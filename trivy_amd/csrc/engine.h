@@ -149,6 +149,7 @@ class GpuEngine {
   std::atomic<uint32_t> cand_recent_{0};  // largest candidate count of the recently collected scans
   Slot slots_[kSlots];
   std::mutex slot_mu_;
+  std::vector<void*> retired_host_;  // outgrown read-back buffers, freed with the engine (slot_mu_)
   bool Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
                  std::vector<uint64_t>* xoff, float* ms);
   bool GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf, const std::vector<uint64_t>& xoff,

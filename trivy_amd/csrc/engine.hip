@@ -2319,6 +2319,7 @@ GpuEngine::~GpuEngine() {
     if (S.h_cnt) hipHostFree(S.h_cnt);
     if (S.h_cands) hipHostFree(S.h_cands);
   }
+  for (void* p : retired_host_) hipHostFree(p);
   for (auto& e : ev_h2d_)
     if (e) hipEventDestroy(e);
   for (auto& e : ev_x_)
@@ -2783,15 +2784,24 @@ bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t
   }
   const uint32_t n_copy = uint32_t(std::min<uint64_t>(cand_cap_, 2 * uint64_t(cand_recent_.load()) + 65536));
   if (S.h_cap < n_copy) {
-    if (S.h_cands) hipHostFree(S.h_cands);
+    // Sized to the device list's capacity (not to the copy, which follows the
+    // recent counts): hipHostFree waits for the whole device, so a slot regrown
+    // in a running pipeline stalled its submitting thread -- holding the GPU
+    // lock -- for 11-19 ms and left the GPU idle 1.7 ms per regrowth
+    // (tools/drain_trace.py, profiles/r04h2).  It regrows only with cand_cap_,
+    // and the old buffer is retired (freed with the engine), not freed here.
+    if (S.h_cands) {
+      std::lock_guard<std::mutex> g(slot_mu_);
+      retired_host_.push_back(S.h_cands);
+    }
     S.h_cands = nullptr;
     S.h_cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&S.h_cands), size_t(n_copy) * sizeof(Candidate),
+    if (hipHostMalloc(reinterpret_cast<void**>(&S.h_cands), size_t(cand_cap_) * sizeof(Candidate),
                       hipHostMallocDefault) != hipSuccess) {
       err_ = "hipHostMalloc failed for the candidate read-back";
       return fail();
     }
-    S.h_cap = n_copy;
+    S.h_cap = cand_cap_;
   }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
   if (n_chunks == 0) n_chunks = 1;
