@@ -71,11 +71,16 @@ typedef struct tsg_tar_stats {
  * batch filled up (*cursor = the entry to resume from), <0 on a malformed
  * archive.  Whiteout (.wh.) and opaque-dir entries are counted, not added. */
 int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st);
-/* Buffer lifetime: the analyzer indexes the next window of entries on a
- * background thread after tsg_collector_add_tar returns 1, so `tar` must stay
- * valid and unchanged until that walk ends -- add_tar returned 0 (end of the
- * archive) or < 0 -- or until tsg_analyzer_walk_end / tsg_analyzer_free
- * returns (call it before freeing the buffer of a walk abandoned midway). */
+/* Walk-ahead (opt-in, off by default): with tsg_analyzer_set_walk_ahead(a, 1)
+ * the analyzer indexes the next window of entries on a background thread after
+ * tsg_collector_add_tar returns 1.  Buffer lifetime in that mode: `tar` must
+ * stay valid and unchanged until the walk ends -- add_tar returned 0 (end of
+ * the archive) or < 0 -- or until tsg_analyzer_walk_end / tsg_analyzer_free /
+ * tsg_analyzer_set_walk_ahead(a, 0) returns (call one before freeing the
+ * buffer of a walk abandoned midway).  With walk-ahead off, nothing reads
+ * `tar` after add_tar returns.  tsg_analyzer_walk_end also drops the walk's
+ * cached window, so a later buffer at the same address starts afresh. */
+int tsg_analyzer_set_walk_ahead(tsg_analyzer* a, int on);
 int tsg_analyzer_walk_end(tsg_analyzer* a);
 
 /* GPU pre-transform mode (empty collector only): files go into the arena as

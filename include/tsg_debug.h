@@ -81,6 +81,14 @@ const char* tsg_debug_rule_anchor(const tsg_compiled* c, uint32_t i);
  * ranks (or TSG_POOL_SHARE processes), minus the per-process reserve. */
 int tsg_debug_pool_budget(void);
 
+/* A scanner's GPU engines' host-memory bookkeeping, summed over its engines:
+ * out[0] retired pinned read-back buffers not yet freed, out[1] retired buffers
+ * freed (by the engine's reaper thread), out[2] the largest candidate capacity,
+ * out[3] pinned read-back bytes held by the ticket slots.  Returns -1 for a
+ * scanner without a GPU engine.  (Bookkeeping for tests; call it between scans.) */
+struct tsg_scanner;
+int tsg_debug_scanner_engine(struct tsg_scanner* s, uint64_t out[4]);
+
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);
 

@@ -388,6 +388,48 @@ def test_device_batches_pipelined_tickets_and_overflow(secret):
         assert got[i].to_dict() == o.scan(paths[i], contents[i])
 
 
+def test_retired_readback_buffers_are_freed(secret):
+    """VERDICT r04 item 7 / ADVICE r04: a ticket slot whose pinned candidate read-back is
+    outgrown (the candidate capacity grew: batches of 80 k, 200 k and 500 k findings) retires
+    the old buffer to the engine's reaper thread, which frees it outside the engine's locks --
+    the retired list drains between scans instead of living as long as the engine.  Every
+    scan's findings stay complete."""
+    import ctypes as c
+    import time
+    import numpy as np
+    import torch
+    s = secret.NewScanner(None)
+    L = s._L
+    L.tsg_debug_scanner_engine.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
+    info = (c.c_uint64 * 4)()
+    caps = []
+    for n in (80000, 200000, 500000):
+        contents = [b"k=AKIA%016d\n" % i for i in range(n)]
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(x) for x in contents])
+        arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+        paths = ["f%06d.txt" % i for i in range(n)]
+        d_arena = torch.from_numpy(arena.copy()).to("cuda:0")
+        d_offs = torch.from_numpy(offs.view(np.int64)).to("cuda:0")
+        for _ in range(3):  # the first overflows and reruns (cand_cap grows); later ones regrow a slot
+            r = s.scan_arena(arena, offs, paths, dev_arena=d_arena.data_ptr(), dev_offsets=d_offs.data_ptr())
+            assert r.stats()["findings"] == n
+            del r
+        assert L.tsg_debug_scanner_engine(s._h, info) == 0
+        caps.append(int(info[2]))
+        del d_arena, d_offs
+    assert caps[0] < caps[1] < caps[2]
+    deadline = time.time() + 20
+    while True:
+        assert L.tsg_debug_scanner_engine(s._h, info) == 0
+        if info[0] == 0 or time.time() > deadline:
+            break
+        time.sleep(0.05)
+    pending, freed, cap, slot_bytes = (int(x) for x in info)
+    assert pending == 0 and freed >= 2, (pending, freed)
+    assert slot_bytes <= 4 * cap * 64  # only the live slots' buffers remain
+
+
 def _allow_paths_batch(rng):
     """Paths around the builtin allow rules' literals (scanner builtin-allow-rules.go):
     every case mix, literals at the start / end / middle, near misses, non-ASCII

@@ -51,6 +51,7 @@ def _declare(L):
     L.tsg_analyzer_new.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_void_p)]
     L.tsg_analyzer_free.argtypes = [c.c_void_p]
     L.tsg_analyzer_walk_end.argtypes = [c.c_void_p]
+    L.tsg_analyzer_set_walk_ahead.argtypes = [c.c_void_p, c.c_int]
     L.tsg_analyzer_required.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64, c.c_int64]
     L.tsg_collector_new.argtypes = [c.c_void_p, c.c_uint64, c.POINTER(c.c_void_p)]
     L.tsg_collector_free.argtypes = [c.c_void_p]
@@ -158,6 +159,7 @@ class Collector:
         """gpu_transform: files enter the arena as read and the CR strip / printable
         extraction runs on the GPU at scan time (tsg_collector_set_gpu_transform)."""
         self._L = analyzer._L
+        self._an = analyzer  # the C collector borrows the analyzer (and its walk state)
         h = c.c_void_p()
         if self._L.tsg_collector_new(analyzer._h, int(arena_bytes), c.byref(h)) != 0:
             raise RuntimeError("tsg_collector_new failed: %s" % _lib.last_error(self._L))
@@ -176,10 +178,16 @@ class Collector:
         return self._L.tsg_collector_add(self._h, p, len(p), _b(dir_), content, len(content))
 
     def add_tar(self, buf, cursor: int, stats: _CTarStats):
-        """Walk the layer from ``cursor``: (1 when full / 0 at the end, next cursor)."""
+        """Walk the layer from ``cursor``: (1 when full / 0 at the end, next cursor).
+        With the analyzer's walk-ahead on, the next window of the layer is indexed on a
+        background thread after a return of 1, so the analyzer keeps ``buf`` alive until
+        the walk ends (0, an error, or SecretAnalyzer.WalkEnd) -- tsg_analyzer.h."""
         cur = c.c_uint64(cursor)
         addr = buf.ctypes.data if hasattr(buf, "ctypes") else c.cast(c.c_char_p(buf), c.c_void_p).value
+        self._an._walk_buf = buf
         rc = self._L.tsg_collector_add_tar(self._h, addr, len(buf), c.byref(cur), c.byref(stats))
+        if rc != 1:  # the walk ended (the C side joined any background index)
+            self._an._walk_buf = None
         if rc < 0:
             raise ValueError("tar layer: %s" % _lib.last_error(self._L))
         return rc, cur.value
@@ -294,6 +302,7 @@ class SecretAnalyzer:
         self.device = device
         self._host_only = host_only
         self._h = None
+        self._walk_buf = None  # the layer buffer of a walk in progress (Collector.add_tar)
         self.scanner = None
         self.configPath = configPath
         if scanner is not None:
@@ -302,17 +311,28 @@ class SecretAnalyzer:
     def _bind(self, scanner, configPath):
         if self._h:
             self._L.tsg_analyzer_free(self._h)
+            self._h = None
+            self._walk_buf = None
         self.scanner = scanner
         self.configPath = configPath
         h = c.c_void_p()
         if self._L.tsg_analyzer_new(scanner._h, _b(configPath), c.byref(h)) != 0:
             raise RuntimeError("tsg_analyzer_new failed: %s" % _lib.last_error(self._L))
         self._h = h
+        # walk-ahead: this object keeps the layer buffer alive until the walk ends
+        self._L.tsg_analyzer_set_walk_ahead(h, 1)
+
+    def WalkEnd(self):
+        """Ends a tar walk (joins its background index): the layer buffer may go after this."""
+        if self._h:
+            self._L.tsg_analyzer_walk_end(self._h)
+        self._walk_buf = None
 
     def __del__(self):
         if getattr(self, "_h", None):
-            self._L.tsg_analyzer_free(self._h)
+            self._L.tsg_analyzer_free(self._h)  # joins a walk's background index
             self._h = None
+        self._walk_buf = None
 
     # --- reference API ------------------------------------------------------
     def Init(self, opt: AnalyzerOptions):  # secret.go:86-101
@@ -435,7 +455,7 @@ class SecretAnalyzer:
         try:
             t_walk, t_wait = _pipeline(colls, fill, take)
         finally:  # the layer buffer may go away after this call (tsg_analyzer.h buffer lifetime)
-            self._L.tsg_analyzer_walk_end(self._h)
+            self.WalkEnd()
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})

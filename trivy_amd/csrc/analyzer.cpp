@@ -754,7 +754,15 @@ void FreeTarWalkCache(TarWalkCache* w) { delete w; }
 void EndTarWalk(TarWalkCache* w) {
   if (!w) return;
   w->Join();
+  // nothing of the ended walk may be reused: a later layer buffer at the same
+  // address must not hit the cached window of this one
   w->ahead_ok = false;
+  w->ahead_tar = nullptr;
+  w->ahead = TarWindow();
+  w->tar = nullptr;
+  w->n = 0;
+  w->w = TarWindow();
+  w->pos = 0;
 }
 }  // namespace tsg
 
@@ -937,7 +945,10 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
   static double t_phase[4];
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const EvalCtx ectx{c->a, c->gpu_xform};
-  static const bool bg_index = !std::getenv("TSG_WALK_BG") || std::atoi(std::getenv("TSG_WALK_BG")) != 0;
+  // the next window on a background thread only when the caller opted in
+  // (tsg_analyzer_set_walk_ahead; TSG_WALK_BG=0 turns it off everywhere)
+  static const bool bg_env = !std::getenv("TSG_WALK_BG") || std::atoi(std::getenv("TSG_WALK_BG")) != 0;
+  const bool bg_index = bg_env && c->a->walk_ahead;
   for (;;) {
     // 1. the cached entries from p on, else the window indexed ahead in the
     // background (when it starts at p), else index a window starting at p
@@ -1074,6 +1085,17 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
 int tsg_analyzer_walk_end(tsg_analyzer* a) {
   std::lock_guard<std::mutex> g(a->walk_mu);
   tsg::EndTarWalk(a->walk);
+  return 0;
+}
+
+int tsg_analyzer_set_walk_ahead(tsg_analyzer* a, int on) {
+  if (!a) {
+    tsg::SetError("tsg_analyzer_set_walk_ahead: null analyzer");
+    return -1;
+  }
+  std::lock_guard<std::mutex> g(a->walk_mu);
+  if (!on) tsg::EndTarWalk(a->walk);  // no background index outlives the switch
+  a->walk_ahead = on != 0;
   return 0;
 }
 

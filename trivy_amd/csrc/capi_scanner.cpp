@@ -563,4 +563,17 @@ const char* tsg_debug_keyword(const tsg_compiled* c, uint32_t k) {
   return k < c->cr.keywords.size() ? c->cr.keywords[k].c_str() : nullptr;
 }
 
+int tsg_debug_scanner_engine(tsg_scanner* s, uint64_t out[4]) {
+  out[0] = out[1] = out[2] = out[3] = 0;
+  if (!s || !s->s || s->s->n_engines() == 0) return -1;
+  for (size_t i = 0; i < s->s->n_engines(); i++) {
+    const tsg::GpuEngine::HostMemInfo m = s->s->engine_at(i)->host_mem_info();
+    out[0] += m.retired_pending;
+    out[1] += m.retired_freed;
+    out[2] = std::max<uint64_t>(out[2], m.cand_cap);
+    out[3] += m.slot_bytes;
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -29,6 +29,10 @@ struct tsg_analyzer {
   // two-collector pipeline alternate on one layer).
   std::mutex walk_mu;
   tsg::TarWalkCache* walk = nullptr;
+  // tsg_analyzer_set_walk_ahead: index the next window of a tar walk on a
+  // background thread (off by default: the layer buffer must then outlive the
+  // call that returned 1, the rule in tsg_analyzer.h).
+  bool walk_ahead = false;
   ~tsg_analyzer() { tsg::FreeTarWalkCache(walk); }
 };
 

@@ -98,10 +98,14 @@ class GpuEngine {
   // GPU before the scan, and the transformed bytes of the files that got
   // candidates come back in *tail.  Concurrent calls are allowed; the caller
   // must NOT hold the engine's device lock: RunHost takes `dev_mu` (the lock
-  // the caller's other scans on this engine use) around each chunk's GPU work.
+  // the caller's other scans on this engine use) around each chunk's GPU work;
+  // a null dev_mu means the engine's own device lock (dev_mu_), which then
+  // must be the only lock guarding this engine's Run / Enqueue calls.  A
+  // failure's text comes back in *err (err_ is shared with the other users of
+  // the engine, so it is not the channel for a call that runs beside them).
   bool RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
-               std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds = nullptr,
-               TailOut* tail = nullptr, std::mutex* dev_mu = nullptr);
+               std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail,
+               std::mutex* dev_mu, std::string* err);
 
   // Split form of Run for pipelined callers: Enqueue (with the engine's lock
   // held) puts the whole GPU phase and the copies of the counters and of the
@@ -149,7 +153,31 @@ class GpuEngine {
   std::atomic<uint32_t> cand_recent_{0};  // largest candidate count of the recently collected scans
   Slot slots_[kSlots];
   std::mutex slot_mu_;
-  std::vector<void*> retired_host_;  // outgrown read-back buffers, freed with the engine (slot_mu_)
+  std::mutex dev_mu_;  // RunHost's device lock when the caller passes none
+  // Outgrown pinned read-back buffers.  hipHostFree waits for the whole
+  // device, so they are not freed by the thread that regrows a slot (it holds
+  // the GPU lock); a reaper thread frees them outside every engine lock, so
+  // only that thread waits for the device.  Nothing references a retired
+  // buffer: a slot is regrown only after Collect released its last ticket.
+  void RetireHost(void* p);
+  void ReaperLoop();
+  std::mutex reap_mu_;
+  std::condition_variable reap_cv_;
+  std::vector<void*> retired_host_;  // (reap_mu_)
+  bool reap_stop_ = false;           // (reap_mu_)
+  std::thread reaper_;               // started with the first retirement
+  std::atomic<uint64_t> retired_pending_{0}, retired_freed_{0};
+
+ public:
+  // Host memory bookkeeping (tests, tsg_debug_scanner_engine): retired
+  // buffers not yet freed, retired buffers freed, the candidate capacity and
+  // the pinned read-back bytes the ticket slots hold.
+  struct HostMemInfo {
+    uint64_t retired_pending, retired_freed, cand_cap, slot_bytes;
+  };
+  HostMemInfo host_mem_info();
+
+ private:
   bool Transform(int b, uint32_t nf, const uint8_t** arena, const uint64_t** offsets, uint64_t* n_bytes,
                  std::vector<uint64_t>* xoff, float* ms);
   bool GatherTail(const std::vector<Candidate>& part, uint32_t f0, uint32_t nf, const std::vector<uint64_t>& xoff,

@@ -60,8 +60,36 @@ constexpr int kScanWaves = kScanThreads / 64;
 // thousands of stores to one thread; a search per chunk cost 20 dependent
 // loads per chunk, 0.32 ms on C2.)
 constexpr uint32_t kK0Run = 16;
+// The per-scan clears ride on K0 (they were three hipMemsetAsync fill kernels
+// per scan, 103 __amd_rocclr_fillBufferAligned launches per 18 C2 scans in
+// profiles/r04final2): the per-file flags and keyword bits, the 16 counters
+// and the full-scan list counters.  Every later kernel of the phase is
+// stream-ordered after K0.
+struct ClearParams {
+  uint32_t* flags;     // n_files
+  uint32_t* kw;        // n_files x kw_words
+  uint64_t n_kw;       // words of kw
+  uint32_t* counters;  // 16
+  uint32_t* fs_ctr;    // 16, or null
+};
+__device__ __forceinline__ void clear_words(uint32_t* p, uint64_t n, uint64_t tid, uint64_t nthr) {
+  // hipMalloc'd buffers are 256-B aligned: 16-B stores, the last n % 4 words singly
+  const uint64_t n4 = n / 4;
+  for (uint64_t i = tid; i < n4; i += nthr) reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
+  if (tid < n % 4) p[4 * n4 + tid] = 0;
+}
 __global__ __launch_bounds__(256) void chunk_map_kernel(const uint64_t* __restrict__ off, uint32_t n_files,
-                                                        uint64_t n_chunks, uint32_t* __restrict__ chunk_file) {
+                                                        uint64_t n_chunks, uint32_t* __restrict__ chunk_file,
+                                                        ClearParams Z) {
+  {
+    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x, nthr = uint64_t(gridDim.x) * blockDim.x;
+    clear_words(Z.flags, n_files, tid, nthr);
+    clear_words(Z.kw, Z.n_kw, tid, nthr);
+    if (tid < 16) {
+      Z.counters[tid] = 0;
+      if (Z.fs_ctr) Z.fs_ctr[tid] = 0;
+    }
+  }
   const uint64_t n_runs = (n_chunks + kK0Run - 1) / kK0Run;
   for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n_runs;
        r += uint64_t(gridDim.x) * blockDim.x) {
@@ -2295,6 +2323,12 @@ GpuEngine::~GpuEngine() {
   }
   ring_cv_.notify_all();
   if (copier_.joinable()) copier_.join();
+  {
+    std::lock_guard<std::mutex> g(reap_mu_);
+    reap_stop_ = true;
+  }
+  reap_cv_.notify_all();
+  if (reaper_.joinable()) reaper_.join();
   hipSetDevice(device_);
   void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
@@ -2319,7 +2353,7 @@ GpuEngine::~GpuEngine() {
     if (S.h_cnt) hipHostFree(S.h_cnt);
     if (S.h_cands) hipHostFree(S.h_cands);
   }
-  for (void* p : retired_host_) hipHostFree(p);
+  for (void* p : retired_host_) hipHostFree(p);  // (the reaper was joined first)
   for (auto& e : ev_h2d_)
     if (e) hipEventDestroy(e);
   for (auto& e : ev_x_)
@@ -2346,6 +2380,42 @@ bool GpuEngine::Ensure(void** p, size_t* cap, size_t need) {
   HIP_OK(hipMalloc(p, n));
   *cap = n;
   return true;
+}
+
+void GpuEngine::RetireHost(void* p) {
+  {
+    std::lock_guard<std::mutex> g(reap_mu_);
+    retired_host_.push_back(p);
+    retired_pending_.fetch_add(1);
+    if (!reaper_.joinable()) reaper_ = std::thread([this] { ReaperLoop(); });
+  }
+  reap_cv_.notify_one();
+}
+
+void GpuEngine::ReaperLoop() {
+  pthread_setname_np(pthread_self(), "tsg-hostfree");
+  std::unique_lock<std::mutex> lk(reap_mu_);
+  for (;;) {
+    reap_cv_.wait(lk, [&] { return reap_stop_ || !retired_host_.empty(); });
+    if (reap_stop_) return;  // the destructor frees what is left
+    std::vector<void*> batch;
+    batch.swap(retired_host_);
+    lk.unlock();
+    (void)hipSetDevice(device_);
+    for (void* p : batch) {
+      (void)hipHostFree(p);  // waits for the device: only this thread
+      retired_pending_.fetch_sub(1);
+      retired_freed_.fetch_add(1);
+    }
+    lk.lock();
+  }
+}
+
+GpuEngine::HostMemInfo GpuEngine::host_mem_info() {
+  HostMemInfo m{retired_pending_.load(), retired_freed_.load(), cand_cap_, 0};
+  std::lock_guard<std::mutex> g(slot_mu_);
+  for (const auto& S : slots_) m.slot_bytes += uint64_t(S.h_cap) * sizeof(Candidate);
+  return m;
 }
 
 bool GpuEngine::EnsureHost(void** p, size_t* cap, size_t need) {
@@ -2481,7 +2551,8 @@ void GpuEngine::CopierLoop() {
 
 bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                         std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail,
-                        std::mutex* dev_mu) {
+                        std::mutex* dev_mu, std::string* err) {
+  if (!dev_mu) dev_mu = &dev_mu_;
   cands->clear();
   BatchStats local;
   if (!st) st = &local;
@@ -2494,11 +2565,9 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     tail->raw.assign(n_files, 1);
     tail->xform_bytes = 0;
   }
-  std::string fail;  // (err_ is written only under dev_mu)
-  auto set_err = [&](const std::string& m) {
-    std::unique_lock<std::mutex> g;
-    if (dev_mu) g = std::unique_lock<std::mutex>(*dev_mu);
-    err_ = m;
+  std::string fail;
+  auto set_err = [&](const std::string& m) {  // the caller's message, not err_ (shared)
+    if (err) *err = m;
     return false;
   };
   if (kinds && !tail) return set_err("RunHost: a transformed batch needs a tail output");
@@ -2547,8 +2616,7 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     }
     RingLog("turn", slot, 0);
     if (ok) {
-      std::unique_lock<std::mutex> g;
-      if (dev_mu) g = std::unique_lock<std::mutex>(*dev_mu);
+      std::unique_lock<std::mutex> g(*dev_mu);
       RingLog("scan-start", slot, 0);
       const uint32_t f0 = cut[k], f1 = cut[k + 1];
       BatchStats cs;
@@ -2789,18 +2857,22 @@ bool GpuEngine::Enqueue(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t
     // in a running pipeline stalled its submitting thread -- holding the GPU
     // lock -- for 11-19 ms and left the GPU idle 1.7 ms per regrowth
     // (tools/drain_trace.py, profiles/r04h2).  It regrows only with cand_cap_,
-    // and the old buffer is retired (freed with the engine), not freed here.
-    if (S.h_cands) {
+    // and the old buffer goes to the reaper thread (RetireHost), which frees it
+    // outside the engine's locks.
+    if (S.h_cands) RetireHost(S.h_cands);
+    {
       std::lock_guard<std::mutex> g(slot_mu_);
-      retired_host_.push_back(S.h_cands);
+      S.h_cands = nullptr;
+      S.h_cap = 0;
     }
-    S.h_cands = nullptr;
-    S.h_cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&S.h_cands), size_t(cand_cap_) * sizeof(Candidate),
-                      hipHostMallocDefault) != hipSuccess) {
+    Candidate* hc = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&hc), size_t(cand_cap_) * sizeof(Candidate), hipHostMallocDefault) !=
+        hipSuccess) {
       err_ = "hipHostMalloc failed for the candidate read-back";
       return fail();
     }
+    std::lock_guard<std::mutex> g(slot_mu_);
+    S.h_cands = hc;
     S.h_cap = cand_cap_;
   }
   uint64_t n_chunks = (n_bytes + kChunk - 1) / kChunk;
@@ -2892,16 +2964,22 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
        !Ensure(&d_fs_wave_, &cap_fs_wave_, size_t(fs_pair_cap_) * 4) ||
        !Ensure(&d_fs_tasks_, &cap_fs_tasks_, size_t(fs_task_cap_) * 4 * sizeof(FsTask))))
     return false;
-  HIP_OK(hipEventRecord(ev[0], stream_));  // the GPU phase: clears, K0 .. finalize
-  HIP_OK(hipMemsetAsync(d_flags_, 0, size_t(n_files) * 4, stream_));
-  HIP_OK(hipMemsetAsync(d_kw_, 0, size_t(n_files) * kw_words_ * 4, stream_));
-  HIP_OK(hipMemsetAsync(d_counters_, 0, 64, stream_));
+  HIP_OK(hipEventRecord(ev[0], stream_));  // the GPU phase: K0 (with the clears) .. finalize
   if (d_item_diag_) HIP_OK(hipMemsetAsync(d_item_diag_, 0, 8 * std::max<size_t>(n_fitems_, 1), stream_));
   {  // every chunk below n_bytes gets its file (no clear needed)
     const uint64_t used = (n_bytes + kChunk - 1) / kChunk;
     const uint64_t runs = (used + kK0Run - 1) / kK0Run;
-    const uint32_t blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((runs + 255) / 256, 8192)));
-    chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, used, static_cast<uint32_t*>(d_chunk_file_));
+    const uint64_t clear_q = (uint64_t(n_files) * (1 + kw_words_) + 3) / 4;  // 16-B clear stores
+    const uint64_t work = std::max(runs, clear_q);
+    const uint32_t blocks = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((work + 255) / 256, 8192)));
+    ClearParams z;
+    z.flags = static_cast<uint32_t*>(d_flags_);
+    z.kw = static_cast<uint32_t*>(d_kw_);
+    z.n_kw = uint64_t(n_files) * kw_words_;
+    z.counters = d_counters_;
+    z.fs_ctr = n_fullscan_rules_ > 0 ? d_fs_ctr_ : nullptr;
+    chunk_map_kernel<<<blocks, 256, 0, stream_>>>(d_offsets, n_files, used, static_cast<uint32_t*>(d_chunk_file_),
+                                                  z);
   }
   // K1: streaming filter -> flagged block records
   FilterParams fp;
@@ -3062,8 +3140,7 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
     fq.task_cap = fs_task_cap_;
     fq.wave_pairs = static_cast<uint32_t*>(d_fs_wave_);
     fq.ctr = d_fs_ctr_;
-    fq.task_min = fs_task_bytes_;
-    HIP_OK(hipMemsetAsync(d_fs_ctr_, 0, 64, stream_));
+    fq.task_min = fs_task_bytes_;  // (fq.ctr was cleared by K0)
     const uint64_t pairs = uint64_t(n_files) * n_fullscan_rules_;
     const uint32_t pb = uint32_t(std::min<uint64_t>(std::max<uint64_t>((pairs + 255) / 256, 1), 4096));
     fs_pairs_kernel<<<pb, 256, 0, stream_>>>(np, fq);
@@ -3122,8 +3199,17 @@ bool GpuEngine::Run(const uint8_t* d_arena, uint64_t n_bytes, const uint64_t* d_
       HIP_OK(hipMemcpy(fc, d_fs_ctr_, sizeof(fc), hipMemcpyDeviceToHost));
       fs_pair_cap_ = std::max<uint32_t>(fs_pair_cap_, fc[0] + fc[0] / 4 + 1024);
       const uint32_t mt = std::max(std::max(fc[1], fc[2]), std::max(fc[3], fc[4]));
-      fs_task_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(fs_task_cap_, uint64_t(mt) + mt / 4 + 1024),
-                                                 0x7FFFFFFFu / sizeof(FsTask) / 4));
+      constexpr uint64_t kMaxTasks = 0x7FFFFFFFu / sizeof(FsTask) / 4;
+      const uint64_t want = uint64_t(mt) + mt / 4 + 1024;
+      if (want > kMaxTasks) {
+        // the lists cannot grow that far: coarser lane tasks instead (any task
+        // size is exact -- each lane starts max_len bytes before its range), so
+        // the scan degrades instead of failing with an overflow on every attempt
+        uint64_t tb = fs_task_bytes_;
+        while (tb < (uint64_t(1) << 26) && want * fs_task_bytes_ / tb > kMaxTasks) tb *= 2;
+        fs_task_bytes_ = uint32_t(tb);
+      }
+      fs_task_cap_ = uint32_t(std::min<uint64_t>(std::max<uint64_t>(fs_task_cap_, want), kMaxTasks));
       continue;
     }
     if (cnt[10]) {  // fold site list overflow

@@ -1215,11 +1215,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   GpuEngine::Ticket ticket;
   if (!in.dev_arena) {  // the staging ring orders concurrent host batches; it takes the lock per chunk
     ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
-                         in.transform ? &tail : nullptr, &gpu_mu_[slot]);
-    if (!ok) {
-      std::lock_guard<std::mutex> g(gpu_mu_[slot]);
-      gpu_err = engine->error();
-    }
+                         in.transform ? &tail : nullptr, &gpu_mu_[slot], &gpu_err);
   } else {
     std::lock_guard<std::mutex> g(gpu_mu_[slot]);
     static const bool tickets = !std::getenv("TSG_TICKETS") || std::atoi(std::getenv("TSG_TICKETS")) != 0;

@@ -228,6 +228,8 @@ class SecretScanner {
   const std::vector<RuleSpec>& rules() const { return rules_; }
   const CompiledRules& compiled() const { return cr_; }
   GpuEngine* engine() { return engines_.empty() ? nullptr : engines_[0].get(); }
+  size_t n_engines() const { return engines_.size(); }
+  GpuEngine* engine_at(size_t i) { return engines_[i].get(); }
   int device() const { return engines_.empty() ? -1 : engines_[0]->device(); }  // -1: no GPU engine
   void set_host_threads(int n) { host_threads_ = n; }
 
