@@ -1,0 +1,136 @@
+# Round-5 GPU iteration: stages chosen by STAGES (space-separated), each under its own time limit,
+# stopping at the first failure.  Usage: gpurun -- 'TAG=r04a STAGES="tests bench diag prof" bash tools/gpu_r05.sh'
+#   tests  : the -m gpu suite (PYTEST_ARGS narrows it)
+#   smoke  : __graft_entry__.smoke()
+#   bench  : the driver-style default line (20 steps, 5 warm-up, CPU baseline, parity, ingest leg)
+#   quick  : C2 without the CPU baseline (BENCH_ARGS adds flags)
+#   diag   : C2 confirm-kernel split (TSG_DIAG_CONFIRM 4 / 8 / 16), 5 steps each
+#   prof   : rocprofv3 --kernel-trace --stats of a short C2 run
+#   wl     : the workloads in WLS (default c3 c3f c4 c1fs c5), with CPU baselines unless WL_ARGS says otherwise
+set -o pipefail
+TAG=${TAG:-r05}
+STAGES=${STAGES:-tests bench}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+for st in $STAGES; do
+  case $st in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests_$TAG.log 2>&1
+      rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
+      rc=$?; tail -2 gpurun_out/smoke_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+      rc=$?; python tools/bench_brief.py gpurun_out/bench_$TAG.json; tail -2 gpurun_out/bench_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
+    dflt)  # the default bench (no flags), DFLT_N times
+      for i in $(seq 1 ${DFLT_N:-2}); do
+        timeout -k 10 600 python bench.py > gpurun_out/dflt_${TAG}_$i.json 2> gpurun_out/dflt_${TAG}_$i.err
+        rc=$?; echo "== default $i"; python tools/bench_brief.py gpurun_out/dflt_${TAG}_$i.json; tail -1 gpurun_out/dflt_${TAG}_$i.err; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    quick)
+      timeout -k 10 400 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/quick_$TAG.json 2> gpurun_out/quick_$TAG.err
+      rc=$?; python tools/bench_brief.py gpurun_out/quick_$TAG.json; tail -2 gpurun_out/quick_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
+    diag)
+      for d in 0 4 8 16; do
+        TSG_DIAG_CONFIRM=$d timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --ingest-steps 0 > gpurun_out/diag${d}_$TAG.json 2> gpurun_out/diag${d}_$TAG.err
+        rc=$?; echo "== diag $d"; python tools/bench_brief.py gpurun_out/diag${d}_$TAG.json; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    prof)
+      cd /tmp
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --ingest-steps 0 > $R/gpurun_out/prof_bench_$TAG.json 2> $R/gpurun_out/prof_$TAG.err
+      rc=$?; cd $R; tail -2 gpurun_out/prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
+      find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
+    c4prof)  # rocprofv3 kernel stats of a short C4 run (the pre-transform kernels per batch)
+      cd /tmp
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/c4prof_$TAG -o run --output-format csv -- python3 $R/bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/c4prof_bench_$TAG.json 2> $R/gpurun_out/c4prof_$TAG.err
+      rc=$?; cd $R; tail -2 gpurun_out/c4prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
+      find gpurun_out/c4prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
+    ingprof)  # the C2 ingest leg under a kernel + memory-copy trace (copy / kernel timeline)
+      cd /tmp
+      timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace -d $R/gpurun_out/ingprof_$TAG -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --warmup-s 0 --no-cpu-baseline --ingest-steps 3 > $R/gpurun_out/ingprof_bench_$TAG.json 2> $R/gpurun_out/ingprof_$TAG.err
+      rc=$?; cd $R; tail -2 gpurun_out/ingprof_$TAG.err; [ $rc -eq 0 ] || exit $rc
+      python tools/bench_brief.py gpurun_out/ingprof_bench_$TAG.json ;;
+    ab)  # C2 A/B of library variants (VARIANTS="base pf ..."; base = the in-tree build), twice interleaved
+      for rep in 1 2; do
+        for v in ${VARIANTS:-base}; do
+          if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
+          TSG_LIB=$L timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > gpurun_out/ab_${TAG}_${v}_$rep.json 2> gpurun_out/ab_${TAG}_${v}_$rep.err
+          rc=$?; echo "== $v $rep"; python tools/bench_brief.py gpurun_out/ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
+    dump)  # candidates of one C3f scan for tools/host_tail_bench.py (CPU profiling of the exact pass)
+      TSG_TAIL_DEBUG=1 TSG_DUMP_CANDS=$R/gpurun_out/cands_${DUMP_WL:-c3f}.bin timeout -k 10 600 python bench.py --workload ${DUMP_WL:-c3f} --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dump_$TAG.json 2> gpurun_out/dump_$TAG.err
+      rc=$?; ls -la gpurun_out/cands_${DUMP_WL:-c3f}.bin; grep -a "tail" gpurun_out/dump_$TAG.err | tail -4; [ $rc -eq 0 ] || exit $rc ;;
+    dumps)  # candidates of one C2 and one C3f scan (tools/host_tail_bench.py)
+      for wl in c2 c3f; do
+        TSG_DUMP_CANDS=$R/gpurun_out/cands_${wl}_$TAG.bin timeout -k 10 600 python bench.py --workload $wl --steps 1 --warmup 0 --warmup-s 0 --ingest-steps 0 --no-cpu-baseline > gpurun_out/dump_${wl}_$TAG.json 2> gpurun_out/dump_${wl}_$TAG.err
+        rc=$?; ls -la gpurun_out/cands_${wl}_$TAG.bin; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    large)  # the > 4 GiB transformed-file test alone (last: it moves ~9 GB through the box)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_large_file.py -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_large_$TAG.log 2>&1
+      rc=$?; tail -3 gpurun_out/gpu_large_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
+    abenv)  # C2 A/B over "variant[:ENV=V ...]" specs ('|'-separated AB_SPECS; variant base = the in-tree build), twice interleaved
+      IFS='|' read -r -a specs <<< "${AB_SPECS:-base}"
+      for rep in 1 2; do
+        for i in "${!specs[@]}"; do
+          sp="${specs[$i]}"; v="${sp%%:*}"; E=""; [ "$sp" != "$v" ] && E="${sp#*:}"
+          if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
+          env TSG_LIB=$L $E timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > gpurun_out/abenv_${TAG}_${i}_$rep.json 2> gpurun_out/abenv_${TAG}_${i}_$rep.err
+          rc=$?; echo "== [$i] $sp $rep"; python tools/bench_brief.py gpurun_out/abenv_${TAG}_${i}_$rep.json; [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
+    ingab)  # ingest leg A/B of library variants (VARIANTS; base = the in-tree build), twice interleaved
+      for rep in 1 2; do
+        for sp in ${VARIANTS:-base}; do  # variant[:ENV=V] (one env assignment)
+          v="${sp%%:*}"; E=""; [ "$sp" != "$v" ] && E="${sp#*:}"
+          if [ "$v" = base ]; then L=""; else L=$R/trivy_amd/_variants/$v/libtsg.so; fi
+          v="$v${E:+_${E//=/}}"
+          env TSG_LIB=$L $E timeout -k 10 400 python bench.py --steps 5 --warmup 2 --warmup-s 0 --no-cpu-baseline --ingest-steps ${INGEST_STEPS:-6} ${BENCH_ARGS:-} > gpurun_out/ingab_${TAG}_${v}_$rep.json 2> gpurun_out/ingab_${TAG}_${v}_$rep.err
+          rc=$?; echo "== $v $rep"; python - gpurun_out/ingab_${TAG}_${v}_$rep.json <<'PYEOF'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+i = d.get("ingest") or {}
+print("value=%s ingest=%s frac_h2d=%s ms=%s" % (d["value"], i.get("value"), i.get("frac_h2d"), i.get("ms_per_step")))
+PYEOF
+          [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
+    c4ab)  # C4 with the defaults and with each env of C4_ENVS ('|'-separated, e.g. "TSG_INGEST_CHUNK_MB=64|TSG_GPU_SLOTS=2"), interleaved
+      IFS='|' read -r -a envs <<< "${C4_ENVS:-TSG_INGEST_CHUNK_MB=64}"
+      for rep in 1 2; do
+        for i in base "${!envs[@]}"; do
+          if [ "$i" = base ]; then E=""; v=base; else E="${envs[$i]}"; v=alt$i; fi
+          env $E timeout -k 10 600 python bench.py --workload c4 --steps ${C4_STEPS:-5} --warmup 2 --no-cpu-baseline ${C4_ARGS:-} > gpurun_out/c4ab_${TAG}_${v}_$rep.json 2> gpurun_out/c4ab_${TAG}_${v}_$rep.err
+          rc=$?; echo "== c4 $v $rep ($E)"; python tools/bench_brief.py gpurun_out/c4ab_${TAG}_${v}_$rep.json; [ $rc -eq 0 ] || exit $rc
+        done
+      done ;;
+    pmc)  # SQ counters per kernel, two passes (tools/gpu_pmc.sh groups 1-2) over a 1-step C2 run
+      cd /tmp
+      i=0
+      for g in "GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAIT_INST_LDS SQ_CYCLES" \
+               "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD"; do
+        i=$((i+1))
+        timeout -s KILL 150 rocprofv3 --pmc $g --kernel-trace -d $R/gpurun_out/pmc_${TAG}_$i -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --warmup-s 0 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > $R/gpurun_out/pmc_${TAG}_$i.json 2> $R/gpurun_out/pmc_${TAG}_$i.err
+        rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        python3 $R/tools/pmc_summary.py $(find $R/gpurun_out/pmc_${TAG}_$i -name '*counter_collection.csv') > $R/gpurun_out/pmc_${TAG}_$i.txt
+        cat $R/gpurun_out/pmc_${TAG}_$i.txt
+      done
+      cd $R ;;
+    fetch)  # HBM traffic: FETCH_SIZE and WRITE_SIZE, one pass each, over a 1-step run (BENCH_ARGS picks the workload)
+      cd /tmp
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace -d $R/gpurun_out/fetch_${TAG}_$c -o pmc --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --warmup-s 0 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > $R/gpurun_out/fetch_${TAG}_$c.json 2> $R/gpurun_out/fetch_${TAG}_$c.err
+        rc=$?; echo "pass $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+        python3 $R/tools/pmc_summary.py $(find $R/gpurun_out/fetch_${TAG}_$c -name '*counter_collection.csv') > $R/gpurun_out/fetch_${TAG}_$c.txt
+        cat $R/gpurun_out/fetch_${TAG}_$c.txt
+      done
+      cd $R ;;
+    wl)
+      for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
+        timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
+        rc=$?; echo "== $wl"; python tools/bench_brief.py gpurun_out/wl_${TAG}_$wl.json; tail -2 gpurun_out/wl_${TAG}_$wl.err; [ $rc -eq 0 ] || exit $rc
+      done ;;
+  esac
+done

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--hints", action="store_true", help="fill Candidate::nl_back on the host first")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3f"],
                     help="corpus / rules of the dump (bench.py --workload; rank 0 seed)")
+    ap.add_argument("--crlf", type=float, default=None,
+                    help="c2: CRLF share of the generated files, stripped as the bench's resident leg does "
+                         "(default 0.05, the bench's default)")
     args = ap.parse_args()
     from oracle import hostlib
     L = hostlib.lib()
@@ -43,7 +46,10 @@ def main():
     t = time.time()
     rules = builtin_rules()
     if args.workload == "c2":
-        C = corpus.generate(int(args.gb * 1e9))
+        crlf = 0.05 if args.crlf is None else args.crlf
+        C = corpus.generate(int(args.gb * 1e9), crlf_share=crlf)
+        if crlf > 0:
+            C = C.stripped()
     else:
         import tempfile
         from trivy_amd.secret import ParseConfig

@@ -232,6 +232,7 @@ class GpuEngine {
   void* d_hits_ = nullptr; size_t cap_hits_ = 0;
   void* d_cands_ = nullptr; size_t cap_cands_ = 0;
   void* d_folds_ = nullptr; size_t cap_folds_ = 0;
+  void* d_wins_ = nullptr; size_t cap_wins_ = 0;  // TSG_K2_PACK experiment: packed confirm windows
   uint32_t* d_counters_ = nullptr;  // [0] hits [1] cands [2] special files [3] hit overflow [4] cand overflow
                                     // [7] flagged-block records [8] record overflow
                                     // [9] fold sites [10] fold-site overflow

@@ -657,6 +657,9 @@ struct ConfirmParams {
   uint32_t t_cmap, t_ccore, t_gitems, t_bgroups, n_cls;
   // literal-window hash (filter.h): keys at u64 [t_hkeys/8], items at u32 [t_hitems/4], 2^hash_bits slots
   uint32_t t_hkeys, t_hitems, hash_bits, hash_buckets;
+  // TSG_K2_PACK experiment: each record's 48-B window packed sequentially (64-B
+  // stride) by pack_kernel, read linearly instead of gathered from the arena
+  const uint8_t* wins;
 };
 
 // Shift-and NFA over arena bytes [fs + start, fs + len), read 16 B at a time
@@ -1039,7 +1042,13 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   // ahead (TSG_C_PREFETCH): the gather of the next blocks' bytes is in flight
   // while this batch's phases run, instead of one dependent global round trip
   // (record -> window bytes) at the top of every batch.
-  auto load_win = [&](uint32_t rec, bool valid, uint4* dst) {
+  auto load_win = [&](uint32_t r, uint32_t rec, bool valid, uint4* dst) {
+    if (P.wins) {  // TSG_K2_PACK: the window packed at record r
+#pragma unroll
+      for (int q = 0; q < kCWin / 16; q++)
+        dst[q] = valid ? load16(P.wins + uint64_t(r) * 64 + 16 * q) : make_uint4(0, 0, 0, 0);
+      return;
+    }
     const uint64_t base = uint64_t(rec) * 16;
     const uint64_t w0 = base >= 16 ? base - 16 : 0;
 #pragma unroll
@@ -1050,7 +1059,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   uint32_t rec_next = r_first < n_recs ? P.recs[r_first] : 0u;
 #if TSG_C_PREFETCH
   uint4 dwn[kCWin / 16];
-  load_win(rec_next, r_first < n_recs, dwn);
+  load_win(r_first, rec_next, r_first < n_recs, dwn);
   uint32_t rec_nn = r_first + stride < n_recs ? P.recs[r_first + stride] : 0u;
 #endif
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave * 64; r0 < n_recs; r0 += stride) {
@@ -1062,11 +1071,11 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
     for (int q = 0; q < kCWin / 16; q++) dw[q] = dwn[q];
     rec_next = rec_nn;
-    load_win(rec_next, r + stride < n_recs, dwn);
+    load_win(r + stride, rec_next, r + stride < n_recs, dwn);
     rec_nn = r + 2 * stride < n_recs ? P.recs[r + 2 * stride] : 0u;
 #else
     rec_next = r + stride < n_recs ? P.recs[r + stride] : 0u;
-    load_win(rec, r < n_recs, dw);
+    load_win(r, rec, r < n_recs, dw);
 #endif
     uint32_t fire_e[4], n_fire = 0;
     if (r < n_recs) {
@@ -1151,6 +1160,26 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
   for (int x = 32; x >= 1; x >>= 1) n_anchor += __shfl_xor(n_anchor, x);
   if (lane == 0 && n_anchor) atomicAdd(&P.counters[11], n_anchor);  // anchor-item matches (stats)
+}
+
+// TSG_K2_PACK experiment: the 48-B window of every flagged
+// block record written to a sequential buffer (64-B stride), so the confirm
+// kernel's phase A reads records linearly instead of gathering 128-B lines
+// the filter kernel streamed long before.  Measures what the confirm kernel
+// would gain if K1 streamed the windows itself.
+__global__ __launch_bounds__(256) void pack_windows_kernel(const uint8_t* __restrict__ arena, uint64_t n_bytes,
+                                                           const uint32_t* __restrict__ recs, uint32_t rec_cap,
+                                                           const uint32_t* __restrict__ counters,
+                                                           uint8_t* __restrict__ wins) {
+  const uint32_t n_recs = counters[7] < rec_cap ? counters[7] : rec_cap;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_recs; r += gridDim.x * blockDim.x) {
+    const uint64_t base = uint64_t(recs[r]) * 16;
+    const uint64_t w0 = base >= 16 ? base - 16 : 0;
+    uint4* d = reinterpret_cast<uint4*>(wins + uint64_t(r) * 64);
+#pragma unroll
+    for (int q = 0; q < kCWin / 16; q++)
+      d[q] = w0 + 16 * q + 16 <= n_bytes + 64 ? load16(arena + w0 + 16 * q) : make_uint4(0, 0, 0, 0);
+  }
 }
 
 // Fold kernel.  Items whose bytes hold a fold rune are invisible to the byte-
@@ -2308,6 +2337,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     }
     c_lds_bytes_ = lds_tabs_ ? fixed + ftabs_bytes_ : ConfirmFixedLds(kCThreadsG);
     if (const char* e = std::getenv("TSG_CONFIRM_LDS_PAD")) c_lds_bytes_ += size_t(std::strtoull(e, nullptr, 10));  // occupancy experiments
+    if (std::getenv("TSG_ENGINE_DEBUG"))
+      std::fprintf(stderr, "confirm LDS: fixed %zu + tables %u (fold prefix %u) = %zu B, limit %zu, %s tables, %d threads\n",
+                   fixed, ftabs_bytes_, ftabs_fold_bytes_, c_lds_bytes_, lds_max, lds_tabs_ ? "LDS" : "global",
+                   lds_tabs_ ? kCThreads : kCThreadsG);
     hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
     if (lds_tabs_)
@@ -2333,7 +2366,7 @@ GpuEngine::~GpuEngine() {
   void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_fs_pairs_, d_fs_tasks_, d_fs_wave_, d_fs_ctr_, d_xlen_, d_xoff_, d_xscan_,
-                d_xf_, d_gfiles_, d_gdst_, d_gbuf_};
+                d_xf_, d_gfiles_, d_gdst_, d_gbuf_, d_wins_};
   for (void* p : ps)
     if (p) hipFree(p);
   for (int b = 0; b < kNStage; b++)
@@ -2394,10 +2427,31 @@ void GpuEngine::RetireHost(void* p) {
 
 void GpuEngine::ReaperLoop() {
   pthread_setname_np(pthread_self(), "tsg-hostfree");
+  // hipHostFree waits for the device by spinning: called while scans keep the
+  // GPU busy it burned a core for the whole run (3 CPU-ms per C2 step, r05a).
+  // So the buffers are freed once this engine is idle -- no ticket in flight,
+  // no host batch in the staging ring -- polled every few ms.
+  auto idle = [&] {
+    {
+      std::lock_guard<std::mutex> g(slot_mu_);
+      for (const auto& S : slots_)
+        if (S.busy) return false;
+    }
+    std::lock_guard<std::mutex> g(ring_mu_);
+    return ring_turn_ == ring_next_;
+  };
   std::unique_lock<std::mutex> lk(reap_mu_);
   for (;;) {
     reap_cv_.wait(lk, [&] { return reap_stop_ || !retired_host_.empty(); });
     if (reap_stop_) return;  // the destructor frees what is left
+    lk.unlock();
+    while (!idle()) {
+      lk.lock();
+      const bool stop = reap_cv_.wait_for(lk, std::chrono::milliseconds(5), [&] { return reap_stop_; });
+      lk.unlock();
+      if (stop) return;
+    }
+    lk.lock();
     std::vector<void*> batch;
     batch.swap(retired_host_);
     lk.unlock();
@@ -3042,6 +3096,16 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   cp.t_hitems = ft_hitems_;
   cp.hash_bits = hash_bits_;
   cp.hash_buckets = hash_buckets_;
+  cp.wins = nullptr;
+  static const bool k2_pack = std::getenv("TSG_K2_PACK") && std::atoi(std::getenv("TSG_K2_PACK")) != 0;
+  if (k2_pack && diag_mode_ == 0) {  // (experiment) the windows packed between K1 and K2, outside K2's events
+    if (!Ensure(&d_wins_, &cap_wins_, size_t(rec_cap_) * 64)) return false;
+    pack_windows_kernel<<<8192, 256, 0, stream_>>>(d_arena, n_bytes, static_cast<const uint32_t*>(d_recs_), rec_cap_,
+                                                   d_counters_, static_cast<uint8_t*>(d_wins_));
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream_));  // re-recorded: K1 + pack count as the scan phase, K2 alone as confirm
+    cp.wins = static_cast<const uint8_t*>(d_wins_);
+  }
   if (diag_mode_ == 0) {
     if (lds_tabs_)
       confirm_kernel<true><<<2048 * 256 / kCThreads, kCThreads, c_lds_bytes_, stream_>>>(cp);
