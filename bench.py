@@ -529,6 +529,11 @@ def main():
     ap.add_argument("--ingest-steps", type=int, default=3,
                     help="c2 resident runs: steps of the extra ingest-inclusive leg (0: skip)")
     ap.add_argument("--arena-mb", type=int, default=256, help="c4: collector arena size")
+    ap.add_argument("--layers", type=int, default=1,
+                    help="c4: the step's bytes as an image of this many layers (sizes 34/26/20/12/8 %% ... of "
+                         "--gb), inspected by --layer-parallel concurrent walks into the one engine "
+                         "(AnalyzeLayers, image.go:202-235); 1 = one layer (AnalyzeLayer)")
+    ap.add_argument("--layer-parallel", type=int, default=3, help="c4 with --layers > 1: concurrent layer walks")
     ap.add_argument("--collectors", type=int, default=3,
                     help="c4/c1fs: collectors filled in turn (collectors - 1 scans in flight during a walk)")
     ap.add_argument("--transform", choices=["gpu", "host"], default="gpu",
@@ -576,6 +581,7 @@ def main():
     cfg_path = None
     t_gen = time.time()
     C = layer = R = None
+    layer_list = None  # c4 --layers > 1
     if args.workload in ("c3", "c3u", "c3f"):
         y, samples = corpus.c3_rules(unanchored_share=0.1 if args.workload == "c3u" else 0.0,
                                      fullscan_share=0.05 if args.workload == "c3f" else 0.0)
@@ -584,7 +590,14 @@ def main():
             f.write(y)
         C = corpus.generate_c3(int(args.gb * 1e9), samples, seed=corpus.SEED + rank)
     elif args.workload == "c4":
-        layer = corpus.generate_layer(int(args.gb * 1e9), seed=corpus.SEED + rank)
+        if args.layers > 1:  # an image: layers of decreasing size, the same total bytes
+            w = [0.34, 0.26, 0.20, 0.12, 0.08] + [0.04] * max(0, args.layers - 5)
+            w = w[:args.layers]
+            layer_list = [corpus.generate_layer(int(args.gb * 1e9 * x / sum(w)), seed=corpus.SEED + rank + 1000 * k)
+                          for k, x in enumerate(w)]
+            layer = layer_list[0]  # (the layer-mode flag below)
+        else:
+            layer = corpus.generate_layer(int(args.gb * 1e9), seed=corpus.SEED + rank)
     elif args.workload == "c1fs":  # a source tree on tmpfs
         base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tmpdir
         fs_root = os.path.join(base, "tsg-c1fs-%d-%d" % (os.getpid(), rank))
@@ -665,12 +678,22 @@ def main():
         t_compile = time.time() - t_c
         gx = args.transform == "gpu"
         colls = [Collector(an, args.arena_mb << 20, gx) for _ in range(args.collectors)]
+        lworkers = an.LayerWorkers(args.layer_parallel, args.arena_mb << 20, args.collectors, gx) \
+            if layer_list is not None else None
 
         def run_steps(n, stats):
             for _ in range(n):
                 st = {}
                 if args.workload == "c1fs":
                     an.AnalyzeFS(layer, stats=st, materialize=False, colls=colls)
+                elif layer_list is not None:  # the image's layers, --layer-parallel walks at once
+                    per = []
+                    t_l = time.time()
+                    an.AnalyzeLayers(layer_list, materialize=False, stats=per, workers=lworkers)
+                    for d in per:  # summed over the layers (walk_s / wait_s: summed over the workers)
+                        for k2, v in d.items():
+                            st[k2] = st.get(k2, 0) + v
+                    st["layers_s"] = time.time() - t_l
                 else:
                     an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
                 stats.append(st)
@@ -825,8 +848,15 @@ def main():
         if fs_wl:
             config_extra["tree"] = "tmpfs (%s)" % os.path.dirname(layer)
         else:
-            config_extra["layer_bytes_per_gpu"] = int(layer.size)
-            config_extra["layer_gbps"] = round(world * int(layer.size) * args.steps / dt / 1e9, 3)
+            lsz = sum(int(x.size) for x in layer_list) if layer_list is not None else int(layer.size)
+            config_extra["layer_bytes_per_gpu"] = lsz
+            config_extra["layer_gbps"] = round(world * lsz * args.steps / dt / 1e9, 3)
+            if layer_list is not None:
+                config_extra["layers"] = [int(x.size) for x in layer_list]
+                config_extra["layer_parallel"] = args.layer_parallel
+                config_extra["pipeline"] = ("%d concurrent layer walks (AnalyzeLayers, image.go:202-235), each %s"
+                                            % (args.layer_parallel, config_extra["pipeline"]))
+                config_extra["walk_s_note"] = "walk_s / wait_s summed over the concurrent layer walks"
     value = world * n_bytes * args.steps / dt / 1e9
     alg_bytes = arena_bytes + 16 * (n_files // emissions)  # 1 B/arena byte + 16 B/file, per scan
     phase = alg_bytes / (gpu_ms * 1e-3) / 1e9  # §8(d): (arena + 16 n_files) / (t_prefilter + t_nfa)

@@ -411,6 +411,51 @@ def test_gpu_analyze_generated_layer_vs_oracle(gpu_transform, n_colls):
     assert len(want) > 20
 
 
+def test_analyze_layers_pipeline_host_logic(host_analyzer):
+    """AnalyzeLayers without a GPU: base layers are never walked (empty results), and a worker's
+    failure (here the scan itself: no GPU engine) stops the pipeline and is raised to the caller."""
+    from trivy_amd import corpus
+    layer = corpus.generate_layer(600_000, seed=corpus.SEED + 31)
+    st = []
+    got = host_analyzer.AnalyzeLayers([layer, layer], base=[True, True], parallel=2, stats=st)
+    assert [r.Secrets for r in got] == [[], []] and st == [None, None]
+    with pytest.raises(RuntimeError):
+        host_analyzer.AnalyzeLayers([layer, layer, layer], base=[True, False, False], parallel=2)
+    with pytest.raises(ValueError):
+        host_analyzer.AnalyzeLayers([layer], base=[True, False])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpu_transform", [False, True])
+def test_gpu_analyze_layers_concurrently_vs_oracle(gpu_transform):
+    """VERDICT r04 item 4 (image.go:202-235): four layers inspected by three concurrent workers,
+    each walking its layer into its own collectors while all feed the one engine; the base
+    layer has the secret analyzer disabled.  Every non-base layer's sorted result equals the
+    oracle's AnalyzeLayer of that layer alone; the base layer's is empty."""
+    from trivy_amd import corpus
+    from trivy_amd.analyzer import AnalyzerOptions, SecretAnalyzer
+    layers = [corpus.generate_layer(sz, seed=corpus.SEED + 40 + k, secrets_per_byte=1.0 / 8192)
+              for k, sz in enumerate([1_200_000, 900_000, 1_500_000, 700_000])]
+    base = [True, False, False, False]
+    a = SecretAnalyzer()
+    a.Init(AnalyzerOptions())
+    st = []
+    got = a.AnalyzeLayers(layers, base=base, parallel=3, arena_bytes=256 << 10, gpu_transform=gpu_transform,
+                          stats=st)
+    assert len(got) == 4 and got[0].Secrets == [] and st[0] is None
+    o = oan.SecretAnalyzer("")
+    n = 0
+    for k in range(1, 4):
+        want = oan.analyze_layer(o, layers[k].tobytes())
+        want.sort(key=lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
+        for s in want:
+            s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
+        assert [_norm_secret(s) for s in got[k].Secrets] == want, k
+        assert st[k]["added"] > 100
+        n += len(want)
+    assert n > 20
+
+
 def test_native_tar_walk_cleans_names(host_analyzer):
     """path.Clean on archive names (walker/tar.go:46-48): "//", "/./", "..", leading "/" and "./"."""
     from trivy_amd.analyzer.secret import Collector, _CTarStats

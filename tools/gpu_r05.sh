@@ -63,6 +63,12 @@ for st in $STAGES; do
     dump)  # candidates of one C3f scan for tools/host_tail_bench.py (CPU profiling of the exact pass)
       TSG_TAIL_DEBUG=1 TSG_DUMP_CANDS=$R/gpurun_out/cands_${DUMP_WL:-c3f}.bin timeout -k 10 600 python bench.py --workload ${DUMP_WL:-c3f} --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dump_$TAG.json 2> gpurun_out/dump_$TAG.err
       rc=$?; ls -la gpurun_out/cands_${DUMP_WL:-c3f}.bin; grep -a "tail" gpurun_out/dump_$TAG.err | tail -4; [ $rc -eq 0 ] || exit $rc ;;
+    c4l)  # C4 under several bench arg sets (C4L_SPECS, '|'-separated), e.g. "--layers 1|--layers 5 --layer-parallel 3"
+      IFS='|' read -r -a specs <<< "${C4L_SPECS:---layers 1}"
+      for i in "${!specs[@]}"; do
+        timeout -k 10 600 python bench.py --workload c4 --steps ${C4_STEPS:-5} --warmup 2 --no-cpu-baseline ${specs[$i]} > gpurun_out/c4l_${TAG}_$i.json 2> gpurun_out/c4l_${TAG}_$i.err
+        rc=$?; echo "== c4 [$i] ${specs[$i]}"; python tools/bench_brief.py gpurun_out/c4l_${TAG}_$i.json; [ $rc -eq 0 ] || exit $rc
+      done ;;
     dumps)  # candidates of one C2 and one C3f scan (tools/host_tail_bench.py)
       for wl in c2 c3f; do
         TSG_DUMP_CANDS=$R/gpurun_out/cands_${wl}_$TAG.bin timeout -k 10 600 python bench.py --workload $wl --steps 1 --warmup 0 --warmup-s 0 --ingest-steps 0 --no-cpu-baseline > gpurun_out/dump_${wl}_$TAG.json 2> gpurun_out/dump_${wl}_$TAG.err

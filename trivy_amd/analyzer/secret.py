@@ -15,6 +15,9 @@ per file, analyzer.go:403-455, becomes a batch collector feeding one arena):
 * ``AnalyzeLayer(tar)``     -- LayerTar.Walk (walker/tar.go:35-103) + AnalyzeFile's
   Required gate + Analyze for every regular file of an uncompressed layer,
   parsed natively into double-buffered pinned arenas (tsg_collector_add_tar)
+* ``AnalyzeLayers(tars, base)`` -- the image artifact's layer pipeline
+  (artifact/image/image.go:202-235): `parallel` layer walks at once into one
+  engine, base layers with the secret analyzer disabled
 
 Every transform runs in libtsg.so (include/tsg_analyzer.h); there is no CPU
 fallback for the scan itself.
@@ -461,6 +464,80 @@ class SecretAnalyzer:
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})
             stats.update({"walk_s": t_walk, "wait_s": t_wait})
         return result
+
+
+    def LayerWorkers(self, parallel: int = 2, arena_bytes: int = 256 << 20, collectors: int = 2,
+                     gpu_transform: bool = False) -> list:
+        """AnalyzeLayers' workers, for reuse across calls: per worker an analyzer bound to this scanner
+        (its own tar-walk state) and its collectors (pinned arenas: allocating them per call would
+        cost a hipHostMalloc each, and freeing them waits for the device)."""
+        out = []
+        for _ in range(max(1, parallel)):
+            sub = SecretAnalyzer(self.scanner, self.configPath, device=self.device, lib=self._L,
+                                 host_only=self._host_only)
+            out.append((sub, [Collector(sub, arena_bytes, gpu_transform) for _ in range(max(1, collectors))]))
+        return out
+
+    def AnalyzeLayers(self, layers: Sequence, base: Optional[Sequence[bool]] = None, parallel: int = 2,
+                      arena_bytes: int = 256 << 20, collectors: int = 2, gpu_transform: bool = False,
+                      materialize: bool = True, stats: Optional[list] = None,
+                      workers: Optional[list] = None) -> List[AnalysisResult]:
+        """The image artifact's layer inspection for this analyzer (pkg/fanal/artifact/image/image.go:
+        202-235): a pipeline of `parallel` workers over the layers, each running inspectLayer's walk
+        (AnalyzeLayer) of one layer at a time; a base layer (base[i] true, the image's base diff IDs)
+        has the secret analyzer disabled (image.go:208-211) and yields an empty result without a walk.
+        Each worker owns an analyzer (its own tar-walk state) and collectors bound to this scanner, so
+        the walks of several layers feed the one engine -- its staging ring interleaves their batches'
+        copies and kernels.  Returns one AnalysisResult per layer, in the order given, each sorted as
+        inspectLayer sorts its result (analyzer.go:225-234).  stats (a list): per layer, the
+        AnalyzeLayer stats dict (None for base layers).  workers: from LayerWorkers (then `parallel`,
+        `arena_bytes`, `collectors` and `gpu_transform` are theirs)."""
+        import threading
+        if self.scanner is None:
+            raise RuntimeError("AnalyzeLayers: the analyzer has no scanner (Init first)")
+        n = len(layers)
+        base = list(base) if base is not None else [False] * n
+        if len(base) != n:
+            raise ValueError("AnalyzeLayers: base flags must match the layers")
+        results: List[Optional[AnalysisResult]] = [None] * n
+        per: List[Optional[dict]] = [None] * n
+        todo = collections.deque(i for i in range(n) if not base[i])
+        for i in range(n):
+            if base[i]:
+                results[i] = AnalysisResult()
+        lock = threading.Lock()
+        errors: List[BaseException] = []
+
+        if workers is None:
+            workers = self.LayerWorkers(min(parallel, max(1, len(todo))), arena_bytes, collectors, gpu_transform)
+
+        def worker(sub, colls):
+            while True:
+                with lock:
+                    if errors or not todo:
+                        return
+                    i = todo.popleft()
+                st: dict = {}
+                try:
+                    r = sub.AnalyzeLayer(layers[i], stats=st, materialize=materialize, colls=colls)
+                except BaseException as e:  # the pipeline stops at the first error (parallel.Pipeline)
+                    with lock:
+                        errors.append(e)
+                    return
+                r.Sort()
+                results[i], per[i] = r, st
+
+        threads = [threading.Thread(target=worker, args=w, name="tsg-layer-%d" % k)
+                   for k, w in enumerate(workers[:max(1, len(todo))])]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
+        if stats is not None:
+            stats[:] = per
+        return results  # type: ignore[return-value]
 
 
 def NewSecretAnalyzer(s=None, configPath: str = "") -> SecretAnalyzer:  # secret.go:79-84

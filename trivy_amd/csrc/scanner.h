@@ -236,6 +236,20 @@ class SecretScanner {
  private:
   void ScanFile(const uint8_t* content, int64_t len, std::string_view path, bool binary,
                 const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const;
+  // HostTail's serial set-up buffers (the per-file counts, the grouped
+  // candidates, the dispatch order), kept across calls: allocated per call,
+  // their first touch (page faults on ~10 MB) was most of the set-up's time.
+  struct TailScratch {
+    std::vector<uint32_t> order;
+    std::vector<uint64_t> key, key2;  // (file << 32 | candidate index), radix-sorted by file
+    std::vector<size_t> starts;
+    std::vector<double> w;
+    std::vector<FileResult> tmp;      // per group
+  };
+  std::unique_ptr<TailScratch> TakeScratch() const;
+  void GiveScratch(std::unique_ptr<TailScratch> s) const;
+  mutable std::mutex scratch_mu_;
+  mutable std::vector<std::unique_ptr<TailScratch>> scratch_free_;
   std::vector<RuleSpec> rules_;
   // Exclude-block regexes (scanner.go:237-275) are compiled after the rules as
   // extra GPU rules without keywords: their candidates bound where a block can
