@@ -69,6 +69,15 @@ for st in $STAGES; do
         timeout -k 10 600 python bench.py --workload c4 --steps ${C4_STEPS:-5} --warmup 2 --no-cpu-baseline ${specs[$i]} > gpurun_out/c4l_${TAG}_$i.json 2> gpurun_out/c4l_${TAG}_$i.err
         rc=$?; echo "== c4 [$i] ${specs[$i]}"; python tools/bench_brief.py gpurun_out/c4l_${TAG}_$i.json; [ $rc -eq 0 ] || exit $rc
       done ;;
+    walkprof)  # the C4 tar walk alone on the box's host cores (no GPU), with the sampling profiler
+      SPROF=$R/gpurun_out/walkprof_$TAG.txt TSG_WALK_DEBUG=1 timeout -k 10 600 python tools/walk_bench.py --gb ${WALK_GB:-15} --reps 3 > gpurun_out/walkprof_$TAG.log 2>&1
+      rc=$?; grep -v "^index:" gpurun_out/walkprof_$TAG.log | tail -4; [ $rc -eq 0 ] || exit $rc
+      python tools/sprof/report.py gpurun_out/walkprof_$TAG.txt libtsg_host > gpurun_out/walkprof_${TAG}_fn.txt 2>&1
+      python tools/sprof/report.py gpurun_out/walkprof_$TAG.txt libtsg_host lines > gpurun_out/walkprof_${TAG}_lines.txt 2>&1
+      head -30 gpurun_out/walkprof_${TAG}_fn.txt ;;
+    tailprof)  # the exact host pass on the box's cores over a dumped candidate list (TAIL_CANDS, TAIL_WL)
+      TSG_TAIL_DEBUG=1 timeout -k 10 600 python tools/host_tail_bench.py ${TAIL_CANDS} --workload ${TAIL_WL:-c2} --gb ${TAIL_GB:-20} --reps 5 > gpurun_out/tailprof_$TAG.log 2>&1
+      rc=$?; grep "serial\|tail \|phases" gpurun_out/tailprof_$TAG.log | tail -6; [ $rc -eq 0 ] || exit $rc ;;
     dumps)  # candidates of one C2 and one C3f scan (tools/host_tail_bench.py)
       for wl in c2 c3f; do
         TSG_DUMP_CANDS=$R/gpurun_out/cands_${wl}_$TAG.bin timeout -k 10 600 python bench.py --workload $wl --steps 1 --warmup 0 --warmup-s 0 --ingest-steps 0 --no-cpu-baseline > gpurun_out/dump_${wl}_$TAG.json 2> gpurun_out/dump_${wl}_$TAG.err

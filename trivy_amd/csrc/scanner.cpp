@@ -78,13 +78,11 @@ size_t RarestIndex(const std::string& kw) {
 // ---------------------------------------------------------------------------
 struct SortData {
   FileFindings* v;
-  const std::vector<RuleSpec>* rules;
+  const uint32_t* rank;  // per rule: the rank of its ID among the rules' IDs (equal IDs, equal rank)
   bool Less(int i, int j) const {
     const FindingOut& a = v->f[size_t(i)];
     const FindingOut& b = v->f[size_t(j)];
-    const std::string& ra = (*rules)[a.rule].id;
-    const std::string& rb = (*rules)[b.rule].id;
-    if (ra != rb) return ra < rb;
+    if (rank[a.rule] != rank[b.rule]) return rank[a.rule] < rank[b.rule];  // RuleID < RuleID
     return v->Match(a) < v->Match(b);
   }
   void Swap(int i, int j) { std::swap(v->f[size_t(i)], v->f[size_t(j)]); }
@@ -286,8 +284,17 @@ void Pdqsort(SortData& d, int a, int b, int limit) {
 
 }  // namespace
 
-void SortFindings(FileFindings* f, const std::vector<RuleSpec>& rules) {
-  SortData d{f, &rules};
+std::vector<uint32_t> RuleRanks(const std::vector<RuleSpec>& rules) {
+  std::vector<uint32_t> idx(rules.size()), rank(rules.size(), 0);
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = uint32_t(i);
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return rules[a].id < rules[b].id; });
+  for (size_t k = 1; k < idx.size(); k++)
+    rank[idx[k]] = rules[idx[k]].id == rules[idx[k - 1]].id ? rank[idx[k - 1]] : uint32_t(k);
+  return rank;
+}
+
+void SortFindings(FileFindings* f, const std::vector<uint32_t>& rule_rank) {
+  SortData d{f, rule_rank.data()};
   int n = int(f->size());
   Pdqsort(d, 0, n, BitsLen(unsigned(n)));
 }
@@ -389,6 +396,7 @@ bool Matcher::Match(const uint8_t* s, size_t n) const {
 SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleSpec> allow,
                              std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err)
     : rules_(std::move(rules)), allow_(std::move(allow)), exclude_(std::move(exclude)) {
+  rule_rank_ = RuleRanks(rules_);
   std::vector<RuleSrc> src;
   for (auto& r : rules_) src.push_back({r.id, r.regex_src, r.keywords, r.has_regex});
   for (size_t g = 0; g < exclude_.size(); g++) {
@@ -650,6 +658,8 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 const bool g_tail_debug = std::getenv("TSG_TAIL_DEBUG") != nullptr;
 std::atomic<int64_t> g_prof[11];  // [8] [9] [10]: bytes memchr'd forward / backward (no hint, in a window) by the line walks
 std::atomic<int64_t> g_wholefile_bytes{0}, g_wholefile_calls{0};  // TSG_TAIL_DEBUG: whole-content gate scans
+constexpr uint32_t kRuleProf = 4096;
+std::atomic<int64_t> g_rule_ns[kRuleProf], g_rule_calls[kRuleProf];
 struct PhaseTimer {
   int k;
   std::chrono::steady_clock::time_point t0;
@@ -768,7 +778,12 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
     m.clear();
     {
       PhaseTimer pt(0);
+      const auto fa0 = g_tail_debug ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
       re->FindAll(content, len, sub, &wins, &m);
+      if (g_tail_debug && r < kRuleProf) {  // per-rule FindAll time (TSG_TAIL_DEBUG)
+        g_rule_ns[r] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - fa0).count();
+        g_rule_calls[r] += 1;
+      }
     }
     if (m.empty()) continue;
     size_t stride = sub ? size_t(2 * (re->num_cap() + 1)) : 2;
@@ -1124,28 +1139,44 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   ff.f.reserve(matched.size());
   ff.lines.reserve(matched.size() * 5);
   ff.text.reserve(matched.size() * 320);  // match line + 4 lines of <= 100 B, typically
+  // With the newline index, line L of the censored content is [line_lo(L), line_hi(L)):
+  // a finding's lines are index arithmetic from the two searches for its start and
+  // end (the walks below made ~12 searches per finding; C3f has 368 k findings).
+  const int64_t n_vnl = int64_t(vnl.size());
+  auto line_lo = [&](int64_t L) { return L > 0 ? vnl[size_t(L - 1)] + 1 : int64_t(0); };
+  auto line_hi = [&](int64_t L) { return L < n_vnl ? vnl[size_t(L)] : len; };
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
     f.rule = mt.first;
-    int64_t start_line_num = nl_before(start);
-    int64_t ls = line_start_of(start);
-    int64_t le = line_end_of(start);
+    int64_t start_line_num, ls, le, end_line_num;
+    if (use_index) {
+      start_line_num = vnl_below(start);
+      ls = line_lo(start_line_num);
+      le = line_hi(start_line_num);
+      end_line_num = vnl_below(end);  // start_line_num + count_nl(start, end)
+    } else {
+      start_line_num = nl_before(start);
+      ls = line_start_of(start);
+      le = line_end_of(start);
+      end_line_num = start_line_num + count_nl(start, end);
+    }
     int64_t mls = ls, mle = le;
     if (le - ls > 100) {
       mls = (start - ls - 30 < 0) ? ls : start - 30;
       mle = (end + 20 > le) ? le : end + 20;
     }
     const uint32_t ml_off = put_censored(mls, mle), ml_len = uint32_t(mle - mls);
-    int64_t end_line_num = start_line_num + count_nl(start, end);
     int64_t code_start = std::max<int64_t>(start_line_num - 2, 0);
     int64_t p = ls;
-    for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
+    if (use_index) p = line_lo(code_start);
+    else
+      for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
     bool found_first = false;
     f.line_lo = uint32_t(ff.lines.size());
     if (!binary) {
       for (int64_t k = code_start; k < end_line_num + 2; k++) {
-        int64_t e = line_end_of(p);
+        int64_t e = use_index ? line_hi(k) : line_end_of(p);
         bool in_cause = k >= start_line_num && k <= end_line_num;
         uint32_t off, n;
         if (e - p > 100 && in_cause) {  // the match line (shared text)
@@ -1181,7 +1212,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
     ff.f.push_back(f);
   }
   PhaseTimer pt4(4);
-  SortFindings(&out->findings, rules_);
+  SortFindings(&out->findings, rule_rank_);
 }
 
 bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst, std::string* err) {
@@ -1501,6 +1532,16 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
                  "scanfile %.1f\n",
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
                  g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
+  if (g_tail_debug) {
+    std::vector<std::pair<int64_t, uint32_t>> top;
+    for (uint32_t r = 0; r < std::min<uint32_t>(kRuleProf, uint32_t(rules_.size())); r++)
+      if (g_rule_ns[r]) top.push_back({g_rule_ns[r].load(), r});
+    std::sort(top.rbegin(), top.rend());
+    for (size_t k = 0; k < top.size() && k < 8; k++)
+      std::fprintf(stderr, "tail findall by rule: %-32s %.1f ms %lld calls\n", rules_[top[k].second].id.c_str(),
+                   top[k].first / 1e6, (long long)g_rule_calls[top[k].second].load());
+    for (uint32_t r = 0; r < kRuleProf; r++) g_rule_ns[r] = 0, g_rule_calls[r] = 0;
+  }
   if (g_tail_debug)
     std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB; line walks: %.1f MB forward, %.1f MB back"
                  " (%.1f MB inside windows)\n", (long long)g_wholefile_calls.load(), g_wholefile_bytes.load() / 1e6,

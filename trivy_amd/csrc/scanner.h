@@ -251,6 +251,7 @@ class SecretScanner {
   mutable std::mutex scratch_mu_;
   mutable std::vector<std::unique_ptr<TailScratch>> scratch_free_;
   std::vector<RuleSpec> rules_;
+  std::vector<uint32_t> rule_rank_;  // RuleRanks(rules_): findings sort by RuleID as integer compares
   // Exclude-block regexes (scanner.go:237-275) are compiled after the rules as
   // extra GPU rules without keywords: their candidates bound where a block can
   // start, so the host's FindAll of each block regex runs on windows instead
@@ -290,6 +291,8 @@ class SecretScanner {
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.
-void SortFindings(FileFindings* f, const std::vector<RuleSpec>& rules);
+// rule_rank: per rule, the rank of its ID in the sorted IDs (RuleRanks).
+void SortFindings(FileFindings* f, const std::vector<uint32_t>& rule_rank);
+std::vector<uint32_t> RuleRanks(const std::vector<RuleSpec>& rules);
 
 }  // namespace tsg
