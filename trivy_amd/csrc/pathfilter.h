@@ -58,7 +58,8 @@ class PathFilter {
   struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    uint32_t* d_cnt = nullptr;
+    uint32_t* d_cnt = nullptr;  // two counters used in turn: each launch zeroes the next one's
+    uint32_t parity = 0;
     uint32_t* h_cnt = nullptr;
     PathHit* d_out = nullptr;
     PathHit* h_out = nullptr;  // pinned: a pageable read-back stalled the engine's stream (5 ms per C2 scan)

@@ -40,7 +40,11 @@ __global__ __launch_bounds__(kPathThreads) void path_filter_kernel(const uint8_t
                                                                    const uint64_t* __restrict__ off, uint32_t n,
                                                                    const PathTable* __restrict__ T,
                                                                    uint32_t* __restrict__ cnt,
+                                                                   uint32_t* __restrict__ cnt_next,
                                                                    PathHit* __restrict__ out) {
+  // the counter of this slot's next launch (stream-ordered after this one): no
+  // fill kernel per call
+  if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
   __shared__ uint64_t sB[256][4];
   __shared__ uint8_t s_rule[256];
   for (uint32_t i = threadIdx.x; i < 256 * 4; i += kPathThreads) (&sB[0][0])[i] = (&T->B[0][0])[i];
@@ -114,6 +118,7 @@ PathFilter::PathFilter(int device, const PathTable& t) : device_(device) {
     ok = ok && hipStreamCreateWithPriority(&S.stream, hipStreamNonBlocking, hi) == hipSuccess &&
          hipEventCreateWithFlags(&S.done, hipEventDisableTiming) == hipSuccess &&
          hipMalloc(reinterpret_cast<void**>(&S.d_cnt), 64) == hipSuccess &&
+         hipMemset(S.d_cnt, 0, 64) == hipSuccess &&
          hipHostMalloc(reinterpret_cast<void**>(&S.h_cnt), 64, hipHostMallocDefault) == hipSuccess;
   if (!ok) err_ = "PathFilter: HIP setup failed";
 }
@@ -183,13 +188,20 @@ bool PathFilter::Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, 
       return fail("hipMalloc", e);
     S->cap = n;
   }
-  if ((e = hipMemsetAsync(S->d_cnt, 0, 4, S->stream)) != hipSuccess) return fail("hipMemsetAsync", e);
+  // this launch's counter was zeroed by the slot's previous launch (or at set-up)
+  uint32_t* cnt = S->d_cnt + S->parity;
+  uint32_t* cnt_next = S->d_cnt + (1 - S->parity);
+  S->parity ^= 1u;
   const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n) + kPathThreads - 1) / kPathThreads, 4096));
-  path_filter_kernel<<<grid, kPathThreads, 0, S->stream>>>(d_paths, d_off, n, d_table_, S->d_cnt, S->d_out);
-  if ((e = hipGetLastError()) != hipSuccess) return fail("path_filter_kernel", e);
+  path_filter_kernel<<<grid, kPathThreads, 0, S->stream>>>(d_paths, d_off, n, d_table_, cnt, cnt_next, S->d_out);
+  if ((e = hipGetLastError()) != hipSuccess) {
+    (void)hipStreamSynchronize(S->stream);  // (a failed launch left cnt_next as it was: clear it for the next call)
+    (void)hipMemset(cnt_next, 0, 4);
+    return fail("path_filter_kernel", e);
+  }
   // the count and as many records as the last call had (+1/8): one round trip when the paths repeat
   const uint32_t guess = std::min<uint32_t>(n, last_k_.load() + last_k_.load() / 8 + 1024);
-  if ((e = hipMemcpyAsync(S->h_cnt, S->d_cnt, 4, hipMemcpyDeviceToHost, S->stream)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(S->h_cnt, cnt, 4, hipMemcpyDeviceToHost, S->stream)) != hipSuccess ||
       (e = hipMemcpyAsync(S->h_out, S->d_out, size_t(guess) * sizeof(PathHit), hipMemcpyDeviceToHost, S->stream)) !=
           hipSuccess ||
       (e = wait()) != hipSuccess)

@@ -656,7 +656,7 @@ bool AllowRulesAllowPath(const std::vector<AllowRuleSpec>& rules, const uint8_t*
 
 // Host-tail phase profile (TSG_TAIL_DEBUG=1 only; otherwise the timers are inert).
 const bool g_tail_debug = std::getenv("TSG_TAIL_DEBUG") != nullptr;
-std::atomic<int64_t> g_prof[11];  // [8] [9] [10]: bytes memchr'd forward / backward (no hint, in a window) by the line walks
+std::atomic<int64_t> g_prof[16];  // [8] [9] [10]: bytes memchr'd forward / backward (no hint, in a window) by the line walks
 std::atomic<int64_t> g_wholefile_bytes{0}, g_wholefile_calls{0};  // TSG_TAIL_DEBUG: whole-content gate scans
 constexpr uint32_t kRuleProf = 4096;
 std::atomic<int64_t> g_rule_ns[kRuleProf], g_rule_calls[kRuleProf];
@@ -1135,6 +1135,10 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
 
   out->kind = kHasFindings;
   ff.binary = binary;
+  if (g_tail_debug) {
+    g_prof[use_index ? 11 : 12] += int64_t(matched.size());
+    g_prof[13] += int64_t(spans.size());
+  }
   PhaseTimer pt3(3);
   ff.f.reserve(matched.size());
   ff.lines.reserve(matched.size() * 5);
@@ -1211,6 +1215,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
     }
     ff.f.push_back(f);
   }
+  if (g_tail_debug) g_prof[14] += int64_t(ff.text.size());
   PhaseTimer pt4(4);
   SortFindings(&out->findings, rule_rank_);
 }
@@ -1532,6 +1537,10 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
                  "scanfile %.1f\n",
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
                  g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
+  if (g_tail_debug)
+    std::fprintf(stderr, "tail findings: %lld with the newline index, %lld by walks; censor spans %lld; text %.1f MB\n",
+                 (long long)g_prof[11].load(), (long long)g_prof[12].load(), (long long)g_prof[13].load(),
+                 g_prof[14] / 1e6);
   if (g_tail_debug) {
     std::vector<std::pair<int64_t, uint32_t>> top;
     for (uint32_t r = 0; r < std::min<uint32_t>(kRuleProf, uint32_t(rules_.size())); r++)
