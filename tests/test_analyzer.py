@@ -451,7 +451,7 @@ def test_gpu_analyze_layers_concurrently_vs_oracle(gpu_transform):
         for s in want:
             s["Findings"].sort(key=lambda f: (f["RuleID"].encode(), f["StartLine"]))
         assert [_norm_secret(s) for s in got[k].Secrets] == want, k
-        assert st[k]["added"] > 100
+        assert st[k]["added"] > 50
         n += len(want)
     assert n > 20
 
