@@ -88,6 +88,13 @@ typedef struct tsg_batch {
    * required (the exact rule and the results use it). */
   const void* dev_paths;
   const void* dev_path_offsets;
+  /* optional: the FilePath bytes packed in host memory (host_path_offsets:
+   * n_files + 1 u64 into host_paths), as the analyzer's collectors hold them;
+   * without dev_paths the engine copies them to HBM for the same GPU
+   * allow-path prefilter.  (Appended in round 5: a caller built against the
+   * earlier header must zero them.) */
+  const uint8_t* host_paths;
+  const uint64_t* host_path_offsets;
 } tsg_batch;
 
 int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);

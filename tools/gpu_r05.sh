@@ -34,7 +34,7 @@ for st in $STAGES; do
       rc=$?; python tools/bench_brief.py gpurun_out/quick_$TAG.json; tail -2 gpurun_out/quick_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
     diag)
       for d in 0 4 8 16; do
-        TSG_DIAG_CONFIRM=$d timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --ingest-steps 0 > gpurun_out/diag${d}_$TAG.json 2> gpurun_out/diag${d}_$TAG.err
+        TSG_DIAG_CONFIRM=$d timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > gpurun_out/diag${d}_$TAG.json 2> gpurun_out/diag${d}_$TAG.err
         rc=$?; echo "== diag $d"; python tools/bench_brief.py gpurun_out/diag${d}_$TAG.json; [ $rc -eq 0 ] || exit $rc
       done ;;
     prof)

@@ -1140,6 +1140,9 @@ int tsg_collector_submit(tsg_collector* c, tsg_pending** out) {
   b.path_lens = c->path_lens.data();
   b.binary = c->binary.data();
   b.transform = c->gpu_xform ? c->kinds.data() : nullptr;
+  // the paths are packed already: the global allow-path rules are prefiltered on the GPU
+  b.host_paths = reinterpret_cast<const uint8_t*>(c->path_pool.data());
+  b.host_path_offsets = c->path_off.data();
   return tsg_scan_submit(const_cast<tsg_scanner*>(c->a->s), &b, out);
 }
 

@@ -254,6 +254,8 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   in.transform = b->transform;
   in.dev_paths = static_cast<const uint8_t*>(b->dev_paths);
   in.dev_path_off = static_cast<const uint64_t*>(b->dev_path_offsets);
+  in.host_paths = b->host_paths;
+  in.host_path_off = b->host_path_offsets;
   std::unique_ptr<tsg_result> r(new tsg_result());
   r->owner = s->s.get();
   tsg::BatchStats gs;

@@ -52,9 +52,20 @@ class PathFilter {
   // that should not queue behind a scan's kernels, nor behind another scan's
   // filter: one shared stream and lock serialised the first scans of a
   // pipeline, each waiting out a filter kernel queued behind a K1).
-  bool Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out, std::string* err);
+  bool Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out, std::string* err) {
+    return RunImpl(d_paths, d_off, nullptr, nullptr, n, out, err);
+  }
+  // The same over paths packed in host memory (the analyzer's collectors:
+  // h_off[i] .. h_off[i+1] into h_paths): staged through the slot's pinned
+  // buffer and copied to HBM on the slot's stream first.
+  bool RunHost(const uint8_t* h_paths, const uint64_t* h_off, uint32_t n, std::vector<PathHit>* out,
+               std::string* err) {
+    return RunImpl(nullptr, nullptr, h_paths, h_off, n, out, err);
+  }
 
  private:
+  bool RunImpl(const uint8_t* d_paths, const uint64_t* d_off, const uint8_t* h_paths, const uint64_t* h_off,
+               uint32_t n, std::vector<PathHit>* out, std::string* err);
   struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -64,6 +75,11 @@ class PathFilter {
     PathHit* d_out = nullptr;
     PathHit* h_out = nullptr;  // pinned: a pageable read-back stalled the engine's stream (5 ms per C2 scan)
     size_t cap = 0;
+    // RunHost: the packed paths and their offsets in HBM, and their pinned staging
+    uint8_t* d_paths = nullptr;
+    size_t paths_cap = 0;
+    uint8_t* h_stage = nullptr;
+    size_t stage_cap = 0;
     bool busy = false;
   };
   static constexpr int kSlots = 4;

@@ -128,6 +128,8 @@ PathFilter::~PathFilter() {
   for (Slot& S : slots_) {
     if (S.d_out) (void)hipFree(S.d_out);
     if (S.h_out) (void)hipHostFree(S.h_out);
+    if (S.d_paths) (void)hipFree(S.d_paths);
+    if (S.h_stage) (void)hipHostFree(S.h_stage);
     if (S.d_cnt) (void)hipFree(S.d_cnt);
     if (S.h_cnt) (void)hipHostFree(S.h_cnt);
     if (S.done) (void)hipEventDestroy(S.done);
@@ -136,8 +138,8 @@ PathFilter::~PathFilter() {
   if (d_table_) (void)hipFree(d_table_);
 }
 
-bool PathFilter::Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, std::vector<PathHit>* out,
-                     std::string* err) {
+bool PathFilter::RunImpl(const uint8_t* d_paths, const uint64_t* d_off, const uint8_t* h_paths,
+                         const uint64_t* h_off, uint32_t n, std::vector<PathHit>* out, std::string* err) {
   out->clear();
   if (n == 0) return true;
   Slot* S = nullptr;
@@ -187,6 +189,32 @@ bool PathFilter::Run(const uint8_t* d_paths, const uint64_t* d_off, uint32_t n, 
             hipSuccess)
       return fail("hipMalloc", e);
     S->cap = n;
+  }
+  if (h_paths) {  // host-packed paths: offsets (rebased to 0) and bytes via pinned staging to HBM
+    const uint64_t p0 = h_off[0], nb = h_off[n] - p0, ob = (uint64_t(n) + 1) * 8;
+    const uint64_t need = ((ob + 15) & ~uint64_t(15)) + nb;
+    if (S->paths_cap < need) {
+      if (S->d_paths) (void)hipFree(S->d_paths);
+      if (S->h_stage) (void)hipHostFree(S->h_stage);
+      S->d_paths = nullptr;
+      S->h_stage = nullptr;
+      S->paths_cap = S->stage_cap = 0;
+      const size_t cap = size_t(need + need / 4 + 4096);
+      if ((e = hipMalloc(reinterpret_cast<void**>(&S->d_paths), cap)) != hipSuccess ||
+          (e = hipHostMalloc(reinterpret_cast<void**>(&S->h_stage), cap, hipHostMallocDefault)) != hipSuccess)
+        return fail("hipMalloc (paths)", e);
+      S->paths_cap = S->stage_cap = cap;
+    }
+    // the previous call's copy out of the staging buffer is done: that call waited for its stream
+    uint64_t* so = reinterpret_cast<uint64_t*>(S->h_stage);
+    for (uint32_t i = 0; i <= n; i++) so[i] = h_off[i] - p0;
+    const uint64_t pb = (ob + 15) & ~uint64_t(15);
+    std::memcpy(S->h_stage + pb, h_paths + p0, size_t(nb));
+    if ((e = hipMemcpyAsync(S->d_paths, S->h_stage, size_t(pb + nb), hipMemcpyHostToDevice, S->stream)) !=
+        hipSuccess)
+      return fail("hipMemcpyAsync (paths)", e);
+    d_off = reinterpret_cast<const uint64_t*>(S->d_paths);
+    d_paths = S->d_paths + pb;
   }
   // this launch's counter was zeroed by the slot's previous launch (or at set-up)
   uint32_t* cnt = S->d_cnt + S->parity;

@@ -1318,11 +1318,13 @@ std::vector<uint8_t> SecretScanner::AllowedPaths(const BatchInput& in) const {
   bool any_path_rule = false;
   for (auto& a : allow_)
     if (a.path) any_path_rule = true;
-  if (any_path_rule && path_filter_ && in.dev_paths && in.dev_path_off) {
+  const bool dev = in.dev_paths && in.dev_path_off, host = in.host_paths && in.host_path_off;
+  if (any_path_rule && path_filter_ && (dev || host)) {
     // the GPU reports the paths that can match; every other path is not allowed
     std::vector<PathHit> hits;
     std::string perr;
-    if (path_filter_->Run(in.dev_paths, in.dev_path_off, in.n_files, &hits, &perr)) {
+    if (dev ? path_filter_->Run(in.dev_paths, in.dev_path_off, in.n_files, &hits, &perr)
+            : path_filter_->RunHost(in.host_paths, in.host_path_off, in.n_files, &hits, &perr)) {
       const size_t blocks = (hits.size() + 1023) / 1024;
       ParallelFor(blocks, host_threads_, [&](size_t b) {
         const size_t lo = b * 1024, hi = std::min<size_t>(lo + 1024, hits.size());

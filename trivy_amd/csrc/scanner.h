@@ -189,6 +189,8 @@ struct BatchInput {
   const uint64_t* file_len = nullptr;
   const uint8_t* dev_paths = nullptr;   // optional: the paths packed in HBM (the allow-path prefilter runs
   const uint64_t* dev_path_off = nullptr;  // on the GPU, pathfilter.h); n_files + 1 offsets, device
+  const uint8_t* host_paths = nullptr;      // optional: the paths packed in host memory (copied to HBM for
+  const uint64_t* host_path_off = nullptr;  // the same prefilter when dev_paths is absent); n_files + 1 offsets
 };
 
 struct HostStats {

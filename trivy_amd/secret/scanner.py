@@ -41,7 +41,8 @@ class _CBatch(c.Structure):
     _fields_ = [("n_files", c.c_uint32), ("host_arena", c.c_void_p), ("host_offsets", c.c_void_p),
                 ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.c_void_p),
                 ("path_lens", c.c_void_p), ("binary", c.c_void_p), ("transform", c.c_void_p),
-                ("dev_paths", c.c_void_p), ("dev_path_offsets", c.c_void_p)]
+                ("dev_paths", c.c_void_p), ("dev_path_offsets", c.c_void_p),
+                ("host_paths", c.c_void_p), ("host_path_offsets", c.c_void_p)]
 
 
 class _CStats(c.Structure):
