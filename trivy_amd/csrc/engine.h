@@ -222,6 +222,9 @@ class GpuEngine {
   uint32_t ft_hkeys_ = 0, ft_hitems_ = 0, hash_bits_ = 0, hash_buckets_ = 0;  // literal-window hash
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
+  bool fold_stage_ = false;        // global-table fold kernel: items + classes staged in LDS
+  size_t fold_stage_bytes_ = 0;
+  uint32_t n_fclasses_ = 0;
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;
   uint32_t rec_cap_ = 0, fold_cap_ = 0, n_fitems_ = 0;
   // per-batch buffers

@@ -1225,6 +1225,9 @@ struct FoldParams {
   uint32_t* hits;
   uint32_t hit_cap;
   uint32_t* counters;
+  // global-table variant (large rule sets): the item records and the byte
+  // classes staged in LDS when they fit (n_classes classes of 8 u32)
+  uint32_t stage_items, n_classes;
 };
 
 constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
@@ -1248,14 +1251,27 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
     const uint4* f = reinterpret_cast<const uint4*>(P.first);
     uint4* df = reinterpret_cast<uint4*>(smem + P.tabs_bytes);
     for (uint32_t i = threadIdx.x; i < P.n_items * 2; i += blockDim.x) df[i] = f[i];
+  } else if (P.stage_items) {
+    // large rule sets: the per-start chain was item -> class id -> class word,
+    // each an L2 round trip (C3: 1.9 ms of waits for 40 k sites); the items and
+    // the classes in LDS leave the class-id bytes as the only global reads
+    const uint4* t = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(P.tabs) + P.t_items);
+    uint4* d = reinterpret_cast<uint4*>(smem);
+    for (uint32_t i = threadIdx.x; i < P.n_items; i += blockDim.x) d[i] = t[i];
+    const uint4* c = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(P.tabs) + P.t_classes);
+    uint4* dc = reinterpret_cast<uint4*>(smem + 16 * size_t(P.n_items));
+    for (uint32_t i = threadIdx.x; i < P.n_classes * 2; i += blockDim.x) dc[i] = c[i];
   }
   __syncthreads();
   const uint8_t* tabs = kLdsTabs ? smem : static_cast<const uint8_t*>(P.tabs);
   const uint32_t* firsts = kLdsTabs ? reinterpret_cast<const uint32_t*>(smem + P.tabs_bytes) : P.first;
-  const FilterItemGpu* items = reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
+  const bool staged = !kLdsTabs && P.stage_items;
+  const FilterItemGpu* items =
+      staged ? reinterpret_cast<const FilterItemGpu*>(smem) : reinterpret_cast<const FilterItemGpu*>(tabs + P.t_items);
   const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(tabs + P.t_item_ids);
   const uint8_t* item_cls = tabs + P.t_item_cls;
-  const uint32_t* classes = reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
+  const uint32_t* classes = staged ? reinterpret_cast<const uint32_t*>(smem + 16 * size_t(P.n_items))
+                                   : reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
   auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* wb = s_win[wave];
@@ -1289,6 +1305,12 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
       if (!((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
       uint64_t p = st, lit_bytes_end = 0;
       bool ok = true, covered = false;
+      // the first positions' class ids up front: independent loads instead of
+      // one dependent round trip per position (global tables)
+      constexpr uint32_t kPre = 6;
+      uint32_t pre[kPre];
+#pragma unroll
+      for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
       for (uint32_t q = 0; q < it.n && ok; q++) {
         if (q == it.lit_end) lit_bytes_end = p;
         if (p >= w1) {
@@ -1296,7 +1318,11 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
           break;
         }
         covered = covered || p == fsite.x;
-        const uint32_t c = item_cls[it.cls_off + q];
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPre; k++)
+          if (q == k) c = pre[k];
+        if (q >= kPre) c = item_cls[it.cls_off + q];
         const uint32_t b = wb[p - w0];
         if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
             (in_cls(c, 'k') || in_cls(c, 'K'))) {
@@ -2160,6 +2186,7 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     }
     ftabs_bytes_ = uint32_t(tb.size());
     n_fitems_ = uint32_t(ft->items.size());
+    n_fclasses_ = uint32_t(ft->classes.size() / 8);
     for (auto& it : ft->items) {
       h_items_kind_.push_back(it.kind);
       h_items_id_.push_back(ft->item_ids[it.ids_off]);
@@ -2346,6 +2373,13 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (lds_tabs_)
       hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           int(ftabs_fold_bytes_ + 32 * n_fitems_));
+    // global-table fold kernel: items + classes in LDS up to 48 KiB (TSG_FOLD_STAGE=0: off)
+    fold_stage_bytes_ = 16 * size_t(n_fitems_) + 32 * size_t(n_fclasses_);
+    const char* fse = std::getenv("TSG_FOLD_STAGE");
+    fold_stage_ = !lds_tabs_ && fold_stage_bytes_ <= 48 * 1024 && (!fse || std::atoi(fse) != 0);
+    if (fold_stage_)
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          int(fold_stage_bytes_));
   }
 }
 
@@ -3125,6 +3159,8 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   fo.t_item_cls = ft_item_cls_;
   fo.t_classes = ft_classes_;
   fo.n_items = n_fitems_;
+  fo.stage_items = fold_stage_ ? 1u : 0u;
+  fo.n_classes = n_fclasses_;
   fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
   fo.first = static_cast<const uint32_t*>(d_fold_first_);
   fo.n_pairs_k = n_fold_pairs_k_;
@@ -3145,7 +3181,7 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
     if (lds_tabs_)
       fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
     else
-      fold_kernel<false><<<2048, 64 * kFoldWaves, 0, stream_>>>(fo);
+      fold_kernel<false><<<2048, 64 * kFoldWaves, fold_stage_ ? fold_stage_bytes_ : 0, stream_>>>(fo);
   }
   HIP_OK(hipGetLastError());
   if (diag_mode_ == 0 && kw_fold_ && n_kwf_ci_ + n_kwf_ck_ > 0) {
