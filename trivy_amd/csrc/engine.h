@@ -223,6 +223,7 @@ class GpuEngine {
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   bool fold_stage_ = false;        // global-table fold kernel: items + classes staged in LDS
+  bool c_stage_classes_ = false;   // global-table confirm kernel: classes staged in LDS
   size_t fold_stage_bytes_ = 0;
   uint32_t n_fclasses_ = 0;
   void* d_recs_ = nullptr; size_t cap_recs_ = 0;

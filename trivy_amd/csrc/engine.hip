@@ -657,6 +657,8 @@ struct ConfirmParams {
   uint32_t t_cmap, t_ccore, t_gitems, t_bgroups, n_cls;
   // literal-window hash (filter.h): keys at u64 [t_hkeys/8], items at u32 [t_hitems/4], 2^hash_bits slots
   uint32_t t_hkeys, t_hitems, hash_bits, hash_buckets;
+  // global-table variant: the n_classes byte classes (8 u32 each) staged in LDS (0: read from tabs)
+  uint32_t n_classes_lds;
   // TSG_K2_PACK experiment: each record's 48-B window packed sequentially (64-B
   // stride) by pack_kernel, read linearly instead of gathered from the arena
   const uint8_t* wins;
@@ -861,6 +863,12 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
   const uint32_t* item_ids = reinterpret_cast<const uint32_t*>(tabs + P.t_item_ids);
   const uint8_t* item_cls = tabs + P.t_item_cls;
   const uint32_t* classes = reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
+  if (!kLdsTabs && P.n_classes_lds) {  // large rule sets: the class words in LDS (one L2 round trip less per position)
+    const uint4* c = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(P.tabs) + P.t_classes);
+    for (uint32_t i = tid; i < P.n_classes_lds * 2; i += blockDim.x) reinterpret_cast<uint4*>(s_tabs)[i] = c[i];
+    __syncthreads();
+    classes = reinterpret_cast<const uint32_t*>(s_tabs);
+  }
   uint8_t* wwin = s_win + wave * 64 * kCWin;  // the wave's 64 windows
   uint64_t* wbase = s_base + wave * 64;      // block base per lane
   uint64_t* wfse = s_fse + wave * 128;       // the file holding the block's first byte, per lane
@@ -885,12 +893,25 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
     // 0.35 ms more -- the sets reject half the literal hits at a lower cost).
     const uint64_t cw0 = base >= 16 ? base - 16 : 0;  // the lane window [cw0, cw0 + kCWin)
     const uint8_t* cwin = wwin + l * kCWin;
+#ifndef TSG_C_PRE
+#define TSG_C_PRE 0
+#endif
+    // global tables: the first positions' class ids loaded up front (independent
+    // loads instead of one dependent round trip per position)
+    constexpr uint32_t kPre = kLdsTabs ? 0 : TSG_C_PRE;
+    uint32_t pre[kPre > 0 ? kPre : 1];
+#pragma unroll
+    for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
     auto sets_ok = [&](uint32_t q0, uint32_t q1) {
       for (uint32_t q = q0; q < q1; q++) {
         if (q >= core_lo && q < it.back) continue;
         const uint64_t pos = uint64_t(start) + q;
         const uint32_t bt = pos - cw0 < uint64_t(kCWin) ? uint32_t(cwin[pos - cw0]) : uint32_t(P.arena[pos]);
-        const uint32_t c = item_cls[it.cls_off + q];
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPre; k++)
+          if (q == k) c = pre[k];
+        if (q >= kPre) c = item_cls[it.cls_off + q];
         if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return false;
       }
       return true;
@@ -2363,6 +2384,13 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       return;
     }
     c_lds_bytes_ = lds_tabs_ ? fixed + ftabs_bytes_ : ConfirmFixedLds(kCThreadsG);
+    // global-table variant: the byte classes in LDS while four workgroups still fit a CU
+    // (TSG_CONFIRM_STAGE_CLASSES=0: off)
+    {
+      const char* sc = std::getenv("TSG_CONFIRM_STAGE_CLASSES");
+      c_stage_classes_ = !lds_tabs_ && c_lds_bytes_ + 32 * size_t(n_fclasses_) <= 40 * 1024 && (!sc || std::atoi(sc) != 0);
+      if (c_stage_classes_) c_lds_bytes_ += 32 * size_t(n_fclasses_);
+    }
     if (const char* e = std::getenv("TSG_CONFIRM_LDS_PAD")) c_lds_bytes_ += size_t(std::strtoull(e, nullptr, 10));  // occupancy experiments
     if (std::getenv("TSG_ENGINE_DEBUG"))
       std::fprintf(stderr, "confirm LDS: fixed %zu + tables %u (fold prefix %u) = %zu B, limit %zu, %s tables, %d threads\n",
@@ -3130,6 +3158,7 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   cp.t_hitems = ft_hitems_;
   cp.hash_bits = hash_bits_;
   cp.hash_buckets = hash_buckets_;
+  cp.n_classes_lds = c_stage_classes_ ? n_fclasses_ : 0u;
   cp.wins = nullptr;
   static const bool k2_pack = std::getenv("TSG_K2_PACK") && std::atoi(std::getenv("TSG_K2_PACK")) != 0;
   if (k2_pack && diag_mode_ == 0) {  // (experiment) the windows packed between K1 and K2, outside K2's events
