@@ -931,10 +931,14 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
                   spans.begin());
   };
   FileFindings& ff = out->findings;
-  auto put_censored = [&](int64_t a, int64_t b) {  // content [a, b) with censored bytes as '*', into ff.text
+  // content [a, b) with censored bytes as '*', into ff.text; k0: a span index at
+  // or below the first span ending after a (a finding's lines ascend: one search)
+  auto put_censored_from = [&](size_t k0, int64_t a, int64_t b) {
     const uint32_t at = uint32_t(ff.text.size());
     ff.text.append(reinterpret_cast<const char*>(content + a), size_t(b - a));
-    for (size_t k = first_span_after(a); k < spans.size() && spans[k].s < b; k++) {
+    size_t k = k0;
+    while (k < spans.size() && spans[k].e <= a) k++;
+    for (; k < spans.size() && spans[k].s < b; k++) {
       int64_t x = std::max(a, spans[k].s), y = std::min(b, spans[k].e);
       if (x < y) std::memset(&ff.text[at + size_t(x - a)], '*', size_t(y - x));
     }
@@ -967,6 +971,7 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   vnl.clear();
   const bool use_index = matched.size() >= 8 && uint64_t(len) <= uint64_t(matched.size()) * 8192;
   if (use_index) {
+    PhaseTimer pt15(15);
     size_t k = 0;
     for (const uint8_t *p = content, *e = content + len; p < e;) {
       const void* q = std::memchr(p, '\n', size_t(e - p));
@@ -1158,7 +1163,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
       start_line_num = vnl_below(start);
       ls = line_lo(start_line_num);
       le = line_hi(start_line_num);
-      end_line_num = vnl_below(end);  // start_line_num + count_nl(start, end)
+      end_line_num = start_line_num;  // vnl_below(end): a match spans few lines
+      while (end_line_num < n_vnl && vnl[size_t(end_line_num)] < end) end_line_num++;
     } else {
       start_line_num = nl_before(start);
       ls = line_start_of(start);
@@ -1170,12 +1176,13 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
       mls = (start - ls - 30 < 0) ? ls : start - 30;
       mle = (end + 20 > le) ? le : end + 20;
     }
-    const uint32_t ml_off = put_censored(mls, mle), ml_len = uint32_t(mle - mls);
     int64_t code_start = std::max<int64_t>(start_line_num - 2, 0);
     int64_t p = ls;
     if (use_index) p = line_lo(code_start);
     else
       for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
+    size_t kspan = first_span_after(p);  // every text below starts at or after p
+    const uint32_t ml_off = put_censored_from(kspan, mls, mle), ml_len = uint32_t(mle - mls);
     bool found_first = false;
     f.line_lo = uint32_t(ff.lines.size());
     if (!binary) {
@@ -1189,7 +1196,8 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
         } else {
           const int64_t q = e - p > 100 ? p + 100 : e;
           n = uint32_t(q - p);
-          off = put_censored(p, q);
+          while (kspan < spans.size() && spans[kspan].e <= p) kspan++;
+          off = put_censored_from(kspan, p, q);
         }
         ff.lines.push_back({k + 1, off, n, in_cause, !found_first && in_cause, false});
         found_first = found_first || in_cause;
@@ -1536,9 +1544,9 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
                  t_ordered - t_sorted, t_par - t_sorted);
   if (g_tail_debug)
     std::fprintf(stderr, "tail phases ms: findall %.1f gate %.1f blocks %.1f findings %.1f sort %.1f allow-loc %.1f go %.1f "
-                 "scanfile %.1f\n",
+                 "scanfile %.1f (newline index %.1f)\n",
                  g_prof[0] / 1e6, g_prof[1] / 1e6, g_prof[2] / 1e6, g_prof[3] / 1e6, g_prof[4] / 1e6,
-                 g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6);
+                 g_prof[5] / 1e6, g_prof[6] / 1e6, g_prof[7] / 1e6, g_prof[15] / 1e6);
   if (g_tail_debug)
     std::fprintf(stderr, "tail findings: %lld with the newline index, %lld by walks; censor spans %lld; text %.1f MB\n",
                  (long long)g_prof[11].load(), (long long)g_prof[12].load(), (long long)g_prof[13].load(),
