@@ -1,6 +1,6 @@
 # Round-5 GPU iteration: stages chosen by STAGES (space-separated), each under its own time limit,
 # stopping at the first failure.  Usage: gpurun -- 'TAG=r04a STAGES="tests bench diag prof" bash tools/gpu_r05.sh'
-#   tests  : the -m gpu suite (PYTEST_ARGS narrows it)
+#   tests  : the -m gpu suite (PYTEST_K: a -k expression; PYTEST_ARGS: more words)
 #   smoke  : __graft_entry__.smoke()
 #   bench  : the driver-style default line (20 steps, 5 warm-up, CPU baseline, parity, ingest leg)
 #   quick  : C2 without the CPU baseline (BENCH_ARGS adds flags)
@@ -16,7 +16,7 @@ R=$GRAFT_REPO_ROOT
 for st in $STAGES; do
   case $st in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests_$TAG.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-} > gpurun_out/gpu_tests_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
