@@ -6,7 +6,8 @@
 #   quick  : C2 without the CPU baseline (BENCH_ARGS adds flags)
 #   diag   : C2 confirm-kernel split (TSG_DIAG_CONFIRM 4 / 8 / 16), 5 steps each
 #   prof   : rocprofv3 --kernel-trace --stats of a short C2 run
-#   wl     : the workloads in WLS (default c3 c3f c4 c1fs c5), with CPU baselines unless WL_ARGS says otherwise
+#   wl     : the workloads in WLS (default c3 c3f c4 c1fs c5), with CPU baselines unless WL_ARGS says otherwise;
+#            WL_ARGS_<wl> adds flags for one workload
 set -o pipefail
 TAG=${TAG:-r05}
 STAGES=${STAGES:-tests bench}
@@ -144,7 +145,8 @@ PYEOF
       cd $R ;;
     wl)
       for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
-        timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
+        xv="WL_ARGS_$wl"  # per-workload flags (WL_ARGS_c3f="--steps 20"; the last --steps wins)
+        timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} ${!xv:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
         rc=$?; echo "== $wl"; python tools/bench_brief.py gpurun_out/wl_${TAG}_$wl.json; tail -2 gpurun_out/wl_${TAG}_$wl.err; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac

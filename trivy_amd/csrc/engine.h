@@ -223,6 +223,8 @@ class GpuEngine {
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   bool fold_stage_ = false;        // global-table fold kernel: items + classes staged in LDS
+  bool fold_wide_ = false;         // staged global-table fold kernel: 16-wave workgroups (TSG_FOLD_WAVES=4: 4)
+  bool fold_check_first_ = false;  // global-table fold kernel: first-byte set test per start (TSG_FOLD_FIRST=1)
   bool c_stage_classes_ = false;   // global-table confirm kernel: classes staged in LDS
   size_t fold_stage_bytes_ = 0;
   uint32_t n_fclasses_ = 0;

@@ -1249,6 +1249,9 @@ struct FoldParams {
   // global-table variant (large rule sets): the item records and the byte
   // classes staged in LDS when they fit (n_classes classes of 8 u32)
   uint32_t stage_items, n_classes;
+  // global tables: test position 0 against the item's first-byte set (one more
+  // dependent global load per start; without it the position loop rejects)
+  uint32_t check_first;
 };
 
 constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
@@ -1260,11 +1263,17 @@ constexpr int kFoldWaves = 4;
 // x + kFoldSpan) go to the wave's LDS window, the lanes split the tasks.  With
 // kLdsTabs the item tables and the position-0 byte sets are staged in LDS.
 // U+0130 sites only flag the file (Go's (?i) does not fold U+0130 onto 'i').
-template <bool kLdsTabs>  // as confirm_kernel
-__global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
+// kWaves waves per workgroup: 16 when the items and classes are staged (~50 KB of
+// LDS: three 4-wave workgroups per CU left 12 waves to hide the global loads)
+#ifndef TSG_FOLD_WIDE_WPE
+#define TSG_FOLD_WIDE_WPE 8  // waves per SIMD asked of the 16-wave variant: 8 = two workgroups per CU (64 VGPRs)
+#endif
+template <bool kLdsTabs, int kWaves = kFoldWaves>  // kLdsTabs as confirm_kernel
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(kWaves == 16 ? TSG_FOLD_WIDE_WPE : 1)))
+void fold_kernel(FoldParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ uint8_t s_win[kFoldWaves][kFoldWin];
-  __shared__ uint32_t s_idx[kFoldWaves][2][64];  // per wave: index lists' exclusive prefix and start, per q
+  __shared__ uint8_t s_win[kWaves][kFoldWin];
+  __shared__ uint32_t s_idx[kWaves][2][64];  // per wave: index lists' exclusive prefix and start, per q
   if (kLdsTabs) {
     const uint4* t = reinterpret_cast<const uint4*>(P.tabs);
     uint4* d = reinterpret_cast<uint4*>(smem);
@@ -1297,7 +1306,7 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* wb = s_win[wave];
   const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
-  for (uint32_t si = blockIdx.x * kFoldWaves + wave; si < n_folds; si += gridDim.x * kFoldWaves) {
+  for (uint32_t si = blockIdx.x * kWaves + wave; si < n_folds; si += gridDim.x * kWaves) {
     const FoldSite fsite = P.folds[si];
     const uint64_t fs = P.off[fsite.f], fe = P.off[fsite.f + 1];
     const uint64_t w0 = fsite.x > fs + kFoldSpan ? fsite.x - kFoldSpan : fs;
@@ -1323,7 +1332,7 @@ __global__ __launch_bounds__(64 * kFoldWaves) void fold_kernel(FoldParams P) {
       const uint32_t* first = firsts + 8ull * ix;
       const uint64_t st = fsite.x - back;
       const uint32_t b0 = wb[st - w0];
-      if (!((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
+      if ((kLdsTabs || P.check_first) && !((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
       uint64_t p = st, lit_bytes_end = 0;
       bool ok = true, covered = false;
       // the first positions' class ids up front: independent loads instead of
@@ -2405,9 +2414,19 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     fold_stage_bytes_ = 16 * size_t(n_fitems_) + 32 * size_t(n_fclasses_);
     const char* fse = std::getenv("TSG_FOLD_STAGE");
     fold_stage_ = !lds_tabs_ && fold_stage_bytes_ <= 48 * 1024 && (!fse || std::atoi(fse) != 0);
+    const char* ffe = std::getenv("TSG_FOLD_FIRST");
+    fold_check_first_ = ffe && std::atoi(ffe) != 0;
+    const char* fwe = std::getenv("TSG_FOLD_WAVES");
+    fold_wide_ = fold_stage_ && (!fwe || std::atoi(fwe) == 16);
+    if (std::getenv("TSG_ENGINE_DEBUG"))
+      std::fprintf(stderr, "fold: %u items, %u classes, staged %s (%zu B), first-byte test %s, %d waves per workgroup\n",
+                   n_fitems_, n_fclasses_,
+                   lds_tabs_ ? "(LDS tables)" : fold_stage_ ? "yes" : "no", fold_stage_bytes_,
+                   lds_tabs_ || fold_check_first_ ? "on" : "off", fold_wide_ ? 16 : kFoldWaves);
     if (fold_stage_)
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          int(fold_stage_bytes_));
+      hipFuncSetAttribute(fold_wide_ ? reinterpret_cast<const void*>(&fold_kernel<false, 16>)
+                                     : reinterpret_cast<const void*>(&fold_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, int(fold_stage_bytes_));
   }
 }
 
@@ -3190,6 +3209,7 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   fo.n_items = n_fitems_;
   fo.stage_items = fold_stage_ ? 1u : 0u;
   fo.n_classes = n_fclasses_;
+  fo.check_first = fold_check_first_ ? 1u : 0u;
   fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
   fo.first = static_cast<const uint32_t*>(d_fold_first_);
   fo.n_pairs_k = n_fold_pairs_k_;
@@ -3209,6 +3229,8 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   if (diag_mode_ == 0) {
     if (lds_tabs_)
       fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
+    else if (fold_wide_)
+      fold_kernel<false, 16><<<2048, 64 * 16, fold_stage_bytes_, stream_>>>(fo);
     else
       fold_kernel<false><<<2048, 64 * kFoldWaves, fold_stage_ ? fold_stage_bytes_ : 0, stream_>>>(fo);
   }
