@@ -206,7 +206,6 @@ class GpuEngine {
   void* d_ftabs_ = nullptr;
   void* d_fold_pairs_ = nullptr;  // fold kernel work list
   void* d_fold_first_ = nullptr;  // per item: bytes that can start it (fold kernel prefilter)
-  void* d_fold_heads_ = nullptr;  // per filter item: its first four class ids (fold kernel, staged)
   uint32_t n_fold_pairs_k_ = 0, n_fold_pairs_s_ = 0, n_fold_cap_k_ = 0, n_fold_cap_s_ = 0;
   void* d_fold_idx_off_ = nullptr;   // fold kernel: capable tasks by (rune kind, q, key byte)
   void* d_fold_idx_items_ = nullptr;
@@ -225,7 +224,7 @@ class GpuEngine {
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   bool fold_stage_ = false;        // global-table fold kernel: items + classes staged in LDS
   bool fold_wide_ = false;         // staged global-table fold kernel: 16-wave workgroups (TSG_FOLD_WAVES=4: 4)
-  bool fold_check_first_ = true;   // unstaged global-table fold kernel: first-byte set test per start (TSG_FOLD_FIRST=0: off)
+  bool fold_check_first_ = true;   // global-table fold kernel: first-byte set test per start (TSG_FOLD_FIRST=0: off)
   bool c_stage_classes_ = false;   // global-table confirm kernel: classes staged in LDS
   size_t fold_stage_bytes_ = 0;
   uint32_t n_fclasses_ = 0;

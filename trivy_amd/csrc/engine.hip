@@ -903,6 +903,11 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
     for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
     auto sets_ok = [&](uint32_t q0, uint32_t q1) {
+      // global tables: the class ids 16 at a time (one aligned 16-B load per 16
+      // positions instead of a dependent byte load per position: an item's
+      // lookahead runs, e.g. [a-z0-9]{32,48}, were one L2 round trip each)
+      uint4 chunk = make_uint4(0, 0, 0, 0);
+      uint32_t chunk_at = ~0u;
       for (uint32_t q = q0; q < q1; q++) {
         if (q >= core_lo && q < it.back) continue;
         const uint64_t pos = uint64_t(start) + q;
@@ -911,7 +916,18 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
         for (uint32_t k = 0; k < kPre; k++)
           if (q == k) c = pre[k];
-        if (q >= kPre) c = item_cls[it.cls_off + q];
+        if (kLdsTabs) {
+          if (q >= kPre) c = item_cls[it.cls_off + q];
+        } else if (q >= kPre) {
+          const uint32_t ci = it.cls_off + q;
+          if ((ci >> 4) != chunk_at) {  // item_cls is 16-B aligned and padded in the table blob
+            chunk_at = ci >> 4;
+            chunk = *reinterpret_cast<const uint4*>(item_cls + (ci & ~15u));
+          }
+          const uint32_t w4 = (ci >> 2) & 3u;
+          const uint32_t w = w4 == 0 ? chunk.x : w4 == 1 ? chunk.y : w4 == 2 ? chunk.z : chunk.w;
+          c = (w >> (8 * (ci & 3u))) & 255u;
+        }
         if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return false;
       }
       return true;
@@ -1252,9 +1268,6 @@ struct FoldParams {
   // global tables: test position 0 against the item's first-byte set (one more
   // dependent global load per start; without it the position loop rejects)
   uint32_t check_first;
-  // staged variant: per item its first four positions' class ids (one byte each),
-  // staged after the classes, so a start's first positions cost no global load
-  const uint32_t* heads;
 };
 
 constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
@@ -1294,8 +1307,6 @@ void fold_kernel(FoldParams P) {
     const uint4* c = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(P.tabs) + P.t_classes);
     uint4* dc = reinterpret_cast<uint4*>(smem + 16 * size_t(P.n_items));
     for (uint32_t i = threadIdx.x; i < P.n_classes * 2; i += blockDim.x) dc[i] = c[i];
-    uint32_t* dh = reinterpret_cast<uint32_t*>(smem + 16 * size_t(P.n_items) + 32 * size_t(P.n_classes));
-    for (uint32_t i = threadIdx.x; i < P.n_items; i += blockDim.x) dh[i] = P.heads[i];
   }
   __syncthreads();
   const uint8_t* tabs = kLdsTabs ? smem : static_cast<const uint8_t*>(P.tabs);
@@ -1307,8 +1318,6 @@ void fold_kernel(FoldParams P) {
   const uint8_t* item_cls = tabs + P.t_item_cls;
   const uint32_t* classes = staged ? reinterpret_cast<const uint32_t*>(smem + 16 * size_t(P.n_items))
                                    : reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
-  const uint32_t* heads =
-      reinterpret_cast<const uint32_t*>(smem + 16 * size_t(P.n_items) + 32 * size_t(P.n_classes));  // (staged)
   auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* wb = s_win[wave];
@@ -1339,24 +1348,17 @@ void fold_kernel(FoldParams P) {
       const uint32_t* first = firsts + 8ull * ix;
       const uint64_t st = fsite.x - back;
       const uint32_t b0 = wb[st - w0];
-      // position 0 against its byte set (+ fold leads): a superset test, skipped
-      // when the class ids are staged (the loop's first step is as cheap)
-      if ((kLdsTabs || (P.check_first && !staged)) && !((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;
+      if ((kLdsTabs || P.check_first) && !((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
       uint64_t p = st, lit_bytes_end = 0;
       bool ok = true, covered = false;
-      // the first positions' class ids up front: from LDS when staged, else
-      // independent loads instead of one dependent round trip per position
+      // the first positions' class ids up front: independent loads instead of
+      // one dependent round trip per position (global tables)
       constexpr uint32_t kPre = 6;
       uint32_t pre[kPre];
-      if (staged) {
-        const uint32_t h = heads[ix];
 #pragma unroll
-        for (uint32_t q = 0; q < kPre; q++) pre[q] = q < 4 ? (h >> (8 * q)) & 255u : 0u;
-      } else {
-#pragma unroll
-        for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
-      }
-      const uint32_t n_pre = staged ? 4u : kPre;
+      for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
+      uint4 chunk = make_uint4(0, 0, 0, 0);  // global tables: class ids 16 at a time (as confirm_kernel)
+      uint32_t chunk_at = ~0u;
       for (uint32_t q = 0; q < it.n && ok; q++) {
         if (q == it.lit_end) lit_bytes_end = p;
         if (p >= w1) {
@@ -1368,7 +1370,20 @@ void fold_kernel(FoldParams P) {
 #pragma unroll
         for (uint32_t k = 0; k < kPre; k++)
           if (q == k) c = pre[k];
-        if (q >= n_pre) c = item_cls[it.cls_off + q];
+        if (q >= kPre) {
+          const uint32_t ci = it.cls_off + q;
+          if (kLdsTabs) {
+            c = item_cls[ci];
+          } else {
+            if ((ci >> 4) != chunk_at) {
+              chunk_at = ci >> 4;
+              chunk = *reinterpret_cast<const uint4*>(item_cls + (ci & ~15u));
+            }
+            const uint32_t w4 = (ci >> 2) & 3u;
+            const uint32_t w = w4 == 0 ? chunk.x : w4 == 1 ? chunk.y : w4 == 2 ? chunk.z : chunk.w;
+            c = (w >> (8 * (ci & 3u))) & 255u;
+          }
+        }
         const uint32_t b = wb[p - w0];
         if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
             (in_cls(c, 'k') || in_cls(c, 'K'))) {
@@ -2284,14 +2299,6 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
       uint8_t* dfm = nullptr;
       if (!Upload(&err_, &dfm, reinterpret_cast<const uint8_t*>(first.data()), first.size() * sizeof(uint32_t))) return;
       d_fold_first_ = dfm;
-      std::vector<uint32_t> heads(std::max<size_t>(ft->items.size(), 1), 0);  // FoldParams::heads
-      for (uint32_t i = 0; i < uint32_t(ft->items.size()); i++) {
-        const FilterItemGpu& it = ft->items[i];
-        for (uint32_t q = 0; q < 4 && q < it.n; q++) heads[i] |= uint32_t(ft->item_cls[it.cls_off + q]) << (8 * q);
-      }
-      uint8_t* dhd = nullptr;
-      if (!Upload(&err_, &dhd, reinterpret_cast<const uint8_t*>(heads.data()), heads.size() * sizeof(uint32_t))) return;
-      d_fold_heads_ = dhd;
       // byte index of the capable tasks (FoldParams idx_*): key = the byte at
       // x - q (position 0, one byte: no other fold rune precedes x) for q > 0,
       // the byte after the rune (position 1, or a fold lead when position 1
@@ -2434,20 +2441,19 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     if (lds_tabs_)
       hipFuncSetAttribute(reinterpret_cast<const void*>(&fold_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           int(ftabs_fold_bytes_ + 32 * n_fitems_));
-    // global-table fold kernel: items, classes and the items' first class ids in
-    // LDS while two 16-wave workgroups fit a CU (TSG_FOLD_STAGE=0: off)
-    fold_stage_bytes_ = 20 * size_t(n_fitems_) + 32 * size_t(n_fclasses_);
+    // global-table fold kernel: items + classes in LDS up to 48 KiB (TSG_FOLD_STAGE=0: off)
+    fold_stage_bytes_ = 16 * size_t(n_fitems_) + 32 * size_t(n_fclasses_);
     const char* fse = std::getenv("TSG_FOLD_STAGE");
-    fold_stage_ = !lds_tabs_ && fold_stage_bytes_ <= 64 * 1024 && (!fse || std::atoi(fse) != 0);
+    fold_stage_ = !lds_tabs_ && fold_stage_bytes_ <= 48 * 1024 && (!fse || std::atoi(fse) != 0);
     const char* ffe = std::getenv("TSG_FOLD_FIRST");
-    fold_check_first_ = !ffe || std::atoi(ffe) != 0;  // (r05g: without it the unstaged kernel took 3.0-3.7 ms, not 2.1)
+    fold_check_first_ = !ffe || std::atoi(ffe) != 0;  // r05g: without it 3.0-3.7 ms instead of 1.6-2.1
     const char* fwe = std::getenv("TSG_FOLD_WAVES");
     fold_wide_ = fold_stage_ && (!fwe || std::atoi(fwe) == 16);
     if (std::getenv("TSG_ENGINE_DEBUG"))
       std::fprintf(stderr, "fold: %u items, %u classes, staged %s (%zu B), first-byte test %s, %d waves per workgroup\n",
                    n_fitems_, n_fclasses_,
                    lds_tabs_ ? "(LDS tables)" : fold_stage_ ? "yes" : "no", fold_stage_bytes_,
-                   lds_tabs_ || (fold_check_first_ && !fold_stage_) ? "on" : "off", fold_wide_ ? 16 : kFoldWaves);
+                   lds_tabs_ || fold_check_first_ ? "on" : "off", fold_wide_ ? 16 : kFoldWaves);
     if (fold_stage_)
       hipFuncSetAttribute(fold_wide_ ? reinterpret_cast<const void*>(&fold_kernel<false, 16>)
                                      : reinterpret_cast<const void*>(&fold_kernel<false>),
@@ -2469,7 +2475,7 @@ GpuEngine::~GpuEngine() {
   reap_cv_.notify_all();
   if (reaper_.joinable()) reaper_.join();
   hipSetDevice(device_);
-  void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_fold_heads_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
+  void* ps[] = {d_item_diag_, d_fold_pairs_, d_kwfold_pairs_, d_fold_idx_off_, d_fold_idx_items_, d_fold_first_, d_reach_, d_core_, d_group_items_, d_bucket_groups_, d_ftabs_, d_folds_, d_recs_, d_anchors_,
                 d_rules_, d_rule_kw_, d_nfa_, d_fullscan_rules_, d_counters_, d_chunk_file_, d_nl_, d_kw_,
                 d_flags_, d_hits_, d_cands_, d_fs_pairs_, d_fs_tasks_, d_fs_wave_, d_fs_ctr_, d_xlen_, d_xoff_, d_xscan_,
                 d_xf_, d_gfiles_, d_gdst_, d_gbuf_, d_wins_};
@@ -3237,7 +3243,6 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   fo.check_first = fold_check_first_ ? 1u : 0u;
   fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
   fo.first = static_cast<const uint32_t*>(d_fold_first_);
-  fo.heads = static_cast<const uint32_t*>(d_fold_heads_);
   fo.n_pairs_k = n_fold_pairs_k_;
   fo.n_pairs_s = n_fold_pairs_s_;
   fo.n_cap_k = n_fold_cap_k_;
