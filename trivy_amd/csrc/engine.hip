@@ -903,11 +903,6 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
     for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
     auto sets_ok = [&](uint32_t q0, uint32_t q1) {
-      // global tables: the class ids 16 at a time (one aligned 16-B load per 16
-      // positions instead of a dependent byte load per position: an item's
-      // lookahead runs, e.g. [a-z0-9]{32,48}, were one L2 round trip each)
-      uint4 chunk = make_uint4(0, 0, 0, 0);
-      uint32_t chunk_at = ~0u;
       for (uint32_t q = q0; q < q1; q++) {
         if (q >= core_lo && q < it.back) continue;
         const uint64_t pos = uint64_t(start) + q;
@@ -916,18 +911,7 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
         for (uint32_t k = 0; k < kPre; k++)
           if (q == k) c = pre[k];
-        if (kLdsTabs) {
-          if (q >= kPre) c = item_cls[it.cls_off + q];
-        } else if (q >= kPre) {
-          const uint32_t ci = it.cls_off + q;
-          if ((ci >> 4) != chunk_at) {  // item_cls is 16-B aligned and padded in the table blob
-            chunk_at = ci >> 4;
-            chunk = *reinterpret_cast<const uint4*>(item_cls + (ci & ~15u));
-          }
-          const uint32_t w4 = (ci >> 2) & 3u;
-          const uint32_t w = w4 == 0 ? chunk.x : w4 == 1 ? chunk.y : w4 == 2 ? chunk.z : chunk.w;
-          c = (w >> (8 * (ci & 3u))) & 255u;
-        }
+        if (q >= kPre) c = item_cls[it.cls_off + q];
         if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return false;
       }
       return true;
@@ -1357,8 +1341,6 @@ void fold_kernel(FoldParams P) {
       uint32_t pre[kPre];
 #pragma unroll
       for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
-      uint4 chunk = make_uint4(0, 0, 0, 0);  // global tables: class ids 16 at a time (as confirm_kernel)
-      uint32_t chunk_at = ~0u;
       for (uint32_t q = 0; q < it.n && ok; q++) {
         if (q == it.lit_end) lit_bytes_end = p;
         if (p >= w1) {
@@ -1370,20 +1352,7 @@ void fold_kernel(FoldParams P) {
 #pragma unroll
         for (uint32_t k = 0; k < kPre; k++)
           if (q == k) c = pre[k];
-        if (q >= kPre) {
-          const uint32_t ci = it.cls_off + q;
-          if (kLdsTabs) {
-            c = item_cls[ci];
-          } else {
-            if ((ci >> 4) != chunk_at) {
-              chunk_at = ci >> 4;
-              chunk = *reinterpret_cast<const uint4*>(item_cls + (ci & ~15u));
-            }
-            const uint32_t w4 = (ci >> 2) & 3u;
-            const uint32_t w = w4 == 0 ? chunk.x : w4 == 1 ? chunk.y : w4 == 2 ? chunk.z : chunk.w;
-            c = (w >> (8 * (ci & 3u))) & 255u;
-          }
-        }
+        if (q >= kPre) c = item_cls[it.cls_off + q];
         const uint32_t b = wb[p - w0];
         if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
             (in_cls(c, 'k') || in_cls(c, 'K'))) {
