@@ -198,3 +198,39 @@ def test_c3f_fullscan_rules_every_file_matches_cpuref(tmp_path):
     chosen = sorted(set(withkw[:40]) | set(rng.sample(small, 60)))
     want = _oracle([(i, C.path(i), C.content(i)) for i in chosen], str(cfg))
     assert _check(C, res, chosen, want) > 10
+
+
+_VARIANT_CASE = {}
+
+
+@pytest.mark.parametrize("env", [
+    {},                                          # items + classes in LDS, 16-wave workgroups, first-byte test
+    {"TSG_FOLD_WAVES": "4"},                      # the same staging in 4-wave workgroups
+    {"TSG_FOLD_STAGE": "0"},                      # global tables, 4-wave workgroups
+    {"TSG_FOLD_STAGE": "0", "TSG_FOLD_FIRST": "0"},  # ... without the first-byte test
+    {"TSG_CONFIRM_STAGE_CLASSES": "0"},            # confirm kernel with its classes in global memory
+], ids=["default", "waves4", "unstaged", "unstaged-nofirst", "confirm-global-classes"])
+def test_c3_global_table_kernel_variants_match_cpuref(tmp_path, monkeypatch, env):
+    """The global-table (2,087-rule) fold and confirm kernels in each selectable shape (engine.hip
+    fold_kernel / confirm_kernel): every file of a C3 corpus holding fold
+    runes byte-identical to the restated reference CPU scan, with the fold sites actually tried."""
+    from bench import full_diff
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    for k in ("TSG_FOLD_WAVES", "TSG_FOLD_STAGE", "TSG_FOLD_FIRST", "TSG_CONFIRM_STAGE_CLASSES"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if "c3" not in _VARIANT_CASE:  # one corpus and one reference scan for every variant
+        y, samples = corpus.c3_rules()
+        cfg = tmp_path / "trivy-secret.yaml"
+        cfg.write_text(y)
+        C = corpus.generate_c3(int(32e6), samples, seed=corpus.SEED + 19, secrets_per_byte=1.0 / 16384)
+        _VARIANT_CASE["c3"] = (C, str(cfg), _cpuref(C, cfg_path=str(cfg)))
+    C, cfg, ref = _VARIANT_CASE["c3"]
+    res = secret.NewScanner(secret.ParseConfig(cfg)).scan_arena(C.arena, C.offsets, C.path_ptrs)
+    st = res.stats()
+    assert st["fold_sites"] > 50, st["fold_sites"]
+    bad, first = full_diff(res, ref, C.n_files)
+    assert bad == 0, (bad, C.path(first) if first is not None else None)
+    assert st["findings"] > 100
