@@ -86,11 +86,13 @@ class HostPool {
     return *p;
   }
 
-  void Run(size_t n, int threads, const std::function<void(size_t)>& fn) {
+  // wide: the job may take the spare workers too (a scan's exact pass when no
+  // other scan is in flight: the end of a run, where nothing else needs the cores)
+  void Run(size_t n, int threads, const std::function<void(size_t)>& fn, bool wide = false) {
     auto job = std::make_shared<PoolJob>();
     job->fn = &fn;
     job->n = n;
-    job->max_helpers = int(std::min<size_t>(size_t(threads - 1), n - 1));
+    job->max_helpers = int(std::min<size_t>({size_t(threads - 1), n - 1, size_t(wide ? n_workers_ : n_steady_)}));
     if (job->max_helpers > 0 && !workers_.empty()) {
       std::lock_guard<std::mutex> g(mu_);
       q_.push_back(job);
@@ -106,6 +108,12 @@ class HostPool {
     const char* e = std::getenv("TSG_POOL_THREADS");
     int n = e ? std::atoi(e) : PoolBudget();
     if (n < 0) n = 0;
+    // spare workers only wide jobs use (TSG_POOL_SPARE; default none)
+    const char* sp = std::getenv("TSG_POOL_SPARE");
+    const int spare = sp ? std::max(0, std::atoi(sp)) : 0;
+    n_steady_ = n;
+    n_workers_ = n + spare;
+    n = n_workers_;
     for (int k = 0; k < n; k++) {
       workers_.emplace_back([this] {
         pthread_setname_np(pthread_self(), "tsg-pool");
@@ -136,19 +144,20 @@ class HostPool {
   std::condition_variable cv_;
   std::deque<std::shared_ptr<PoolJob>> q_;
   std::vector<std::thread> workers_;
+  int n_steady_ = 0, n_workers_ = 0;  // helpers a job may take: ordinary / wide
 };
 
 // fn(i) for i in [0, n) on up to `threads` threads (the caller's included),
 // indices handed out one at a time; the helpers come from the shared pool.
 template <typename F>
-void ParallelFor(size_t n, int threads, F fn) {
+void ParallelFor(size_t n, int threads, F fn, bool wide = false) {
   if (n == 0) return;
   if (threads <= 1 || n < 2) {
     for (size_t i = 0; i < n; i++) fn(i);
     return;
   }
   const std::function<void(size_t)> f = [&fn](size_t i) { fn(i); };
-  HostPool::Get().Run(n, threads, f);
+  HostPool::Get().Run(n, threads, f, wide);
 }
 
 }  // namespace tsg

@@ -1230,6 +1230,11 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
 
 bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst, std::string* err) {
   double t0 = NowMs();
+  struct Active {
+    std::atomic<int>& n;
+    explicit Active(std::atomic<int>& c) : n(c) { n.fetch_add(1); }
+    ~Active() { n.fetch_sub(1); }
+  } active(active_scans_);
   HostStats hs;
   std::vector<Candidate> cands;
   uint64_t n_bytes = in.n_files ? in.host_offsets[in.n_files] : 0;
@@ -1526,6 +1531,10 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     ScanFile(data, len, std::string_view(p, pn), in.binary && in.binary[f], t_group.data(), t_group.size(), &tmp[k],
              gpu_windows);
   };
+  // no other scan in flight (the end of a run): the pool's spare workers join in,
+  // the last scan's exact pass being all that is left (TSG_DRAIN_WIDE=0: never)
+  static const bool drain_wide = !std::getenv("TSG_DRAIN_WIDE") || std::atoi(std::getenv("TSG_DRAIN_WIDE")) != 0;
+  const bool wide = drain_wide && active_scans_.load() <= 1;
   ParallelFor(n_items, host_threads_, [&](size_t it) {
     if (it < top) {
       scan_group(order[it]);
@@ -1537,7 +1546,7 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
       if (kk + 1 < kk1) prefetch_group(order[kk + 1]);
       scan_group(order[kk]);
     }
-  });
+  }, wide);
   const double t_par = NowMs();
   if (g_tail_debug)
     std::fprintf(stderr, "tail serial ms: sort+setup %.1f (order %.1f) parallel %.1f\n", t_sorted - t2,
