@@ -620,7 +620,7 @@ int IndexEntries(const EvalCtx* c, const uint8_t* tar, uint64_t n, uint64_t p, u
       Evaluate(c, tar, &e);
       spec[s].push_back(std::move(e));
     }
-  });
+  }, true);
   // The merge plans ranges of the speculative vectors (and of the rare
   // sequential fallbacks) first, reading only positions and sizes; *out then
   // gets pointers to the entries, filled in parallel.
@@ -677,7 +677,7 @@ int IndexEntries(const EvalCtx* c, const uint8_t* tar, uint64_t n, uint64_t p, u
     out->resize(at.back());
     tsg::ParallelFor(plan.size(), threads, [&](size_t k) {
       for (size_t i = plan[k].lo; i < plan[k].hi; i++) (*out)[at[k] + (i - plan[k].lo)] = &(*plan[k].v)[i];
-    });
+    }, true);
   }
   if (dbg) {
     size_t n_spec = 0;
@@ -860,7 +860,7 @@ size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry*>
       q.skipped += e.state == 1;
     }
     q.entries = kAcceptBlock;
-  });
+  }, true);
   // the blocks that fit, and each one's starting row
   std::vector<Sum> at(1);
   uint64_t acct = c->acct(), used = c->used;
@@ -903,7 +903,7 @@ size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry*>
       c->path_off[f + 1] = pp;
       f++;
     }
-  });
+  }, true);
   for (size_t b = 0; b < m; b++) {
     const Sum& q = sum[b];
     c->used += q.used;
@@ -1060,7 +1060,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
         else tsg::StripCR(tar + e.data, e.size, dst);
       }
       _mm_sfence();
-    });
+    }, true);
     std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
     if (dbg) {
       const double t4 = now();

@@ -356,7 +356,7 @@ bool ListTree(tsg_fs_walk* w, int threads) {
       closedir(dp);
       // os.ReadDir: sorted by filename (byte order)
       std::sort(out.begin(), out.end(), [](const DirNode::Child& a, const DirNode::Child& b) { return a.name < b.name; });
-    });
+    }, true);
     if (fail) {
       tsg::SetError(fail_msg);
       return false;
@@ -511,7 +511,7 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
         x.state = 2;
         x.out_len = x.bin ? f.size + f.size / 5 + 1 : f.size;  // the largest transformed size
       }
-    });
+    }, true);
     size_t k = 0;
     bool full = false;
     std::vector<size_t> added;
@@ -570,7 +570,7 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
       } else {
         final_len[j] = int64_t(tsg::StripCR(dst, uint64_t(r), dst));
       }
-    });
+    }, true);
     if (read_err && read_err != EACCES && read_err != ENOENT) {
       tsg::SetError(std::string("fs walk: read error: ") + std::strerror(read_err));
       return -1;

@@ -53,7 +53,7 @@ struct PoolJob {
 // reserve (the callers, the GPU-driving thread and the allow-path pass run
 // beside the pool; going over a quota stalls every thread for the rest of the
 // period: on a 16-CPU box 12 workers measured 12% above 15).
-inline int PoolBudget() {
+inline int PoolCpus() {
   int aff = 0, online = int(std::thread::hardware_concurrency());
   cpu_set_t set;
   CPU_ZERO(&set);
@@ -71,23 +71,33 @@ inline int PoolBudget() {
     std::fclose(f);
   }
   if (q > 0 && per > 0) cpus = std::min(cpus, double(q) / double(per) / ranks);
-  const int c = std::max(1, int(cpus));
-  const int reserve = c >= 16 ? 4 : std::max(1, c / 4);
-  return std::max(1, c - reserve);
+  return std::max(1, int(cpus));
 }
+inline int PoolReserve(int c) { return c >= 16 ? 4 : std::max(1, c / 4); }
+inline int PoolBudget() {
+  const int c = PoolCpus();
+  return std::max(1, c - PoolReserve(c));
+}
+
+// Spare workers beside PoolBudget(): reserve - 1 (3 on the 16-CPU box), taken only
+// by wide jobs -- the tar / FS walks (the host-bound C4 and c1fs paths, where the
+// GPU-driving and allow-path threads the reserve is for are mostly idle: C4 38 -> 40
+// GB/s at 15 workers, profiles/r05/r05l) and a scan's exact pass when no other scan
+// is in flight (the drain at the end of a run).
+inline int PoolSpare() { return std::max(0, PoolReserve(PoolCpus()) - 1); }
 
 class HostPool {
  public:
   // TSG_POOL_THREADS workers; default PoolBudget() (12 on the 16-CPU-quota
   // one-GPU box; 12 per rank for 8 ranks sharing a 128-CPU quota; 15 with 16
-  // cores and no quota).
+  // cores and no quota) plus PoolSpare() that only wide jobs take.
   static HostPool& Get() {
     static HostPool* p = new HostPool();  // never destroyed: workers may be parked at exit
     return *p;
   }
 
-  // wide: the job may take the spare workers too (a scan's exact pass when no
-  // other scan is in flight: the end of a run, where nothing else needs the cores)
+  // wide: the job may take the spare workers too (the walks; a scan's exact pass
+  // when no other scan is in flight: the end of a run, where nothing else needs the cores)
   void Run(size_t n, int threads, const std::function<void(size_t)>& fn, bool wide = false) {
     auto job = std::make_shared<PoolJob>();
     job->fn = &fn;
@@ -108,9 +118,10 @@ class HostPool {
     const char* e = std::getenv("TSG_POOL_THREADS");
     int n = e ? std::atoi(e) : PoolBudget();
     if (n < 0) n = 0;
-    // spare workers only wide jobs use (TSG_POOL_SPARE; default none)
+    // spare workers only wide jobs use (TSG_POOL_SPARE; default PoolSpare(), none
+    // when TSG_POOL_THREADS fixes the pool)
     const char* sp = std::getenv("TSG_POOL_SPARE");
-    const int spare = sp ? std::max(0, std::atoi(sp)) : 0;
+    const int spare = sp ? std::max(0, std::atoi(sp)) : e ? 0 : PoolSpare();
     n_steady_ = n;
     n_workers_ = n + spare;
     n = n_workers_;
