@@ -1532,9 +1532,11 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
              gpu_windows);
   };
   // no other scan in flight (the end of a run): the pool's spare workers join in,
-  // the last scan's exact pass being all that is left (TSG_DRAIN_WIDE=0: never)
+  // the last scan's exact pass being all that is left (TSG_DRAIN_WIDE=0: never;
+  // TSG_TAIL_WIDE=1: every exact pass)
   static const bool drain_wide = !std::getenv("TSG_DRAIN_WIDE") || std::atoi(std::getenv("TSG_DRAIN_WIDE")) != 0;
-  const bool wide = drain_wide && active_scans_.load() <= 1;
+  static const bool tail_wide = std::getenv("TSG_TAIL_WIDE") && std::atoi(std::getenv("TSG_TAIL_WIDE")) != 0;
+  const bool wide = tail_wide || (drain_wide && active_scans_.load() <= 1);
   ParallelFor(n_items, host_threads_, [&](size_t it) {
     if (it < top) {
       scan_group(order[it]);
