@@ -1318,6 +1318,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     }
   }
   HostTail(tin, &cands, out, &hs, &allowed, true);
+  if (gst && gst->ms_total > 0) host_bound_.store(hs.ms_exact > 1.5 * double(gst->ms_total));
   hs.ms_allow = ms_allow;  // overlapped with the GPU phase
   hs.ms_gpu = t1 - t0;
   hs.ms_total = NowMs() - t0;
@@ -1536,7 +1537,10 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   // TSG_TAIL_WIDE=1: every exact pass)
   static const bool drain_wide = !std::getenv("TSG_DRAIN_WIDE") || std::atoi(std::getenv("TSG_DRAIN_WIDE")) != 0;
   static const bool tail_wide = std::getenv("TSG_TAIL_WIDE") && std::atoi(std::getenv("TSG_TAIL_WIDE")) != 0;
-  const bool wide = tail_wide || (drain_wide && active_scans_.load() <= 1);
+  // host-bound batches (the last exact pass outlasted 1.5x its GPU phase, e.g.
+  // finding-dense C3f: 40 vs 9 ms) take them too (TSG_TAIL_ADAPT=0: never)
+  static const bool adapt = !std::getenv("TSG_TAIL_ADAPT") || std::atoi(std::getenv("TSG_TAIL_ADAPT")) != 0;
+  const bool wide = tail_wide || (drain_wide && active_scans_.load() <= 1) || (adapt && host_bound_.load());
   ParallelFor(n_items, host_threads_, [&](size_t it) {
     if (it < top) {
       scan_group(order[it]);

@@ -271,7 +271,8 @@ class SecretScanner {
   std::vector<std::unique_ptr<GpuEngine>> engines_;
   std::unique_ptr<std::mutex[]> gpu_mu_;
   std::atomic<uint32_t> next_slot_{0};
-  std::atomic<int> active_scans_{0};  // Scan calls in progress: alone, the exact pass may take the pool's spare workers
+  std::atomic<int> active_scans_{0};
+  std::atomic<bool> host_bound_{false};  // the last scan's exact pass outlasted 1.5x its GPU phase  // Scan calls in progress: alone, the exact pass may take the pool's spare workers
   std::string err_;
   int host_threads_ = 0;
   bool compiled_ok_ = false;
