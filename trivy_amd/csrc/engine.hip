@@ -1252,6 +1252,7 @@ struct FoldParams {
   // global tables: test position 0 against the item's first-byte set (one more
   // dependent global load per start; without it the position loop rejects)
   uint32_t check_first;
+  uint32_t diag;  // TSG_DIAG_FOLD (timing only, findings wrong): 1 skips sites with another rune before, 2 the others
 };
 
 constexpr int kFoldSpan = 3 * 48;  // an item (<= 48 positions, <= 3 bytes each) starts at most this far back
@@ -1325,6 +1326,8 @@ void fold_kernel(FoldParams P) {
         other = true;
     }
     other = __ballot(other) != 0;
+    if ((P.diag & 1u) && other) continue;
+    if ((P.diag & 2u) && !other) continue;
     // one start: item `ix` beginning `back` bytes before the rune, matched fold-tolerantly
     auto try_start = [&](uint32_t ix, uint32_t back) {
       if (fsite.x < w0 + back) return;
@@ -3210,6 +3213,8 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   fo.stage_items = fold_stage_ ? 1u : 0u;
   fo.n_classes = n_fclasses_;
   fo.check_first = fold_check_first_ ? 1u : 0u;
+  static const uint32_t fold_diag = std::getenv("TSG_DIAG_FOLD") ? uint32_t(std::atoi(std::getenv("TSG_DIAG_FOLD"))) : 0u;
+  fo.diag = fold_diag;
   fo.pairs = static_cast<const FoldPair*>(d_fold_pairs_);
   fo.first = static_cast<const uint32_t*>(d_fold_first_);
   fo.n_pairs_k = n_fold_pairs_k_;
