@@ -1260,9 +1260,11 @@ constexpr int kFoldIdxQ = 64;      // capable positions q < kFoldIdxQ go through
 constexpr int kFoldWin = 2 * kFoldSpan + 16;
 constexpr int kFoldWaves = 4;
 
-// One wave per fold site (no workgroup barriers): the bytes [x - kFoldSpan,
-// x + kFoldSpan) go to the wave's LDS window, the lanes split the tasks.  With
-// kLdsTabs the item tables and the position-0 byte sets are staged in LDS.
+// One wave per fold site: the bytes [x - kFoldSpan, x + kFoldSpan) go to the
+// wave's LDS window, the lanes split the tasks; a site with another fold rune
+// before it (start-range tasks over every item) is handed to the whole
+// workgroup (below).  With kLdsTabs the item tables and the position-0 byte
+// sets are staged in LDS.
 // U+0130 sites only flag the file (Go's (?i) does not fold U+0130 onto 'i').
 // kWaves waves per workgroup: 16 when the items and classes are staged (~50 KB of
 // LDS: three 4-wave workgroups per CU left 12 waves to hide the global loads)
@@ -1305,120 +1307,173 @@ void fold_kernel(FoldParams P) {
                                    : reinterpret_cast<const uint32_t*>(tabs + P.t_classes);
   auto in_cls = [&](uint32_t c, uint32_t b) { return (classes[c * 8 + (b >> 5)] >> (b & 31)) & 1u; };
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t* wb = s_win[wave];
+  struct SiteCtx {
+    uint64_t x, w0, w1, fs;  // the rune, its window [w0, w1), the file start
+    uint32_t f;
+    const uint8_t* wb;       // the window's bytes in LDS
+  };
+  // one start: item `ix` beginning `back` bytes before the rune, matched fold-tolerantly
+  auto try_start = [&](const SiteCtx& S, uint32_t ix, uint32_t back) {
+    if (S.x < S.w0 + back) return;
+    const FilterItemGpu it = items[ix];
+    const uint32_t* first = firsts + 8ull * ix;
+    const uint64_t st = S.x - back;
+    const uint32_t b0 = S.wb[st - S.w0];
+    if ((kLdsTabs || P.check_first) && !((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
+    uint64_t p = st, lit_bytes_end = 0;
+    bool ok = true, covered = false;
+    // the first positions' class ids up front: independent loads instead of
+    // one dependent round trip per position (global tables)
+    constexpr uint32_t kPre = 6;
+    uint32_t pre[kPre];
+#pragma unroll
+    for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
+    for (uint32_t q = 0; q < it.n && ok; q++) {
+      if (q == it.lit_end) lit_bytes_end = p;
+      if (p >= S.w1) {
+        ok = false;
+        break;
+      }
+      covered = covered || p == S.x;
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kPre; k++)
+        if (q == k) c = pre[k];
+      if (q >= kPre) c = item_cls[it.cls_off + q];
+      const uint32_t b = S.wb[p - S.w0];
+      if (b == 0xE2 && p + 2 < S.w1 && S.wb[p + 1 - S.w0] == 0x84 && S.wb[p + 2 - S.w0] == 0xAA &&
+          (in_cls(c, 'k') || in_cls(c, 'K'))) {
+        p += 3;
+      } else if (b == 0xC5 && p + 1 < S.w1 && S.wb[p + 1 - S.w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
+        p += 2;
+      } else if (in_cls(c, b)) {
+        p += 1;
+      } else {
+        ok = false;
+      }
+    }
+    if (!ok || !covered) return;
+    if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
+    for (uint32_t d = 0; d < it.n_ids; d++)
+      put_hit(P.hits, P.hit_cap, P.counters, S.f, lit_bytes_end - S.fs, item_ids[it.ids_off + d]);
+  };
+  // A site with another fold rune before it tries every start range of every
+  // item (thousands of tasks of up to 12 starts: C3 ~1.3 ms of the kernel's 1.7
+  // were the few waves holding such sites, TSG_DIAG_FOLD): those sites go to
+  // the whole workgroup, the others stay one per wave.  The workgroup walks its
+  // sites kWaves at a time, in step, so the barriers below are uniform.
+  __shared__ uint64_t s_site[kWaves][4];  // x, w0, w1, fs of a wave's cooperative site
+  __shared__ uint32_t s_coop[kWaves];     // per wave: 0, or 1 | (U+212A ? 2 : 0) for a cooperative site
+  __shared__ uint32_t s_coop_f[kWaves];   // its file
   const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
-  for (uint32_t si = blockIdx.x * kWaves + wave; si < n_folds; si += gridDim.x * kWaves) {
-    const FoldSite fsite = P.folds[si];
-    const uint64_t fs = P.off[fsite.f], fe = P.off[fsite.f + 1];
-    const uint64_t w0 = fsite.x > fs + kFoldSpan ? fsite.x - kFoldSpan : fs;
-    const uint64_t w1 = fsite.x + kFoldSpan < fe ? fsite.x + kFoldSpan : fe;  // window [w0, w1)
-    wave_sync();
-    for (uint32_t i = lane; i < uint32_t(w1 - w0); i += 64) wb[i] = P.arena[w0 + i];
-    wave_sync();
-    const uint32_t lead = wb[fsite.x - w0];
-    if (lead == 0xC4) continue;  // U+0130: uniform per wave
-    const bool kay = lead == 0xE2;  // U+212A, else U+017F
-    bool other = false;  // another foldable rune before x (then starts are not x - q)
-    for (uint64_t p = w0 + lane; p < fsite.x; p += 64) {
-      const uint32_t b = wb[p - w0];
-      if ((b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA) ||
-          (b == 0xC5 && p + 1 < w1 && wb[p + 1 - w0] == 0xBF))
-        other = true;
-    }
-    other = __ballot(other) != 0;
-    if ((P.diag & 1u) && other) continue;
-    if ((P.diag & 2u) && !other) continue;
-    // one start: item `ix` beginning `back` bytes before the rune, matched fold-tolerantly
-    auto try_start = [&](uint32_t ix, uint32_t back) {
-      if (fsite.x < w0 + back) return;
-      const FilterItemGpu it = items[ix];
-      const uint32_t* first = firsts + 8ull * ix;
-      const uint64_t st = fsite.x - back;
-      const uint32_t b0 = wb[st - w0];
-      if ((kLdsTabs || P.check_first) && !((first[b0 >> 5] >> (b0 & 31)) & 1u)) return;  // position 0 fails (superset test)
-      uint64_t p = st, lit_bytes_end = 0;
-      bool ok = true, covered = false;
-      // the first positions' class ids up front: independent loads instead of
-      // one dependent round trip per position (global tables)
-      constexpr uint32_t kPre = 6;
-      uint32_t pre[kPre];
-#pragma unroll
-      for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
-      for (uint32_t q = 0; q < it.n && ok; q++) {
-        if (q == it.lit_end) lit_bytes_end = p;
-        if (p >= w1) {
-          ok = false;
-          break;
-        }
-        covered = covered || p == fsite.x;
-        uint32_t c = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kPre; k++)
-          if (q == k) c = pre[k];
-        if (q >= kPre) c = item_cls[it.cls_off + q];
-        const uint32_t b = wb[p - w0];
-        if (b == 0xE2 && p + 2 < w1 && wb[p + 1 - w0] == 0x84 && wb[p + 2 - w0] == 0xAA &&
-            (in_cls(c, 'k') || in_cls(c, 'K'))) {
-          p += 3;
-        } else if (b == 0xC5 && p + 1 < w1 && wb[p + 1 - w0] == 0xBF && (in_cls(c, 's') || in_cls(c, 'S'))) {
-          p += 2;
-        } else if (in_cls(c, b)) {
-          p += 1;
-        } else {
-          ok = false;
-        }
-      }
-      if (!ok || !covered) return;
-      if (it.lit_end >= it.n) lit_bytes_end = p + (it.lit_end - it.n);  // literal longer than the checked part
-      for (uint32_t d = 0; d < it.n_ids; d++)
-        put_hit(P.hits, P.hit_cap, P.counters, fsite.f, lit_bytes_end - fs, item_ids[it.ids_off + d]);
-    };
-    const FoldPair* pairs = P.pairs + (other ? (kay ? 0 : P.n_pairs_k)
-                                             : P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k));
-    const uint32_t n_pairs = other ? (kay ? P.n_pairs_k : P.n_pairs_s) : (kay ? P.n_cap_k : P.n_cap_s);
-    if (!other && P.use_idx) {
-      // indexed capable tasks: lane q looks up its list by the key byte, a
-      // wave prefix sum spreads the lists' tasks over the lanes
-      const uint32_t q = lane;
-      const uint32_t rl = kay ? 3u : 2u;
-      uint32_t key = 256;
-      if (q == 0) key = fsite.x + rl < w1 ? wb[fsite.x + rl - w0] : 256u;
-      else if (fsite.x >= w0 + q) key = wb[fsite.x - q - w0];
-      uint32_t lo = 0, cnt = 0;
-      if (key < 256) {
-        const uint32_t* o = P.idx_off + (size_t(kay ? 0 : 1) * kFoldIdxQ + q) * 257 + key;
-        lo = o[0];
-        cnt = o[1] - lo;
-      }
-      uint32_t incl = cnt;  // inclusive prefix over the lanes
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t v = __shfl_up(incl, d);
-        if (lane >= uint32_t(d)) incl += v;
-      }
-      const uint32_t total = __shfl(incl, 63);
-      uint32_t* ex = s_idx[wave][0];
-      uint32_t* lw = s_idx[wave][1];
+  for (uint32_t base = blockIdx.x * kWaves; base < n_folds; base += gridDim.x * kWaves) {
+    const uint32_t si = base + wave;
+    uint32_t coop = 0;  // wave-uniform
+    if (si < n_folds) {
+      const FoldSite fsite = P.folds[si];
+      SiteCtx S;
+      S.x = fsite.x;
+      S.f = fsite.f;
+      S.fs = P.off[fsite.f];
+      const uint64_t fe = P.off[fsite.f + 1];
+      S.w0 = fsite.x > S.fs + kFoldSpan ? fsite.x - kFoldSpan : S.fs;
+      S.w1 = fsite.x + kFoldSpan < fe ? fsite.x + kFoldSpan : fe;  // window [w0, w1)
+      uint8_t* wb = s_win[wave];
+      S.wb = wb;
+      for (uint32_t i = lane; i < uint32_t(S.w1 - S.w0); i += 64) wb[i] = P.arena[S.w0 + i];
       wave_sync();
-      ex[lane] = incl - cnt;
-      lw[lane] = lo;
-      wave_sync();
-      for (uint32_t t = lane; t < total; t += 64) {
-        uint32_t a = 0, b = 63;  // the lane (q) whose range holds t: the largest with ex[q] <= t
-        while (a < b) {
-          const uint32_t m = (a + b + 1) >> 1;
-          if (ex[m] <= t) a = m;
-          else b = m - 1;
+      const uint32_t lead = wb[S.x - S.w0];
+      if (lead != 0xC4) {  // U+0130 sites only flag the file (uniform per wave)
+        const bool kay = lead == 0xE2;  // U+212A, else U+017F
+        bool other = false;  // another foldable rune before x (then starts are not x - q)
+        for (uint64_t p = S.w0 + lane; p < S.x; p += 64) {
+          const uint32_t b = wb[p - S.w0];
+          if ((b == 0xE2 && p + 2 < S.w1 && wb[p + 1 - S.w0] == 0x84 && wb[p + 2 - S.w0] == 0xAA) ||
+              (b == 0xC5 && p + 1 < S.w1 && wb[p + 1 - S.w0] == 0xBF))
+            other = true;
         }
-        try_start(P.idx_items[lw[a] + (t - ex[a])], a);
+        other = __ballot(other) != 0;
+        const bool skip = ((P.diag & 1u) && other) || ((P.diag & 2u) && !other);
+        if (other && !skip) {
+          coop = 1u | (kay ? 2u : 0u);
+          if (lane == 0) {
+            s_site[wave][0] = S.x;
+            s_site[wave][1] = S.w0;
+            s_site[wave][2] = S.w1;
+            s_site[wave][3] = S.fs;
+            s_coop_f[wave] = S.f;
+          }
+        } else if (!skip) {
+          const FoldPair* pairs = P.pairs + P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k);
+          const uint32_t n_pairs = kay ? P.n_cap_k : P.n_cap_s;
+          if (P.use_idx) {
+            // indexed capable tasks: lane q looks up its list by the key byte, a
+            // wave prefix sum spreads the lists' tasks over the lanes
+            const uint32_t q = lane;
+            const uint32_t rl = kay ? 3u : 2u;
+            uint32_t key = 256;
+            if (q == 0) key = S.x + rl < S.w1 ? wb[S.x + rl - S.w0] : 256u;
+            else if (S.x >= S.w0 + q) key = wb[S.x - q - S.w0];
+            uint32_t lo = 0, cnt = 0;
+            if (key < 256) {
+              const uint32_t* o = P.idx_off + (size_t(kay ? 0 : 1) * kFoldIdxQ + q) * 257 + key;
+              lo = o[0];
+              cnt = o[1] - lo;
+            }
+            uint32_t incl = cnt;  // inclusive prefix over the lanes
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+              const uint32_t v = __shfl_up(incl, d);
+              if (lane >= uint32_t(d)) incl += v;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            uint32_t* ex = s_idx[wave][0];
+            uint32_t* lw = s_idx[wave][1];
+            wave_sync();
+            ex[lane] = incl - cnt;
+            lw[lane] = lo;
+            wave_sync();
+            for (uint32_t t = lane; t < total; t += 64) {
+              uint32_t a = 0, b = 63;  // the lane (q) whose range holds t: the largest with ex[q] <= t
+              while (a < b) {
+                const uint32_t m = (a + b + 1) >> 1;
+                if (ex[m] <= t) a = m;
+                else b = m - 1;
+              }
+              try_start(S, P.idx_items[lw[a] + (t - ex[a])], a);
+            }
+            // tasks outside the index (q >= kFoldIdxQ or single-position items) follow in the pair list
+          }
+          const uint32_t t0 = P.use_idx ? (kay ? P.n_cap_k_idx : P.n_cap_s_idx) : 0u;
+          for (uint32_t t = t0 + lane; t < n_pairs; t += 64) {
+            const FoldPair fp = pairs[t];
+            for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(S, fp.item, back);
+          }
+        }
       }
-      // tasks outside the index (q >= kFoldIdxQ or single-position items) follow in the pair list
     }
-    const uint32_t t0 = (!other && P.use_idx) ? (kay ? P.n_cap_k_idx : P.n_cap_s_idx) : 0u;
-    for (uint32_t t = t0 + lane; t < n_pairs; t += 64) {
-      const FoldPair fp = pairs[t];
-      for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(fp.item, back);
+    if (lane == 0) s_coop[wave] = coop;
+    __syncthreads();
+    // the workgroup's cooperative sites, one after another, their range tasks over every thread
+    for (uint32_t w2 = 0; w2 < uint32_t(kWaves); w2++) {
+      const uint32_t c = s_coop[w2];
+      if (!c) continue;  // uniform: every thread reads the same word
+      SiteCtx S;
+      S.x = s_site[w2][0];
+      S.w0 = s_site[w2][1];
+      S.w1 = s_site[w2][2];
+      S.fs = s_site[w2][3];
+      S.f = s_coop_f[w2];
+      S.wb = s_win[w2];
+      const bool kay = (c & 2u) != 0;
+      const FoldPair* pairs = P.pairs + (kay ? 0 : P.n_pairs_k);
+      const uint32_t n_pairs = kay ? P.n_pairs_k : P.n_pairs_s;
+      for (uint32_t t = threadIdx.x; t < n_pairs; t += blockDim.x) {
+        const FoldPair fp = pairs[t];
+        for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(S, fp.item, back);
+      }
     }
+    __syncthreads();  // the windows are refilled by the next round
   }
 }
 
