@@ -419,6 +419,7 @@ struct NfaParams {
   uint32_t n_fullscan_rules;
   uint32_t fs_chunk;       // full-scan chunk bytes per lane (min; files of > 64 chunks use larger ones)
   uint32_t kw_fold;        // kwfold_kernel ran: with no fold-site overflow the keyword bits are exact in every file
+  uint32_t diag;           // TSG_DIAG_VERIFY (timing only): 1 verifies only 1-word NFAs' hits, 2 only the wider ones
 };
 
 // The keyword bits of file f may miss occurrences through U+0130 / U+212A
@@ -1601,6 +1602,7 @@ __global__ __launch_bounds__(256, 6) void verify_hits_kernel(NfaParams P) {
     hit_unpack(P.hits + 3ull * i, &f, &end, &aid);
     const AnchorInfo a = P.anchors[aid];
     const RuleGpu rg = P.rules[a.rule];  // keyword gates are evaluated lazily by the host tail
+    if (((P.diag & 1u) && rg.nfa_words > 1) || ((P.diag & 2u) && rg.nfa_words <= 1)) continue;
     const uint32_t ff = P.flags[f];
     // A closed ASCII keyword gate in a file without U+0130 / U+212A is exactly
     // MatchKeywords == false (scanner.go:409): the host would drop every match
@@ -3333,6 +3335,8 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   np.hits = static_cast<const uint32_t*>(d_hits_);
   np.hit_cap = hit_cap_;
   np.counters = d_counters_;
+  static const uint32_t verify_diag = std::getenv("TSG_DIAG_VERIFY") ? uint32_t(std::atoi(std::getenv("TSG_DIAG_VERIFY"))) : 0u;
+  np.diag = verify_diag;
   np.cands = static_cast<Candidate*>(d_cands_);
   np.cand_cap = cand_cap_;
   np.fullscan_rules = d_fullscan_rules_;
