@@ -904,49 +904,15 @@ __global__ __launch_bounds__(ConfirmThreads<kLdsTabs>(), TSG_C_MINW) void confir
 #pragma unroll
     for (uint32_t q = 0; q < kPre; q++) pre[q] = q < it.n ? item_cls[it.cls_off + q] : 0u;
     auto sets_ok = [&](uint32_t q0, uint32_t q1) {
-      // global tables (large rule sets): positions past the lane's window read 16
-      // arena bytes per aligned load (an item's lookahead run, e.g. [a-z0-9]{32,48},
-      // was one dependent byte load per position) and the class ids likewise (the
-      // arena is readable 64 B past its end; item_cls is 16-B aligned and padded
-      // in the table blob)
-      uint4 bytes = make_uint4(0, 0, 0, 0), ids = make_uint4(0, 0, 0, 0);
-      uint64_t bytes_at = ~uint64_t(0);
-      uint32_t ids_at = ~0u;
-      auto byte_of = [](const uint4& v, uint32_t i) {
-        const uint32_t w = (i >> 2) == 0 ? v.x : (i >> 2) == 1 ? v.y : (i >> 2) == 2 ? v.z : v.w;
-        return (w >> (8 * (i & 3u))) & 255u;
-      };
       for (uint32_t q = q0; q < q1; q++) {
         if (q >= core_lo && q < it.back) continue;
         const uint64_t pos = uint64_t(start) + q;
-        uint32_t bt;
-        if (pos - cw0 < uint64_t(kCWin)) {
-          bt = cwin[pos - cw0];
-        } else if (kLdsTabs) {  // builtin-sized items: a few positions past the window
-          bt = P.arena[pos];
-        } else {
-          if ((pos >> 4) != bytes_at) {
-            bytes_at = pos >> 4;
-            bytes = load16(P.arena + (pos & ~uint64_t(15)));
-          }
-          bt = byte_of(bytes, uint32_t(pos & 15));
-        }
+        const uint32_t bt = pos - cw0 < uint64_t(kCWin) ? uint32_t(cwin[pos - cw0]) : uint32_t(P.arena[pos]);
         uint32_t c = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kPre; k++)
           if (q == k) c = pre[k];
-        if (q >= kPre) {
-          const uint32_t ci = it.cls_off + q;
-          if (kLdsTabs) {
-            c = item_cls[ci];
-          } else {
-            if ((ci >> 4) != ids_at) {
-              ids_at = ci >> 4;
-              ids = *reinterpret_cast<const uint4*>(item_cls + (ci & ~15u));
-            }
-            c = byte_of(ids, ci & 15u);
-          }
-        }
+        if (q >= kPre) c = item_cls[it.cls_off + q];
         if (!((classes[c * 8 + (bt >> 5)] >> (bt & 31)) & 1u)) return false;
       }
       return true;
