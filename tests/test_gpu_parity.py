@@ -273,6 +273,34 @@ def test_fold_runes_in_custom_rule_items(secret, tmp_path):
     assert _compare_corpus(secret, files, str(cfg)) > 100
 
 
+def test_fold_runes_dense_with_a_large_rule_set(secret, tmp_path):
+    """The global-table fold kernel (2,000 generated rules + custom fold-rune rules): files dense in
+    U+212A / U+017F so most fold sites have another rune before them -- the sites the kernel hands
+    to the whole workgroup -- mixed with ordinary ones, vs the oracle."""
+    from trivy_amd import corpus
+    y, samples = corpus.c3_rules()
+    extra = (
+        "  - id: kw-assign\n    category: Custom\n    title: KW\n    severity: HIGH\n"
+        "    regex: '(?i)(?P<key>kwsk01[a-z0-9_ .\\-,]{0,25})(=|:=|:).{0,5}[''\"](?P<secret>[a-z0-9]{16})[''\"]'\n"
+        "    secret-group-name: secret\n    keywords: [kwsk01]\n"
+        "  - id: ci-token\n    category: Custom\n    title: CI\n    severity: LOW\n"
+        "    regex: '(?i)sks_[a-z]{6}'\n")
+    assert y.startswith("rules:\n")
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text("rules:\n" + extra + y[len("rules:\n"):])
+    K, S = "\u212a", "\u017f"
+    bodies = ["kwsk01 = '0123456789abcdef'", K + "wsk01 = 'abcdefabcdef0123'", "kw" + S + "k01: \"0123456789abcdef\"",
+              S + "ks_abcdef", "s" + K + "s_ABCDEF", K * 3 + " " + S * 5 + " " + K + "wsk01='aaaaaaaaaaaaaaaa'"]
+    bodies += [smp.decode() for smp in samples[:20]]
+    rng = random.Random(11)
+    files = []
+    for i in range(24):
+        parts = [rng.choice(bodies) for _ in range(rng.randint(2, 6))]
+        sep = "\n" + (K + S) * rng.randint(0, 3) + " "
+        files.append(("d%02d.txt" % i, sep.join(parts).encode()))
+    assert _compare_corpus(secret, files, str(cfg)) > 20
+
+
 def test_host_batches_stream_in_chunks(secret, monkeypatch):
     """Host-resident batches (RunHost) streamed through the staging ring in many chunks
     (TSG_INGEST_CHUNK_MB), pipelined submissions included, give the device-resident
