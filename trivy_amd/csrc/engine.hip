@@ -1269,6 +1269,9 @@ constexpr int kFoldWaves = 4;
 // U+0130 sites only flag the file (Go's (?i) does not fold U+0130 onto 'i').
 // kWaves waves per workgroup: 16 when the items and classes are staged (~50 KB of
 // LDS: three 4-wave workgroups per CU left 12 waves to hide the global loads)
+#ifndef TSG_FOLD_COOP_TASKS
+#define TSG_FOLD_COOP_TASKS 512  // a site with more capable tasks than this goes to the whole workgroup
+#endif
 #ifndef TSG_FOLD_WIDE_WPE
 #define TSG_FOLD_WIDE_WPE 8  // waves per SIMD asked of the 16-wave variant: 8 = two workgroups per CU (64 VGPRs)
 #endif
@@ -1364,8 +1367,9 @@ void fold_kernel(FoldParams P) {
   // the whole workgroup, the others stay one per wave.  The workgroup walks its
   // sites kWaves at a time, in step, so the barriers below are uniform.
   __shared__ uint64_t s_site[kWaves][4];  // x, w0, w1, fs of a wave's cooperative site
-  __shared__ uint32_t s_coop[kWaves];     // per wave: 0, or 1 | (U+212A ? 2 : 0) for a cooperative site
+  __shared__ uint32_t s_coop[kWaves];     // per wave: 0, or 1 | (U+212A ? 2 : 0) | (capable tasks ? 4 : 0) for a cooperative site
   __shared__ uint32_t s_coop_f[kWaves];   // its file
+  __shared__ uint32_t s_total[kWaves];    // a heavy capable-task site's indexed task count (| 4 in s_coop)
   const uint32_t n_folds = P.counters[9] < P.fold_cap ? P.counters[9] : P.fold_cap;
   for (uint32_t base = blockIdx.x * kWaves; base < n_folds; base += gridDim.x * kWaves) {
     const uint32_t si = base + wave;
@@ -1407,6 +1411,9 @@ void fold_kernel(FoldParams P) {
         } else if (!skip) {
           const FoldPair* pairs = P.pairs + P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k);
           const uint32_t n_pairs = kay ? P.n_cap_k : P.n_cap_s;
+          uint32_t total = 0;  // indexed capable tasks
+          uint32_t* ex = s_idx[wave][0];
+          uint32_t* lw = s_idx[wave][1];
           if (P.use_idx) {
             // indexed capable tasks: lane q looks up its list by the key byte, a
             // wave prefix sum spreads the lists' tasks over the lanes
@@ -1427,13 +1434,26 @@ void fold_kernel(FoldParams P) {
               const uint32_t v = __shfl_up(incl, d);
               if (lane >= uint32_t(d)) incl += v;
             }
-            const uint32_t total = __shfl(incl, 63);
-            uint32_t* ex = s_idx[wave][0];
-            uint32_t* lw = s_idx[wave][1];
+            total = __shfl(incl, 63);
             wave_sync();
             ex[lane] = incl - cnt;
             lw[lane] = lo;
             wave_sync();
+          }
+          // tasks outside the index (q >= kFoldIdxQ or single-position items) follow in the pair list
+          const uint32_t t0 = P.use_idx ? (kay ? P.n_cap_k_idx : P.n_cap_s_idx) : 0u;
+          if (total + (n_pairs > t0 ? n_pairs - t0 : 0u) > uint32_t(TSG_FOLD_COOP_TASKS)) {
+            // a heavy site (many items take the rune's byte context): the workgroup's too
+            coop = 1u | (kay ? 2u : 0u) | 4u;
+            if (lane == 0) {
+              s_site[wave][0] = S.x;
+              s_site[wave][1] = S.w0;
+              s_site[wave][2] = S.w1;
+              s_site[wave][3] = S.fs;
+              s_coop_f[wave] = S.f;
+              s_total[wave] = total;
+            }
+          } else {
             for (uint32_t t = lane; t < total; t += 64) {
               uint32_t a = 0, b = 63;  // the lane (q) whose range holds t: the largest with ex[q] <= t
               while (a < b) {
@@ -1443,12 +1463,10 @@ void fold_kernel(FoldParams P) {
               }
               try_start(S, P.idx_items[lw[a] + (t - ex[a])], a);
             }
-            // tasks outside the index (q >= kFoldIdxQ or single-position items) follow in the pair list
-          }
-          const uint32_t t0 = P.use_idx ? (kay ? P.n_cap_k_idx : P.n_cap_s_idx) : 0u;
-          for (uint32_t t = t0 + lane; t < n_pairs; t += 64) {
-            const FoldPair fp = pairs[t];
-            for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(S, fp.item, back);
+            for (uint32_t t = t0 + lane; t < n_pairs; t += 64) {
+              const FoldPair fp = pairs[t];
+              for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(S, fp.item, back);
+            }
           }
         }
       }
@@ -1467,6 +1485,28 @@ void fold_kernel(FoldParams P) {
       S.f = s_coop_f[w2];
       S.wb = s_win[w2];
       const bool kay = (c & 2u) != 0;
+      if (c & 4u) {  // a heavy capable-task site: its index lists (the owner wave's s_idx), then the pair list
+        const uint32_t total = s_total[w2];
+        const uint32_t* ex = s_idx[w2][0];
+        const uint32_t* lw = s_idx[w2][1];
+        for (uint32_t t = threadIdx.x; t < total; t += blockDim.x) {
+          uint32_t a = 0, b = 63;
+          while (a < b) {
+            const uint32_t m = (a + b + 1) >> 1;
+            if (ex[m] <= t) a = m;
+            else b = m - 1;
+          }
+          try_start(S, P.idx_items[lw[a] + (t - ex[a])], a);
+        }
+        const FoldPair* pairs = P.pairs + P.n_pairs_k + P.n_pairs_s + (kay ? 0 : P.n_cap_k);
+        const uint32_t n_pairs = kay ? P.n_cap_k : P.n_cap_s;
+        const uint32_t t0 = P.use_idx ? (kay ? P.n_cap_k_idx : P.n_cap_s_idx) : 0u;
+        for (uint32_t t = t0 + threadIdx.x; t < n_pairs; t += blockDim.x) {
+          const FoldPair fp = pairs[t];
+          for (uint32_t back = fp.lo; back <= fp.hi; back++) try_start(S, fp.item, back);
+        }
+        continue;
+      }
       const FoldPair* pairs = P.pairs + (kay ? 0 : P.n_pairs_k);
       const uint32_t n_pairs = kay ? P.n_pairs_k : P.n_pairs_s;
       for (uint32_t t = threadIdx.x; t < n_pairs; t += blockDim.x) {
