@@ -1317,8 +1317,13 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
       std::fclose(fp);
     }
   }
+  const double t_tail = NowMs();
   HostTail(tin, &cands, out, &hs, &allowed, true);
   if (gst && gst->ms_total > 0) host_bound_.store(hs.ms_exact > 1.5 * double(gst->ms_total));
+  static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;
+  if (times)
+    std::fprintf(stderr, "scan times ms: to candidates %.2f, to the tail %.2f, tail %.2f (%zu candidates)\n", t1 - t0,
+                 t_tail - t1, NowMs() - t_tail, cands.size());
   hs.ms_allow = ms_allow;  // overlapped with the GPU phase
   hs.ms_gpu = t1 - t0;
   hs.ms_total = NowMs() - t0;
@@ -1591,6 +1596,11 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   }
   double t3 = NowMs();
   if (g_tail_debug) std::fprintf(stderr, "tail serial ms: collect %.1f\n", t3 - t_par);
+  static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;  // one line per pass, no per-file timers
+  if (times)
+    std::fprintf(stderr, "tail times ms: kind %.2f group %.2f results %.2f order %.2f parallel %.2f collect %.2f"
+                 " (files %zu, wide %d)\n", t2 - t1, t_grouped - t2, t_sorted - t_grouped, t_ordered - t_sorted,
+                 t_par - t_ordered, t3 - t_par, nf, int(wide));
   GiveScratch(std::move(scr));
   hs->ms_allow = t2 - t1;
   hs->ms_exact = t3 - t2;
