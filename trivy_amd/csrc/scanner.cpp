@@ -1591,15 +1591,27 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     std::fprintf(stderr, "tail whole-content gate scans: %lld calls, %.1f MB; line walks: %.1f MB forward, %.1f MB back"
                  " (%.1f MB inside windows)\n", (long long)g_wholefile_calls.load(), g_wholefile_bytes.load() / 1e6,
                  g_prof[8] / 1e6, (g_prof[9] + g_prof[10]) / 1e6, g_prof[10] / 1e6);
-  out->found_files.reserve(nf);
-  out->found.reserve(nf);
+  // the files with findings, in file order: positions by one pass, then the
+  // findings moved into place in parallel
+  std::vector<uint32_t>& at = scr->order;  // (the dispatch order is no longer needed)
+  at.resize(nf);
+  size_t n_found = 0;
   for (size_t k = 0; k < nf; k++) {
-    if (tmp[k].kind != kHasFindings) continue;
-    const uint32_t f = group_file(k);
-    out->kind[f] = uint8_t(kHasFindings);
-    out->found_files.push_back(f);
-    out->found.push_back(std::move(tmp[k].findings));
+    at[k] = uint32_t(n_found);
+    n_found += tmp[k].kind == kHasFindings;
   }
+  out->found_files.resize(n_found);
+  out->found.allocate(n_found);
+  constexpr size_t kMoveBlock = 2048;
+  ParallelFor((nf + kMoveBlock - 1) / kMoveBlock, host_threads_, [&](size_t blk) {
+    for (size_t k = blk * kMoveBlock, e = std::min(nf, k + kMoveBlock); k < e; k++) {
+      if (tmp[k].kind != kHasFindings) continue;
+      const uint32_t f = group_file(k);
+      out->kind[f] = uint8_t(kHasFindings);
+      out->found_files[at[k]] = f;
+      out->found.emplace(at[k], std::move(tmp[k].findings));
+    }
+  }, wide);
   double t3 = NowMs();
   if (g_tail_debug) std::fprintf(stderr, "tail serial ms: collect %.1f\n", t3 - t_par);
   static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;  // one line per pass, no per-file timers
