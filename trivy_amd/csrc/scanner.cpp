@@ -1458,11 +1458,14 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   {
     std::vector<double>& w = scr->w;
     w.resize(nf);
-    for (size_t k = 0; k < nf; k++) {
-      const uint32_t f = group_file(k);
-      const uint64_t flen = in.file_data ? in.file_len[f] : in.host_offsets[f + 1] - in.host_offsets[f];
-      w[k] = double(starts[k + 1] - starts[k]) * double(flen + 4096);
-    }
+    constexpr size_t kWBlock = 4096;  // (random reads of the file lengths: spread over the pool)
+    ParallelFor((nf + kWBlock - 1) / kWBlock, host_threads_, [&](size_t blk) {
+      for (size_t k = blk * kWBlock, e = std::min(nf, k + kWBlock); k < e; k++) {
+        const uint32_t f = group_file(k);
+        const uint64_t flen = in.file_data ? in.file_len[f] : in.host_offsets[f + 1] - in.host_offsets[f];
+        w[k] = double(starts[k + 1] - starts[k]) * double(flen + 4096);
+      }
+    });
     const size_t top = std::min<size_t>(nf, 1024);  // the LPT head, dispatched one group at a time below
     auto heavier = [&](uint32_t x, uint32_t y) { return w[x] > w[y] || (w[x] == w[y] && x < y); };
     if (top < nf) {
