@@ -223,6 +223,7 @@ class GpuEngine {
   size_t c_lds_bytes_ = 0;
   bool lds_tabs_ = true;  // confirm/fold kernels stage the item tables in LDS
   bool fold_stage_ = false;        // global-table fold kernel: items + classes staged in LDS
+  uint32_t fold_grid_ = 2048;      // workgroups of the LDS-table fold kernel (TSG_FOLD_GRID)
   bool fold_wide_ = false;         // staged global-table fold kernel: 16-wave workgroups (TSG_FOLD_WAVES=4: 4)
   bool fold_check_first_ = true;   // global-table fold kernel: first-byte set test per start (TSG_FOLD_FIRST=0: off)
   bool c_stage_classes_ = false;   // global-table confirm kernel: classes staged in LDS

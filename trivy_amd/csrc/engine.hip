@@ -2516,6 +2516,8 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     fold_stage_ = !lds_tabs_ && fold_stage_bytes_ <= 48 * 1024 && (!fse || std::atoi(fse) != 0);
     const char* ffe = std::getenv("TSG_FOLD_FIRST");
     fold_check_first_ = !ffe || std::atoi(ffe) != 0;  // r05g: without it 3.0-3.7 ms instead of 1.6-2.1
+    // LDS-table fold kernel's grid: every workgroup stages the tables first (TSG_FOLD_GRID)
+    if (const char* fg = std::getenv("TSG_FOLD_GRID")) fold_grid_ = uint32_t(std::max(1, std::atoi(fg)));
     const char* fwe = std::getenv("TSG_FOLD_WAVES");
     fold_wide_ = fold_stage_ && (!fwe || std::atoi(fwe) == 16);
     if (std::getenv("TSG_ENGINE_DEBUG"))
@@ -3330,7 +3332,7 @@ bool GpuEngine::EnqueuePhase(const uint8_t* d_arena, uint64_t n_bytes, const uin
   fo.counters = d_counters_;
   if (diag_mode_ == 0) {
     if (lds_tabs_)
-      fold_kernel<true><<<2048, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
+      fold_kernel<true><<<fold_grid_, 64 * kFoldWaves, ftabs_fold_bytes_ + 32 * n_fitems_, stream_>>>(fo);
     else if (fold_wide_)
       fold_kernel<false, 16><<<2048, 64 * 16, fold_stage_bytes_, stream_>>>(fo);
     else
