@@ -21,6 +21,7 @@
  */
 #ifndef TSG_SCANNER_H
 #define TSG_SCANNER_H
+#include <stddef.h>
 #include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
@@ -88,22 +89,37 @@ typedef struct tsg_batch {
    * required (the exact rule and the results use it). */
   const void* dev_paths;
   const void* dev_path_offsets;
-  /* optional: the FilePath bytes packed in host memory (host_path_offsets:
-   * n_files + 1 u64 into host_paths), as the analyzer's collectors hold them;
-   * without dev_paths the engine copies them to HBM for the same GPU
-   * allow-path prefilter.  (Appended in round 5: a caller built against the
-   * earlier header must zero them.) */
+} tsg_batch;  /* frozen: the layout of round 4; later fields go to tsg_batch_ext */
+
+/* Versioned batch.  struct_size is sizeof(tsg_batch_ext) as the caller was
+ * built: the library reads only the fields that size covers, and refuses a
+ * size it does not know (status <0, tsg_last_error names the sizes it knows),
+ * so a caller built against an older or newer header never has fields read
+ * past the end of its struct.  Known sizes: TSG_BATCH_EXT_SIZE_V1 (112 on
+ * the 64-bit ABI).  The plain tsg_batch entry points read the frozen fields
+ * only (a caller built against the round-4 header passes exactly those). */
+typedef struct tsg_batch_ext {
+  uint32_t struct_size;
+  tsg_batch base;
+  /* v1: the FilePath bytes packed in host memory (host_path_offsets: n_files
+   * + 1 u64 into host_paths), as the analyzer's collectors hold them; without
+   * base.dev_paths the engine copies them to HBM for the same GPU allow-path
+   * prefilter (NULL: the host runs the rules over every path). */
   const uint8_t* host_paths;
   const uint64_t* host_path_offsets;
-} tsg_batch;
+} tsg_batch_ext;
+#define TSG_BATCH_EXT_SIZE_V1 ((uint32_t)(offsetof(tsg_batch_ext, host_path_offsets) + sizeof(const uint64_t*)))
+#define TSG_BATCH_EXT_SIZE TSG_BATCH_EXT_SIZE_V1  /* what this header's callers set */
 
 int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);
+int tsg_scan_ext(tsg_scanner* s, const tsg_batch_ext* batch, tsg_result** out);
 /* Pipelined scanning: tsg_scan on a background thread.  The GPU phases of
  * the scans in flight on one scanner run one after another (one HIP stream);
  * a batch's exact host pass overlaps the next batch's kernels.  The batch's
  * buffers stay borrowed until tsg_scan_wait returns. */
 typedef struct tsg_pending tsg_pending;
 int tsg_scan_submit(tsg_scanner* s, const tsg_batch* batch, tsg_pending** out);
+int tsg_scan_submit_ext(tsg_scanner* s, const tsg_batch_ext* batch, tsg_pending** out);
 int tsg_scan_wait(tsg_pending* p, tsg_result** out); /* frees p */
 void tsg_result_free(tsg_result* r);
 

@@ -17,6 +17,9 @@
 #include <memory>
 #include <string>
 #include <vector>
+#include <thread>
+#include <chrono>
+#include <atomic>
 
 #include "capi_internal.h"
 #include "goregex.h"
@@ -175,6 +178,26 @@ int tsg_cpuref_scan(const tsg_global* g, const tsg_batch* b, int threads, tsg_re
   std::vector<tsg::Candidate> cands;
   for (auto& v : per_file) cands.insert(cands.end(), v.begin(), v.end());
   return Tail(std::move(sc), b, &cands, out);
+}
+
+int tsg_debug_pool_peak(int callers, uint64_t n, int item_us, int wide, int* steady, int* workers) {
+  std::atomic<int> in{0}, peak{0};
+  std::vector<std::thread> ts;
+  for (int k = 0; k < callers; k++)
+    ts.emplace_back([&] {
+      tsg::ParallelFor(size_t(n), 1 << 20, [&](size_t) {
+        const int now = in.fetch_add(1) + 1;
+        int p = peak.load();
+        while (now > p && !peak.compare_exchange_weak(p, now)) {
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(item_us));
+        in.fetch_sub(1);
+      }, wide != 0);
+    });
+  for (auto& t : ts) t.join();
+  *steady = tsg::HostPool::Get().steady();
+  *workers = tsg::HostPool::Get().workers();
+  return peak.load();
 }
 
 }  // extern "C"

@@ -36,6 +36,12 @@ int tsg_debug_scanner_host_only(const tsg_global* g, tsg_scanner** out);
  * the analyzer's --parallel goroutines).  Result: as tsg_scan. */
 int tsg_cpuref_scan(const tsg_global* g, const tsg_batch* b, int threads, tsg_result** out);
 
+/* The host pool (trivy_amd/csrc/parallel.h) under `callers` concurrent
+ * ParallelFor jobs of n items each (each item sleeps `item_us`), all wide or
+ * all ordinary: returns the peak number of threads inside the jobs' bodies at
+ * once, and the pool's steady / total worker counts. */
+int tsg_debug_pool_peak(int callers, uint64_t n, int item_us, int wide, int* steady, int* workers);
+
 #ifdef __cplusplus
 }
 #endif

@@ -518,3 +518,38 @@ def test_allow_paths_gpu_prefilter_vs_oracle(secret, tmp_path, custom):
             assert g.to_dict() == want, path
             n_allowed += int(bool(want.get("FilePath")) and not want.get("Findings"))
         assert n_allowed > 100
+
+
+def test_batch_layouts_round4_and_ext(secret):
+    """The frozen tsg_batch (the round-4 layout, no path fields: tsg_scan) and the versioned
+    tsg_batch_ext with host-packed paths (tsg_scan_ext: the GPU allow-path prefilter over them) give
+    the same results, equal to the oracle's; a bogus struct_size is refused."""
+    import ctypes as c
+    import numpy as np
+    from trivy_amd import _lib
+    from trivy_amd.secret.scanner import _CBatch, _CBatchExt
+    rng = random.Random(11)
+    paths = _allow_paths_batch(rng)[:1500]
+    s = secret.NewScanner(None)
+    o = osc.new_scanner(None)
+    contents = [b"AKIA" + b"Q" * 16 + b"\n" if i % 3 == 0 else b"t=ghp_" + b"a1B2" * 9 + b"\n" for i in range(len(paths))]
+    offs = np.zeros(len(paths) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in contents])
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+    pb = [x.encode() for x in paths]
+    hpaths = np.frombuffer(b"".join(pb) + b"\0" * 16, dtype=np.uint8)
+    hpoffs = np.zeros(len(pb) + 1, dtype=np.uint64)
+    hpoffs[1:] = np.cumsum([len(x) for x in pb])
+    old = s.scan_arena(arena, offs, paths).secrets(paths)
+    ext = s.scan_arena(arena, offs, paths, host_paths=hpaths, host_path_offsets=hpoffs).secrets(paths)
+    n_allowed = 0
+    for path, b, g1, g2 in zip(paths, contents, old, ext):
+        want = o.scan(path, b)
+        assert g1.to_dict() == want, path
+        assert g2.to_dict() == want, path
+        n_allowed += int(bool(want.get("FilePath")) and not want.get("Findings"))
+    assert n_allowed > 50
+    b = _CBatchExt(12345, _CBatch(len(paths), arena.ctypes.data, offs.ctypes.data))
+    h = c.c_void_p()
+    assert s._L.tsg_scan_ext(s._h, c.byref(b), c.byref(h)) < 0
+    assert "struct_size 12345" in _lib.last_error(s._L)

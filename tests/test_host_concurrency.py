@@ -6,7 +6,9 @@ tools/sanitize.sh runs these (and the host-tail / analyzer / allow-path tests)
 against ASan+UBSan and TSan builds of the host library.
 """
 import ctypes as c
+import os
 import threading
+from pathlib import Path
 
 import numpy as np
 
@@ -14,6 +16,8 @@ from oracle import hostlib
 from tests.corpus import make_corpus
 from trivy_amd.secret import NewScanner
 from trivy_amd.secret.scanner import ScanResult, _CBatch, _declare
+
+ROOT = Path(__file__).resolve().parent.parent
 
 
 def _batch(files):
@@ -154,3 +158,25 @@ def test_result_json_range_then_whole():
     whole = r.raw()
     assert len(whole) == len(files) and whole[150:200] == tail
     assert r.raw(0, 10) == whole[:10] and r.raw() == whole
+
+
+def test_pool_spare_workers_take_wide_jobs_only():
+    """Concurrent ordinary ParallelFor jobs (pipelined scans' exact passes, allow-path passes) share the
+    pool's steady workers: at most steady + callers threads run their bodies at once, however many jobs
+    overlap; wide jobs (the walks, the drain) may also use the spare workers.  Run in a fresh process so
+    the pool is built from the env given here."""
+    import subprocess
+    import sys
+    code = ("import ctypes as c\nfrom oracle import hostlib\nL = hostlib.lib()\n"
+            "L.tsg_debug_pool_peak.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int, c.POINTER(c.c_int), "
+            "c.POINTER(c.c_int)]\n"
+            "s, w = c.c_int(), c.c_int()\n"
+            "for wide in (0, 1):\n"
+            "    print(L.tsg_debug_pool_peak(3, 600, 300, wide, c.byref(s), c.byref(w)), s.value, w.value)\n")
+    env = dict(os.environ, TSG_POOL_THREADS="4", TSG_POOL_SPARE="3")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=str(ROOT), check=True, capture_output=True,
+                         text=True, timeout=120).stdout.split("\n")
+    narrow, wide = [list(map(int, l.split())) for l in out[:2]]
+    assert narrow[1:] == [4, 7] and wide[1:] == [4, 7]
+    assert narrow[0] <= 4 + 3, narrow
+    assert wide[0] >= 4 + 3 + 1, wide  # the spare workers did join the wide jobs

@@ -334,3 +334,60 @@ def test_host_tail_dense_findings_line_index(tmp_path):
         assert g.to_dict() == want, p
         n += len(want["Findings"] or [])
     assert n > 600
+
+
+def test_host_tail_file_ids_past_2_pow_22():
+    """Candidates of files whose ids need more than two 11-bit radix digits (>= 2^22, about 4.2 M
+    files in one batch) are still grouped per file: the tail's LSD radix sort runs its passes over the
+    file bits only.  Records shuffled so each file's candidates are interleaved with the others'."""
+    import random
+    key, gh = b"AKIA" + b"Q" * 16, b"ghp_" + b"a1B2" * 9
+    real = [(b"a = 1\nk = " + key + b"\n" + b"t=" + gh + b"\n"),
+            (b"t=" + gh + b"\nzz\nk = " + key + b"\n"),
+            (b"nothing here\n"),
+            (b"k = " + key + b" " + b"x" * 150 + b" t=" + gh + b"\n" + b"k = " + key + b"\n")]
+    ids = [3, (1 << 21) + 5, (1 << 22) - 1, 1 << 22, (1 << 22) + 7, (1 << 23) + 11, (1 << 23) + 12]
+    n_files = (1 << 23) + 64
+    body = {f: real[k % len(real)] for k, f in enumerate(ids)}
+    lens = np.zeros(n_files, dtype=np.uint64)
+    for f, b in body.items():
+        lens[f] = len(b)
+    offs = np.zeros(n_files + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    arena = np.zeros(int(offs[-1]) + 16, dtype=np.uint8)
+    for f, b in body.items():
+        arena[int(offs[f]):int(offs[f]) + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    path = c.create_string_buffer(b"src/x.txt")
+    own = {f: c.create_string_buffer(b"src/f%d.txt" % f) for f in ids}
+    ptrs = np.full(n_files, c.addressof(path), dtype=np.uint64)
+    plen = np.full(n_files, 9, dtype=np.uint64)
+    for f, s in own.items():
+        ptrs[f] = c.addressof(s)
+        plen[f] = len(s.value)
+    L = hostlib.lib()
+    _declare(L)
+    rules, allow, exclude = _assemble(None)
+    cg = CGlobal(rules, allow, exclude)
+    batch = _CBatch(n_files, arena.ctypes.data, offs.ctypes.data, None, None, ptrs.ctypes.data,
+                    plen.ctypes.data, None)
+    files = [(own[f].value.decode(), body[f]) for f in ids]
+    cands = _windowed_candidates(files, len(rules), 40, True)
+    cands["file"] = np.array(ids, dtype=np.uint32)[cands["file"]]
+    cands = cands[np.random.default_rng(5).permutation(len(cands))]
+    h = c.c_void_p()
+    if L.tsg_debug_host_tail_cands(c.byref(cg.g), c.byref(batch), cands.ctypes.data, len(cands), c.byref(h)) != 0:
+        raise RuntimeError(hostlib.last_error())
+    res = ScanResult(_Owner(L), h)
+    o = osc.new_scanner(None)
+    n = 0
+    for (p, b), f in zip(files, ids):
+        want = o.scan(p, b)
+        assert res.secrets([p], lo=f)[0].to_dict() == want, p
+        for g in (f - 1, f + 1):  # the neighbours stay empty
+            if g not in body and g < n_files:
+                assert res.secrets(["src/x.txt"], lo=g)[0].to_dict() == osc.new_scanner(None).scan("src/x.txt", b"")
+        n += len(want["Findings"] or [])
+    rec = res.records()
+    assert len(rec) == n > 10
+    assert np.all(np.diff(rec["file"].astype(np.int64)) >= 0)
+    assert set(rec["file"].tolist()) <= set(ids)

@@ -1132,18 +1132,19 @@ int tsg_collector_set_gpu_transform(tsg_collector* c, int on) {
 
 int tsg_collector_submit(tsg_collector* c, tsg_pending** out) {
   c->BuildPaths();
-  tsg_batch b{};
-  b.n_files = c->files();
-  b.host_arena = c->arena;
-  b.host_offsets = c->offs.data();
-  b.paths = c->path_ptrs.data();
-  b.path_lens = c->path_lens.data();
-  b.binary = c->binary.data();
-  b.transform = c->gpu_xform ? c->kinds.data() : nullptr;
+  tsg_batch_ext b{};
+  b.struct_size = TSG_BATCH_EXT_SIZE;
+  b.base.n_files = c->files();
+  b.base.host_arena = c->arena;
+  b.base.host_offsets = c->offs.data();
+  b.base.paths = c->path_ptrs.data();
+  b.base.path_lens = c->path_lens.data();
+  b.base.binary = c->binary.data();
+  b.base.transform = c->gpu_xform ? c->kinds.data() : nullptr;
   // the paths are packed already: the global allow-path rules are prefiltered on the GPU
   b.host_paths = reinterpret_cast<const uint8_t*>(c->path_pool.data());
   b.host_path_offsets = c->path_off.data();
-  return tsg_scan_submit(const_cast<tsg_scanner*>(c->a->s), &b, out);
+  return tsg_scan_submit_ext(const_cast<tsg_scanner*>(c->a->s), &b, out);
 }
 
 void tsg_collector_reset(tsg_collector* c) { c->Reset(); }

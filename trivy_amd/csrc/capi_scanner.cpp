@@ -218,17 +218,49 @@ struct tsg_pending {
   std::string err;
 };
 
-int tsg_scan_submit(tsg_scanner* s, const tsg_batch* b, tsg_pending** out) {
+namespace {
+
+// tsg_batch_ext sizes this library reads (tsg_scanner.h): the fields past
+// `base` that a caller's struct_size covers
+bool CheckExtSize(const tsg_batch_ext* b) {
+  if (!b) {
+    tsg::SetError("tsg_scan_ext: NULL batch");
+    return false;
+  }
+  if (b->struct_size != TSG_BATCH_EXT_SIZE_V1) {
+    tsg::SetError("tsg_scan_ext: tsg_batch_ext.struct_size " + std::to_string(b->struct_size) +
+                  " is not a size this library knows (v1 = " + std::to_string(TSG_BATCH_EXT_SIZE_V1) + ")");
+    return false;
+  }
+  return true;
+}
+
+int ScanImpl(tsg_scanner* s, const tsg_batch* b, const uint8_t* host_paths, const uint64_t* host_path_off,
+             tsg_result** out);
+
+}  // namespace
+
+int tsg_scan_submit_ext(tsg_scanner* s, const tsg_batch_ext* b, tsg_pending** out) {
+  if (!CheckExtSize(b)) return -1;
   std::unique_ptr<tsg_pending> p(new tsg_pending());
-  const tsg_batch bc = *b;
+  const tsg_batch bc = b->base;
+  const uint8_t* hp = b->host_paths;
+  const uint64_t* hpo = b->host_path_offsets;
   tsg_pending* pp = p.get();
-  pp->th = std::thread([s, bc, pp] {
+  pp->th = std::thread([s, bc, hp, hpo, pp] {
     pthread_setname_np(pthread_self(), "tsg-scan");
-    pp->rc = tsg_scan(s, &bc, &pp->r);
+    pp->rc = ScanImpl(s, &bc, hp, hpo, &pp->r);
     if (pp->rc != 0) pp->err = tsg_last_error();
   });
   *out = p.release();
   return 0;
+}
+
+int tsg_scan_submit(tsg_scanner* s, const tsg_batch* b, tsg_pending** out) {
+  tsg_batch_ext e{};
+  e.struct_size = TSG_BATCH_EXT_SIZE_V1;
+  e.base = *b;  // (the frozen layout only: nothing past it is read)
+  return tsg_scan_submit_ext(s, &e, out);
 }
 
 int tsg_scan_wait(tsg_pending* p, tsg_result** out) {
@@ -241,7 +273,17 @@ int tsg_scan_wait(tsg_pending* p, tsg_result** out) {
   return rc;
 }
 
-int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
+int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) { return ScanImpl(s, b, nullptr, nullptr, out); }
+
+int tsg_scan_ext(tsg_scanner* s, const tsg_batch_ext* b, tsg_result** out) {
+  if (!CheckExtSize(b)) return -1;
+  return ScanImpl(s, &b->base, b->host_paths, b->host_path_offsets, out);
+}
+
+namespace {
+
+int ScanImpl(tsg_scanner* s, const tsg_batch* b, const uint8_t* host_paths, const uint64_t* host_path_off,
+             tsg_result** out) {
   tsg::BatchInput in;
   in.n_files = b->n_files;
   in.host_arena = b->host_arena;
@@ -254,8 +296,8 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   in.transform = b->transform;
   in.dev_paths = static_cast<const uint8_t*>(b->dev_paths);
   in.dev_path_off = static_cast<const uint64_t*>(b->dev_path_offsets);
-  in.host_paths = b->host_paths;
-  in.host_path_off = b->host_path_offsets;
+  in.host_paths = host_paths;
+  in.host_path_off = host_path_off;
   std::unique_ptr<tsg_result> r(new tsg_result());
   r->owner = s->s.get();
   tsg::BatchStats gs;
@@ -296,6 +338,8 @@ int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) {
   *out = r.release();
   return 0;
 }
+
+}  // namespace
 
 void tsg_result_free(tsg_result* r) { ResultReaper::Get().Push(r); }
 

@@ -25,6 +25,7 @@ struct PoolJob {
   const std::function<void(size_t)>* fn = nullptr;
   size_t n = 0;
   int max_helpers = 0;
+  bool wide = false;  // the pool's spare workers may help too
   std::atomic<size_t> next{0};
   std::atomic<size_t> done{0};
   int helpers = 0;  // guarded by the pool mutex
@@ -103,6 +104,7 @@ class HostPool {
     job->fn = &fn;
     job->n = n;
     job->max_helpers = int(std::min<size_t>({size_t(threads - 1), n - 1, size_t(wide ? n_workers_ : n_steady_)}));
+    job->wide = wide;
     if (job->max_helpers > 0 && !workers_.empty()) {
       std::lock_guard<std::mutex> g(mu_);
       q_.push_back(job);
@@ -126,26 +128,42 @@ class HostPool {
     n_workers_ = n + spare;
     n = n_workers_;
     for (int k = 0; k < n; k++) {
-      workers_.emplace_back([this] {
-        pthread_setname_np(pthread_self(), "tsg-pool");
-        Loop();
+      const bool spare_worker = k >= n_steady_;
+      workers_.emplace_back([this, spare_worker] {
+        pthread_setname_np(pthread_self(), spare_worker ? "tsg-pool-spare" : "tsg-pool");
+        Loop(spare_worker);
       });
       workers_.back().detach();
     }
   }
 
-  void Loop() {
+  // A spare worker takes wide jobs only, so ordinary jobs -- however many run at
+  // once (pipelined scans' exact passes, allow-path passes) -- never have more
+  // than n_steady_ pool threads between them besides their callers.
+  void Loop(bool spare_worker) {
     for (;;) {
       std::shared_ptr<PoolJob> job;
       {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
           while (!q_.empty() && q_.front()->next.load() >= q_.front()->n) q_.pop_front();  // all handed out
-          if (!q_.empty()) break;
+          auto it = q_.begin();
+          while (it != q_.end()) {
+            if ((*it)->next.load() >= (*it)->n) {
+              it = q_.erase(it);
+            } else if (spare_worker && !(*it)->wide) {
+              ++it;
+            } else {
+              break;
+            }
+          }
+          if (it != q_.end()) {
+            job = *it;
+            if (++job->helpers >= job->max_helpers) q_.erase(it);
+            break;
+          }
           cv_.wait(lk);
         }
-        job = q_.front();
-        if (++job->helpers >= job->max_helpers) q_.pop_front();
       }
       job->Work();
     }
@@ -156,6 +174,10 @@ class HostPool {
   std::deque<std::shared_ptr<PoolJob>> q_;
   std::vector<std::thread> workers_;
   int n_steady_ = 0, n_workers_ = 0;  // helpers a job may take: ordinary / wide
+
+ public:
+  int steady() const { return n_steady_; }
+  int workers() const { return n_workers_; }
 };
 
 // fn(i) for i in [0, n) on up to `threads` threads (the caller's included),

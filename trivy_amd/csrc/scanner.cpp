@@ -1427,7 +1427,12 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
       max_file = std::max(max_file, cands[i].file);
     }
     constexpr int kDigit = 11;
-    for (int shift = 32; shift == 32 || (max_file >> (shift - 32)) != 0; shift += kDigit) {
+    // passes over the file bits only (32, 43, 54: the key is 64 bits wide), and
+    // only as many as max_file needs; each shift count stays below the width of
+    // what it shifts (a `max_file >> 33` / `key >> 65` wraps on x86 and the extra
+    // pass would sort on candidate-index bits, splitting a file's group)
+    for (int shift = 32; shift < 64; shift += kDigit) {
+      if (shift > 32 && (uint64_t(max_file) >> (shift - 32)) == 0) break;
       uint32_t hist[(1 << kDigit) + 1] = {};
       for (size_t i = 0; i < nc; i++) hist[((key[i] >> shift) & ((1u << kDigit) - 1)) + 1]++;
       for (int d = 0; d < (1 << kDigit); d++) hist[d + 1] += hist[d];
@@ -1528,7 +1533,12 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     const size_t a = starts[k], b = starts[k + 1];
     const uint32_t f = group_file(k);
     tmp[k].kind = kNoFindings;
-    if (allowed[f]) return;
+    if (allowed[f]) {
+      // no stale FileFindings from an earlier pass (its arena belongs to a result
+      // that may be gone) stays behind in the reused scratch
+      tmp[k].findings = FileFindings(nullptr);
+      return;
+    }
     tmp[k].findings = FileFindings(thread_arena());
     thread_local std::vector<Candidate> t_group;  // this group's records, gathered
     t_group.clear();

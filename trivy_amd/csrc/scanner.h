@@ -16,6 +16,7 @@
 #include <string>
 #include <string_view>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "engine.h"
@@ -130,6 +131,11 @@ struct ArenaAlloc {
   template <class U>
   bool operator!=(const ArenaAlloc<U>& o) const { return a != o.a; }
 };
+
+// a FileFindings' elements live in a ResultArena freed whole; the scratch reuse
+// in HostTail move-assigns over old ones without running element destructors
+static_assert(std::is_trivially_destructible<FindingOut>::value && std::is_trivially_destructible<LineOut>::value,
+              "arena-held findings records must be trivially destructible");
 
 struct FileFindings {
   explicit FileFindings(ResultArena* a = nullptr)

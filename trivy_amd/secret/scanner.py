@@ -41,8 +41,15 @@ class _CBatch(c.Structure):
     _fields_ = [("n_files", c.c_uint32), ("host_arena", c.c_void_p), ("host_offsets", c.c_void_p),
                 ("dev_arena", c.c_void_p), ("dev_offsets", c.c_void_p), ("paths", c.c_void_p),
                 ("path_lens", c.c_void_p), ("binary", c.c_void_p), ("transform", c.c_void_p),
-                ("dev_paths", c.c_void_p), ("dev_path_offsets", c.c_void_p),
+                ("dev_paths", c.c_void_p), ("dev_path_offsets", c.c_void_p)]  # frozen (round-4 layout)
+
+
+class _CBatchExt(c.Structure):  # tsg_batch_ext: struct_size first, then the fields past tsg_batch
+    _fields_ = [("struct_size", c.c_uint32), ("base", _CBatch),
                 ("host_paths", c.c_void_p), ("host_path_offsets", c.c_void_p)]
+
+
+BATCH_EXT_SIZE_V1 = c.sizeof(_CBatchExt)  # TSG_BATCH_EXT_SIZE_V1
 
 
 class _CStats(c.Structure):
@@ -74,6 +81,8 @@ def _declare(L):
     L.tsg_scanner_allow_path.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64]
     L.tsg_scan.argtypes = [c.c_void_p, c.POINTER(_CBatch), c.POINTER(c.c_void_p)]
     L.tsg_scan_submit.argtypes = [c.c_void_p, c.POINTER(_CBatch), c.POINTER(c.c_void_p)]
+    L.tsg_scan_ext.argtypes = [c.c_void_p, c.POINTER(_CBatchExt), c.POINTER(c.c_void_p)]
+    L.tsg_scan_submit_ext.argtypes = [c.c_void_p, c.POINTER(_CBatchExt), c.POINTER(c.c_void_p)]
     L.tsg_scan_wait.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L.tsg_result_free.argtypes = [c.c_void_p]
     L.tsg_result_json.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_uint64)]
@@ -286,9 +295,11 @@ class Scanner:
         return (arena_buf, offs, parr, plen, bin_arr, transform), batch
 
     def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None, dev_paths=None,
-                   dev_path_offsets=None):
+                   dev_path_offsets=None, host_paths=None, host_path_offsets=None):
         """One batch (tsg_scan).  dev_arena / dev_offsets: the contents already in HBM;
-        dev_paths / dev_path_offsets: the paths packed in HBM (GPU allow-path prefilter)."""
+        dev_paths / dev_path_offsets: the paths packed in HBM (GPU allow-path prefilter);
+        host_paths / host_path_offsets (numpy u8 / u64): the paths packed in host memory, passed
+        through the versioned tsg_batch_ext (tsg_scan_ext)."""
         n = len(offsets) - 1
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -307,7 +318,11 @@ class Scanner:
                         bin_arr.ctypes.data if bin_arr is not None else None, None,
                         dev_paths, dev_path_offsets)
         h = c.c_void_p()
-        rc = self._L.tsg_scan(self._h, c.byref(batch), c.byref(h))
+        if host_paths is not None:
+            ext = _CBatchExt(BATCH_EXT_SIZE_V1, batch, host_paths.ctypes.data, host_path_offsets.ctypes.data)
+            rc = self._L.tsg_scan_ext(self._h, c.byref(ext), c.byref(h))
+        else:
+            rc = self._L.tsg_scan(self._h, c.byref(batch), c.byref(h))
         if rc != 0:
             raise RuntimeError("tsg_scan failed: %s" % _lib.last_error(self._L))
         return ScanResult(self, h)
