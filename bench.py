@@ -501,9 +501,71 @@ def _bind_numa(device):
         return None
 
 
+def _launch_ranks(argv, n):
+    """--gpus N (N > 1) without a torchrun environment: start the N rank processes of this same
+    command through torch.distributed.run (one rank per GPU, LOCAL_RANK = device) and return
+    their exit code.  Runs before anything in this process touches the GPU (a child process,
+    never an exec); the ranks print the one JSON line (rank 0)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def _dry_run(args, rank, world):
+    """--dry-run (CPU, gloo): the launcher's rank / world plumbing, the barrier-bracketed timing with
+    the max over ranks, and the rank-0 findings gather (shard.gather_records) on synthetic records --
+    no GPU, no corpus.  Prints the bench's JSON shape with n_gpus = the world that ran."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from trivy_amd import shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    rng = np.random.default_rng(rank)
+    dt = 0.0
+    for _ in range(args.steps):
+        if world > 1:
+            dist.barrier()
+        t0 = time.time()
+        rec = np.zeros(64, dtype=[("file", "<u4"), ("rule", "<u4"), ("start_line", "<i8"), ("end_line", "<i8"),
+                                  ("digest", "<u8")])
+        rec["file"] = rng.integers(0, 1000, 64)
+        rec["rule"] = rng.integers(0, 3, 64)
+        rec["start_line"] = rng.integers(1, 100, 64)
+        dt += time.time() - t0
+    gathered = None
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        paths = np.array([b"r%d/f%04d" % (rank, f) for f in rec["file"]])
+        merged = shard.gather_records(rec, paths, ["a", "b", "c"])
+        if merged is not None:
+            gathered = {"findings": int(len(merged["records"])), "ranks": int(len(set(merged["ranks"].tolist())))}
+    if rank == 0:
+        if world != args.gpus:
+            sys.exit("--gpus %d but %d ranks ran" % (args.gpus, world))
+        print(json.dumps({"metric": "dry run (no GPU)", "value": 0.0, "unit": "GB/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": 0, "ms_per_step": round(dt / max(1, args.steps) * 1e3, 4),
+                          "scaling": "weak", "gather": gathered}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node: one rank per GPU.  Under torchrun (WORLD_SIZE set) it must equal the "
+                         "world size; without it, N > 1 starts the N ranks itself (torch.distributed.run)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only (tests): the rank / world plumbing, timing and gather on synthetic records")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 50 for c2: a depth-3 pipeline's fill and drain are then a few %% of the "
                          "timed region, as in a long scan job; 10 for the other workloads)")
@@ -561,9 +623,15 @@ def main():
     if args.cpu_sample_mb is None:
         args.cpu_sample_mb = cpu_mb_default
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # N ranks, started before any GPU call
+        sys.exit(_launch_ranks(sys.argv[1:], args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return _dry_run(args, rank, world)
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (one rank per GPU)" % (args.gpus, world))
 
     import numpy as np
     import torch
@@ -809,9 +877,10 @@ def main():
     breakdown.update({k: round(avg(k), 3) for k in ("ms_fullscan_kernel", "ms_gpu_total", "ms_host_gpu_phase",
                                                      "ms_host_exact")})
     if layer is None:
-        n_bytes, n_files = C.n_bytes * emissions, C.n_files * emissions  # per step
-        if R is not None:  # the files' bytes as read (pre-strip numerator)
-            n_bytes = R.n_bytes
+        # per step: the arena bytes the timed steps scan.  (C2's files as read are 0.07 % larger --
+        # the 5 % CRLF files' '\r' -- but the resident leg strips them while packing, before timing:
+        # they are not counted; the ingest leg strips inside its timed region and counts them.)
+        n_bytes, n_files = C.n_bytes * emissions, C.n_files * emissions
         arena_bytes = C.n_bytes  # per scan
         counts = {k: int(last[k]) for k in ("flagged_blocks", "anchor_hits", "follow_hits", "fullscan_pairs", "fold_sites",
                                             "candidates", "special_files", "findings")}
@@ -827,6 +896,8 @@ def main():
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
                         "crlf_files": int(R.crlf.sum()) if R is not None else 0,
                         "arena_bytes_after_cr_strip": C.n_bytes,
+                        "input_bytes_as_read": R.n_bytes if R is not None else C.n_bytes,
+                        "value_numerator": "arena bytes (after the CR strip done while packing, before timing)",
                         "emissions_per_step": emissions, "pool_bytes": C.n_bytes,
                         "resident": "host (page-locked), H2D in the timed region" if args.ingest
                         else "HBM (copied once before timing)"}
@@ -941,6 +1012,10 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "gather": gathered,
+            "legs": ("N=1: resident steps, ingest leg (c2), oracle parity sample, CPU baseline" if world == 1 else
+                     "N>1: resident steps and the rank-0 findings gather only; the ingest leg, the parity sample "
+                     "and the CPU baseline run at N=1 (every rank would page-lock its corpus / rerun the CPU "
+                     "reference)"),
             "breakdown_ms": breakdown,
             "host_cpu": host_cpu,
             "counts": counts,

@@ -89,6 +89,12 @@ int tsg_debug_pool_budget(void);
 struct tsg_scanner;
 int tsg_debug_scanner_engine(struct tsg_scanner* s, uint64_t out[4]);
 
+/* Where a scanner makes the findings of HBM-resident batches (tsg_batch.dev_arena):
+ * on = 1 the GPU (trivy_amd/csrc/materialize.h, the default; TSG_GPU_FINDINGS=0
+ * at scanner creation turns it off), 0 the host.  Returns the previous setting,
+ * -1 for a scanner without a GPU engine.  (A/B and parity tests.) */
+int tsg_debug_scanner_gpu_findings(struct tsg_scanner* s, int on);
+
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);
 

@@ -193,3 +193,29 @@ def test_two_rank_records_gather_sorted(tmp_path):
     ids = ["zeta", "alpha", "mid"]
     keys = [(p, ids[r], int(s)) for p, r, s in zip(paths, rec["rule"], rec["start_line"])]
     assert keys == sorted(keys)
+
+
+def test_bench_gpus_flag_launches_the_ranks():
+    """`bench.py --gpus 2` without a torchrun environment starts two rank processes itself
+    (torch.distributed.run, one rank per GPU) before anything touches a GPU; --dry-run runs the
+    rank / world plumbing, the max-over-ranks timing and the rank-0 findings gather on gloo.  The
+    line reports the world that ran, and a --gpus / WORLD_SIZE disagreement fails loudly."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3
+    assert d["gather"] == {"findings": 128, "ranks": 2}
+    env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env2, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "--gpus 2 but WORLD_SIZE=1" in r.stderr

@@ -622,4 +622,9 @@ int tsg_debug_scanner_engine(tsg_scanner* s, uint64_t out[4]) {
   return 0;
 }
 
+int tsg_debug_scanner_gpu_findings(tsg_scanner* s, int on) {
+  if (!s || !s->s) return -1;
+  return s->s->SetGpuFindings(on);
+}
+
 }  // extern "C"

@@ -450,6 +450,15 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
       return;
     }
   }
+  // findings of HBM-resident batches made on the GPU (TSG_GPU_FINDINGS=0: on the host)
+  const char* gf = std::getenv("TSG_GPU_FINDINGS");
+  gpu_findings_.store(!gf || std::atoi(gf) != 0 ? 1 : 0);
+  mat_.reset(new FindingMaterializer(device));
+  if (!mat_->ok()) {
+    err_ = mat_->error();
+    *err = err_;
+    return;
+  }
 }
 
 void SecretScanner::BuildAllowPathFilter() {
@@ -689,6 +698,16 @@ thread_local ScanScratch t_scan;
 void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_view path, bool binary,
                              const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const {
   PhaseTimer pt_all(7);
+  MatchFile(content, len, path, c, nc, gpu_windows);
+  if (t_scan.matched.empty()) {
+    out->kind = kNoFindings;
+    return;
+  }
+  FindingsHost(content, len, path, binary, c, nc, out);
+}
+
+void SecretScanner::MatchFile(const uint8_t* content, int64_t len, std::string_view path, const Candidate* c,
+                              size_t nc, bool gpu_windows) const {
   const uint8_t* P = reinterpret_cast<const uint8_t*>(path.data());
   ScanScratch& S = t_scan;
   std::vector<std::pair<uint32_t, Loc>>& matched = S.matched;
@@ -700,24 +719,6 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   std::string lowered;
   bool lowered_done = false;
   bool fold_done = false, fold_runes = false;
-  // (wlo, nl_before) anchors for line numbers
-  std::vector<std::pair<int64_t, int64_t>>& nla = S.nla;
-  nla.clear();
-  for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
-  std::sort(nla.begin(), nla.end());
-  // the GPU's last-three-newlines before each window (Candidate::nl_back)
-  std::vector<const Candidate*>& hints = S.hints;
-  hints.clear();
-  static const bool use_hints = !std::getenv("TSG_NL_HINTS") || std::atoi(std::getenv("TSG_NL_HINTS")) != 0;
-  for (size_t i = 0; i < nc && use_hints; i++)
-    if (c[i].nl_back[0] != kNlUnknown && c[i].nl_back[0] != 0) hints.push_back(&c[i]);  // 0: never a GPU value
-  std::sort(hints.begin(), hints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
-  // and the first three at or after it (Candidate::nl_fwd)
-  std::vector<const Candidate*>& fhints = S.fhints;
-  fhints.clear();
-  for (size_t i = 0; i < nc && use_hints; i++)
-    if (c[i].nl_fwd[0] != kNlUnknown) fhints.push_back(&c[i]);
-  std::sort(fhints.begin(), fhints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
 
   // the candidates are sorted by rule: real rules first, then the exclude-block rules
   const uint32_t n_real = uint32_t(rules_.size());
@@ -906,10 +907,31 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
       censor.push_back(loc);
     }
   }
-  if (matched.empty()) {
-    out->kind = kNoFindings;
-    return;
-  }
+}
+
+void SecretScanner::FindingsHost(const uint8_t* content, int64_t len, std::string_view path, bool binary,
+                                 const Candidate* c, size_t nc, FileResult* out) const {
+  ScanScratch& S = t_scan;
+  std::vector<std::pair<uint32_t, Loc>>& matched = S.matched;
+  std::vector<Loc>& censor = S.censor;
+  // (wlo, nl_before) anchors for line numbers
+  std::vector<std::pair<int64_t, int64_t>>& nla = S.nla;
+  nla.clear();
+  for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
+  std::sort(nla.begin(), nla.end());
+  // the GPU's last-three-newlines before each window (Candidate::nl_back)
+  std::vector<const Candidate*>& hints = S.hints;
+  hints.clear();
+  static const bool use_hints = !std::getenv("TSG_NL_HINTS") || std::atoi(std::getenv("TSG_NL_HINTS")) != 0;
+  for (size_t i = 0; i < nc && use_hints; i++)
+    if (c[i].nl_back[0] != kNlUnknown && c[i].nl_back[0] != 0) hints.push_back(&c[i]);  // 0: never a GPU value
+  std::sort(hints.begin(), hints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
+  // and the first three at or after it (Candidate::nl_fwd)
+  std::vector<const Candidate*>& fhints = S.fhints;
+  fhints.clear();
+  for (size_t i = 0; i < nc && use_hints; i++)
+    if (c[i].nl_fwd[0] != kNlUnknown) fhints.push_back(&c[i]);
+  std::sort(fhints.begin(), fhints.end(), [](const Candidate* a, const Candidate* b) { return a->wlo < b->wlo; });
 
   // findLocation runs on the censored buffer (scanner.go:438-439): newlines
   // inside a censored span are '*' there.  Spans merged and sorted:
@@ -1228,6 +1250,62 @@ void SecretScanner::ScanFile(const uint8_t* content, int64_t len, std::string_vi
   SortFindings(&out->findings, rule_rank_);
 }
 
+void SecretScanner::GpuFindingsInput(const uint8_t* content, const Candidate* c, size_t nc, FileResult* out) const {
+  ScanScratch& S = t_scan;
+  // the anchors: (wlo, raw '\n' before wlo) of every candidate window of the file
+  std::vector<std::pair<int64_t, int64_t>>& nla = S.nla;
+  nla.clear();
+  for (size_t i = 0; i < nc; i++) nla.push_back({c[i].wlo, c[i].nl_before});
+  std::sort(nla.begin(), nla.end());
+  // the censor spans, merged and sorted (as FindingsHost), each with the '\n'
+  // inside the spans before it, then the sentinel
+  std::vector<Loc>& spans = S.spans;
+  spans.assign(S.censor.begin(), S.censor.end());
+  std::sort(spans.begin(), spans.end(), [](const Loc& a, const Loc& b) { return a.s < b.s; });
+  out->gs.clear();
+  int64_t nl = 0;
+  for (auto& z : spans) {
+    if (z.e <= z.s) continue;
+    if (!out->gs.empty() && z.s <= out->gs.back().e) {
+      MatSpan& b = out->gs.back();
+      if (z.e > b.e) {  // (the '\n' of the grown part)
+        for (const uint8_t *p = content + b.e, *e = content + z.e; p < e;) {
+          const void* q = std::memchr(p, '\n', size_t(e - p));
+          if (!q) break;
+          nl++;
+          p = static_cast<const uint8_t*>(q) + 1;
+        }
+        b.e = z.e;
+      }
+      continue;
+    }
+    out->gs.push_back({z.s, z.e, nl});
+    for (const uint8_t *p = content + z.s, *e = content + z.e; p < e;) {
+      const void* q = std::memchr(p, '\n', size_t(e - p));
+      if (!q) break;
+      nl++;
+      p = static_cast<const uint8_t*>(q) + 1;
+    }
+  }
+  out->gs.push_back({INT64_MAX, INT64_MAX, nl});
+  out->gm.clear();
+  uint64_t tb = 0;
+  for (auto& mt : S.matched) {
+    const int64_t st = mt.second.s, en = mt.second.e;
+    int64_t a_wlo = 0, a_nl = 0;
+    auto it = std::upper_bound(nla.begin(), nla.end(), std::make_pair(st, INT64_MAX));
+    if (it != nla.begin()) {
+      --it;
+      a_wlo = it->first;
+      a_nl = it->second;
+    }
+    out->gm.push_back({mt.first, 0, st, en, a_wlo, a_nl});
+    tb += uint64_t(std::max<int64_t>(100, en - st + 50)) + 400;  // match text + <= 4 lines of <= 100 B
+  }
+  out->text_bound = tb;
+  out->gpu = true;
+}
+
 bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst, HostStats* hst, std::string* err) {
   double t0 = NowMs();
   struct Active {
@@ -1318,7 +1396,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     }
   }
   const double t_tail = NowMs();
-  HostTail(tin, &cands, out, &hs, &allowed, true);
+  if (!HostTail(tin, &cands, out, &hs, &allowed, true, err)) return false;
   if (gst && gst->ms_total > 0) host_bound_.store(hs.ms_exact > 1.5 * double(gst->ms_total));
   static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;
   if (times)
@@ -1388,8 +1466,11 @@ void SecretScanner::GiveScratch(std::unique_ptr<TailScratch> s) const {
   if (scratch_free_.size() < 8) scratch_free_.push_back(std::move(s));  // (as many as scans run at once)
 }
 
-void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, BatchResult* out,
-                             HostStats* hs, const std::vector<uint8_t>* allowed_pre, bool gpu_windows) const {
+bool SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands_p, BatchResult* out,
+                             HostStats* hs, const std::vector<uint8_t>* allowed_pre, bool gpu_windows,
+                             std::string* err) const {
+  std::string err_local;
+  if (!err) err = &err_local;
   std::vector<Candidate>& cands = *cands_p;
   out->found_files.clear();
   out->found.clear();
@@ -1529,10 +1610,14 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     }
     return t_arena;
   };
+  // toFinding / findLocation on the GPU (materialize.h) when the arena is resident in HBM
+  const bool gpu_mat = mat_ && gpu_windows && gpu_findings_.load() != 0 && in.dev_arena && in.dev_offsets &&
+                       !in.file_data;
   auto scan_group = [&](size_t k) {
     const size_t a = starts[k], b = starts[k + 1];
     const uint32_t f = group_file(k);
     tmp[k].kind = kNoFindings;
+    tmp[k].gpu = false;
     if (allowed[f]) {
       // no stale FileFindings from an earlier pass (its arena belongs to a result
       // that may be gone) stays behind in the reused scratch
@@ -1553,8 +1638,19 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     size_t pn = in.path_lens ? size_t(in.path_lens[f]) : std::strlen(p);
     const uint8_t* data = in.file_data ? in.file_data[f] : in.host_arena + in.host_offsets[f];
     const int64_t len = int64_t(in.file_data ? in.file_len[f] : in.host_offsets[f + 1] - in.host_offsets[f]);
-    ScanFile(data, len, std::string_view(p, pn), in.binary && in.binary[f], t_group.data(), t_group.size(), &tmp[k],
-             gpu_windows);
+    const bool bin = in.binary && in.binary[f];
+    if (!gpu_mat) {
+      ScanFile(data, len, std::string_view(p, pn), bin, t_group.data(), t_group.size(), &tmp[k], gpu_windows);
+      return;
+    }
+    PhaseTimer pt_all(7);
+    MatchFile(data, len, std::string_view(p, pn), t_group.data(), t_group.size(), gpu_windows);
+    if (t_scan.matched.empty()) return;
+    if (bin) {  // (Code{}, Match from the path and title: nothing for the GPU)
+      FindingsHost(data, len, std::string_view(p, pn), bin, t_group.data(), t_group.size(), &tmp[k]);
+      return;
+    }
+    GpuFindingsInput(data, t_group.data(), t_group.size(), &tmp[k]);
   };
   // no other scan in flight (the end of a run): the pool's spare workers join in,
   // the last scan's exact pass being all that is left (TSG_DRAIN_WIDE=0: never;
@@ -1577,6 +1673,13 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
       scan_group(order[kk]);
     }
   }, wide);
+  const double t_par0 = NowMs();
+  double ms_mat_gpu = 0;
+  if (gpu_mat && !GpuFindings(in, scr.get(), nf, [&](size_t k) { return group_file(k); }, thread_arena, wide,
+                              &ms_mat_gpu, err)) {
+    GiveScratch(std::move(scr));
+    return false;
+  }
   const double t_par = NowMs();
   if (g_tail_debug)
     std::fprintf(stderr, "tail serial ms: sort+setup %.1f (order %.1f) parallel %.1f\n", t_sorted - t2,
@@ -1629,15 +1732,98 @@ void SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
   if (g_tail_debug) std::fprintf(stderr, "tail serial ms: collect %.1f\n", t3 - t_par);
   static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;  // one line per pass, no per-file timers
   if (times)
-    std::fprintf(stderr, "tail times ms: kind %.2f group %.2f results %.2f order %.2f parallel %.2f collect %.2f"
-                 " (files %zu, wide %d)\n", t2 - t1, t_grouped - t2, t_sorted - t_grouped, t_ordered - t_sorted,
-                 t_par - t_ordered, t3 - t_par, nf, int(wide));
+    std::fprintf(stderr, "tail times ms: kind %.2f group %.2f results %.2f order %.2f parallel %.2f (gpu findings %.2f, "
+                 "of which GPU %.2f) collect %.2f (files %zu, wide %d)\n", t2 - t1, t_grouped - t2, t_sorted - t_grouped,
+                 t_ordered - t_sorted, t_par0 - t_ordered, t_par - t_par0, ms_mat_gpu, t3 - t_par, nf, int(wide));
   GiveScratch(std::move(scr));
   hs->ms_allow = t2 - t1;
   hs->ms_exact = t3 - t2;
   hs->candidates = cands.size();
   hs->files_with_candidates = nf;
   hs->findings = out->n_findings();
+  return true;
+}
+
+template <class GroupFile, class ArenaOf>
+bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t nf, GroupFile group_file,
+                                ArenaOf& thread_arena, bool wide, double* ms_gpu, std::string* err) const {
+  std::vector<FileResult>& tmp = scr->tmp;
+  std::vector<uint32_t>& gk = scr->gk;  // groups whose findings the GPU makes, in file order
+  gk.clear();
+  for (size_t k = 0; k < nf; k++)
+    if (tmp[k].gpu) gk.push_back(uint32_t(k));
+  // calls of bounded size: the text offsets of one call are 32-bit
+  constexpr uint64_t kTextCap = uint64_t(1) << 31, kMatchCap = uint64_t(1) << 26;
+  std::vector<uint64_t>& m0 = scr->gm0;
+  std::vector<uint64_t>& s0 = scr->gs0;
+  size_t a = 0;
+  while (a < gk.size()) {
+    size_t b = a;
+    uint64_t nm = 0, ns = 0, tb = 0;
+    m0.clear();
+    s0.clear();
+    while (b < gk.size()) {
+      const FileResult& R = tmp[gk[b]];
+      if (b > a && (nm + R.gm.size() > kMatchCap || tb + R.text_bound > kTextCap)) break;
+      m0.push_back(nm);
+      s0.push_back(ns);
+      nm += R.gm.size();
+      ns += R.gs.size();
+      tb += R.text_bound;
+      b++;
+    }
+    if (tb > kTextCap || nm > kMatchCap) {
+      *err = "GPU findings: one file's findings exceed a call's bounds";
+      return false;
+    }
+    FindingMaterializer::Job* job = mat_->Begin(uint32_t(b - a), uint32_t(nm), uint32_t(ns), tb, err);
+    if (!job) return false;
+    MatFile* F = mat_->files(job);
+    MatMatch* M = mat_->matches(job);
+    MatSpan* Sp = mat_->spans(job);
+    constexpr size_t kBlk = 256;
+    const size_t n = b - a;
+    ParallelFor((n + kBlk - 1) / kBlk, host_threads_, [&](size_t blk) {
+      for (size_t i = blk * kBlk, e = std::min(n, i + kBlk); i < e; i++) {
+        const FileResult& R = tmp[gk[a + i]];
+        F[i] = MatFile{group_file(gk[a + i]), uint32_t(m0[i]), uint32_t(R.gm.size()), uint32_t(s0[i]),
+                       uint32_t(R.gs.size()), 0};
+        MatMatch* mo = M + m0[i];
+        for (size_t q = 0; q < R.gm.size(); q++) {
+          mo[q] = R.gm[q];
+          mo[q].fidx = uint32_t(i);
+        }
+        std::memcpy(Sp + s0[i], R.gs.data(), R.gs.size() * sizeof(MatSpan));
+      }
+    }, wide);
+    const double g0 = NowMs();
+    if (!mat_->Run(job, in.dev_arena, in.dev_offsets, err)) {
+      mat_->End(job);
+      return false;
+    }
+    *ms_gpu += NowMs() - g0;
+    const FindingOut* fo = mat_->findings(job);
+    const LineOut* lo = mat_->lines(job);
+    const char* tx = mat_->text(job);
+    const uint64_t* pref = mat_->pref(job);
+    ParallelFor((n + kBlk - 1) / kBlk, host_threads_, [&](size_t blk) {
+      for (size_t i = blk * kBlk, e = std::min(n, i + kBlk); i < e; i++) {
+        FileResult& R = tmp[gk[a + i]];
+        const size_t x = m0[i], y = x + R.gm.size();
+        const uint64_t p0 = pref[x], p1 = pref[y];
+        FileFindings& ff = R.findings;
+        ff = FileFindings(thread_arena());
+        ff.f.assign(fo + x, fo + y);
+        ff.lines.assign(lo + uint32_t(p0), lo + uint32_t(p1));
+        ff.text.assign(tx + (p0 >> 32), tx + (p1 >> 32));
+        SortFindings(&ff, rule_rank_);
+        R.kind = kHasFindings;
+      }
+    }, wide);
+    mat_->End(job);
+    a = b;
+  }
+  return true;
 }
 
 }  // namespace tsg

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "materialize.h"
 #include "pathfilter.h"
 #include "goregex.h"
 #include "rules.h"
@@ -64,20 +65,9 @@ struct RuleSpec {
   std::vector<uint16_t> kw_rare;           // per entry: index of its least frequent letter (memchr key)
 };
 
-// Findings of one file, flat: records plus one text pool for every match and
-// code line (three allocations per file, whatever the finding count).
-struct LineOut {
-  int64_t number;
-  uint32_t off, len;  // content in FileFindings::text
-  bool is_cause, first_cause, last_cause;
-};
-
-struct FindingOut {
-  uint32_t rule;
-  int64_t start_line, end_line;
-  uint32_t match_off, match_len;  // in FileFindings::text
-  uint32_t line_lo, line_hi;      // into FileFindings::lines
-};
+// Findings of one file, flat: records (LineOut, FindingOut: materialize.h)
+// plus one text pool for every match and code line (three allocations per
+// file, whatever the finding count).
 
 // Bump allocator for one batch's findings: each host thread of the exact
 // pass fills its own, and the batch result frees them whole -- per file the
@@ -159,6 +149,13 @@ enum FileKind : uint32_t { kNoFindings = 0, kAllowedPath = 1, kHasFindings = 2 }
 struct FileResult {
   FileKind kind = kNoFindings;
   FileFindings findings;
+  // GPU materialisation (materialize.h): the file's locations and censor spans
+  // (with the sentinel), set by the exact pass, turned into findings after the
+  // batch-wide GPU pass
+  bool gpu = false;
+  std::vector<MatMatch> gm;
+  std::vector<MatSpan> gs;
+  uint64_t text_bound = 0;
 };
 
 // Files' findings in one allocation, constructed in place by the exact pass's
@@ -269,8 +266,10 @@ class SecretScanner {
   // gpu_windows: the candidates came from the GPU engine, so the exclude-block
   // regexes (compiled as extra rules) have candidate windows too; otherwise
   // (host-only callers) each exclude regex sweeps the whole file.
-  void HostTail(const BatchInput& in, std::vector<Candidate>* cands, BatchResult* out, HostStats* hs,
-                const std::vector<uint8_t>* allowed = nullptr, bool gpu_windows = false) const;
+  // False (with *err) only when the GPU findings pass fails.
+  bool HostTail(const BatchInput& in, std::vector<Candidate>* cands, BatchResult* out, HostStats* hs,
+                const std::vector<uint8_t>* allowed = nullptr, bool gpu_windows = false,
+                std::string* err = nullptr) const;
   std::vector<uint8_t> AllowedPaths(const BatchInput& in) const;
   // Global.AllowPath (scanner.go:57-59)
   bool AllowPath(const uint8_t* p, size_t n) const;
@@ -286,6 +285,15 @@ class SecretScanner {
  private:
   void ScanFile(const uint8_t* content, int64_t len, std::string_view path, bool binary,
                 const Candidate* c, size_t nc, FileResult* out, bool gpu_windows) const;
+  // ScanFile in two parts: the surviving locations of the rules (scanner.go:394-436)
+  // into the calling thread's scratch (matched, censor), then toFinding /
+  // findLocation / sort on the host (:438-457) from them
+  void MatchFile(const uint8_t* content, int64_t len, std::string_view path, const Candidate* c, size_t nc,
+                 bool gpu_windows) const;
+  void FindingsHost(const uint8_t* content, int64_t len, std::string_view path, bool binary, const Candidate* c,
+                    size_t nc, FileResult* out) const;
+  // the GPU materialisation's uploads of one file (materialize.h), from the scratch of MatchFile
+  void GpuFindingsInput(const uint8_t* content, const Candidate* c, size_t nc, FileResult* out) const;
   // HostTail's serial set-up buffers (the per-file counts, the grouped
   // candidates, the dispatch order), kept across calls: allocated per call,
   // their first touch (page faults on ~10 MB) was most of the set-up's time.
@@ -295,7 +303,13 @@ class SecretScanner {
     std::vector<size_t> starts;
     std::vector<double> w;
     std::vector<FileResult> tmp;      // per group
+    std::vector<uint32_t> gk;         // GPU findings: the groups, their first location / span
+    std::vector<uint64_t> gm0, gs0;
   };
+  // the findings of the groups HostTail marked `gpu`, made by mat_ (materialize.h)
+  template <class GroupFile, class ArenaOf>
+  bool GpuFindings(const BatchInput& in, TailScratch* scr, size_t nf, GroupFile group_file, ArenaOf& thread_arena,
+                   bool wide, double* ms_gpu, std::string* err) const;
   std::unique_ptr<TailScratch> TakeScratch() const;
   void GiveScratch(std::unique_ptr<TailScratch> s) const;
   mutable std::mutex scratch_mu_;
@@ -340,6 +354,13 @@ class SecretScanner {
   bool AllowPathRules(const uint8_t* p, size_t n, uint64_t lit_rules) const;
   // GPU allow-path prefilter (pathfilter.h): built when every path rule has usable literals
   std::unique_ptr<PathFilter> path_filter_;
+  std::unique_ptr<FindingMaterializer> mat_;  // GPU findings of HBM-resident batches
+  std::atomic<int> gpu_findings_{1};
+
+ public:
+  // 1 / 0: GPU / host findings for HBM-resident batches (tests, A/B); returns the
+  // previous setting, -1 without a GPU engine
+  int SetGpuFindings(int on) { return mat_ ? gpu_findings_.exchange(on ? 1 : 0) : -1; }
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.

@@ -327,6 +327,12 @@ class Scanner:
             raise RuntimeError("tsg_scan failed: %s" % _lib.last_error(self._L))
         return ScanResult(self, h)
 
+    def set_gpu_findings(self, on: bool) -> int:
+        """Findings of HBM-resident batches on the GPU (materialize.h, default) or on the host
+        (tsg_debug_scanner_gpu_findings); returns the previous setting."""
+        self._L.tsg_debug_scanner_gpu_findings.argtypes = [c.c_void_p, c.c_int]
+        return self._L.tsg_debug_scanner_gpu_findings(self._h, 1 if on else 0)
+
     def table_info(self):
         t = _CTableInfo()
         self._L.tsg_scanner_table_info(self._h, c.byref(t))
