@@ -113,16 +113,36 @@ def _compile(v):
     return GoRegexp(v)
 
 
+def _yaml_value(node):
+    """gopkg.in/yaml.v3 (go.mod:132) into the Config's Go types: a scalar decoded into a string
+    field (and into Regexp.UnmarshalYAML, scanner.go:75-87, which compiles value.Value) is the
+    node's text as written -- `0x1F` stays "0x1F", `true` stays "true" -- and a plain null
+    scalar (~ / null / Null / NULL / empty) is the zero value (None here)."""
+    if node is None:
+        return None
+    if isinstance(node, yaml.MappingNode):
+        return {_yaml_value(k): _yaml_value(v) for k, v in node.value}
+    if isinstance(node, yaml.SequenceNode):
+        return [_yaml_value(v) for v in node.value]
+    if node.style is None and node.value in ("~", "null", "Null", "NULL", ""):
+        return None
+    return node.value
+
+
+def _go_string(v):  # a string field: its text, "" for null
+    return "" if v is None else v
+
+
 def _allow_rules_from_yaml(items):
     out = []
     for a in items or []:
-        out.append(AllowRule(id=a.get("id", "") or "", description=a.get("description", "") or "",
+        out.append(AllowRule(id=_go_string(a.get("id")), description=_go_string(a.get("description")),
                              regex=_compile(a.get("regex")), path=_compile(a.get("path"))))
     return out
 
 
 def _exclude_from_yaml(block):
-    return [_compile(r) for r in ((block or {}).get("regexes") or [])]
+    return [_compile(_go_string(r)) for r in ((block or {}).get("regexes") or [])]
 
 
 def convert_severity(sev) -> str:  # scanner.go:310-318
@@ -148,22 +168,22 @@ def parse_config(config_path):  # scanner.go:277-307
     p = Path(config_path)
     if not p.exists():
         return None
-    doc = yaml.safe_load(p.read_text()) or {}
+    doc = _yaml_value(yaml.compose(p.read_text(), Loader=yaml.SafeLoader)) or {}
     c = Config()
-    c.enable_builtin_rule_ids = [str(x) for x in doc.get("enable-builtin-rules") or []]
-    c.disable_rule_ids = [str(x) for x in doc.get("disable-rules") or []]
-    c.disable_allow_rule_ids = [str(x) for x in doc.get("disable-allow-rules") or []]
+    c.enable_builtin_rule_ids = [_go_string(x) for x in doc.get("enable-builtin-rules") or []]
+    c.disable_rule_ids = [_go_string(x) for x in doc.get("disable-rules") or []]
+    c.disable_allow_rule_ids = [_go_string(x) for x in doc.get("disable-allow-rules") or []]
     for r in doc.get("rules") or []:
         c.custom_rules.append(Rule(
-            id=str(r.get("id", "") or ""), category=str(r.get("category", "") or ""),
-            title=str(r.get("title", "") or ""),
+            id=_go_string(r.get("id")), category=_go_string(r.get("category")),
+            title=_go_string(r.get("title")),
             severity=convert_severity(r.get("severity")),
             regex=_compile(r.get("regex")),
-            keywords=[str(k) for k in (r.get("keywords") or [])],
+            keywords=[_go_string(k) for k in (r.get("keywords") or [])],
             path=_compile(r.get("path")),
             allow_rules=_allow_rules_from_yaml(r.get("allow-rules")),
             exclude_block=_exclude_from_yaml(r.get("exclude-block")),
-            secret_group_name=str(r.get("secret-group-name", "") or "")))
+            secret_group_name=_go_string(r.get("secret-group-name"))))
     c.custom_allow_rules = _allow_rules_from_yaml(doc.get("allow-rules"))
     c.exclude_block = _exclude_from_yaml(doc.get("exclude-block"))
     return c

@@ -121,4 +121,4 @@ def test_gpu_findings_dense_corpus_vs_oracle():
         want = o.scan(p, b)
         assert g.to_dict() == want, p
         n += len(want["Findings"] or [])
-    assert n > 1000
+    assert n > 400

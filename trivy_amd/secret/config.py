@@ -68,6 +68,53 @@ class Config:  # scanner.go:29-43
     ExcludeBlock: ExcludeBlock = field(default_factory=ExcludeBlock)
 
 
+# yaml.v3 (gopkg.in/yaml.v3 v3.0.1, go.mod:132) decodes a scalar into a Go `string` field -- and
+# Regexp.UnmarshalYAML compiles value.Value (scanner.go:75-87) -- as the node's source text: `id: 0`
+# is "0", `regex: 0x1F` is "0x1F", `title: true` is "true"; only a plain null (~, null, Null, NULL or
+# nothing) is the zero value ("" / a nil *Regexp).  So the document is composed into nodes and read
+# by their text, not constructed with PyYAML's YAML 1.1 typing (0x1F -> 31, on -> True).
+_PLAIN_NULL = ("~", "null", "Null", "NULL", "")
+
+
+def _node(n, where="config"):
+    if n is None:
+        return None
+    if isinstance(n, yaml.MappingNode):
+        out = {}
+        for k, v in n.value:
+            out[_text(_node(k, where), where)] = _node(v, where)
+        return out
+    if isinstance(n, yaml.SequenceNode):
+        return [_node(v, where) for v in n.value]
+    if n.style is None and n.value in _PLAIN_NULL:
+        return None
+    return n.value
+
+
+def _text(v, where) -> str:  # a Go string field
+    if v is None:
+        return ""
+    if not isinstance(v, str):
+        raise ConfigError("secrets config decode error: %s: cannot unmarshal a %s into a string"
+                          % (where, "sequence" if isinstance(v, list) else "mapping"))
+    return v
+
+
+def _texts(v, where):  # a Go []string field
+    if v is None:
+        return []
+    if not isinstance(v, list):
+        raise ConfigError("secrets config decode error: %s: cannot unmarshal a scalar into a list" % where)
+    return [_text(x, where) for x in v]
+
+
+def _load_yaml(text):
+    try:
+        return _node(yaml.compose(text, Loader=yaml.SafeLoader)) or {}
+    except yaml.YAMLError as e:
+        raise ConfigError("secrets config decode error: %s" % e)
+
+
 def convert_severity(sev) -> str:  # scanner.go:310-318
     sev = "" if sev is None else str(sev)
     if sev.lower() in ("low", "medium", "high", "critical", "unknown"):
@@ -78,7 +125,7 @@ def convert_severity(sev) -> str:  # scanner.go:310-318
 def _allow_rules(items, where):
     out = []
     for a in items or []:
-        out.append(AllowRule(ID=str(a.get("id", "") or ""), Description=str(a.get("description", "") or ""),
+        out.append(AllowRule(ID=_text(a.get("id"), where), Description=_text(a.get("description"), where),
                              Regex=_check_regex(a.get("regex"), where),
                              Path=_check_regex(a.get("path"), where)))
     return out
@@ -86,8 +133,8 @@ def _allow_rules(items, where):
 
 def _exclude(block, where):
     block = block or {}
-    return ExcludeBlock(Description=str(block.get("description", "") or ""),
-                        Regexes=[_check_regex(r, where) for r in (block.get("regexes") or [])])
+    return ExcludeBlock(Description=_text(block.get("description"), where),
+                        Regexes=[_check_regex(_text(r, where), where) for r in (block.get("regexes") or [])])
 
 
 def ParseConfig(config_path) -> Optional[Config]:  # scanner.go:277-307
@@ -96,25 +143,22 @@ def ParseConfig(config_path) -> Optional[Config]:  # scanner.go:277-307
     p = Path(config_path)
     if not p.exists():
         return None
-    try:
-        doc = yaml.safe_load(p.read_text()) or {}
-    except yaml.YAMLError as e:
-        raise ConfigError("secrets config decode error: %s" % e)
+    doc = _load_yaml(p.read_text())
     c = Config()
-    c.EnableBuiltinRuleIDs = [str(x) for x in doc.get("enable-builtin-rules") or []]
-    c.DisableRuleIDs = [str(x) for x in doc.get("disable-rules") or []]
-    c.DisableAllowRuleIDs = [str(x) for x in doc.get("disable-allow-rules") or []]
+    c.EnableBuiltinRuleIDs = _texts(doc.get("enable-builtin-rules"), "enable-builtin-rules")
+    c.DisableRuleIDs = _texts(doc.get("disable-rules"), "disable-rules")
+    c.DisableAllowRuleIDs = _texts(doc.get("disable-allow-rules"), "disable-allow-rules")
     for r in doc.get("rules") or []:
-        rid = str(r.get("id", "") or "")
+        rid = _text(r.get("id"), "rules")
         c.CustomRules.append(Rule(
-            ID=rid, Category=str(r.get("category", "") or ""), Title=str(r.get("title", "") or ""),
-            Severity=convert_severity(r.get("severity")),
+            ID=rid, Category=_text(r.get("category"), rid), Title=_text(r.get("title"), rid),
+            Severity=convert_severity(_text(r.get("severity"), rid)),
             Regex=_check_regex(r.get("regex"), rid),
-            Keywords=[str(k) for k in (r.get("keywords") or [])],
+            Keywords=_texts(r.get("keywords"), rid),
             Path=_check_regex(r.get("path"), rid),
             AllowRules=_allow_rules(r.get("allow-rules"), rid),
             ExcludeBlock=_exclude(r.get("exclude-block"), rid),
-            SecretGroupName=str(r.get("secret-group-name", "") or "")))
+            SecretGroupName=_text(r.get("secret-group-name"), rid)))
     c.CustomAllowRules = _allow_rules(doc.get("allow-rules"), "allow-rules")
     c.ExcludeBlock = _exclude(doc.get("exclude-block"), "exclude-block")
     return c
