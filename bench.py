@@ -602,6 +602,9 @@ def main():
                     help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
                          "the walk's host threads")
     ap.add_argument("--pool-gb", type=float, default=64.0, help="c5: page-locked host pool size")
+    ap.add_argument("--calib-mb", type=float, default=16.0,
+                    help="rule compiler calibration sample: the first MB of the corpus (as a scan job would hand "
+                         "the scanner its first batch; tsg_compile_options) -- 0: the static byte prior only")
     ap.add_argument("--traffic-file", default=None,
                     help="PMC traffic summary (default: the newest profiles/traffic_rNN_<workload>.json, c2: traffic_rNN.json)")
     args = ap.parse_args()
@@ -709,7 +712,8 @@ def main():
             d_poffs = torch.from_numpy(poffs.view(np.int64)).to(dev)
         torch.cuda.synchronize()
         t_c = time.time()
-        sc = secret.NewScanner(secret.ParseConfig(cfg_path) if cfg_path else None, device=local)
+        calib = C.arena[:min(C.n_bytes, int(args.calib_mb * 1e6))] if args.calib_mb > 0 else None
+        sc = secret.NewScanner(secret.ParseConfig(cfg_path) if cfg_path else None, device=local, calibration=calib)
         t_compile = time.time() - t_c
 
         def submit():
@@ -894,6 +898,7 @@ def main():
         breakdown["ms_last_scan_after_gpu"] = round(last["ms_host_total"] - last["ms_host_gpu_phase"], 3)
         breakdown["ms_timed_minus_gpu"] = round(dt * 1e3 - args.steps * emissions * gpu_ms, 3)
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
+                        "calibration_sample_bytes": int(calib.size) if calib is not None else 0,
                         "crlf_files": int(R.crlf.sum()) if R is not None else 0,
                         "arena_bytes_after_cr_strip": C.n_bytes,
                         "input_bytes_as_read": R.n_bytes if R is not None else C.n_bytes,

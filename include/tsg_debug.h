@@ -52,6 +52,11 @@ typedef struct tsg_debug_rule_info {
   uint32_t n_kw;
 } tsg_debug_rule_info;
 int tsg_debug_compile(const struct tsg_global* g, tsg_compiled** out);
+/* The same with compiler options (tsg_scanner.h tsg_compile_options); out_calibrated (optional):
+ * the anchors the calibration sample moved to a class run. */
+struct tsg_compile_options;
+int tsg_debug_compile_ex(const struct tsg_global* g, const struct tsg_compile_options* opt, tsg_compiled** out,
+                         uint32_t* out_calibrated);
 void tsg_debug_compiled_free(tsg_compiled* c);
 int tsg_debug_compiled_info(const tsg_compiled* c, struct tsg_table_info* out);
 int tsg_debug_rule(const tsg_compiled* c, uint32_t i, tsg_debug_rule_info* out);
@@ -90,10 +95,11 @@ struct tsg_scanner;
 int tsg_debug_scanner_engine(struct tsg_scanner* s, uint64_t out[4]);
 
 /* Where a scanner makes the findings of HBM-resident batches (tsg_batch.dev_arena):
- * on = 1 the GPU (trivy_amd/csrc/materialize.h, the default; TSG_GPU_FINDINGS=0
- * at scanner creation turns it off), 0 the host.  Returns the previous setting,
- * -1 for a scanner without a GPU engine.  (A/B and parity tests.) */
-int tsg_debug_scanner_gpu_findings(struct tsg_scanner* s, int on);
+ * mode 1 the GPU (trivy_amd/csrc/materialize.h), 0 the host, 2 (the default;
+ * TSG_GPU_FINDINGS at scanner creation) the GPU while the exact host pass is
+ * the bound (the last scan's outlasted 1.5x its GPU phase).  Returns the
+ * previous mode, -1 for a scanner without a GPU engine.  (A/B and parity tests.) */
+int tsg_debug_scanner_gpu_findings(struct tsg_scanner* s, int mode);
 
 /* Thread-local text of the last error. */
 const char* tsg_last_error(void);

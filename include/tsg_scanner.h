@@ -63,6 +63,21 @@ typedef struct tsg_result tsg_result;
 
 /* Compile the rule set (keyword/anchor automaton + relaxed NFAs) and bind a HIP device. */
 int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out);
+
+/* Compiler options (versioned like tsg_batch_ext: struct_size first, unknown
+ * sizes refused).  v1: calib / calib_bytes, an optional sample of the bytes
+ * the scanner will see (e.g. the first batch of a scan job): a rule with both
+ * a literal and a class-run anchor then takes the one that fires less on it
+ * (trivy_amd/csrc/rules.h CompileOptions).  Findings never depend on it --
+ * only which prefilter item finds the candidates. */
+typedef struct tsg_compile_options {
+  uint32_t struct_size;
+  uint32_t reserved;
+  const uint8_t* calib;
+  uint64_t calib_bytes;
+} tsg_compile_options;
+#define TSG_COMPILE_OPTIONS_SIZE_V1 ((uint32_t)(offsetof(tsg_compile_options, calib_bytes) + sizeof(uint64_t)))
+int tsg_scanner_new_ex(const tsg_global* g, int device, const tsg_compile_options* opt, tsg_scanner** out);
 void tsg_scanner_free(tsg_scanner* s);
 /* 1 if path is globally allowed (Global.AllowPath), else 0. */
 int tsg_scanner_allow_path(const tsg_scanner* s, const char* path, uint64_t len);

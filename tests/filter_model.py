@@ -25,13 +25,21 @@ class RuleInfo(c.Structure):  # tsg_debug_rule_info (include/tsg_debug.h)
 
 
 class FilterModel:
-    def __init__(self, rules):
+    def __init__(self, rules, calibration=None):
+        """calibration: a byte sample for the compiler's anchor choice (tsg_compile_options)."""
+        from trivy_amd.secret.scanner import compile_options
         L = _lib.lib()
         self._cg = CGlobal(rules, [], [])
         h = c.c_void_p()
-        L.tsg_debug_compile.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
-        if L.tsg_debug_compile(c.byref(self._cg.g), c.byref(h)) != 0:
+        L.tsg_debug_compile_ex.argtypes = [c.c_void_p, c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_uint32)]
+        opt = None
+        if calibration is not None:
+            self._calib, opt = compile_options(calibration)
+        ncal = c.c_uint32()
+        if L.tsg_debug_compile_ex(c.byref(self._cg.g), c.byref(opt) if opt is not None else None, c.byref(h),
+                                  c.byref(ncal)) != 0:
             raise ValueError(_lib.last_error())
+        self.n_calibrated = ncal.value
         self.h = h
         L.tsg_debug_filter.argtypes = [c.c_void_p] + [c.c_void_p] * 9
         shape = (c.c_uint32 * 3)()

@@ -60,8 +60,10 @@ def _pack(contents):
     return arena, offs
 
 
-def _check(rules, contents):
-    model = FilterModel(rules)
+def _check(rules, contents, calibration=None):
+    model = FilterModel(rules, calibration=calibration)
+    if calibration is not None:
+        assert model.n_calibrated >= 1  # (the samples below make the compiler move an anchor)
     anchors = _anchors(model)
     arena, offs = _pack(contents)
     hits, folds = model.run(arena, offs)
@@ -216,3 +218,26 @@ def test_class_run_anchors_cover_matches():
     rng = random.Random(11)
     n, _ = _check(rules, _planted_texts(rng, rules[-len(srcs):], 60))
     assert n > 40
+
+
+def _calibration_sample(seed):
+    """Bytes in which some builtin literal anchors are common words (linear, heroku, intercom,
+    mailgun ...) and hex / base64 runs are rare: the compiler then anchors those rules on their
+    class runs (tsg_compile_options)."""
+    rng = random.Random(seed)
+    words = [b"linear ", b"linear-gradient(", b"heroku ", b"intercom ", b"mailgun ", b"asana ", b"discord ",
+             b"the ", b"value = ", b"x", b"\n", b"if (a) ", b"return b; "]
+    return b"".join(rng.choice(words) for _ in range(200000))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_calibrated_anchors_cover_matches(seed):
+    """With a calibration sample the rule compiler may anchor a rule on a class run instead of its
+    literal (rules.cpp CompileRules): every match must still be covered (the class run is a fixed run
+    every match holds, at a bounded offset)."""
+    rules = builtin_rules()
+    rng = random.Random(500 + seed)
+    texts = _planted_texts(rng, rules, 120)
+    texts += [b"color: linear-gradient(" + t for t in texts[:20]]
+    n, _ = _check(rules, texts, calibration=_calibration_sample(seed))
+    assert n > 50

@@ -234,3 +234,58 @@ def test_c3_global_table_kernel_variants_match_cpuref(tmp_path, monkeypatch, env
     bad, first = full_diff(res, ref, C.n_files)
     assert bad == 0, (bad, C.path(first) if first is not None else None)
     assert st["findings"] > 100
+
+
+def _resident(s, C):
+    """C's arena and offsets copied to HBM, scanned from there (the bench's resident path: the GPU
+    finding materialisation, materialize.hip, needs the arena in HBM)."""
+    import torch
+    d_arena = torch.from_numpy(np.ascontiguousarray(C.arena)).to("cuda:0")
+    d_offs = torch.from_numpy(np.ascontiguousarray(C.offsets).view(np.int64)).to("cuda:0")
+    res = s.scan_arena(C.arena, C.offsets, C.path_ptrs, dev_arena=d_arena.data_ptr(), dev_offsets=d_offs.data_ptr())
+    torch.cuda.synchronize()
+    return res
+
+
+def test_c2_corpus_resident_gpu_findings_calibrated_every_file():
+    """The bench's exact configuration at 256 MB: a scanner compiled with a calibration sample (the
+    corpus head; a rule compiler anchor choice: linear-client-secret on its class run), the arena in
+    HBM, findings made on the GPU (materialize.hip) -- every file byte-identical to the restated
+    reference CPU scan."""
+    from bench import full_diff
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    C = corpus.generate(int(256e6), seed=corpus.SEED + 23)
+    s = secret.NewScanner(None, calibration=C.arena[:16000000])
+    assert any("(calibrated)" in s.rule_anchor(i) for i in range(len(s.Rules)))
+    s.set_gpu_findings(True)
+    res = _resident(s, C)
+    ref = _cpuref(C)
+    bad, first = full_diff(res, ref, C.n_files)
+    assert bad == 0, (bad, C.path(first) if first is not None else None)
+    assert res.stats()["findings"] > 500
+
+
+def test_c3f_resident_gpu_findings_every_file(tmp_path):
+    """C3f (finding-dense: the materialisation's target) resident in HBM with GPU findings: every
+    file vs the restated reference CPU scan, a sample vs the oracle."""
+    from bench import full_diff
+    from trivy_amd import corpus
+    import trivy_amd.secret as secret
+    y, samples = corpus.c3_rules(fullscan_share=0.05)
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(y)
+    C = corpus.generate_c3(int(48e6), samples, seed=corpus.SEED + 29, secrets_per_byte=1.0 / 16384)
+    s = secret.NewScanner(secret.ParseConfig(str(cfg)), calibration=C.arena[:4000000])
+    s.set_gpu_findings(True)
+    res = _resident(s, C)
+    ref = _cpuref(C, cfg_path=str(cfg))
+    bad, first = full_diff(res, ref, C.n_files)
+    assert bad == 0, (bad, C.path(first) if first is not None else None)
+    assert res.stats()["findings"] > 20000
+    rng = random.Random(8)
+    sizes = np.diff(C.offsets.astype(np.int64))
+    small = [i for i in range(C.n_files) if sizes[i] < 200000]
+    chosen = sorted(rng.sample(small, 60))
+    want = _oracle([(i, C.path(i), C.content(i)) for i in chosen], str(cfg))
+    assert _check(C, res, chosen, want) > 10

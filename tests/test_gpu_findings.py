@@ -82,11 +82,11 @@ def test_gpu_findings_edge_cases_vs_oracle_and_host(seed):
     files = _edge_files(seed)
     s = secret.NewScanner(None)
     o = osc.new_scanner(None)
-    assert s.set_gpu_findings(True) == 1  # (the default)
+    assert s.set_gpu_findings(True) == 2  # (the default: auto)
     gpu, r = _resident_scan(s, files)
     s.set_gpu_findings(False)
     host, _ = _resident_scan(s, files)
-    s.set_gpu_findings(True)
+    s.set_gpu_findings(2)
     n = 0
     for (p, b), g, h in zip(files, gpu, host):
         want = o.scan(p, b)
@@ -114,6 +114,7 @@ def test_gpu_findings_dense_corpus_vs_oracle():
         out.append(b[last:])
         files.append((p, b"".join(out)))
     s = secret.NewScanner(None)
+    s.set_gpu_findings(True)
     o = osc.new_scanner(None)
     got, _ = _resident_scan(s, files)
     n = 0

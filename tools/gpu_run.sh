@@ -1,14 +1,15 @@
-# Round-4 GPU iteration: stages chosen by STAGES (space-separated), each under its own time limit,
-# stopping at the first failure.  Usage: gpurun -- 'TAG=r04a STAGES="tests bench diag prof" bash tools/gpu_r04.sh'
-#   tests  : the -m gpu suite (PYTEST_ARGS narrows it)
+# GPU iteration runner (rounds 5-6): stages chosen by STAGES (space-separated), each under its own time limit,
+# stopping at the first failure.  Usage: gpurun -- 'TAG=r04a STAGES="tests bench diag prof" bash tools/gpu_run.sh'
+#   tests  : the -m gpu suite (PYTEST_K: a -k expression; PYTEST_ARGS: more words)
 #   smoke  : __graft_entry__.smoke()
 #   bench  : the driver-style default line (20 steps, 5 warm-up, CPU baseline, parity, ingest leg)
 #   quick  : C2 without the CPU baseline (BENCH_ARGS adds flags)
 #   diag   : C2 confirm-kernel split (TSG_DIAG_CONFIRM 4 / 8 / 16), 5 steps each
 #   prof   : rocprofv3 --kernel-trace --stats of a short C2 run
-#   wl     : the workloads in WLS (default c3 c3f c4 c1fs c5), with CPU baselines unless WL_ARGS says otherwise
+#   wl     : the workloads in WLS (default c3 c3f c4 c1fs c5), with CPU baselines unless WL_ARGS says otherwise;
+#            WL_ARGS_<wl> adds flags for one workload
 set -o pipefail
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 STAGES=${STAGES:-tests bench}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -16,7 +17,7 @@ R=$GRAFT_REPO_ROOT
 for st in $STAGES; do
   case $st in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests_$TAG.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-} > gpurun_out/gpu_tests_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
@@ -34,7 +35,7 @@ for st in $STAGES; do
       rc=$?; python tools/bench_brief.py gpurun_out/quick_$TAG.json; tail -2 gpurun_out/quick_$TAG.err; [ $rc -eq 0 ] || exit $rc ;;
     diag)
       for d in 0 4 8 16; do
-        TSG_DIAG_CONFIRM=$d timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --ingest-steps 0 > gpurun_out/diag${d}_$TAG.json 2> gpurun_out/diag${d}_$TAG.err
+        TSG_DIAG_CONFIRM=$d timeout -k 10 300 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --ingest-steps 0 ${BENCH_ARGS:-} > gpurun_out/diag${d}_$TAG.json 2> gpurun_out/diag${d}_$TAG.err
         rc=$?; echo "== diag $d"; python tools/bench_brief.py gpurun_out/diag${d}_$TAG.json; [ $rc -eq 0 ] || exit $rc
       done ;;
     prof)
@@ -63,6 +64,26 @@ for st in $STAGES; do
     dump)  # candidates of one C3f scan for tools/host_tail_bench.py (CPU profiling of the exact pass)
       TSG_TAIL_DEBUG=1 TSG_DUMP_CANDS=$R/gpurun_out/cands_${DUMP_WL:-c3f}.bin timeout -k 10 600 python bench.py --workload ${DUMP_WL:-c3f} --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dump_$TAG.json 2> gpurun_out/dump_$TAG.err
       rc=$?; ls -la gpurun_out/cands_${DUMP_WL:-c3f}.bin; grep -a "tail" gpurun_out/dump_$TAG.err | tail -4; [ $rc -eq 0 ] || exit $rc ;;
+    c4l)  # C4 under several bench arg sets (C4L_SPECS, '|'-separated), e.g. "--layers 1|--layers 5 --layer-parallel 3"
+      IFS='|' read -r -a specs <<< "${C4L_SPECS:---layers 1}"
+      for i in "${!specs[@]}"; do
+        timeout -k 10 600 python bench.py --workload c4 --steps ${C4_STEPS:-5} --warmup 2 --no-cpu-baseline ${specs[$i]} > gpurun_out/c4l_${TAG}_$i.json 2> gpurun_out/c4l_${TAG}_$i.err
+        rc=$?; echo "== c4 [$i] ${specs[$i]}"; python tools/bench_brief.py gpurun_out/c4l_${TAG}_$i.json; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    walkprof)  # the C4 tar walk alone on the box's host cores (no GPU), with the sampling profiler
+      SPROF=$R/gpurun_out/walkprof_$TAG.txt TSG_WALK_DEBUG=1 timeout -k 10 600 python tools/walk_bench.py --gb ${WALK_GB:-15} --reps 3 > gpurun_out/walkprof_$TAG.log 2>&1
+      rc=$?; grep -v "^index:" gpurun_out/walkprof_$TAG.log | tail -4; [ $rc -eq 0 ] || exit $rc
+      python tools/sprof/report.py gpurun_out/walkprof_$TAG.txt libtsg_host > gpurun_out/walkprof_${TAG}_fn.txt 2>&1
+      python tools/sprof/report.py gpurun_out/walkprof_$TAG.txt libtsg_host lines > gpurun_out/walkprof_${TAG}_lines.txt 2>&1
+      head -30 gpurun_out/walkprof_${TAG}_fn.txt ;;
+    tailprof)  # the exact host pass on the box's cores over a dumped candidate list (TAIL_CANDS, TAIL_WL)
+      TSG_TAIL_DEBUG=1 timeout -k 10 600 python tools/host_tail_bench.py ${TAIL_CANDS} --workload ${TAIL_WL:-c2} --gb ${TAIL_GB:-20} --reps 5 > gpurun_out/tailprof_$TAG.log 2>&1
+      rc=$?; grep "serial\|tail \|phases" gpurun_out/tailprof_$TAG.log | tail -6; [ $rc -eq 0 ] || exit $rc ;;
+    dumps)  # candidates of one C2 and one C3f scan (tools/host_tail_bench.py)
+      for wl in c2 c3f; do
+        TSG_DUMP_CANDS=$R/gpurun_out/cands_${wl}_$TAG.bin timeout -k 10 600 python bench.py --workload $wl --steps 1 --warmup 0 --warmup-s 0 --ingest-steps 0 --no-cpu-baseline > gpurun_out/dump_${wl}_$TAG.json 2> gpurun_out/dump_${wl}_$TAG.err
+        rc=$?; ls -la gpurun_out/cands_${wl}_$TAG.bin; [ $rc -eq 0 ] || exit $rc
+      done ;;
     large)  # the > 4 GiB transformed-file test alone (last: it moves ~9 GB through the box)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_large_file.py -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_large_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_large_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
@@ -122,9 +143,17 @@ PYEOF
         cat $R/gpurun_out/fetch_${TAG}_$c.txt
       done
       cd $R ;;
+    runs)  # bench lines RUNS="name:args|name:args" (each its own time limit), e.g. "c3f6:--workload c3f --depth 6"
+      IFS='|' read -r -a rs <<< "${RUNS}"
+      for r in "${rs[@]}"; do
+        n="${r%%:*}"; a="${r#*:}"
+        timeout -k 10 600 python bench.py $a > gpurun_out/run_${TAG}_$n.json 2> gpurun_out/run_${TAG}_$n.err
+        rc=$?; echo "== $n ($a)"; python tools/bench_brief.py gpurun_out/run_${TAG}_$n.json; tail -1 gpurun_out/run_${TAG}_$n.err; [ $rc -eq 0 ] || exit $rc
+      done ;;
     wl)
       for wl in ${WLS:-c3 c3f c4 c1fs c5}; do
-        timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
+        xv="WL_ARGS_$wl"  # per-workload flags (WL_ARGS_c3f="--steps 20"; the last --steps wins)
+        timeout -k 10 900 python bench.py --workload $wl --steps 5 --warmup 2 ${WL_ARGS:-} ${!xv:-} > gpurun_out/wl_${TAG}_$wl.json 2> gpurun_out/wl_${TAG}_$wl.err
         rc=$?; echo "== $wl"; python tools/bench_brief.py gpurun_out/wl_${TAG}_$wl.json; tail -2 gpurun_out/wl_${TAG}_$wl.err; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac

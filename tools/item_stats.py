@@ -36,9 +36,17 @@ def item_occ(fm, a, it):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=float, default=16)
+    ap.add_argument("--calib-mb", type=float, default=0,
+                    help="compile with a calibration sample of this size (tsg_compile_options), generated with "
+                         "another seed than the evaluated sample")
     args = ap.parse_args()
     rules = builtin_rules()
-    fm = FilterModel(rules)
+    calib = None
+    if args.calib_mb > 0:
+        K = corpus.generate(int(args.calib_mb * 1e6), seed=corpus.SEED + 7777)
+        calib = K.arena[:K.n_bytes].copy()
+    fm = FilterModel(rules, calibration=calib)
+    print("anchors moved by the calibration sample: %d" % fm.n_calibrated)
     C = corpus.generate(int(args.mb * 1e6))
     a = C.arena[:C.n_bytes]
     print("sample: %d files, %.1f MB" % (C.n_files, C.n_bytes / 1e6))

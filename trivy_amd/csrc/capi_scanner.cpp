@@ -165,7 +165,27 @@ void JsonStr(std::string* o, const std::string& s) {
 
 extern "C" {
 
+namespace {
+bool CompileOpts(const tsg_compile_options* o, tsg::CompileOptions* co) {
+  if (!o) return true;
+  if (o->struct_size != TSG_COMPILE_OPTIONS_SIZE_V1) {
+    tsg::SetError("tsg_compile_options.struct_size " + std::to_string(o->struct_size) +
+                  " is not a size this library knows (v1 = " + std::to_string(TSG_COMPILE_OPTIONS_SIZE_V1) + ")");
+    return false;
+  }
+  co->calib = o->calib;
+  co->calib_n = o->calib ? o->calib_bytes : 0;
+  return true;
+}
+}  // namespace
+
 int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out) {
+  return tsg_scanner_new_ex(g, device, nullptr, out);
+}
+
+int tsg_scanner_new_ex(const tsg_global* g, int device, const tsg_compile_options* opt, tsg_scanner** out) {
+  tsg::CompileOptions co;
+  if (!CompileOpts(opt, &co)) return -1;
   std::string err;
   std::vector<tsg::RuleSpec> rules;
   std::vector<tsg::AllowRuleSpec> allow;
@@ -176,7 +196,7 @@ int tsg_scanner_new(const tsg_global* g, int device, tsg_scanner** out) {
     return -1;
   }
   std::unique_ptr<tsg_scanner> s(new tsg_scanner());
-  s->s.reset(new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), device, &err));
+  s->s.reset(new tsg::SecretScanner(std::move(rules), std::move(allow), std::move(exclude), device, &err, &co));
   if (!s->s->ok()) {
     tsg::SetError(err.empty() ? s->s->error() : err);
     return -2;
@@ -519,7 +539,12 @@ const char* tsg_scanner_rule_anchor(const tsg_scanner* s, uint32_t i) {
 
 // ---- tsg_debug.h: rule compiler inspection (no GPU) ------------------------
 
-int tsg_debug_compile(const tsg_global* g, tsg_compiled** out) {
+int tsg_debug_compile(const tsg_global* g, tsg_compiled** out) { return tsg_debug_compile_ex(g, nullptr, out, nullptr); }
+
+int tsg_debug_compile_ex(const tsg_global* g, const tsg_compile_options* opt, tsg_compiled** out,
+                         uint32_t* out_calibrated) {
+  tsg::CompileOptions co;
+  if (!CompileOpts(opt, &co)) return -1;
   std::string err;
   std::vector<tsg::RuleSrc> src;
   for (uint32_t i = 0; i < g->n_rules; i++) {
@@ -529,10 +554,11 @@ int tsg_debug_compile(const tsg_global* g, tsg_compiled** out) {
     src.push_back(std::move(s));
   }
   std::unique_ptr<tsg_compiled> c(new tsg_compiled());
-  if (!tsg::CompileRules(src, &c->cr, &err)) {
+  if (!tsg::CompileRules(src, &c->cr, &err, &co)) {
     tsg::SetError(err);
     return -1;
   }
+  if (out_calibrated) *out_calibrated = c->cr.n_calibrated_anchors;
   *out = c.release();
   return 0;
 }

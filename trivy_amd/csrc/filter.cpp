@@ -56,17 +56,36 @@ B256 ToB256(const ByteSet& s) {
   return r;
 }
 
+// T[g * 256 + m] = prior mass of mask m over bytes 8g..8g+7
+std::vector<double> PriorTable(const std::vector<double>& f) {
+  std::vector<double> t(32 * 256, 0.0);
+  for (int g = 0; g < 32; g++)
+    for (int m = 0; m < 256; m++)
+      for (int k = 0; k < 8; k++)
+        if ((m >> k) & 1) t[size_t(g) * 256 + size_t(m)] += f[size_t(8 * g + k)];
+  return t;
+}
+
+// The prior of the BuildFilter / ItemWindow call running on this thread: the
+// static one, or a calibration sample's byte frequencies (CompileOptions).
+thread_local const std::vector<double>* t_prior_table = nullptr;
+
+struct PriorScope {
+  std::vector<double> table;
+  const std::vector<double>* saved;
+  explicit PriorScope(const std::vector<double>* prior) : saved(t_prior_table) {
+    if (prior) {
+      table = PriorTable(*prior);
+      t_prior_table = &table;
+    }
+  }
+  ~PriorScope() { t_prior_table = saved; }
+};
+
 // P(byte in s) under the prior: 32 lookups of 8-byte groups.
 double SetProb(const B256& s) {
-  static const std::vector<double> T = [] {  // T[g * 256 + m] = prior mass of mask m over bytes 8g..8g+7
-    const auto& f = BytePrior();
-    std::vector<double> t(32 * 256, 0.0);
-    for (int g = 0; g < 32; g++)
-      for (int m = 0; m < 256; m++)
-        for (int k = 0; k < 8; k++)
-          if ((m >> k) & 1) t[size_t(g) * 256 + size_t(m)] += f[size_t(8 * g + k)];
-    return t;
-  }();
+  static const std::vector<double> T_static = PriorTable(BytePrior());
+  const std::vector<double>& T = t_prior_table ? *t_prior_table : T_static;
   if (s.all()) return 1.0;
   double p = 0;
   for (int g = 0; g < 32; g++) p += T[size_t(g) * 256 + ((s.w[g >> 3] >> (8 * (g & 7))) & 0xFF)];
@@ -107,8 +126,27 @@ double Cost(const B256* u) { return WindowProb(u, kFilterSlots); }  // unused sl
 
 }  // namespace
 
+void ItemWindow(const FilterItem& it, uint32_t window, size_t* start, size_t* len, const std::vector<double>* prior) {
+  PriorScope scope(prior);
+  const size_t m = it.sets.size();
+  size_t w = 0, wl = std::min<size_t>(m, window);
+  double best = std::numeric_limits<double>::infinity();
+  for (size_t s = 0; s + wl <= m; s++) {
+    B256 win[kFilterSlots];
+    for (size_t q = s; q < s + wl; q++) win[q - s] = ToB256(it.sets[q]);
+    const double c = WindowProb(win, int(wl));
+    if (c < best) {
+      best = c;
+      w = s;
+    }
+  }
+  *start = w;
+  *len = wl;
+}
+
 bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t n_buckets, FilterTables* out,
-                 std::string* err) {
+                 std::string* err, const std::vector<double>* prior) {
+  PriorScope scope(prior);
   if ((n_buckets != 8 && n_buckets != 16) || window < 2 || window > uint32_t(kFilterSlots)) {
     *err = "unsupported prefilter shape";
     return false;
@@ -127,6 +165,7 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     std::map<std::string, size_t> seen;
     for (auto& it : items) {
       std::string key(1, char(it.kind));
+      key += char('0' + it.group);
       key += std::to_string(it.lit_end) + ":";
       for (auto& b : it.sets) key += b.to_string();
       auto f = seen.find(key);
@@ -152,17 +191,8 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     }
     const size_t m = it.sets.size();
     // least frequent window of <= kFilterSlots positions
-    size_t w = 0, wl = std::min<size_t>(m, S);
-    double best = std::numeric_limits<double>::infinity();
-    for (size_t s = 0; s + wl <= m; s++) {
-      B256 win[kFilterSlots];
-      for (size_t q = s; q < s + wl; q++) win[q - s] = ToB256(it.sets[q]);
-      const double c = WindowProb(win, int(wl));
-      if (c < best) {
-        best = c;
-        w = s;
-      }
-    }
+    size_t w = 0, wl = 0;
+    ItemWindow(it, S, &w, &wl, nullptr);  // (under this call's prior)
     for (int s = 0; s < kFilterSlots; s++) cl[i].u[s].set_all();
     for (size_t q = 0; q < wl; q++) cl[i].u[S - wl + q] = ToB256(it.sets[w + q]);
     cl[i].members = {uint32_t(i)};
@@ -218,7 +248,7 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
     }
   }
   auto delta_of = [&](size_t i, size_t j) {
-    if (solo[i] || solo[j]) return std::numeric_limits<double>::infinity();
+    if (solo[i] || solo[j] || uniq[i].group != uniq[j].group) return std::numeric_limits<double>::infinity();
     B256 u[kFilterSlots];
     return merged(cl[i], cl[j], u) - cl[i].cost - cl[j].cost;
   };
@@ -246,6 +276,10 @@ bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t
         bi = i;
         bj = best[i];
       }
+    if (bd == kInf) {  // (more solo items / groups than buckets)
+      *err = "prefilter: no bucket merge left (solo items or groups exceed the buckets)";
+      return false;
+    }
     if (bj < bi) std::swap(bi, bj);
     B256 u[kFilterSlots];
     double c = merged(cl[bi], cl[bj], u);

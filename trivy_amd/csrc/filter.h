@@ -86,7 +86,13 @@ TSG_HOST_DEVICE inline uint32_t WindowHash(uint64_t key, uint32_t bits) {
 // Static byte-frequency prior of source/text bytes (sums to 1).
 const std::vector<double>& BytePrior();
 
+// prior: byte frequencies to use instead of BytePrior() (a calibration sample's, CompileOptions)
 bool BuildFilter(const std::vector<FilterItem>& items, uint32_t window, uint32_t n_buckets, FilterTables* out,
-                 std::string* err);
+                 std::string* err, const std::vector<double>* prior = nullptr);
+
+// The window BuildFilter keeps of an item: its least likely `window` (or fewer)
+// consecutive positions under the prior, [*start, *start + *len).
+void ItemWindow(const FilterItem& it, uint32_t window, size_t* start, size_t* len,
+                const std::vector<double>* prior = nullptr);
 
 }  // namespace tsg

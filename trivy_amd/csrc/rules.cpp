@@ -1,6 +1,7 @@
 // Rule compiler (see rules.h).  Superset arguments are in DESIGN.md §2-3.
 #include "rules.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 #include "filter.h"
@@ -316,7 +317,13 @@ bool ExactSet(const Node& n, ByteSet* out);
 // likely 6-position window is below kClassRunMaxProb (printable-uniform prior);
 // a commoner run would cost more than the gated full scans.
 constexpr double kClassRunMaxProb = 1e-5;
-bool ExtractClassRun(const Regex& re, Cand* best) {
+// with a calibration sample (CompileOptions) a rule with a literal anchor also
+// considers class runs up to this prior probability: the sample decides
+constexpr double kClassRunCalibProb = 1e-3;
+// every_run (calibration): each run under max_prob that is not simply a literal
+// (a run of literal characters is the literal anchor's business), by prior
+bool ExtractClassRun(const Regex& re, Cand* best, double max_prob = kClassRunMaxProb,
+                     std::vector<std::pair<double, Cand>>* every_run = nullptr) {
   const std::vector<Node>& nodes = re.nodes();
   Analyzer an(nodes, false), anf(nodes, true);
   std::vector<int> items;
@@ -328,7 +335,7 @@ bool ExtractClassRun(const Regex& re, Cand* best) {
     return double(n) / 97.0;
   };
   int64_t olo = 0, ohi = 0, ohf = 0;
-  double best_p = kClassRunMaxProb;
+  double best_p = max_prob;
   bool have = false;
   for (size_t k = 0; k < items.size() && ohi < kInf; k++) {
     std::vector<int> pos;
@@ -366,8 +373,7 @@ bool ExtractClassRun(const Regex& re, Cand* best) {
         for (size_t q = a; q < a + wl; q++) pw *= ps[q];
         p_run = a == 0 ? pw : std::min(p_run, pw);
       }
-      if (p_run < best_p) {
-        best_p = p_run;
+      auto make = [&]() {
         Cand cd{{std::string(pos.size(), '\x01')}, olo, ohi};
         cd.ohi_fold = ohf;
         cd.follow.push_back(std::vector<int>(items.begin() + long(j), items.end()));
@@ -375,7 +381,16 @@ bool ExtractClassRun(const Regex& re, Cand* best) {
         cd.pre_k = k;
         cd.variants.push_back({cd.lits[0], pos});
         cd.class_run = true;
-        *best = cd;
+        return cd;
+      };
+      if (every_run && p_run < max_prob) {
+        bool literal = true;
+        for (size_t q = k; q < j && literal; q++) literal = LitChar(nodes[items[q]]) >= 0;
+        if (!literal) every_run->push_back({p_run, make()});
+      }
+      if (p_run < best_p) {
+        best_p = p_run;
+        *best = make();
         have = true;
       }
     }
@@ -1075,7 +1090,91 @@ std::vector<std::string> RequiredLiterals(const Regex& re) {
   return best.lits;
 }
 
-bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err) {
+namespace {
+
+// The prefilter item of anchor literal li of `best`: the sets before it, the
+// literal's sets (the union over same-folded variants), the lookahead sets.
+FilterItem AnchorItem(const Regex& re, const Cand& best, size_t li, uint32_t aid) {
+  const std::string& l = best.lits[li];
+  FilterItem fi;
+  fi.kind = kItemAnchor;
+  fi.id = aid;
+  std::vector<int> top;
+  Analyzer(re.nodes(), false).Flatten(re.root(), &top);
+  fi.sets = BeforeSets(re.nodes(), top, best.pre_k, 16);
+  std::vector<ByteSet> lit(l.size());
+  for (auto& v : best.variants) {
+    if (v.first != l) continue;
+    for (size_t q = 0; q < l.size() && q < v.second.size(); q++) {
+      ByteSet b;
+      if (ExactSet(re.nodes()[v.second[q]], &b)) lit[q] |= b;
+      else lit[q].set();
+    }
+  }
+  for (auto& b : lit)
+    if (b.none()) b.set();
+  fi.sets.insert(fi.sets.end(), lit.begin(), lit.end());
+  fi.lit_end = uint32_t(fi.sets.size());
+  // the tighter of the two lookahead computations, position by position
+  // (both are supersets of every match's bytes; the exact one stops
+  // early on non-ASCII sets, the relaxed one on ended fixed items)
+  auto after = AfterSets(re.nodes(), best.follow[li], 16);
+  const auto exact = AfterSetsExact(re.nodes(), best.follow[li], 16);
+  for (size_t q = 0; q < exact.size(); q++) {
+    if (q < after.size()) after[q] &= exact[q];
+    else after.push_back(exact[q]);
+  }
+  fi.sets.insert(fi.sets.end(), after.begin(), after.end());
+  return fi;
+}
+
+uint32_t FilterWindow() {
+  const char* e = std::getenv("TSG_FILTER_WINDOW");  // model experiments
+  return e ? uint32_t(std::atoi(e)) : 6u;
+}
+
+// What an item costs on a calibration sample: the positions where its
+// prefilter window matches (K1 fires, each a flagged block for K2) plus those
+// where the whole item does (K2's exact anchor-item matches).
+uint64_t SampleCost(const FilterItem& it, const uint8_t* a, uint64_t n, const std::vector<double>* prior) {
+  const size_t m = it.sets.size();
+  if (m == 0 || n < m) return 0;
+  size_t ws = 0, wl = 0;
+  ItemWindow(it, FilterWindow(), &ws, &wl, prior);
+  std::vector<std::array<uint8_t, 256>> T(m);
+  for (size_t q = 0; q < m; q++)
+    for (int b = 0; b < 256; b++) T[q][size_t(b)] = it.sets[q].test(size_t(b)) ? 1 : 0;
+  size_t piv = ws;  // the window's narrowest position first
+  for (size_t q = ws; q < ws + wl; q++)
+    if (it.sets[q].count() < it.sets[piv].count()) piv = q;
+  uint64_t win = 0, item = 0;
+  for (uint64_t p = 0; p + m <= n; p++) {
+    if (!T[piv][a[p + piv]]) continue;
+    bool ok = true;
+    for (size_t q = ws; q < ws + wl && ok; q++) ok = T[q][a[p + q]] != 0;
+    if (!ok) continue;
+    win++;
+    for (size_t q = 0; q < m && ok; q++) ok = T[q][a[p + q]] != 0;
+    item += ok;
+  }
+  return win + item;
+}
+
+}  // namespace
+
+bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err, const CompileOptions* opt) {
+  // a calibration sample's byte frequencies replace the static prior of the
+  // prefilter's window choice and clustering (TSG_CALIB_PRIOR=0: keep the static one)
+  std::vector<double> cal_prior;
+  const std::vector<double>* cal_prior_p = nullptr;
+  const char* cp_env = std::getenv("TSG_CALIB_PRIOR");
+  if (opt && opt->calib && opt->calib_n && (!cp_env || std::atoi(cp_env) != 0)) {
+    std::vector<uint64_t> h(256, 0);
+    for (uint64_t i = 0; i < opt->calib_n; i++) h[opt->calib[i]]++;
+    cal_prior.resize(256);
+    for (int b = 0; b < 256; b++) cal_prior[size_t(b)] = (double(h[size_t(b)]) + 0.5) / (double(opt->calib_n) + 128.0);
+    cal_prior_p = &cal_prior;
+  }
   std::map<std::string, uint32_t> kw_ids;
   out->rules.clear();
   out->regex.clear();
@@ -1160,9 +1259,45 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
       Cand best{{}, 0, 0};
       const char* cr_env = std::getenv("TSG_CLASS_RUNS");  // 0: literal anchors only (full-scan tests)
       const bool class_runs = !cr_env || std::atoi(cr_env) != 0;
-      if (ExtractAnchor(*re, &best) || (class_runs && ExtractClassRun(*re, &best))) {
+      bool have = ExtractAnchor(*re, &best);
+      bool calibrated = false;
+      if (!have) {
+        have = class_runs && ExtractClassRun(*re, &best);
+      } else if (class_runs && opt && opt->calib && opt->calib_n) {
+        // both kinds of anchor: the calibration sample decides (the class run
+        // when it costs under half the literal's, and the literal is not rare)
+        Cand run{{}, 0, 0};
+        std::vector<std::pair<double, Cand>> runs;
+        ExtractClassRun(*re, &run, kClassRunCalibProb, &runs);
+        if (!runs.empty()) {
+          uint64_t c_lit = 0;
+          for (size_t li = 0; li < best.lits.size(); li++)
+            c_lit += SampleCost(AnchorItem(*re, best, li, 0), opt->calib, opt->calib_n, cal_prior_p);
+          // only a literal that fires often enough to matter (>= 1e-4 per sample byte) is moved:
+          // the moved items' windows take buckets of their own (FilterItem::group)
+          const uint64_t kCalibMinCost = std::max<uint64_t>(16, opt->calib_n / 10000);
+          std::sort(runs.begin(), runs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+          if (runs.size() > 4) runs.resize(4);  // the likeliest candidates by the prior
+          for (auto& cr : runs) {
+            if (c_lit < kCalibMinCost) break;  // a rare literal stays
+            const uint64_t c_run = SampleCost(AnchorItem(*re, cr.second, 0, 0), opt->calib, opt->calib_n, cal_prior_p);
+            if (std::getenv("TSG_CALIB_DEBUG"))
+              std::fprintf(stderr, "calib %s: literal %llu, class run of %zu at [%lld,%lld] %llu\n", r.id.c_str(),
+                           (unsigned long long)c_lit, cr.second.lits[0].size(), (long long)cr.second.olo,
+                           (long long)cr.second.ohi, (unsigned long long)c_run);
+            if (2 * c_run < c_lit) {
+              best = cr.second;
+              c_lit = c_run;
+              calibrated = true;
+            }
+          }
+          if (calibrated) out->n_calibrated_anchors++;
+        }
+      }
+      if (have) {
         rg.anchored = 1;
         desc = "[" + std::to_string(best.olo) + "," + std::to_string(best.ohi) + "]";
+        if (calibrated) desc += " (calibrated)";
         for (size_t li = 0; li < best.lits.size(); li++) {
           const std::string& l = best.lits[li];
           uint32_t aid = uint32_t(out->anchors.size());
@@ -1174,38 +1309,8 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
           ai.off_hi_fold = int32_t(std::min<int64_t>(best.ohi_fold, 1 << 30));
           out->anchors.push_back(ai);
           out->anchor_req.push_back(FollowReqs(re->nodes(), best.follow[li]));
-          {  // prefilter item: prefix sets + literal sets (union over same-folded variants) + lookahead sets
-            FilterItem fi;
-            fi.kind = kItemAnchor;
-            fi.id = aid;
-            std::vector<int> top;
-            Analyzer(re->nodes(), false).Flatten(re->root(), &top);
-            fi.sets = BeforeSets(re->nodes(), top, best.pre_k, 16);
-            std::vector<ByteSet> lit(l.size());
-            for (auto& v : best.variants) {
-              if (v.first != l) continue;
-              for (size_t q = 0; q < l.size() && q < v.second.size(); q++) {
-                ByteSet b;
-                if (ExactSet(re->nodes()[v.second[q]], &b)) lit[q] |= b;
-                else lit[q].set();
-              }
-            }
-            for (auto& b : lit)
-              if (b.none()) b.set();
-            fi.sets.insert(fi.sets.end(), lit.begin(), lit.end());
-            fi.lit_end = uint32_t(fi.sets.size());
-            // the tighter of the two lookahead computations, position by position
-            // (both are supersets of every match's bytes; the exact one stops
-            // early on non-ASCII sets, the relaxed one on ended fixed items)
-            auto after = AfterSets(re->nodes(), best.follow[li], 16);
-            const auto exact = AfterSetsExact(re->nodes(), best.follow[li], 16);
-            for (size_t q = 0; q < exact.size(); q++) {
-              if (q < after.size()) after[q] &= exact[q];
-              else after.push_back(exact[q]);
-            }
-            fi.sets.insert(fi.sets.end(), after.begin(), after.end());
-            out->items.push_back(std::move(fi));
-          }
+          out->items.push_back(AnchorItem(*re, best, li, aid));  // prefilter item
+          if (calibrated) out->items.back().group = 1;
           desc += best.class_run ? " <" + std::to_string(l.size()) + " classes>" : " " + l;
         }
       } else {
@@ -1240,11 +1345,10 @@ bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::stri
     }
   }
   {
-    uint32_t nb = 16, nw = 6;
+    uint32_t nb = 16, nw = FilterWindow();
     if (const char* e = std::getenv("TSG_FILTER_BUCKETS")) nb = uint32_t(std::atoi(e));
-    if (const char* e = std::getenv("TSG_FILTER_WINDOW")) nw = uint32_t(std::atoi(e));  // model experiments
     auto ft = std::make_shared<FilterTables>();
-    if (!BuildFilter(out->items, nw, nb, ft.get(), err)) return false;
+    if (!BuildFilter(out->items, nw, nb, ft.get(), err, cal_prior_p)) return false;
     out->filter = ft;
   }
   return true;

@@ -97,6 +97,9 @@ struct FilterItem {
   uint32_t id;       // keyword id / anchor id / fold rune (0 U+0130, 1 U+212A, 2 U+017F)
   uint32_t lit_end;  // anchors: positions from the item start to the literal end
   std::vector<ByteSet> sets;
+  // clustering group: items share buckets only within their group (1: anchors
+  // a calibration sample chose, whose windows the static prior misprices)
+  uint8_t group = 0;
 };
 
 struct CompiledRules {
@@ -114,6 +117,7 @@ struct CompiledRules {
   std::vector<std::unique_ptr<Regex>> regex;  // exact engines (host pass)
   uint32_t n_fullscan_rules = 0;
   uint32_t n_redundant_gates = 0;
+  uint32_t n_calibrated_anchors = 0;  // class-run anchors a calibration sample chose over a literal
 
   uint32_t kw_words() const { return (uint32_t(keywords.size()) + 31) / 32; }
 };
@@ -122,7 +126,19 @@ struct CompiledRules {
 // `re` contains, or empty if none is known.  Used as a MatchString prefilter.
 std::vector<std::string> RequiredLiterals(const Regex& re);
 
+// Optional inputs of the compiler.  calib: a sample of the bytes the scanner
+// will see (e.g. its first batch).  With one, a rule that has both a literal
+// anchor and a class-run anchor takes the one whose prefilter item fires less
+// on the sample (K1 window fires + K2 item matches), instead of the static
+// byte prior's choice -- the prior cannot know that a dictionary word such as
+// `linear` (builtin-rules.go:623) is common in source trees.
+struct CompileOptions {
+  const uint8_t* calib = nullptr;
+  uint64_t calib_n = 0;
+};
+
 // Compile; returns false with *err on a regex/limits error.
-bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err);
+bool CompileRules(const std::vector<RuleSrc>& src, CompiledRules* out, std::string* err,
+                  const CompileOptions* opt = nullptr);
 
 }  // namespace tsg

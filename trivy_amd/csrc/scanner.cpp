@@ -394,7 +394,8 @@ bool Matcher::Match(const uint8_t* s, size_t n) const {
 }
 
 SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleSpec> allow,
-                             std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err)
+                             std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err,
+                             const CompileOptions* opt)
     : rules_(std::move(rules)), allow_(std::move(allow)), exclude_(std::move(exclude)) {
   rule_rank_ = RuleRanks(rules_);
   std::vector<RuleSrc> src;
@@ -410,7 +411,7 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
       src.push_back({"exclude-block:" + rules_[r].id + ":" + std::to_string(k), rules_[r].exclude[k]->pattern(), {},
                      true});
     }
-  if (!CompileRules(src, &cr_, &err_)) {
+  if (!CompileRules(src, &cr_, &err_, opt)) {
     *err = err_;
     return;
   }
@@ -450,9 +451,10 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
       return;
     }
   }
-  // findings of HBM-resident batches made on the GPU (TSG_GPU_FINDINGS=0: on the host)
+  // findings of HBM-resident batches: 2 (default) on the GPU while the exact
+  // pass is the bound, 1 always on the GPU, 0 on the host (TSG_GPU_FINDINGS)
   const char* gf = std::getenv("TSG_GPU_FINDINGS");
-  gpu_findings_.store(!gf || std::atoi(gf) != 0 ? 1 : 0);
+  gpu_findings_.store(gf ? std::max(0, std::min(2, std::atoi(gf))) : 2);
   mat_.reset(new FindingMaterializer(device));
   if (!mat_->ok()) {
     err_ = mat_->error();
@@ -1611,8 +1613,11 @@ bool SecretScanner::HostTail(const BatchInput& in, std::vector<Candidate>* cands
     return t_arena;
   };
   // toFinding / findLocation on the GPU (materialize.h) when the arena is resident in HBM
-  const bool gpu_mat = mat_ && gpu_windows && gpu_findings_.load() != 0 && in.dev_arena && in.dev_offsets &&
-                       !in.file_data;
+  // (auto: when the last scan's exact pass outlasted 1.5x its GPU phase -- finding-dense batches, C3f:
+  // the GPU pass costs GPU time beside the next scans' kernels, which a GPU-bound pipeline (C2) pays)
+  const int gf_mode = gpu_findings_.load();
+  const bool gpu_mat = mat_ && gpu_windows && (gf_mode == 1 || (gf_mode == 2 && host_bound_.load())) &&
+                       in.dev_arena && in.dev_offsets && !in.file_data;
   auto scan_group = [&](size_t k) {
     const size_t a = starts[k], b = starts[k + 1];
     const uint32_t f = group_file(k);
@@ -1776,6 +1781,7 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
       *err = "GPU findings: one file's findings exceed a call's bounds";
       return false;
     }
+    const double f0 = NowMs();
     FindingMaterializer::Job* job = mat_->Begin(uint32_t(b - a), uint32_t(nm), uint32_t(ns), tb, err);
     if (!job) return false;
     MatFile* F = mat_->files(job);
@@ -1801,7 +1807,8 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
       mat_->End(job);
       return false;
     }
-    *ms_gpu += NowMs() - g0;
+    const double g1 = NowMs();
+    *ms_gpu += g1 - g0;
     const FindingOut* fo = mat_->findings(job);
     const LineOut* lo = mat_->lines(job);
     const char* tx = mat_->text(job);
@@ -1821,6 +1828,11 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
       }
     }, wide);
     mat_->End(job);
+    static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;
+    if (times)
+      std::fprintf(stderr, "gpu findings ms: slot+fill %.2f gpu %.2f assemble+sort %.2f (files %zu, findings %llu, "
+                   "spans %llu)\n", g0 - f0, g1 - g0, NowMs() - g1, b - a, (unsigned long long)nm,
+                   (unsigned long long)ns);
     a = b;
   }
   return true;

@@ -247,7 +247,8 @@ class SecretScanner {
  public:
   // device < 0: no GPU engine (test hooks only: tsg_debug_host_tail)
   SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleSpec> allow,
-                std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err);
+                std::vector<std::unique_ptr<Regex>> exclude, int device, std::string* err,
+                const CompileOptions* opt = nullptr);
   bool ok() const {
     if (!compiled_ok_) return false;
     if (no_engine_) return true;
@@ -355,12 +356,12 @@ class SecretScanner {
   // GPU allow-path prefilter (pathfilter.h): built when every path rule has usable literals
   std::unique_ptr<PathFilter> path_filter_;
   std::unique_ptr<FindingMaterializer> mat_;  // GPU findings of HBM-resident batches
-  std::atomic<int> gpu_findings_{1};
+  std::atomic<int> gpu_findings_{2};
 
  public:
-  // 1 / 0: GPU / host findings for HBM-resident batches (tests, A/B); returns the
-  // previous setting, -1 without a GPU engine
-  int SetGpuFindings(int on) { return mat_ ? gpu_findings_.exchange(on ? 1 : 0) : -1; }
+  // 1 / 0 / 2: GPU / host / auto (GPU while host-bound) findings for HBM-resident
+  // batches (tests, A/B); returns the previous setting, -1 without a GPU engine
+  int SetGpuFindings(int mode) { return mat_ ? gpu_findings_.exchange(std::max(0, std::min(2, mode))) : -1; }
 };
 
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.

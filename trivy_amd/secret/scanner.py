@@ -52,6 +52,21 @@ class _CBatchExt(c.Structure):  # tsg_batch_ext: struct_size first, then the fie
 BATCH_EXT_SIZE_V1 = c.sizeof(_CBatchExt)  # TSG_BATCH_EXT_SIZE_V1
 
 
+class _CCompileOptions(c.Structure):  # tsg_compile_options (versioned: struct_size first)
+    _fields_ = [("struct_size", c.c_uint32), ("reserved", c.c_uint32), ("calib", c.c_void_p),
+                ("calib_bytes", c.c_uint64)]
+
+
+COMPILE_OPTIONS_SIZE_V1 = c.sizeof(_CCompileOptions)
+
+
+def compile_options(calibration):
+    """(buffer kept alive, tsg_compile_options) for a calibration sample."""
+    buf = np.frombuffer(calibration, dtype=np.uint8) if isinstance(calibration, (bytes, bytearray)) \
+        else np.ascontiguousarray(calibration, dtype=np.uint8)
+    return buf, _CCompileOptions(COMPILE_OPTIONS_SIZE_V1, 0, buf.ctypes.data if len(buf) else None, len(buf))
+
+
 class _CStats(c.Structure):
     _fields_ = [(n, c.c_uint64) for n in ("bytes", "files", "anchor_hits", "candidates", "special_files",
                                           "findings")] + \
@@ -77,6 +92,7 @@ def _declare(L):
     if getattr(L, "_tsg_scanner_declared", False):
         return
     L.tsg_scanner_new.argtypes = [c.POINTER(_CGlobal), c.c_int, c.POINTER(c.c_void_p)]
+    L.tsg_scanner_new_ex.argtypes = [c.POINTER(_CGlobal), c.c_int, c.c_void_p, c.POINTER(c.c_void_p)]
     L.tsg_scanner_free.argtypes = [c.c_void_p]
     L.tsg_scanner_allow_path.argtypes = [c.c_void_p, c.c_char_p, c.c_uint64]
     L.tsg_scan.argtypes = [c.c_void_p, c.POINTER(_CBatch), c.POINTER(c.c_void_p)]
@@ -212,7 +228,7 @@ class Scanner:
     """secret.Scanner: an assembled Global bound to one HIP device."""
 
     def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude_regexes: Sequence[str],
-                 device: int = 0, lib=None, host_only: bool = False):
+                 device: int = 0, lib=None, host_only: bool = False, calibration=None):
         """lib: the C-ABI library (default libtsg.so).  host_only (tests): a scanner without a
         GPU engine from the oracle's library (oracle/hostlib.py), whose tsg_scan fails."""
         self.Rules = list(rules)
@@ -226,6 +242,9 @@ class Scanner:
         h = c.c_void_p()
         if host_only:
             rc = L.tsg_debug_scanner_host_only(c.byref(g), c.byref(h))
+        elif calibration is not None:
+            keep, opt = compile_options(calibration)
+            rc = L.tsg_scanner_new_ex(c.byref(g), int(device), c.byref(opt), c.byref(h))
         else:
             rc = L.tsg_scanner_new(c.byref(g), int(device), c.byref(h))
         if rc != 0:
@@ -327,11 +346,12 @@ class Scanner:
             raise RuntimeError("tsg_scan failed: %s" % _lib.last_error(self._L))
         return ScanResult(self, h)
 
-    def set_gpu_findings(self, on: bool) -> int:
-        """Findings of HBM-resident batches on the GPU (materialize.h, default) or on the host
-        (tsg_debug_scanner_gpu_findings); returns the previous setting."""
+    def set_gpu_findings(self, mode) -> int:
+        """Findings of HBM-resident batches on the GPU (materialize.h; True / 1), on the host
+        (False / 0) or on the GPU while the exact pass is the bound (2, the default)
+        (tsg_debug_scanner_gpu_findings); returns the previous mode."""
         self._L.tsg_debug_scanner_gpu_findings.argtypes = [c.c_void_p, c.c_int]
-        return self._L.tsg_debug_scanner_gpu_findings(self._h, 1 if on else 0)
+        return self._L.tsg_debug_scanner_gpu_findings(self._h, int(mode))
 
     def table_info(self):
         t = _CTableInfo()
@@ -451,11 +471,14 @@ def HostRegister(buf, lib=None):
     return lambda: L.tsg_host_unregister(buf.ctypes.data)
 
 
-def NewScanner(config: Optional[Config], device: int = 0, lib=None, host_only: bool = False) -> Scanner:
-    """scanner.go:320-364."""
+def NewScanner(config: Optional[Config], device: int = 0, lib=None, host_only: bool = False,
+               calibration=None) -> Scanner:
+    """scanner.go:320-364.  calibration (optional, bytes / uint8 array): a sample of the bytes the
+    scanner will see, e.g. its first batch -- the rule compiler then picks between a rule's literal
+    and class-run anchors by their fire rates on it (tsg_compile_options); findings never change."""
     b_rules, b_allow = builtin_rules(), builtin_allow_rules()
     if config is None:
-        return Scanner(b_rules, b_allow, [], device, lib, host_only)
+        return Scanner(b_rules, b_allow, [], device, lib, host_only, calibration)
     enabled = b_rules
     if config.EnableBuiltinRuleIDs:
         enabled = [r for r in b_rules if r.ID in config.EnableBuiltinRuleIDs]
@@ -463,4 +486,4 @@ def NewScanner(config: Optional[Config], device: int = 0, lib=None, host_only: b
     rules = [r for r in enabled if r.ID not in config.DisableRuleIDs]
     allow = b_allow + list(config.CustomAllowRules)
     allow = [a for a in allow if a.ID not in config.DisableAllowRuleIDs]
-    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device, lib, host_only)
+    return Scanner(rules, allow, list(config.ExcludeBlock.Regexes), device, lib, host_only, calibration)
