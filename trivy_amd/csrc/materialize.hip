@@ -216,11 +216,11 @@ __global__ __launch_bounds__(kMatThreads) void mat_locate_kernel(
         n++;
       }
       L.nlines = n;
+      // the cause line's text is the match text: cut (> 100 B) it is the match line
+      // (scanner.go:535-537), uncut the match text is the whole line (:520-528)
       uint64_t text = uint64_t(mle - mls);
-      for (uint32_t i = 0; i < n; i++) {
-        const int64_t ll = L.le[i] - L.lb[i];
-        if (!(ll > kLineCut && i == L.cause)) text += uint64_t(min(ll, kLineCut));
-      }
+      for (uint32_t i = 0; i < n; i++)
+        if (i != L.cause) text += uint64_t(min(L.le[i] - L.lb[i], kLineCut));
       locs[m] = L;
       cnt[m] = (text << 32) | n;
     }
@@ -264,8 +264,8 @@ __global__ __launch_bounds__(kMatThreads) void mat_write_kernel(
     for (uint32_t i = 0; i < L.nlines; i++) {
       const int64_t ll = L.le[i] - L.lb[i];
       const bool cause = i == L.cause;
-      uint32_t o = t_rel, n = mlen;
-      if (!(ll > kLineCut && cause)) {  // own text: the first 100 B (scanner.go:538-541)
+      uint32_t o = t_rel, n = mlen;  // the cause line shares the match text (its bytes, see above)
+      if (!cause) {  // own text: the first 100 B (scanner.go:538-541)
         n = uint32_t(min(ll, kLineCut));
         o = t_rel + off;
         copy_censored(arena, fs, L.lb[i], L.lb[i] + n, sp, F.ns, text + tpos + off, lane);
