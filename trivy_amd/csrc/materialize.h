@@ -104,7 +104,7 @@ class FindingMaterializer {
   void End(Job* j);
 
  private:
-  static constexpr int kSlots = 4;
+  static constexpr int kSlots = 6;  // (a depth-6 pipeline's exact passes at once)
   struct Slot;
   Slot* slots_ = nullptr;
   std::mutex mu_;

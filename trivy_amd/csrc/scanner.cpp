@@ -1813,8 +1813,27 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
     const LineOut* lo = mat_->lines(job);
     const char* tx = mat_->text(job);
     const uint64_t* pref = mat_->pref(job);
-    ParallelFor((n + kBlk - 1) / kBlk, host_threads_, [&](size_t blk) {
-      for (size_t i = blk * kBlk, e = std::min(n, i + kBlk); i < e; i++) {
+    // the files with the most findings first, one per item (each is a pdqsort of
+    // its findings on one thread: a multi-MiB file with tens of thousands of them
+    // dispatched late set the pass's length), the rest in blocks
+    std::vector<uint32_t>& ord = scr->gord;
+    ord.resize(n);
+    for (size_t i = 0; i < n; i++) ord[i] = uint32_t(i);
+    const size_t head = std::min<size_t>(n, 256);
+    auto heavier = [&](uint32_t x, uint32_t y) {
+      const size_t cx = tmp[gk[a + x]].gm.size(), cy = tmp[gk[a + y]].gm.size();
+      return cx != cy ? cx > cy : x < y;
+    };
+    if (head < n) std::nth_element(ord.begin(), ord.begin() + long(head), ord.end(), heavier);
+    std::sort(ord.begin(), ord.begin() + long(head), heavier);
+    if (head < n) std::sort(ord.begin() + long(head), ord.end());  // the rest in file order
+    constexpr size_t kBlk2 = 64;
+    const size_t n_items = head + (n - head + kBlk2 - 1) / kBlk2;
+    ParallelFor(n_items, host_threads_, [&](size_t it) {
+      const size_t lo_i = it < head ? it : head + (it - head) * kBlk2;
+      const size_t hi_i = it < head ? it + 1 : std::min(n, lo_i + kBlk2);
+      for (size_t oi = lo_i; oi < hi_i; oi++) {
+        const size_t i = ord[oi];
         FileResult& R = tmp[gk[a + i]];
         const size_t x = m0[i], y = x + R.gm.size();
         const uint64_t p0 = pref[x], p1 = pref[y];

@@ -306,6 +306,7 @@ class SecretScanner {
     std::vector<FileResult> tmp;      // per group
     std::vector<uint32_t> gk;         // GPU findings: the groups, their first location / span
     std::vector<uint64_t> gm0, gs0;
+    std::vector<uint32_t> gord;       // GPU findings: the assembly order (heaviest files first)
   };
   // the findings of the groups HostTail marked `gpu`, made by mat_ (materialize.h)
   template <class GroupFile, class ArenaOf>
