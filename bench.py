@@ -598,9 +598,11 @@ def main():
     ap.add_argument("--layer-parallel", type=int, default=3, help="c4 with --layers > 1: concurrent layer walks")
     ap.add_argument("--collectors", type=int, default=3,
                     help="c4/c1fs: collectors filled in turn (collectors - 1 scans in flight during a walk)")
-    ap.add_argument("--transform", choices=["gpu", "host"], default="gpu",
+    ap.add_argument("--transform", choices=["gpu", "host", "gather"], default="gpu",
                     help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
-                         "the walk's host threads")
+                         "the walk's host threads; gather: GPU pre-transform and no arena copy at all -- the GPU "
+                         "gathers each batch's files from the layer (page-locked and device-mapped once before "
+                         "timing, as a pinned layer-buffer pool would hold it)")
     ap.add_argument("--pool-gb", type=float, default=64.0, help="c5: page-locked host pool size")
     ap.add_argument("--calib-mb", type=float, default=16.0,
                     help="rule compiler calibration sample: the first MB of the corpus (as a scan job would hand "
@@ -695,6 +697,7 @@ def main():
     h2d_peak = None
     host_leg = [False]  # the ingest leg of a resident run: submit() streams the host arena
     emissions = 1
+    layer_unreg = []  # c4 --transform gather: the mapped layers' unregister calls
     if layer is None:
         dev = torch.device("cuda", local)
         if args.ingest:
@@ -748,10 +751,15 @@ def main():
         an = SecretAnalyzer(device=local)
         an.Init(AnalyzerOptions())
         t_compile = time.time() - t_c
-        gx = args.transform == "gpu"
-        colls = [Collector(an, args.arena_mb << 20, gx) for _ in range(args.collectors)]
-        lworkers = an.LayerWorkers(args.layer_parallel, args.arena_mb << 20, args.collectors, gx) \
+        gx = args.transform in ("gpu", "gather")
+        gth = args.transform == "gather"
+        colls = [Collector(an, args.arena_mb << 20, gx, gather=gth) for _ in range(args.collectors)]
+        lworkers = an.LayerWorkers(args.layer_parallel, args.arena_mb << 20, args.collectors, gx, gth) \
             if layer_list is not None else None
+        if gth and args.workload == "c4":  # the layer-buffer pool: registered once, outside the timed region
+            t_r = time.time()
+            layer_unreg = [secret.HostRegister(x, mapped=True) for x in (layer_list or [layer])]
+            register_s = time.time() - t_r
 
         def run_steps(n, stats):
             for _ in range(n):
@@ -761,13 +769,13 @@ def main():
                 elif layer_list is not None:  # the image's layers, --layer-parallel walks at once
                     per = []
                     t_l = time.time()
-                    an.AnalyzeLayers(layer_list, materialize=False, stats=per, workers=lworkers)
+                    an.AnalyzeLayers(layer_list, materialize=False, stats=per, workers=lworkers, registered=gth)
                     for d in per:  # summed over the layers (walk_s / wait_s: summed over the workers)
                         for k2, v in d.items():
                             st[k2] = st.get(k2, 0) + v
                     st["layers_s"] = time.time() - t_l
                 else:
-                    an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls)
+                    an.AnalyzeLayer(layer, stats=st, materialize=False, colls=colls, registered=gth)
                 stats.append(st)
 
     last_res = [None]  # the last step's ScanResult (findings checked against the oracle below)
@@ -921,6 +929,11 @@ def main():
                         "arena_bytes_per_gpu": arena_bytes, "files_analyzed_per_gpu": n_files,
                         "arena_mb": args.arena_mb, "pipeline": "%d collectors (walk k+1 || scans k-%d..k)" % (args.collectors, args.collectors - 2),
                         "pre_transform": args.transform}
+        if args.transform == "gather" and not fs_wl:
+            config_extra["layer_register_s"] = round(register_s, 3)
+            config_extra["gather_note"] = ("batches point into the layer (tsg_batch_ext v2 gather_base/gather_src); "
+                                           "the GPU reads the files over PCIe from the mapped layer; the layer's "
+                                           "one-time page-lock + map (layer_register_s) is outside the timed region")
         if fs_wl:
             config_extra["tree"] = "tmpfs (%s)" % os.path.dirname(layer)
         else:
@@ -1046,6 +1059,8 @@ def main():
         unregister()
     if unregister_leg is not None:
         unregister_leg()
+    for u in layer_unreg:
+        u()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -58,7 +58,8 @@ void tsg_collector_free(tsg_collector* c);
 #define TSG_FULL (-2)    /* the batch is full: submit (or reset) and add again */
 /* Analyze's pre-scan half for one file (dir = AnalysisInput.Dir; "" means a
  * file extracted from an image, whose path gets the "/" prefix).  Returns the
- * file's index in the batch (>= 0), TSG_SKIPPED or TSG_FULL. */
+ * file's index in the batch (>= 0), TSG_SKIPPED or TSG_FULL; -3 (error set)
+ * when the arena cannot grow or the collector gathers (tsg_collector_set_gather). */
 int64_t tsg_collector_add(tsg_collector* c, const char* path, uint64_t path_len, const char* dir,
                           const uint8_t* content, uint64_t size);
 
@@ -88,6 +89,15 @@ int tsg_analyzer_walk_end(tsg_analyzer* a);
  * (tsg_batch.transform).  The batch limit then counts each file's largest
  * transformed size. */
 int tsg_collector_set_gpu_transform(tsg_collector* c, int on);
+/* Gather mode (round 6; GPU-transform collectors, tar walks only): the walk no
+ * longer copies a file's bytes into the arena -- the batch records where the
+ * layer holds them, and the GPU gathers them from the layer buffer itself
+ * (tsg_batch_ext v2 gather_base / gather_src).  The layer buffer must be
+ * page-locked and device-mapped (tsg_host_register_mapped) for the whole walk
+ * and until the batch's tsg_scan_wait.  A batch holds one layer's files: a
+ * tsg_collector_add_tar on another buffer returns 1 (full) while the batch is
+ * not empty.  tsg_collector_add / _add_fs fail in this mode. */
+int tsg_collector_set_gather(tsg_collector* c, int on);
 
 /* FS.Walk (pkg/fanal/walker/fs.go:25-78) feeding a collector: the tree under
  * root in filepath.WalkDir order, skip_dirs / skip_files as utils.SkipPath

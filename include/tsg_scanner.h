@@ -111,7 +111,7 @@ typedef struct tsg_batch {
  * size it does not know (status <0, tsg_last_error names the sizes it knows),
  * so a caller built against an older or newer header never has fields read
  * past the end of its struct.  Known sizes: TSG_BATCH_EXT_SIZE_V1 (112 on
- * the 64-bit ABI).  The plain tsg_batch entry points read the frozen fields
+ * the 64-bit ABI), TSG_BATCH_EXT_SIZE_V2 (128).  The plain tsg_batch entry points read the frozen fields
  * only (a caller built against the round-4 header passes exactly those). */
 typedef struct tsg_batch_ext {
   uint32_t struct_size;
@@ -122,9 +122,18 @@ typedef struct tsg_batch_ext {
    * prefilter (NULL: the host runs the rules over every path). */
   const uint8_t* host_paths;
   const uint64_t* host_path_offsets;
+  /* v2 (round 6): gather_base / gather_src, with base.transform set and
+   * base.host_arena NULL -- file f's bytes as read are gather_base +
+   * gather_src[f] .. + (host_offsets[f + 1] - host_offsets[f]) in page-locked,
+   * device-mapped host memory (tsg_host_register_mapped; a tar layer as the
+   * analyzer's collectors hold it): the GPU gathers them itself, no host copy.
+   * host_offsets still lay out the batch (the files back to back). */
+  const uint8_t* gather_base;
+  const uint64_t* gather_src;
 } tsg_batch_ext;
 #define TSG_BATCH_EXT_SIZE_V1 ((uint32_t)(offsetof(tsg_batch_ext, host_path_offsets) + sizeof(const uint64_t*)))
-#define TSG_BATCH_EXT_SIZE TSG_BATCH_EXT_SIZE_V1  /* what this header's callers set */
+#define TSG_BATCH_EXT_SIZE_V2 ((uint32_t)(offsetof(tsg_batch_ext, gather_src) + sizeof(const uint64_t*)))
+#define TSG_BATCH_EXT_SIZE TSG_BATCH_EXT_SIZE_V2  /* what this header's callers set */
 
 int tsg_scan(tsg_scanner* s, const tsg_batch* batch, tsg_result** out);
 int tsg_scan_ext(tsg_scanner* s, const tsg_batch_ext* batch, tsg_result** out);
@@ -202,6 +211,9 @@ int tsg_result_stats(const tsg_result* r, tsg_stats* out);
  * the next submitted batches overlap the kernels): the Go caller's pinned arena
  * pool.  Unregister before freeing it. */
 int tsg_host_register(void* p, uint64_t bytes);
+/* The same, also mapped into the device's address space, so kernels read it
+ * directly (tsg_batch_ext.gather_base: a tar layer the GPU gathers from). */
+int tsg_host_register_mapped(void* p, uint64_t bytes);
 int tsg_host_unregister(void* p);
 
 /* Compiled-table facts (for reports/tests). */

@@ -64,9 +64,10 @@ def _c_layout(tmp_path):
     """sizeof / offsetof of the batch structs as a C compiler lays them out from include/tsg_scanner.h."""
     import subprocess
     src = tmp_path / "probe.c"
-    src.write_text('#include <stdio.h>\n#include "tsg_scanner.h"\nint main(void){printf("%zu %zu %zu %zu %u\\n",'
+    src.write_text('#include <stdio.h>\n#include "tsg_scanner.h"\nint main(void){printf("%zu %zu %zu %zu %u %zu %u\\n",'
                    ' sizeof(tsg_batch), sizeof(tsg_batch_ext), offsetof(tsg_batch_ext, base),'
-                   ' offsetof(tsg_batch_ext, host_paths), (unsigned)TSG_BATCH_EXT_SIZE_V1); return 0;}\n')
+                   ' offsetof(tsg_batch_ext, host_paths), (unsigned)TSG_BATCH_EXT_SIZE_V1,'
+                   ' offsetof(tsg_batch_ext, gather_base), (unsigned)TSG_BATCH_EXT_SIZE_V2); return 0;}\n')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-std=c99", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
     return [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
@@ -75,12 +76,14 @@ def _c_layout(tmp_path):
 def test_batch_struct_layouts(tmp_path):
     """The frozen tsg_batch is the round-4 layout (11 fields, no host paths); tsg_batch_ext carries
     struct_size first; the ctypes mirror agrees with the C compiler."""
-    from trivy_amd.secret.scanner import _CBatch, _CBatchExt, BATCH_EXT_SIZE_V1
-    size_b, size_e, off_base, off_hp, v1 = _c_layout(tmp_path)
+    from trivy_amd.secret.scanner import _CBatch, _CBatchExt, BATCH_EXT_SIZE_V1, BATCH_EXT_SIZE_V2
+    size_b, size_e, off_base, off_hp, v1, off_gb, v2 = _c_layout(tmp_path)
     assert size_b == 8 + 10 * 8 == ctypes.sizeof(_CBatch)  # n_files (+pad) and ten pointers
     assert off_base == _CBatchExt.base.offset == 8
     assert off_hp == _CBatchExt.host_paths.offset
-    assert v1 == size_e == BATCH_EXT_SIZE_V1 == 112
+    # v1 (round 5) ends after the host paths; v2 (round 6) adds the gather fields after them
+    assert v1 == off_gb == _CBatchExt.gather_base.offset == BATCH_EXT_SIZE_V1 == 112
+    assert v2 == size_e == ctypes.sizeof(_CBatchExt) == BATCH_EXT_SIZE_V2 == 128
 
 
 def test_scan_ext_refuses_unknown_struct_size():
@@ -89,7 +92,7 @@ def test_scan_ext_refuses_unknown_struct_size():
     from trivy_amd.secret.scanner import _CBatchExt, _declare, BATCH_EXT_SIZE_V1
     L = _lib.lib()
     _declare(L)
-    for bogus in (0, 7, BATCH_EXT_SIZE_V1 - 8, BATCH_EXT_SIZE_V1 + 8, 0xFFFFFFFF):
+    for bogus in (0, 7, BATCH_EXT_SIZE_V1 - 8, BATCH_EXT_SIZE_V1 + 8, BATCH_EXT_SIZE_V1 + 24, 0xFFFFFFFF):
         b = _CBatchExt()
         b.struct_size = bogus
         h = ctypes.c_void_p()

@@ -73,6 +73,7 @@ def _declare(L):
     L.tsg_collector_submit.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L.tsg_collector_reset.argtypes = [c.c_void_p]
     L.tsg_collector_set_gpu_transform.argtypes = [c.c_void_p, c.c_int]
+    L.tsg_collector_set_gather.argtypes = [c.c_void_p, c.c_int]
     L.tsg_scan_wait.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     L._tsg_analyzer_declared = True
 
@@ -158,9 +159,14 @@ def _read(content) -> bytes:
 class Collector:
     """A batch arena (tsg_collector): Analyze's pre-scan half for many files."""
 
-    def __init__(self, analyzer: "SecretAnalyzer", arena_bytes: int = 256 << 20, gpu_transform: bool = False):
+    def __init__(self, analyzer: "SecretAnalyzer", arena_bytes: int = 256 << 20, gpu_transform: bool = False,
+                 gather: bool = False):
         """gpu_transform: files enter the arena as read and the CR strip / printable
-        extraction runs on the GPU at scan time (tsg_collector_set_gpu_transform)."""
+        extraction runs on the GPU at scan time (tsg_collector_set_gpu_transform).
+        gather (needs gpu_transform; tar walks): the walk copies nothing -- the GPU gathers
+        the batch's files from the layer buffer, which the caller registers with
+        HostRegister(buf, mapped=True) and keeps until the batch is waited on; one batch
+        holds one layer's files (tsg_collector_set_gather)."""
         self._L = analyzer._L
         self._an = analyzer  # the C collector borrows the analyzer (and its walk state)
         h = c.c_void_p()
@@ -169,6 +175,9 @@ class Collector:
         self._h = h
         if gpu_transform and self._L.tsg_collector_set_gpu_transform(h, 1) != 0:
             raise RuntimeError("tsg_collector_set_gpu_transform failed: %s" % _lib.last_error(self._L))
+        if gather and self._L.tsg_collector_set_gather(h, 1) != 0:
+            raise RuntimeError("tsg_collector_set_gather failed: %s" % _lib.last_error(self._L))
+        self.gather = bool(gather)
         self._keep = []
 
     def __del__(self):
@@ -430,11 +439,16 @@ class SecretAnalyzer:
 
     def AnalyzeLayer(self, layer, arena_bytes: int = 256 << 20, stats: Optional[dict] = None,
                      materialize: bool = True, colls: Optional[List[Collector]] = None,
-                     gpu_transform: bool = False) -> AnalysisResult:
+                     gpu_transform: bool = False, gather: bool = False,
+                     registered: bool = False) -> AnalysisResult:
         """Every regular file of an uncompressed tar layer (bytes or a uint8 numpy array),
         as the image artifact's AnalyzeFile(dir="") would run it.  The collectors (two by
         default) are filled in turn while the others' batches are on the GPU.  materialize=False
-        (bench): findings stay in the engine; stats gets the summed scan counters."""
+        (bench): findings stay in the engine; stats gets the summed scan counters.
+        gather (with gpu_transform; or collectors made with gather=True): the GPU reads the files
+        in the layer itself (no arena copy); the layer, a uint8 numpy array, is registered
+        page-locked and mapped for the call unless `registered` says the caller holds it so
+        (HostRegister(layer, mapped=True): a pinned layer-buffer pool registers once)."""
         result = AnalysisResult()
         scan_tot: dict = {}
 
@@ -446,8 +460,14 @@ class SecretAnalyzer:
                 for k2, v in out.items():
                     scan_tot[k2] = scan_tot.get(k2, 0) + v
         st = _CTarStats()
-        colls = colls or [Collector(self, arena_bytes, gpu_transform), Collector(self, arena_bytes, gpu_transform)]
+        colls = colls or [Collector(self, arena_bytes, gpu_transform or gather, gather) for _ in range(2)]
         cursor = 0
+        unregister = None
+        if any(cl.gather for cl in colls) and not registered:
+            from ..secret.scanner import HostRegister
+            if not hasattr(layer, "ctypes"):
+                raise TypeError("AnalyzeLayer(gather): the layer must be a numpy uint8 array")
+            unregister = HostRegister(layer, self._L, mapped=True)
 
         def fill(coll):
             nonlocal cursor
@@ -459,6 +479,8 @@ class SecretAnalyzer:
             t_walk, t_wait = _pipeline(colls, fill, take)
         finally:  # the layer buffer may go away after this call (tsg_analyzer.h buffer lifetime)
             self.WalkEnd()
+            if unregister is not None:  # every batch read from it was waited on (_pipeline)
+                unregister()
         if stats is not None:
             stats.update({n: getattr(st, n) for n, _ in st._fields_})
             stats.update({"scan_" + k2: v for k2, v in scan_tot.items()})
@@ -467,7 +489,7 @@ class SecretAnalyzer:
 
 
     def LayerWorkers(self, parallel: int = 2, arena_bytes: int = 256 << 20, collectors: int = 2,
-                     gpu_transform: bool = False) -> list:
+                     gpu_transform: bool = False, gather: bool = False) -> list:
         """AnalyzeLayers' workers, for reuse across calls: per worker an analyzer bound to this scanner
         (its own tar-walk state) and its collectors (pinned arenas: allocating them per call would
         cost a hipHostMalloc each, and freeing them waits for the device)."""
@@ -475,13 +497,15 @@ class SecretAnalyzer:
         for _ in range(max(1, parallel)):
             sub = SecretAnalyzer(self.scanner, self.configPath, device=self.device, lib=self._L,
                                  host_only=self._host_only)
-            out.append((sub, [Collector(sub, arena_bytes, gpu_transform) for _ in range(max(1, collectors))]))
+            out.append((sub, [Collector(sub, arena_bytes, gpu_transform or gather, gather)
+                              for _ in range(max(1, collectors))]))
         return out
 
     def AnalyzeLayers(self, layers: Sequence, base: Optional[Sequence[bool]] = None, parallel: int = 2,
                       arena_bytes: int = 256 << 20, collectors: int = 2, gpu_transform: bool = False,
                       materialize: bool = True, stats: Optional[list] = None,
-                      workers: Optional[list] = None) -> List[AnalysisResult]:
+                      workers: Optional[list] = None, gather: bool = False,
+                      registered: bool = False) -> List[AnalysisResult]:
         """The image artifact's layer inspection for this analyzer (pkg/fanal/artifact/image/image.go:
         202-235): a pipeline of `parallel` workers over the layers, each running inspectLayer's walk
         (AnalyzeLayer) of one layer at a time; a base layer (base[i] true, the image's base diff IDs)
@@ -491,7 +515,8 @@ class SecretAnalyzer:
         copies and kernels.  Returns one AnalysisResult per layer, in the order given, each sorted as
         inspectLayer sorts its result (analyzer.go:225-234).  stats (a list): per layer, the
         AnalyzeLayer stats dict (None for base layers).  workers: from LayerWorkers (then `parallel`,
-        `arena_bytes`, `collectors` and `gpu_transform` are theirs)."""
+        `arena_bytes`, `collectors`, `gpu_transform` and `gather` are theirs).  gather / registered:
+        as AnalyzeLayer (the layers are then uint8 numpy arrays)."""
         import threading
         if self.scanner is None:
             raise RuntimeError("AnalyzeLayers: the analyzer has no scanner (Init first)")
@@ -509,7 +534,8 @@ class SecretAnalyzer:
         errors: List[BaseException] = []
 
         if workers is None:
-            workers = self.LayerWorkers(min(parallel, max(1, len(todo))), arena_bytes, collectors, gpu_transform)
+            workers = self.LayerWorkers(min(parallel, max(1, len(todo))), arena_bytes, collectors, gpu_transform,
+                                        gather)
 
         def worker(sub, colls):
             while True:
@@ -519,7 +545,8 @@ class SecretAnalyzer:
                     i = todo.popleft()
                 st: dict = {}
                 try:
-                    r = sub.AnalyzeLayer(layers[i], stats=st, materialize=materialize, colls=colls)
+                    r = sub.AnalyzeLayer(layers[i], stats=st, materialize=materialize, colls=colls,
+                                         registered=registered)
                 except BaseException as e:  # the pipeline stops at the first error (parallel.Pipeline)
                     with lock:
                         errors.append(e)

@@ -423,6 +423,10 @@ void tsg_collector_free(tsg_collector* c) { delete c; }
 
 int64_t tsg_collector_add(tsg_collector* c, const char* path, uint64_t path_len, const char* dir,
                           const uint8_t* content, uint64_t size) {
+  if (c->gather) {
+    tsg::SetError("tsg_collector_add: the collector gathers from tar layers (tsg_collector_set_gather)");
+    return -3;
+  }
   return Add(c, path, path_len, !dir || !*dir, content, size);
 }
 
@@ -885,6 +889,7 @@ size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry*>
   c->path_pool.resize(p0 + tot.pbytes);
   c->binary.resize(f0 + tot.files);
   if (c->gpu_xform) c->kinds.resize(f0 + tot.files);
+  if (c->gather) c->gsrc.resize(f0 + tot.files);
   tsg::ParallelFor(m, c->threads, [&](size_t b) {
     size_t f = f0 + at[b].files, pp = p0 + at[b].pbytes;
     uint64_t u = u0 + at[b].used;
@@ -894,6 +899,7 @@ size_t AcceptBlocks(tsg_collector* c, const uint8_t* tar, std::vector<TarEntry*>
       e.out_off = u;
       u += c->gpu_xform ? e.size : e.out_len;
       if (c->gpu_xform) c->kinds[f] = e.bin ? 2 : 1;
+      if (c->gather) c->gsrc[f] = e.data;
       c->binary[f] = e.bin;
       c->offs[f + 1] = u;
       const std::string_view fp = e.path(tar);
@@ -936,6 +942,10 @@ extern "C" {
 int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint64_t* cursor, tsg_tar_stats* st) {
   tsg_tar_stats local{};
   if (!st) st = &local;
+  if (c->gather) {  // a gathered batch holds one layer's files (one gather_base)
+    if (c->files() > 0 && c->gbase != tar) return 1;
+    c->gbase = tar;
+  }
   std::lock_guard<std::mutex> walk_lock(c->a->walk_mu);
   if (!c->a->walk) c->a->walk = new tsg::TarWalkCache();
   tsg::TarWalkCache& W = *c->a->walk;
@@ -1031,6 +1041,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
           c->used += e.out_len;
         }
         c->offs.push_back(c->used);
+        if (c->gather) c->gsrc.push_back(e.data);
         c->path_pool.push_back('/');  // Dir "" (image files, secret.go:130-135)
         const std::string_view fp = e.path(tar);
       c->path_pool.append(fp.data(), fp.size());
@@ -1049,8 +1060,9 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
     }
     W.pos = k;
     double t3 = dbg ? now() : 0;
-    // 3. copy / transform the accepted contents
-    tsg::ParallelFor((k - k0 + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
+    // 3. copy / transform the accepted contents (gather mode: nothing to copy,
+    // the GPU reads them in the layer buffer)
+    if (!c->gather) tsg::ParallelFor((k - k0 + kBlock - 1) / kBlock, c->threads, [&](size_t b) {
       for (size_t i = k0 + b * kBlock; i < std::min(k, k0 + (b + 1) * kBlock); i++) {
         const TarEntry& e = *W.w.ents[i];
         if (e.state != 2) continue;
@@ -1061,7 +1073,7 @@ int tsg_collector_add_tar(tsg_collector* c, const uint8_t* tar, uint64_t n, uint
       }
       _mm_sfence();
     }, true);
-    std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
+    if (!c->gather) std::memset(c->arena + c->used, 0, 64);  // the engine reads up to 64 B past the end
     if (dbg) {
       const double t4 = now();
       t_phase[0] += t1 - t0;
@@ -1108,7 +1120,7 @@ int tsg_collector_file(const tsg_collector* c, uint32_t i, const char** path, ui
   if (i >= c->files()) return -1;
   *path = c->path_pool.data() + c->path_off[i];
   *path_len = c->path_off[i + 1] - c->path_off[i];
-  *content = c->arena + c->offs[i];
+  *content = c->gather ? c->gbase + c->gsrc[i] : c->arena + c->offs[i];
   *len = c->offs[i + 1] - c->offs[i];
   *binary = c->binary[i];
   if (c->gpu_xform) {  // as it will be scanned: transformed here (tests / host-language mirror only)
@@ -1118,6 +1130,19 @@ int tsg_collector_file(const tsg_collector* c, uint32_t i, const char** path, ui
                             : tsg::StripCR(*content, n, c->scratch.data());
     *content = c->scratch.data();
   }
+  return 0;
+}
+
+int tsg_collector_set_gather(tsg_collector* c, int on) {
+  if (c->files() > 0) {
+    tsg::SetError("tsg_collector_set_gather: the batch is not empty");
+    return -1;
+  }
+  if (on && !c->gpu_xform) {
+    tsg::SetError("tsg_collector_set_gather: gather mode needs the GPU pre-transform (tsg_collector_set_gpu_transform)");
+    return -1;
+  }
+  c->gather = on != 0;
   return 0;
 }
 
@@ -1144,6 +1169,11 @@ int tsg_collector_submit(tsg_collector* c, tsg_pending** out) {
   // the paths are packed already: the global allow-path rules are prefiltered on the GPU
   b.host_paths = reinterpret_cast<const uint8_t*>(c->path_pool.data());
   b.host_path_offsets = c->path_off.data();
+  if (c->gather) {  // the GPU reads the files in the layer buffer
+    b.base.host_arena = nullptr;
+    b.gather_base = c->gbase;
+    b.gather_src = c->gsrc.data();
+  }
   return tsg_scan_submit_ext(const_cast<tsg_scanner*>(c->a->s), &b, out);
 }
 

@@ -217,6 +217,16 @@ int tsg_host_register(void* p, uint64_t bytes) {
   return 0;
 }
 
+int tsg_host_register_mapped(void* p, uint64_t bytes) {
+  if (!p || !bytes) return 0;
+  const hipError_t e = hipHostRegister(p, size_t(bytes), hipHostRegisterMapped);
+  if (e != hipSuccess) {
+    tsg::SetError(std::string("hipHostRegister (mapped): ") + hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
 int tsg_host_unregister(void* p) {
   if (!p) return 0;
   const hipError_t e = hipHostUnregister(p);
@@ -247,16 +257,34 @@ bool CheckExtSize(const tsg_batch_ext* b) {
     tsg::SetError("tsg_scan_ext: NULL batch");
     return false;
   }
-  if (b->struct_size != TSG_BATCH_EXT_SIZE_V1) {
+  if (b->struct_size != TSG_BATCH_EXT_SIZE_V1 && b->struct_size != TSG_BATCH_EXT_SIZE_V2) {
     tsg::SetError("tsg_scan_ext: tsg_batch_ext.struct_size " + std::to_string(b->struct_size) +
-                  " is not a size this library knows (v1 = " + std::to_string(TSG_BATCH_EXT_SIZE_V1) + ")");
+                  " is not a size this library knows (v1 = " + std::to_string(TSG_BATCH_EXT_SIZE_V1) +
+                  ", v2 = " + std::to_string(TSG_BATCH_EXT_SIZE_V2) + ")");
     return false;
   }
   return true;
 }
 
-int ScanImpl(tsg_scanner* s, const tsg_batch* b, const uint8_t* host_paths, const uint64_t* host_path_off,
-             tsg_result** out);
+struct ExtFields {  // the fields past tsg_batch that a caller's struct_size covers
+  const uint8_t* host_paths = nullptr;
+  const uint64_t* host_path_off = nullptr;
+  const uint8_t* gather_base = nullptr;
+  const uint64_t* gather_src = nullptr;
+};
+
+ExtFields ExtOf(const tsg_batch_ext* b) {
+  ExtFields e;
+  e.host_paths = b->host_paths;
+  e.host_path_off = b->host_path_offsets;
+  if (b->struct_size >= TSG_BATCH_EXT_SIZE_V2) {
+    e.gather_base = b->gather_base;
+    e.gather_src = b->gather_src;
+  }
+  return e;
+}
+
+int ScanImpl(tsg_scanner* s, const tsg_batch* b, const ExtFields& x, tsg_result** out);
 
 }  // namespace
 
@@ -264,12 +292,11 @@ int tsg_scan_submit_ext(tsg_scanner* s, const tsg_batch_ext* b, tsg_pending** ou
   if (!CheckExtSize(b)) return -1;
   std::unique_ptr<tsg_pending> p(new tsg_pending());
   const tsg_batch bc = b->base;
-  const uint8_t* hp = b->host_paths;
-  const uint64_t* hpo = b->host_path_offsets;
+  const ExtFields x = ExtOf(b);
   tsg_pending* pp = p.get();
-  pp->th = std::thread([s, bc, hp, hpo, pp] {
+  pp->th = std::thread([s, bc, x, pp] {
     pthread_setname_np(pthread_self(), "tsg-scan");
-    pp->rc = ScanImpl(s, &bc, hp, hpo, &pp->r);
+    pp->rc = ScanImpl(s, &bc, x, &pp->r);
     if (pp->rc != 0) pp->err = tsg_last_error();
   });
   *out = p.release();
@@ -293,17 +320,16 @@ int tsg_scan_wait(tsg_pending* p, tsg_result** out) {
   return rc;
 }
 
-int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) { return ScanImpl(s, b, nullptr, nullptr, out); }
+int tsg_scan(tsg_scanner* s, const tsg_batch* b, tsg_result** out) { return ScanImpl(s, b, ExtFields(), out); }
 
 int tsg_scan_ext(tsg_scanner* s, const tsg_batch_ext* b, tsg_result** out) {
   if (!CheckExtSize(b)) return -1;
-  return ScanImpl(s, &b->base, b->host_paths, b->host_path_offsets, out);
+  return ScanImpl(s, &b->base, ExtOf(b), out);
 }
 
 namespace {
 
-int ScanImpl(tsg_scanner* s, const tsg_batch* b, const uint8_t* host_paths, const uint64_t* host_path_off,
-             tsg_result** out) {
+int ScanImpl(tsg_scanner* s, const tsg_batch* b, const ExtFields& x, tsg_result** out) {
   tsg::BatchInput in;
   in.n_files = b->n_files;
   in.host_arena = b->host_arena;
@@ -316,8 +342,14 @@ int ScanImpl(tsg_scanner* s, const tsg_batch* b, const uint8_t* host_paths, cons
   in.transform = b->transform;
   in.dev_paths = static_cast<const uint8_t*>(b->dev_paths);
   in.dev_path_off = static_cast<const uint64_t*>(b->dev_path_offsets);
-  in.host_paths = host_paths;
-  in.host_path_off = host_path_off;
+  in.host_paths = x.host_paths;
+  in.host_path_off = x.host_path_off;
+  in.gather_base = x.gather_base;
+  in.gather_src = x.gather_src;
+  if (in.gather_base && (!in.gather_src || !in.transform || in.dev_arena)) {
+    tsg::SetError("tsg_scan: a gathered batch needs gather_src and transform, and no dev_arena");
+    return -1;
+  }
   std::unique_ptr<tsg_result> r(new tsg_result());
   r->owner = s->s.get();
   tsg::BatchStats gs;

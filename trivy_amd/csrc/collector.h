@@ -48,6 +48,11 @@ struct tsg_collector {
   bool gpu_xform = false;
   uint64_t bound = 0;
   std::vector<uint8_t> kinds;
+  // gather mode (tsg_collector_set_gather): the files stay in the layer buffer
+  // gbase at gsrc[f]; the arena holds nothing (offs still lay the batch out)
+  bool gather = false;
+  const uint8_t* gbase = nullptr;
+  std::vector<uint64_t> gsrc;
   mutable std::vector<uint8_t> scratch;  // tsg_collector_file's transformed copy (GPU mode)
   int threads = 16;    // ingest threads (TSG_HOST_THREADS)
   std::vector<uint64_t> offs{0};
@@ -100,6 +105,8 @@ struct tsg_collector {
   void Reset() {
     used = input_bytes = bound = 0;
     kinds.clear();
+    gbase = nullptr;
+    gsrc.clear();
     offs.assign(1, 0);
     path_pool.clear();
     path_off.assign(1, 0);

@@ -103,9 +103,15 @@ class GpuEngine {
   // must be the only lock guarding this engine's Run / Enqueue calls.  A
   // failure's text comes back in *err (err_ is shared with the other users of
   // the engine, so it is not the channel for a call that runs beside them).
+  // gather_base / gather_src (optional, with kinds): the files are not in
+  // h_arena (NULL then) but at gather_base + gather_src[f] in page-locked,
+  // device-mapped host memory (a registered tar layer); each chunk is gathered
+  // from there into its staging buffer by a kernel (xform.h GatherHostFiles)
+  // instead of one DMA copy -- no host copy of the file bytes.
   bool RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail,
-               std::mutex* dev_mu, std::string* err);
+               std::mutex* dev_mu, std::string* err, const uint8_t* gather_base = nullptr,
+               const uint64_t* gather_src = nullptr);
 
   // Split form of Run for pipelined callers: Enqueue (with the engine's lock
   // held) puts the whole GPU phase and the copies of the counters and of the
@@ -287,6 +293,10 @@ class GpuEngine {
   bool EnsureHost(void** p, size_t* cap, size_t need);
   // GPU pre-transform (xform.h): per-chunk kinds, lengths, transformed offsets and bytes, the gather
   void* d_kind_[kNStage] = {}; size_t cap_kind_[kNStage] = {};
+  // host-memory gather (RunHost gather_base): per staging buffer the chunk's source
+  // offsets + work items (device) and their pinned staging
+  void* d_gsrc_[kNStage] = {}; size_t cap_gsrc_[kNStage] = {};
+  void* h_gsrc_[kNStage] = {}; size_t cap_h_gsrc_[kNStage] = {};
   void* d_xlen_ = nullptr; size_t cap_xlen_ = 0;
   void* d_xoff_ = nullptr; size_t cap_xoff_ = 0;
   void* d_xscan_ = nullptr; size_t cap_xscan_ = 0;

@@ -2553,8 +2553,11 @@ GpuEngine::~GpuEngine() {
   for (void* p : ps)
     if (p) hipFree(p);
   for (int b = 0; b < kNStage; b++)
-    for (void* p : {d_stage_[b], d_stage_off_[b], d_kind_[b]})
+  {
+    for (void* p : {d_stage_[b], d_stage_off_[b], d_kind_[b], d_gsrc_[b]})
       if (p) hipFree(p);
+    if (h_gsrc_[b]) hipHostFree(h_gsrc_[b]);
+  }
   for (auto& e : ev_)
     if (e) hipEventDestroy(e);
   for (auto& e : ev_copied_)
@@ -2689,6 +2692,8 @@ struct GpuEngine::HostCall {
   const uint8_t* h_arena;
   const uint64_t* h_offsets;
   const uint8_t* kinds;
+  const uint8_t* gather_dev = nullptr;  // device address of the mapped gather_base (RunHost)
+  const uint64_t* gather_src = nullptr;
   bool cancelled = false;  // ring_mu_: a chunk failed; the call's later slots are not copied
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // first copy issued / last chunk scanned
   bool ev0_recorded = false;
@@ -2743,6 +2748,45 @@ bool GpuEngine::CopyChunk(const StageJob& j, std::string* err) {
     j.call->ev0_recorded = true;
   }
   uint8_t* d = static_cast<uint8_t*>(d_stage_[b]);
+  if (c.gather_dev) {
+    // the chunk's files gathered from the mapped host buffer by a kernel on the
+    // copy stream: their source offsets and (file, piece) items staged first
+    // (the pinned staging is reusable: ev_copied_[b] completed above)
+    std::vector<GatherItem> items;
+    items.reserve(nf);
+    for (uint32_t f = 0; f < nf; f++) {
+      const uint64_t len = c.h_offsets[j.f0 + f + 1] - c.h_offsets[j.f0 + f];
+      for (uint32_t q = 0; uint64_t(q) * kGatherPiece < len; q++) items.push_back(GatherItem{f, q});
+    }
+    const size_t src_bytes = (size_t(nf) + 1) * 8, item_bytes = items.size() * sizeof(GatherItem);
+    const size_t need = src_bytes + item_bytes + 16;
+    if ((x = grow(&d_gsrc_[b], &cap_gsrc_[b], need, 0)) != hipSuccess) return fail("gather hipMalloc", x);
+    if (cap_h_gsrc_[b] < need) {
+      if (h_gsrc_[b]) hipHostFree(h_gsrc_[b]);
+      h_gsrc_[b] = nullptr;
+      cap_h_gsrc_[b] = 0;
+      if ((x = hipHostMalloc(&h_gsrc_[b], need + need / 2, hipHostMallocDefault)) != hipSuccess)
+        return fail("gather hipHostMalloc", x);
+      cap_h_gsrc_[b] = need + need / 2;
+    }
+    uint8_t* hs = static_cast<uint8_t*>(h_gsrc_[b]);
+    std::memcpy(hs, c.gather_src + j.f0, size_t(nf) * 8);
+    std::memcpy(hs + src_bytes, items.data(), item_bytes);
+    uint8_t* ds = static_cast<uint8_t*>(d_gsrc_[b]);
+    if ((x = hipMemcpyAsync(d_stage_off_[b], h_off_[b], (size_t(nf) + 1) * 8, hipMemcpyHostToDevice, copy_stream_)) !=
+            hipSuccess ||
+        (x = hipMemcpyAsync(ds, hs, src_bytes + item_bytes, hipMemcpyHostToDevice, copy_stream_)) != hipSuccess ||
+        (x = GatherHostFiles(c.gather_dev, reinterpret_cast<const uint64_t*>(ds),
+                             static_cast<const uint64_t*>(d_stage_off_[b]),
+                             reinterpret_cast<const GatherItem*>(ds + src_bytes), uint32_t(items.size()), d,
+                             copy_stream_)) != hipSuccess ||
+        (x = hipMemsetAsync(d + (e - a), 0, 64, copy_stream_)) != hipSuccess ||
+        (c.kinds && (x = hipMemcpyAsync(d_kind_[b], c.kinds + j.f0, nf, hipMemcpyHostToDevice, copy_stream_)) !=
+                        hipSuccess) ||
+        (x = hipEventRecord(ev_copied_[b], copy_stream_)) != hipSuccess)
+      return fail("chunk gather", x);
+    return true;
+  }
   // in pieces of at most 1 GiB (a lone file can make a chunk of many GiB)
   for (uint64_t p = a; p < e; p += uint64_t(1) << 30)
     if ((x = hipMemcpyAsync(d + (p - a), c.h_arena + p, std::min<uint64_t>(e - p, uint64_t(1) << 30),
@@ -2773,7 +2817,8 @@ void GpuEngine::CopierLoop() {
     lk.unlock();
     std::string e;
     RingLog("copy-issue", j.slot, ring_turn_);
-    RingLog("copy-src", j.slot, (reinterpret_cast<uintptr_t>(j.call->h_arena + j.call->h_offsets[j.f0]) & 0xFFFFF) |
+    RingLog("copy-src", j.slot, (reinterpret_cast<uintptr_t>(j.call->h_arena ? j.call->h_arena + j.call->h_offsets[j.f0]
+                                                                               : nullptr) & 0xFFFFF) |
                                     (uint64_t(j.call->h_offsets[j.f1] - j.call->h_offsets[j.f0]) << 20));
     const bool ok = !skip && CopyChunk(j, &e);
     RingLog("copy-issued", j.slot, 0);
@@ -2788,7 +2833,8 @@ void GpuEngine::CopierLoop() {
 
 bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t* h_offsets, uint32_t n_files,
                         std::vector<Candidate>* cands, BatchStats* st, const uint8_t* kinds, TailOut* tail,
-                        std::mutex* dev_mu, std::string* err) {
+                        std::mutex* dev_mu, std::string* err, const uint8_t* gather_base,
+                        const uint64_t* gather_src) {
   if (!dev_mu) dev_mu = &dev_mu_;
   cands->clear();
   BatchStats local;
@@ -2808,7 +2854,16 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
     return false;
   };
   if (kinds && !tail) return set_err("RunHost: a transformed batch needs a tail output");
+  if (gather_base && (!gather_src || !kinds)) return set_err("RunHost: a gathered batch needs source offsets and kinds");
   if (n_files == 0) return true;
+  const uint8_t* gather_dev = nullptr;
+  if (gather_base) {  // the device address of the mapped host buffer (tsg_host_register_mapped)
+    void* dp = nullptr;
+    if (hipSetDevice(device_) != hipSuccess ||
+        hipHostGetDevicePointer(&dp, const_cast<uint8_t*>(gather_base), 0) != hipSuccess || !dp)
+      return set_err("RunHost: the gather buffer is not page-locked and mapped (tsg_host_register_mapped)");
+    gather_dev = static_cast<const uint8_t*>(dp);
+  }
   std::vector<uint64_t> tail_len;  // per file: transformed bytes kept for the host (0: not a candidate file)
   if (kinds) tail_len.assign(n_files, 0);
   // chunk boundaries (file indices)
@@ -2820,6 +2875,8 @@ bool GpuEngine::RunHost(const uint8_t* h_arena, uint64_t n_bytes, const uint64_t
   cut.push_back(n_files);
   const size_t n_chunks = cut.size() - 1;
   HostCall call{h_arena, h_offsets, kinds};
+  call.gather_dev = gather_dev;
+  call.gather_src = gather_src;
   if (hipSetDevice(device_) != hipSuccess || hipEventCreate(&call.ev0) != hipSuccess ||
       hipEventCreate(&call.ev1) != hipSuccess) {
     if (call.ev0) hipEventDestroy(call.ev0);

@@ -468,6 +468,10 @@ int tsg_fs_walk_stats(const tsg_fs_walk* w, tsg_fs_stats* st) {
 }
 
 int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st) {
+  if (c->gather) {
+    tsg::SetError("tsg_collector_add_fs: the collector gathers from tar layers (tsg_collector_set_gather)");
+    return -1;
+  }
   tsg_fs_add_stats local{};
   if (!st) st = &local;
   if (!w->listed) {

@@ -1345,7 +1345,7 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
   GpuEngine::Ticket ticket;
   if (!in.dev_arena) {  // the staging ring orders concurrent host batches; it takes the lock per chunk
     ok = engine->RunHost(in.host_arena, n_bytes, in.host_offsets, in.n_files, &cands, gst, in.transform,
-                         in.transform ? &tail : nullptr, &gpu_mu_[slot], &gpu_err);
+                         in.transform ? &tail : nullptr, &gpu_mu_[slot], &gpu_err, in.gather_base, in.gather_src);
   } else {
     std::lock_guard<std::mutex> g(gpu_mu_[slot]);
     static const bool tickets = !std::getenv("TSG_TICKETS") || std::atoi(std::getenv("TSG_TICKETS")) != 0;
@@ -1379,8 +1379,8 @@ bool SecretScanner::Scan(const BatchInput& in, BatchResult* out, BatchStats* gst
     for (const Candidate& c : cands) {
       const uint32_t f = c.file;
       if (f >= in.n_files || fdata[f]) continue;
-      if (tail.raw[f]) {
-        fdata[f] = in.host_arena + in.host_offsets[f];
+      if (tail.raw[f]) {  // as read: in the batch arena, or where the gather took it from
+        fdata[f] = in.gather_base ? in.gather_base + in.gather_src[f] : in.host_arena + in.host_offsets[f];
         flen[f] = in.host_offsets[f + 1] - in.host_offsets[f];
       } else {
         fdata[f] = tail.buf.data() + tail.off[f];
@@ -1829,29 +1829,48 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
     if (head < n) std::sort(ord.begin() + long(head), ord.end());  // the rest in file order
     constexpr size_t kBlk2 = 64;
     const size_t n_items = head + (n - head + kBlk2 - 1) / kBlk2;
+    static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;
+    std::atomic<uint64_t> us_copy{0}, us_sort{0}, us_max{0};  // (TSG_TAIL_TIMES)
     ParallelFor(n_items, host_threads_, [&](size_t it) {
       const size_t lo_i = it < head ? it : head + (it - head) * kBlk2;
       const size_t hi_i = it < head ? it + 1 : std::min(n, lo_i + kBlk2);
+      double c_ms = 0, s_ms = 0;
       for (size_t oi = lo_i; oi < hi_i; oi++) {
         const size_t i = ord[oi];
         FileResult& R = tmp[gk[a + i]];
         const size_t x = m0[i], y = x + R.gm.size();
         const uint64_t p0 = pref[x], p1 = pref[y];
+        const double t0 = times ? NowMs() : 0;
         FileFindings& ff = R.findings;
         ff = FileFindings(thread_arena());
         ff.f.assign(fo + x, fo + y);
         ff.lines.assign(lo + uint32_t(p0), lo + uint32_t(p1));
         ff.text.assign(tx + (p0 >> 32), tx + (p1 >> 32));
+        const double t1 = times ? NowMs() : 0;
         SortFindings(&ff, rule_rank_);
         R.kind = kHasFindings;
+        if (times) {
+          const double t2 = NowMs();
+          c_ms += t1 - t0;
+          s_ms += t2 - t1;
+        }
+      }
+      if (times) {
+        us_copy += uint64_t(c_ms * 1e3);
+        us_sort += uint64_t(s_ms * 1e3);
+        const uint64_t tot = uint64_t((c_ms + s_ms) * 1e3);
+        uint64_t m = us_max.load();
+        while (tot > m && !us_max.compare_exchange_weak(m, tot)) {
+        }
       }
     }, wide);
     mat_->End(job);
-    static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;
     if (times)
       std::fprintf(stderr, "gpu findings ms: slot+fill %.2f gpu %.2f assemble+sort %.2f (files %zu, findings %llu, "
-                   "spans %llu)\n", g0 - f0, g1 - g0, NowMs() - g1, b - a, (unsigned long long)nm,
-                   (unsigned long long)ns);
+                   "spans %llu; thread-ms copy %.2f sort %.2f, longest item %.2f; lines %u text %.1f MB)\n",
+                   g0 - f0, g1 - g0, NowMs() - g1, b - a, (unsigned long long)nm, (unsigned long long)ns,
+                   us_copy.load() * 1e-3, us_sort.load() * 1e-3, us_max.load() * 1e-3, uint32_t(pref[nm]),
+                   double(pref[nm] >> 32) * 1e-6);
     a = b;
   }
   return true;

@@ -236,6 +236,10 @@ struct BatchInput {
   const uint64_t* dev_path_off = nullptr;  // on the GPU, pathfilter.h); n_files + 1 offsets, device
   const uint8_t* host_paths = nullptr;      // optional: the paths packed in host memory (copied to HBM for
   const uint64_t* host_path_off = nullptr;  // the same prefilter when dev_paths is absent); n_files + 1 offsets
+  // optional (with transform; host_arena NULL): file f's bytes as read are at gather_base + gather_src[f]
+  // in page-locked, device-mapped memory; the engine gathers them on the GPU (GpuEngine::RunHost)
+  const uint8_t* gather_base = nullptr;
+  const uint64_t* gather_src = nullptr;
 };
 
 struct HostStats {

@@ -42,4 +42,20 @@ inline uint64_t XformMaxOut(uint64_t n_bytes, uint32_t n_files) { return n_bytes
 hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t* files, const uint64_t* dst_off,
                        uint32_t n, uint8_t* dst, hipStream_t s);
 
+// Gather of a host batch's files straight from page-locked, device-mapped host
+// memory (a registered tar layer: each file's data where the tar holds it) into
+// a staging arena: dst[dst_off[f] .. dst_off[f + 1]) = src[src_off[f] ..).  One
+// wave per item of up to kGatherPiece bytes of one file (items: (file, piece),
+// built by the host); 16-B aligned destination stores (byte stores at a file's
+// two ragged ends), source words by aligned loads and a byte shift.  The reads
+// may touch up to 16 bytes before a file's data and 32 past its end, which a tar
+// holds (the 512-B header before, the 512-B block padding and the end-of-archive
+// blocks after).
+constexpr uint32_t kGatherPiece = 16384;
+struct GatherItem {
+  uint32_t file, piece;
+};
+hipError_t GatherHostFiles(const uint8_t* src_dev, const uint64_t* src_off, const uint64_t* dst_off,
+                           const GatherItem* items, uint32_t n_items, uint8_t* dst, hipStream_t s);
+
 }  // namespace tsg

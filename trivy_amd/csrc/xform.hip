@@ -1038,3 +1038,82 @@ hipError_t GatherFiles(const uint8_t* src, const uint64_t* xoff, const uint32_t*
 }
 
 }  // namespace tsg
+
+namespace tsg {
+namespace {
+
+__device__ __forceinline__ uint32_t word_at(const uint4& a, const uint4& b, uint32_t k) {  // word k of a:b
+  switch (k) {
+    case 0: return a.x;
+    case 1: return a.y;
+    case 2: return a.z;
+    case 3: return a.w;
+    case 4: return b.x;
+    case 5: return b.y;
+    case 6: return b.z;
+    default: return b.w;
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_host_kernel(const uint8_t* __restrict__ src,
+                                                          const uint64_t* __restrict__ src_off,
+                                                          const uint64_t* __restrict__ dst_off,
+                                                          const GatherItem* __restrict__ items, uint32_t n_items,
+                                                          uint8_t* __restrict__ dst) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t it = blockIdx.x * 4u + wave; it < n_items; it += gridDim.x * 4u) {
+    const GatherItem g = items[it];
+    const uint64_t f0 = dst_off[g.file], f1 = dst_off[g.file + 1];
+    const uint64_t d0 = f0 + uint64_t(g.piece) * kGatherPiece;
+    const uint64_t d1 = min(f1, d0 + kGatherPiece);
+    if (d0 >= d1) continue;
+    const uint64_t s0 = src_off[g.file] + (d0 - f0);  // source of byte d0
+    // destination blocks [align16(d0), d1): block B takes source bytes from
+    // B + (s0 - d0); its aligned source block A and A + 16 (the next lane's A)
+    const uint64_t b_lo = d0 & ~uint64_t(15);
+    const uint64_t a_lo = (b_lo + s0 - d0) & ~uint64_t(15);  // (b_lo + s0 - d0 >= s0 - 15 >= 0 in a tar)
+    const uint32_t r = uint32_t((b_lo + s0 - d0) & 15u);     // byte shift, the same for every block
+    for (uint64_t k = 0; b_lo + 16 * k < d1; k += 64) {
+      const uint64_t B = b_lo + 16 * (k + lane);
+      const uint64_t A = a_lo + 16 * (k + lane);
+      const bool live = B < d1;
+      uint4 a = make_uint4(0, 0, 0, 0), nxt;
+      if (live) a = *reinterpret_cast<const uint4*>(src + A);
+      // the block after A: the next lane's, the last lane (or the last live one) loads it
+      nxt.x = __shfl_down(a.x, 1);
+      nxt.y = __shfl_down(a.y, 1);
+      nxt.z = __shfl_down(a.z, 1);
+      nxt.w = __shfl_down(a.w, 1);
+      if (live && (lane == 63 || B + 16 >= d1) && r) nxt = *reinterpret_cast<const uint4*>(src + A + 16);
+      if (!live) continue;
+      uint32_t o[4];
+      const uint32_t q = r >> 2, sh = r & 3u;
+#pragma unroll
+      for (uint32_t w = 0; w < 4; w++) {
+        const uint32_t lo = word_at(a, nxt, q + w), hi = word_at(a, nxt, q + w + 1 > 7 ? 7 : q + w + 1);
+        o[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+      }
+      if (B >= d0 && B + 16 <= d1) {
+        *reinterpret_cast<uint4*>(dst + B) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {  // a ragged end: only the item's bytes (the neighbours belong to other files / items)
+        for (uint32_t j = 0; j < 16; j++) {
+          const uint64_t x = B + j;
+          if (x >= d0 && x < d1) dst[x] = uint8_t(o[j >> 2] >> (8 * (j & 3)));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t GatherHostFiles(const uint8_t* src_dev, const uint64_t* src_off, const uint64_t* dst_off,
+                           const GatherItem* items, uint32_t n_items, uint8_t* dst, hipStream_t s) {
+  if (!n_items) return hipSuccess;
+  const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n_items) + 3) / 4, 8192));
+  gather_host_kernel<<<grid, 256, 0, s>>>(src_dev, src_off, dst_off, items, n_items, dst);
+  return hipGetLastError();
+}
+
+}  // namespace tsg

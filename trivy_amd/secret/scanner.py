@@ -46,10 +46,12 @@ class _CBatch(c.Structure):
 
 class _CBatchExt(c.Structure):  # tsg_batch_ext: struct_size first, then the fields past tsg_batch
     _fields_ = [("struct_size", c.c_uint32), ("base", _CBatch),
-                ("host_paths", c.c_void_p), ("host_path_offsets", c.c_void_p)]
+                ("host_paths", c.c_void_p), ("host_path_offsets", c.c_void_p),
+                ("gather_base", c.c_void_p), ("gather_src", c.c_void_p)]
 
 
-BATCH_EXT_SIZE_V1 = c.sizeof(_CBatchExt)  # TSG_BATCH_EXT_SIZE_V1
+BATCH_EXT_SIZE_V1 = _CBatchExt.gather_base.offset  # TSG_BATCH_EXT_SIZE_V1 (round 5: host paths)
+BATCH_EXT_SIZE_V2 = c.sizeof(_CBatchExt)  # TSG_BATCH_EXT_SIZE_V2 (round 6: + gather_base / gather_src)
 
 
 class _CCompileOptions(c.Structure):  # tsg_compile_options (versioned: struct_size first)
@@ -112,6 +114,7 @@ def _declare(L):
     L.tsg_scanner_rule_anchor.argtypes = [c.c_void_p, c.c_uint32]
     L.tsg_scanner_rule_anchor.restype = c.c_char_p
     L.tsg_host_register.argtypes = [c.c_void_p, c.c_uint64]
+    L.tsg_host_register_mapped.argtypes = [c.c_void_p, c.c_uint64]
     L.tsg_host_unregister.argtypes = [c.c_void_p]
     L._tsg_scanner_declared = True
 
@@ -461,12 +464,15 @@ class ScanResult:
         return out
 
 
-def HostRegister(buf, lib=None):
+def HostRegister(buf, lib=None, mapped: bool = False):
     """Page-lock a numpy buffer (tsg_host_register) so host-resident batches in it stream
-    asynchronously to the GPU; returns an unregister callable."""
+    asynchronously to the GPU; returns an unregister callable.  mapped: also map it into the
+    device's address space (tsg_host_register_mapped) -- a tar layer a gathering collector's
+    batches are read from (Collector(gather=True))."""
     L = lib if lib is not None else _lib.lib()
     _declare(L)
-    if L.tsg_host_register(buf.ctypes.data, buf.nbytes) != 0:
+    reg = L.tsg_host_register_mapped if mapped else L.tsg_host_register
+    if reg(buf.ctypes.data, buf.nbytes) != 0:
         raise RuntimeError("tsg_host_register failed: %s" % _lib.last_error(L))
     return lambda: L.tsg_host_unregister(buf.ctypes.data)
 
