@@ -553,3 +553,66 @@ def test_batch_layouts_round4_and_ext(secret):
     h = c.c_void_p()
     assert s._L.tsg_scan_ext(s._h, c.byref(b), c.byref(h)) < 0
     assert "struct_size 12345" in _lib.last_error(s._L)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [5, 6])
+def test_gather_batch_vs_arena_and_oracle(secret, seed):
+    """tsg_batch_ext v2 gather: the files lie at arbitrary offsets and
+    alignments of a page-locked, device-mapped buffer and the GPU gathers them (xform.hip
+    GatherHostFiles: 16-KiB pieces, kU loads in flight per lane, the byte shift between source and
+    destination alignment) before the pre-transform.  Sizes from 0 to 70 KiB cross the 4-KiB
+    iteration and 16-KiB piece boundaries with secrets planted across them; CRLF text and binary
+    (.pyc-like) files.  Results equal the copied-arena scan's and the oracle's."""
+    import numpy as np
+    from oracle import analyzer as oan
+    rng = random.Random(seed)
+    s = secret.NewScanner(None)
+    o = osc.new_scanner(None)
+    sizes = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1500, 4095, 4096, 4097, 8200, 16383, 16384, 16385,
+             40000, 70000] + [rng.randrange(0, 6000) for _ in range(120)]
+    rng.shuffle(sizes)
+    secrets_ = [b"AKIA" + b"Q" * 16, b"ghp_" + b"a1B2" * 9, b"glpat-" + b"x" * 20]
+    contents, kinds, paths = [], [], []
+    for i, n in enumerate(sizes):
+        b = bytearray(rng.choice(b"abcdefgh ;=\n") for _ in range(n))
+        for at in (4090, 4096 - 10, 16384 - 12, 16384 * 2 - 5, rng.randrange(0, max(1, n))):
+            sec = rng.choice(secrets_)
+            if at + len(sec) + 2 < n:
+                b[at:at + len(sec) + 2] = b" " + sec + b"\n"
+        if i % 7 == 3:  # CRLF text
+            b = bytearray(bytes(b).replace(b"\n", b"\r\n"))
+        kind = 1
+        if i % 11 == 5 and n > 64:  # a binary file: printable runs
+            b[0:4] = b"\x00\x01\x02\x03"
+            kind = 2
+        contents.append(bytes(b))
+        kinds.append(kind)
+        paths.append("f%03d.%s" % (i, "pyc" if kind == 2 else "txt"))
+    # the source buffer: each file after a random gap (>= 16 B before, 32 B after)
+    src_off, pos = [], 64
+    for b in contents:
+        pos += rng.randrange(16, 600)
+        src_off.append(pos)
+        pos += len(b) + 32
+    src = np.zeros(pos + 4096, dtype=np.uint8)
+    for at, b in zip(src_off, contents):
+        src[at:at + len(b)] = np.frombuffer(b, dtype=np.uint8) if b else src[at:at]
+    dst = np.zeros(len(contents) + 1, dtype=np.uint64)
+    dst[1:] = np.cumsum([len(b) for b in contents])  # the batch layout: the files as read, packed
+    arena = np.frombuffer(b"".join(contents) + b"\0" * 64, dtype=np.uint8)
+    kind_arr = np.array(kinds, dtype=np.uint8)
+    unreg = secret.HostRegister(src, mapped=True)
+    try:
+        got = s.scan_arena(None, dst, paths, gather_base=src, gather_src=np.array(src_off, dtype=np.uint64),
+                           transform=kind_arr, binary=[k == 2 for k in kinds]).secrets(paths)
+    finally:
+        unreg()
+    ref = s.scan_arena(arena, dst, paths, transform=kind_arr, binary=[k == 2 for k in kinds]).secrets(paths)
+    n = 0
+    for p, b, k, g, r in zip(paths, contents, kinds, got, ref):
+        t = oan.extract_printable_bytes(b) if k == 2 else b.replace(b"\r", b"")
+        want = o.scan(p, t, binary=k == 2)
+        assert g.to_dict() == r.to_dict() == want, p
+        n += len(want.get("Findings") or [])
+    assert n > 100

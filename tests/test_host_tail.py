@@ -94,6 +94,41 @@ def test_host_tail_many_findings_sort_order():
     assert len(want["Findings"]) > 12
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_host_tail_sort_keys_ties_and_prefixes(tmp_path, seed):
+    """The findings sort compares packed keys (RuleID rank, the match's first 12 bytes, zero-padded)
+    before whole matches: matches equal in those 12 bytes, matches that are prefixes of others,
+    NUL bytes against the padding, exact duplicates on different lines, and two rules whose IDs
+    order opposite to their definition -- the pdqsort permutation is the oracle's."""
+    import random
+    rng = random.Random(seed)
+    cfg_path = tmp_path / "trivy-secret.yaml"
+    cfg_path.write_text(
+        "rules:\n"
+        "  - id: zz-pfx\n    category: Custom\n    title: Z\n    severity: LOW\n"
+        "    regex: 'PFX[a-c\\x00]{0,20}'\n"
+        "  - id: aa-pfx\n    category: Custom\n    title: A\n    severity: LOW\n"
+        "    regex: 'QFX[ab]{0,14}'\n")
+    cfg = ParseConfig(str(cfg_path))
+    alpha = [b"a", b"b", b"c", b"\x00"]
+    lines, pool = [], []
+    for i in range(600):
+        if pool and rng.random() < 0.2:
+            m = rng.choice(pool)  # an exact duplicate, elsewhere in the file
+        elif rng.random() < 0.3:
+            m = b"QFX" + b"".join(rng.choice(alpha[:2]) for _ in range(rng.randrange(0, 15)))
+        else:
+            head = b"aaaaaaaaa" if rng.random() < 0.5 else b""  # 12-byte ties
+            m = b"PFX" + head + b"".join(rng.choice(alpha) for _ in range(rng.randrange(0, 21 - len(head))))
+        pool.append(m)
+        lines.append(b"v%d = %s ;" % (i, m))
+    body = b"\n".join(lines)
+    got = host_tail_scan(cfg, [("ties.txt", body)])[0]
+    want = osc.new_scanner(osc.parse_config(str(cfg_path))).scan("ties.txt", body)
+    assert got.to_dict() == want
+    assert len(want["Findings"]) > 500
+
+
 def test_host_tail_lazy_keyword_gate(tmp_path):
     """MatchKeywords is evaluated after the windowed search: keyword inside the match,
     elsewhere in the file (either case), only via U+0130 / U+212A folding, inside a

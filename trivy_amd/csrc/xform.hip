@@ -1060,6 +1060,12 @@ __global__ __launch_bounds__(256) void gather_host_kernel(const uint8_t* __restr
                                                           const uint64_t* __restrict__ dst_off,
                                                           const GatherItem* __restrict__ items, uint32_t n_items,
                                                           uint8_t* __restrict__ dst) {
+  // The source is host memory read over PCIe (~2-3 us a load): each lane issues
+  // kU + 1 16-B loads before it waits, so a wave keeps ~4 KiB in flight and the
+  // small grid (GatherHostFiles) ~2 MiB -- past the link's bandwidth-delay
+  // product -- while it holds only a few wave slots of the CUs the scan kernels
+  // of the other batches run on.
+  constexpr uint32_t kU = 4;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (uint32_t it = blockIdx.x * 4u + wave; it < n_items; it += gridDim.x * 4u) {
@@ -1074,32 +1080,52 @@ __global__ __launch_bounds__(256) void gather_host_kernel(const uint8_t* __restr
     const uint64_t b_lo = d0 & ~uint64_t(15);
     const uint64_t a_lo = (b_lo + s0 - d0) & ~uint64_t(15);  // (b_lo + s0 - d0 >= s0 - 15 >= 0 in a tar)
     const uint32_t r = uint32_t((b_lo + s0 - d0) & 15u);     // byte shift, the same for every block
-    for (uint64_t k = 0; b_lo + 16 * k < d1; k += 64) {
-      const uint64_t B = b_lo + 16 * (k + lane);
-      const uint64_t A = a_lo + 16 * (k + lane);
-      const bool live = B < d1;
-      uint4 a = make_uint4(0, 0, 0, 0), nxt;
-      if (live) a = *reinterpret_cast<const uint4*>(src + A);
-      // the block after A: the next lane's, the last lane (or the last live one) loads it
-      nxt.x = __shfl_down(a.x, 1);
-      nxt.y = __shfl_down(a.y, 1);
-      nxt.z = __shfl_down(a.z, 1);
-      nxt.w = __shfl_down(a.w, 1);
-      if (live && (lane == 63 || B + 16 >= d1) && r) nxt = *reinterpret_cast<const uint4*>(src + A + 16);
-      if (!live) continue;
-      uint32_t o[4];
-      const uint32_t q = r >> 2, sh = r & 3u;
+    for (uint64_t k = 0; b_lo + 16 * k < d1; k += 64 * kU) {
+      // the blocks of kU groups of 64, and one past the last live one (its
+      // source is the last live block's next); lane 63 of the last group also
+      // loads the block after the iteration's last
+      uint4 a[kU];
 #pragma unroll
-      for (uint32_t w = 0; w < 4; w++) {
-        const uint32_t lo = word_at(a, nxt, q + w), hi = word_at(a, nxt, q + w + 1 > 7 ? 7 : q + w + 1);
-        o[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+      for (uint32_t u = 0; u < kU; u++) {
+        const uint64_t j = k + 64 * u + lane;
+        a[u] = make_uint4(0, 0, 0, 0);
+        if (b_lo + 16 * j < d1 + 16) a[u] = *reinterpret_cast<const uint4*>(src + a_lo + 16 * j);
       }
-      if (B >= d0 && B + 16 <= d1) {
-        *reinterpret_cast<uint4*>(dst + B) = make_uint4(o[0], o[1], o[2], o[3]);
-      } else {  // a ragged end: only the item's bytes (the neighbours belong to other files / items)
-        for (uint32_t j = 0; j < 16; j++) {
-          const uint64_t x = B + j;
-          if (x >= d0 && x < d1) dst[x] = uint8_t(o[j >> 2] >> (8 * (j & 3)));
+      uint4 ex = make_uint4(0, 0, 0, 0);
+      const uint64_t j_ex = k + 64 * kU;  // (lane 63 of the last group: block j_ex - 1)
+      if (r && lane == 63 && b_lo + 16 * (j_ex - 1) < d1) ex = *reinterpret_cast<const uint4*>(src + a_lo + 16 * j_ex);
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+        const uint64_t B = b_lo + 16 * (k + 64 * u + lane);
+        uint4 nxt;
+        nxt.x = __shfl_down(a[u].x, 1);
+        nxt.y = __shfl_down(a[u].y, 1);
+        nxt.z = __shfl_down(a[u].z, 1);
+        nxt.w = __shfl_down(a[u].w, 1);
+        if (u + 1 < kU) {  // lane 63: lane 0's block of the next group
+          const uint4 n0 = make_uint4(__builtin_amdgcn_readlane(a[u + 1 < kU ? u + 1 : u].x, 0),
+                                      __builtin_amdgcn_readlane(a[u + 1 < kU ? u + 1 : u].y, 0),
+                                      __builtin_amdgcn_readlane(a[u + 1 < kU ? u + 1 : u].z, 0),
+                                      __builtin_amdgcn_readlane(a[u + 1 < kU ? u + 1 : u].w, 0));
+          if (lane == 63) nxt = n0;
+        } else if (lane == 63) {
+          nxt = ex;
+        }
+        if (B >= d1) continue;
+        uint32_t o[4];
+        const uint32_t q = r >> 2, sh = r & 3u;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; w++) {
+          const uint32_t lo = word_at(a[u], nxt, q + w), hi = word_at(a[u], nxt, q + w + 1 > 7 ? 7 : q + w + 1);
+          o[w] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+        }
+        if (B >= d0 && B + 16 <= d1) {
+          *reinterpret_cast<uint4*>(dst + B) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {  // a ragged end: only the item's bytes (the neighbours belong to other files / items)
+          for (uint32_t jb = 0; jb < 16; jb++) {
+            const uint64_t x = B + jb;
+            if (x >= d0 && x < d1) dst[x] = uint8_t(o[jb >> 2] >> (8 * (jb & 3)));
+          }
         }
       }
     }
@@ -1111,7 +1137,9 @@ __global__ __launch_bounds__(256) void gather_host_kernel(const uint8_t* __restr
 hipError_t GatherHostFiles(const uint8_t* src_dev, const uint64_t* src_off, const uint64_t* dst_off,
                            const GatherItem* items, uint32_t n_items, uint8_t* dst, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n_items) + 3) / 4, 8192));
+  // 128 workgroups (512 waves, two wave slots per CU): enough loads in flight
+  // for the link (gather_host_kernel), few slots taken from the scan kernels
+  const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n_items) + 3) / 4, 128));
   gather_host_kernel<<<grid, 256, 0, s>>>(src_dev, src_off, dst_off, items, n_items, dst);
   return hipGetLastError();
 }

@@ -317,12 +317,20 @@ class Scanner:
         return (arena_buf, offs, parr, plen, bin_arr, transform), batch
 
     def scan_arena(self, arena, offsets, paths, binary=None, dev_arena=None, dev_offsets=None, dev_paths=None,
-                   dev_path_offsets=None, host_paths=None, host_path_offsets=None):
+                   dev_path_offsets=None, host_paths=None, host_path_offsets=None, gather_base=None,
+                   gather_src=None, transform=None):
         """One batch (tsg_scan).  dev_arena / dev_offsets: the contents already in HBM;
         dev_paths / dev_path_offsets: the paths packed in HBM (GPU allow-path prefilter);
         host_paths / host_path_offsets (numpy u8 / u64): the paths packed in host memory, passed
-        through the versioned tsg_batch_ext (tsg_scan_ext)."""
+        through the versioned tsg_batch_ext (tsg_scan_ext).  gather_base (a uint8 array registered
+        with HostRegister(mapped=True)) / gather_src (u64): file f's bytes as read are
+        gather_base[gather_src[f]:][:offsets[f+1]-offsets[f]] -- arena None, transform (u8 per file:
+        1 text, 2 binary) required (tsg_batch_ext v2)."""
         n = len(offsets) - 1
+        if gather_base is not None:
+            if arena is not None or transform is None or gather_src is None:
+                raise ValueError("scan_arena(gather): arena None, gather_src and transform required")
+            arena = np.zeros(1, np.uint8)  # (not passed: host_arena is NULL in a gathered batch)
         arena_buf = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
         if isinstance(paths, np.ndarray) and paths.dtype == np.uint64:
@@ -335,12 +343,21 @@ class Scanner:
             paths_addr = c.cast(parr, c.c_void_p).value
             plen_ptr = plen.ctypes.data
         bin_arr = np.array(binary, dtype=np.uint8) if binary is not None else None
-        batch = _CBatch(n, arena_buf.ctypes.data, offs.ctypes.data,
+        kinds = np.ascontiguousarray(transform, dtype=np.uint8) if transform is not None else None
+        batch = _CBatch(n, None if gather_base is not None else arena_buf.ctypes.data, offs.ctypes.data,
                         dev_arena, dev_offsets, paths_addr, plen_ptr,
-                        bin_arr.ctypes.data if bin_arr is not None else None, None,
+                        bin_arr.ctypes.data if bin_arr is not None else None,
+                        kinds.ctypes.data if kinds is not None else None,
                         dev_paths, dev_path_offsets)
         h = c.c_void_p()
-        if host_paths is not None:
+        if gather_base is not None:
+            gsrc = np.ascontiguousarray(gather_src, dtype=np.uint64)
+            ext = _CBatchExt(BATCH_EXT_SIZE_V2, batch,
+                             host_paths.ctypes.data if host_paths is not None else None,
+                             host_path_offsets.ctypes.data if host_path_offsets is not None else None,
+                             gather_base.ctypes.data, gsrc.ctypes.data)
+            rc = self._L.tsg_scan_ext(self._h, c.byref(ext), c.byref(h))
+        elif host_paths is not None:
             ext = _CBatchExt(BATCH_EXT_SIZE_V1, batch, host_paths.ctypes.data, host_path_offsets.ctypes.data)
             rc = self._L.tsg_scan_ext(self._h, c.byref(ext), c.byref(h))
         else:
