@@ -45,7 +45,7 @@ for st in $STAGES; do
       find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
     c4prof)  # rocprofv3 kernel stats of a short C4 run (the pre-transform kernels per batch)
       cd /tmp
-      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/c4prof_$TAG -o run --output-format csv -- python3 $R/bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/c4prof_bench_$TAG.json 2> $R/gpurun_out/c4prof_$TAG.err
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/c4prof_$TAG -o run --output-format csv -- python3 $R/bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline ${C4PROF_ARGS:-} > $R/gpurun_out/c4prof_bench_$TAG.json 2> $R/gpurun_out/c4prof_$TAG.err
       rc=$?; cd $R; tail -2 gpurun_out/c4prof_$TAG.err; [ $rc -eq 0 ] || exit $rc
       find gpurun_out/c4prof_$TAG -name '*kernel_stats.csv' -exec cat {} \; ;;
     ingprof)  # the C2 ingest leg under a kernel + memory-copy trace (copy / kernel timeline)

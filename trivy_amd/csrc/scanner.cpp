@@ -76,36 +76,17 @@ size_t RarestIndex(const std::string& kw) {
 // ---------------------------------------------------------------------------
 // Go sort.Slice = pdqsort_func (sort/zsortfunc.go), restated.
 // ---------------------------------------------------------------------------
-// The sort runs over compact keys -- (RuleID rank, the match's first 12 bytes
-// big-endian, zero-padded) and the finding's index -- and permutes the findings
-// once at the end.  Less decides from the keys whenever they differ (the first
-// differing byte, or a shorter match reading as 0 bytes against a longer one
-// whose byte there is nonzero) and compares the whole matches otherwise, so it
-// answers every Less exactly as the RuleID / Match comparison would: pdqsort
-// makes the same moves, the permutation is the reference's.
-struct SortKey {
-  uint64_t a, b;  // rank << 32 | match[0..4) ; match[4..12)
-  uint32_t idx, pad;
-};
-
 struct SortData {
-  SortKey* k;
-  const FileFindings* v;
+  FileFindings* v;
+  const uint32_t* rank;  // per rule: the rank of its ID among the rules' IDs (equal IDs, equal rank)
   bool Less(int i, int j) const {
-    const SortKey& x = k[i];
-    const SortKey& y = k[j];
-    if (x.a != y.a) return x.a < y.a;  // RuleID < RuleID, or the first match bytes
-    if (x.b != y.b) return x.b < y.b;
-    return v->Match(v->f[x.idx]) < v->Match(v->f[y.idx]);
+    const FindingOut& a = v->f[size_t(i)];
+    const FindingOut& b = v->f[size_t(j)];
+    if (rank[a.rule] != rank[b.rule]) return rank[a.rule] < rank[b.rule];  // RuleID < RuleID
+    return v->Match(a) < v->Match(b);
   }
-  void Swap(int i, int j) { std::swap(k[i], k[j]); }
+  void Swap(int i, int j) { std::swap(v->f[size_t(i)], v->f[size_t(j)]); }
 };
-
-inline uint64_t BigEndianPrefix(std::string_view m, size_t at, size_t n) {  // bytes [at, at + n), zero-padded
-  uint64_t r = 0;
-  for (size_t q = 0; q < n; q++) r = (r << 8) | (at + q < m.size() ? uint8_t(m[at + q]) : 0u);
-  return r;
-}
 
 void InsertionSort(SortData& d, int a, int b) {
   for (int i = a + 1; i < b; i++)
@@ -312,22 +293,14 @@ std::vector<uint32_t> RuleRanks(const std::vector<RuleSpec>& rules) {
   return rank;
 }
 
+// (A variant sorting packed keys -- RuleID rank and the match's first 12 bytes --
+// measured slower on C3f: its findings' matches are censored line windows, runs
+// of '*' equal well past 12 bytes, so the keys tie and the whole-match compare
+// runs anyway, behind an indirection.)
 void SortFindings(FileFindings* f, const std::vector<uint32_t>& rule_rank) {
-  const int n = int(f->size());
-  if (n < 2) return;
-  thread_local std::vector<SortKey> keys;
-  thread_local std::vector<FindingOut> perm;
-  keys.resize(size_t(n));
-  for (int i = 0; i < n; i++) {
-    const FindingOut& x = f->f[size_t(i)];
-    const std::string_view m = f->Match(x);
-    keys[size_t(i)] = SortKey{(uint64_t(rule_rank[x.rule]) << 32) | BigEndianPrefix(m, 0, 4),
-                              BigEndianPrefix(m, 4, 8), uint32_t(i), 0};
-  }
-  SortData d{keys.data(), f};
+  SortData d{f, rule_rank.data()};
+  int n = int(f->size());
   Pdqsort(d, 0, n, BitsLen(unsigned(n)));
-  perm.assign(f->f.begin(), f->f.end());
-  for (int i = 0; i < n; i++) f->f[size_t(i)] = perm[keys[size_t(i)].idx];
 }
 
 bool SimpleLiteral(const std::string& src, std::vector<std::string>* lits, bool* begin, bool* end) {
