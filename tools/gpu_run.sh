@@ -64,6 +64,16 @@ for st in $STAGES; do
     dump)  # candidates of one C3f scan for tools/host_tail_bench.py (CPU profiling of the exact pass)
       TSG_TAIL_DEBUG=1 TSG_DUMP_CANDS=$R/gpurun_out/cands_${DUMP_WL:-c3f}.bin timeout -k 10 600 python bench.py --workload ${DUMP_WL:-c3f} --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/dump_$TAG.json 2> gpurun_out/dump_$TAG.err
       rc=$?; ls -la gpurun_out/cands_${DUMP_WL:-c3f}.bin; grep -a "tail" gpurun_out/dump_$TAG.err | tail -4; [ $rc -eq 0 ] || exit $rc ;;
+    k1x)  # the K1 inner-loop experiments (tools/k1x.hip, built in-tree beforehand), K1X_ONLY: variant indices
+      timeout -k 10 400 python tools/k1x.py --gb ${K1X_GB:-20} --reps 5 ${K1X_ONLY:+--only $K1X_ONLY} > gpurun_out/k1x_$TAG.log 2>&1
+      rc=$?; cat gpurun_out/k1x_$TAG.log | grep -v "^$" | tail -40; [ $rc -eq 0 ] || exit $rc ;;
+    k1xpmc)  # SQ counters of chosen k1x variants (one --pmc pass per counter set)
+      cd /tmp
+      for v in ${K1X_ONLY:-19}; do
+        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_BUSY_CYCLES -d $R/gpurun_out/k1xpmc_${TAG}_$v -o run --output-format csv -- python3 $R/tools/k1x.py --gb ${K1X_GB:-20} --reps 1 --only $v > $R/gpurun_out/k1xpmc_${TAG}_$v.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || { cd $R; tail -5 gpurun_out/k1xpmc_${TAG}_$v.log; exit $rc; }
+      done
+      cd $R ;;
     c4l)  # C4 under several bench arg sets (C4L_SPECS, '|'-separated), e.g. "--layers 1|--layers 5 --layer-parallel 3"
       IFS='|' read -r -a specs <<< "${C4L_SPECS:---layers 1}"
       for i in "${!specs[@]}"; do

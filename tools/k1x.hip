@@ -10,8 +10,12 @@
 //         2: 8 buckets, ds_read_b64 table replicated 32x)
 //   LB    bytes per lane per tile
 //   GRP   table reads issued ahead of the chain (per stream)
-//   MODE  0 full, 1 LDS reads only (no chain), 2 chain on data-derived words
-//         (no LDS), 3 loads only
+//   MODE  0 full, 1 LDS reads only (no chain; every word XOR-ed so the reads stay
+//         b128), 2 the full loop's VALU with the row = its v_perm address (no LDS;
+//         round 6: before, a multiply per word inflated the VALU), 3 loads only, 4 full with a rolling ring of GRP table rows
+//         (row k + GRP read as row k is applied: GRP reads in flight at every
+//         step, no group-boundary drain), 5 = 4 with sched_group_barrier
+//         pinning the order (1 ds_read after every row's 4 v_lshl_or)
 //   STR   independent shift-or streams per lane (2: the lane's chunk halves,
 //         the second warmed up on the 5 bytes before it)
 //   MINW  workgroups of 1024 per CU (__launch_bounds__ min waves per SIMD / 4)
@@ -37,13 +41,12 @@ struct Row {
 template <int NREG, int MODE>
 __device__ __forceinline__ Row<NREG> rd(const uint8_t* sb, uint32_t word, uint32_t k, uint32_t laneoff) {
   Row<NREG> r;
-  if (MODE == 2) {
-    const uint32_t x = (word >> (8 * k)) & 0xFFu;
+  const uint32_t a = __builtin_amdgcn_perm(word, laneoff, 0x0C0C0000u | ((4u + k) << 8));
+  if (MODE == 2 || MODE == 6) {  // the row = the address itself: the full loop's VALU, no LDS
 #pragma unroll
-    for (int i = 0; i < NREG; i++) r.w[i] = (x * (0x01010101u + 2 * i)) | (laneoff << i);
+    for (int i = 0; i < NREG; i++) r.w[i] = a;
     return r;
   }
-  const uint32_t a = __builtin_amdgcn_perm(word, laneoff, 0x0C0C0000u | ((4u + k) << 8));
   if (NREG == 4) {
     const uint4 v = *reinterpret_cast<const uint4*>(sb + a);
     r.w[0] = v.x;
@@ -128,10 +131,39 @@ __global__ __launch_bounds__(1024, 4 * MINW) void k1x(const uint8_t* __restrict_
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) {
           Row<NREG> m = rd<NREG, 0>(s_tab, wd, k, laneoff);
-          x ^= m.w[0] ^ m.w[NREG - 1];
+#pragma unroll
+          for (int w = 0; w < NREG; w++) x ^= m.w[w];  // every word: the whole ds_read_b128 stays
         }
       }
       sink ^= x ^ p0 ^ p1;
+      return;
+    }
+    if (MODE == 4 || MODE == 5) {  // rolling ring (STR 1)
+      uint32_t st[NREG];
+#pragma unroll
+      for (int i = 0; i < NREG; i++) st[i] = ~0u;
+      apply<NREG>(rd<NREG, 0>(s_tab, p0, 3, laneoff), st);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) apply<NREG>(rd<NREG, 0>(s_tab, p1, k, laneoff), st);
+      Row<NREG> ring[GRP];
+#pragma unroll
+      for (int q = 0; q < GRP; q++) ring[q] = rd<NREG, 0>(s_tab, wsel(cur, q >> 2), q & 3, laneoff);
+      uint32_t acc = ~0u;
+#pragma unroll
+      for (int k = 0; k < LB; k++) {
+        apply<NREG>(ring[k % GRP], st);
+        if (k + GRP < LB) ring[k % GRP] = rd<NREG, 0>(s_tab, wsel(cur, (k + GRP) >> 2), (k + GRP) & 3, laneoff);
+        if (k % 3 == 2 || k % 16 == 15) acc &= all_and<NREG>(st);
+        if (k % 4 == 3) nl += __popc(~st[NREG - 1] & 0x8888u);
+        if (k % 16 == 15) {
+          flagged += (acc | ~kFire) != ~0u;
+          acc = ~0u;
+        }
+        if (MODE == 5) {
+          __builtin_amdgcn_sched_group_barrier(0x0002, NREG + 2, 0);  // the row's VALU (+ perm / and)
+          __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);         // then the next row's ds_read
+        }
+      }
       return;
     }
     constexpr int SL = LB / STR;  // bytes per stream
@@ -139,7 +171,7 @@ __global__ __launch_bounds__(1024, 4 * MINW) void k1x(const uint8_t* __restrict_
 #pragma unroll
     for (int s = 0; s < STR; s++)
 #pragma unroll
-      for (int i = 0; i < NREG; i++) st[s][i] = ~0u;
+      for (int i = 0; i < NREG; i++) st[s][i] = ~0u ^ uint32_t(MODE == 2 ? i : 0);  // (MODE 2: distinct chains)
     // warm-up: 5 bytes before each stream
     {
       Row<NREG> m0 = rd<NREG, MODE>(s_tab, p0, 3, laneoff);
@@ -238,6 +270,19 @@ const Variant kVariants[] = {
     V("r4 lb64 g16 lds-only 2wg", 4, 64, 16, 1, 1, 2),
     V("r4 lb64 g16 no-lds 2wg", 4, 64, 16, 2, 1, 2),
     V("r2 lb64 g16 full s1 2wg", 2, 64, 16, 0, 1, 2),
+    // round 6: rolling ring of table rows instead of read groups
+    V("r4 lb64 ring4 s1 2wg", 4, 64, 4, 4, 1, 2),
+    V("r4 lb64 ring6 s1 2wg", 4, 64, 6, 4, 1, 2),
+    V("r4 lb64 ring8 s1 2wg", 4, 64, 8, 4, 1, 2),
+    V("r4 lb64 ring4 sgb s1 2wg", 4, 64, 4, 5, 1, 2),
+    V("r4 lb64 ring6 sgb s1 2wg", 4, 64, 6, 5, 1, 2),
+    V("r4 lb64 ring8 sgb s1 2wg", 4, 64, 8, 5, 1, 2),
+    V("r4 lb64 ring4 s1", 4, 64, 4, 4, 1, 1),
+    V("r4 lb64 ring8 s1", 4, 64, 8, 4, 1, 1),
+    V("r4 lb64 ring8 sgb s1", 4, 64, 8, 5, 1, 1),
+    V("r4 lb64 ring12 sgb s1", 4, 64, 12, 5, 1, 1),
+    V("r4 lb64 g8 lds-only 2wg", 4, 64, 8, 1, 1, 2),
+    V("r4 lb64 g8 no-lds 2wg", 4, 64, 8, 2, 1, 2),
 };
 #undef V
 
