@@ -644,6 +644,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    # one rank per GPU; on a box with fewer GPUs than ranks (a rehearsal of the N-rank path, e.g.
+    # --gpus 2 on one GPU) the ranks share devices round-robin and the line says so
+    n_dev = torch.cuda.device_count()  # (does not initialise the GPU)
+    shared_devices = 0 < n_dev < world  # the same on every rank of the node
+    local = local % n_dev if n_dev > 0 else local
     torch.cuda.set_device(local)
     numa_node = _bind_numa(local) if args.numa == "gpu" else None
 
@@ -1024,7 +1029,10 @@ def main():
             "config": dict({"workload": wl_desc % args.gb, "workload_id": args.workload,
                             "parallelism": "files sharded, dp%d" % world,
                             "rules_compile_s": round(t_compile, 2),
-                            "host_numa_node": numa_node}, **config_extra),
+                            "host_numa_node": numa_node}, **config_extra,
+                           **({"devices_shared": "%d ranks on %d GPU(s), round-robin: a rehearsal of the "
+                                                 "N-rank path, not a scaling number" % (world, n_dev)}
+                              if shared_devices else {})),
             "roofline": roofline,
             "ingest": ingest,
             "cpu_baseline": cpu,

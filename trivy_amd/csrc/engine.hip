@@ -2486,8 +2486,15 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     // overrides (tuning).
     size_t lds_max = 160 * 1024 * size_t(kCThreads) / 1024;  // 16 waves per CU
     if (const char* e = std::getenv("TSG_LDS_TABS_MAX")) lds_max = size_t(std::strtoull(e, nullptr, 10));
-    lds_tabs_ = fixed + ftabs_bytes_ <= lds_max &&
-                ftabs_fold_bytes_ + 32 * size_t(n_fitems_) + kFoldWaves * kFoldWin <= 64 * 1024;  // fold kernel too
+    // the fold kernel too: its dynamic tables beside its whole static LDS (windows,
+    // index lists, cooperative-site state), as the compiler laid it out
+    size_t fold_static = kFoldWaves * kFoldWin;
+    {
+      hipFuncAttributes fa{};
+      if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fold_kernel<true>)) == hipSuccess)
+        fold_static = std::max(fold_static, size_t(fa.sharedSizeBytes));
+    }
+    lds_tabs_ = fixed + ftabs_bytes_ <= lds_max && ftabs_fold_bytes_ + 32 * size_t(n_fitems_) + fold_static <= 64 * 1024;
     if (!item_diag_path_.empty() && hipMalloc(&d_item_diag_, 8 * std::max<size_t>(n_fitems_, 1)) != hipSuccess) {
       err_ = "hipMalloc item diag";
       return;
@@ -2502,9 +2509,10 @@ GpuEngine::GpuEngine(const CompiledRules& cr, int device) : device_(device) {
     }
     if (const char* e = std::getenv("TSG_CONFIRM_LDS_PAD")) c_lds_bytes_ += size_t(std::strtoull(e, nullptr, 10));  // occupancy experiments
     if (std::getenv("TSG_ENGINE_DEBUG"))
-      std::fprintf(stderr, "confirm LDS: fixed %zu + tables %u (fold prefix %u) = %zu B, limit %zu, %s tables, %d threads\n",
+      std::fprintf(stderr, "confirm LDS: fixed %zu + tables %u (fold prefix %u) = %zu B, limit %zu, %s tables, %d threads; "
+                   "fold kernel static LDS %zu B\n",
                    fixed, ftabs_bytes_, ftabs_fold_bytes_, c_lds_bytes_, lds_max, lds_tabs_ ? "LDS" : "global",
-                   lds_tabs_ ? kCThreads : kCThreadsG);
+                   lds_tabs_ ? kCThreads : kCThreadsG, fold_static);
     hipFuncSetAttribute(reinterpret_cast<const void*>(lds_tabs_ ? &confirm_kernel<true> : &confirm_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, int(c_lds_bytes_));
     if (lds_tabs_)
