@@ -200,4 +200,24 @@ int tsg_debug_pool_peak(int callers, uint64_t n, int item_us, int wide, int* ste
   return peak.load();
 }
 
+int tsg_debug_sort_findings(uint32_t n, const uint32_t* rule, const uint32_t* rule_rank, uint32_t n_rules,
+                            const char* text, uint64_t text_len, const uint32_t* match_off, const uint32_t* match_len,
+                            int threads, uint32_t* out_order) {
+  tsg::FileFindings ff;
+  ff.text.assign(text, size_t(text_len));
+  ff.f.resize(n);
+  for (uint32_t i = 0; i < n; i++) {
+    ff.f[i] = tsg::FindingOut{};
+    ff.f[i].rule = rule[i];
+    ff.f[i].start_line = int64_t(i);  // the original position, read back as the permutation
+    ff.f[i].match_off = match_off[i];
+    ff.f[i].match_len = match_len[i];
+  }
+  const std::vector<uint32_t> rank(rule_rank, rule_rank + n_rules);
+  if (threads > 0) tsg::SortFindingsParallel(&ff, rank, threads, false);
+  else tsg::SortFindings(&ff, rank);
+  for (uint32_t i = 0; i < n; i++) out_order[i] = uint32_t(ff.f[i].start_line);
+  return 0;
+}
+
 }  // extern "C"

@@ -42,6 +42,14 @@ int tsg_cpuref_scan(const tsg_global* g, const tsg_batch* b, int threads, tsg_re
  * once, and the pool's steady / total worker counts. */
 int tsg_debug_pool_peak(int callers, uint64_t n, int item_us, int wide, int* steady, int* workers);
 
+/* The findings sort (scanner.go:452-457, pdqsort): n findings with rule ids,
+ * RuleID ranks and match texts; threads 0 = SortFindings, > 0 =
+ * SortFindingsParallel on that many pool threads.  out_order[i] = the original
+ * index of the finding sorted to position i. */
+int tsg_debug_sort_findings(uint32_t n, const uint32_t* rule, const uint32_t* rule_rank, uint32_t n_rules,
+                            const char* text, uint64_t text_len, const uint32_t* match_off, const uint32_t* match_len,
+                            int threads, uint32_t* out_order);
+
 #ifdef __cplusplus
 }
 #endif

@@ -426,3 +426,46 @@ def test_host_tail_file_ids_past_2_pow_22():
     assert len(rec) == n > 10
     assert np.all(np.diff(rec["file"].astype(np.int64)) >= 0)
     assert set(rec["file"].tolist()) <= set(ids)
+
+
+def _sort_case(rng, n, n_rules=4):
+    """n findings: rule ids (two rules share an ID rank), matches from runs of '*' and a few letters
+    (censored windows: long common prefixes, many exact ties)."""
+    rank = np.array([2, 0, 2, 1][:n_rules], dtype=np.uint32)
+    rule = rng.integers(0, n_rules, n).astype(np.uint32)
+    pool = [b"*" * int(rng.integers(10, 60)) + bytes(rng.choice(list(b"ab *"), int(rng.integers(0, 5))))
+            for _ in range(max(8, n // 6))]
+    texts = [pool[int(rng.integers(0, len(pool)))] for _ in range(n)]
+    off = np.zeros(n, dtype=np.uint32)
+    off[1:] = np.cumsum([len(t) for t in texts])[:-1]
+    return rule, rank, b"".join(texts), off, np.array([len(t) for t in texts], dtype=np.uint32), texts
+
+
+def _native_sort(L, rule, rank, text, off, ln, threads):
+    n = len(rule)
+    out = np.zeros(n, dtype=np.uint32)
+    L.tsg_debug_sort_findings.argtypes = [c.c_uint32, c.c_void_p, c.c_void_p, c.c_uint32, c.c_char_p, c.c_uint64,
+                                          c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    assert L.tsg_debug_sort_findings(n, rule.ctypes.data, rank.ctypes.data, len(rank), text, len(text),
+                                     off.ctypes.data, ln.ctypes.data, threads, out.ctypes.data) == 0
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_findings_sort_parallel_equals_sequential(seed):
+    """SortFindingsParallel (the heaviest files' sort after GPU materialisation) spreads pdqsort's
+    independent recursive calls over the pool; its permutation -- ties included -- is the sequential
+    pdqsort's, and at a size the Python restatement finishes, Go's sort.Slice's (oracle/gosort.py)."""
+    from oracle import gosort
+    L = hostlib.lib()
+    rng = np.random.default_rng(seed)
+    rule, rank, text, off, ln, _ = _sort_case(rng, 120_000)
+    seq = _native_sort(L, rule, rank, text, off, ln, 0)
+    for threads in (2, 8, 16):
+        assert np.array_equal(_native_sort(L, rule, rank, text, off, ln, threads), seq), threads
+    rule, rank, text, off, ln, texts = _sort_case(rng, 6000)
+    seq = _native_sort(L, rule, rank, text, off, ln, 0)
+    assert np.array_equal(_native_sort(L, rule, rank, text, off, ln, 8), seq)
+    items = list(range(len(rule)))
+    gosort.sort_slice(items, lambda i, j: (rank[rule[i]], texts[i]) < (rank[rule[j]], texts[j]))
+    assert np.array_equal(np.array(items, dtype=np.uint32), seq)

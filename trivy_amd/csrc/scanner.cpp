@@ -15,6 +15,8 @@
 #include <cstring>
 #include <functional>
 #include <thread>
+#include <condition_variable>
+#include <mutex>
 
 namespace tsg {
 
@@ -236,7 +238,17 @@ int Partition(SortData& d, int a, int b, int pivot, bool* already) {
   return j;
 }
 
-void Pdqsort(SortData& d, int a, int b, int limit) {
+// A recursive call of pdqsort works on its own range and reads only the element
+// before it (a pivot, or an element equal to one, that an enclosing call put in
+// its final place), so the calls are independent: `spawn` (when set) takes the
+// ones of at least `min_spawn` elements to run on other threads, and the moves
+// each makes are the sequential sort's.
+struct SortSpawn {
+  virtual void Push(int a, int b, int limit) = 0;
+  int min_spawn = 1 << 30;
+};
+
+void Pdqsort(SortData& d, int a, int b, int limit, SortSpawn* spawn = nullptr) {
   bool was_balanced = true, was_partitioned = true;
   for (;;) {
     int length = b - a;
@@ -272,11 +284,13 @@ void Pdqsort(SortData& d, int a, int b, int limit) {
     int left = mid - a, right = b - mid, thr = length / 8;
     if (left < right) {
       was_balanced = left >= thr;
-      Pdqsort(d, a, mid, limit);
+      if (spawn && left >= spawn->min_spawn) spawn->Push(a, mid, limit);
+      else Pdqsort(d, a, mid, limit, spawn);
       a = mid + 1;
     } else {
       was_balanced = right >= thr;
-      Pdqsort(d, mid + 1, b, limit);
+      if (spawn && right >= spawn->min_spawn) spawn->Push(mid + 1, b, limit);
+      else Pdqsort(d, mid + 1, b, limit, spawn);
       b = mid;
     }
   }
@@ -301,6 +315,53 @@ void SortFindings(FileFindings* f, const std::vector<uint32_t>& rule_rank) {
   SortData d{f, rule_rank.data()};
   int n = int(f->size());
   Pdqsort(d, 0, n, BitsLen(unsigned(n)));
+}
+
+// The same permutation with the independent recursive calls (SortSpawn) spread
+// over `threads` pool threads: a file with tens of thousands of findings (C3f's
+// heaviest holds ~50 k) otherwise sorts on one thread for ~8 ms while the
+// scan's other work has drained.  Must not run inside another ParallelFor item.
+void SortFindingsParallel(FileFindings* f, const std::vector<uint32_t>& rule_rank, int threads, bool wide) {
+  const int n = int(f->size());
+  if (threads <= 1 || n < 4096) return SortFindings(f, rule_rank);
+  struct Task {
+    int a, b, limit;
+  };
+  struct Queue : SortSpawn {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Task> q;
+    int active = 0;
+    void Push(int a, int b, int limit) override {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        q.push_back(Task{a, b, limit});
+      }
+      cv.notify_one();
+    }
+  } Q;
+  Q.min_spawn = std::max(1024, n / (8 * threads));
+  Q.q.push_back(Task{0, n, BitsLen(unsigned(n))});
+  ParallelFor(size_t(threads), threads, [&](size_t) {
+    SortData d{f, rule_rank.data()};
+    for (;;) {
+      Task t;
+      {
+        std::unique_lock<std::mutex> lk(Q.mu);
+        Q.cv.wait(lk, [&] { return !Q.q.empty() || Q.active == 0; });
+        if (Q.q.empty()) return;  // nothing queued and nothing running: done
+        t = Q.q.back();
+        Q.q.pop_back();
+        Q.active++;
+      }
+      Pdqsort(d, t.a, t.b, t.limit, &Q);
+      {
+        std::lock_guard<std::mutex> g(Q.mu);
+        Q.active--;
+      }
+      Q.cv.notify_all();
+    }
+  }, wide);
 }
 
 bool SimpleLiteral(const std::string& src, std::vector<std::string>* lits, bool* begin, bool* end) {
@@ -1831,11 +1892,34 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
     if (head < n) std::nth_element(ord.begin(), ord.begin() + long(head), ord.end(), heavier);
     std::sort(ord.begin(), ord.begin() + long(head), heavier);
     if (head < n) std::sort(ord.begin() + long(head), ord.end());  // the rest in file order
+    // the heaviest files first, each sorted by all the threads (SortFindingsParallel):
+    // one of ~50 k findings alone is an ~8-ms pdqsort
+    size_t heavy = 0;
+    static const size_t kHeavy = [] {
+      const char* e = std::getenv("TSG_SORT_PAR_MIN");
+      return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(16384);
+    }();
+    while (heavy < head && heavy < 8 && tmp[gk[a + ord[heavy]]].gm.size() >= kHeavy) {
+      const size_t i = ord[heavy];
+      FileResult& R = tmp[gk[a + i]];
+      const size_t x = m0[i], y = x + R.gm.size();
+      const uint64_t p0 = pref[x], p1 = pref[y];
+      FileFindings& ff = R.findings;
+      ff = FileFindings(thread_arena());
+      ff.f.assign(fo + x, fo + y);
+      ff.lines.assign(lo + uint32_t(p0), lo + uint32_t(p1));
+      ff.text.assign(tx + (p0 >> 32), tx + (p1 >> 32));
+      SortFindingsParallel(&ff, rule_rank_, host_threads_, wide);
+      R.kind = kHasFindings;
+      heavy++;
+    }
+    const double h1 = NowMs();
     constexpr size_t kBlk2 = 64;
     const size_t n_items = head + (n - head + kBlk2 - 1) / kBlk2;
     static const bool times = std::getenv("TSG_TAIL_TIMES") != nullptr;
     std::atomic<uint64_t> us_copy{0}, us_sort{0}, us_max{0};  // (TSG_TAIL_TIMES)
     ParallelFor(n_items, host_threads_, [&](size_t it) {
+      if (it < heavy) return;  // (sorted above)
       const size_t lo_i = it < head ? it : head + (it - head) * kBlk2;
       const size_t hi_i = it < head ? it + 1 : std::min(n, lo_i + kBlk2);
       double c_ms = 0, s_ms = 0;
@@ -1871,8 +1955,9 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
     mat_->End(job);
     if (times)
       std::fprintf(stderr, "gpu findings ms: slot+fill %.2f gpu %.2f assemble+sort %.2f (files %zu, findings %llu, "
-                   "spans %llu; thread-ms copy %.2f sort %.2f, longest item %.2f; lines %u text %.1f MB)\n",
-                   g0 - f0, g1 - g0, NowMs() - g1, b - a, (unsigned long long)nm, (unsigned long long)ns,
+                   "spans %llu; heavy files %zu in %.2f; thread-ms copy %.2f sort %.2f, longest item %.2f; lines %u "
+                   "text %.1f MB)\n",
+                   g0 - f0, g1 - g0, NowMs() - g1, b - a, (unsigned long long)nm, (unsigned long long)ns, heavy, h1 - g1,
                    us_copy.load() * 1e-3, us_sort.load() * 1e-3, us_max.load() * 1e-3, uint32_t(pref[nm]),
                    double(pref[nm] >> 32) * 1e-6);
     a = b;

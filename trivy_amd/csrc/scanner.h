@@ -372,6 +372,9 @@ class SecretScanner {
 // Go sort.Slice restatement (pdqsort_func) on findings, scanner.go:452-457.
 // rule_rank: per rule, the rank of its ID in the sorted IDs (RuleRanks).
 void SortFindings(FileFindings* f, const std::vector<uint32_t>& rule_rank);
+// SortFindings' permutation, the independent pdqsort calls spread over the pool
+// (not from inside a ParallelFor item)
+void SortFindingsParallel(FileFindings* f, const std::vector<uint32_t>& rule_rank, int threads, bool wide);
 std::vector<uint32_t> RuleRanks(const std::vector<RuleSpec>& rules);
 
 }  // namespace tsg
