@@ -1892,14 +1892,17 @@ bool SecretScanner::GpuFindings(const BatchInput& in, TailScratch* scr, size_t n
     if (head < n) std::nth_element(ord.begin(), ord.begin() + long(head), ord.end(), heavier);
     std::sort(ord.begin(), ord.begin() + long(head), heavier);
     if (head < n) std::sort(ord.begin() + long(head), ord.end());  // the rest in file order
-    // the heaviest files first, each sorted by all the threads (SortFindingsParallel):
-    // one of ~50 k findings alone is an ~8-ms pdqsort
+    // a wide pass (the pipeline's last scan: the pool is otherwise idle) sorts the
+    // heaviest files first, each by all the threads (SortFindingsParallel): one of
+    // ~50 k findings alone is an ~8-ms pdqsort.  Beside other scans' passes the
+    // threads are taken, and that costs more than it saves (C3f at depth 6: the
+    // four heavy files 13-17 ms vs 8 ms as single items beside the rest)
     size_t heavy = 0;
     static const size_t kHeavy = [] {
       const char* e = std::getenv("TSG_SORT_PAR_MIN");
       return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(16384);
     }();
-    while (heavy < head && heavy < 8 && tmp[gk[a + ord[heavy]]].gm.size() >= kHeavy) {
+    while (wide && heavy < head && heavy < 8 && tmp[gk[a + ord[heavy]]].gm.size() >= kHeavy) {
       const size_t i = ord[heavy];
       FileResult& R = tmp[gk[a + i]];
       const size_t x = m0[i], y = x + R.gm.size();
