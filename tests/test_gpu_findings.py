@@ -82,11 +82,11 @@ def test_gpu_findings_edge_cases_vs_oracle_and_host(seed):
     files = _edge_files(seed)
     s = secret.NewScanner(None)
     o = osc.new_scanner(None)
-    assert s.set_gpu_findings(True) == 2  # (the default: auto)
+    assert s.set_gpu_findings(True) == 0  # (the default: on the host)
     gpu, r = _resident_scan(s, files)
     s.set_gpu_findings(False)
     host, _ = _resident_scan(s, files)
-    s.set_gpu_findings(2)
+    s.set_gpu_findings(0)
     n = 0
     for (p, b), g, h in zip(files, gpu, host):
         want = o.scan(p, b)

@@ -516,10 +516,16 @@ SecretScanner::SecretScanner(std::vector<RuleSpec> rules, std::vector<AllowRuleS
       return;
     }
   }
-  // findings of HBM-resident batches: 2 (default) on the GPU while the exact
-  // pass is the bound, 1 always on the GPU, 0 on the host (TSG_GPU_FINDINGS)
+  // findings of HBM-resident batches: 0 (default) on the host, 1 always on the
+  // GPU, 2 on the GPU while the exact pass is the bound (TSG_GPU_FINDINGS).  The
+  // host is the default because it measured faster on C3f, the finding-dense
+  // case the GPU pass was built for: 536 vs 474 GB/s at depth 4, 578 vs 516 at
+  // depth 6 (one box, 20 steps, profiles/r06/c3f) -- the GPU pass frees ~4 of
+  // 16 host CPUs, but its round trip behind the other scans' kernels (6-8 ms)
+  // and the host-side copy and sort that remain cost more latency than the
+  // freed CPUs return
   const char* gf = std::getenv("TSG_GPU_FINDINGS");
-  gpu_findings_.store(gf ? std::max(0, std::min(2, std::atoi(gf))) : 2);
+  gpu_findings_.store(gf ? std::max(0, std::min(2, std::atoi(gf))) : 0);
   mat_.reset(new FindingMaterializer(device));
   if (!mat_->ok()) {
     err_ = mat_->error();

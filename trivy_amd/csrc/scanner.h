@@ -361,7 +361,7 @@ class SecretScanner {
   // GPU allow-path prefilter (pathfilter.h): built when every path rule has usable literals
   std::unique_ptr<PathFilter> path_filter_;
   std::unique_ptr<FindingMaterializer> mat_;  // GPU findings of HBM-resident batches
-  std::atomic<int> gpu_findings_{2};
+  std::atomic<int> gpu_findings_{0};
 
  public:
   // 1 / 0 / 2: GPU / host / auto (GPU while host-bound) findings for HBM-resident

@@ -368,7 +368,7 @@ class Scanner:
 
     def set_gpu_findings(self, mode) -> int:
         """Findings of HBM-resident batches on the GPU (materialize.h; True / 1), on the host
-        (False / 0) or on the GPU while the exact pass is the bound (2, the default)
+        (False / 0, the default) or on the GPU while the exact pass is the bound (2)
         (tsg_debug_scanner_gpu_findings); returns the previous mode."""
         self._L.tsg_debug_scanner_gpu_findings.argtypes = [c.c_void_p, c.c_int]
         return self._L.tsg_debug_scanner_gpu_findings(self._h, int(mode))
