@@ -580,7 +580,9 @@ def main():
     ap.add_argument("--cpu-sample-mb", type=float, default=None, help="CPU-baseline sample (first files)")
     ap.add_argument("--parity-mb", type=float, default=None, help="oracle parity sample (first files)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=4, help="scans in flight (pipelined submission)")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="scans in flight (pipelined submission); default 4, c3f 6 (its exact host pass is the "
+                         "bound: 578 vs 536 GB/s at depth 6 vs 4, profiles/r06/c3f/y_r06p_*)")
     ap.add_argument("--crlf", type=float, default=0.05,
                     help="c2: share of CRLF files (SURVEY §8(d)); stripped while packing the HBM arena")
     ap.add_argument("--numa", choices=["gpu", "off"], default="gpu",
@@ -596,8 +598,9 @@ def main():
                          "--gb), inspected by --layer-parallel concurrent walks into the one engine "
                          "(AnalyzeLayers, image.go:202-235); 1 = one layer (AnalyzeLayer)")
     ap.add_argument("--layer-parallel", type=int, default=3, help="c4 with --layers > 1: concurrent layer walks")
-    ap.add_argument("--collectors", type=int, default=3,
-                    help="c4/c1fs: collectors filled in turn (collectors - 1 scans in flight during a walk)")
+    ap.add_argument("--collectors", type=int, default=None,
+                    help="c4/c1fs: collectors filled in turn (collectors - 1 scans in flight during a walk); "
+                         "default c4 6, c1fs 3")
     ap.add_argument("--transform", choices=["gpu", "host", "gather"], default="gpu",
                     help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
                          "the walk's host threads; gather: GPU pre-transform and no arena copy at all -- the GPU "
@@ -612,6 +615,10 @@ def main():
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 50 if args.workload == "c2" else 10
+    if args.depth is None:
+        args.depth = 6 if args.workload == "c3f" else 4
+    if args.collectors is None:  # c4: 6 (39.5-41.8 vs 37.6-38.1 GB/s with 3, profiles/r06/c4)
+        args.collectors = 6 if args.workload == "c4" else 3
     if args.warmup_s is None:  # only when the warm-up steps are not given explicitly
         args.warmup_s = 10.0 if args.workload == "c2" and args.warmup is None else 0.0
     if args.warmup is None:
