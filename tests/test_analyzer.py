@@ -316,6 +316,20 @@ def test_native_walk_gather_vs_oracle(host_analyzer, layer_30mb, arena_mb):
     assert (batches == 1) == (arena_mb == 64)
 
 
+def test_collector_needs_an_initialised_analyzer():
+    """A collector over an analyzer without a scanner is refused (it used to dereference NULL)."""
+    import ctypes
+    from trivy_amd.analyzer import SecretAnalyzer
+    from trivy_amd.analyzer.secret import Collector
+    a = SecretAnalyzer(lib=hostlib.lib(), host_only=True)
+    with pytest.raises(RuntimeError, match="Init first"):
+        Collector(a, 1 << 20)
+    L = hostlib.lib()
+    L.tsg_collector_new.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+    h = ctypes.c_void_p()
+    assert L.tsg_collector_new(None, 1 << 20, ctypes.byref(h)) < 0 and not h.value
+
+
 def test_collector_gather_mode_rules(host_analyzer):
     """Gather mode needs the GPU pre-transform, takes tar walks only, and holds one layer per batch:
     a walk of another buffer reports the batch full (1) without adding anything."""

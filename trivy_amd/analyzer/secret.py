@@ -169,6 +169,8 @@ class Collector:
         holds one layer's files (tsg_collector_set_gather)."""
         self._L = analyzer._L
         self._an = analyzer  # the C collector borrows the analyzer (and its walk state)
+        if not analyzer._h:
+            raise RuntimeError("Collector: the analyzer has no scanner (Init first)")
         h = c.c_void_p()
         if self._L.tsg_collector_new(analyzer._h, int(arena_bytes), c.byref(h)) != 0:
             raise RuntimeError("tsg_collector_new failed: %s" % _lib.last_error(self._L))

@@ -407,6 +407,10 @@ int tsg_analyzer_required(const tsg_analyzer* a, const char* path, uint64_t path
 }
 
 int tsg_collector_new(tsg_analyzer* a, uint64_t arena_bytes, tsg_collector** out) {
+  if (!a || !out) {
+    tsg::SetError("tsg_collector_new: null analyzer or out");
+    return -1;
+  }
   auto* c = new tsg_collector();
   c->a = a;
   c->device = a->s->s->device();

@@ -55,6 +55,7 @@ struct tsg_collector {
   std::vector<uint64_t> gsrc;
   mutable std::vector<uint8_t> scratch;  // tsg_collector_file's transformed copy (GPU mode)
   int threads = 16;    // ingest threads (TSG_HOST_THREADS)
+  std::vector<uint8_t> fs_scratch;  // FS walk: a window's small files, read whole by the first pass
   std::vector<uint64_t> offs{0};
   std::string path_pool;
   std::vector<uint64_t> path_off{0};

@@ -480,12 +480,17 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
   }
   const std::string base = w->root_is_file ? std::string() : w->root + "/";
   // per file of a window: Required, the 300-byte head (IsBinary), the arena
-  // size it needs; then accept in order, then read the accepted ones
+  // size it needs; then accept in order, then read the accepted ones.  A small
+  // required file is read whole by the first pass (into the window's scratch):
+  // one open / read / close instead of two, the second pass copies it
   struct Cand {
     int state;  // 0 not required, 1 binary skipped, 2 added, 3 vanished
     bool bin;
     uint64_t size, out_len, out_off;
+    uint64_t scr_off;  // small files: offset in the scratch (kNoScratch: read in the second pass)
+    int64_t scr_len;   // bytes read into the scratch
   };
+  constexpr uint64_t kSmall = 64 << 10, kNoScratch = ~uint64_t(0);
   for (;;) {
     if (w->next >= w->files.size()) return 0;
     const uint64_t room = c->limit > c->acct() ? c->limit - c->acct() : 0;
@@ -495,14 +500,39 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
     while (hi < w->files.size() && (hi == w->next || want < room + room / 2)) want += w->files[hi++].size;
     const size_t lo = w->next, n = hi - lo;
     std::vector<Cand> cd(n);
+    std::vector<uint8_t> req(n);
+    tsg::ParallelFor((n + 255) / 256, c->threads, [&](size_t b) {
+      for (size_t i = b * 256; i < std::min(n, b * 256 + 256); i++) {
+        const auto& f = w->files[lo + i];
+        req[i] = tsg::RequiredPath(c->a, f.rel.data(), f.rel.size(), int64_t(f.size)) ? 1 : 0;
+      }
+    }, true);
+    uint64_t scr_total = 0;
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t sz = w->files[lo + i].size;
+      cd[i] = Cand{0, false, sz, 0, 0, kNoScratch, 0};
+      if (req[i] && sz <= kSmall) {
+        cd[i].scr_off = scr_total;
+        scr_total += sz;
+      }
+    }
+    if (c->fs_scratch.size() < scr_total) c->fs_scratch.resize(scr_total + scr_total / 4);
+    uint8_t* scr = c->fs_scratch.data();
     tsg::ParallelFor((n + 31) / 32, c->threads, [&](size_t b) {
       for (size_t i = b * 32; i < std::min(n, b * 32 + 32); i++) {
         const auto& f = w->files[lo + i];
         Cand& x = cd[i];
-        x = Cand{0, false, f.size, 0, 0};
-        if (!tsg::RequiredPath(c->a, f.rel.data(), f.rel.size(), int64_t(f.size))) continue;
-        uint8_t head[300];
-        const int64_t h = ReadInto(w->root_is_file ? w->root : base + f.rel, head, std::min<uint64_t>(300, f.size));
+        if (!req[i]) continue;
+        uint8_t head_buf[300];
+        const uint8_t* head = head_buf;
+        int64_t h;
+        if (x.scr_off != kNoScratch) {  // small: the whole file now
+          x.scr_len = ReadInto(w->root_is_file ? w->root : base + f.rel, scr + x.scr_off, f.size);
+          h = x.scr_len < 0 ? -1 : std::min<int64_t>(300, x.scr_len);
+          head = scr + x.scr_off;
+        } else {
+          h = ReadInto(w->root_is_file ? w->root : base + f.rel, head_buf, std::min<uint64_t>(300, f.size));
+        }
         if (h < 0) {
           x.state = 3;
           continue;
@@ -560,7 +590,13 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
       const Cand& x = cd[added[j]];
       const auto& f = w->files[lo + added[j]];
       uint8_t* dst = c->arena + x.out_off;
-      const int64_t r = ReadInto(w->root_is_file ? w->root : base + f.rel, dst, x.size);
+      int64_t r;
+      if (x.scr_off != kNoScratch) {  // read whole by the first pass
+        r = x.scr_len;
+        std::memcpy(dst, scr + x.scr_off, size_t(r));
+      } else {
+        r = ReadInto(w->root_is_file ? w->root : base + f.rel, dst, x.size);
+      }
       if (r < 0) {
         read_err = errno ? errno : EIO;
         final_len[j] = 0;
