@@ -144,6 +144,12 @@ constexpr int kFNlTiles = 16;                       // tiles whose newline count
 #define TSG_K1_WGS 2
 #endif
 constexpr int kFWgPerCu = TSG_K1_WGS;  // 1: leaves ~80 KiB of LDS per CU to a concurrent scan's confirm kernel
+#ifndef TSG_K1_NONL
+#define TSG_K1_NONL 0
+#endif
+#ifndef TSG_K1_NOQUEUE
+#define TSG_K1_NOQUEUE 0
+#endif
 #ifndef TSG_K1_READAHEAD
 #define TSG_K1_READAHEAD 4
 #endif
@@ -339,6 +345,12 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
       for (int j = 0; j < kFBlocks; j++)
         nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
     }
+#if TSG_K1_NONL  // timing diagnostic only (wrong line numbers): no newline staging
+    if (nl == 0xFFFFFFFFu) P.counters[8] = nl;
+    (void)flush_nl;
+    if (false)
+#endif
+    {
     // newlines per 1-KiB chunk = per 16-lane DPP row: a row_shr 1/2/4/8 sum puts it in the row's last lane
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x111, 0xF, 0xF, true));
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x112, 0xF, 0xF, true));
@@ -347,6 +359,11 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     static_assert(kChunk / kFLane == 16, "one newline chunk per DPP row");
     if ((lane & 15) == 15) reinterpret_cast<uint16_t*>(NL + nl_slots)[lane >> 4] = uint16_t(nl);
     if (++nl_slots == kFNlTiles) flush_nl(tt);
+    }
+#if TSG_K1_NOQUEUE  // timing diagnostic only (no records: K2 sees nothing)
+    if (flagged == 0xFFFFFFFFu) P.counters[8] = flagged;
+    return;
+#endif
     // the flagged block columns, compacted (record = arena byte / 16)
     const uint32_t rec0 = uint32_t(tt * (kFTile / 16)) + lane * kFBlocks;
 #pragma unroll
