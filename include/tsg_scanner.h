@@ -127,7 +127,10 @@ typedef struct tsg_batch_ext {
    * gather_src[f] .. + (host_offsets[f + 1] - host_offsets[f]) in page-locked,
    * device-mapped host memory (tsg_host_register_mapped; a tar layer as the
    * analyzer's collectors hold it): the GPU gathers them itself, no host copy.
-   * host_offsets still lay out the batch (the files back to back). */
+   * host_offsets still lay out the batch (the files back to back).  The GPU
+   * reads aligned 16-B blocks: the 16 bytes before each file's data and the 32
+   * after its end must lie in the mapped region too (a tar's 512-B headers and
+   * padding provide them). */
   const uint8_t* gather_base;
   const uint64_t* gather_src;
 } tsg_batch_ext;
