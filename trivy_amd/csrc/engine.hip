@@ -150,6 +150,13 @@ constexpr int kFWgPerCu = TSG_K1_WGS;  // 1: leaves ~80 KiB of LDS per CU to a c
 #ifndef TSG_K1_NOQUEUE
 #define TSG_K1_NOQUEUE 0
 #endif
+#ifndef TSG_K1_QMODE  // timing diagnostic only: 1 the queue never flushes to global, 2 ballots only
+#define TSG_K1_QMODE 0
+#endif
+#ifndef TSG_K1_GROUPQ  // flagged blocks compacted once per kFGroup tiles (0: per tile and block column)
+#define TSG_K1_GROUPQ 1
+#endif
+constexpr uint32_t kFGroup = 8;  // tiles per compaction: 4 flag bits each, 32 per lane
 #ifndef TSG_K1_READAHEAD
 #define TSG_K1_READAHEAD 4
 #endif
@@ -221,7 +228,9 @@ __device__ __forceinline__ void load_reach_lds(uint8_t* s_reach, const uint32_t*
 // VGPRs and LDS go to a concurrent scan's confirm kernel)
 __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
+#if !TSG_K1_GROUPQ
   __shared__ uint32_t s_queue[kScanWaves * kFQueue];
+#endif
   __shared__ uint64_t s_nl[kScanWaves * kFNlTiles];  // per wave: the last tiles' 4 chunk counts
   const int tid = threadIdx.x;
   load_reach_lds(s_reach, P.reach, 16, tid, blockDim.x);
@@ -229,10 +238,14 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
   const uint32_t lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6);
   const uint32_t laneoff = (lane & 15) * 16;
+#if !TSG_K1_GROUPQ
   uint32_t* Q = s_queue + wave * kFQueue;
+#endif
   uint64_t* NL = s_nl + wave * kFNlTiles;
   uint32_t nl_slots = 0;  // wave-uniform: tiles staged in NL
+#if !TSG_K1_GROUPQ
   uint32_t qn = 0;  // wave-uniform
+#endif
   // Each wave streams one contiguous range of tiles, so lane 0's 8-byte
   // prefix is lane 63's last 8 bytes of the wave's previous tile (carried in
   // scalar registers) -- only the range's first tile loads it.
@@ -258,7 +271,53 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) dst[j] = load16(lp + 16 * j);
   };
+#if TSG_K1_GROUPQ
+  // Flagged blocks: each lane keeps 4 bits per tile for kFGroup consecutive
+  // tiles of its range, then one compaction writes the group's records to the
+  // global list -- a wave prefix sum of the lanes' counts, one atomic per group,
+  // each lane storing its own.  (Per tile and block column, a ballot + mbcnt +
+  // LDS queue with a branch each cost K1 ~0.5 ms, its flushes another ~0.5 ms
+  // on C2: TSG_K1_QMODE / TSG_K1_NOQUEUE A/Bs, profiles/r06/k1.)
+  uint32_t fl_acc = 0;  // per lane: bit 4 * (tile - grp_t0) + block column
+  uint32_t grp_n = 0;   // wave-uniform: tiles in the group so far
+  uint64_t grp_t0 = 0;  // wave-uniform: the group's first tile
+  auto compact = [&]() {  // wave-uniform; before the next tile's loads are issued (the atomic's wait)
+    const uint32_t cnt = __popc(fl_acc);
+    // inclusive wave prefix sum by DPP: row_shr 1/2/4/8 within the 16-lane rows,
+    // then row_bcast 15 / 31 carry the rows' totals (gfx9 DPP)
+    uint32_t incl = cnt;
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x111, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x112, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x114, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x118, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x142, 0xA, 0xF, false));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x143, 0xC, 0xF, false));
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    if (total) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&P.counters[7], total);
+      uint32_t at = __builtin_amdgcn_readfirstlane(base) + incl - cnt;
+      const uint32_t rec0 = __builtin_amdgcn_readfirstlane(uint32_t(grp_t0 * (kFTile / 16))) + lane * kFBlocks;
+      uint32_t m = fl_acc;
+      while (m) {
+        const uint32_t b = uint32_t(__builtin_ctz(m));
+        m &= m - 1;
+        const uint32_t rec = rec0 + ((b >> 2) << 8) + (b & 3u);  // tile grp_t0 + b / 4, column b % 4
+        if (at < P.rec_cap) P.recs[at] = rec;
+        else P.counters[8] = 1;
+        at++;
+      }
+    }
+    fl_acc = 0;
+    grp_n = 0;
+  };
+#else
   auto flush = [&]() {  // wave-uniform
+#if TSG_K1_QMODE
+    if (qn == 0xFFFFFFFFu) P.counters[8] = qn;
+    qn = 0;
+    return;
+#endif
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&P.counters[7], qn);
     base = __builtin_amdgcn_readfirstlane(base);
@@ -268,6 +327,7 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     }
     qn = 0;
   };
+#endif
   // Global stores are rare on purpose: on gfx9 a store counts in vmcnt like
   // the loads, so a store per tile would make the next tile's wait for its
   // prefetched data also wait for the store's completion.
@@ -357,6 +417,7 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x114, 0xF, 0xF, true));
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x118, 0xF, 0xF, true));
     static_assert(kChunk / kFLane == 16, "one newline chunk per DPP row");
+    static_assert(kFTile / 16 == 256, "a tile's records: 256 blocks");
     if ((lane & 15) == 15) reinterpret_cast<uint16_t*>(NL + nl_slots)[lane >> 4] = uint16_t(nl);
     if (++nl_slots == kFNlTiles) flush_nl(tt);
     }
@@ -364,6 +425,11 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     if (flagged == 0xFFFFFFFFu) P.counters[8] = flagged;
     return;
 #endif
+#if TSG_K1_GROUPQ
+    if (grp_n == 0) grp_t0 = tt;
+    fl_acc |= flagged << (4 * grp_n);
+    grp_n++;
+#else
     // the flagged block columns, compacted (record = arena byte / 16)
     const uint32_t rec0 = uint32_t(tt * (kFTile / 16)) + lane * kFBlocks;
 #pragma unroll
@@ -374,16 +440,25 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
         if (qn + 64 > kFQueue) flush();  // wave-uniform; rare (> 128 records since the last flush)
         const uint32_t below =
             __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+#if TSG_K1_QMODE != 2
         if (fj) Q[qn + below] = rec0 + uint32_t(j);
+#else
+        if (fj && below == 0xFFFFu) P.counters[8] = rec0;
+#endif
         qn += uint32_t(__popcll(m));
       }
     }
+#endif
   };
   // A flush's atomicAdd returns the records' base: waiting for it waits for every
   // older vector-memory op too, so it goes before the next tile's loads are issued
   // (then it only waits for the loads the coming tile needs at once anyway).
   auto flush_due = [&]() {
+#if TSG_K1_GROUPQ
+    if (grp_n == kFGroup) compact();
+#else
     if (qn >= kFFlushAt) flush();
+#endif
   };
   using Full = std::false_type;
   // whole tiles; the arena's partial last tile (if any) is the last of its wave's range
@@ -408,7 +483,11 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     tile(bufA, t, std::true_type());
     t++;
   }
+#if TSG_K1_GROUPQ
+  if (grp_n) compact();
+#else
   if (qn) flush();
+#endif
   if (nl_slots) flush_nl(t - 1);
 }
 
