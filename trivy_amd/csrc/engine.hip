@@ -228,9 +228,7 @@ __device__ __forceinline__ void load_reach_lds(uint8_t* s_reach, const uint32_t*
 // VGPRs and LDS go to a concurrent scan's confirm kernel)
 __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t s_reach[65536];
-#if !TSG_K1_GROUPQ
   __shared__ uint32_t s_queue[kScanWaves * kFQueue];
-#endif
   __shared__ uint64_t s_nl[kScanWaves * kFNlTiles];  // per wave: the last tiles' 4 chunk counts
   const int tid = threadIdx.x;
   load_reach_lds(s_reach, P.reach, 16, tid, blockDim.x);
@@ -238,14 +236,10 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
   const uint32_t lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6);
   const uint32_t laneoff = (lane & 15) * 16;
-#if !TSG_K1_GROUPQ
   uint32_t* Q = s_queue + wave * kFQueue;
-#endif
   uint64_t* NL = s_nl + wave * kFNlTiles;
   uint32_t nl_slots = 0;  // wave-uniform: tiles staged in NL
-#if !TSG_K1_GROUPQ
   uint32_t qn = 0;  // wave-uniform
-#endif
   // Each wave streams one contiguous range of tiles, so lane 0's 8-byte
   // prefix is lane 63's last 8 bytes of the wave's previous tile (carried in
   // scalar registers) -- only the range's first tile loads it.
@@ -271,47 +265,6 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
 #pragma unroll
     for (int j = 0; j < kFBlocks; j++) dst[j] = load16(lp + 16 * j);
   };
-#if TSG_K1_GROUPQ
-  // Flagged blocks: each lane keeps 4 bits per tile for kFGroup consecutive
-  // tiles of its range, then one compaction writes the group's records to the
-  // global list -- a wave prefix sum of the lanes' counts, one atomic per group,
-  // each lane storing its own.  (Per tile and block column, a ballot + mbcnt +
-  // LDS queue with a branch each cost K1 ~0.5 ms, its flushes another ~0.5 ms
-  // on C2: TSG_K1_QMODE / TSG_K1_NOQUEUE A/Bs, profiles/r06/k1.)
-  uint32_t fl_acc = 0;  // per lane: bit 4 * (tile - grp_t0) + block column
-  uint32_t grp_n = 0;   // wave-uniform: tiles in the group so far
-  uint64_t grp_t0 = 0;  // wave-uniform: the group's first tile
-  auto compact = [&]() {  // wave-uniform; before the next tile's loads are issued (the atomic's wait)
-    const uint32_t cnt = __popc(fl_acc);
-    // inclusive wave prefix sum by DPP: row_shr 1/2/4/8 within the 16-lane rows,
-    // then row_bcast 15 / 31 carry the rows' totals (gfx9 DPP)
-    uint32_t incl = cnt;
-    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x111, 0xF, 0xF, true));
-    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x112, 0xF, 0xF, true));
-    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x114, 0xF, 0xF, true));
-    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x118, 0xF, 0xF, true));
-    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x142, 0xA, 0xF, false));
-    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x143, 0xC, 0xF, false));
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    if (total) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&P.counters[7], total);
-      uint32_t at = __builtin_amdgcn_readfirstlane(base) + incl - cnt;
-      const uint32_t rec0 = __builtin_amdgcn_readfirstlane(uint32_t(grp_t0 * (kFTile / 16))) + lane * kFBlocks;
-      uint32_t m = fl_acc;
-      while (m) {
-        const uint32_t b = uint32_t(__builtin_ctz(m));
-        m &= m - 1;
-        const uint32_t rec = rec0 + ((b >> 2) << 8) + (b & 3u);  // tile grp_t0 + b / 4, column b % 4
-        if (at < P.rec_cap) P.recs[at] = rec;
-        else P.counters[8] = 1;
-        at++;
-      }
-    }
-    fl_acc = 0;
-    grp_n = 0;
-  };
-#else
   auto flush = [&]() {  // wave-uniform
 #if TSG_K1_QMODE
     if (qn == 0xFFFFFFFFu) P.counters[8] = qn;
@@ -326,6 +279,58 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
       else P.counters[8] = 1;
     }
     qn = 0;
+  };
+#if TSG_K1_GROUPQ
+  // Flagged blocks: each lane keeps 4 bits per tile for kFGroup consecutive
+  // tiles of its range; one compaction per group appends the group's records
+  // to the wave's LDS queue (a DPP wave prefix sum of the lanes' counts, each
+  // lane writing its own), and the queue goes to the global list in flushes of
+  // >= kFFlushAt records (one atomic each).  Per tile and block column, the
+  // ballot + mbcnt + branch appends cost K1 ~0.5 ms on C2; an atomic per group
+  // instead of the queue serialised on the one counter (+2 ms; TSG_K1_QMODE /
+  // TSG_K1_NOQUEUE A/Bs, profiles/r06/k1).
+  uint32_t fl_acc = 0;  // per lane: bit 4 * (tile - grp_t0) + block column
+  uint32_t grp_n = 0;   // wave-uniform: tiles in the group so far
+  uint64_t grp_t0 = 0;  // wave-uniform: the group's first tile
+  auto compact = [&]() {  // wave-uniform; before the next tile's loads are issued (a flush's wait)
+    const uint32_t cnt = __popc(fl_acc);
+    // inclusive wave prefix sum by DPP: row_shr 1/2/4/8 within the 16-lane rows,
+    // then row_bcast 15 / 31 carry the rows' totals (gfx9 DPP)
+    uint32_t incl = cnt;
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x111, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x112, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x114, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x118, 0xF, 0xF, true));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x142, 0xA, 0xF, false));
+    incl += uint32_t(__builtin_amdgcn_update_dpp(0, int(incl), 0x143, 0xC, 0xF, false));
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    if (total) {
+      if (qn + total > kFQueue) flush();
+      const uint32_t rec0 = __builtin_amdgcn_readfirstlane(uint32_t(grp_t0 * (kFTile / 16))) + lane * kFBlocks;
+      uint32_t m = fl_acc;
+      if (total <= kFQueue) {  // into the queue
+        uint32_t at = qn + incl - cnt;
+        while (m) {
+          const uint32_t b = uint32_t(__builtin_ctz(m));
+          m &= m - 1;
+          Q[at++] = rec0 + ((b >> 2) << 8) + (b & 3u);  // tile grp_t0 + b / 4, column b % 4
+        }
+        qn += total;
+      } else {  // a group denser than the queue: straight to the global list
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&P.counters[7], total);
+        uint32_t at = __builtin_amdgcn_readfirstlane(base) + incl - cnt;
+        while (m) {
+          const uint32_t b = uint32_t(__builtin_ctz(m));
+          m &= m - 1;
+          if (at < P.rec_cap) P.recs[at] = rec0 + ((b >> 2) << 8) + (b & 3u);
+          else P.counters[8] = 1;
+          at++;
+        }
+      }
+    }
+    fl_acc = 0;
+    grp_n = 0;
   };
 #endif
   // Global stores are rare on purpose: on gfx9 a store counts in vmcnt like
@@ -456,9 +461,8 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
   auto flush_due = [&]() {
 #if TSG_K1_GROUPQ
     if (grp_n == kFGroup) compact();
-#else
-    if (qn >= kFFlushAt) flush();
 #endif
+    if (qn >= kFFlushAt) flush();
   };
   using Full = std::false_type;
   // whole tiles; the arena's partial last tile (if any) is the last of its wave's range
@@ -485,9 +489,8 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
   }
 #if TSG_K1_GROUPQ
   if (grp_n) compact();
-#else
-  if (qn) flush();
 #endif
+  if (qn) flush();
   if (nl_slots) flush_nl(t - 1);
 }
 
