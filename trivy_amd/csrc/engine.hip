@@ -144,15 +144,6 @@ constexpr int kFNlTiles = 16;                       // tiles whose newline count
 #define TSG_K1_WGS 2
 #endif
 constexpr int kFWgPerCu = TSG_K1_WGS;  // 1: leaves ~80 KiB of LDS per CU to a concurrent scan's confirm kernel
-#ifndef TSG_K1_NONL
-#define TSG_K1_NONL 0
-#endif
-#ifndef TSG_K1_NOQUEUE
-#define TSG_K1_NOQUEUE 0
-#endif
-#ifndef TSG_K1_QMODE  // timing diagnostic only: 1 the queue never flushes to global, 2 ballots only
-#define TSG_K1_QMODE 0
-#endif
 #ifndef TSG_K1_GROUPQ  // flagged blocks compacted once per kFGroup tiles (0: per tile and block column)
 #define TSG_K1_GROUPQ 1
 #endif
@@ -266,11 +257,6 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     for (int j = 0; j < kFBlocks; j++) dst[j] = load16(lp + 16 * j);
   };
   auto flush = [&]() {  // wave-uniform
-#if TSG_K1_QMODE
-    if (qn == 0xFFFFFFFFu) P.counters[8] = qn;
-    qn = 0;
-    return;
-#endif
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&P.counters[7], qn);
     base = __builtin_amdgcn_readfirstlane(base);
@@ -285,10 +271,12 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
   // tiles of its range; one compaction per group appends the group's records
   // to the wave's LDS queue (a DPP wave prefix sum of the lanes' counts, each
   // lane writing its own), and the queue goes to the global list in flushes of
-  // >= kFFlushAt records (one atomic each).  Per tile and block column, the
-  // ballot + mbcnt + branch appends cost K1 ~0.5 ms on C2; an atomic per group
-  // instead of the queue serialised on the one counter (+2 ms; TSG_K1_QMODE /
-  // TSG_K1_NOQUEUE A/Bs, profiles/r06/k1).
+  // >= kFFlushAt records (one atomic each).  Against the per-tile, per-column
+  // ballot appends (TSG_K1_GROUPQ=0) it measured equal to 0.2 ms faster on C2;
+  // an atomic per group straight to the global list instead of the queue
+  // serialised on the one counter (K1 5.5 -> 7.5 ms).  (Diagnostic builds that
+  // dropped the queue let the compiler delete the filter itself -- only the
+  // newline bucket's word stayed live -- so they measured nothing: DESIGN §4.1.)
   uint32_t fl_acc = 0;  // per lane: bit 4 * (tile - grp_t0) + block column
   uint32_t grp_n = 0;   // wave-uniform: tiles in the group so far
   uint64_t grp_t0 = 0;  // wave-uniform: the group's first tile
@@ -410,11 +398,6 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
       for (int j = 0; j < kFBlocks; j++)
         nl += nl_count4(cur[j].x) + nl_count4(cur[j].y) + nl_count4(cur[j].z) + nl_count4(cur[j].w);
     }
-#if TSG_K1_NONL  // timing diagnostic only (wrong line numbers): no newline staging
-    if (nl == 0xFFFFFFFFu) P.counters[8] = nl;
-    (void)flush_nl;
-    if (false)
-#endif
     {
     // newlines per 1-KiB chunk = per 16-lane DPP row: a row_shr 1/2/4/8 sum puts it in the row's last lane
     nl += uint32_t(__builtin_amdgcn_update_dpp(0, int(nl), 0x111, 0xF, 0xF, true));
@@ -426,10 +409,6 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
     if ((lane & 15) == 15) reinterpret_cast<uint16_t*>(NL + nl_slots)[lane >> 4] = uint16_t(nl);
     if (++nl_slots == kFNlTiles) flush_nl(tt);
     }
-#if TSG_K1_NOQUEUE  // timing diagnostic only (no records: K2 sees nothing)
-    if (flagged == 0xFFFFFFFFu) P.counters[8] = flagged;
-    return;
-#endif
 #if TSG_K1_GROUPQ
     if (grp_n == 0) grp_t0 = tt;
     fl_acc |= flagged << (4 * grp_n);
@@ -445,11 +424,7 @@ __global__ __launch_bounds__(kScanThreads, 8) void filter_kernel(FilterParams P)
         if (qn + 64 > kFQueue) flush();  // wave-uniform; rare (> 128 records since the last flush)
         const uint32_t below =
             __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-#if TSG_K1_QMODE != 2
         if (fj) Q[qn + below] = rec0 + uint32_t(j);
-#else
-        if (fj && below == 0xFFFFu) P.counters[8] = rec0;
-#endif
         qn += uint32_t(__popcll(m));
       }
     }
