@@ -139,7 +139,10 @@ constexpr int kFTile = 64 * kFLane;  // 4 KiB per wave tile
 constexpr int kFFlushAt = 128;                      // flush the flagged-block queue at >= this many
 constexpr int kFQueue = kFFlushAt + 64;             // per-wave queue entries (a block column appends <= 64)
 constexpr int kFChunks = kFTile / 1024;             // newline chunks per tile (kChunk = 1 KiB)
-constexpr int kFNlTiles = 16;                       // tiles whose newline counts a wave stages in LDS
+#ifndef TSG_K1_NLTILES
+#define TSG_K1_NLTILES 16
+#endif
+constexpr int kFNlTiles = TSG_K1_NLTILES;           // tiles whose newline counts a wave stages in LDS
 #ifndef TSG_K1_WGS
 #define TSG_K1_WGS 2
 #endif
