@@ -1155,6 +1155,10 @@ int tsg_collector_set_gpu_transform(tsg_collector* c, int on) {
     tsg::SetError("tsg_collector_set_gpu_transform: the batch is not empty");
     return -1;
   }
+  if (!on && c->gather) {
+    tsg::SetError("tsg_collector_set_gpu_transform: gather mode needs the GPU pre-transform (tsg_collector_set_gather 0 first)");
+    return -1;
+  }
   c->gpu_xform = on != 0;
   return 0;
 }
