@@ -764,6 +764,16 @@ struct ScanScratch {
   std::vector<const Candidate*> hints, fhints;
   std::vector<Window> wins;
   std::vector<int64_t> m, span_nl, vnl;
+  // line texts already in the file's FileFindings::text, by line number (a
+  // direct-mapped cache; `gen` tags the file it belongs to)
+  struct LineText {
+    uint64_t gen;
+    int64_t line;
+    uint32_t off, len;
+  };
+  static constexpr size_t kLineCache = 256;
+  LineText line_cache[kLineCache] = {};
+  uint64_t gen = 0;
 };
 thread_local ScanScratch t_scan;
 }  // namespace
@@ -1240,6 +1250,17 @@ void SecretScanner::FindingsHost(const uint8_t* content, int64_t len, std::strin
     g_prof[13] += int64_t(spans.size());
   }
   PhaseTimer pt3(3);
+  // a line's censored text (its first 100 B, or all of it when shorter) is the
+  // same for every finding whose code window holds it: stored once per file, its
+  // range shared (finding-dense files repeat their neighbouring lines ~5x)
+  const uint64_t gen = ++S.gen;
+  auto line_text = [&](int64_t k, size_t kspan, int64_t a, int64_t b) -> uint32_t {  // line k = content [a, b)
+    ScanScratch::LineText& e = S.line_cache[size_t(k) & (ScanScratch::kLineCache - 1)];
+    if (e.gen == gen && e.line == k) return e.off;
+    const uint32_t off = put_censored_from(kspan, a, b);
+    e = ScanScratch::LineText{gen, k, off, uint32_t(b - a)};
+    return off;
+  };
   ff.f.reserve(matched.size());
   ff.lines.reserve(matched.size() * 5);
   ff.text.reserve(matched.size() * 320);  // match line + 4 lines of <= 100 B, typically
@@ -1277,7 +1298,10 @@ void SecretScanner::FindingsHost(const uint8_t* content, int64_t len, std::strin
     else
       for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
     size_t kspan = first_span_after(p);  // every text below starts at or after p
-    const uint32_t ml_off = put_censored_from(kspan, mls, mle), ml_len = uint32_t(mle - mls);
+    // the match line: the whole line when it is <= 100 B (then the cause line's text too)
+    const uint32_t ml_off = le - ls > 100 ? put_censored_from(kspan, mls, mle)
+                                          : line_text(start_line_num, first_span_after(ls), ls, le);
+    const uint32_t ml_len = uint32_t(mle - mls);
     bool found_first = false;
     f.line_lo = uint32_t(ff.lines.size());
     if (!binary) {
@@ -1292,7 +1316,7 @@ void SecretScanner::FindingsHost(const uint8_t* content, int64_t len, std::strin
           const int64_t q = e - p > 100 ? p + 100 : e;
           n = uint32_t(q - p);
           while (kspan < spans.size() && spans[kspan].e <= p) kspan++;
-          off = put_censored_from(kspan, p, q);
+          off = line_text(k, kspan, p, q);
         }
         ff.lines.push_back({k + 1, off, n, in_cause, !found_first && in_cause, false});
         found_first = found_first || in_cause;
