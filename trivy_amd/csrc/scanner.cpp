@@ -85,6 +85,7 @@ struct SortData {
     const FindingOut& a = v->f[size_t(i)];
     const FindingOut& b = v->f[size_t(j)];
     if (rank[a.rule] != rank[b.rule]) return rank[a.rule] < rank[b.rule];  // RuleID < RuleID
+    if (a.match_off == b.match_off && a.match_len == b.match_len) return false;  // one shared text: equal
     return v->Match(a) < v->Match(b);
   }
   void Swap(int i, int j) { std::swap(v->f[size_t(i)], v->f[size_t(j)]); }
