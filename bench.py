@@ -666,6 +666,7 @@ def main():
     cfg_path = None
     t_gen = time.time()
     C = layer = R = None
+    r_crlf = r_bytes = 0  # c2: the files as read (CRLF files, bytes)
     layer_list = None  # c4 --layers > 1
     if args.workload in ("c3", "c3u", "c3f"):
         y, samples = corpus.c3_rules(unanchored_share=0.1 if args.workload == "c3u" else 0.0,
@@ -697,11 +698,14 @@ def main():
     else:
         # C2: 5 % of the files CRLF.  The files as read (R) are CR-stripped while
         # packed into the arena (secret.go:121; the analyzer's packing step, before timing) and the
-        # HBM-resident steps scan the stripped arena C; the value's numerator is R's bytes (pre-strip,
-        # §8(d)).  The ingest leg streams R itself and strips it on the GPU inside its timed region.
+        # HBM-resident steps scan the stripped arena C; the value counts C's bytes.  The ingest leg
+        # streams R itself and strips it on the GPU inside its timed region.
         R = corpus.generate(int(args.gb * 1e9), seed=corpus.SEED + rank, crlf_share=args.crlf)
         C = R.stripped() if args.crlf > 0 else R
-        if args.crlf <= 0:
+        r_crlf, r_bytes = int(R.crlf.sum()), int(R.n_bytes)
+        # R feeds only the ingest leg (single-process C2 runs): otherwise free it -- under torchrun
+        # each rank would hold its corpus twice (2 x 20 GB of host memory per GPU)
+        if args.crlf <= 0 or world > 1 or args.ingest or args.ingest_steps <= 0:
             R = None
     t_gen = time.time() - t_gen
     kinds_raw = np.ones(R.n_files, dtype=np.uint8) if R is not None else None  # every text file: CR strip
@@ -919,9 +923,9 @@ def main():
         breakdown["ms_timed_minus_gpu"] = round(dt * 1e3 - args.steps * emissions * gpu_ms, 3)
         config_extra = {"bytes_per_gpu": n_bytes, "files_per_gpu": n_files, "pipeline_depth": args.depth,
                         "calibration_sample_bytes": int(calib.size) if calib is not None else 0,
-                        "crlf_files": int(R.crlf.sum()) if R is not None else 0,
+                        "crlf_files": r_crlf,
                         "arena_bytes_after_cr_strip": C.n_bytes,
-                        "input_bytes_as_read": R.n_bytes if R is not None else C.n_bytes,
+                        "input_bytes_as_read": r_bytes or C.n_bytes,
                         "value_numerator": "arena bytes (after the CR strip done while packing, before timing)",
                         "emissions_per_step": emissions, "pool_bytes": C.n_bytes,
                         "resident": "host (page-locked), H2D in the timed region" if args.ingest
