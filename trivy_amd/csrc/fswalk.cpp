@@ -490,6 +490,7 @@ int tsg_collector_add_fs(tsg_collector* c, tsg_fs_walk* w, tsg_fs_add_stats* st)
     uint64_t scr_off;  // small files: offset in the scratch (kNoScratch: read in the second pass)
     int64_t scr_len;   // bytes read into the scratch
   };
+  // (the scratch holds at most a window's small files: <= 1.5x the batch size)
   constexpr uint64_t kSmall = 64 << 10, kNoScratch = ~uint64_t(0);
   for (;;) {
     if (w->next >= w->files.size()) return 0;
