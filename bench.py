@@ -768,7 +768,7 @@ def main():
         an.Init(AnalyzerOptions())
         t_compile = time.time() - t_c
         gx = args.transform in ("gpu", "gather")
-        gth = args.transform == "gather"
+        gth = args.transform == "gather" and args.workload == "c4"  # (tar layers only)
         colls = [Collector(an, args.arena_mb << 20, gx, gather=gth) for _ in range(args.collectors)]
         lworkers = an.LayerWorkers(args.layer_parallel, args.arena_mb << 20, args.collectors, gx, gth) \
             if layer_list is not None else None
@@ -1018,7 +1018,9 @@ def main():
                 parity = cpu.pop("parity", None)
             else:
                 sample = corpus.generate_layer(int(args.cpu_sample_mb * 1e6), seed=corpus.SEED + rank)
-                res_l = an.AnalyzeLayer(sample, colls=[Collector(an, args.arena_mb << 20, gx)
+                # (the same ingest mode as the timed steps: with --transform gather the sample's
+                # batches are gathered from it, AnalyzeLayer page-locks and maps it for the call)
+                res_l = an.AnalyzeLayer(sample, colls=[Collector(an, args.arena_mb << 20, gx, gather=gth)
                                                        for _ in range(args.collectors)])
                 cpu = cpu_baseline_layer_cpp(sample, cores, gpu_result=res_l, parity_bytes=int(args.parity_mb * 1e6))
                 parity = cpu.pop("parity", None)
