@@ -1139,7 +1139,11 @@ hipError_t GatherHostFiles(const uint8_t* src_dev, const uint64_t* src_off, cons
   if (!n_items) return hipSuccess;
   // 128 workgroups (512 waves, two wave slots per CU): enough loads in flight
   // for the link (gather_host_kernel), few slots taken from the scan kernels
-  const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n_items) + 3) / 4, 128));
+  static const uint64_t max_grid = [] {  // TSG_GATHER_GRID: tuning knob
+    const char* e = std::getenv("TSG_GATHER_GRID");
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : uint64_t(128);
+  }();
+  const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n_items) + 3) / 4, max_grid));
   gather_host_kernel<<<grid, 256, 0, s>>>(src_dev, src_off, dst_off, items, n_items, dst);
   return hipGetLastError();
 }
