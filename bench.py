@@ -601,11 +601,12 @@ def main():
     ap.add_argument("--collectors", type=int, default=None,
                     help="c4/c1fs: collectors filled in turn (collectors - 1 scans in flight during a walk); "
                          "default c4 6, c1fs 3")
-    ap.add_argument("--transform", choices=["gpu", "host", "gather"], default="gpu",
-                    help="c4: CR strip / printable extraction on the GPU (bytes as read in the arena) or on "
-                         "the walk's host threads; gather: GPU pre-transform and no arena copy at all -- the GPU "
-                         "gathers each batch's files from the layer (page-locked and device-mapped once before "
-                         "timing, as a pinned layer-buffer pool would hold it)")
+    ap.add_argument("--transform", choices=["gpu", "host", "gather"], default="gather",
+                    help="c4: gather (default): GPU pre-transform and no arena copy at all -- the GPU gathers each "
+                         "batch's files from the layer (page-locked and device-mapped once before timing, as a "
+                         "pinned layer-buffer pool would hold it); gpu: the walk copies the bytes as read into the "
+                         "pinned arena and the GPU transforms them; host: the walk's threads transform while "
+                         "copying")
     ap.add_argument("--pool-gb", type=float, default=64.0, help="c5: page-locked host pool size")
     ap.add_argument("--calib-mb", type=float, default=16.0,
                     help="rule compiler calibration sample: the first MB of the corpus (as a scan job would hand "

@@ -1137,11 +1137,13 @@ __global__ __launch_bounds__(256) void gather_host_kernel(const uint8_t* __restr
 hipError_t GatherHostFiles(const uint8_t* src_dev, const uint64_t* src_off, const uint64_t* dst_off,
                            const GatherItem* items, uint32_t n_items, uint8_t* dst, hipStream_t s) {
   if (!n_items) return hipSuccess;
-  // 128 workgroups (512 waves, two wave slots per CU): enough loads in flight
-  // for the link (gather_host_kernel), few slots taken from the scan kernels
+  // 32 workgroups (128 waves, ~640 KiB of loads in flight): enough for the link
+  // (gather_host_kernel), few wave slots taken from the scan kernels of the
+  // batches in flight.  C4 by grid: 16 -> 33, 24-48 -> 42-43, 64 -> 40, 128 ->
+  // 37-38, 512 -> 35 GB/s (profiles/r06/c4/c4ab_r06gg*)
   static const uint64_t max_grid = [] {  // TSG_GATHER_GRID: tuning knob
     const char* e = std::getenv("TSG_GATHER_GRID");
-    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : uint64_t(128);
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : uint64_t(32);
   }();
   const uint32_t grid = uint32_t(std::min<uint64_t>((uint64_t(n_items) + 3) / 4, max_grid));
   gather_host_kernel<<<grid, 256, 0, s>>>(src_dev, src_off, dst_off, items, n_items, dst);
