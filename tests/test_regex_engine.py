@@ -51,7 +51,10 @@ PATTERNS = ([r["regex"] for r in BUILTIN["rules"]]
                r"[^\x00-\x7f]+", r"\x{FFFD}", r"(?U)a+b", r"(?i)k+s", r"^", r"$", r"(?i)[^k]",
                # one greedy class repeat (FindAll's class-run path, goregex.cpp FindAllRun)
                r"(?i)[a-z0-9/+]{32,48}", r"[0-9]{3}", r"(?P<secret>[a-f0-9]{8,})", r"(?i)[ks]{2,4}",
-               r"[^\s]{3,5}", r"((?:[a-c]){2,3})", r"(?i)(?P<x>[k-s]+)", r"\S{4}", r"[^a]{1,2}", r"[\x{FFFD}a]{2}"])
+               r"[^\s]{3,5}", r"((?:[a-c]){2,3})", r"(?i)(?P<x>[k-s]+)", r"\S{4}", r"[^a]{1,2}", r"[\x{FFFD}a]{2}",
+               # literals (Regex::Match's byte search, goregex.cpp MatchLiteral) and near-literals that are not
+               r"(?i)example", r"abc", r"(?i)(ex)(?:am)ple", r"a\.b", r"(?i)akia", r"[xX]y", r"(?i)ke", r"(?i)s",
+               r"(?i)ſ", r"é", r"(?i)^ex"])
 
 NOISE = ["the quick brown fox ", "key=", "secret: ", "\n", "  ", "'", '"', "AKIA", "ghp_",
          "sk_live_", "K", "ſ", "İ", "é", "日本", "\udcff", "-----BEGIN ", "=>",
@@ -144,5 +147,35 @@ def test_backtracker_equals_pike_vm(idx):
                 L.tsg_debug_regex_engine(mode)
                 res.append(_lib.regex_find_all(pat, text, submatch=True, windows=wins))
             assert res[0] == res[1] == res[2], (pat, text, wins)
+    finally:
+        L.tsg_debug_regex_engine(0)
+
+
+LITERALS = [r"(?i)example", r"abc", r"(?i)(ex)(?:am)ple", r"a\.b", r"(?i)akia", r"[xX]y", r"x", r"(?i)ghp_",
+            # not literals (fold orbits past ASCII, non-ASCII runes, anchors): the engines decide
+            r"(?i)ke", r"(?i)s", r"(?i)ſ", r"é", r"(?i)^ex", r"ex$", r"\bex"]
+
+
+def test_literal_match_equals_engine():
+    """Regex::Match's byte search for literal regexes (goregex.cpp MatchLiteral, auto
+    mode only) against the Pike VM (mode 1) and the oracle, on texts with mixed case,
+    the fold-special runes K (U+212A) / ſ (U+017F) / İ (U+0130) and invalid UTF-8."""
+    rng = random.Random(4242)
+    L = _lib.lib()
+    alphabet = ["e", "E", "x", "X", "a", "A", "m", "p", "l", "L", "k", "K", "s", "ſ", "K", "İ", "é", "\udcff",
+                "b", "c", ".", "y", "Y", "i", "g", "h", "_", "\n"]
+    try:
+        for pat in LITERALS:
+            ref = GoRegexp(pat)
+            for _ in range(150):
+                parts = [rng.choice(alphabet) for _ in range(rng.randint(0, 14))]
+                if rng.random() < 0.3:
+                    parts.insert(rng.randint(0, len(parts)), sample_regex(pat, rng).decode("utf-8", "surrogateescape"))
+                text = "".join(parts).encode("utf-8", "surrogateescape")
+                L.tsg_debug_regex_engine(0)
+                auto = _lib.regex_match(pat, text)
+                L.tsg_debug_regex_engine(1)
+                vm = _lib.regex_match(pat, text)
+                assert auto == vm == ref.match_string(text), (pat, text)
     finally:
         L.tsg_debug_regex_engine(0)

@@ -916,6 +916,7 @@ std::unique_ptr<Regex> Regex::Compile(const std::string& pattern, std::string* e
   }
   re->ComputeFirstBytes();
   re->DetectRun();
+  re->DetectLiteral();
   {  // instructions whose only predecessor is one rune instruction (Backtracker chain skip)
     std::vector<uint32_t> preds(re->prog_.size(), 0);
     std::vector<uint8_t> from_rune(re->prog_.size(), 0);
@@ -1402,8 +1403,9 @@ thread_local Backtracker t_bt;  // per host thread: its visited rows and job sta
 // allocating (a Pike VM per call cost 15% of the host tail, mostly in the
 // allow-path regexes); the Pike VM only past its row budget.
 bool Regex::Match(const uint8_t* s, int64_t n) const {
-  Backtracker& bt = t_bt;
   const int mode = g_regex_engine.load(std::memory_order_relaxed);
+  if (lit_ok_ && mode == 0) return MatchLiteral(s, n);
+  Backtracker& bt = t_bt;
   if (mode != 1) {
     bt.max_rows_ = mode == 2 ? 8 : Backtracker::kMaxRows;
     bool overflow = false;
@@ -1412,6 +1414,54 @@ bool Regex::Match(const uint8_t* s, int64_t n) const {
   }
   Machine m(this, 0);
   return m.Search(s, n, 0, nullptr);
+}
+
+void Regex::DetectLiteral() {
+  if (anchored_begin_) return;
+  int x = root_;
+  while (nodes_[size_t(x)].op == NodeOp::Capture) x = nodes_[size_t(x)].subs[0];
+  std::vector<int> parts;
+  const Node& top = nodes_[size_t(x)];
+  if (top.op == NodeOp::Cat) {
+    for (int sub : top.subs) {
+      int y = sub;
+      while (nodes_[size_t(y)].op == NodeOp::Capture) y = nodes_[size_t(y)].subs[0];
+      if (nodes_[size_t(y)].op == NodeOp::Empty) continue;
+      parts.push_back(y);
+    }
+  } else {
+    parts.push_back(x);
+  }
+  if (parts.empty() || parts.size() > 64) return;
+  std::vector<uint8_t> a, b;
+  for (int y : parts) {
+    const Node& nd = nodes_[size_t(y)];
+    if (nd.op != NodeOp::Class) return;
+    uint32_t runes[2], k = 0;
+    for (const auto& rg : nd.ranges)
+      for (uint32_t r = rg.first; r <= rg.second; r++) {
+        if (r >= 0x80 || k == 2) return;
+        runes[k++] = r;
+      }
+    if (k == 0) return;
+    a.push_back(uint8_t(runes[0]));
+    b.push_back(uint8_t(runes[k - 1]));
+  }
+  lit_a_ = std::move(a);
+  lit_b_ = std::move(b);
+  lit_ok_ = true;
+}
+
+bool Regex::MatchLiteral(const uint8_t* s, int64_t n) const {
+  const int64_t L = int64_t(lit_a_.size());
+  const uint8_t a0 = lit_a_[0], b0 = lit_b_[0];
+  for (int64_t p = 0; p + L <= n; p++) {
+    if (s[p] != a0 && s[p] != b0) continue;
+    int64_t j = 1;
+    while (j < L && (s[p + j] == lit_a_[size_t(j)] || s[p + j] == lit_b_[size_t(j)])) j++;
+    if (j == L) return true;
+  }
+  return false;
 }
 
 void Regex::DetectRun() {

@@ -114,6 +114,16 @@ class Regex {
   RuneRanges run_cls_;
   uint64_t run_ascii_[2] = {};
   void DetectRun();
+  // A regex that is a concatenation of classes of one or two ASCII runes each
+  // (a literal, (?i) letters folding only to their other case -- not k / s, whose
+  // orbits hold U+212A / U+017F), possibly inside capture groups: Match is a
+  // byte search (an ASCII class matches only the one-byte rune, never a byte
+  // inside a multi-byte one).  The builtin allow rule `examples` ((?i)example)
+  // runs on every match of the exact pass.
+  bool lit_ok_ = false;
+  std::vector<uint8_t> lit_a_, lit_b_;  // position k: byte lit_a_[k] or lit_b_[k]
+  void DetectLiteral();
+  bool MatchLiteral(const uint8_t* s, int64_t n) const;
   void FindAllRun(const uint8_t* s, int64_t n, bool submatch, const std::vector<Window>* wins,
                   std::vector<int64_t>* out) const;
   void ComputeFirstBytes();
