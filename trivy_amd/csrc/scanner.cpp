@@ -1271,13 +1271,52 @@ void SecretScanner::FindingsHost(const uint8_t* content, int64_t len, std::strin
   const int64_t n_vnl = int64_t(vnl.size());
   auto line_lo = [&](int64_t L) { return L > 0 ? vnl[size_t(L - 1)] + 1 : int64_t(0); };
   auto line_hi = [&](int64_t L) { return L < n_vnl ? vnl[size_t(L)] : len; };
+  // A rule's matches ascend: the searches for a finding's start line and first
+  // span gallop from the previous finding's answers while positions ascend.
+  int64_t fg_pos = -1, fg_line = 0, fg_p = -1;
+  size_t fg_span = 0;
+  auto vnl_below_f = [&](int64_t pos) {  // vnl_below(pos)
+    int64_t h = 0;
+    if (pos >= fg_pos && fg_pos >= 0) {
+      h = fg_line;  // vnl[0 .. h) < fg_pos <= pos
+      int64_t step = 1;
+      while (h + step <= n_vnl && vnl[size_t(h + step - 1)] < pos) {
+        h += step;
+        step <<= 1;
+      }
+      h = int64_t(std::lower_bound(vnl.begin() + h, vnl.begin() + std::min(h + step, n_vnl), pos) - vnl.begin());
+    } else {
+      h = vnl_below(pos);
+    }
+    fg_pos = pos;
+    fg_line = h;
+    return h;
+  };
+  auto first_span_after_f = [&](int64_t a) {  // first_span_after(a)
+    size_t k;
+    if (a >= fg_p && fg_p >= 0) {
+      k = fg_span;  // spans [0, k) end at or before fg_p <= a
+      size_t step = 1;
+      while (k + step <= spans.size() && spans[k + step - 1].e <= a) {
+        k += step;
+        step <<= 1;
+      }
+      k = size_t(std::upper_bound(spans.begin() + k, spans.begin() + std::min(k + step, spans.size()), a,
+                                  [](int64_t v, const Loc& z) { return v < z.e; }) - spans.begin());
+    } else {
+      k = first_span_after(a);
+    }
+    fg_p = a;
+    fg_span = k;
+    return k;
+  };
   for (auto& mt : matched) {  // toFinding / findLocation :475-558
     int64_t start = mt.second.s, end = mt.second.e;
     FindingOut f;
     f.rule = mt.first;
     int64_t start_line_num, ls, le, end_line_num;
     if (use_index) {
-      start_line_num = vnl_below(start);
+      start_line_num = vnl_below_f(start);
       ls = line_lo(start_line_num);
       le = line_hi(start_line_num);
       end_line_num = start_line_num;  // vnl_below(end): a match spans few lines
@@ -1298,10 +1337,11 @@ void SecretScanner::FindingsHost(const uint8_t* content, int64_t len, std::strin
     if (use_index) p = line_lo(code_start);
     else
       for (int64_t k = start_line_num; k > code_start; k--) p = line_start_of(p - 1);
-    size_t kspan = first_span_after(p);  // every text below starts at or after p
-    // the match line: the whole line when it is <= 100 B (then the cause line's text too)
+    size_t kspan = first_span_after_f(p);  // every text below starts at or after p
+    // the match line: the whole line when it is <= 100 B (then the cause line's text too);
+    // kspan is at or below the first span ending after ls (p <= ls)
     const uint32_t ml_off = le - ls > 100 ? put_censored_from(kspan, mls, mle)
-                                          : line_text(start_line_num, first_span_after(ls), ls, le);
+                                          : line_text(start_line_num, kspan, ls, le);
     const uint32_t ml_len = uint32_t(mle - mls);
     bool found_first = false;
     f.line_lo = uint32_t(ff.lines.size());
