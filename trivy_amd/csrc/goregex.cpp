@@ -1494,6 +1494,7 @@ void Regex::DetectRun() {
   run_ascii_[0] = run_ascii_[1] = 0;
   for (uint32_t b = 0; b < 128; b++)
     if (InRanges(run_cls_, b)) run_ascii_[b >> 6] |= uint64_t(1) << (b & 63);
+  for (uint32_t b = 0; b < 256; b++) run_tbl_[b] = b >= 0x80 ? 2 : uint8_t((run_ascii_[b >> 6] >> (b & 63)) & 1);
   run_min_ = r.min;
   run_max_ = r.max;
   run_ok_ = true;
@@ -1527,11 +1528,16 @@ void Regex::FindAllRun(const uint8_t* s, int64_t n, bool submatch, const std::ve
     int64_t q = pos, k = 0;
     int w = 1;
     while (q < n && k < lim) {
-      const uint8_t b = s[q];
+      const uint8_t t = run_tbl_[s[q]];
+      if (t == 1) {  // an ASCII member: the common case
+        q++;
+        k++;
+        continue;
+      }
       bool in;
-      if (b < 0x80) {
+      if (t == 0) {
         w = 1;
-        in = (run_ascii_[b >> 6] >> (b & 63)) & 1;
+        in = false;
       } else {
         const Rune r = DecodeRune(s, n, q);
         w = r.width;

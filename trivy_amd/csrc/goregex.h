@@ -113,6 +113,7 @@ class Regex {
   int run_min_ = 0, run_max_ = 0;  // run_max_ < 0: unbounded
   RuneRanges run_cls_;
   uint64_t run_ascii_[2] = {};
+  uint8_t run_tbl_[256] = {};  // per byte: 1 an ASCII class member, 0 an ASCII non-member, 2 a rune to decode
   void DetectRun();
   // A regex that is a concatenation of classes of one or two ASCII runes each
   // (a literal, (?i) letters folding only to their other case -- not k / s, whose
