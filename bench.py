@@ -581,8 +581,8 @@ def main():
     ap.add_argument("--parity-mb", type=float, default=None, help="oracle parity sample (first files)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=None,
-                    help="scans in flight (pipelined submission); default 4, c3f 6 (its exact host pass is the "
-                         "bound: 578 vs 536 GB/s at depth 6 vs 4, profiles/r06/c3f/y_r06p_*)")
+                    help="scans in flight (pipelined submission); default 4, c3f 8 (its exact host pass is the "
+                         "bound: 773 / 755 / 670 GB/s at depth 8 / 6 / 4, profiles/r06/c3f/depth/)")
     ap.add_argument("--crlf", type=float, default=0.05,
                     help="c2: share of CRLF files (SURVEY §8(d)); stripped while packing the HBM arena")
     ap.add_argument("--numa", choices=["gpu", "off"], default="gpu",
@@ -617,7 +617,7 @@ def main():
     if args.steps is None:
         args.steps = 50 if args.workload == "c2" else 10
     if args.depth is None:
-        args.depth = 6 if args.workload == "c3f" else 4
+        args.depth = 8 if args.workload == "c3f" else 4
     if args.collectors is None:  # c4: 6 (39.5-41.8 vs 37.6-38.1 GB/s with 3, profiles/r06/c4)
         args.collectors = 6 if args.workload == "c4" else 3
     if args.warmup_s is None:  # only when the warm-up steps are not given explicitly
