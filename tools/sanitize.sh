@@ -33,8 +33,8 @@ if [ "$MODE" = asan ] || [ "$MODE" = all ]; then
   lib=$(build asan "-fsanitize=address,undefined -fno-sanitize-recover=undefined") || exit 1
   LD_PRELOAD=$(g++ -print-file-name=libasan.so):$(g++ -print-file-name=libubsan.so) \
   ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=0 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
-  TSG_HOSTLIB=$ROOT/$lib python -m pytest $TESTS -q -m "not gpu" -p no:cacheprovider > profiles/sanitize_${SAN_TAG:-r05}_asan_ubsan.log 2>&1
-  r=$?; tail -3 profiles/sanitize_${SAN_TAG:-r05}_asan_ubsan.log; [ $r -eq 0 ] || rc=$r
+  TSG_HOSTLIB=$ROOT/$lib python -m pytest $TESTS -q -m "not gpu" -p no:cacheprovider > profiles/sanitize_${SAN_TAG:-r06}_asan_ubsan.log 2>&1
+  r=$?; tail -3 profiles/sanitize_${SAN_TAG:-r06}_asan_ubsan.log; [ $r -eq 0 ] || rc=$r
 fi
 if [ "$MODE" = tsan ] || [ "$MODE" = all ]; then
   lib=$(build tsan "-fsanitize=thread") || exit 1
@@ -46,7 +46,7 @@ if [ "$MODE" = tsan ] || [ "$MODE" = all ]; then
   LD_PRELOAD=$(readlink -f $(g++ -print-file-name=libtsan.so)) \
   TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0:second_deadlock_stack=1 \
   TSG_HOSTLIB=$ROOT/$lib python -m pytest ${TSAN_TESTS:-tests/test_host_concurrency.py tests/test_host_tail.py tests/test_analyzer.py} \
-    -q -m "not gpu" -k "not pool_budget and not pool_spare" -p no:cacheprovider > profiles/sanitize_${SAN_TAG:-r05}_tsan.log 2>&1
-  r=$?; tail -3 profiles/sanitize_${SAN_TAG:-r05}_tsan.log; [ $r -eq 0 ] || rc=$r
+    -q -m "not gpu" -k "not pool_budget and not pool_spare" -p no:cacheprovider > profiles/sanitize_${SAN_TAG:-r06}_tsan.log 2>&1
+  r=$?; tail -3 profiles/sanitize_${SAN_TAG:-r06}_tsan.log; [ $r -eq 0 ] || rc=$r
 fi
 exit $rc
